@@ -1,0 +1,39 @@
+// SwiGLU activation for gfx950: out = silu(gate) * up, input [T, 2F] = [gate | up].
+// Grid-stride, 16-byte vector loads/stores (8 x bf16 per lane), capped grid.
+#include "common.h"
+#include "kernels.h"
+
+namespace akap {
+
+__global__ __launch_bounds__(256) void silu_and_mul_kernel(bf16* __restrict__ out,
+                                                            const bf16* __restrict__ in, long T,
+                                                            int F, int in_stride) {
+  const int vpr = F / 8;  // vectors per row
+  const long total = T * vpr;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long t = i / vpr;
+    const int c = (int)(i % vpr) * 8;
+    const bf16* row = in + t * in_stride;
+    bf16x8 g = *reinterpret_cast<const bf16x8*>(row + c);
+    bf16x8 u = *reinterpret_cast<const bf16x8*>(row + F + c);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = bf2f(g[j]);
+      // silu rounded to bf16 first (matches torch: silu(gate) is a bf16 tensor)
+      const float sx = bf2f(f2bf(x / (1.f + __expf(-x))));
+      o[j] = f2bf(sx * bf2f(u[j]));
+    }
+    *reinterpret_cast<bf16x8*>(out + t * F + c) = o;
+  }
+}
+
+void launch_silu_and_mul(void* out, const void* in, long T, int F, int in_stride, hipStream_t s) {
+  if (T == 0) return;
+  const long total = T * (F / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  silu_and_mul_kernel<<<(int)blocks, 256, 0, s>>>((bf16*)out, (const bf16*)in, T, F, in_stride);
+}
+
+}  // namespace akap

@@ -1,0 +1,313 @@
+// Paged attention (prefill + decode) for gfx950 on MFMA 16x16x32 bf16.
+//
+// Design (MI355X-first, not a port of a CUDA warp kernel):
+//  * One wave owns 16 "query rows".  A query row is a flattened (token, q-head of
+//    the kv group) pair, so GQA heads that share a kv head share every K/V load.
+//    Decode (1 token, G heads) and prefill (many tokens) run the same wave body.
+//  * Scores are computed transposed, S^T = K . Q^T (rows = 16 kv tokens, cols = 16
+//    query rows), so after the MFMA each lane holds 8 scores of ONE query row:
+//    the online-softmax max / sum need only 2 cross-lane steps (xor 16, 32) and the
+//    score registers are directly the B operand of the next MFMA.
+//  * Rows of the two 16-token S tiles map to tokens 8*(r>>2) + 4*tile + (r&3), which
+//    makes lane group g hold tokens 8g..8g+7 contiguous -> O^T = V^T . P^T takes V^T
+//    straight from the dim-major V cache ([blk, Hkv, D, BS]) with 16-byte loads:
+//    no LDS transpose, no ds_bpermute.  O^T keeps the query row on the lane, so the
+//    softmax rescale is lane-local.
+//  * K operand: K cache [blk, Hkv, BS, D]; each lane loads 16 B per MFMA k-chunk.
+//  * Decode: grid (seq, kv_head, partition); 4 waves split a partition's 32-token
+//    chunks and combine through LDS; partitions are combined by a reduce kernel.
+//  * Prefill: grid (q-tile, kv_head); each wave walks the causal range of its rows.
+#include "common.h"
+#include "kernels.h"
+
+namespace akap {
+
+constexpr int kD = 128;
+constexpr int kNC = kD / 32;  // MFMA k-chunks over the head dim
+constexpr int kND = kD / 16;  // 16-wide dim tiles of O^T
+
+struct WaveState {
+  f32x4 o[kND];
+  float m;  // running max of this lane's query row (log2 domain)
+  float l;  // partial denominator (this lane's 8 tokens per chunk)
+};
+
+__device__ __forceinline__ void wave_state_init(WaveState& st) {
+#pragma unroll
+  for (int n = 0; n < kND; ++n) st.o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  st.m = -1e30f;
+  st.l = 0.f;
+}
+
+// Process one 32-token KV chunk starting at absolute kv position t0.
+// limit: last kv position this lane's query row may attend to (-1 => none).
+template <bool MASK>
+__device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC],
+                                           const bf16* __restrict__ k_cache,
+                                           const bf16* __restrict__ v_cache,
+                                           const int* __restrict__ bt, int kv_len, int kvh,
+                                           int Hkv, int BS, int t0, int limit, float scale_log2) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int r = lane & 15;
+  bf16x8 ka[2][kNC];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    int tok = t0 + 8 * (r >> 2) + 4 * tt + (r & 3);
+    tok = min(tok, kv_len - 1);
+    const int blk = bt[tok / BS];
+    const int off = tok % BS;
+    const bf16* kp = k_cache + (((size_t)blk * Hkv + kvh) * BS + off) * kD + 8 * g;
+#pragma unroll
+    for (int c = 0; c < kNC; ++c) ka[tt][c] = *reinterpret_cast<const bf16x8*>(kp + 32 * c);
+  }
+  int vt = t0 + 8 * g;
+  vt = min(vt, (kv_len - 1) & ~7);
+  const int vblk = bt[vt / BS];
+  const int voff = vt % BS;
+  const bf16* vp = v_cache + ((size_t)vblk * Hkv + kvh) * kD * BS + voff + (size_t)r * BS;
+  bf16x8 vb[kND];
+#pragma unroll
+  for (int n = 0; n < kND; ++n) vb[n] = *reinterpret_cast<const bf16x8*>(vp + (size_t)16 * n * BS);
+
+  f32x4 s[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int c = 0; c < kNC; ++c) {
+    s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[0][c], qb[c], s[0], 0, 0, 0);
+    s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[1][c], qb[c], s[1], 0, 0, 0);
+  }
+  float sv[8];
+  float cmax = -INFINITY;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = s[tt][i] * scale_log2;
+      if (MASK) {
+        const int tok = t0 + 8 * g + 4 * tt + i;
+        if (tok > limit) x = -INFINITY;
+      }
+      sv[4 * tt + i] = x;
+      cmax = fmaxf(cmax, x);
+    }
+  cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+  cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+  const float m_new = fmaxf(st.m, cmax);
+  const float alpha = exp2f(st.m - m_new);
+  st.m = m_new;
+  bf16x8 pb;
+  float psum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float p = exp2f(sv[j] - m_new);
+    psum += p;
+    pb[j] = f2bf(p);
+  }
+  st.l = st.l * alpha + psum;
+#pragma unroll
+  for (int n = 0; n < kND; ++n) {
+    st.o[n] *= alpha;
+    st.o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[n], pb, st.o[n], 0, 0, 0);
+  }
+}
+
+// Load this lane's Q^T operand for query row (lane & 15) (zeros if invalid).
+__device__ __forceinline__ void load_q(bf16x8 (&qb)[kNC], const bf16* qrow_ptr, bool valid) {
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int c = 0; c < kNC; ++c) {
+    if (valid)
+      qb[c] = *reinterpret_cast<const bf16x8*>(qrow_ptr + 32 * c + 8 * g);
+    else
+      qb[c] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+// ----------------------------------------------------------------------------------
+// Prefill / chunked-prefill / prefix-cached attention.
+// grid.x = q tiles (64 flattened rows each: 4 waves x 16), grid.y = kv heads.
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
+  const int tile = blockIdx.x;
+  const int kvh = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int seq = p.tile_seq[tile];
+  const int q0 = p.q_start[seq];
+  const int q_len = p.q_start[seq + 1] - q0;
+  const int kv_len = p.seq_lens[seq];
+  const int G = p.G;
+  const int row = p.tile_row[tile] + 16 * w + (lane & 15);
+  const int pos = row / G;
+  const int hig = row % G;
+  const bool valid = pos < q_len;
+  const int limit = valid ? (kv_len - q_len + pos) : -1;
+  const bf16* qptr = p.q + ((size_t)(q0 + pos) * p.Hq + kvh * G + hig) * kD;
+  bf16x8 qb[kNC];
+  load_q(qb, qptr, valid);
+  const int wave_limit = (int)wave_max((float)limit);
+  const int wave_min = -(int)wave_max((float)(valid ? -limit : -(1 << 30)));
+  const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
+  WaveState st;
+  wave_state_init(st);
+  if (wave_limit >= 0) {
+    int t0 = 0;
+    // chunks fully inside every row's causal window need no mask
+    for (; t0 + 31 <= wave_min; t0 += 32)
+      attn_chunk<false>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
+                        p.scale_log2);
+    for (; t0 <= wave_limit; t0 += 32)
+      attn_chunk<true>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
+                       p.scale_log2);
+  }
+  float l = st.l;
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!valid) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  bf16* op = p.out + ((size_t)(q0 + pos) * p.Hq + kvh * G + hig) * kD;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int n = 0; n < kND; ++n) {
+    bf16x4 o4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o4[i] = f2bf(st.o[n][i] * inv);
+    *reinterpret_cast<bf16x4*>(op + 16 * n + 4 * g) = o4;
+  }
+}
+
+// ----------------------------------------------------------------------------------
+// Decode: one new token per sequence, rows = the G q-heads of one kv head.
+// grid = (num_seqs, Hkv, num_parts); 4 waves split the partition's chunks.
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void paged_attn_decode_kernel(AttnParams p) {
+  const int seq = blockIdx.x;
+  const int kvh = blockIdx.y;
+  const int part = blockIdx.z;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  const int G = p.G;
+  const int kv_len = p.seq_lens[seq];
+  const int pstart = part * p.part_size;
+  const int pend = min(kv_len, pstart + p.part_size);
+  const int qr = lane & 15;
+  const bool valid = qr < G && kv_len > 0;
+  const int q_tok = p.q_start ? p.q_start[seq] : seq;
+  const bf16* qptr = p.q + ((size_t)q_tok * p.Hq + kvh * G + qr) * kD;
+
+  __shared__ float o_s[4][16][kD + 4];
+  __shared__ float m_s[4][16];
+  __shared__ float l_s[4][16];
+
+  WaveState st;
+  wave_state_init(st);
+  if (pstart < pend) {
+    bf16x8 qb[kNC];
+    load_q(qb, qptr, valid);
+    const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
+    const int limit = kv_len - 1;
+    for (int t0 = pstart + 32 * w; t0 < pend; t0 += 128) {
+      if (t0 + 31 < kv_len)
+        attn_chunk<false>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
+                          p.scale_log2);
+      else
+        attn_chunk<true>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
+                         p.scale_log2);
+    }
+  }
+  float l = st.l;
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+#pragma unroll
+  for (int n = 0; n < kND; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o_s[w][qr][16 * n + 4 * g + i] = st.o[n][i];
+  if (g == 0) {
+    m_s[w][qr] = st.m;
+    l_s[w][qr] = l;
+  }
+  __syncthreads();
+  // combine: thread -> (row, 8 dims)
+  const int row = threadIdx.x >> 4;
+  const int d0 = (threadIdx.x & 15) * 8;
+  if (row >= G) return;
+  float M = -1e30f;
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, m_s[ww][row]);
+  float L = 0.f;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) {
+    const float f = exp2f(m_s[ww][row] - M);
+    L += f * l_s[ww][row];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f * o_s[ww][row][d0 + j];
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  if (p.num_parts == 1) {
+    bf16* op = p.out + ((size_t)q_tok * p.Hq + kvh * G + row) * kD + d0;
+    bf16x8 o8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o8[j] = f2bf(acc[j] * inv);
+    *reinterpret_cast<bf16x8*>(op) = o8;
+  } else {
+    const size_t pidx = ((size_t)(seq * p.Hkv + kvh) * p.num_parts + part) * G + row;
+    float* po = p.part_o + pidx * kD + d0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) po[j] = acc[j] * inv;
+    if ((threadIdx.x & 15) == 0) {
+      p.part_m[pidx] = L > 0.f ? M : -1e30f;
+      p.part_l[pidx] = L;
+    }
+  }
+}
+
+// Combine split-KV partitions: grid (num_seqs, Hkv), 256 threads = (16 rows x 16 lanes x 8 dims).
+__global__ __launch_bounds__(256) void paged_attn_reduce_kernel(AttnParams p) {
+  const int seq = blockIdx.x;
+  const int kvh = blockIdx.y;
+  const int G = p.G;
+  const int row = threadIdx.x >> 4;
+  const int d0 = (threadIdx.x & 15) * 8;
+  if (row >= G) return;
+  const int kv_len = p.seq_lens[seq];
+  const int nparts = min(p.num_parts, (kv_len + p.part_size - 1) / p.part_size);
+  const size_t base = ((size_t)(seq * p.Hkv + kvh) * p.num_parts) * G + row;
+  float M = -1e30f;
+  for (int q = 0; q < nparts; ++q) M = fmaxf(M, p.part_m[base + (size_t)q * G]);
+  float L = 0.f;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int q = 0; q < nparts; ++q) {
+    const size_t idx = base + (size_t)q * G;
+    const float f = exp2f(p.part_m[idx] - M) * p.part_l[idx];
+    L += f;
+    const f32x4* po = reinterpret_cast<const f32x4*>(p.part_o + idx * kD + d0);
+    f32x4 a = po[0], b = po[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] += f * a[j];
+      acc[4 + j] += f * b[j];
+    }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const int q_tok = p.q_start ? p.q_start[seq] : seq;
+  bf16* op = p.out + ((size_t)q_tok * p.Hq + kvh * G + row) * kD + d0;
+  bf16x8 o8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o8[j] = f2bf(acc[j] * inv);
+  *reinterpret_cast<bf16x8*>(op) = o8;
+}
+
+void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s) {
+  if (num_tiles == 0) return;
+  paged_attn_prefill_kernel<<<dim3(num_tiles, p.Hkv), 256, 0, s>>>(p);
+}
+
+void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) {
+  if (num_seqs == 0) return;
+  paged_attn_decode_kernel<<<dim3(num_seqs, p.Hkv, p.num_parts), 256, 0, s>>>(p);
+  if (p.num_parts > 1) paged_attn_reduce_kernel<<<dim3(num_seqs, p.Hkv), 256, 0, s>>>(p);
+}
+
+}  // namespace akap

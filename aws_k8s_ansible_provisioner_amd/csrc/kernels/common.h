@@ -1,0 +1,93 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels.
+//
+// Everything here assumes wave64, 16-byte vector memory ops and bf16 storage.
+// No CUDA compatibility layer: these are CDNA4 intrinsics used directly.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace akap {
+
+constexpr int kWave = 64;
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+// Full-wave reductions (64 lanes) using DPP/permute via __shfl_xor.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64, <= 1024. `scratch` needs 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = lane < nw ? scratch[lane] : 0.f;
+  r = wave_sum(r);
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_max(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = lane < nw ? scratch[lane] : -INFINITY;
+  r = wave_max(r);
+  __syncthreads();
+  return r;
+}
+
+// XCD-aware bijective remap of a 1-D workgroup id (cdna_hip_programming §5, T1):
+// consecutive logical tiles land on the same XCD (shared L2).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = orig % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / 8;
+}
+
+// Counter-based RNG (splitmix-style hash), deterministic per (seed, a, b).
+__device__ __forceinline__ uint32_t hash3(uint64_t seed, uint32_t a, uint32_t b) {
+  uint64_t x = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(a + 1)) ^ ((uint64_t)b << 32 | b);
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32);
+}
+
+__device__ __forceinline__ float uniform01(uint64_t seed, uint32_t a, uint32_t b) {
+  // (0, 1] open at 0 so -log(u) is finite.
+  return ((hash3(seed, a, b) >> 8) + 1) * (1.0f / 16777216.0f);
+}
+
+}  // namespace akap

@@ -1,0 +1,85 @@
+// Host-visible launchers of the gfx950 kernels.  Pure HIP: no torch headers here,
+// so every .hip translation unit compiles in seconds; torch glue lives in ops.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace akap {
+
+// ---- norm.hip ----
+void launch_rmsnorm(void* out, const void* x, const void* w, int rows, int d, int x_stride,
+                    int out_stride, float eps, hipStream_t s);
+void launch_fused_add_rmsnorm(void* out, void* residual, const void* x, const void* w, int rows,
+                              int d, int x_stride, int out_stride, float eps, hipStream_t s);
+
+// ---- rope_cache.hip ----
+void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, void* k_cache,
+                               void* v_cache, const int64_t* positions, const int64_t* slots,
+                               const float* cos_sin, const void* q_w, const void* k_w, int T,
+                               int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
+                               hipStream_t s);
+void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void* v_cache,
+                              const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s);
+
+// ---- activation.hip ----
+void launch_silu_and_mul(void* out, const void* in, long T, int F, int in_stride, hipStream_t s);
+
+// ---- attention.hip ----
+struct AttnParams {
+  const __bf16* q;        // [T, Hq, D]
+  const __bf16* k_cache;  // [NB, Hkv, BS, D]
+  const __bf16* v_cache;  // [NB, Hkv, D, BS]
+  __bf16* out;            // [T, Hq, D]
+  const int* block_tables;  // [B, bt_stride]
+  int bt_stride;
+  const int* seq_lens;  // [B] kv length incl. the new tokens
+  const int* q_start;   // [B+1] cumulative query tokens (nullptr for pure decode)
+  int Hq, Hkv, G, BS;
+  float scale_log2;
+  // prefill tiling (host-built): per 64-row tile its sequence and first flattened row
+  const int* tile_seq;
+  const int* tile_row;
+  // decode split-KV
+  int num_parts, part_size;
+  float* part_m;  // [B, Hkv, parts, G]
+  float* part_l;
+  float* part_o;  // [B, Hkv, parts, G, D]
+};
+void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s);
+void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s);
+
+// ---- sampling.hip ----
+struct SampleParams {
+  const float* logits;  // [B, V] (row stride ld)
+  int ld, V;
+  const float* temperature;  // [B] (<=0 => greedy)
+  const int* top_k;          // [B] (<=0 => off)
+  const float* top_p;        // [B] (>=1 => off)
+  const int64_t* seeds;      // [B]
+  const int* steps;          // [B] per-request step counter mixed into the RNG
+  int64_t* out_tokens;       // [B]
+  float* out_logprobs;       // [B] log-prob of the sampled token (may be null)
+};
+void launch_sample(const SampleParams& p, int B, hipStream_t s);
+void launch_argmax(const void* logits, int ld, int V, int is_bf16, int64_t* out, int B,
+                   hipStream_t s);
+
+// ---- moe.hip ----
+void launch_moe_topk_softmax(const void* logits, int ld, int E, int K, float* topk_w,
+                             int32_t* topk_ids, int T, int renormalize, hipStream_t s);
+void launch_moe_align(const int32_t* topk_ids, int n, int E, int block, int32_t* sorted_ids,
+                      int32_t* expert_offsets, int32_t* num_padded, hipStream_t s);
+
+// ---- kv_transfer.hip ----
+// The paged cache is `planes` planes (layer x {K,V}) of [NB, block_elems] bf16.
+void launch_kv_gather(const void* cache, long plane_stride, int planes, int block_elems,
+                      const int* block_ids, int nblk, void* out, hipStream_t s);
+void launch_kv_scatter(const void* in, void* cache, long plane_stride, int planes,
+                       int block_elems, const int* block_ids, int nblk, hipStream_t s);
+
+// ---- embedding.hip ----
+void launch_embedding(const int64_t* ids, const void* table, void* out, int T, int d,
+                      int vocab_start, int vocab_end, hipStream_t s);
+
+}  // namespace akap

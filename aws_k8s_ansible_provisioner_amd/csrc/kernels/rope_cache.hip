@@ -1,0 +1,161 @@
+// Fused post-QKV-projection epilogue for gfx950:
+//   per-head RMSNorm on q and k (Qwen3; optional)  ->  NeoX rotary on q and k
+//   -> q written contiguous [T, Hq, D]; k, v scattered into the paged KV cache.
+//
+// One pass over the QKV activations instead of three (norm, rope, cache write).
+// D/8 lanes own one head: lane i holds dims [4i, 4i+4) and their rotary partners
+// [D/2 + 4i, D/2 + 4i + 4) so the rotate-half pairing is lane-local.  cos/sin come
+// from a host-precomputed fp32 table [max_pos, D] (cos | sin), no on-device trig.
+//
+// Paged cache layouts (MI355X-first, chosen so the attention kernels can issue
+// 16-byte MFMA-operand loads with no transpose):
+//   K cache: [num_blocks, Hkv, BS, D]   (token-major inside a block)
+//   V cache: [num_blocks, Hkv, D, BS]   (dim-major inside a block = V^T)
+#include "common.h"
+#include "kernels.h"
+
+namespace akap {
+
+template <int D>
+__global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
+    const bf16* __restrict__ qkv, int qkv_stride, bf16* __restrict__ q_out,
+    bf16* __restrict__ k_cache, bf16* __restrict__ v_cache, const int64_t* __restrict__ positions,
+    const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
+    const bf16* __restrict__ q_w, const bf16* __restrict__ k_w, int T, int Hq, int Hkv, int BS,
+    float eps, int apply_rope) {
+  constexpr int LPH = D / 8;  // lanes per head
+  constexpr int HALF = D / 2;
+  const int heads_total = Hq + 2 * Hkv;
+  const int item = (blockIdx.x * 256 + threadIdx.x) / LPH;
+  const int li = threadIdx.x % LPH;
+  if (item >= T * heads_total) return;
+  const int t = item / heads_total;
+  const int h = item % heads_total;
+  const bf16* src = qkv + (size_t)t * qkv_stride + h * D;
+  bf16x4 a = *reinterpret_cast<const bf16x4*>(src + 4 * li);
+  bf16x4 b = *reinterpret_cast<const bf16x4*>(src + HALF + 4 * li);
+  float xa[4], xb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { xa[j] = bf2f(a[j]); xb[j] = bf2f(b[j]); }
+
+  const bool is_q = h < Hq;
+  const bool is_k = !is_q && h < Hq + Hkv;
+  if (is_q || is_k) {
+    const bf16* nw = is_q ? q_w : k_w;
+    if (nw != nullptr) {
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
+#pragma unroll
+      for (int o = LPH / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, LPH);
+      const float inv = rsqrtf(ss / (float)D + eps);
+      bf16x4 wa = *reinterpret_cast<const bf16x4*>(nw + 4 * li);
+      bf16x4 wb = *reinterpret_cast<const bf16x4*>(nw + HALF + 4 * li);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // round-trip through bf16 like the reference module (norm output is bf16)
+        xa[j] = bf2f(f2bf(xa[j] * inv * bf2f(wa[j])));
+        xb[j] = bf2f(f2bf(xb[j] * inv * bf2f(wb[j])));
+      }
+    }
+    if (apply_rope) {
+      const float* cs = cos_sin + (size_t)positions[t] * D;
+      f32x4 c = *reinterpret_cast<const f32x4*>(cs + 4 * li);
+      f32x4 s = *reinterpret_cast<const f32x4*>(cs + HALF + 4 * li);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x1 = xa[j], x2 = xb[j];
+        xa[j] = x1 * c[j] - x2 * s[j];
+        xb[j] = x2 * c[j] + x1 * s[j];
+      }
+    }
+  }
+  bf16x4 oa, ob;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { oa[j] = f2bf(xa[j]); ob[j] = f2bf(xb[j]); }
+  if (is_q) {
+    bf16* dst = q_out + ((size_t)t * Hq + h) * D;
+    *reinterpret_cast<bf16x4*>(dst + 4 * li) = oa;
+    *reinterpret_cast<bf16x4*>(dst + HALF + 4 * li) = ob;
+    return;
+  }
+  const int64_t slot = slots[t];
+  if (slot < 0) return;
+  const int64_t blk = slot / BS;
+  const int off = (int)(slot % BS);
+  if (is_k) {
+    const int kh = h - Hq;
+    bf16* dst = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D;
+    *reinterpret_cast<bf16x4*>(dst + 4 * li) = oa;
+    *reinterpret_cast<bf16x4*>(dst + HALF + 4 * li) = ob;
+  } else {
+    const int vh = h - Hq - Hkv;
+    bf16* dst = v_cache + ((size_t)blk * Hkv + vh) * D * BS + off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dst[(size_t)(4 * li + j) * BS] = oa[j];
+      dst[(size_t)(HALF + 4 * li + j) * BS] = ob[j];
+    }
+  }
+}
+
+void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, void* k_cache,
+                               void* v_cache, const int64_t* positions, const int64_t* slots,
+                               const float* cos_sin, const void* q_w, const void* k_w, int T,
+                               int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
+                               hipStream_t s) {
+  if (T == 0) return;
+  const long items = (long)T * (Hq + 2 * Hkv);
+  const int lph = D / 8;
+  const long threads = items * lph;
+  dim3 grid((threads + 255) / 256);
+  if (D == 128) {
+    qk_norm_rope_cache_kernel<128><<<grid, 256, 0, s>>>(
+        (const bf16*)qkv, qkv_stride, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions,
+        slots, cos_sin, (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope);
+  } else if (D == 64) {
+    qk_norm_rope_cache_kernel<64><<<grid, 256, 0, s>>>(
+        (const bf16*)qkv, qkv_stride, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions,
+        slots, cos_sin, (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope);
+  }
+}
+
+// Plain scatter of already-final K/V rows into the paged cache (used by the
+// P/D KV receiver and by tests).  k, v: [T, Hkv, D].
+template <int D>
+__global__ __launch_bounds__(256) void reshape_and_cache_kernel(
+    const bf16* __restrict__ k, const bf16* __restrict__ v, bf16* __restrict__ k_cache,
+    bf16* __restrict__ v_cache, const int64_t* __restrict__ slots, int T, int Hkv, int BS) {
+  constexpr int LPH = D / 8;
+  const int item = (blockIdx.x * 256 + threadIdx.x) / LPH;
+  const int li = threadIdx.x % LPH;
+  if (item >= T * Hkv) return;
+  const int t = item / Hkv, h = item % Hkv;
+  const int64_t slot = slots[t];
+  if (slot < 0) return;
+  const int64_t blk = slot / BS;
+  const int off = (int)(slot % BS);
+  bf16x8 kv = *reinterpret_cast<const bf16x8*>(k + ((size_t)t * Hkv + h) * D + 8 * li);
+  bf16x8 vv = *reinterpret_cast<const bf16x8*>(v + ((size_t)t * Hkv + h) * D + 8 * li);
+  *reinterpret_cast<bf16x8*>(k_cache + (((size_t)blk * Hkv + h) * BS + off) * D + 8 * li) = kv;
+  bf16* vd = v_cache + ((size_t)blk * Hkv + h) * D * BS + off;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) vd[(size_t)(8 * li + j) * BS] = vv[j];
+}
+
+void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void* v_cache,
+                              const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s) {
+  if (T == 0) return;
+  const long threads = (long)T * Hkv * (D / 8);
+  dim3 grid((threads + 255) / 256);
+  if (D == 128)
+    reshape_and_cache_kernel<128><<<grid, 256, 0, s>>>((const bf16*)k, (const bf16*)v,
+                                                      (bf16*)k_cache, (bf16*)v_cache, slots, T,
+                                                      Hkv, BS);
+  else if (D == 64)
+    reshape_and_cache_kernel<64><<<grid, 256, 0, s>>>((const bf16*)k, (const bf16*)v,
+                                                     (bf16*)k_cache, (bf16*)v_cache, slots, T,
+                                                     Hkv, BS);
+}
+
+}  // namespace akap

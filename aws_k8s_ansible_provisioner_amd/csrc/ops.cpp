@@ -1,0 +1,293 @@
+// torch custom-op registrations (namespace `akap`) for the gfx950 kernels.
+//
+// Every op launches on the caller's current HIP stream, allocates nothing and
+// never synchronises, so all of them are hipGraph-capturable (engine decode path).
+// PyTorch on ROCm names the GPU dispatch key "CUDA"; kernels are HIP/CDNA4 only.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels/kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_GPU(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define CHECK_LAST_CONTIG(x) TORCH_CHECK((x).stride(-1) == 1, #x " must have unit last stride")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+
+void rmsnorm(Tensor out, Tensor x, Tensor w, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(out);
+  const int d = x.size(-1);
+  TORCH_CHECK(d % 8 == 0, "hidden size must be a multiple of 8");
+  const int rows = x.numel() / d;
+  const c10::DeviceGuard g(x.device());
+  akap::launch_rmsnorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), rows, d,
+                       x.dim() > 1 ? x.stride(-2) : d, out.dim() > 1 ? out.stride(-2) : d,
+                       (float)eps, cur_stream());
+}
+
+void fused_add_rmsnorm(Tensor out, Tensor residual, Tensor x, Tensor w, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_CONTIG(residual); CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(out);
+  const int d = x.size(-1);
+  TORCH_CHECK(d % 8 == 0, "hidden size must be a multiple of 8");
+  const int rows = x.numel() / d;
+  const c10::DeviceGuard g(x.device());
+  akap::launch_fused_add_rmsnorm(out.data_ptr(), residual.data_ptr(), x.data_ptr(), w.data_ptr(),
+                                 rows, d, x.dim() > 1 ? x.stride(-2) : d,
+                                 out.dim() > 1 ? out.stride(-2) : d, (float)eps, cur_stream());
+}
+
+void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache,
+                        Tensor positions, Tensor slots, Tensor cos_sin,
+                        std::optional<Tensor> q_w, std::optional<Tensor> k_w, int64_t Hq,
+                        int64_t Hkv, double eps, bool apply_rope) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv); CHECK_CONTIG(q_out);
+  CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong,
+              "positions/slots must be int64");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat, "cos_sin cache must be fp32");
+  const int T = qkv.size(0);
+  const int D = k_cache.size(3);
+  const int BS = k_cache.size(2);
+  TORCH_CHECK(D == 128 || D == 64, "head_dim must be 64 or 128");
+  TORCH_CHECK(v_cache.size(2) == D && v_cache.size(3) == BS, "v_cache must be [NB,Hkv,D,BS]");
+  TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D, "qkv too narrow");
+  TORCH_CHECK(positions.numel() >= T && slots.numel() >= T, "positions/slots too short");
+  const c10::DeviceGuard g(qkv.device());
+  akap::launch_qk_norm_rope_cache(
+      qkv.data_ptr(), qkv.stride(0), q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+      positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+      q_w ? q_w->data_ptr() : nullptr, k_w ? k_w->data_ptr() : nullptr, T, Hq, Hkv, D, BS,
+      (float)eps, apply_rope ? 1 : 0, cur_stream());
+}
+
+void reshape_and_cache(Tensor k, Tensor v, Tensor k_cache, Tensor v_cache, Tensor slots) {
+  CHECK_GPU(k); CHECK_CONTIG(k); CHECK_CONTIG(v); CHECK_BF16(k); CHECK_BF16(v);
+  const int T = k.size(0), Hkv = k.size(1), D = k.size(2);
+  const int BS = k_cache.size(2);
+  TORCH_CHECK(D == 128 || D == 64, "head_dim must be 64 or 128");
+  const c10::DeviceGuard g(k.device());
+  akap::launch_reshape_and_cache(k.data_ptr(), v.data_ptr(), k_cache.data_ptr(),
+                                 v_cache.data_ptr(), slots.data_ptr<int64_t>(), T, Hkv, D, BS,
+                                 cur_stream());
+}
+
+void silu_and_mul(Tensor out, Tensor x) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_LAST_CONTIG(x); CHECK_CONTIG(out);
+  const int F = x.size(-1) / 2;
+  TORCH_CHECK(F % 8 == 0, "ffn size must be a multiple of 8");
+  const long T = x.numel() / x.size(-1);
+  const c10::DeviceGuard g(x.device());
+  akap::launch_silu_and_mul(out.data_ptr(), x.data_ptr(), T, F,
+                            x.dim() > 1 ? x.stride(-2) : 2 * F, cur_stream());
+}
+
+akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_cache,
+                             Tensor& block_tables, Tensor& seq_lens, int64_t G, double scale) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out); CHECK_CONTIG(k_cache);
+  CHECK_CONTIG(v_cache);
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt,
+              "block_tables / seq_lens must be int32");
+  TORCH_CHECK(block_tables.stride(1) == 1, "block_tables rows must be contiguous");
+  akap::AttnParams p{};
+  p.q = (const __bf16*)q.data_ptr();
+  p.k_cache = (const __bf16*)k_cache.data_ptr();
+  p.v_cache = (const __bf16*)v_cache.data_ptr();
+  p.out = (__bf16*)out.data_ptr();
+  p.block_tables = block_tables.data_ptr<int>();
+  p.bt_stride = block_tables.stride(0);
+  p.seq_lens = seq_lens.data_ptr<int>();
+  p.Hq = q.size(1);
+  p.Hkv = k_cache.size(1);
+  p.G = G;
+  p.BS = k_cache.size(2);
+  TORCH_CHECK(q.size(2) == 128 && k_cache.size(3) == 128, "attention kernels need head_dim 128");
+  TORCH_CHECK(p.Hq == p.Hkv * G, "Hq must equal Hkv * G");
+  TORCH_CHECK(p.BS % 8 == 0 && (p.BS % 32 == 0 || 32 % p.BS == 0), "block size must be 8/16/32/64..");
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  return p;
+}
+
+void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache,
+                             Tensor block_tables, Tensor seq_lens, Tensor q_start,
+                             Tensor tile_seq, Tensor tile_row, int64_t G, double scale) {
+  auto p = attn_params(out, q, k_cache, v_cache, block_tables, seq_lens, G, scale);
+  TORCH_CHECK(q_start.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
+                  tile_row.scalar_type() == at::kInt,
+              "q_start/tile maps must be int32");
+  p.q_start = q_start.data_ptr<int>();
+  p.tile_seq = tile_seq.data_ptr<int>();
+  p.tile_row = tile_row.data_ptr<int>();
+  const c10::DeviceGuard g(q.device());
+  akap::launch_paged_attn_prefill(p, tile_seq.numel(), cur_stream());
+}
+
+void paged_attention_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache,
+                            Tensor block_tables, Tensor seq_lens, std::optional<Tensor> q_start,
+                            Tensor part_m, Tensor part_l, Tensor part_o, int64_t num_parts,
+                            int64_t part_size, int64_t G, double scale) {
+  auto p = attn_params(out, q, k_cache, v_cache, block_tables, seq_lens, G, scale);
+  TORCH_CHECK(G <= 16, "decode kernel supports up to 16 q heads per kv head");
+  TORCH_CHECK(part_size % 128 == 0 && part_size > 0, "part_size must be a multiple of 128");
+  const int B = seq_lens.numel();
+  p.q_start = q_start ? q_start->data_ptr<int>() : nullptr;
+  p.num_parts = num_parts;
+  p.part_size = part_size;
+  if (num_parts > 1) {
+    TORCH_CHECK(part_o.numel() >= (int64_t)B * p.Hkv * num_parts * G * 128,
+                "part_o workspace too small");
+    TORCH_CHECK(part_m.numel() >= (int64_t)B * p.Hkv * num_parts * G, "part_m too small");
+    p.part_m = part_m.data_ptr<float>();
+    p.part_l = part_l.data_ptr<float>();
+    p.part_o = part_o.data_ptr<float>();
+  }
+  const c10::DeviceGuard g(q.device());
+  akap::launch_paged_attn_decode(p, B, cur_stream());
+}
+
+void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
+            Tensor steps, Tensor out_tokens, Tensor out_logprobs) {
+  CHECK_GPU(logits);
+  TORCH_CHECK(logits.scalar_type() == at::kFloat, "sampler expects fp32 logits");
+  CHECK_LAST_CONTIG(logits);
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && top_p.scalar_type() == at::kFloat,
+              "temperature/top_p fp32");
+  TORCH_CHECK(top_k.scalar_type() == at::kInt && steps.scalar_type() == at::kInt, "int32");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong && out_tokens.scalar_type() == at::kLong, "int64");
+  const int B = logits.size(0);
+  akap::SampleParams p{};
+  p.logits = logits.data_ptr<float>();
+  p.ld = logits.stride(0);
+  p.V = logits.size(1);
+  p.temperature = temperature.data_ptr<float>();
+  p.top_k = top_k.data_ptr<int>();
+  p.top_p = top_p.data_ptr<float>();
+  p.seeds = seeds.data_ptr<int64_t>();
+  p.steps = steps.data_ptr<int>();
+  p.out_tokens = out_tokens.data_ptr<int64_t>();
+  p.out_logprobs = out_logprobs.numel() ? out_logprobs.data_ptr<float>() : nullptr;
+  const c10::DeviceGuard g(logits.device());
+  akap::launch_sample(p, B, cur_stream());
+}
+
+void argmax(Tensor logits, Tensor out) {
+  CHECK_GPU(logits); CHECK_LAST_CONTIG(logits);
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
+              "argmax expects bf16/fp32");
+  TORCH_CHECK(out.scalar_type() == at::kLong, "out int64");
+  const c10::DeviceGuard g(logits.device());
+  akap::launch_argmax(logits.data_ptr(), logits.stride(0), logits.size(1),
+                      logits.scalar_type() == at::kBFloat16, out.data_ptr<int64_t>(),
+                      logits.size(0), cur_stream());
+}
+
+void moe_topk_softmax(Tensor logits, Tensor topk_w, Tensor topk_ids, bool renorm) {
+  CHECK_GPU(logits); CHECK_BF16(logits); CHECK_LAST_CONTIG(logits);
+  TORCH_CHECK(logits.size(1) <= 256, "at most 256 experts");
+  const c10::DeviceGuard g(logits.device());
+  akap::launch_moe_topk_softmax(logits.data_ptr(), logits.stride(0), logits.size(1),
+                                topk_w.size(1), topk_w.data_ptr<float>(),
+                                topk_ids.data_ptr<int32_t>(), logits.size(0), renorm ? 1 : 0,
+                                cur_stream());
+}
+
+void moe_align(Tensor topk_ids, int64_t E, int64_t block, Tensor sorted_ids, Tensor offsets,
+               Tensor num_padded) {
+  CHECK_GPU(topk_ids); CHECK_CONTIG(topk_ids);
+  const int n = topk_ids.numel();
+  TORCH_CHECK(sorted_ids.numel() >= n + E * (block - 1), "sorted_ids too small");
+  const c10::DeviceGuard g(topk_ids.device());
+  akap::launch_moe_align(topk_ids.data_ptr<int32_t>(), n, E, block,
+                         sorted_ids.data_ptr<int32_t>(), offsets.data_ptr<int32_t>(),
+                         num_padded.data_ptr<int32_t>(), cur_stream());
+}
+
+void kv_gather(Tensor cache, Tensor block_ids, Tensor out) {
+  // cache: [planes, NB, ...block...]
+  CHECK_GPU(cache); CHECK_CONTIG(cache); CHECK_CONTIG(out);
+  const int planes = cache.size(0);
+  const long plane_stride = cache.stride(0);
+  const int block_elems = cache.stride(1);
+  TORCH_CHECK(block_elems % 2048 == 0 || block_elems % 8 == 0, "block must be 16B multiple");
+  TORCH_CHECK(out.numel() >= (int64_t)planes * block_ids.numel() * block_elems, "out too small");
+  const c10::DeviceGuard g(cache.device());
+  akap::launch_kv_gather(cache.data_ptr(), plane_stride, planes, block_elems,
+                         block_ids.data_ptr<int>(), block_ids.numel(), out.data_ptr(),
+                         cur_stream());
+}
+
+void kv_scatter(Tensor buf, Tensor cache, Tensor block_ids) {
+  CHECK_GPU(cache); CHECK_CONTIG(cache); CHECK_CONTIG(buf);
+  const int planes = cache.size(0);
+  const c10::DeviceGuard g(cache.device());
+  akap::launch_kv_scatter(buf.data_ptr(), cache.data_ptr(), cache.stride(0), planes,
+                          cache.stride(1), block_ids.data_ptr<int>(), block_ids.numel(),
+                          cur_stream());
+}
+
+void embedding(Tensor ids, Tensor table, Tensor out, int64_t vocab_start, int64_t vocab_end) {
+  CHECK_GPU(ids); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CONTIG(out);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
+  const int d = table.size(1);
+  TORCH_CHECK(d % 8 == 0, "embedding dim multiple of 8");
+  const c10::DeviceGuard g(ids.device());
+  akap::launch_embedding(ids.data_ptr<int64_t>(), table.data_ptr(), out.data_ptr(), ids.numel(),
+                         d, vocab_start, vocab_end, cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(akap, m) {
+  m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
+  m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
+  m.def(
+      "qk_norm_rope_cache(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, "
+      "Tensor positions, Tensor slots, Tensor cos_sin, Tensor? q_w, Tensor? k_w, int Hq, int Hkv, "
+      "float eps, bool apply_rope) -> ()");
+  m.def("reshape_and_cache(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
+  m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
+  m.def(
+      "paged_attention_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
+      "Tensor block_tables, Tensor seq_lens, Tensor q_start, Tensor tile_seq, Tensor tile_row, "
+      "int G, float scale) -> ()");
+  m.def(
+      "paged_attention_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
+      "Tensor block_tables, Tensor seq_lens, Tensor? q_start, Tensor(b!) part_m, Tensor(c!) part_l, "
+      "Tensor(d!) part_o, int num_parts, int part_size, int G, float scale) -> ()");
+  m.def(
+      "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
+      "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs) -> ()");
+  m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
+  m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
+  m.def(
+      "moe_align(Tensor topk_ids, int E, int block, Tensor(a!) sorted_ids, Tensor(b!) offsets, "
+      "Tensor(c!) num_padded) -> ()");
+  m.def("kv_gather(Tensor cache, Tensor block_ids, Tensor(a!) out) -> ()");
+  m.def("kv_scatter(Tensor buf, Tensor(a!) cache, Tensor block_ids) -> ()");
+  m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start, int vocab_end) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(akap, CUDA, m) {
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.impl("qk_norm_rope_cache", &qk_norm_rope_cache);
+  m.impl("reshape_and_cache", &reshape_and_cache);
+  m.impl("silu_and_mul", &silu_and_mul);
+  m.impl("paged_attention_prefill", &paged_attention_prefill);
+  m.impl("paged_attention_decode", &paged_attention_decode);
+  m.impl("sample", &sample);
+  m.impl("argmax", &argmax);
+  m.impl("moe_topk_softmax", &moe_topk_softmax);
+  m.impl("moe_align", &moe_align);
+  m.impl("kv_gather", &kv_gather);
+  m.impl("kv_scatter", &kv_scatter);
+  m.impl("embedding", &embedding);
+}

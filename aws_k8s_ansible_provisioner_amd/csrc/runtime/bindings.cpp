@@ -1,0 +1,128 @@
+// pybind11 bindings of the host runtime (module `_runtime`).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "block_manager.h"
+#include "scheduler.h"
+
+namespace py = pybind11;
+using namespace akap_rt;
+
+template <typename T>
+static T* ptr_of(py::dict& d, const char* k, size_t min_elems) {
+  auto a = d[k].cast<py::array_t<T, py::array::c_style>>();
+  if ((size_t)a.size() < min_elems) throw std::invalid_argument(std::string("buffer too small: ") + k);
+  return a.mutable_data();
+}
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "MI355X serving engine host runtime: paged KV block manager + batch scheduler";
+
+  py::class_<BlockManager>(m, "BlockManager")
+      .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"),
+           py::arg("enable_prefix_cache") = true)
+      .def_property_readonly("num_blocks", &BlockManager::num_blocks)
+      .def_property_readonly("block_size", &BlockManager::block_size)
+      .def_property_readonly("num_free", &BlockManager::num_free)
+      .def("usage", &BlockManager::usage)
+      .def("allocate", &BlockManager::allocate)
+      .def("free_blocks", &BlockManager::free_blocks)
+      .def("register_full", &BlockManager::register_full)
+      .def("reset_prefix_cache", &BlockManager::reset_prefix_cache)
+      .def("match_prefix",
+           [](BlockManager& bm, const std::vector<int32_t>& toks, int max_tokens) {
+             std::vector<int32_t> b;
+             std::vector<uint64_t> h;
+             int n = bm.match_prefix(toks, max_tokens, b, h);
+             return py::make_tuple(n, b, h);
+           })
+      .def_static("hash_block", [](uint64_t parent, const std::vector<int32_t>& t) {
+        return BlockManager::hash_block(parent, t.data(), (int)t.size());
+      });
+
+  py::class_<SchedConfig>(m, "SchedConfig")
+      .def(py::init<>())
+      .def_readwrite("max_num_seqs", &SchedConfig::max_num_seqs)
+      .def_readwrite("max_num_batched_tokens", &SchedConfig::max_num_batched_tokens)
+      .def_readwrite("max_model_len", &SchedConfig::max_model_len)
+      .def_readwrite("block_size", &SchedConfig::block_size)
+      .def_readwrite("gqa_group", &SchedConfig::gqa_group)
+      .def_readwrite("tile_rows", &SchedConfig::tile_rows)
+      .def_readwrite("eos_id", &SchedConfig::eos_id)
+      .def_readwrite("max_blocks_per_seq", &SchedConfig::max_blocks_per_seq);
+
+  py::class_<Scheduler>(m, "Scheduler")
+      .def(py::init<const SchedConfig&, int, bool>(), py::arg("config"), py::arg("num_blocks"),
+           py::arg("prefix_cache") = true)
+      .def("add_request", &Scheduler::add_request, py::arg("id"), py::arg("prompt"),
+           py::arg("max_tokens"), py::arg("min_tokens") = 0, py::arg("ignore_eos") = false,
+           py::arg("stop_ids") = std::vector<int32_t>{})
+      .def("abort_request", &Scheduler::abort_request)
+      .def("release", &Scheduler::release)
+      .def("schedule",
+           [](Scheduler& s, py::dict bufs) {
+             const auto& c = s.config();
+             BatchBuffers b{};
+             b.cap_tokens = bufs["input_ids"].cast<py::array>().size();
+             b.input_ids = ptr_of<int64_t>(bufs, "input_ids", b.cap_tokens);
+             b.positions = ptr_of<int64_t>(bufs, "positions", b.cap_tokens);
+             b.slots = ptr_of<int64_t>(bufs, "slots", b.cap_tokens);
+             b.seq_lens = ptr_of<int32_t>(bufs, "seq_lens", c.max_num_seqs);
+             b.q_start = ptr_of<int32_t>(bufs, "q_start", c.max_num_seqs + 1);
+             b.block_tables = ptr_of<int32_t>(bufs, "block_tables",
+                                              (size_t)c.max_num_seqs * c.max_blocks_per_seq);
+             b.cap_tiles = bufs["tile_seq"].cast<py::array>().size();
+             b.tile_seq = ptr_of<int32_t>(bufs, "tile_seq", b.cap_tiles);
+             b.tile_row = ptr_of<int32_t>(bufs, "tile_row", b.cap_tiles);
+             b.logits_idx = ptr_of<int64_t>(bufs, "logits_idx", c.max_num_seqs);
+             b.req_ids = ptr_of<int64_t>(bufs, "req_ids", c.max_num_seqs);
+             b.sample_mask = ptr_of<int32_t>(bufs, "sample_mask", c.max_num_seqs);
+             StepInfo i;
+             {
+               py::gil_scoped_release nogil;
+               i = s.schedule(b);
+             }
+             py::dict d;
+             d["is_prefill"] = i.is_prefill;
+             d["num_seqs"] = i.num_seqs;
+             d["num_tokens"] = i.num_tokens;
+             d["num_tiles"] = i.num_tiles;
+             d["num_samples"] = i.num_samples;
+             d["max_seq_len"] = i.max_seq_len;
+             d["num_preempted"] = i.num_preempted;
+             return d;
+           })
+      .def("update",
+           [](Scheduler& s, py::array_t<int64_t, py::array::c_style> toks) {
+             std::vector<int64_t> ids;
+             std::vector<int32_t> t, f;
+             s.update(toks.data(), (int)toks.size(), ids, t, f);
+             return py::make_tuple(ids, t, f);
+           })
+      .def_property_readonly("num_waiting", &Scheduler::num_waiting)
+      .def_property_readonly("num_running", &Scheduler::num_running)
+      .def("has_work", &Scheduler::has_work)
+      .def("block_table", &Scheduler::block_table)
+      .def("kv_usage", [](const Scheduler& s) { return s.blocks().usage(); })
+      .def("num_free_blocks", [](const Scheduler& s) { return s.blocks().num_free(); })
+      .def("prefix_stats", [](const Scheduler& s) {
+        return py::make_tuple(s.blocks().prefix_hits(), s.blocks().prefix_queries());
+      })
+      .def("reset_prefix_cache", [](Scheduler& s) { s.blocks_mut().reset_prefix_cache(); })
+      .def_property_readonly("total_preemptions", &Scheduler::total_preemptions)
+      .def("request_info", [](const Scheduler& s, int64_t id) -> py::object {
+        auto r = s.get(id);
+        if (!r) return py::none();
+        py::dict d;
+        d["num_prompt"] = r->num_prompt;
+        d["num_tokens"] = (int)r->tokens.size();
+        d["num_computed"] = r->num_computed;
+        d["num_cached"] = r->num_cached;
+        d["status"] = r->status;
+        d["finish"] = r->finish;
+        d["num_preempt"] = r->num_preempt;
+        d["tokens"] = r->tokens;
+        return d;
+      });
+}

@@ -1,0 +1,251 @@
+#include "scheduler.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace akap_rt {
+
+Scheduler::Scheduler(const SchedConfig& cfg, int num_blocks, bool prefix_cache)
+    : cfg_(cfg), bm_(num_blocks, cfg.block_size, prefix_cache) {
+  if (cfg_.max_blocks_per_seq * cfg_.block_size < cfg_.max_model_len)
+    throw std::invalid_argument("max_blocks_per_seq * block_size < max_model_len");
+}
+
+void Scheduler::add_request(int64_t id, const std::vector<int32_t>& prompt, int max_tokens,
+                            int min_tokens, bool ignore_eos, const std::vector<int32_t>& stop_ids) {
+  if (reqs_.count(id)) throw std::invalid_argument("duplicate request id");
+  if (prompt.empty()) throw std::invalid_argument("empty prompt");
+  if ((int)prompt.size() >= cfg_.max_model_len)
+    throw std::invalid_argument("prompt longer than max_model_len");
+  auto r = std::make_unique<Request>();
+  r->id = id;
+  r->tokens = prompt;
+  r->num_prompt = (int)prompt.size();
+  r->max_tokens = std::max(1, max_tokens);
+  r->min_tokens = min_tokens;
+  r->ignore_eos = ignore_eos;
+  r->stop_ids = stop_ids;
+  waiting_.push_back(r.get());
+  reqs_.emplace(id, std::move(r));
+}
+
+const Request* Scheduler::get(int64_t id) const {
+  auto it = reqs_.find(id);
+  return it == reqs_.end() ? nullptr : it->second.get();
+}
+
+std::vector<int32_t> Scheduler::block_table(int64_t id) const {
+  auto r = get(id);
+  return r ? r->blocks : std::vector<int32_t>{};
+}
+
+void Scheduler::release(int64_t id) {
+  auto it = reqs_.find(id);
+  if (it != reqs_.end() && it->second->status == FINISHED) reqs_.erase(it);
+}
+
+bool Scheduler::abort_request(int64_t id) {
+  auto it = reqs_.find(id);
+  if (it == reqs_.end()) return false;
+  Request* r = it->second.get();
+  if (r->status == FINISHED) return false;
+  if (r->status == WAITING) {
+    waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), r), waiting_.end());
+  } else {
+    running_.erase(std::remove(running_.begin(), running_.end(), r), running_.end());
+  }
+  last_sampled_.erase(std::remove(last_sampled_.begin(), last_sampled_.end(), r),
+                      last_sampled_.end());
+  finish(*r, FINISH_ABORT);
+  return true;
+}
+
+void Scheduler::finish(Request& r, int reason) {
+  if (!r.blocks.empty()) bm_.free_blocks(r.blocks);
+  r.blocks.clear();
+  r.hashes.clear();
+  r.status = FINISHED;
+  r.finish = reason;
+}
+
+bool Scheduler::ensure_blocks(Request& r, int num_tokens) {
+  const int need = (num_tokens + cfg_.block_size - 1) / cfg_.block_size;
+  if (need > cfg_.max_blocks_per_seq) return false;
+  while ((int)r.blocks.size() < need) {
+    const int b = bm_.allocate();
+    if (b < 0) return false;
+    r.blocks.push_back(b);
+  }
+  return true;
+}
+
+void Scheduler::publish_full_blocks(Request& r) {
+  const int bs = cfg_.block_size;
+  while ((int)r.hashes.size() < (int)r.blocks.size() &&
+         ((int)r.hashes.size() + 1) * bs <= r.num_computed) {
+    const int i = (int)r.hashes.size();
+    const uint64_t parent = i ? r.hashes[i - 1] : 0;
+    const uint64_t h = BlockManager::hash_block(parent, r.tokens.data() + i * bs, bs);
+    bm_.register_full(r.blocks[i], h);
+    r.hashes.push_back(h);
+  }
+}
+
+void Scheduler::preempt(Request& r) {
+  bm_.free_blocks(r.blocks);
+  r.blocks.clear();
+  r.hashes.clear();
+  r.num_computed = 0;
+  r.prefix_checked = false;
+  r.status = WAITING;
+  r.num_preempt += 1;
+  ++preemptions_;
+  running_.erase(std::remove(running_.begin(), running_.end(), &r), running_.end());
+  waiting_.push_front(&r);
+}
+
+StepInfo Scheduler::schedule(BatchBuffers& buf) {
+  StepInfo info;
+  last_sampled_.clear();
+  const int bs = cfg_.block_size;
+  const int mb = cfg_.max_blocks_per_seq;
+  std::vector<std::pair<Request*, int>> sched;  // (request, q_len)
+
+  // ---------------- prefill (chunked) ----------------
+  int budget = std::min(cfg_.max_num_batched_tokens, buf.cap_tokens);
+  for (Request* r : running_) {
+    const int remaining = (int)r->tokens.size() - r->num_computed;
+    if (remaining <= 1 || budget <= 0) continue;
+    if ((int)sched.size() >= cfg_.max_num_seqs) break;
+    const int q = std::min(remaining, budget);
+    if (!ensure_blocks(*r, r->num_computed + q)) break;
+    sched.emplace_back(r, q);
+    budget -= q;
+  }
+  while (!waiting_.empty() && budget > 0 &&
+         (int)running_.size() < cfg_.max_num_seqs && (int)sched.size() < cfg_.max_num_seqs) {
+    Request* r = waiting_.front();
+    if (!r->prefix_checked) {
+      r->prefix_checked = true;
+      std::vector<int32_t> hb;
+      std::vector<uint64_t> hh;
+      const int hit = bm_.match_prefix(r->tokens, (int)r->tokens.size() - 1, hb, hh);
+      r->blocks = hb;
+      r->hashes = hh;
+      r->num_computed = hit;
+      r->num_cached = hit;
+    }
+    const int remaining = (int)r->tokens.size() - r->num_computed;
+    const int q = std::min(remaining, budget);
+    // keep a small reserve so admitted sequences can decode a few steps
+    if (!ensure_blocks(*r, r->num_computed + q)) break;
+    waiting_.pop_front();
+    r->status = RUNNING;
+    running_.push_back(r);
+    sched.emplace_back(r, q);
+    budget -= q;
+  }
+
+  if (!sched.empty()) {
+    info.is_prefill = 1;
+  } else {
+    // ---------------- decode ----------------
+    // oldest first; preempt from the young end when the pool runs dry
+    size_t i = 0;
+    while (i < running_.size()) {
+      Request* r = running_[i];
+      if ((int)sched.size() >= cfg_.max_num_seqs) break;
+      if (ensure_blocks(*r, r->num_computed + 1)) {
+        sched.emplace_back(r, 1);
+        ++i;
+        continue;
+      }
+      // out of blocks (or seq too long): preempt the youngest other sequence
+      Request* victim = running_.back();
+      if ((int)r->blocks.size() >= mb) {
+        finish(*r, FINISH_LENGTH);
+        running_.erase(running_.begin() + i);
+        continue;
+      }
+      preempt(*victim);
+      ++info.num_preempted;
+      if (victim == r) break;
+    }
+  }
+
+  // ---------------- flatten ----------------
+  int T = 0, tiles = 0, ns = 0;
+  for (size_t s = 0; s < sched.size(); ++s) {
+    Request* r = sched[s].first;
+    const int q = sched[s].second;
+    if (T + q > buf.cap_tokens) throw std::runtime_error("token buffer too small");
+    buf.q_start[s] = T;
+    const int start = r->num_computed;
+    for (int j = 0; j < q; ++j) {
+      const int pos = start + j;
+      buf.input_ids[T + j] = r->tokens[pos];
+      buf.positions[T + j] = pos;
+      buf.slots[T + j] = (int64_t)r->blocks[pos / bs] * bs + pos % bs;
+    }
+    const int kv = start + q;
+    buf.seq_lens[s] = kv;
+    info.max_seq_len = std::max(info.max_seq_len, kv);
+    int32_t* row = buf.block_tables + (size_t)s * mb;
+    const int nb = (int)r->blocks.size();
+    for (int b = 0; b < mb; ++b) row[b] = b < nb ? r->blocks[b] : 0;
+    buf.req_ids[s] = r->id;
+    if (info.is_prefill) {
+      const int rows = q * cfg_.gqa_group;
+      for (int t0 = 0; t0 < rows; t0 += cfg_.tile_rows) {
+        if (tiles >= buf.cap_tiles) throw std::runtime_error("tile buffer too small");
+        buf.tile_seq[tiles] = (int)s;
+        buf.tile_row[tiles] = t0;
+        ++tiles;
+      }
+    }
+    r->num_computed = kv;
+    const bool sample = kv == (int)r->tokens.size();
+    buf.sample_mask[s] = sample ? 1 : 0;
+    if (sample) {
+      buf.logits_idx[ns++] = T + q - 1;
+      last_sampled_.push_back(r);
+    }
+    T += q;
+  }
+  buf.q_start[sched.size()] = T;
+  info.num_seqs = (int)sched.size();
+  info.num_tokens = T;
+  info.num_tiles = tiles;
+  info.num_samples = ns;
+  return info;
+}
+
+void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_ids,
+                       std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish) {
+  if (n != (int)last_sampled_.size()) throw std::invalid_argument("sample count mismatch");
+  for (Request* r : running_) publish_full_blocks(*r);
+  for (int i = 0; i < n; ++i) {
+    Request* r = last_sampled_[i];
+    const int32_t tok = (int32_t)tokens[i];
+    r->tokens.push_back(tok);
+    int reason = NOT_FINISHED;
+    const int gen = r->num_generated();
+    if (!r->ignore_eos && gen > r->min_tokens - 1 && tok == cfg_.eos_id) reason = FINISH_STOP;
+    if (reason == NOT_FINISHED && gen >= r->min_tokens)
+      for (int32_t s : r->stop_ids)
+        if (s == tok) { reason = FINISH_STOP; break; }
+    if (reason == NOT_FINISHED &&
+        (gen >= r->max_tokens || (int)r->tokens.size() >= cfg_.max_model_len))
+      reason = FINISH_LENGTH;
+    out_ids.push_back(r->id);
+    out_tokens.push_back(tok);
+    out_finish.push_back(reason);
+    if (reason != NOT_FINISHED) {
+      running_.erase(std::remove(running_.begin(), running_.end(), r), running_.end());
+      finish(*r, reason);
+    }
+  }
+  last_sampled_.clear();
+}
+
+}  // namespace akap_rt

@@ -1,0 +1,122 @@
+// Continuous-batching scheduler core (host side, C++).
+//
+// Per engine step it picks the work, allocates KV blocks, and writes the flattened
+// batch description (token ids, positions, paged-cache slots, block tables, cu-seqlens,
+// attention tile map, logits rows) straight into caller-owned pinned buffers, so the
+// Python engine loop does no per-token work.  Policy:
+//   * chunked prefill under a token budget (prefill-first: best TTFT / throughput);
+//   * otherwise one decode token for every running sequence;
+//   * out of KV blocks -> preempt the youngest running sequence (recompute later).
+#pragma once
+
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "block_manager.h"
+
+namespace akap_rt {
+
+enum ReqStatus : int { WAITING = 0, RUNNING = 1, FINISHED = 2 };
+enum FinishReason : int { NOT_FINISHED = 0, FINISH_LENGTH = 1, FINISH_STOP = 2, FINISH_ABORT = 3 };
+
+struct Request {
+  int64_t id = 0;
+  std::vector<int32_t> tokens;  // prompt + generated
+  int num_prompt = 0;
+  int max_tokens = 16;
+  int min_tokens = 0;
+  bool ignore_eos = false;
+  std::vector<int32_t> stop_ids;
+  int num_computed = 0;  // tokens whose K/V are in the cache
+  int num_cached = 0;    // prefix-cache hit tokens (first schedule)
+  std::vector<int32_t> blocks;
+  std::vector<uint64_t> hashes;  // hashes of full, published blocks
+  int status = WAITING;
+  int finish = NOT_FINISHED;
+  int num_preempt = 0;
+  bool prefix_checked = false;
+  int num_generated() const { return (int)tokens.size() - num_prompt; }
+};
+
+struct SchedConfig {
+  int max_num_seqs = 256;
+  int max_num_batched_tokens = 8192;
+  int max_model_len = 4096;
+  int block_size = 32;
+  int gqa_group = 1;      // q heads per kv head (prefill tile map)
+  int tile_rows = 64;     // flattened query rows per prefill attention workgroup
+  int eos_id = -1;
+  int max_blocks_per_seq = 128;
+};
+
+// Views into caller buffers (numpy, pinned).  Sizes are checked by the binding.
+struct BatchBuffers {
+  int64_t* input_ids;
+  int64_t* positions;
+  int64_t* slots;
+  int32_t* seq_lens;
+  int32_t* q_start;
+  int32_t* block_tables;  // [max_num_seqs, max_blocks_per_seq]
+  int32_t* tile_seq;
+  int32_t* tile_row;
+  int64_t* logits_idx;
+  int64_t* req_ids;       // per scheduled seq
+  int32_t* sample_mask;   // per scheduled seq: 1 if its last token is sampled
+  int cap_tokens, cap_tiles;
+};
+
+struct StepInfo {
+  int is_prefill = 0;
+  int num_seqs = 0;
+  int num_tokens = 0;
+  int num_tiles = 0;
+  int num_samples = 0;
+  int max_seq_len = 0;
+  int num_preempted = 0;
+};
+
+class Scheduler {
+ public:
+  Scheduler(const SchedConfig& cfg, int num_blocks, bool prefix_cache);
+
+  void add_request(int64_t id, const std::vector<int32_t>& prompt, int max_tokens, int min_tokens,
+                   bool ignore_eos, const std::vector<int32_t>& stop_ids);
+  bool abort_request(int64_t id);
+  StepInfo schedule(BatchBuffers& buf);
+  // tokens[i] is the sample for the i-th sampled sequence of the last step.
+  // Emits (id, token, finish_reason) triples for every sampled sequence.
+  void update(const int64_t* tokens, int n, std::vector<int64_t>& out_ids,
+              std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish);
+
+  int num_waiting() const { return (int)waiting_.size(); }
+  int num_running() const { return (int)running_.size(); }
+  bool has_work() const { return !waiting_.empty() || !running_.empty(); }
+  const BlockManager& blocks() const { return bm_; }
+  BlockManager& blocks_mut() { return bm_; }
+  const Request* get(int64_t id) const;
+  std::vector<int32_t> block_table(int64_t id) const;
+  int64_t total_preemptions() const { return preemptions_; }
+  const SchedConfig& config() const { return cfg_; }
+  // drop a finished request's bookkeeping (called by the engine after delivery)
+  void release(int64_t id);
+
+ private:
+  bool ensure_blocks(Request& r, int num_tokens);
+  void publish_full_blocks(Request& r);
+  void preempt(Request& r);
+  void finish(Request& r, int reason);
+
+  SchedConfig cfg_;
+  BlockManager bm_;
+  std::unordered_map<int64_t, std::unique_ptr<Request>> reqs_;
+  std::deque<Request*> waiting_;
+  std::vector<Request*> running_;
+  std::vector<Request*> last_sampled_;  // order of samples in the last step
+  int64_t preemptions_ = 0;
+};
+
+}  // namespace akap_rt

@@ -1,0 +1,134 @@
+"""Mixture-of-experts FFN (Mixtral) with tensor-parallel or expert-parallel experts.
+
+Routing is the HIP `moe_topk_softmax` kernel; token grouping is `moe_align` (expert-
+sorted, tile-padded index list).  Two placements:
+  * "tp": every rank holds all experts with the FFN dim split by tp (one all-reduce,
+    like a dense layer) -- best at small batch on a single xGMI node;
+  * "ep": rank e holds experts [e*E/ep, (e+1)*E/ep) whole; tokens are dispatched and
+    combined with two RCCL all_to_all_single calls over the EP (=dp x tp) group.
+Expert GEMMs run per expert on the grouped, contiguous token slices (hipBLASLt).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..parallel import comm
+from ..parallel.state import ParallelState
+
+
+class MoEBlock:
+    def __init__(self, cfg, ps: ParallelState, device, dtype, g: torch.Generator,
+                 full_then_shard: bool, mode: Optional[str] = None):
+        self.cfg = cfg
+        self.ps = ps
+        self.device = device
+        self.dtype = dtype
+        self.E = cfg.num_experts
+        self.K = cfg.experts_per_token
+        self.mode = mode or os.environ.get("AKAP_MOE_MODE", "tp")
+        d, Fn = cfg.hidden_size, cfg.intermediate_size
+        tp, r = ps.tp_size, ps.tp_rank
+
+        def rand(*shape):
+            t = torch.empty(*shape, dtype=torch.float32, device=g.device)
+            t.normal_(0.0, 0.02, generator=g)
+            return t.to(dtype)
+
+        if self.mode == "ep":
+            ep = ps.world_size
+            if self.E % ep:
+                raise ValueError("num_experts must divide by the EP size")
+            self.ep, self.ep_rank = ep, ps.rank
+            self.e_local = self.E // ep
+            self.e0 = self.ep_rank * self.e_local
+            self.f_local = Fn
+        else:
+            self.ep, self.ep_rank = 1, 0
+            self.e_local, self.e0 = self.E, 0
+            self.f_local = Fn // tp
+        self.router = rand(self.E, d).to(device)
+        if full_then_shard:
+            w1 = rand(self.E, Fn, d)
+            w3 = rand(self.E, Fn, d)
+            w2 = rand(self.E, d, Fn)
+            if self.mode == "ep":
+                sl = slice(self.e0, self.e0 + self.e_local)
+                w13 = torch.cat([w1[sl], w3[sl]], 1)
+                w2s = w2[sl]
+            else:
+                fs = slice(r * self.f_local, (r + 1) * self.f_local)
+                w13 = torch.cat([w1[:, fs], w3[:, fs]], 1)
+                w2s = w2[:, :, fs]
+            self.w13 = w13.contiguous().to(device)
+            self.w2 = w2s.contiguous().to(device)
+        else:
+            self.w13 = rand(self.e_local, 2 * self.f_local, d).to(device)
+            self.w2 = rand(self.e_local, d, self.f_local).to(device)
+
+    def numel(self) -> int:
+        return self.router.numel() + self.w13.numel() + self.w2.numel()
+
+    def load_state_dict(self, sd: dict, prefix: str) -> None:
+        r, tp = self.ps.tp_rank, self.ps.tp_size
+        self.router.copy_(sd[prefix + "block_sparse_moe.gate.weight"])
+        for j in range(self.e_local):
+            e = self.e0 + j
+            p = f"{prefix}block_sparse_moe.experts.{e}."
+            w1, w3, w2 = sd[p + "w1.weight"], sd[p + "w3.weight"], sd[p + "w2.weight"]
+            if self.mode != "ep":
+                fs = slice(r * self.f_local, (r + 1) * self.f_local)
+                w1, w3, w2 = w1[fs], w3[fs], w2[:, fs]
+            self.w13[j].copy_(torch.cat([w1, w3], 0))
+            self.w2[j].copy_(w2)
+
+    def _experts(self, x: torch.Tensor, counts: list[int]) -> torch.Tensor:
+        """x: tokens grouped by local expert (counts[j] rows for expert j)."""
+        out = torch.empty(x.shape[0], x.shape[1], dtype=x.dtype, device=x.device)
+        o = 0
+        for j, c in enumerate(counts):
+            if c == 0:
+                continue
+            seg = x[o:o + c]
+            h = ops.silu_and_mul(F.linear(seg, self.w13[j]))
+            out[o:o + c] = F.linear(h, self.w2[j])
+            o += c
+        return out
+
+    def forward(self, h: torch.Tensor) -> torch.Tensor:
+        T, d = h.shape
+        logits = F.linear(h, self.router)
+        w, ids = ops.moe_topk_softmax(logits, self.K, renormalize=True)
+        flat = ids.reshape(-1).long()
+        order = torch.argsort(flat, stable=True)
+        tok_of = order // self.K
+        if self.mode == "ep":
+            owner = flat[order] // self.e_local
+            send_counts = torch.bincount(owner, minlength=self.ep)
+            recv_counts = torch.empty_like(send_counts)
+            torch.distributed.all_to_all_single(recv_counts, send_counts)
+            sc, rc = send_counts.tolist(), recv_counts.tolist()
+            x_send = h[tok_of]
+            e_send = flat[order].to(torch.int32)
+            x_recv = comm.all_to_all(x_send, rc, sc)
+            e_recv = comm.all_to_all(e_send, rc, sc).long() - self.e0
+            o2 = torch.argsort(e_recv, stable=True)
+            counts = torch.bincount(e_recv, minlength=self.e_local).tolist()
+            y_sorted = self._experts(x_recv[o2], counts)
+            y_recv = torch.empty_like(y_sorted)
+            y_recv[o2] = y_sorted
+            y_back = comm.all_to_all(y_recv, sc, rc)
+        else:
+            counts = torch.bincount(flat, minlength=self.E).tolist()
+            y_back = self._experts(h[tok_of], counts)
+        wt = w.reshape(-1)[order].to(torch.float32)
+        out = torch.zeros(T, d, dtype=torch.float32, device=h.device)
+        out.index_add_(0, tok_of, y_back.float() * wt[:, None])
+        out = out.to(h.dtype)
+        if self.mode != "ep":
+            comm.tp_all_reduce(out)
+        return out

@@ -1,0 +1,285 @@
+"""Decoder-only transformer (Qwen3 / Llama-3 / Mixtral) on the gfx950 kernels.
+
+MI355X-first structure (not a module-per-op port):
+  * fused weights: one QKV projection [ (Hq+2Hkv)*D, d ] and one gate|up projection
+    [2F, d] per layer, so each layer is 4 large hipBLASLt GEMMs + 5 hand-written kernels
+    (fused add+RMSNorm x2, QK-norm+RoPE+KV-write, paged attention, SiLU*mul);
+  * the residual stream is updated in place by the fused add+norm kernel;
+  * tensor parallel: QKV / gate_up column-split by heads / ffn rows, O / down row-split
+    with one RCCL all-reduce each, vocab-parallel embedding + LM head;
+  * everything in forward() is allocation-stable and sync-free on the decode path, so
+    the engine captures it in a hipGraph per batch-size bucket.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as ref
+from ..parallel import comm
+from ..parallel.state import ParallelState, get_state
+from .config import ModelConfig
+from .moe import MoEBlock
+
+
+@dataclasses.dataclass
+class AttnBatch:
+    """Flattened batch description consumed by the attention kernels."""
+    is_prefill: bool
+    positions: torch.Tensor      # [T] int64
+    slots: torch.Tensor          # [T] int64 (-1 = padding)
+    block_tables: torch.Tensor   # [B, max_blocks] int32
+    seq_lens: torch.Tensor       # [B] int32
+    q_start: torch.Tensor        # [B+1] int32
+    tile_seq: Optional[torch.Tensor] = None  # prefill tile map
+    tile_row: Optional[torch.Tensor] = None
+    num_parts: int = 1           # decode split-KV partitions
+    part_size: int = 512
+    workspace: Optional[tuple] = None
+
+
+@dataclasses.dataclass
+class LayerWeights:
+    ln1: torch.Tensor
+    ln2: torch.Tensor
+    w_qkv: torch.Tensor
+    w_o: torch.Tensor
+    q_norm: Optional[torch.Tensor]
+    k_norm: Optional[torch.Tensor]
+    w_gate_up: Optional[torch.Tensor]
+    w_down: Optional[torch.Tensor]
+    moe: Optional[MoEBlock] = None
+
+
+def _shard_rows(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
+    n = w.shape[0] // size
+    return w[rank * n:(rank + 1) * n]
+
+
+def _shard_cols(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
+    n = w.shape[1] // size
+    return w[:, rank * n:(rank + 1) * n]
+
+
+class DecoderLM:
+    """Weights + forward for one tensor-parallel rank."""
+
+    def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu",
+                 dtype: torch.dtype = torch.bfloat16, seed: int = 0,
+                 pstate: Optional[ParallelState] = None, max_model_len: int = 4096,
+                 full_then_shard: bool = False):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.ps = pstate or get_state()
+        tp, r = self.ps.tp_size, self.ps.tp_rank
+        if cfg.num_heads % tp:
+            raise ValueError("num_heads must divide by tp")
+        self.hq = cfg.num_heads // tp
+        self.hkv = max(1, cfg.num_kv_heads // tp)
+        self.kv_replicas = max(1, tp // cfg.num_kv_heads)
+        self.D = cfg.head_dim
+        self.ffn = cfg.intermediate_size // tp
+        self.vocab_per = math.ceil(cfg.vocab_size / tp)
+        self.vocab_start = r * self.vocab_per
+        self.vocab_end = min(cfg.vocab_size, self.vocab_start + self.vocab_per)
+        self.scale = 1.0 / math.sqrt(self.D)
+        self._init_weights(seed, full_then_shard)
+        self.cos_sin = ref.rope_cos_sin(min(cfg.max_position, max(max_model_len, 16)), self.D,
+                                        cfg.rope_theta, cfg.rope_scaling, device=self.device)
+
+    # ------------------------------------------------------------------ weights
+    def _rand(self, g: torch.Generator, *shape, std: float = 0.02) -> torch.Tensor:
+        t = torch.empty(*shape, dtype=torch.float32, device=g.device)
+        t.normal_(0.0, std, generator=g)
+        return t.to(self.dtype)
+
+    def _init_weights(self, seed: int, full_then_shard: bool) -> None:
+        cfg, tp, r = self.cfg, self.ps.tp_size, self.ps.tp_rank
+        d, D = cfg.hidden_size, self.D
+        gdev = self.device if self.device.type == "cuda" else torch.device("cpu")
+        # Full-then-shard (tests): identical logical weights for any tp.  Otherwise each
+        # rank draws only its shard (70B at TP=8 never materialises the full model).
+        g = torch.Generator(device=gdev)
+        g.manual_seed(seed if full_then_shard else seed * 1000 + r)
+        to = dict(device=self.device)
+        one = lambda n: torch.ones(n, dtype=self.dtype, **to)  # noqa: E731
+
+        def rows(full_rows, cols, shard_rows):
+            if full_then_shard:
+                return _shard_rows(self._rand(g, full_rows, cols), r, tp).to(**to)
+            return self._rand(g, shard_rows, cols).to(**to)
+
+        vp = self.vocab_per
+        if full_then_shard:
+            emb_full = self._rand(g, vp * tp, d)
+            emb_full[cfg.vocab_size:] = 0
+            self.embed = emb_full[r * vp:(r + 1) * vp].contiguous().to(**to)
+        else:
+            self.embed = self._rand(g, vp, d).to(**to)
+            self.embed[self.vocab_end - self.vocab_start:] = 0
+        self.layers: list[LayerWeights] = []
+        for _ in range(cfg.num_layers):
+            if full_then_shard:
+                wq = self._rand(g, cfg.q_size, d)
+                wk = self._rand(g, cfg.kv_size, d)
+                wv = self._rand(g, cfg.kv_size, d)
+                wo = self._rand(g, d, cfg.q_size)
+                q_sh = _shard_rows(wq, r, tp)
+                k0, k1 = self._kv_head_range()
+                k_sh, v_sh = wk[k0 * D:k1 * D], wv[k0 * D:k1 * D]
+                w_qkv = torch.cat([q_sh, k_sh, v_sh], 0).contiguous().to(**to)
+                w_o = _shard_cols(wo, r, tp).contiguous().to(**to)
+            else:
+                w_qkv = self._rand(g, (self.hq + 2 * self.hkv) * D, d).to(**to)
+                w_o = self._rand(g, d, self.hq * D).to(**to)
+            qn = one(D) if cfg.qk_norm else None
+            kn = one(D) if cfg.qk_norm else None
+            if cfg.is_moe:
+                moe = MoEBlock(cfg, self.ps, self.device, self.dtype, g, full_then_shard)
+                lw = LayerWeights(one(d), one(d), w_qkv, w_o, qn, kn, None, None, moe)
+            else:
+                if full_then_shard:
+                    wg = self._rand(g, cfg.intermediate_size, d)
+                    wu = self._rand(g, cfg.intermediate_size, d)
+                    wd = self._rand(g, d, cfg.intermediate_size)
+                    w_gu = torch.cat([_shard_rows(wg, r, tp), _shard_rows(wu, r, tp)], 0).contiguous().to(**to)
+                    w_d = _shard_cols(wd, r, tp).contiguous().to(**to)
+                else:
+                    w_gu = self._rand(g, 2 * self.ffn, d).to(**to)
+                    w_d = self._rand(g, d, self.ffn).to(**to)
+                lw = LayerWeights(one(d), one(d), w_qkv, w_o, qn, kn, w_gu, w_d)
+            self.layers.append(lw)
+        self.final_norm = one(d)
+        if cfg.tie_embeddings:
+            self.lm_head = self.embed
+        elif full_then_shard:
+            lm = self._rand(g, vp * tp, d)
+            lm[cfg.vocab_size:] = 0
+            self.lm_head = lm[r * vp:(r + 1) * vp].contiguous().to(**to)
+        else:
+            self.lm_head = self._rand(g, vp, d).to(**to)
+            self.lm_head[self.vocab_end - self.vocab_start:] = 0
+
+    def _kv_head_range(self) -> tuple[int, int]:
+        """kv heads owned by this TP rank (replicated when tp > num_kv_heads)."""
+        tp, r, H = self.ps.tp_size, self.ps.tp_rank, self.cfg.num_kv_heads
+        if H >= tp:
+            return r * H // tp, (r + 1) * H // tp
+        h = r // (tp // H)
+        return h, h + 1
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.final_norm.numel()
+        if self.lm_head is not self.embed:
+            n += self.lm_head.numel()
+        for lw in self.layers:
+            for t in (lw.ln1, lw.ln2, lw.w_qkv, lw.w_o, lw.q_norm, lw.k_norm, lw.w_gate_up,
+                      lw.w_down):
+                if t is not None:
+                    n += t.numel()
+            if lw.moe is not None:
+                n += lw.moe.numel()
+        return n * 2
+
+    def load_state_dict(self, sd: dict) -> None:
+        """Load HF-named tensors (safetensors from the model PVC) into the fused layout."""
+        cfg, tp, r = self.cfg, self.ps.tp_size, self.ps.tp_rank
+        cp = lambda dst, src: dst.copy_(src.to(dst.dtype))  # noqa: E731
+        emb = sd["model.embed_tokens.weight"]
+        n = self.vocab_end - self.vocab_start
+        cp(self.embed[:n], emb[self.vocab_start:self.vocab_end])
+        for i, lw in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            cp(lw.ln1, sd[p + "input_layernorm.weight"])
+            cp(lw.ln2, sd[p + "post_attention_layernorm.weight"])
+            q = _shard_rows(sd[p + "self_attn.q_proj.weight"], r, tp)
+            k0, k1 = self._kv_head_range()
+            D = self.D
+            k = sd[p + "self_attn.k_proj.weight"][k0 * D:k1 * D]
+            v = sd[p + "self_attn.v_proj.weight"][k0 * D:k1 * D]
+            cp(lw.w_qkv, torch.cat([q, k, v], 0))
+            cp(lw.w_o, _shard_cols(sd[p + "self_attn.o_proj.weight"], r, tp))
+            if lw.q_norm is not None:
+                cp(lw.q_norm, sd[p + "self_attn.q_norm.weight"])
+                cp(lw.k_norm, sd[p + "self_attn.k_norm.weight"])
+            if lw.moe is not None:
+                lw.moe.load_state_dict(sd, p)
+            else:
+                g_ = _shard_rows(sd[p + "mlp.gate_proj.weight"], r, tp)
+                u_ = _shard_rows(sd[p + "mlp.up_proj.weight"], r, tp)
+                cp(lw.w_gate_up, torch.cat([g_, u_], 0))
+                cp(lw.w_down, _shard_cols(sd[p + "mlp.down_proj.weight"], r, tp))
+        cp(self.final_norm, sd["model.norm.weight"])
+        if not cfg.tie_embeddings:
+            cp(self.lm_head[:n], sd["lm_head.weight"][self.vocab_start:self.vocab_end])
+
+    # ------------------------------------------------------------------ kv cache
+    def allocate_kv_cache(self, num_blocks: int, block_size: int) -> torch.Tensor:
+        """One allocation [L, 2, NB, Hkv*BS*D] (K block = [Hkv,BS,D], V block = [Hkv,D,BS]),
+        zero-filled so never-written slots read as finite zeros."""
+        per_block = self.hkv * block_size * self.D
+        return torch.zeros(self.cfg.num_layers, 2, num_blocks, per_block, dtype=self.dtype,
+                           device=self.device)
+
+    def cache_views(self, kv: torch.Tensor, block_size: int):
+        NB = kv.shape[2]
+        ks = [kv[l, 0].view(NB, self.hkv, block_size, self.D) for l in range(kv.shape[0])]
+        vs = [kv[l, 1].view(NB, self.hkv, self.D, block_size) for l in range(kv.shape[0])]
+        return ks, vs
+
+    # ------------------------------------------------------------------ forward
+    def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
+        x = ops.embedding(ids, self.embed, vocab_start=self.vocab_start, vocab_end=self.vocab_end)
+        return comm.tp_all_reduce(x)
+
+    def _attention(self, q, batch: AttnBatch, kc, vc, out):
+        if batch.is_prefill:
+            ops.paged_attention_prefill(out, q, kc, vc, batch.block_tables, batch.seq_lens,
+                                        batch.q_start, batch.tile_seq, batch.tile_row,
+                                        self.hq // self.hkv, self.scale)
+        else:
+            ops.paged_attention_decode(out, q, kc, vc, batch.block_tables, batch.seq_lens,
+                                       self.hq // self.hkv, self.scale, workspace=batch.workspace,
+                                       num_parts=batch.num_parts, part_size=batch.part_size)
+        return out
+
+    def forward(self, input_ids: torch.Tensor, batch: AttnBatch, k_caches, v_caches
+                ) -> torch.Tensor:
+        cfg = self.cfg
+        T = input_ids.shape[0]
+        eps = cfg.rms_eps
+        x = self.embed_tokens(input_ids)
+        residual = x
+        h = ops.rms_norm(x, self.layers[0].ln1, eps)
+        x = None
+        for li, lw in enumerate(self.layers):
+            if li > 0:
+                h, residual = ops.fused_add_rms_norm(x, residual, lw.ln1, eps)
+            qkv = F.linear(h, lw.w_qkv)
+            q = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+            ops.qk_norm_rope_cache(qkv, q, k_caches[li], v_caches[li], batch.positions,
+                                   batch.slots, self.cos_sin, lw.q_norm, lw.k_norm, self.hq,
+                                   self.hkv, eps, True)
+            attn = torch.empty_like(q)
+            self._attention(q, batch, k_caches[li], v_caches[li], attn)
+            o = comm.tp_all_reduce(F.linear(attn.view(T, self.hq * self.D), lw.w_o))
+            h, residual = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
+            if lw.moe is not None:
+                x = lw.moe.forward(h)
+            else:
+                gu = F.linear(h, lw.w_gate_up)
+                x = comm.tp_all_reduce(F.linear(ops.silu_and_mul(gu), lw.w_down))
+        h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
+        return h
+
+    def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(h, self.lm_head)
+        if self.ps.tp_size > 1:
+            logits = comm.tp_all_gather_last(logits)
+        return logits[:, : self.cfg.vocab_size]

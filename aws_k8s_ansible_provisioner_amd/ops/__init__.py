@@ -1,0 +1,244 @@
+"""Python entry points of the gfx950 kernels.
+
+Every op dispatches on the device of its inputs:
+  * GPU tensors  -> the hand-written HIP kernel in ``_C.so`` (``torch.ops.akap.*``).
+    If the extension is missing on a GPU box this RAISES -- there is no silent
+    eager fallback on the GPU path.
+  * CPU tensors  -> a plain PyTorch reference of the same op (used by the CPU test
+    suite, the CPU mock engine and as the numerics oracle of the GPU tests).
+
+Layouts shared with the kernels (see csrc/kernels/rope_cache.hip):
+  K cache [num_blocks, Hkv, BS, D], V cache [num_blocks, Hkv, D, BS] (V^T per block).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB = os.path.join(_PKG, "_C.so")
+_loaded = False
+_load_error: Optional[str] = None
+
+
+def load_native(required: bool = False) -> bool:
+    """Load ``_C.so`` (torch.ops.akap).  Returns True when available."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    if not os.path.exists(_LIB):
+        _load_error = f"{_LIB} not built (run python -m aws_k8s_ansible_provisioner_amd.build_ext)"
+    else:
+        try:
+            torch.ops.load_library(_LIB)
+            _loaded = True
+        except Exception as e:  # pragma: no cover - depends on the box
+            _load_error = repr(e)
+    if required and not _loaded:
+        raise RuntimeError("native HIP kernels unavailable: " + str(_load_error))
+    return _loaded
+
+
+def native_available() -> bool:
+    return load_native(False)
+
+
+def _native(t: torch.Tensor) -> bool:
+    if t.is_cuda:
+        load_native(required=True)
+        return True
+    return False
+
+
+# ----------------------------------------------------------------------------- norms
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None):
+    if out is None:
+        out = torch.empty_like(x)
+    if _native(x):
+        torch.ops.akap.rmsnorm(out, x, w, eps)
+        return out
+    out.copy_(ref.rms_norm(x, w, eps))
+    return out
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                       out: Optional[torch.Tensor] = None):
+    """residual += x (in place); returns (rmsnorm(residual), residual)."""
+    if out is None:
+        out = torch.empty_like(x)
+    if _native(x):
+        torch.ops.akap.fused_add_rmsnorm(out, residual, x, w, eps)
+        return out, residual
+    r = (x.float() + residual.float()).to(x.dtype)
+    residual.copy_(r)
+    out.copy_(ref.rms_norm(r, w, eps))
+    return out, residual
+
+
+# ----------------------------------------------------------------------------- rope/cache
+def qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
+                       num_q_heads: int, num_kv_heads: int, eps: float, apply_rope: bool = True):
+    if _native(qkv):
+        torch.ops.akap.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin,
+                                          q_w, k_w, num_q_heads, num_kv_heads, eps, apply_rope)
+        return q_out
+    ref.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
+                           num_q_heads, num_kv_heads, eps, apply_rope)
+    return q_out
+
+
+def reshape_and_cache(k, v, k_cache, v_cache, slots):
+    if _native(k):
+        torch.ops.akap.reshape_and_cache(k, v, k_cache, v_cache, slots)
+        return
+    ref.reshape_and_cache(k, v, k_cache, v_cache, slots)
+
+
+# ----------------------------------------------------------------------------- mlp
+def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
+    F = x.shape[-1] // 2
+    if out is None:
+        out = torch.empty(*x.shape[:-1], F, dtype=x.dtype, device=x.device)
+    if _native(x):
+        torch.ops.akap.silu_and_mul(out, x)
+        return out
+    out.copy_(ref.silu_and_mul(x))
+    return out
+
+
+# ----------------------------------------------------------------------------- attention
+def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_start, tile_seq,
+                            tile_row, gqa_group: int, scale: float):
+    if _native(q):
+        torch.ops.akap.paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens,
+                                               q_start, tile_seq, tile_row, gqa_group, scale)
+        return out
+    out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale))
+    return out
+
+
+def paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens, gqa_group: int,
+                           scale: float, workspace=None, num_parts: int = 1,
+                           part_size: int = 512, q_start=None):
+    if _native(q):
+        if workspace is None:
+            B = seq_lens.numel()
+            Hkv = k_cache.shape[1]
+            workspace = decode_workspace(B, Hkv, gqa_group, num_parts, q.device)
+        pm, pl, po = workspace
+        torch.ops.akap.paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens,
+                                              q_start, pm, pl, po, num_parts, part_size,
+                                              gqa_group, scale)
+        return out
+    if q_start is None:
+        q_start = torch.arange(seq_lens.numel() + 1, dtype=torch.int32)
+    out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale))
+    return out
+
+
+def decode_workspace(max_seqs: int, num_kv_heads: int, gqa_group: int, num_parts: int,
+                     device) -> tuple:
+    n = max(1, max_seqs * num_kv_heads * max(num_parts, 1) * gqa_group)
+    pm = torch.empty(n, dtype=torch.float32, device=device)
+    pl = torch.empty(n, dtype=torch.float32, device=device)
+    po = torch.empty(n * 128 if num_parts > 1 else 1, dtype=torch.float32, device=device)
+    return pm, pl, po
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out_logprobs=None):
+    B = logits.shape[0]
+    if out_tokens is None:
+        out_tokens = torch.empty(B, dtype=torch.int64, device=logits.device)
+    if out_logprobs is None:
+        out_logprobs = torch.empty(B, dtype=torch.float32, device=logits.device)
+    if _native(logits):
+        torch.ops.akap.sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens,
+                              out_logprobs)
+        return out_tokens, out_logprobs
+    t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps)
+    out_tokens.copy_(t)
+    out_logprobs.copy_(lp)
+    return out_tokens, out_logprobs
+
+
+def argmax(logits, out=None):
+    if out is None:
+        out = torch.empty(logits.shape[0], dtype=torch.int64, device=logits.device)
+    if _native(logits):
+        torch.ops.akap.argmax(logits, out)
+        return out
+    out.copy_(logits.float().argmax(dim=-1))
+    return out
+
+
+# ----------------------------------------------------------------------------- misc
+def embedding(ids, table, out=None, vocab_start: int = 0, vocab_end: Optional[int] = None):
+    if vocab_end is None:
+        vocab_end = vocab_start + table.shape[0]
+    if out is None:
+        out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
+    if _native(ids):
+        torch.ops.akap.embedding(ids, table, out, vocab_start, vocab_end)
+        return out
+    out.copy_(ref.embedding(ids, table, vocab_start, vocab_end))
+    return out
+
+
+def moe_topk_softmax(router_logits, top_k: int, renormalize: bool = True):
+    T = router_logits.shape[0]
+    w = torch.empty(T, top_k, dtype=torch.float32, device=router_logits.device)
+    ids = torch.empty(T, top_k, dtype=torch.int32, device=router_logits.device)
+    if _native(router_logits):
+        torch.ops.akap.moe_topk_softmax(router_logits, w, ids, renormalize)
+        return w, ids
+    rw, rid = ref.moe_topk_softmax(router_logits, top_k, renormalize)
+    w.copy_(rw)
+    ids.copy_(rid)
+    return w, ids
+
+
+def moe_align(topk_ids, num_experts: int, block: int):
+    n = topk_ids.numel()
+    cap = n + num_experts * (block - 1)
+    cap = (cap + block - 1) // block * block
+    dev = topk_ids.device
+    sorted_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    offsets = torch.empty(num_experts + 1, dtype=torch.int32, device=dev)
+    num_padded = torch.empty(1, dtype=torch.int32, device=dev)
+    if _native(topk_ids):
+        torch.ops.akap.moe_align(topk_ids.contiguous(), num_experts, block, sorted_ids, offsets,
+                                 num_padded)
+        return sorted_ids, offsets, num_padded
+    s, o, npad = ref.moe_align(topk_ids, num_experts, block, cap)
+    sorted_ids.copy_(s)
+    offsets.copy_(o)
+    num_padded.fill_(npad)
+    return sorted_ids, offsets, num_padded
+
+
+def kv_gather(cache_planes, block_ids, out=None):
+    planes = cache_planes.shape[0]
+    blk = cache_planes[0, 0].numel()
+    if out is None:
+        out = torch.empty(planes, block_ids.numel(), blk, dtype=cache_planes.dtype,
+                          device=cache_planes.device)
+    if _native(cache_planes):
+        torch.ops.akap.kv_gather(cache_planes, block_ids, out)
+        return out
+    out.copy_(cache_planes.reshape(planes, cache_planes.shape[1], blk)[:, block_ids.long()])
+    return out
+
+
+def kv_scatter(buf, cache_planes, block_ids):
+    if _native(cache_planes):
+        torch.ops.akap.kv_scatter(buf, cache_planes, block_ids)
+        return
+    planes = cache_planes.shape[0]
+    blk = cache_planes[0, 0].numel()
+    view = cache_planes.view(planes, cache_planes.shape[1], blk)
+    view[:, block_ids.long()] = buf.view(planes, block_ids.numel(), blk)

@@ -1,0 +1,197 @@
+"""Plain-PyTorch (fp32-accumulating) reference implementations of every kernel.
+
+They define the semantics the HIP kernels are tested against and serve the CPU
+engine path.  Cache layouts: K [NB, Hkv, BS, D], V [NB, Hkv, D, BS].
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    inv = torch.rsqrt(xf.pow(2).mean(dim=-1, keepdim=True) + eps)
+    return (xf * inv * w.float()).to(x.dtype)
+
+
+def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
+    F = x.shape[-1] // 2
+    g, u = x[..., :F], x[..., F:]
+    return (torch.nn.functional.silu(g.float()).to(x.dtype).float() * u.float()).to(x.dtype)
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, scaling: dict | None = None,
+                 device=None) -> torch.Tensor:
+    """fp32 table [max_pos, D] = [cos | sin] for NeoX-style (rotate-half) rotary."""
+    inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        lo = scaling.get("low_freq_factor", 1.0)
+        hi = scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        low_wl, high_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv_freq
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > low_wl, inv_freq / factor, inv_freq)
+        mid = (wl <= low_wl) & (wl >= high_wl)
+        scaled = torch.where(mid, (1 - smooth) * inv_freq / factor + smooth * inv_freq, scaled)
+        inv_freq = scaled
+    t = torch.arange(max_pos, dtype=torch.float64)
+    freqs = torch.outer(t, inv_freq)
+    cs = torch.cat([freqs.cos(), freqs.sin()], dim=-1).float()
+    return cs.to(device) if device is not None else cs
+
+
+def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
+    """x [T, H, D] (float) -> rotated (float)."""
+    D = x.shape[-1]
+    half = D // 2
+    cs = cos_sin[positions.long()]
+    c = cs[:, None, :half]
+    s = cs[:, None, half:]
+    x1, x2 = x[..., :half], x[..., half:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+def write_cache(k: torch.Tensor, v: torch.Tensor, k_cache, v_cache, slots) -> None:
+    BS = k_cache.shape[2]
+    for t in range(k.shape[0]):
+        s = int(slots[t])
+        if s < 0:
+            continue
+        b, o = divmod(s, BS)
+        k_cache[b, :, o, :] = k[t].to(k_cache.dtype)
+        v_cache[b, :, :, o] = v[t].to(v_cache.dtype)
+
+
+def qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w, Hq,
+                       Hkv, eps, apply_rope_flag=True):
+    T = qkv.shape[0]
+    D = k_cache.shape[3]
+    q = qkv[:, : Hq * D].reshape(T, Hq, D)
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].reshape(T, Hkv, D)
+    v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(T, Hkv, D)
+    if q_w is not None:
+        q = rms_norm(q, q_w, eps)
+    if k_w is not None:
+        k = rms_norm(k, k_w, eps)
+    qf, kf = q.float(), k.float()
+    if apply_rope_flag:
+        qf = apply_rope(qf, positions[:T], cos_sin)
+        kf = apply_rope(kf, positions[:T], cos_sin)
+    q_out.copy_(qf.to(q_out.dtype).reshape(q_out.shape))
+    write_cache(kf.to(qkv.dtype), v, k_cache, v_cache, slots[:T])
+
+
+def reshape_and_cache(k, v, k_cache, v_cache, slots):
+    write_cache(k, v, k_cache, v_cache, slots)
+
+
+def gather_kv(k_cache, v_cache, block_table, kv_len: int):
+    """-> K [kv_len, Hkv, D], V [kv_len, Hkv, D] from the paged caches."""
+    BS = k_cache.shape[2]
+    nb = (kv_len + BS - 1) // BS
+    blocks = block_table[:nb].long()
+    K = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * BS, k_cache.shape[1], -1)[:kv_len]
+    V = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * BS, v_cache.shape[1], -1)[:kv_len]
+    return K, V
+
+
+def paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale):
+    """Causal attention of each sequence's new tokens over its paged context.
+    q [T, Hq, D]; q_start [B+1] cumulative; seq_lens [B] (kv incl. new tokens)."""
+    out = torch.zeros_like(q)
+    B = seq_lens.numel()
+    Hq = q.shape[1]
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    for b in range(B):
+        q0, q1 = int(q_start[b]), int(q_start[b + 1])
+        ql = q1 - q0
+        if ql == 0:
+            continue
+        kv = int(seq_lens[b])
+        K, V = gather_kv(k_cache, v_cache, block_tables[b], kv)
+        Kf = K.float().repeat_interleave(G, dim=1)  # [kv, Hq, D]
+        Vf = V.float().repeat_interleave(G, dim=1)
+        qf = q[q0:q1].float()  # [ql, Hq, D]
+        s = torch.einsum("qhd,khd->hqk", qf, Kf) * scale
+        qpos = torch.arange(kv - ql, kv).view(-1, 1)
+        kpos = torch.arange(kv).view(1, -1)
+        s = s.masked_fill((kpos > qpos)[None], float("-inf"))
+        p = torch.softmax(s, dim=-1)
+        o = torch.einsum("hqk,khd->qhd", p, Vf)
+        out[q0:q1] = o.to(q.dtype)
+    return out
+
+
+def sample(logits, temperature, top_k, top_p, seeds, steps):
+    """Reference sampler: greedy for T<=0; else top-k, then top-p (on the top-k
+    renormalised distribution), then a draw.  Draws use torch's RNG seeded per row,
+    so only the distribution (not the exact token) matches the kernel."""
+    B, V = logits.shape
+    toks = torch.empty(B, dtype=torch.int64)
+    lps = torch.empty(B, dtype=torch.float32)
+    for i in range(B):
+        x = logits[i].float().cpu()
+        T = float(temperature[i])
+        if T <= 0:
+            toks[i] = int(x.argmax())
+            lps[i] = 0.0
+            continue
+        z = x / T
+        logp = torch.log_softmax(z, dim=-1)
+        keep = torch.ones(V, dtype=torch.bool)
+        k = int(top_k[i])
+        if 0 < k < V:
+            kth = torch.topk(z, k).values[-1]
+            keep &= z >= kth
+        p = float(top_p[i])
+        if p < 1.0:
+            zz = z.masked_fill(~keep, float("-inf"))
+            probs = torch.softmax(zz, dim=-1)
+            sp, si = probs.sort(descending=True)
+            cum = sp.cumsum(0)
+            n = int((cum < p).sum()) + 1
+            thr = sp[min(n, V) - 1]
+            keep &= probs >= thr
+        g = torch.Generator().manual_seed(int(seeds[i]) * 1000003 + int(steps[i]))
+        zz = z.masked_fill(~keep, float("-inf"))
+        pr = torch.softmax(zz, dim=-1)
+        t = int(torch.multinomial(pr, 1, generator=g))
+        toks[i] = t
+        lps[i] = float(logp[t])
+    return toks.to(logits.device), lps.to(logits.device)
+
+
+def embedding(ids, table, vs, ve):
+    ids = ids.long()
+    mask = (ids >= vs) & (ids < ve)
+    local = (ids - vs).clamp(0, table.shape[0] - 1)
+    out = table[local]
+    return out * mask[:, None].to(out.dtype)
+
+
+def moe_topk_softmax(logits, top_k, renorm=True):
+    p = torch.softmax(logits.float(), dim=-1)
+    w, ids = torch.topk(p, top_k, dim=-1)
+    if renorm:
+        w = w / w.sum(dim=-1, keepdim=True)
+    return w, ids.to(torch.int32)
+
+
+def moe_align(topk_ids, E, block, cap):
+    flat = topk_ids.reshape(-1).long().cpu()
+    n = flat.numel()
+    sorted_ids = torch.full((cap,), n, dtype=torch.int32)
+    offsets = torch.zeros(E + 1, dtype=torch.int32)
+    acc = 0
+    for e in range(E):
+        idx = (flat == e).nonzero().flatten()
+        offsets[e] = acc
+        sorted_ids[acc:acc + idx.numel()] = idx.to(torch.int32)
+        acc += (idx.numel() + block - 1) // block * block
+    offsets[E] = acc
+    return sorted_ids.to(topk_ids.device), offsets.to(topk_ids.device), acc

@@ -1,0 +1,57 @@
+"""Collectives used by the model (TP / EP / P-D) on RCCL over xGMI.
+
+MI355X nodes are a fully-connected xGMI mesh (7 links x ~153 GB/s per GPU), not a
+switch: a ring all-reduce is bound by one link per hop.  The policy here:
+  * small decode-time all-reduces (a few KB-MB per layer) -> one RCCL all_reduce
+    call in-place on the activation (RCCL picks its LL/LL128 protocols for these);
+  * vocab-parallel logits -> all_gather into a pre-allocated buffer;
+  * MoE token dispatch/combine -> all_to_all_single with explicit split sizes;
+  * KV hand-off (P/D) -> one packed send/recv per request (see parallel/kv_transfer.py).
+All functions are no-ops for a group of size 1, so single-GPU code paths pay nothing.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .state import get_state
+
+
+def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    st = get_state()
+    if st.tp_size == 1:
+        return x
+    dist.all_reduce(x, group=st.tp_group)
+    return x
+
+
+def tp_all_gather_last(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Gather shards along the last dim: [.., n] x tp -> [.., n*tp]."""
+    st = get_state()
+    if st.tp_size == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(st.tp_size)]
+    dist.all_gather(parts, x.contiguous(), group=st.tp_group)
+    res = torch.cat(parts, dim=-1)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def all_to_all(x: torch.Tensor, out_splits: list[int], in_splits: list[int], group=None
+               ) -> torch.Tensor:
+    out = x.new_empty((sum(out_splits),) + tuple(x.shape[1:]))
+    dist.all_to_all_single(out, x.contiguous(), out_splits, in_splits, group=group)
+    return out
+
+
+def broadcast_object(obj, src: int = 0, group=None):
+    st = get_state()
+    if st.world_size == 1:
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src, group=group)
+    return lst[0]

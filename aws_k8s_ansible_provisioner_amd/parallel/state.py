@@ -1,0 +1,104 @@
+"""Process-group state: one process per GPU, torch.distributed over RCCL ("nccl" on ROCm).
+
+Groups:
+  * world  -- every engine rank of this job
+  * tp     -- tensor-parallel group (contiguous ranks: TP stays inside one node's xGMI mesh)
+  * dp     -- ranks with the same tp rank (replica / expert-parallel axis)
+
+On CPU (tests) the same code runs on the gloo backend.
+"""
+from __future__ import annotations
+
+import dataclasses
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclasses.dataclass
+class ParallelState:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    tp_size: int = 1
+    tp_rank: int = 0
+    dp_size: int = 1
+    dp_rank: int = 0
+    tp_group: Optional[object] = None
+    dp_group: Optional[object] = None
+    backend: str = "none"
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_STATE = ParallelState()
+
+
+def get_state() -> ParallelState:
+    return _STATE
+
+
+def env_rank_info() -> tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
+                     device: Optional[str] = None, timeout_s: int = 600) -> ParallelState:
+    """Initialise torch.distributed from torchrun env vars and build TP/DP groups.
+
+    backend: "nccl" (RCCL over xGMI on MI355X) when GPUs are present, else "gloo".
+    """
+    global _STATE
+    rank, world, local = env_rank_info()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        kw = dict(backend=backend, rank=rank, world_size=world,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(**kw)
+    elif backend == "nccl" and torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if world % tp_size != 0:
+        raise ValueError(f"world size {world} not divisible by tp {tp_size}")
+    st = ParallelState(rank=rank, world_size=world, local_rank=local, tp_size=tp_size,
+                       tp_rank=rank % tp_size, dp_size=world // tp_size, dp_rank=rank // tp_size,
+                       backend=backend if world > 1 else "none")
+    if world > 1:
+        for g in range(world // tp_size):
+            ranks = list(range(g * tp_size, (g + 1) * tp_size))
+            grp = dist.new_group(ranks)
+            if rank in ranks:
+                st.tp_group = grp
+        for t in range(tp_size):
+            ranks = list(range(t, world, tp_size))
+            grp = dist.new_group(ranks)
+            if rank in ranks:
+                st.dp_group = grp
+    _STATE = st
+    return st
+
+
+def set_state(st: ParallelState) -> None:
+    global _STATE
+    _STATE = st
+
+
+def destroy() -> None:
+    global _STATE
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _STATE = ParallelState()

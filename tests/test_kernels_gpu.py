@@ -1,0 +1,262 @@
+"""Numerics of the hand-written gfx950 HIP kernels vs the fp32 PyTorch references.
+
+Every test here runs the HIP kernel (torch.ops.akap.*) on the GPU and compares it
+with ops.reference on the same inputs.  Requires an MI355X.
+"""
+import math
+
+import pytest
+import torch
+
+from aws_k8s_ansible_provisioner_amd import ops
+from aws_k8s_ansible_provisioner_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    ops.load_native(required=True)
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    lim = atol + rtol * b.abs()
+    assert bool((err <= lim).all()), f"max err {err.max().item():.4g} (atol {atol})"
+
+
+@pytest.mark.parametrize("d", [128, 1024, 4096, 8192, 1000])
+@pytest.mark.parametrize("rows", [1, 7, 300])
+def test_rmsnorm(d, rows):
+    torch.manual_seed(0)
+    x = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(d, device=DEV, dtype=torch.bfloat16)
+    out = ops.rms_norm(x, w, 1e-6)
+    _close(out, ref.rms_norm(x.cpu(), w.cpu(), 1e-6), atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("d", [1024, 4096])
+def test_fused_add_rmsnorm(d):
+    torch.manual_seed(1)
+    x = torch.randn(33, d, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(33, d, device=DEV, dtype=torch.bfloat16)
+    r_ref = (x.float().cpu() + r.float().cpu()).bfloat16()
+    out, r2 = ops.fused_add_rms_norm(x, r, torch.ones(d, device=DEV, dtype=torch.bfloat16), 1e-5)
+    _close(r2, r_ref, atol=1e-6)
+    _close(out, ref.rms_norm(r_ref, torch.ones(d, dtype=torch.bfloat16), 1e-5), atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("T,F", [(1, 3072), (37, 3072), (513, 14336)])
+def test_silu_and_mul(T, F):
+    x = torch.randn(T, 2 * F, device=DEV, dtype=torch.bfloat16)
+    _close(ops.silu_and_mul(x), ref.silu_and_mul(x.cpu()), atol=2e-2, rtol=1e-2)
+
+
+def _rand_cache(nb, hkv, bs, d=128, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    k = torch.randn(nb, hkv, bs, d, generator=g).bfloat16()
+    v = torch.randn(nb, hkv, d, bs, generator=g).bfloat16()
+    return k, v
+
+
+@pytest.mark.parametrize("qk_norm", [True, False])
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8)])
+def test_qk_norm_rope_cache(qk_norm, hq, hkv):
+    torch.manual_seed(2)
+    T, D, BS, NB = 45, 128, 32, 16
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int64)
+    slots = torch.randperm(NB * BS)[:T].to(torch.int64)
+    slots[3] = -1
+    cs = ref.rope_cos_sin(4096, D, 1e6)
+    qw = torch.randn(D).bfloat16() if qk_norm else None
+    kw = torch.randn(D).bfloat16() if qk_norm else None
+    kc, vc = torch.zeros(NB, hkv, BS, D).bfloat16(), torch.zeros(NB, hkv, D, BS).bfloat16()
+    q_ref = torch.empty(T, hq, D).bfloat16()
+    ref.qk_norm_rope_cache(qkv, q_ref, kc, vc, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
+    kg, vg = kc.zero_().to(DEV), vc.zero_().to(DEV)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.qk_norm_rope_cache(qkv, q_ref, kc2, vc2, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
+    q_out = torch.empty(T, hq, D, device=DEV, dtype=torch.bfloat16)
+    ops.qk_norm_rope_cache(qkv.to(DEV), q_out, kg, vg, pos.to(DEV), slots.to(DEV), cs.to(DEV),
+                           None if qw is None else qw.to(DEV), None if kw is None else kw.to(DEV),
+                           hq, hkv, 1e-6)
+    _close(q_out, q_ref, atol=3e-2, rtol=2e-2)
+    _close(kg, kc2, atol=3e-2, rtol=2e-2)
+    _close(vg, vc2, atol=0)
+
+
+def _setup_attn(seqs, hq, hkv, bs, seed=0):
+    """seqs: list of (kv_len, q_len). Returns tensors on CPU."""
+    g = torch.Generator().manual_seed(seed)
+    D = 128
+    nb_per = [math.ceil(kv / bs) for kv, _ in seqs]
+    NB = sum(nb_per) + 3
+    perm = torch.randperm(NB, generator=g)
+    kc, vc = _rand_cache(NB, hkv, bs, D, seed)
+    maxb = max(nb_per)
+    bt = torch.zeros(len(seqs), maxb, dtype=torch.int32)
+    i = 0
+    for s, n in enumerate(nb_per):
+        bt[s, :n] = perm[i:i + n].to(torch.int32)
+        i += n
+    q_start = torch.zeros(len(seqs) + 1, dtype=torch.int32)
+    for s, (_, ql) in enumerate(seqs):
+        q_start[s + 1] = q_start[s] + ql
+    T = int(q_start[-1])
+    q = torch.randn(T, hq, D, generator=g).bfloat16()
+    seq_lens = torch.tensor([kv for kv, _ in seqs], dtype=torch.int32)
+    return q, kc, vc, bt, seq_lens, q_start
+
+
+def _tiles(seqs, G):
+    ts, tr = [], []
+    for s, (_, ql) in enumerate(seqs):
+        for r in range(0, ql * G, 64):
+            ts.append(s)
+            tr.append(r)
+    return torch.tensor(ts, dtype=torch.int32), torch.tensor(tr, dtype=torch.int32)
+
+
+@pytest.mark.parametrize("bs", [16, 32])
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (8, 8)])
+def test_paged_attention_prefill(bs, hq, hkv):
+    seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (520, 7), (64, 1)]
+    q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, bs, seed=bs + hq)
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, kc, vc, bt, sl, qs, scale)
+    ts, tr = _tiles(seqs, hq // hkv)
+    out = torch.empty_like(q).to(DEV)
+    ops.paged_attention_prefill(out, q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV),
+                                qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv, scale)
+    _close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("num_parts,part_size", [(1, 4096), (8, 256), (3, 512)])
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (64, 8), (32, 8)])
+def test_paged_attention_decode(num_parts, part_size, hq, hkv):
+    lens = [1, 31, 32, 33, 200, 777, 1500]
+    if num_parts * part_size < max(lens):
+        lens = [min(x, num_parts * part_size) for x in lens]
+    seqs = [(kv, 1) for kv in lens]
+    q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=num_parts)
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, kc, vc, bt, sl, qs, scale)
+    out = torch.empty_like(q).to(DEV)
+    G = hq // hkv
+    ws = ops.decode_workspace(len(seqs), hkv, G, num_parts, DEV)
+    ops.paged_attention_decode(out, q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV), G,
+                               scale, workspace=ws, num_parts=num_parts, part_size=part_size)
+    _close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+def test_decode_attention_large_score_spike():
+    """Force the online-softmax rescale branch: a single huge-score key late in the sequence."""
+    seqs = [(900, 1)]
+    q, kc, vc, bt, sl, qs = _setup_attn(seqs, 16, 8, 32, seed=5)
+    b = int(bt[0, 27])
+    kc[b, :, 5, :] = q[0, ::2, :] * 8  # key 869 aligns with every q head of each kv head
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, kc, vc, bt, sl, qs, scale)
+    for parts, ps in [(1, 1024), (4, 256)]:
+        out = torch.empty_like(q).to(DEV)
+        ops.paged_attention_decode(out, q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV),
+                                   2, scale, num_parts=parts, part_size=ps)
+        _close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+def test_argmax_and_greedy_sample():
+    torch.manual_seed(3)
+    B, V = 9, 151936
+    logits = torch.randn(B, V, device=DEV)
+    logits[4, 77777] = 100.0
+    exp = logits.argmax(-1)
+    assert torch.equal(ops.argmax(logits), exp)
+    assert torch.equal(ops.argmax(logits.bfloat16()), logits.bfloat16().float().argmax(-1))
+    zeros = torch.zeros(B, device=DEV)
+    tok, _ = ops.sample(logits, zeros, torch.zeros(B, dtype=torch.int32, device=DEV),
+                        torch.ones(B, device=DEV), torch.arange(B, device=DEV),
+                        torch.zeros(B, dtype=torch.int32, device=DEV))
+    assert torch.equal(tok, exp)
+
+
+def test_sampling_distribution_topk_topp():
+    torch.manual_seed(4)
+    V, N = 64, 4000
+    base = torch.randn(V) * 2
+    logits = base.expand(N, V).contiguous().to(DEV)
+    temp = torch.full((N,), 0.8, device=DEV)
+    seeds = torch.full((N,), 1234, dtype=torch.int64, device=DEV)
+    steps = torch.arange(N, dtype=torch.int32, device=DEV)
+    # plain temperature
+    tok, lp = ops.sample(logits, temp, torch.zeros(N, dtype=torch.int32, device=DEV),
+                         torch.ones(N, device=DEV), seeds, steps)
+    p = torch.softmax(base / 0.8, -1)
+    freq = torch.bincount(tok.cpu(), minlength=V).float() / N
+    assert (freq - p).abs().max() < 0.03
+    _close(lp, torch.log(p[tok.cpu()]), atol=1e-3)
+    # top-k
+    k = 5
+    tok, _ = ops.sample(logits, temp, torch.full((N,), k, dtype=torch.int32, device=DEV),
+                        torch.ones(N, device=DEV), seeds, steps)
+    top = set(torch.topk(base, k).indices.tolist())
+    assert set(tok.cpu().tolist()) <= top
+    assert len(set(tok.cpu().tolist())) == k
+    # top-p
+    tp = 0.7
+    tok, _ = ops.sample(logits, temp, torch.zeros(N, dtype=torch.int32, device=DEV),
+                        torch.full((N,), tp, device=DEV), seeds, steps)
+    sp, si = p.sort(descending=True)
+    n = int((sp.cumsum(0) < tp).sum()) + 1
+    nucleus = set(si[:n].tolist())
+    assert set(tok.cpu().tolist()) <= nucleus
+    # reproducible per (seed, step)
+    tok2, _ = ops.sample(logits, temp, torch.zeros(N, dtype=torch.int32, device=DEV),
+                         torch.full((N,), tp, device=DEV), seeds, steps)
+    assert torch.equal(tok, tok2)
+
+
+def test_embedding_vocab_parallel():
+    table = torch.randn(1000, 1024, dtype=torch.bfloat16)
+    ids = torch.tensor([0, 5, 999, 1500, 250], dtype=torch.int64)
+    exp = ref.embedding(ids, table, 0, 1000)
+    out = ops.embedding(ids.to(DEV), table.to(DEV))
+    _close(out, exp, atol=0)
+    exp2 = ref.embedding(ids, table[200:600], 200, 600)
+    out2 = ops.embedding(ids.to(DEV), table[200:600].contiguous().to(DEV), vocab_start=200,
+                         vocab_end=600)
+    _close(out2, exp2, atol=0)
+
+
+def test_moe_routing():
+    torch.manual_seed(6)
+    T, E, K = 300, 8, 2
+    logits = torch.randn(T, E, dtype=torch.bfloat16)
+    w, ids = ops.moe_topk_softmax(logits.to(DEV), K)
+    rw, rid = ref.moe_topk_softmax(logits, K)
+    assert torch.equal(ids.cpu(), rid)
+    _close(w, rw, atol=1e-4)
+    s, off, npad = ops.moe_align(ids, E, 16)
+    off = off.cpu()
+    s = s.cpu()
+    flat = ids.cpu().reshape(-1)
+    for e in range(E):
+        seg = s[off[e]:off[e + 1]]
+        real = seg[seg < T * K]
+        assert set(real.tolist()) == set((flat == e).nonzero().flatten().tolist())
+        assert (off[e + 1] - off[e]) % 16 == 0
+    assert int(npad) == int(off[-1])
+
+
+def test_kv_gather_scatter_roundtrip():
+    planes, NB = 6, 20
+    cache = torch.randn(planes, NB, 8, 32, 128, dtype=torch.bfloat16, device=DEV)
+    ids = torch.tensor([3, 17, 0, 9], dtype=torch.int32, device=DEV)
+    buf = ops.kv_gather(cache, ids)
+    assert torch.equal(buf.view(planes, 4, -1), cache.view(planes, NB, -1)[:, ids.long()])
+    dst = torch.zeros_like(cache)
+    ids2 = torch.tensor([1, 2, 5, 19], dtype=torch.int32, device=DEV)
+    ops.kv_scatter(buf, dst, ids2)
+    assert torch.equal(dst.view(planes, NB, -1)[:, ids2.long()], buf.view(planes, 4, -1))
