@@ -57,7 +57,8 @@ PYBIND11_MODULE(_runtime, m) {
            py::arg("prefix_cache") = true)
       .def("add_request", &Scheduler::add_request, py::arg("id"), py::arg("prompt"),
            py::arg("max_tokens"), py::arg("min_tokens") = 0, py::arg("ignore_eos") = false,
-           py::arg("stop_ids") = std::vector<int32_t>{})
+           py::arg("stop_ids") = std::vector<int32_t>{}, py::arg("temperature") = 0.f,
+           py::arg("top_p") = 1.f, py::arg("top_k") = 0, py::arg("seed") = 0)
       .def("abort_request", &Scheduler::abort_request)
       .def("release", &Scheduler::release)
       .def("schedule",
@@ -78,6 +79,11 @@ PYBIND11_MODULE(_runtime, m) {
              b.logits_idx = ptr_of<int64_t>(bufs, "logits_idx", c.max_num_seqs);
              b.req_ids = ptr_of<int64_t>(bufs, "req_ids", c.max_num_seqs);
              b.sample_mask = ptr_of<int32_t>(bufs, "sample_mask", c.max_num_seqs);
+             b.temperature = ptr_of<float>(bufs, "temperature", c.max_num_seqs);
+             b.top_p = ptr_of<float>(bufs, "top_p", c.max_num_seqs);
+             b.top_k = ptr_of<int32_t>(bufs, "top_k", c.max_num_seqs);
+             b.seeds = ptr_of<int64_t>(bufs, "seeds", c.max_num_seqs);
+             b.steps = ptr_of<int32_t>(bufs, "steps", c.max_num_seqs);
              StepInfo i;
              {
                py::gil_scoped_release nogil;

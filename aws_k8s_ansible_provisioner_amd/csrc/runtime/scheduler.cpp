@@ -12,7 +12,8 @@ Scheduler::Scheduler(const SchedConfig& cfg, int num_blocks, bool prefix_cache)
 }
 
 void Scheduler::add_request(int64_t id, const std::vector<int32_t>& prompt, int max_tokens,
-                            int min_tokens, bool ignore_eos, const std::vector<int32_t>& stop_ids) {
+                            int min_tokens, bool ignore_eos, const std::vector<int32_t>& stop_ids,
+                            float temperature, float top_p, int top_k, int64_t seed) {
   if (reqs_.count(id)) throw std::invalid_argument("duplicate request id");
   if (prompt.empty()) throw std::invalid_argument("empty prompt");
   if ((int)prompt.size() >= cfg_.max_model_len)
@@ -25,6 +26,10 @@ void Scheduler::add_request(int64_t id, const std::vector<int32_t>& prompt, int 
   r->min_tokens = min_tokens;
   r->ignore_eos = ignore_eos;
   r->stop_ids = stop_ids;
+  r->temperature = temperature;
+  r->top_p = top_p;
+  r->top_k = top_k;
+  r->seed = seed;
   waiting_.push_back(r.get());
   reqs_.emplace(id, std::move(r));
 }
@@ -207,6 +212,11 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     const bool sample = kv == (int)r->tokens.size();
     buf.sample_mask[s] = sample ? 1 : 0;
     if (sample) {
+      buf.temperature[ns] = r->temperature;
+      buf.top_p[ns] = r->top_p;
+      buf.top_k[ns] = r->top_k;
+      buf.seeds[ns] = r->seed;
+      buf.steps[ns] = r->num_generated();
       buf.logits_idx[ns++] = T + q - 1;
       last_sampled_.push_back(r);
     }

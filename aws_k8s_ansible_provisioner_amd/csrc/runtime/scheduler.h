@@ -39,6 +39,11 @@ struct Request {
   int finish = NOT_FINISHED;
   int num_preempt = 0;
   bool prefix_checked = false;
+  // sampling parameters (consumed by the on-GPU sampler, indexed per sample row)
+  float temperature = 0.f;
+  float top_p = 1.f;
+  int top_k = 0;
+  int64_t seed = 0;
   int num_generated() const { return (int)tokens.size() - num_prompt; }
 };
 
@@ -66,6 +71,12 @@ struct BatchBuffers {
   int64_t* logits_idx;
   int64_t* req_ids;       // per scheduled seq
   int32_t* sample_mask;   // per scheduled seq: 1 if its last token is sampled
+  // per sample row
+  float* temperature;
+  float* top_p;
+  int32_t* top_k;
+  int64_t* seeds;
+  int32_t* steps;
   int cap_tokens, cap_tiles;
 };
 
@@ -84,7 +95,8 @@ class Scheduler {
   Scheduler(const SchedConfig& cfg, int num_blocks, bool prefix_cache);
 
   void add_request(int64_t id, const std::vector<int32_t>& prompt, int max_tokens, int min_tokens,
-                   bool ignore_eos, const std::vector<int32_t>& stop_ids);
+                   bool ignore_eos, const std::vector<int32_t>& stop_ids, float temperature = 0.f,
+                   float top_p = 1.f, int top_k = 0, int64_t seed = 0);
   bool abort_request(int64_t id);
   StepInfo schedule(BatchBuffers& buf);
   // tokens[i] is the sample for the i-th sampled sequence of the last step.

@@ -1,0 +1,64 @@
+"""Engine / sampling configuration (argument names mirror the vLLM OpenAI server so the
+llm-d style manifests and the reference's smoke test keep working)."""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    model: str = "qwen3-0.6b"
+    served_model_name: Optional[str] = None
+    max_model_len: int = 4096
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 16384
+    block_size: int = 32
+    gpu_memory_utilization: float = 0.90
+    num_gpu_blocks: Optional[int] = None      # override the memory-derived block count
+    enable_prefix_caching: bool = True
+    enforce_eager: bool = False               # disable hipGraph decode
+    cuda_graph_max_bs: Optional[int] = None   # largest captured decode batch
+    tensor_parallel_size: int = 1
+    seed: int = 0
+    device: str = "auto"                      # "auto" | "cuda" | "cpu"
+    load_format: str = "random"               # "random" | "safetensors"
+    weights_path: Optional[str] = None
+    chat_template: Optional[str] = None
+    decode_part_size: int = 512               # split-KV partition (tokens)
+    kv_role: str = "both"                     # "both" | "prefill" | "decode" (P/D)
+    init_std: float = 0.02                    # random-init weight scale
+
+    def resolved_device(self) -> str:
+        if self.device != "auto":
+            return self.device
+        import torch
+
+        return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+@dataclasses.dataclass
+class SamplingParams:
+    max_tokens: int = 16
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = 0
+    min_tokens: int = 0
+    seed: Optional[int] = None
+    stop_token_ids: list = dataclasses.field(default_factory=list)
+    stop: list = dataclasses.field(default_factory=list)  # stop strings (post-detokenize)
+    ignore_eos: bool = False
+    logprobs: Optional[int] = None
+    n: int = 1
+
+    def normalized(self) -> "SamplingParams":
+        p = dataclasses.replace(self)
+        if p.top_k is None or p.top_k < 0:
+            p.top_k = 0
+        if p.top_p is None or p.top_p <= 0:
+            p.top_p = 1.0
+        if p.temperature is None:
+            p.temperature = 1.0
+        if p.temperature < 1e-5:
+            p.temperature = 0.0
+        return p

@@ -1,0 +1,225 @@
+"""LLMEngine: request bookkeeping around the C++ scheduler and the model runner.
+
+One engine = one model replica (one GPU, or one TP group where every rank runs the
+same step in lock-step: rank 0 schedules and broadcasts the step, see parallel/tp_worker).
+"""
+from __future__ import annotations
+
+import dataclasses
+import itertools
+import threading
+import time
+from typing import Iterable, Optional, Union
+
+import numpy as np
+
+from .. import _runtime_loader
+from ..models.config import ModelConfig, get_config
+from ..utils.metrics import EngineMetrics
+from ..utils.tokenizer import get_tokenizer
+from .config import EngineConfig, SamplingParams
+from .model_runner import ModelRunner
+
+FINISH_REASONS = {0: None, 1: "length", 2: "stop", 3: "abort"}
+
+
+@dataclasses.dataclass
+class RequestState:
+    req_id: str
+    iid: int
+    prompt: Optional[str]
+    prompt_ids: list
+    params: SamplingParams
+    arrival: float
+    output_ids: list = dataclasses.field(default_factory=list)
+    logprobs: list = dataclasses.field(default_factory=list)
+    first_token_time: Optional[float] = None
+    last_token_time: Optional[float] = None
+    finish_reason: Optional[str] = None
+    finished: bool = False
+    text: str = ""
+
+
+@dataclasses.dataclass
+class RequestOutput:
+    req_id: str
+    prompt_ids: list
+    output_ids: list
+    new_ids: list
+    text: str
+    delta_text: str
+    finished: bool
+    finish_reason: Optional[str]
+    ttft: Optional[float] = None
+    num_cached_tokens: int = 0
+
+
+class LLMEngine:
+    def __init__(self, ecfg: EngineConfig, mcfg: Optional[ModelConfig] = None, pstate=None,
+                 log=print, runner: Optional[ModelRunner] = None):
+        self.ecfg = ecfg
+        self.mcfg = mcfg or get_config(ecfg.model)
+        self.model_name = ecfg.served_model_name or self.mcfg.hf_id
+        self.log = log
+        self.runner = runner or ModelRunner(ecfg, self.mcfg, pstate, log=log)
+        rt = _runtime_loader.load()
+        sc = rt.SchedConfig()
+        sc.max_num_seqs = ecfg.max_num_seqs
+        sc.max_num_batched_tokens = ecfg.max_num_batched_tokens
+        sc.max_model_len = ecfg.max_model_len
+        sc.block_size = ecfg.block_size
+        sc.gqa_group = self.runner.G
+        sc.tile_rows = 64
+        sc.eos_id = self.mcfg.eos_id
+        sc.max_blocks_per_seq = self.runner.max_blocks
+        self.sched = rt.Scheduler(sc, self.runner.num_blocks, ecfg.enable_prefix_caching)
+        self.tokenizer = get_tokenizer(ecfg.weights_path, self.mcfg.vocab_size, self.mcfg.bos_id,
+                                       self.mcfg.eos_id)
+        self.metrics = EngineMetrics(self.model_name)
+        self.reqs: dict[int, RequestState] = {}
+        self.by_name: dict[str, int] = {}
+        self._ids = itertools.count(1)
+        self._lock = threading.Lock()
+        self._pending_aborts: list[int] = []
+        self.steps = 0
+        self.last_prefix = (0, 0)
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, req_id: Optional[str], prompt: Union[str, list, None],
+                    params: Optional[SamplingParams] = None,
+                    prompt_ids: Optional[list] = None) -> str:
+        params = (params or SamplingParams()).normalized()
+        if prompt_ids is None:
+            if isinstance(prompt, str):
+                prompt_ids = self.tokenizer.encode(prompt)
+            else:
+                prompt_ids = list(prompt or [])
+        prompt_ids = [int(t) for t in prompt_ids]
+        if not prompt_ids:
+            prompt_ids = [self.mcfg.bos_id]
+        if len(prompt_ids) >= self.ecfg.max_model_len:
+            raise ValueError(f"prompt has {len(prompt_ids)} tokens; max_model_len is "
+                             f"{self.ecfg.max_model_len}")
+        max_tokens = min(params.max_tokens, self.ecfg.max_model_len - len(prompt_ids))
+        iid = next(self._ids)
+        req_id = req_id or f"req-{iid}"
+        seed = params.seed if params.seed is not None else (iid * 7919 + self.ecfg.seed)
+        st = RequestState(req_id, iid, prompt if isinstance(prompt, str) else None, prompt_ids,
+                          params, time.time())
+        with self._lock:
+            self.sched.add_request(iid, prompt_ids, max_tokens, params.min_tokens,
+                                   params.ignore_eos, list(params.stop_token_ids),
+                                   float(params.temperature), float(params.top_p),
+                                   int(params.top_k), int(seed))
+            self.reqs[iid] = st
+            self.by_name[req_id] = iid
+        self.metrics.req_total.inc(model_name=self.model_name)
+        return req_id
+
+    def abort_request(self, req_id: str) -> bool:
+        with self._lock:
+            iid = self.by_name.get(req_id)
+            if iid is None:
+                return False
+            ok = self.sched.abort_request(iid)
+            st = self.reqs.pop(iid, None)
+            self.by_name.pop(req_id, None)
+            self.sched.release(iid)
+        if st is not None:
+            st.finished, st.finish_reason = True, "abort"
+        return ok
+
+    def has_unfinished(self) -> bool:
+        return self.sched.has_work()
+
+    @property
+    def num_unfinished(self) -> int:
+        return self.sched.num_running + self.sched.num_waiting
+
+    # ------------------------------------------------------------------ step
+    def step(self) -> list[RequestOutput]:
+        t0 = time.time()
+        with self._lock:
+            info = self.sched.schedule(self.runner.host_buffers())
+        if info["num_seqs"] == 0:
+            return []
+        if info["num_preempted"]:
+            self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
+        toks = self.runner.execute(info)
+        now = time.time()
+        with self._lock:
+            ids, new, fin = self.sched.update(np.ascontiguousarray(toks, dtype=np.int64))
+        m, name = self.metrics, self.model_name
+        if info["is_prefill"]:
+            m.prompt_tokens.inc(info["num_tokens"], model_name=name)
+        m.gen_tokens.inc(len(ids), model_name=name)
+        m.step_time.observe(now - t0, model_name=name,
+                            phase="prefill" if info["is_prefill"] else "decode")
+        outs = []
+        for iid, tok, f in zip(ids, new, fin):
+            st = self.reqs.get(iid)
+            if st is None:
+                continue
+            st.output_ids.append(int(tok))
+            if st.first_token_time is None:
+                st.first_token_time = now
+                m.ttft.observe(now - st.arrival, model_name=name)
+            elif st.last_token_time is not None:
+                m.tpot.observe(now - st.last_token_time, model_name=name)
+            st.last_token_time = now
+            reason = FINISH_REASONS.get(int(f))
+            delta = self.tokenizer.decode_token(int(tok)) if not (
+                reason == "stop" and int(tok) == self.mcfg.eos_id) else ""
+            st.text += delta
+            if reason is None and st.params.stop:
+                for s in st.params.stop:
+                    if s and s in st.text:
+                        st.text = st.text[: st.text.index(s)]
+                        reason = "stop"
+                        with self._lock:
+                            self.sched.abort_request(iid)
+                        break
+            if reason is not None:
+                st.finished, st.finish_reason = True, reason
+                m.success.inc(model_name=name, finished_reason=reason)
+                m.e2e.observe(now - st.arrival, model_name=name)
+                m.duration.observe(now - st.arrival, model_name=name)
+                info_r = self.sched.request_info(iid)
+                cached = info_r["num_cached"] if info_r else 0
+                with self._lock:
+                    self.sched.release(iid)
+                    self.reqs.pop(iid, None)
+                    self.by_name.pop(st.req_id, None)
+            else:
+                cached = 0
+            outs.append(RequestOutput(st.req_id, st.prompt_ids, list(st.output_ids), [int(tok)],
+                                      st.text, delta, st.finished, st.finish_reason,
+                                      (st.first_token_time - st.arrival)
+                                      if st.first_token_time else None, cached))
+        self.steps += 1
+        self._update_gauges()
+        return outs
+
+    def _update_gauges(self) -> None:
+        m, name = self.metrics, self.model_name
+        m.running.set(self.sched.num_running, model_name=name)
+        m.waiting.set(self.sched.num_waiting, model_name=name)
+        m.active.set(self.sched.num_running + self.sched.num_waiting, model_name=name)
+        m.kv_usage.set(self.sched.kv_usage(), model_name=name)
+
+    # ------------------------------------------------------------------ offline API
+    def generate(self, prompts: Iterable, params: Optional[SamplingParams] = None,
+                 prompt_ids: Optional[list] = None) -> list[RequestOutput]:
+        names = []
+        if prompt_ids is not None:
+            for p in prompt_ids:
+                names.append(self.add_request(None, None, params, prompt_ids=p))
+        else:
+            for p in prompts:
+                names.append(self.add_request(None, p, params))
+        final: dict[str, RequestOutput] = {}
+        while self.has_unfinished():
+            for o in self.step():
+                if o.finished:
+                    final[o.req_id] = o
+        return [final[n] for n in names if n in final]

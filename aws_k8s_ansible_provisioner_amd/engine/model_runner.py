@@ -1,0 +1,224 @@
+"""Model runner: weights, the paged KV cache, device batch buffers and hipGraph decode.
+
+* KV cache: ONE allocation [L, 2, NB, Hkv*BS*D] sized from the HBM left after weights
+  (288 GB per MI355X -> millions of cached tokens for small models), zero-filled.
+* Host->device: the C++ scheduler writes the batch into pinned host buffers; the runner
+  issues a handful of non-blocking H2D copies into persistent device buffers.
+* Decode: the whole step -- embedding, 28+ layers, LM head, fp32 cast, sampler -- is
+  captured once per batch-size bucket into a hipGraph (torch.cuda.CUDAGraph is hipGraph
+  on ROCm) and replayed with padded rows (seq_len 0, slot -1 => no work, no cache write).
+* Prefill / chunked prefill: eager, variable T, tile-mapped MFMA attention.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.config import ModelConfig
+from ..models.transformer import AttnBatch, DecoderLM
+from ..parallel.state import ParallelState, get_state
+from .config import EngineConfig
+
+DEFAULT_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320,
+                   384, 448, 512]
+
+
+class ModelRunner:
+    def __init__(self, ecfg: EngineConfig, mcfg: ModelConfig,
+                 pstate: Optional[ParallelState] = None, log=print):
+        self.ecfg, self.mcfg = ecfg, mcfg
+        self.ps = pstate or get_state()
+        self.log = log
+        dev = ecfg.resolved_device()
+        if dev == "cuda":
+            self.device = torch.device("cuda", torch.cuda.current_device())
+            ops.load_native(required=True)  # GPU path never falls back to eager PyTorch
+        else:
+            self.device = torch.device("cpu")
+        self.is_gpu = self.device.type == "cuda"
+        t0 = time.time()
+        self.model = DecoderLM(mcfg, self.device, seed=ecfg.seed, pstate=self.ps,
+                               max_model_len=ecfg.max_model_len, init_std=ecfg.init_std)
+        if ecfg.load_format == "safetensors" and ecfg.weights_path:
+            from .weights import load_safetensors_dir
+
+            self.model.load_state_dict(load_safetensors_dir(ecfg.weights_path))
+        self.log(f"[runner] model {mcfg.name} ready in {time.time() - t0:.1f}s "
+                 f"({self.model.weight_bytes() / 2**30:.2f} GiB weights/rank)")
+        self.bs = ecfg.block_size
+        self.max_blocks = math.ceil(ecfg.max_model_len / self.bs)
+        self.G = self.model.hq // self.model.hkv
+        self.max_seqs = ecfg.max_num_seqs
+        self.cap_tokens = max(ecfg.max_num_batched_tokens, self.max_seqs)
+        self.cap_tiles = self.cap_tokens * self.G // 64 + self.max_seqs + 1
+        self.num_blocks = ecfg.num_gpu_blocks or self._derive_num_blocks()
+        self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
+        self.k_caches, self.v_caches = self.model.cache_views(self.kv, self.bs)
+        self.log(f"[runner] KV cache: {self.num_blocks} blocks x {self.bs} tokens "
+                 f"({self.kv.numel() * 2 / 2**30:.1f} GiB)")
+        self.part_size = ecfg.decode_part_size
+        self.num_parts = max(1, math.ceil(ecfg.max_model_len / self.part_size))
+        self._alloc_buffers()
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_pool = None
+        self.buckets: list[int] = []
+        if self.is_gpu and not ecfg.enforce_eager:
+            self.capture_graphs()
+
+    # ------------------------------------------------------------------ sizing
+    def _derive_num_blocks(self) -> int:
+        per_block = self.mcfg.num_layers * 2 * self.model.hkv * self.bs * self.model.D * 2
+        if not self.is_gpu:
+            return max(64, min(4096, (self.max_seqs * self.ecfg.max_model_len) // self.bs + 8))
+        torch.cuda.synchronize()
+        free, total = torch.cuda.mem_get_info(self.device)
+        used = total - free
+        d = self.mcfg.hidden_size
+        width = d * 4 + (self.model.hq + 2 * self.model.hkv) * self.model.D + 3 * self.model.ffn
+        act = self.cap_tokens * width * 2 * 3 + self.max_seqs * self.mcfg.vocab_size * 12
+        reserve = act + 3 * 2**30
+        budget = total * self.ecfg.gpu_memory_utilization - used - reserve
+        n = int(budget // per_block)
+        if n < self.max_blocks:
+            raise RuntimeError(f"not enough HBM for the KV cache ({budget / 2**30:.1f} GiB)")
+        return n
+
+    def _pinned(self, n, dtype):
+        t = torch.zeros(n, dtype=dtype, pin_memory=self.is_gpu)
+        return t
+
+    def _alloc_buffers(self) -> None:
+        S, T, TL, mb = self.max_seqs, self.cap_tokens, self.cap_tiles, self.max_blocks
+        spec = {
+            "input_ids": (T, torch.int64), "positions": (T, torch.int64), "slots": (T, torch.int64),
+            "seq_lens": (S, torch.int32), "q_start": (S + 1, torch.int32),
+            "block_tables": (S * mb, torch.int32), "tile_seq": (TL, torch.int32),
+            "tile_row": (TL, torch.int32), "logits_idx": (S, torch.int64),
+            "req_ids": (S, torch.int64), "sample_mask": (S, torch.int32),
+            "temperature": (S, torch.float32), "top_p": (S, torch.float32),
+            "top_k": (S, torch.int32), "seeds": (S, torch.int64), "steps": (S, torch.int32),
+        }
+        self.h = {k: self._pinned(n, dt) for k, (n, dt) in spec.items()}
+        self.np = {k: v.numpy() for k, v in self.h.items()}
+        self.d = {k: torch.zeros(n, dtype=dt, device=self.device) for k, (n, dt) in spec.items()
+                  if k not in ("req_ids", "sample_mask")}
+        self.d_bt = self.d["block_tables"].view(S, mb)
+        self.out_tokens = torch.zeros(S, dtype=torch.int64, device=self.device)
+        self.out_logprobs = torch.zeros(S, dtype=torch.float32, device=self.device)
+        self.workspace = ops.decode_workspace(S, self.model.hkv, self.G, self.num_parts,
+                                              self.device)
+
+    def host_buffers(self) -> dict:
+        return self.np
+
+    def _h2d(self, key: str, n: int) -> torch.Tensor:
+        dst = self.d[key][:n]
+        dst.copy_(self.h[key][:n], non_blocking=True)
+        return dst
+
+    # ------------------------------------------------------------------ execution
+    def _sample(self, logits: torch.Tensor, n: int):
+        return ops.sample(logits, self.d["temperature"][:n], self.d["top_k"][:n],
+                          self.d["top_p"][:n], self.d["seeds"][:n], self.d["steps"][:n],
+                          out_tokens=self.out_tokens[:n], out_logprobs=self.out_logprobs[:n])
+
+    def execute_prefill(self, info: dict) -> torch.Tensor:
+        T, B, nt, ns = info["num_tokens"], info["num_seqs"], info["num_tiles"], info["num_samples"]
+        mb = self.max_blocks
+        ids = self._h2d("input_ids", T)
+        pos = self._h2d("positions", T)
+        slots = self._h2d("slots", T)
+        sl = self._h2d("seq_lens", B)
+        qs = self._h2d("q_start", B + 1)
+        self._h2d("block_tables", B * mb)
+        ts = self._h2d("tile_seq", nt)
+        tr = self._h2d("tile_row", nt)
+        lidx = self._h2d("logits_idx", ns)
+        for k in ("temperature", "top_p", "top_k", "seeds", "steps"):
+            self._h2d(k, ns)
+        batch = AttnBatch(True, pos, slots, self.d_bt[:B], sl, qs, ts, tr)
+        h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
+        if ns == 0:
+            return self.out_tokens[:0]
+        logits = self.model.compute_logits(h.index_select(0, lidx)).float()
+        toks, _ = self._sample(logits, ns)
+        return toks
+
+    def _decode_body(self, n: int) -> None:
+        batch = AttnBatch(False, self.d["positions"][:n], self.d["slots"][:n], self.d_bt[:n],
+                          self.d["seq_lens"][:n], self.d["q_start"][:n + 1], None, None,
+                          self.num_parts, self.part_size, self.workspace)
+        h = self.model.forward(self.d["input_ids"][:n], batch, self.k_caches, self.v_caches)
+        logits = self.model.compute_logits(h).float()
+        self._sample(logits, n)
+
+    def _pad_host(self, B: int, n: int) -> None:
+        if n <= B:
+            return
+        npd = self.np
+        npd["input_ids"][B:n] = 0
+        npd["positions"][B:n] = 0
+        npd["slots"][B:n] = -1
+        npd["seq_lens"][B:n] = 0
+        npd["temperature"][B:n] = 0.0
+        npd["top_p"][B:n] = 1.0
+        npd["top_k"][B:n] = 0
+        npd["seeds"][B:n] = 0
+        npd["steps"][B:n] = 0
+
+    def execute_decode(self, info: dict) -> torch.Tensor:
+        B = info["num_seqs"]
+        n = B
+        graph = None
+        if self.graphs:
+            for b in self.buckets:
+                if b >= B:
+                    n, graph = b, self.graphs[b]
+                    break
+        self._pad_host(B, n)
+        mb = self.max_blocks
+        for k in ("input_ids", "positions", "slots", "seq_lens", "temperature", "top_p", "top_k",
+                  "seeds", "steps"):
+            self._h2d(k, n)
+        self._h2d("block_tables", n * mb)
+        if graph is not None:
+            graph.replay()
+        else:
+            self._decode_body(n)
+        return self.out_tokens[:B]
+
+    def execute(self, info: dict) -> np.ndarray:
+        toks = self.execute_prefill(info) if info["is_prefill"] else self.execute_decode(info)
+        return toks.to("cpu").numpy()
+
+    # ------------------------------------------------------------------ graphs
+    def capture_graphs(self) -> None:
+        maxbs = min(self.ecfg.cuda_graph_max_bs or self.max_seqs, self.max_seqs)
+        self.buckets = [b for b in DEFAULT_BUCKETS if b <= maxbs]
+        if not self.buckets or self.buckets[-1] < maxbs:
+            self.buckets.append(maxbs)
+        t0 = time.time()
+        # safe static contents: every row is padding
+        self._pad_host(0, self.max_seqs)
+        for k in ("input_ids", "positions", "slots", "seq_lens", "temperature", "top_p", "top_k",
+                  "seeds", "steps"):
+            self._h2d(k, self.max_seqs)
+        torch.cuda.synchronize()
+        self.graph_pool = torch.cuda.graph_pool_handle()
+        stream = torch.cuda.Stream()
+        for b in reversed(self.buckets):
+            with torch.cuda.stream(stream):
+                self._decode_body(b)  # warm-up (hipBLASLt heuristics, allocator)
+            stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
+                self._decode_body(b)
+            self.graphs[b] = g
+        torch.cuda.synchronize()
+        self.log(f"[runner] captured {len(self.graphs)} decode hipGraphs "
+                 f"(bs {self.buckets[0]}..{self.buckets[-1]}) in {time.time() - t0:.1f}s")

@@ -23,7 +23,7 @@ from ..parallel.state import ParallelState
 
 class MoEBlock:
     def __init__(self, cfg, ps: ParallelState, device, dtype, g: torch.Generator,
-                 full_then_shard: bool, mode: Optional[str] = None):
+                 full_then_shard: bool, mode: Optional[str] = None, std: float = 0.02):
         self.cfg = cfg
         self.ps = ps
         self.device = device
@@ -36,7 +36,7 @@ class MoEBlock:
 
         def rand(*shape):
             t = torch.empty(*shape, dtype=torch.float32, device=g.device)
-            t.normal_(0.0, 0.02, generator=g)
+            t.normal_(0.0, std, generator=g)
             return t.to(dtype)
 
         if self.mode == "ep":

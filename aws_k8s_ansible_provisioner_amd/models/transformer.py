@@ -72,8 +72,9 @@ class DecoderLM:
     def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu",
                  dtype: torch.dtype = torch.bfloat16, seed: int = 0,
                  pstate: Optional[ParallelState] = None, max_model_len: int = 4096,
-                 full_then_shard: bool = False):
+                 full_then_shard: bool = False, init_std: float = 0.02):
         self.cfg = cfg
+        self.init_std = init_std
         self.device = torch.device(device)
         self.dtype = dtype
         self.ps = pstate or get_state()
@@ -94,9 +95,9 @@ class DecoderLM:
                                         cfg.rope_theta, cfg.rope_scaling, device=self.device)
 
     # ------------------------------------------------------------------ weights
-    def _rand(self, g: torch.Generator, *shape, std: float = 0.02) -> torch.Tensor:
+    def _rand(self, g: torch.Generator, *shape, std: Optional[float] = None) -> torch.Tensor:
         t = torch.empty(*shape, dtype=torch.float32, device=g.device)
-        t.normal_(0.0, std, generator=g)
+        t.normal_(0.0, self.init_std if std is None else std, generator=g)
         return t.to(self.dtype)
 
     def _init_weights(self, seed: int, full_then_shard: bool) -> None:
@@ -109,11 +110,6 @@ class DecoderLM:
         g.manual_seed(seed if full_then_shard else seed * 1000 + r)
         to = dict(device=self.device)
         one = lambda n: torch.ones(n, dtype=self.dtype, **to)  # noqa: E731
-
-        def rows(full_rows, cols, shard_rows):
-            if full_then_shard:
-                return _shard_rows(self._rand(g, full_rows, cols), r, tp).to(**to)
-            return self._rand(g, shard_rows, cols).to(**to)
 
         vp = self.vocab_per
         if full_then_shard:
@@ -141,7 +137,8 @@ class DecoderLM:
             qn = one(D) if cfg.qk_norm else None
             kn = one(D) if cfg.qk_norm else None
             if cfg.is_moe:
-                moe = MoEBlock(cfg, self.ps, self.device, self.dtype, g, full_then_shard)
+                moe = MoEBlock(cfg, self.ps, self.device, self.dtype, g, full_then_shard,
+                               std=self.init_std)
                 lw = LayerWeights(one(d), one(d), w_qkv, w_o, qn, kn, None, None, moe)
             else:
                 if full_then_shard:

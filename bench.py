@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Serving benchmark: output tok/s + p50 TTFT (BASELINE.json headline) on MI355X.
+
+One "step" = one WAVE of a fixed synthetic serving workload per GPU: `--num-requests`
+requests (random token ids, `--input-len` prompt tokens, exactly `--output-len`
+generated tokens, ignore_eos) all submitted at t=0 to the continuous-batching engine
+and served to completion (chunked prefill + hipGraph decode).  Every wave uses fresh
+random prompts, so prefix caching gets no hits.
+
+Multi-GPU (torchrun, one process per GPU): every rank serves its own wave on its own
+GPU -- a data-parallel replica, exactly how the gateway scales the deployment (weak
+scaling: per-GPU work is fixed).  Ranks are synchronised with barriers around the K
+timed waves; value = total output tokens of all ranks / max rank wall time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="qwen3-0.6b")
+    ap.add_argument("--num-requests", type=int, default=256)
+    ap.add_argument("--input-len", type=int, default=512)
+    ap.add_argument("--output-len", type=int, default=256)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
+    ap.add_argument("--block-size", type=int, default=32)
+    ap.add_argument("--max-model-len", type=int, default=2048)
+    ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="extra untimed waves run after timing (for rocprofv3 captures)")
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+    from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
+    from aws_k8s_ansible_provisioner_amd.models.config import get_config
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != a.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
+    gpu = torch.cuda.is_available() and a.device != "cpu"
+    if gpu:
+        torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if gpu else "gloo"
+        kw = {"device_id": torch.device("cuda", local)} if gpu else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+
+    mcfg = get_config(a.model)
+    ecfg = EngineConfig(model=a.model, max_model_len=a.max_model_len,
+                        max_num_seqs=a.max_num_seqs,
+                        max_num_batched_tokens=a.max_num_batched_tokens,
+                        block_size=a.block_size, enforce_eager=a.enforce_eager,
+                        device="cuda" if gpu else "cpu", seed=1234 + rank,
+                        num_gpu_blocks=None if gpu else 512)
+    log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if rank == 0 else (lambda *x: None)
+    eng = LLMEngine(ecfg, mcfg, log=log)
+    sp = SamplingParams(max_tokens=a.output_len, temperature=a.temperature, ignore_eos=True)
+    rng = np.random.default_rng(1000 + rank)
+    vocab_hi = min(mcfg.vocab_size, 150000)
+
+    def wave():
+        prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
+        outs = eng.generate(None, sp, prompt_ids=prompts)
+        ntok = sum(len(o.output_ids) for o in outs)
+        ttfts = [o.ttft for o in outs if o.ttft is not None]
+        return ntok, ttfts
+
+    def barrier():
+        if gpu:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        if gpu:
+            torch.cuda.synchronize()
+
+    for i in range(a.warmup):
+        t = time.time()
+        wave()
+        log(f"[bench] warmup wave {i} {time.time() - t:.2f}s")
+    barrier()
+    t0 = time.perf_counter()
+    total, ttfts = 0, []
+    for i in range(a.steps):
+        n, tt = wave()
+        total += n
+        ttfts += tt
+    barrier()
+    el = time.perf_counter() - t0
+    for _ in range(a.profile_steps):
+        wave()
+
+    p50_local = statistics.median(ttfts) if ttfts else 0.0
+    stats = torch.tensor([float(total), el, p50_local], dtype=torch.float64)
+    if world > 1:
+        dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+        t_tok = torch.tensor([float(total)], dtype=torch.float64, device=dev)
+        t_el = torch.tensor([el], dtype=torch.float64, device=dev)
+        t_all = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_reduce(t_tok)
+        dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
+        dist.all_gather(t_all, torch.tensor([p50_local], dtype=torch.float64, device=dev))
+        stats = torch.tensor([t_tok.item(), t_el.item(),
+                              statistics.median([x.item() for x in t_all])])
+    tok, el, p50 = float(stats[0]), float(stats[1]), float(stats[2])
+    if rank == 0:
+        res = {
+            "metric": "output tok/s + p50 TTFT",
+            "value": round(tok / el, 2),
+            "unit": "output tok/s",
+            "n_gpus": world if world > 1 else a.gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic random token-id prompts, random-init weights",
+            "p50_ttft_ms": round(p50 * 1000, 2),
+            "config": {
+                "model": mcfg.hf_id,
+                "global_batch": a.num_requests * max(world, 1),
+                "seq_len": a.input_len + a.output_len,
+                "input_len": a.input_len,
+                "output_len": a.output_len,
+                "requests_per_gpu": a.num_requests,
+                "parallelism": f"dp{max(world, 1)}",
+                "max_num_seqs": a.max_num_seqs,
+                "sampling": "greedy" if a.temperature <= 0 else f"T={a.temperature}",
+                "hipgraph_decode": not a.enforce_eager,
+            },
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,65 @@
+"""End-to-end engine on the GPU: HIP kernels + paged KV + hipGraph decode vs a dense
+fp32 cache-free reference forward on the same weights (teacher-forced)."""
+import pytest
+import torch
+
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
+from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logits
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(model, eager=False, **kw):
+    cfg = dict(model=model, device="cuda", max_model_len=512, max_num_seqs=16,
+               max_num_batched_tokens=128, block_size=32, num_gpu_blocks=128, init_std=0.1,
+               enforce_eager=eager, cuda_graph_max_bs=16)
+    cfg.update(kw)
+    return LLMEngine(EngineConfig(**cfg), log=lambda *a: None)
+
+
+def _check_teacher_forced(eng, prompt, out, tol=0.15):
+    """Every generated token must be (near-)argmax of the dense reference logits."""
+    seq = list(prompt) + list(out)
+    logits = dense_logits(eng.runner.model, seq).float().cpu()
+    for i, tok in enumerate(out):
+        row = logits[len(prompt) - 1 + i]
+        scale = row.std().item() + 1e-6
+        gap = (row.max() - row[tok]).item() / scale
+        assert gap <= tol, f"step {i}: token {tok} is {gap:.3f} std below the argmax"
+
+
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama"])
+@pytest.mark.parametrize("eager", [False, True])
+def test_engine_matches_dense_reference(model, eager):
+    eng = _engine(model, eager)
+    prompts = [list(range(5, 90)), [100, 101], [7, 8, 9] * 30, list(range(5, 90)),
+               list(range(300, 340))]
+    outs = eng.generate(None, SamplingParams(max_tokens=12, temperature=0, ignore_eos=True),
+                        prompt_ids=prompts)
+    assert len(outs) == len(prompts)
+    for p, o in zip(prompts, outs):
+        assert len(o.output_ids) == 12
+        _check_teacher_forced(eng, p, o.output_ids)
+    hits, queries = eng.sched.prefix_stats()
+    assert hits >= 1  # the repeated prompt reused cached blocks
+
+
+def test_qwen3_0_6b_shapes_one_step():
+    """Real Qwen3-0.6B shapes: first generated token agrees with the dense reference."""
+    eng = _engine("qwen3-0.6b", max_model_len=256, num_gpu_blocks=64, init_std=0.02)
+    prompts = [list(range(1000, 1100)), list(range(50, 60))]
+    outs = eng.generate(None, SamplingParams(max_tokens=3, temperature=0, ignore_eos=True),
+                        prompt_ids=prompts)
+    for p, o in zip(prompts, outs):
+        _check_teacher_forced(eng, p, o.output_ids, tol=0.2)
+
+
+def test_sampled_generation_runs_with_topk_topp():
+    eng = _engine("tiny-qwen3")
+    sp = SamplingParams(max_tokens=16, temperature=0.9, top_k=20, top_p=0.9, ignore_eos=True,
+                        seed=7)
+    a = eng.generate(None, sp, prompt_ids=[[5, 6, 7]])[0].output_ids
+    b = eng.generate(None, sp, prompt_ids=[[5, 6, 7]])[0].output_ids
+    assert a == b  # seeded requests are reproducible
+    assert len(a) == 16
