@@ -29,6 +29,12 @@ PYBIND11_MODULE(_runtime, m) {
       .def("allocate", &BlockManager::allocate)
       .def("free_blocks", &BlockManager::free_blocks)
       .def("register_full", &BlockManager::register_full)
+      .def("output_tokens", [](const Scheduler& s, int64_t id) {
+        auto r = s.get(id);
+        std::vector<int32_t> out;
+        if (r) out.assign(r->tokens.begin() + r->num_prompt, r->tokens.end());
+        return out;
+      })
       .def("reset_prefix_cache", &BlockManager::reset_prefix_cache)
       .def("match_prefix",
            [](BlockManager& bm, const std::vector<int32_t>& toks, int max_tokens) {
@@ -58,7 +64,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def("add_request", &Scheduler::add_request, py::arg("id"), py::arg("prompt"),
            py::arg("max_tokens"), py::arg("min_tokens") = 0, py::arg("ignore_eos") = false,
            py::arg("stop_ids") = std::vector<int32_t>{}, py::arg("temperature") = 0.f,
-           py::arg("top_p") = 1.f, py::arg("top_k") = 0, py::arg("seed") = 0)
+           py::arg("top_p") = 1.f, py::arg("top_k") = 0, py::arg("seed") = 0,
+           py::arg("stream") = false)
       .def("abort_request", &Scheduler::abort_request)
       .def("release", &Scheduler::release)
       .def("schedule",
@@ -102,9 +109,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def("update",
            [](Scheduler& s, py::array_t<int64_t, py::array::c_style> toks) {
              std::vector<int64_t> ids;
-             std::vector<int32_t> t, f;
-             s.update(toks.data(), (int)toks.size(), ids, t, f);
-             return py::make_tuple(ids, t, f);
+             std::vector<int32_t> t, f, first;
+             s.update(toks.data(), (int)toks.size(), ids, t, f, first);
+             return py::make_tuple(ids, t, f, first);
            })
       .def_property_readonly("num_waiting", &Scheduler::num_waiting)
       .def_property_readonly("num_running", &Scheduler::num_running)
@@ -114,6 +121,12 @@ PYBIND11_MODULE(_runtime, m) {
       .def("num_free_blocks", [](const Scheduler& s) { return s.blocks().num_free(); })
       .def("prefix_stats", [](const Scheduler& s) {
         return py::make_tuple(s.blocks().prefix_hits(), s.blocks().prefix_queries());
+      })
+      .def("output_tokens", [](const Scheduler& s, int64_t id) {
+        auto r = s.get(id);
+        std::vector<int32_t> out;
+        if (r) out.assign(r->tokens.begin() + r->num_prompt, r->tokens.end());
+        return out;
       })
       .def("reset_prefix_cache", [](Scheduler& s) { s.blocks_mut().reset_prefix_cache(); })
       .def_property_readonly("total_preemptions", &Scheduler::total_preemptions)
@@ -129,6 +142,7 @@ PYBIND11_MODULE(_runtime, m) {
         d["finish"] = r->finish;
         d["num_preempt"] = r->num_preempt;
         d["tokens"] = r->tokens;
+        d["stream"] = r->stream;
         return d;
       });
 }

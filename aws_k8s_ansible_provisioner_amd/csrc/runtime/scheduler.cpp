@@ -13,7 +13,8 @@ Scheduler::Scheduler(const SchedConfig& cfg, int num_blocks, bool prefix_cache)
 
 void Scheduler::add_request(int64_t id, const std::vector<int32_t>& prompt, int max_tokens,
                             int min_tokens, bool ignore_eos, const std::vector<int32_t>& stop_ids,
-                            float temperature, float top_p, int top_k, int64_t seed) {
+                            float temperature, float top_p, int top_k, int64_t seed,
+                            bool stream) {
   if (reqs_.count(id)) throw std::invalid_argument("duplicate request id");
   if (prompt.empty()) throw std::invalid_argument("empty prompt");
   if ((int)prompt.size() >= cfg_.max_model_len)
@@ -30,6 +31,7 @@ void Scheduler::add_request(int64_t id, const std::vector<int32_t>& prompt, int 
   r->top_p = top_p;
   r->top_k = top_k;
   r->seed = seed;
+  r->stream = stream;
   waiting_.push_back(r.get());
   reqs_.emplace(id, std::move(r));
 }
@@ -231,7 +233,8 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
 }
 
 void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_ids,
-                       std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish) {
+                       std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish,
+                       std::vector<int32_t>& out_first) {
   if (n != (int)last_sampled_.size()) throw std::invalid_argument("sample count mismatch");
   for (Request* r : running_) publish_full_blocks(*r);
   for (int i = 0; i < n; ++i) {
@@ -247,9 +250,13 @@ void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_i
     if (reason == NOT_FINISHED &&
         (gen >= r->max_tokens || (int)r->tokens.size() >= cfg_.max_model_len))
       reason = FINISH_LENGTH;
-    out_ids.push_back(r->id);
-    out_tokens.push_back(tok);
-    out_finish.push_back(reason);
+    const bool first = gen == 1;
+    if (first || reason != NOT_FINISHED || r->stream) {
+      out_ids.push_back(r->id);
+      out_tokens.push_back(tok);
+      out_finish.push_back(reason);
+      out_first.push_back(first ? 1 : 0);
+    }
     if (reason != NOT_FINISHED) {
       running_.erase(std::remove(running_.begin(), running_.end(), r), running_.end());
       finish(*r, reason);

@@ -44,6 +44,7 @@ struct Request {
   float top_p = 1.f;
   int top_k = 0;
   int64_t seed = 0;
+  bool stream = false;  // report every token (else only first token + finish)
   int num_generated() const { return (int)tokens.size() - num_prompt; }
 };
 
@@ -96,13 +97,15 @@ class Scheduler {
 
   void add_request(int64_t id, const std::vector<int32_t>& prompt, int max_tokens, int min_tokens,
                    bool ignore_eos, const std::vector<int32_t>& stop_ids, float temperature = 0.f,
-                   float top_p = 1.f, int top_k = 0, int64_t seed = 0);
+                   float top_p = 1.f, int top_k = 0, int64_t seed = 0, bool stream = false);
   bool abort_request(int64_t id);
   StepInfo schedule(BatchBuffers& buf);
   // tokens[i] is the sample for the i-th sampled sequence of the last step.
-  // Emits (id, token, finish_reason) triples for every sampled sequence.
+  // Emits (id, token, finish_reason, is_first) events only for sequences that got their
+  // first token, finished, or stream -- O(events) host work per step, not O(batch).
   void update(const int64_t* tokens, int n, std::vector<int64_t>& out_ids,
-              std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish);
+              std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish,
+              std::vector<int32_t>& out_first);
 
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }

@@ -38,6 +38,7 @@ class RequestState:
     finish_reason: Optional[str] = None
     finished: bool = False
     text: str = ""
+    stream: bool = False
 
 
 @dataclasses.dataclass
@@ -83,11 +84,14 @@ class LLMEngine:
         self._pending_aborts: list[int] = []
         self.steps = 0
         self.last_prefix = (0, 0)
+        self.timers = {"schedule": 0.0, "execute": 0.0, "post": 0.0}
 
     # ------------------------------------------------------------------ requests
     def add_request(self, req_id: Optional[str], prompt: Union[str, list, None],
                     params: Optional[SamplingParams] = None,
-                    prompt_ids: Optional[list] = None) -> str:
+                    prompt_ids: Optional[list] = None, stream: bool = False) -> str:
+        """Queue a request.  stream=True reports every token (server SSE); otherwise the
+        engine reports only the first token (TTFT) and the finished output."""
         params = (params or SamplingParams()).normalized()
         if prompt_ids is None:
             if isinstance(prompt, str):
@@ -106,11 +110,12 @@ class LLMEngine:
         seed = params.seed if params.seed is not None else (iid * 7919 + self.ecfg.seed)
         st = RequestState(req_id, iid, prompt if isinstance(prompt, str) else None, prompt_ids,
                           params, time.time())
+        st.stream = stream or bool(params.stop)
         with self._lock:
             self.sched.add_request(iid, prompt_ids, max_tokens, params.min_tokens,
                                    params.ignore_eos, list(params.stop_token_ids),
                                    float(params.temperature), float(params.top_p),
-                                   int(params.top_k), int(seed))
+                                   int(params.top_k), int(seed), st.stream)
             self.reqs[iid] = st
             self.by_name[req_id] = iid
         self.metrics.req_total.inc(model_name=self.model_name)
@@ -145,59 +150,77 @@ class LLMEngine:
             return []
         if info["num_preempted"]:
             self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
+        t1 = time.time()
         toks = self.runner.execute(info)
         now = time.time()
+        self.timers["schedule"] += t1 - t0
+        self.timers["execute"] += now - t1
         with self._lock:
-            ids, new, fin = self.sched.update(np.ascontiguousarray(toks, dtype=np.int64))
+            ids, new, fin, first = self.sched.update(np.ascontiguousarray(toks, dtype=np.int64))
         m, name = self.metrics, self.model_name
         if info["is_prefill"]:
             m.prompt_tokens.inc(info["num_tokens"], model_name=name)
-        m.gen_tokens.inc(len(ids), model_name=name)
+        m.gen_tokens.inc(info["num_samples"], model_name=name)
         m.step_time.observe(now - t0, model_name=name,
                             phase="prefill" if info["is_prefill"] else "decode")
         outs = []
-        for iid, tok, f in zip(ids, new, fin):
+        for iid, tok, f, fst in zip(ids, new, fin, first):
             st = self.reqs.get(iid)
             if st is None:
                 continue
-            st.output_ids.append(int(tok))
-            if st.first_token_time is None:
+            if fst:
                 st.first_token_time = now
                 m.ttft.observe(now - st.arrival, model_name=name)
-            elif st.last_token_time is not None:
-                m.tpot.observe(now - st.last_token_time, model_name=name)
-            st.last_token_time = now
-            reason = FINISH_REASONS.get(int(f))
-            delta = self.tokenizer.decode_token(int(tok)) if not (
-                reason == "stop" and int(tok) == self.mcfg.eos_id) else ""
-            st.text += delta
-            if reason is None and st.params.stop:
-                for s in st.params.stop:
-                    if s and s in st.text:
-                        st.text = st.text[: st.text.index(s)]
-                        reason = "stop"
-                        with self._lock:
-                            self.sched.abort_request(iid)
-                        break
+            reason = FINISH_REASONS.get(f)
+            if st.stream:
+                st.output_ids.append(tok)
+                delta = "" if (reason == "stop" and tok == self.mcfg.eos_id) else \
+                    self.tokenizer.decode_token(tok)
+                st.text += delta
+                if reason is None and st.params.stop:
+                    for s_ in st.params.stop:
+                        if s_ and s_ in st.text:
+                            cut = st.text.index(s_)
+                            delta = delta[: max(0, len(delta) - (len(st.text) - cut))]
+                            st.text = st.text[:cut]
+                            reason = "stop"
+                            with self._lock:
+                                self.sched.abort_request(iid)
+                            break
+            else:
+                delta = ""
+            cached = 0
             if reason is not None:
+                if not st.stream:
+                    out_ids = self.sched.output_tokens(iid)
+                    if reason == "stop" and out_ids and out_ids[-1] == self.mcfg.eos_id:
+                        st.text = self.tokenizer.decode(out_ids[:-1])
+                    else:
+                        st.text = self.tokenizer.decode(out_ids)
+                    st.output_ids = list(out_ids)
+                    delta = st.text
                 st.finished, st.finish_reason = True, reason
+                n = len(st.output_ids)
                 m.success.inc(model_name=name, finished_reason=reason)
                 m.e2e.observe(now - st.arrival, model_name=name)
                 m.duration.observe(now - st.arrival, model_name=name)
+                if n > 1 and st.first_token_time is not None:
+                    m.tpot.observe((now - st.first_token_time) / (n - 1), model_name=name)
                 info_r = self.sched.request_info(iid)
                 cached = info_r["num_cached"] if info_r else 0
                 with self._lock:
                     self.sched.release(iid)
                     self.reqs.pop(iid, None)
                     self.by_name.pop(st.req_id, None)
-            else:
-                cached = 0
-            outs.append(RequestOutput(st.req_id, st.prompt_ids, list(st.output_ids), [int(tok)],
-                                      st.text, delta, st.finished, st.finish_reason,
+            elif not st.stream:
+                continue  # first-token event of a non-streaming request: metrics only
+            outs.append(RequestOutput(st.req_id, st.prompt_ids, st.output_ids, [tok], st.text,
+                                      delta, st.finished, st.finish_reason,
                                       (st.first_token_time - st.arrival)
                                       if st.first_token_time else None, cached))
         self.steps += 1
         self._update_gauges()
+        self.timers["post"] += time.time() - now
         return outs
 
     def _update_gauges(self) -> None:

@@ -12,6 +12,7 @@
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Optional
 
@@ -203,6 +204,15 @@ class ModelRunner:
         if not self.buckets or self.buckets[-1] < maxbs:
             self.buckets.append(maxbs)
         t0 = time.time()
+        tunable = os.environ.get("AKAP_TUNABLEOP", "0") == "1"
+        if tunable:
+            # PyTorch-ROCm TunableOp: benchmark hipBLASLt/rocBLAS solutions for every decode
+            # GEMM shape once, before capture (the graph then bakes in the winner).
+            torch.cuda.tunable.enable(True)
+            torch.cuda.tunable.tuning_enable(True)
+            torch.cuda.tunable.set_max_tuning_iterations(30)
+            torch.cuda.tunable.set_filename(os.environ.get(
+                "AKAP_TUNABLEOP_FILE", os.path.join(os.getcwd(), "tunableop_results.csv")))
         # safe static contents: every row is padding
         self._pad_host(0, self.max_seqs)
         for k in ("input_ids", "positions", "slots", "seq_lens", "temperature", "top_p", "top_k",
@@ -220,5 +230,7 @@ class ModelRunner:
                 self._decode_body(b)
             self.graphs[b] = g
         torch.cuda.synchronize()
+        if tunable:
+            torch.cuda.tunable.tuning_enable(False)
         self.log(f"[runner] captured {len(self.graphs)} decode hipGraphs "
                  f"(bs {self.buckets[0]}..{self.buckets[-1]}) in {time.time() - t0:.1f}s")

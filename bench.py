@@ -111,6 +111,7 @@ def main() -> int:
         ttfts += tt
     barrier()
     el = time.perf_counter() - t0
+    log(f"[bench] host timers (all waves): {eng.timers}  steps={eng.steps}")
     for _ in range(a.profile_steps):
         wave()
 

@@ -1,0 +1,155 @@
+"""C++ host runtime: paged KV block manager + continuous-batching scheduler (CPU)."""
+import numpy as np
+import pytest
+
+from aws_k8s_ansible_provisioner_amd import _runtime_loader
+
+rt = _runtime_loader.load()
+
+
+def test_block_manager_alloc_free_and_prefix_cache():
+    bm = rt.BlockManager(8, 4, True)
+    assert bm.num_free == 8
+    blocks = [bm.allocate() for _ in range(3)]
+    assert len(set(blocks)) == 3 and bm.num_free == 5
+    toks = list(range(100, 112))
+    h0 = rt.BlockManager.hash_block(0, toks[0:4])
+    h1 = rt.BlockManager.hash_block(h0, toks[4:8])
+    bm.register_full(blocks[0], h0)
+    bm.register_full(blocks[1], h1)
+    bm.free_blocks(blocks)
+    assert bm.num_free == 8  # cached blocks are evictable, counted free
+    n, hit, hashes = bm.match_prefix(toks, 11)
+    assert n == 8 and hit == blocks[:2] and hashes == [h0, h1]
+    # a different first block breaks the chain
+    n2, _, _ = bm.match_prefix([1] + toks[1:], 11)
+    assert n2 == 0
+    bm.free_blocks(hit)
+    # exhaust the pool: evicts cached blocks (LRU), never hands out a block twice
+    got = [bm.allocate() for _ in range(8)]
+    assert sorted(got) == list(range(8))
+    assert bm.allocate() == -1
+    with pytest.raises(Exception):
+        bm.free_blocks([got[0], got[0]])
+
+
+def _bufs(max_seqs, cap_tokens, mb, tiles=256):
+    return {
+        "input_ids": np.zeros(cap_tokens, np.int64), "positions": np.zeros(cap_tokens, np.int64),
+        "slots": np.zeros(cap_tokens, np.int64), "seq_lens": np.zeros(max_seqs, np.int32),
+        "q_start": np.zeros(max_seqs + 1, np.int32),
+        "block_tables": np.zeros(max_seqs * mb, np.int32),
+        "tile_seq": np.zeros(tiles, np.int32), "tile_row": np.zeros(tiles, np.int32),
+        "logits_idx": np.zeros(max_seqs, np.int64), "req_ids": np.zeros(max_seqs, np.int64),
+        "sample_mask": np.zeros(max_seqs, np.int32),
+        "temperature": np.zeros(max_seqs, np.float32), "top_p": np.zeros(max_seqs, np.float32),
+        "top_k": np.zeros(max_seqs, np.int32), "seeds": np.zeros(max_seqs, np.int64),
+        "steps": np.zeros(max_seqs, np.int32),
+    }
+
+
+def _sched(num_blocks=64, bs=4, max_seqs=4, budget=16, max_len=64, prefix=True, G=2):
+    c = rt.SchedConfig()
+    c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = max_seqs, budget, max_len
+    c.block_size, c.gqa_group, c.tile_rows, c.eos_id = bs, G, 64, 2
+    c.max_blocks_per_seq = max_len // bs
+    return rt.Scheduler(c, num_blocks, prefix), _bufs(max_seqs, max(budget, max_seqs), max_len // bs)
+
+
+def test_chunked_prefill_then_decode_and_slots():
+    s, b = _sched(budget=8)
+    s.add_request(1, list(range(10, 22)), 3, temperature=0.5, top_k=7, seed=99)  # 12 tokens
+    i = s.schedule(b)
+    assert i["is_prefill"] and i["num_tokens"] == 8 and i["num_samples"] == 0
+    assert list(b["positions"][:8]) == list(range(8))
+    bt = b["block_tables"][:16]
+    slots = [bt[p // 4] * 4 + p % 4 for p in range(8)]
+    assert list(b["slots"][:8]) == slots
+    assert s.update(np.zeros(0, np.int64))[0] == []
+    i = s.schedule(b)
+    assert i["is_prefill"] and i["num_tokens"] == 4 and i["num_samples"] == 1
+    assert b["logits_idx"][0] == 3 and b["top_k"][0] == 7 and b["seeds"][0] == 99
+    assert b["temperature"][0] == pytest.approx(0.5) and b["steps"][0] == 0
+    ids, toks, fin, first = s.update(np.array([55], np.int64))
+    assert ids == [1] and toks == [55] and fin == [0] and first == [1]
+    i = s.schedule(b)
+    assert not i["is_prefill"] and i["num_seqs"] == 1 and i["num_tokens"] == 1
+    assert b["input_ids"][0] == 55 and b["positions"][0] == 12 and b["seq_lens"][0] == 13
+    assert b["steps"][0] == 1
+    s.update(np.array([56], np.int64))
+    s.schedule(b)
+    ids, toks, fin, first = s.update(np.array([57], np.int64))
+    assert fin == [1]  # length
+    assert s.output_tokens(1) == [55, 56, 57]
+    assert not s.has_work()
+
+
+def test_prefill_tile_map_counts_gqa_rows():
+    s, b = _sched(budget=64, max_len=128, G=4)
+    s.add_request(1, list(range(3, 40)), 2)  # 37 tokens * 4 rows = 148 rows -> 3 tiles
+    s.add_request(2, [5, 6], 2)               # 2 * 4 = 8 rows -> 1 tile
+    i = s.schedule(b)
+    assert i["num_tiles"] == 4
+    assert list(b["tile_seq"][:4]) == [0, 0, 0, 1] and list(b["tile_row"][:4]) == [0, 64, 128, 0]
+    assert list(b["q_start"][:3]) == [0, 37, 39]
+
+
+def test_eos_stop_ids_and_min_tokens():
+    s, b = _sched()
+    s.add_request(1, [5, 6, 7], 10)  # eos=2 stops
+    s.add_request(2, [5, 6, 8], 10, min_tokens=2)  # eos ignored before min_tokens
+    s.add_request(3, [5, 6, 9], 10, stop_ids=[77])
+    s.add_request(4, [5, 6, 10], 10, ignore_eos=True)
+    s.schedule(b)
+    ids, toks, fin, first = s.update(np.array([2, 2, 77, 2], np.int64))
+    res = dict(zip(ids, fin))
+    assert res[1] == 2 and res[2] == 0 and res[3] == 2 and res[4] == 0
+
+
+def test_prefix_cache_hit_on_second_request():
+    s, b = _sched(budget=64)
+    p = list(range(20, 37))  # 17 tokens -> 4 full blocks
+    s.add_request(1, p, 1)
+    s.schedule(b)
+    s.update(np.array([9], np.int64))
+    s.add_request(2, p, 1)
+    i = s.schedule(b)
+    assert i["num_tokens"] == 1  # 16 cached tokens, only the last prompt token computed
+    assert s.request_info(2)["num_cached"] == 16
+    hits, queries = s.prefix_stats()
+    assert hits == 1
+
+
+def test_preemption_when_pool_exhausted():
+    s, b = _sched(num_blocks=6, bs=4, max_seqs=4, budget=32, max_len=32)
+    s.add_request(1, list(range(3, 11)), 12)  # 8 tokens = 2 blocks
+    s.add_request(2, list(range(3, 11)) * 1, 12, stop_ids=[])
+    s.add_request(3, list(range(13, 21)), 12)
+    s.schedule(b)
+    s.update(np.array([1, 1, 1], np.int64)[: 3])
+    preempted = 0
+    for _ in range(12):
+        i = s.schedule(b)
+        if i["num_seqs"] == 0:
+            break
+        preempted += i["num_preempted"]
+        s.update(np.full(i["num_samples"], 4, np.int64))
+    assert preempted >= 1 and s.total_preemptions >= 1
+    # everything eventually finishes with all blocks returned
+    for _ in range(200):
+        if not s.has_work():
+            break
+        i = s.schedule(b)
+        s.update(np.full(i["num_samples"], 4, np.int64))
+    assert not s.has_work()
+    assert s.num_free_blocks() == 6
+
+
+def test_abort():
+    s, b = _sched()
+    s.add_request(1, [5, 6, 7], 10)
+    s.add_request(2, [5, 6, 8], 10)
+    assert s.abort_request(1)
+    assert not s.abort_request(1)
+    i = s.schedule(b)
+    assert i["num_seqs"] == 1 and b["req_ids"][0] == 2
