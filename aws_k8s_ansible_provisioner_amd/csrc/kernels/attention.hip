@@ -39,18 +39,20 @@ __device__ __forceinline__ void wave_state_init(WaveState& st) {
   st.l = 0.f;
 }
 
-// Process one 32-token KV chunk starting at absolute kv position t0.
-// limit: last kv position this lane's query row may attend to (-1 => none).
-template <bool MASK>
-__device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC],
-                                           const bf16* __restrict__ k_cache,
+// Register-staged operands of one 32-token KV chunk.
+struct ChunkRegs {
+  bf16x8 ka[2][kNC];  // K tile rows (A operand of S^T = K . Q^T)
+  bf16x8 vb[kND];     // V^T tiles (A operand of O^T = V^T . P^T)
+};
+
+// Issue the loads of the 32-token chunk at absolute kv position t0.
+__device__ __forceinline__ void load_chunk(ChunkRegs& c, const bf16* __restrict__ k_cache,
                                            const bf16* __restrict__ v_cache,
                                            const int* __restrict__ bt, int kv_len, int kvh,
-                                           int Hkv, int BS, int t0, int limit, float scale_log2) {
+                                           int Hkv, int BS, int t0) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int r = lane & 15;
-  bf16x8 ka[2][kNC];
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     int tok = t0 + 8 * (r >> 2) + 4 * tt + (r & 3);
@@ -59,22 +61,29 @@ __device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC
     const int off = tok % BS;
     const bf16* kp = k_cache + (((size_t)blk * Hkv + kvh) * BS + off) * kD + 8 * g;
 #pragma unroll
-    for (int c = 0; c < kNC; ++c) ka[tt][c] = *reinterpret_cast<const bf16x8*>(kp + 32 * c);
+    for (int cc = 0; cc < kNC; ++cc) c.ka[tt][cc] = *reinterpret_cast<const bf16x8*>(kp + 32 * cc);
   }
   int vt = t0 + 8 * g;
   vt = min(vt, (kv_len - 1) & ~7);
   const int vblk = bt[vt / BS];
   const int voff = vt % BS;
   const bf16* vp = v_cache + ((size_t)vblk * Hkv + kvh) * kD * BS + voff + (size_t)r * BS;
-  bf16x8 vb[kND];
 #pragma unroll
-  for (int n = 0; n < kND; ++n) vb[n] = *reinterpret_cast<const bf16x8*>(vp + (size_t)16 * n * BS);
+  for (int n = 0; n < kND; ++n) c.vb[n] = *reinterpret_cast<const bf16x8*>(vp + (size_t)16 * n * BS);
+}
 
+// Scores, online softmax and P.V for one staged chunk.
+// limit: last kv position this lane's query row may attend to (-1 => none).
+template <bool MASK>
+__device__ __forceinline__ void compute_chunk(WaveState& st, const bf16x8 (&qb)[kNC],
+                                              const ChunkRegs& c, int t0, int limit,
+                                              float scale_log2) {
+  const int g = (threadIdx.x & 63) >> 4;
   f32x4 s[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int c = 0; c < kNC; ++c) {
-    s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[0][c], qb[c], s[0], 0, 0, 0);
-    s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[1][c], qb[c], s[1], 0, 0, 0);
+  for (int cc = 0; cc < kNC; ++cc) {
+    s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.ka[0][cc], qb[cc], s[0], 0, 0, 0);
+    s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.ka[1][cc], qb[cc], s[1], 0, 0, 0);
   }
   float sv[8];
   float cmax = -INFINITY;
@@ -99,16 +108,27 @@ __device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC
   float psum = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float p = exp2f(sv[j] - m_new);
-    psum += p;
-    pb[j] = f2bf(p);
+    const float pj = exp2f(sv[j] - m_new);
+    psum += pj;
+    pb[j] = f2bf(pj);
   }
   st.l = st.l * alpha + psum;
 #pragma unroll
   for (int n = 0; n < kND; ++n) {
     st.o[n] *= alpha;
-    st.o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[n], pb, st.o[n], 0, 0, 0);
+    st.o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.vb[n], pb, st.o[n], 0, 0, 0);
   }
+}
+
+template <bool MASK>
+__device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC],
+                                           const bf16* __restrict__ k_cache,
+                                           const bf16* __restrict__ v_cache,
+                                           const int* __restrict__ bt, int kv_len, int kvh,
+                                           int Hkv, int BS, int t0, int limit, float scale_log2) {
+  ChunkRegs c;
+  load_chunk(c, k_cache, v_cache, bt, kv_len, kvh, Hkv, BS, t0);
+  compute_chunk<MASK>(st, qb, c, t0, limit, scale_log2);
 }
 
 // Load this lane's Q^T operand for query row (lane & 15) (zeros if invalid).
@@ -180,6 +200,7 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
 // Decode: one new token per sequence, rows = the G q-heads of one kv head.
 // grid = (num_seqs, Hkv, num_parts); 4 waves split the partition's chunks.
 // ----------------------------------------------------------------------------------
+template <bool PREFETCH>
 __global__ __launch_bounds__(256) void paged_attn_decode_kernel(AttnParams p) {
   const int seq = blockIdx.x;
   const int kvh = blockIdx.y;
@@ -207,13 +228,32 @@ __global__ __launch_bounds__(256) void paged_attn_decode_kernel(AttnParams p) {
     load_q(qb, qptr, valid);
     const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
     const int limit = kv_len - 1;
-    for (int t0 = pstart + 32 * w; t0 < pend; t0 += 128) {
-      if (t0 + 31 < kv_len)
-        attn_chunk<false>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
-                          p.scale_log2);
-      else
-        attn_chunk<true>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
-                         p.scale_log2);
+    if constexpr (PREFETCH) {
+      // register double buffer: chunk i+1's loads are in flight during chunk i's MFMAs
+      int t0 = pstart + 32 * w;
+      if (t0 < pend) {
+        ChunkRegs cur;
+        load_chunk(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+        for (; t0 < pend; t0 += 128) {
+          ChunkRegs nxt;
+          const bool more = t0 + 128 < pend;
+          if (more) load_chunk(nxt, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0 + 128);
+          if (t0 + 31 < kv_len)
+            compute_chunk<false>(st, qb, cur, t0, limit, p.scale_log2);
+          else
+            compute_chunk<true>(st, qb, cur, t0, limit, p.scale_log2);
+          if (more) cur = nxt;
+        }
+      }
+    } else {
+      for (int t0 = pstart + 32 * w; t0 < pend; t0 += 128) {
+        if (t0 + 31 < kv_len)
+          attn_chunk<false>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0,
+                            limit, p.scale_log2);
+        else
+          attn_chunk<true>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0,
+                           limit, p.scale_log2);
+      }
     }
   }
   float l = st.l;
@@ -306,7 +346,10 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s
 
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) {
   if (num_seqs == 0) return;
-  paged_attn_decode_kernel<<<dim3(num_seqs, p.Hkv, p.num_parts), 256, 0, s>>>(p);
+  if (p.flags & 1)
+    paged_attn_decode_kernel<true><<<dim3(num_seqs, p.Hkv, p.num_parts), 256, 0, s>>>(p);
+  else
+    paged_attn_decode_kernel<false><<<dim3(num_seqs, p.Hkv, p.num_parts), 256, 0, s>>>(p);
   if (p.num_parts > 1) paged_attn_reduce_kernel<<<dim3(num_seqs, p.Hkv), 256, 0, s>>>(p);
 }
 

@@ -45,6 +45,7 @@ struct AttnParams {
   float* part_m;  // [B, Hkv, parts, G]
   float* part_l;
   float* part_o;  // [B, Hkv, parts, G, D]
+  int flags;      // bit0: register double-buffered K/V prefetch in decode
 };
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s);
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s);

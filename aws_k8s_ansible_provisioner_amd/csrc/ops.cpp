@@ -3,6 +3,7 @@
 // Every op launches on the caller's current HIP stream, allocates nothing and
 // never synchronises, so all of them are hipGraph-capturable (engine decode path).
 // PyTorch on ROCm names the GPU dispatch key "CUDA"; kernels are HIP/CDNA4 only.
+#include <cstdlib>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -90,6 +91,14 @@ void silu_and_mul(Tensor out, Tensor x) {
                             x.dim() > 1 ? x.stride(-2) : 2 * F, cur_stream());
 }
 
+int attn_flags() {
+  static int f = [] {
+    const char* e = std::getenv("AKAP_ATTN_FLAGS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return f;
+}
+
 akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_cache,
                              Tensor& block_tables, Tensor& seq_lens, int64_t G, double scale) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out); CHECK_CONTIG(k_cache);
@@ -113,6 +122,7 @@ akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_
   TORCH_CHECK(p.Hq == p.Hkv * G, "Hq must equal Hkv * G");
   TORCH_CHECK(p.BS % 8 == 0 && (p.BS % 32 == 0 || 32 % p.BS == 0), "block size must be 8/16/32/64..");
   p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.flags = attn_flags();
   return p;
 }
 

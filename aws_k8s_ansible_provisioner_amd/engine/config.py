@@ -25,7 +25,6 @@ class EngineConfig:
     load_format: str = "random"               # "random" | "safetensors"
     weights_path: Optional[str] = None
     chat_template: Optional[str] = None
-    decode_part_size: int = 512               # split-KV partition (tokens)
     kv_role: str = "both"                     # "both" | "prefill" | "decode" (P/D)
     init_std: float = 0.02                    # random-init weight scale
 

@@ -122,19 +122,30 @@ class LLMEngine:
         return req_id
 
     def abort_request(self, req_id: str) -> bool:
+        """Thread-safe abort.  Applied at the next step boundary (never between a step's
+        schedule and update), so it can be called from HTTP handler threads."""
         with self._lock:
             iid = self.by_name.get(req_id)
             if iid is None:
                 return False
-            ok = self.sched.abort_request(iid)
-            st = self.reqs.pop(iid, None)
-            self.by_name.pop(req_id, None)
-            self.sched.release(iid)
-        if st is not None:
-            st.finished, st.finish_reason = True, "abort"
-        return ok
+            self._pending_aborts.append(iid)
+        return True
+
+    def _apply_aborts(self) -> None:
+        with self._lock:
+            pend, self._pending_aborts = self._pending_aborts, []
+            for iid in pend:
+                self.sched.abort_request(iid)
+                st = self.reqs.pop(iid, None)
+                if st is not None:
+                    self.by_name.pop(st.req_id, None)
+                    st.finished, st.finish_reason = True, "abort"
+                    self.metrics.success.inc(model_name=self.model_name, finished_reason="abort")
+                self.sched.release(iid)
 
     def has_unfinished(self) -> bool:
+        if self._pending_aborts:
+            self._apply_aborts()
         return self.sched.has_work()
 
     @property
@@ -144,6 +155,8 @@ class LLMEngine:
     # ------------------------------------------------------------------ step
     def step(self) -> list[RequestOutput]:
         t0 = time.time()
+        if self._pending_aborts:
+            self._apply_aborts()
         with self._lock:
             info = self.sched.schedule(self.runner.host_buffers())
         if info["num_seqs"] == 0:

@@ -1,0 +1,346 @@
+"""OpenAI-compatible HTTP server for one engine replica (the llm-d "model server").
+
+Routes (contract observed by the reference: llm-d-test.yaml:32-78 and the OTel scrape
+of /metrics on :8000, otel-observability-setup.yaml:337-391):
+  GET  /v1/models            -> model list (id = served model name, e.g. Qwen/Qwen3-0.6B)
+  POST /v1/completions       -> text completion (stream / non-stream, OpenAI schema)
+  POST /v1/chat/completions  -> chat completion through a Jinja chat template
+  POST /tokenize, /detokenize
+  GET  /health, /ready, /version, /metrics (Prometheus text)
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import contextlib
+import json
+import os
+import time
+import uuid
+from typing import Any, Optional
+
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+
+from .. import __version__
+from ..engine.config import EngineConfig, SamplingParams
+from ..utils import chat_template
+from .async_engine import AsyncEngine, EngineDeadError
+
+
+def _err(status: int, msg: str, typ: str = "invalid_request_error") -> JSONResponse:
+    return JSONResponse({"object": "error", "message": msg, "type": typ, "code": status},
+                        status_code=status)
+
+
+def _sampling_from(body: dict, default_max: int = 16) -> SamplingParams:
+    stop = body.get("stop") or []
+    if isinstance(stop, str):
+        stop = [stop]
+    max_tokens = body.get("max_tokens", body.get("max_completion_tokens"))
+    return SamplingParams(
+        max_tokens=int(max_tokens) if max_tokens is not None else default_max,
+        temperature=float(body.get("temperature", 1.0) if body.get("temperature") is not None else 1.0),
+        top_p=float(body.get("top_p", 1.0) if body.get("top_p") is not None else 1.0),
+        top_k=int(body.get("top_k", 0) or 0),
+        min_tokens=int(body.get("min_tokens", 0) or 0),
+        seed=body.get("seed"),
+        stop=list(stop),
+        stop_token_ids=list(body.get("stop_token_ids") or []),
+        ignore_eos=bool(body.get("ignore_eos", False)),
+        n=int(body.get("n", 1) or 1),
+    )
+
+
+def _prompts_of(prompt) -> list:
+    """OpenAI 'prompt' may be str | list[str] | list[int] | list[list[int]]."""
+    if isinstance(prompt, str):
+        return [prompt]
+    if isinstance(prompt, list) and prompt and all(isinstance(x, int) for x in prompt):
+        return [prompt]
+    if isinstance(prompt, list):
+        return list(prompt)
+    raise ValueError("prompt must be a string, a list of strings or token ids")
+
+
+class OpenAIServer:
+    def __init__(self, aengine: AsyncEngine, served_name: str, chat_tmpl: Optional[str],
+                 max_model_len: int):
+        self.ae = aengine
+        self.name = served_name
+        self.template = chat_template.load_template(chat_tmpl)
+        self.max_model_len = max_model_len
+        self.created = int(time.time())
+        self.app = self._build()
+
+    # ------------------------------------------------------------------ helpers
+    def _model_ok(self, body: dict) -> Optional[JSONResponse]:
+        m = body.get("model")
+        if m is not None and m != self.name:
+            return _err(404, f"The model `{m}` does not exist.", "NotFoundError")
+        return None
+
+    async def _collect(self, prompt, sp: SamplingParams, rid: str, prompt_ids=None):
+        final = None
+        async for o in self.ae.generate(prompt, sp, rid, prompt_ids=prompt_ids, stream=False):
+            final = o
+        return final
+
+    # ------------------------------------------------------------------ routes
+    def _build(self) -> FastAPI:
+        @contextlib.asynccontextmanager
+        async def lifespan(_app):
+            if not self.ae._thread.is_alive():
+                self.ae.start(asyncio.get_running_loop())
+            yield
+            self.ae.stop()
+
+        app = FastAPI(title="akap MI355X OpenAI server", version=__version__, lifespan=lifespan)
+        eng = self.ae.engine
+
+        @app.get("/health")
+        async def health():
+            if not self.ae.healthy:
+                return _err(503, "engine dead", "ServiceUnavailable")
+            return {"status": "ok"}
+
+        @app.get("/ready")
+        async def ready():
+            return await health()
+
+        @app.get("/version")
+        async def version():
+            return {"version": __version__, "backend": "akap-mi355x", "model": self.name}
+
+        @app.get("/metrics")
+        async def metrics():
+            eng._update_gauges()
+            return PlainTextResponse(eng.metrics.render(),
+                                     media_type="text/plain; version=0.0.4; charset=utf-8")
+
+        @app.get("/v1/models")
+        async def models():
+            return {"object": "list", "data": [{
+                "id": self.name, "object": "model", "created": self.created,
+                "owned_by": "akap", "root": self.name, "parent": None,
+                "max_model_len": self.max_model_len}]}
+
+        @app.post("/tokenize")
+        async def tokenize(req: Request):
+            body = await req.json()
+            if "messages" in body:
+                text = chat_template.render(body["messages"], self.template,
+                                            body.get("add_generation_prompt", True))
+            else:
+                text = body.get("prompt", "")
+            toks = eng.tokenizer.encode(text)
+            return {"tokens": toks, "count": len(toks), "max_model_len": self.max_model_len}
+
+        @app.post("/detokenize")
+        async def detokenize(req: Request):
+            body = await req.json()
+            return {"prompt": eng.tokenizer.decode(body.get("tokens", []))}
+
+        @app.post("/v1/completions")
+        async def completions(req: Request):
+            try:
+                body = await req.json()
+            except Exception:
+                return _err(400, "invalid JSON body")
+            bad = self._model_ok(body)
+            if bad:
+                return bad
+            try:
+                sp = _sampling_from(body)
+                prompts = _prompts_of(body.get("prompt", ""))
+            except (ValueError, TypeError) as e:
+                return _err(400, str(e))
+            cid = f"cmpl-{uuid.uuid4().hex}"
+            created = int(time.time())
+            if body.get("stream"):
+                if len(prompts) != 1 or sp.n != 1:
+                    return _err(400, "streaming supports a single prompt with n=1")
+                return StreamingResponse(self._stream_completion(cid, created, prompts[0], sp,
+                                                                 body), media_type="text/event-stream")
+            try:
+                jobs = []
+                for i, p in enumerate(prompts):
+                    for j in range(sp.n):
+                        pid = p if isinstance(p, list) else None
+                        jobs.append(self._collect(p if isinstance(p, str) else None, sp,
+                                                  f"{cid}-{i}-{j}", prompt_ids=pid))
+                outs = await asyncio.gather(*jobs)
+            except EngineDeadError as e:
+                return _err(500, "engine failure: " + str(e)[:200], "InternalServerError")
+            except ValueError as e:
+                return _err(400, str(e))
+            choices, ptok, ctok = [], 0, 0
+            for k, o in enumerate(outs):
+                text = o.text
+                if body.get("echo") and isinstance(prompts[k // sp.n], str):
+                    text = prompts[k // sp.n] + text
+                choices.append({"index": k, "text": text, "logprobs": None,
+                                "finish_reason": o.finish_reason, "stop_reason": None})
+                ctok += len(o.output_ids)
+                if k % sp.n == 0:
+                    ptok += len(o.prompt_ids)
+            return {"id": cid, "object": "text_completion", "created": created,
+                    "model": self.name, "choices": choices,
+                    "usage": {"prompt_tokens": ptok, "completion_tokens": ctok,
+                              "total_tokens": ptok + ctok}}
+
+        @app.post("/v1/chat/completions")
+        async def chat(req: Request):
+            try:
+                body = await req.json()
+            except Exception:
+                return _err(400, "invalid JSON body")
+            bad = self._model_ok(body)
+            if bad:
+                return bad
+            msgs = body.get("messages")
+            if not isinstance(msgs, list) or not msgs:
+                return _err(400, "messages must be a non-empty list")
+            tmpl = self.template
+            if body.get("chat_template"):
+                try:
+                    tmpl = chat_template.load_template(body["chat_template"])
+                except ValueError as e:
+                    return _err(400, str(e))
+            try:
+                prompt = chat_template.render(msgs, tmpl, body.get("add_generation_prompt", True))
+                sp = _sampling_from(body, default_max=max(16, self.max_model_len // 4))
+            except Exception as e:
+                return _err(400, f"chat template error: {e}")
+            cid = f"chatcmpl-{uuid.uuid4().hex}"
+            created = int(time.time())
+            if body.get("stream"):
+                return StreamingResponse(self._stream_chat(cid, created, prompt, sp, body),
+                                         media_type="text/event-stream")
+            try:
+                outs = await asyncio.gather(*[self._collect(prompt, sp, f"{cid}-{j}")
+                                              for j in range(sp.n)])
+            except EngineDeadError as e:
+                return _err(500, "engine failure: " + str(e)[:200], "InternalServerError")
+            except ValueError as e:
+                return _err(400, str(e))
+            choices = [{"index": j, "message": {"role": "assistant", "content": o.text},
+                        "logprobs": None, "finish_reason": o.finish_reason}
+                       for j, o in enumerate(outs)]
+            ptok = len(outs[0].prompt_ids)
+            ctok = sum(len(o.output_ids) for o in outs)
+            return {"id": cid, "object": "chat.completion", "created": created,
+                    "model": self.name, "choices": choices,
+                    "usage": {"prompt_tokens": ptok, "completion_tokens": ctok,
+                              "total_tokens": ptok + ctok}}
+
+        return app
+
+    # ------------------------------------------------------------------ SSE
+    async def _stream_completion(self, cid, created, prompt, sp, body):
+        pid = prompt if isinstance(prompt, list) else None
+        ptext = prompt if isinstance(prompt, str) else None
+        n_out, n_prompt = 0, 0
+        try:
+            async for o in self.ae.generate(ptext, sp, cid, prompt_ids=pid, stream=True):
+                n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
+                chunk = {"id": cid, "object": "text_completion", "created": created,
+                         "model": self.name, "choices": [{
+                             "index": 0, "text": o.delta_text, "logprobs": None,
+                             "finish_reason": o.finish_reason if o.finished else None}]}
+                yield f"data: {json.dumps(chunk)}\n\n"
+        except Exception as e:  # surface errors in-band, as vLLM does
+            yield f"data: {json.dumps({'error': {'message': str(e)[:300]}})}\n\n"
+        if (body.get("stream_options") or {}).get("include_usage"):
+            u = {"id": cid, "object": "text_completion", "created": created, "model": self.name,
+                 "choices": [], "usage": {"prompt_tokens": n_prompt, "completion_tokens": n_out,
+                                          "total_tokens": n_prompt + n_out}}
+            yield f"data: {json.dumps(u)}\n\n"
+        yield "data: [DONE]\n\n"
+
+    async def _stream_chat(self, cid, created, prompt, sp, body):
+        first = {"id": cid, "object": "chat.completion.chunk", "created": created,
+                 "model": self.name, "choices": [{"index": 0, "delta": {"role": "assistant",
+                                                                        "content": ""},
+                                                  "finish_reason": None}]}
+        yield f"data: {json.dumps(first)}\n\n"
+        n_out, n_prompt = 0, 0
+        try:
+            async for o in self.ae.generate(prompt, sp, cid, stream=True):
+                n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
+                chunk = {"id": cid, "object": "chat.completion.chunk", "created": created,
+                         "model": self.name, "choices": [{
+                             "index": 0, "delta": {"content": o.delta_text} if o.delta_text else {},
+                             "finish_reason": o.finish_reason if o.finished else None}]}
+                yield f"data: {json.dumps(chunk)}\n\n"
+        except Exception as e:
+            yield f"data: {json.dumps({'error': {'message': str(e)[:300]}})}\n\n"
+        if (body.get("stream_options") or {}).get("include_usage"):
+            u = {"id": cid, "object": "chat.completion.chunk", "created": created,
+                 "model": self.name, "choices": [],
+                 "usage": {"prompt_tokens": n_prompt, "completion_tokens": n_out,
+                           "total_tokens": n_prompt + n_out}}
+            yield f"data: {json.dumps(u)}\n\n"
+        yield "data: [DONE]\n\n"
+
+
+def make_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser("akap-serve", description="MI355X OpenAI-compatible server")
+    ap.add_argument("--model", default=os.environ.get("AKAP_MODEL", "qwen3-0.6b"))
+    ap.add_argument("--served-model-name", default=None)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
+    ap.add_argument("--block-size", type=int, default=32)
+    ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
+    ap.add_argument("--num-gpu-blocks", type=int, default=None)
+    ap.add_argument("--tensor-parallel-size", "-tp", type=int, default=1)
+    ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--no-enable-prefix-caching", action="store_true")
+    ap.add_argument("--chat-template", default=None)
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--load-format", default="random", choices=["random", "safetensors"])
+    ap.add_argument("--weights-path", default=None)
+    ap.add_argument("--kv-role", default="both", choices=["both", "prefill", "decode"])
+    return ap
+
+
+def engine_config_from_args(a) -> EngineConfig:
+    return EngineConfig(
+        model=a.model, served_model_name=a.served_model_name, max_model_len=a.max_model_len,
+        max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_num_batched_tokens,
+        block_size=a.block_size, gpu_memory_utilization=a.gpu_memory_utilization,
+        num_gpu_blocks=a.num_gpu_blocks, enable_prefix_caching=not a.no_enable_prefix_caching,
+        enforce_eager=a.enforce_eager, tensor_parallel_size=a.tensor_parallel_size, seed=a.seed,
+        device=a.device, load_format=a.load_format, weights_path=a.weights_path,
+        chat_template=a.chat_template, kv_role=a.kv_role)
+
+
+def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:
+    from ..engine.llm_engine import LLMEngine
+
+    eng = engine or LLMEngine(ecfg)
+    ae = AsyncEngine(eng)
+    srv = OpenAIServer(ae, eng.model_name, ecfg.chat_template, ecfg.max_model_len)
+    return srv.app, ae
+
+
+def main(argv: Optional[list] = None) -> None:
+    import uvicorn
+
+    a = make_parser().parse_args(argv)
+    ecfg = engine_config_from_args(a)
+    if a.tensor_parallel_size > 1:
+        from ..parallel.tp_worker import serve_tp
+
+        serve_tp(ecfg, a.host, a.port)
+        return
+    app, _ = build_app(ecfg)
+    uvicorn.run(app, host=a.host, port=a.port, log_level="info", access_log=False)
+
+
+if __name__ == "__main__":
+    main()

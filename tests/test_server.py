@@ -1,0 +1,105 @@
+"""OpenAI API server on the CPU engine: the reference smoke test's contract
+(llm-d-test.yaml:32-78: GET /v1/models contains the model id; POST /v1/completions with
+{"model", "prompt"} and no max_tokens), plus chat, streaming, errors and /metrics."""
+import json
+
+import pytest
+from fastapi.testclient import TestClient
+
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig
+from aws_k8s_ansible_provisioner_amd.server.api_server import build_app
+
+MODEL = "Qwen/Qwen3-0.6B"
+
+
+@pytest.fixture(scope="module")
+def client():
+    ecfg = EngineConfig(model="tiny-qwen3", served_model_name=MODEL, device="cpu",
+                        max_model_len=256, max_num_seqs=8, max_num_batched_tokens=64,
+                        block_size=16, num_gpu_blocks=128, chat_template="default")
+    app, ae = build_app(ecfg)
+    with TestClient(app) as c:
+        yield c
+
+
+def test_models_lists_served_model(client):
+    r = client.get("/v1/models")
+    assert r.status_code == 200
+    assert MODEL in r.text
+    assert r.json()["data"][0]["id"] == MODEL
+
+
+def test_reference_smoke_completion(client):
+    r = client.post("/v1/completions", json={"model": MODEL, "prompt": "Who are you?"})
+    assert r.status_code == 200, r.text
+    j = r.json()
+    assert j["object"] == "text_completion" and j["model"] == MODEL
+    assert j["usage"]["completion_tokens"] <= 16 and j["usage"]["prompt_tokens"] == 12
+    assert j["choices"][0]["finish_reason"] in ("length", "stop")
+
+
+def test_batch_prompts_token_ids_and_n(client):
+    r = client.post("/v1/completions", json={"prompt": [[5, 6, 7], [8, 9]], "max_tokens": 4,
+                                             "temperature": 0, "n": 2, "ignore_eos": True})
+    j = r.json()
+    assert len(j["choices"]) == 4
+    assert all(c["finish_reason"] == "length" for c in j["choices"])
+    assert j["usage"]["completion_tokens"] == 16
+    # greedy: both samples of a prompt agree
+    assert j["choices"][0]["text"] == j["choices"][1]["text"]
+
+
+def test_streaming_completion_sse(client):
+    with client.stream("POST", "/v1/completions",
+                       json={"prompt": "abc", "max_tokens": 5, "temperature": 0, "stream": True,
+                             "ignore_eos": True,
+                             "stream_options": {"include_usage": True}}) as r:
+        lines = [l for l in r.iter_lines() if l.startswith("data: ")]
+    assert lines[-1] == "data: [DONE]"
+    chunks = [json.loads(l[6:]) for l in lines[:-1]]
+    assert chunks[-1]["usage"]["completion_tokens"] == 5
+    fins = [c["choices"][0]["finish_reason"] for c in chunks if c["choices"]]
+    assert fins[-1] == "length" and fins.count("length") == 1
+
+
+def test_chat_completion_and_stream(client):
+    msgs = [{"role": "system", "content": "be brief"}, {"role": "user", "content": "hi"}]
+    r = client.post("/v1/chat/completions", json={"model": MODEL, "messages": msgs,
+                                                  "max_tokens": 6, "temperature": 0})
+    j = r.json()
+    assert j["object"] == "chat.completion"
+    assert j["choices"][0]["message"]["role"] == "assistant"
+    with client.stream("POST", "/v1/chat/completions",
+                       json={"messages": msgs, "max_tokens": 3, "stream": True,
+                             "temperature": 0, "ignore_eos": True}) as r:
+        lines = [l for l in r.iter_lines() if l.startswith("data: ")]
+    first = json.loads(lines[0][6:])
+    assert first["choices"][0]["delta"]["role"] == "assistant"
+    assert lines[-1] == "data: [DONE]"
+
+
+def test_chat_template_override_and_tokenize(client):
+    msgs = [{"role": "user", "content": "Hi"}]
+    r = client.post("/tokenize", json={"messages": msgs})
+    assert r.json()["count"] == len("User: Hi\n\nAssistant:")
+    r = client.post("/v1/chat/completions", json={"messages": msgs, "chat_template": "phi",
+                                                  "max_tokens": 2})
+    assert r.status_code == 200
+
+
+def test_errors(client):
+    assert client.post("/v1/completions", json={"model": "nope", "prompt": "x"}).status_code == 404
+    assert client.post("/v1/completions", json={"prompt": {"bad": 1}}).status_code == 400
+    assert client.post("/v1/chat/completions", json={"messages": []}).status_code == 400
+    too_long = list(range(5, 400))
+    assert client.post("/v1/completions", json={"prompt": too_long}).status_code == 400
+
+
+def test_health_and_metrics(client):
+    assert client.get("/health").json()["status"] == "ok"
+    m = client.get("/metrics").text
+    for name in ["vllm:num_requests_running", "vllm:prompt_tokens_total",
+                 "vllm:generation_tokens_total", "vllm:time_to_first_token_seconds_bucket",
+                 "vllm:gpu_cache_usage_perc", "vllm_request_total", "vllm_active_requests",
+                 "vllm_request_duration_seconds_bucket"]:
+        assert name in m, name
