@@ -1,0 +1,188 @@
+"""Endpoint picker (the llm-d "EPP"): chooses the model-server pod for each request.
+
+Scoring (higher is better), per candidate endpoint e:
+  queue    = 1 / (1 + waiting_e + 0.25 * running_e + inflight_e)      (load)
+  kv       = 1 - kv_usage_e                                            (KV headroom)
+  prefix   = matched_prefix_blocks_e / request_blocks                   (cache affinity)
+  score    = w_queue * queue + w_kv * kv + w_prefix * prefix
+Endpoints that are unhealthy, or whose metrics are stale, are filtered out.  The prefix
+index is the gateway's own memory of which endpoint served which prompt-prefix block
+hashes (same chained-hash scheme as the engine's prefix cache, computed on the prompt
+text in fixed-size character blocks), so routing is cache-aware without asking pods.
+
+Disaggregated prefill/decode: with both roles present and a prompt of at least
+`pd_threshold` characters, `pick_pd` returns a (prefill, decode) pair.
+"""
+from __future__ import annotations
+
+import dataclasses
+import hashlib
+import random
+import threading
+import time
+from collections import OrderedDict
+from typing import Optional
+
+
+@dataclasses.dataclass
+class Endpoint:
+    url: str
+    role: str = "both"  # both | prefill | decode
+    healthy: bool = True
+    running: float = 0.0
+    waiting: float = 0.0
+    kv_usage: float = 0.0
+    inflight: int = 0
+    last_scrape: float = 0.0
+    failures: int = 0
+    served: int = 0
+
+    def load_score(self) -> float:
+        return 1.0 / (1.0 + self.waiting + 0.25 * self.running + self.inflight)
+
+
+def prefix_hashes(text: str, block_chars: int = 64, max_blocks: int = 64) -> list[int]:
+    hs, parent = [], b""
+    n = min(len(text) // block_chars, max_blocks)
+    for i in range(n):
+        h = hashlib.blake2b(parent + text[i * block_chars:(i + 1) * block_chars].encode(),
+                            digest_size=8).digest()
+        hs.append(int.from_bytes(h, "little"))
+        parent = h
+    return hs
+
+
+class PrefixIndex:
+    """LRU map: prefix-block hash -> endpoint url."""
+
+    def __init__(self, capacity: int = 200_000):
+        self.cap = capacity
+        self.map: OrderedDict[int, str] = OrderedDict()
+        self.lock = threading.Lock()
+
+    def match(self, hashes: list[int]) -> dict[str, int]:
+        """Per endpoint: number of leading prefix blocks it is known to hold."""
+        out: dict[str, int] = {}
+        with self.lock:
+            for i, h in enumerate(hashes):
+                url = self.map.get(h)
+                if url is None:
+                    break
+                self.map.move_to_end(h)
+                out[url] = i + 1
+        return out
+
+    def insert(self, hashes: list[int], url: str) -> None:
+        with self.lock:
+            for h in hashes:
+                self.map[h] = url
+                self.map.move_to_end(h)
+            while len(self.map) > self.cap:
+                self.map.popitem(last=False)
+
+
+@dataclasses.dataclass
+class PickerConfig:
+    w_queue: float = 1.0
+    w_kv: float = 1.0
+    w_prefix: float = 2.0
+    stale_after_s: float = 15.0
+    pd_threshold_chars: int = 512
+    block_chars: int = 64
+
+
+class EndpointPicker:
+    def __init__(self, endpoints: list[Endpoint], cfg: Optional[PickerConfig] = None,
+                 seed: int = 0):
+        self.cfg = cfg or PickerConfig()
+        self.eps: dict[str, Endpoint] = {e.url: e for e in endpoints}
+        self.prefix = PrefixIndex()
+        self.rng = random.Random(seed)
+        self.lock = threading.Lock()
+
+    # ---------------------------------------------------------------- membership
+    def set_endpoints(self, urls_roles: list[tuple[str, str]]) -> None:
+        with self.lock:
+            keep = {}
+            for url, role in urls_roles:
+                keep[url] = self.eps.get(url) or Endpoint(url, role)
+                keep[url].role = role
+            self.eps = keep
+
+    def endpoints(self) -> list[Endpoint]:
+        return list(self.eps.values())
+
+    def update_metrics(self, url: str, running: float, waiting: float, kv: float) -> None:
+        e = self.eps.get(url)
+        if e is None:
+            return
+        e.running, e.waiting, e.kv_usage = running, waiting, kv
+        e.last_scrape = time.time()
+        e.healthy = True
+        e.failures = 0
+
+    def mark_failure(self, url: str, hard: bool = False) -> None:
+        e = self.eps.get(url)
+        if e is None:
+            return
+        e.failures += 1
+        if hard or e.failures >= 3:
+            e.healthy = False
+
+    # ---------------------------------------------------------------- scoring
+    def _candidates(self, roles: tuple[str, ...]) -> list[Endpoint]:
+        now = time.time()
+        c = [e for e in self.eps.values() if e.healthy and e.role in roles and
+             (e.last_scrape == 0.0 or now - e.last_scrape < self.cfg.stale_after_s)]
+        if not c:  # degrade gracefully: anything healthy in the role set
+            c = [e for e in self.eps.values() if e.healthy and e.role in roles]
+        return c
+
+    def score(self, e: Endpoint, prefix_match: dict[str, int], nblocks: int) -> float:
+        cfg = self.cfg
+        p = (prefix_match.get(e.url, 0) / nblocks) if nblocks else 0.0
+        return (cfg.w_queue * e.load_score() + cfg.w_kv * (1.0 - e.kv_usage)
+                + cfg.w_prefix * p)
+
+    def pick(self, prompt_text: str = "", roles: tuple[str, ...] = ("both",)) -> Optional[Endpoint]:
+        cands = self._candidates(roles)
+        if not cands:
+            return None
+        hs = prefix_hashes(prompt_text, self.cfg.block_chars)
+        match = self.prefix.match(hs)
+        best, best_s = [], -1e30
+        for e in cands:
+            s = self.score(e, match, len(hs))
+            if s > best_s + 1e-9:
+                best, best_s = [e], s
+            elif abs(s - best_s) <= 1e-9:
+                best.append(e)
+        chosen = self.rng.choice(best)
+        if hs:
+            self.prefix.insert(hs, chosen.url)
+        chosen.served += 1
+        return chosen
+
+    def pick_pd(self, prompt_text: str) -> tuple[Optional[Endpoint], Optional[Endpoint]]:
+        """(prefill, decode) for disaggregated serving, or (None, endpoint) when the
+        request should run monolithically (short prompt or no P/D pool)."""
+        has_p = any(e.role == "prefill" and e.healthy for e in self.eps.values())
+        has_d = any(e.role == "decode" and e.healthy for e in self.eps.values())
+        if has_p and has_d and len(prompt_text) >= self.cfg.pd_threshold_chars:
+            return self.pick(prompt_text, ("prefill",)), self.pick(prompt_text, ("decode",))
+        return None, self.pick(prompt_text, ("both", "decode"))
+
+
+def parse_prometheus(text: str) -> dict[str, float]:
+    """Sum samples per metric name (labels dropped) from Prometheus text format."""
+    out: dict[str, float] = {}
+    for line in text.splitlines():
+        if not line or line[0] == "#":
+            continue
+        try:
+            name_part, val = line.rsplit(" ", 1)
+            name = name_part.split("{", 1)[0]
+            out[name] = out.get(name, 0.0) + float(val)
+        except ValueError:
+            continue
+    return out

@@ -1,0 +1,152 @@
+"""Gateway + endpoint picker: scoring, prefix affinity, P/D pairing, failover, and an
+end-to-end run of the reference smoke test (llm-d-test.yaml) through the gateway in
+front of two real CPU engine servers."""
+import asyncio
+import json
+import socket
+import threading
+import time
+
+import aiohttp
+import pytest
+import uvicorn
+from aiohttp import web
+
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig
+from aws_k8s_ansible_provisioner_amd.gateway.picker import (Endpoint, EndpointPicker,
+                                                            PickerConfig, parse_prometheus,
+                                                            prefix_hashes)
+from aws_k8s_ansible_provisioner_amd.gateway.server import Gateway, _parse_dns, _parse_targets
+from aws_k8s_ansible_provisioner_amd.server.api_server import build_app
+
+MODEL = "Qwen/Qwen3-0.6B"
+
+
+def test_picker_prefers_least_loaded_and_kv_headroom():
+    p = EndpointPicker([Endpoint("a"), Endpoint("b"), Endpoint("c")])
+    p.update_metrics("a", running=10, waiting=5, kv=0.9)
+    p.update_metrics("b", running=1, waiting=0, kv=0.2)
+    p.update_metrics("c", running=4, waiting=1, kv=0.5)
+    assert p.pick("x").url == "b"
+    p.mark_failure("b", hard=True)
+    assert p.pick("x").url == "c"
+
+
+def test_picker_prefix_affinity():
+    p = EndpointPicker([Endpoint("a"), Endpoint("b")], PickerConfig(w_prefix=5.0))
+    for u in "ab":
+        p.update_metrics(u, 0, 0, 0.0)
+    doc = "shared system prompt " * 40
+    first = p.pick(doc + " q1").url
+    # same long prefix -> same endpoint even when it is slightly busier
+    p.update_metrics(first, running=2, waiting=0, kv=0.1)
+    assert p.pick(doc + " q2").url == first
+    assert len(prefix_hashes(doc, 64)) == len(doc) // 64
+
+
+def test_picker_pd_pairs():
+    eps = [Endpoint("p1", "prefill"), Endpoint("d1", "decode"), Endpoint("m1", "both")]
+    p = EndpointPicker(eps, PickerConfig(pd_threshold_chars=100))
+    pre, dec = p.pick_pd("y" * 200)
+    assert pre.url == "p1" and dec.url == "d1"
+    pre, dec = p.pick_pd("short")
+    assert pre is None and dec.url in ("m1", "d1")
+
+
+def test_parsers():
+    m = parse_prometheus('# HELP x\nvllm:num_requests_running{model_name="m"} 3.0\n'
+                         'vllm:num_requests_running{model_name="n"} 2\nbad line\n')
+    assert m["vllm:num_requests_running"] == 5.0
+    assert _parse_targets("a:8000@prefill,http://b:9/") == [("http://a:8000", "prefill"),
+                                                            ("http://b:9", "both")]
+    assert _parse_dns("svc.ns.svc.cluster.local:8000@decode") == [
+        ("svc.ns.svc.cluster.local", 8000, "decode")]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Uvicorn(threading.Thread):
+    def __init__(self, app, port):
+        super().__init__(daemon=True)
+        self.server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port,
+                                                    log_level="error"))
+
+    def run(self):
+        self.server.run()
+
+
+@pytest.fixture(scope="module")
+def two_engines():
+    servers, urls = [], []
+    for i in range(2):
+        ecfg = EngineConfig(model="tiny-qwen3", served_model_name=MODEL, device="cpu",
+                            max_model_len=256, max_num_seqs=8, max_num_batched_tokens=64,
+                            block_size=16, num_gpu_blocks=128, seed=i)
+        app, _ = build_app(ecfg)
+        port = _free_port()
+        t = _Uvicorn(app, port)
+        t.start()
+        servers.append(t)
+        urls.append(f"http://127.0.0.1:{port}")
+    for u in urls:
+        for _ in range(200):
+            try:
+                import urllib.request
+                urllib.request.urlopen(u + "/health", timeout=1)
+                break
+            except Exception:
+                time.sleep(0.05)
+    yield urls
+    for t in servers:
+        t.server.should_exit = True
+
+
+def test_gateway_end_to_end_reference_smoke(two_engines):
+    async def run():
+        gw = Gateway([(u, "both") for u in two_engines] + [("http://127.0.0.1:9", "both")], [],
+                     scrape_interval=0.2)
+        app = gw.app()
+        runner = web.AppRunner(app)
+        await runner.setup()
+        port = _free_port()
+        site = web.TCPSite(runner, "127.0.0.1", port)
+        await site.start()
+        base = f"http://127.0.0.1:{port}"
+        try:
+            await asyncio.sleep(0.5)
+            async with aiohttp.ClientSession() as s:
+                # llm-d-test.yaml:32-59 -- GET /v1/models through the gateway
+                async with s.get(base + "/v1/models") as r:
+                    text = await r.text()
+                assert MODEL in text
+                # llm-d-test.yaml:61-78 -- POST /v1/completions through the gateway
+                for _ in range(6):
+                    async with s.post(base + "/v1/completions",
+                                      json={"model": MODEL, "prompt": "Who are you?"}) as r:
+                        assert r.status == 200
+                        j = await r.json()
+                        assert j["choices"][0]["text"] is not None
+                # streaming passthrough
+                async with s.post(base + "/v1/chat/completions",
+                                  json={"messages": [{"role": "user", "content": "hi"}],
+                                        "max_tokens": 3, "stream": True}) as r:
+                    body = await r.text()
+                assert body.rstrip().endswith("data: [DONE]")
+                async with s.get(base + "/health") as r:
+                    h = await r.json()
+                assert len(h["endpoints"]) == 2  # the dead :9 endpoint was ejected
+                async with s.get(base + "/metrics") as r:
+                    m = await r.text()
+                assert "akap_gateway_requests_total" in m
+            served = {e.url: e.served for e in gw.picker.endpoints()}
+            assert sum(served.values()) >= 7
+        finally:
+            await runner.cleanup()
+
+    asyncio.run(run())
