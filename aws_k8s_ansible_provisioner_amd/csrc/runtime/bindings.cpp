@@ -129,6 +129,16 @@ PYBIND11_MODULE(_runtime, m) {
         return out;
       })
       .def("reset_prefix_cache", [](Scheduler& s) { s.blocks_mut().reset_prefix_cache(); })
+      .def("set_hold_kv", &Scheduler::set_hold_kv)
+      .def("held_blocks", &Scheduler::held_blocks)
+      .def("free_held", &Scheduler::free_held)
+      .def_property_readonly("num_held", &Scheduler::num_held)
+      .def("reserve_prefilled", &Scheduler::reserve_prefilled, py::arg("id"), py::arg("tokens"),
+           py::arg("num_prompt"), py::arg("max_tokens"), py::arg("min_tokens") = 0,
+           py::arg("ignore_eos") = false, py::arg("stop_ids") = std::vector<int32_t>{},
+           py::arg("temperature") = 0.f, py::arg("top_p") = 1.f, py::arg("top_k") = 0,
+           py::arg("seed") = 0, py::arg("stream") = false)
+      .def("activate", &Scheduler::activate)
       .def_property_readonly("total_preemptions", &Scheduler::total_preemptions)
       .def("request_info", [](const Scheduler& s, int64_t id) -> py::object {
         auto r = s.get(id);

@@ -51,6 +51,64 @@ void Scheduler::release(int64_t id) {
   if (it != reqs_.end() && it->second->status == FINISHED) reqs_.erase(it);
 }
 
+void Scheduler::set_hold_kv(int64_t id, bool hold) {
+  auto it = reqs_.find(id);
+  if (it != reqs_.end()) it->second->hold_kv = hold;
+}
+
+std::vector<int32_t> Scheduler::held_blocks(int64_t id) const {
+  auto it = held_.find(id);
+  return it == held_.end() ? std::vector<int32_t>{} : it->second;
+}
+
+void Scheduler::free_held(int64_t id) {
+  auto it = held_.find(id);
+  if (it == held_.end()) return;
+  bm_.free_blocks(it->second);
+  held_.erase(it);
+}
+
+std::vector<int32_t> Scheduler::reserve_prefilled(
+    int64_t id, const std::vector<int32_t>& tokens, int num_prompt, int max_tokens,
+    int min_tokens, bool ignore_eos, const std::vector<int32_t>& stop_ids, float temperature,
+    float top_p, int top_k, int64_t seed, bool stream) {
+  if (reqs_.count(id)) throw std::invalid_argument("duplicate request id");
+  if (num_prompt <= 0 || (int)tokens.size() != num_prompt + 1)
+    throw std::invalid_argument("reserve_prefilled: tokens must be prompt + first token");
+  if ((int)tokens.size() >= cfg_.max_model_len)
+    throw std::invalid_argument("prompt longer than max_model_len");
+  auto r = std::make_unique<Request>();
+  r->id = id;
+  r->tokens = tokens;
+  r->num_prompt = num_prompt;
+  r->max_tokens = std::max(1, max_tokens);
+  r->min_tokens = min_tokens;
+  r->ignore_eos = ignore_eos;
+  r->stop_ids = stop_ids;
+  r->temperature = temperature;
+  r->top_p = top_p;
+  r->top_k = top_k;
+  r->seed = seed;
+  r->stream = stream;
+  r->prefix_checked = true;
+  if (!ensure_blocks(*r, num_prompt)) {
+    if (!r->blocks.empty()) bm_.free_blocks(r->blocks);
+    return {};
+  }
+  r->num_computed = num_prompt;
+  r->status = PENDING_KV;
+  std::vector<int32_t> out = r->blocks;
+  reqs_.emplace(id, std::move(r));
+  return out;
+}
+
+void Scheduler::activate(int64_t id) {
+  auto it = reqs_.find(id);
+  if (it == reqs_.end() || it->second->status != PENDING_KV) return;
+  it->second->status = RUNNING;
+  running_.push_back(it->second.get());
+}
+
 bool Scheduler::abort_request(int64_t id) {
   auto it = reqs_.find(id);
   if (it == reqs_.end()) return false;
@@ -58,6 +116,7 @@ bool Scheduler::abort_request(int64_t id) {
   if (r->status == FINISHED) return false;
   if (r->status == WAITING) {
     waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), r), waiting_.end());
+  } else if (r->status == PENDING_KV) {
   } else {
     running_.erase(std::remove(running_.begin(), running_.end(), r), running_.end());
   }
@@ -68,7 +127,11 @@ bool Scheduler::abort_request(int64_t id) {
 }
 
 void Scheduler::finish(Request& r, int reason) {
-  if (!r.blocks.empty()) bm_.free_blocks(r.blocks);
+  if (r.hold_kv && reason != FINISH_ABORT && !r.blocks.empty()) {
+    held_[r.id] = r.blocks;  // P/D: ownership moves to the transfer agent
+  } else if (!r.blocks.empty()) {
+    bm_.free_blocks(r.blocks);
+  }
   r.blocks.clear();
   r.hashes.clear();
   r.status = FINISHED;

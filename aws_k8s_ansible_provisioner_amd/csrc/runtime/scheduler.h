@@ -20,7 +20,7 @@
 
 namespace akap_rt {
 
-enum ReqStatus : int { WAITING = 0, RUNNING = 1, FINISHED = 2 };
+enum ReqStatus : int { WAITING = 0, RUNNING = 1, FINISHED = 2, PENDING_KV = 3 };
 enum FinishReason : int { NOT_FINISHED = 0, FINISH_LENGTH = 1, FINISH_STOP = 2, FINISH_ABORT = 3 };
 
 struct Request {
@@ -45,6 +45,7 @@ struct Request {
   int top_k = 0;
   int64_t seed = 0;
   bool stream = false;  // report every token (else only first token + finish)
+  bool hold_kv = false; // P/D prefill side: keep KV blocks after finishing (for transfer)
   int num_generated() const { return (int)tokens.size() - num_prompt; }
 };
 
@@ -119,6 +120,23 @@ class Scheduler {
   // drop a finished request's bookkeeping (called by the engine after delivery)
   void release(int64_t id);
 
+  // ---- disaggregated prefill/decode ----
+  void set_hold_kv(int64_t id, bool hold);
+  // prefill side: blocks of a finished hold_kv request (kept until free_held)
+  std::vector<int32_t> held_blocks(int64_t id) const;
+  void free_held(int64_t id);
+  // decode side: register a request whose prompt KV arrives from a prefill engine.
+  // tokens = prompt + first generated token.  Allocates the prompt's blocks and
+  // returns them (empty if the pool is short); the request is not scheduled until
+  // activate().
+  std::vector<int32_t> reserve_prefilled(int64_t id, const std::vector<int32_t>& tokens,
+                                         int num_prompt, int max_tokens, int min_tokens,
+                                         bool ignore_eos, const std::vector<int32_t>& stop_ids,
+                                         float temperature, float top_p, int top_k,
+                                         int64_t seed, bool stream);
+  void activate(int64_t id);
+  size_t num_held() const { return held_.size(); }
+
  private:
   bool ensure_blocks(Request& r, int num_tokens);
   void publish_full_blocks(Request& r);
@@ -131,6 +149,7 @@ class Scheduler {
   std::deque<Request*> waiting_;
   std::vector<Request*> running_;
   std::vector<Request*> last_sampled_;  // order of samples in the last step
+  std::unordered_map<int64_t, std::vector<int32_t>> held_;
   int64_t preemptions_ = 0;
 };
 

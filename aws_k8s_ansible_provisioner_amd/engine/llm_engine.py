@@ -39,6 +39,7 @@ class RequestState:
     finished: bool = False
     text: str = ""
     stream: bool = False
+    hold_kv: bool = False
 
 
 @dataclasses.dataclass
@@ -53,6 +54,7 @@ class RequestOutput:
     finish_reason: Optional[str]
     ttft: Optional[float] = None
     num_cached_tokens: int = 0
+    kv_transfer_params: Optional[dict] = None
 
 
 class LLMEngine:
@@ -85,11 +87,13 @@ class LLMEngine:
         self.steps = 0
         self.last_prefix = (0, 0)
         self.timers = {"schedule": 0.0, "execute": 0.0, "post": 0.0}
+        self.rank = self.runner.ps.rank
 
     # ------------------------------------------------------------------ requests
     def add_request(self, req_id: Optional[str], prompt: Union[str, list, None],
                     params: Optional[SamplingParams] = None,
-                    prompt_ids: Optional[list] = None, stream: bool = False) -> str:
+                    prompt_ids: Optional[list] = None, stream: bool = False,
+                    kv_transfer_params: Optional[dict] = None) -> str:
         """Queue a request.  stream=True reports every token (server SSE); otherwise the
         engine reports only the first token (TTFT) and the finished output."""
         params = (params or SamplingParams()).normalized()
@@ -105,17 +109,23 @@ class LLMEngine:
             raise ValueError(f"prompt has {len(prompt_ids)} tokens; max_model_len is "
                              f"{self.ecfg.max_model_len}")
         max_tokens = min(params.max_tokens, self.ecfg.max_model_len - len(prompt_ids))
+        hold = bool(kv_transfer_params and kv_transfer_params.get("do_remote_decode"))
+        if hold:
+            max_tokens = 1  # P/D prefill: first token only, KV kept for the decode engine
         iid = next(self._ids)
         req_id = req_id or f"req-{iid}"
         seed = params.seed if params.seed is not None else (iid * 7919 + self.ecfg.seed)
         st = RequestState(req_id, iid, prompt if isinstance(prompt, str) else None, prompt_ids,
                           params, time.time())
         st.stream = stream or bool(params.stop)
+        st.hold_kv = hold
         with self._lock:
             self.sched.add_request(iid, prompt_ids, max_tokens, params.min_tokens,
                                    params.ignore_eos, list(params.stop_token_ids),
                                    float(params.temperature), float(params.top_p),
                                    int(params.top_k), int(seed), st.stream)
+            if hold:
+                self.sched.set_hold_kv(iid, True)
             self.reqs[iid] = st
             self.by_name[req_id] = iid
         self.metrics.req_total.inc(model_name=self.model_name)
@@ -130,6 +140,46 @@ class LLMEngine:
                 return False
             self._pending_aborts.append(iid)
         return True
+
+    # ------------------------------------------------------------------ P/D
+    def held_blocks(self, transfer_id: int) -> list:
+        with self._lock:
+            return list(self.sched.held_blocks(int(transfer_id)))
+
+    def free_held(self, transfer_id: int) -> None:
+        with self._lock:
+            self.sched.free_held(int(transfer_id))
+
+    def reserve_prefilled(self, req_id: str, prompt_ids: list, first_token: int,
+                          params: SamplingParams, stream: bool = False):
+        """Decode side of P/D: allocate blocks for a remotely prefilled prompt.
+        Returns (iid, block_ids); block_ids is empty when the KV pool is short."""
+        params = params.normalized()
+        prompt_ids = [int(t) for t in prompt_ids]
+        max_tokens = min(params.max_tokens, self.ecfg.max_model_len - len(prompt_ids))
+        iid = next(self._ids)
+        seed = params.seed if params.seed is not None else (iid * 7919 + self.ecfg.seed)
+        st = RequestState(req_id, iid, None, prompt_ids, params, time.time())
+        st.stream = stream or bool(params.stop)
+        st.first_token_time = st.arrival
+        st.output_ids = [int(first_token)]
+        st.text = self.tokenizer.decode_token(int(first_token)) if st.stream else ""
+        with self._lock:
+            blocks = self.sched.reserve_prefilled(
+                iid, prompt_ids + [int(first_token)], len(prompt_ids), max_tokens,
+                params.min_tokens, params.ignore_eos, list(params.stop_token_ids),
+                float(params.temperature), float(params.top_p), int(params.top_k), int(seed),
+                st.stream)
+            if blocks:
+                self.reqs[iid] = st
+                self.by_name[req_id] = iid
+        if blocks:
+            self.metrics.req_total.inc(model_name=self.model_name)
+        return iid, list(blocks)
+
+    def activate(self, iid: int) -> None:
+        with self._lock:
+            self.sched.activate(int(iid))
 
     def _apply_aborts(self) -> None:
         with self._lock:
@@ -227,10 +277,15 @@ class LLMEngine:
                     self.by_name.pop(st.req_id, None)
             elif not st.stream:
                 continue  # first-token event of a non-streaming request: metrics only
+            kvp = None
+            if st.hold_kv and st.finished:
+                kvp = {"transfer_id": iid, "num_prompt": len(st.prompt_ids),
+                       "prompt_token_ids": st.prompt_ids, "first_token": st.output_ids[0],
+                       "remote_rank": self.rank, "num_blocks": len(self.sched.held_blocks(iid))}
             outs.append(RequestOutput(st.req_id, st.prompt_ids, st.output_ids, [tok], st.text,
                                       delta, st.finished, st.finish_reason,
                                       (st.first_token_time - st.arrival)
-                                      if st.first_token_time else None, cached))
+                                      if st.first_token_time else None, cached, kvp))
         self.steps += 1
         self._update_gauges()
         self.timers["post"] += time.time() - now

@@ -183,7 +183,9 @@ class Gateway:
             pre.inflight -= 1
         out = dict(body)
         if isinstance(j, dict) and j.get("kv_transfer_params"):
-            out["kv_transfer_params"] = j["kv_transfer_params"]
+            kvp = dict(j["kv_transfer_params"])
+            kvp["remote_url"] = pre.url
+            out["kv_transfer_params"] = kvp
         return out
 
     async def handle_models(self, request: web.Request) -> web.Response:

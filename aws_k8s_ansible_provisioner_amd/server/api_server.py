@@ -80,9 +80,10 @@ class OpenAIServer:
             return _err(404, f"The model `{m}` does not exist.", "NotFoundError")
         return None
 
-    async def _collect(self, prompt, sp: SamplingParams, rid: str, prompt_ids=None):
+    async def _collect(self, prompt, sp: SamplingParams, rid: str, prompt_ids=None, kvp=None):
         final = None
-        async for o in self.ae.generate(prompt, sp, rid, prompt_ids=prompt_ids, stream=False):
+        async for o in self.ae.generate(prompt, sp, rid, prompt_ids=prompt_ids, stream=False,
+                                        kv_transfer_params=kvp):
             final = o
         return final
 
@@ -141,6 +142,20 @@ class OpenAIServer:
             body = await req.json()
             return {"prompt": eng.tokenizer.decode(body.get("tokens", []))}
 
+        @app.post("/kv/push")
+        async def kv_push(req: Request):
+            """P/D prefill side: send a held request's KV to the decode rank."""
+            body = await req.json()
+            if self.ae.kv_agent is None:
+                return _err(400, "not a P/D prefill server")
+            tid = int(body["transfer_id"])
+            blocks = eng.held_blocks(tid)
+            if not blocks:
+                return _err(404, f"no held KV for transfer {tid}")
+            self.ae.kv_agent.send_blocks(blocks, int(body["dst_rank"]),
+                                         on_done=lambda: eng.free_held(tid))
+            return {"ok": True, "num_blocks": len(blocks)}
+
         @app.post("/v1/completions")
         async def completions(req: Request):
             try:
@@ -168,12 +183,15 @@ class OpenAIServer:
                     for j in range(sp.n):
                         pid = p if isinstance(p, list) else None
                         jobs.append(self._collect(p if isinstance(p, str) else None, sp,
-                                                  f"{cid}-{i}-{j}", prompt_ids=pid))
+                                                  f"{cid}-{i}-{j}", prompt_ids=pid,
+                                                  kvp=body.get("kv_transfer_params")))
                 outs = await asyncio.gather(*jobs)
             except EngineDeadError as e:
                 return _err(500, "engine failure: " + str(e)[:200], "InternalServerError")
             except ValueError as e:
                 return _err(400, str(e))
+            except RuntimeError as e:
+                return _err(503, str(e), "ServiceUnavailable")
             choices, ptok, ctok = [], 0, 0
             for k, o in enumerate(outs):
                 text = o.text
@@ -184,10 +202,13 @@ class OpenAIServer:
                 ctok += len(o.output_ids)
                 if k % sp.n == 0:
                     ptok += len(o.prompt_ids)
-            return {"id": cid, "object": "text_completion", "created": created,
+            resp = {"id": cid, "object": "text_completion", "created": created,
                     "model": self.name, "choices": choices,
                     "usage": {"prompt_tokens": ptok, "completion_tokens": ctok,
                               "total_tokens": ptok + ctok}}
+            if outs and outs[0].kv_transfer_params:
+                resp["kv_transfer_params"] = outs[0].kv_transfer_params
+            return resp
 
         @app.post("/v1/chat/completions")
         async def chat(req: Request):
@@ -218,21 +239,27 @@ class OpenAIServer:
                 return StreamingResponse(self._stream_chat(cid, created, prompt, sp, body),
                                          media_type="text/event-stream")
             try:
-                outs = await asyncio.gather(*[self._collect(prompt, sp, f"{cid}-{j}")
+                outs = await asyncio.gather(*[self._collect(prompt, sp, f"{cid}-{j}",
+                                                            kvp=body.get("kv_transfer_params"))
                                               for j in range(sp.n)])
             except EngineDeadError as e:
                 return _err(500, "engine failure: " + str(e)[:200], "InternalServerError")
             except ValueError as e:
                 return _err(400, str(e))
+            except RuntimeError as e:
+                return _err(503, str(e), "ServiceUnavailable")
             choices = [{"index": j, "message": {"role": "assistant", "content": o.text},
                         "logprobs": None, "finish_reason": o.finish_reason}
                        for j, o in enumerate(outs)]
             ptok = len(outs[0].prompt_ids)
             ctok = sum(len(o.output_ids) for o in outs)
-            return {"id": cid, "object": "chat.completion", "created": created,
+            resp = {"id": cid, "object": "chat.completion", "created": created,
                     "model": self.name, "choices": choices,
                     "usage": {"prompt_tokens": ptok, "completion_tokens": ctok,
                               "total_tokens": ptok + ctok}}
+            if outs and outs[0].kv_transfer_params:
+                resp["kv_transfer_params"] = outs[0].kv_transfer_params
+            return resp
 
         return app
 
@@ -242,7 +269,8 @@ class OpenAIServer:
         ptext = prompt if isinstance(prompt, str) else None
         n_out, n_prompt = 0, 0
         try:
-            async for o in self.ae.generate(ptext, sp, cid, prompt_ids=pid, stream=True):
+            async for o in self.ae.generate(ptext, sp, cid, prompt_ids=pid, stream=True,
+                                            kv_transfer_params=body.get("kv_transfer_params")):
                 n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
                 chunk = {"id": cid, "object": "text_completion", "created": created,
                          "model": self.name, "choices": [{
@@ -266,7 +294,8 @@ class OpenAIServer:
         yield f"data: {json.dumps(first)}\n\n"
         n_out, n_prompt = 0, 0
         try:
-            async for o in self.ae.generate(prompt, sp, cid, stream=True):
+            async for o in self.ae.generate(prompt, sp, cid, stream=True,
+                                            kv_transfer_params=body.get("kv_transfer_params")):
                 n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
                 chunk = {"id": cid, "object": "chat.completion.chunk", "created": created,
                          "model": self.name, "choices": [{
@@ -324,6 +353,10 @@ def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:
 
     eng = engine or LLMEngine(ecfg)
     ae = AsyncEngine(eng)
+    if ecfg.kv_role in ("prefill", "decode"):
+        from ..parallel.kv_transfer import KVTransferAgent
+
+        ae.kv_agent = KVTransferAgent(eng.runner.kv)
     srv = OpenAIServer(ae, eng.model_name, ecfg.chat_template, ecfg.max_model_len)
     return srv.app, ae
 
@@ -338,6 +371,12 @@ def main(argv: Optional[list] = None) -> None:
 
         serve_tp(ecfg, a.host, a.port)
         return
+    if a.kv_role != "both":
+        # P/D: this process is one rank of the prefill/decode KV-transfer group (torchrun)
+        from ..parallel.state import init_distributed
+
+        backend = os.environ.get("AKAP_DIST_BACKEND") or ("gloo" if a.device == "cpu" else None)
+        init_distributed(tp_size=1, backend=backend)
     app, _ = build_app(ecfg)
     uvicorn.run(app, host=a.host, port=a.port, log_level="info", access_log=False)
 

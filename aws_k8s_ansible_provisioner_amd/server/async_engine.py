@@ -8,7 +8,9 @@ thread parks on an Event, so an idle pod burns no CPU.
 from __future__ import annotations
 
 import asyncio
+import json
 import threading
+import urllib.request
 import time
 import traceback
 from typing import AsyncIterator, Optional
@@ -29,7 +31,8 @@ class AsyncEngine:
         self._wake = threading.Event()
         self._stop = False
         self.dead: Optional[str] = None
-        self.step_hook = step_hook  # e.g. P/D KV hand-off after prefill
+        self.step_hook = step_hook
+        self.kv_agent = None  # parallel.kv_transfer.KVTransferAgent for P/D roles
         self._thread = threading.Thread(target=self._run, name="engine-loop", daemon=True)
         self.started = time.time()
 
@@ -70,14 +73,22 @@ class AsyncEngine:
                 self.loop.call_soon_threadsafe(q.put_nowait, EngineDeadError(self.dead))
 
     async def generate(self, prompt, params: SamplingParams, req_id: str,
-                       prompt_ids: Optional[list] = None, stream: bool = False
+                       prompt_ids: Optional[list] = None, stream: bool = False,
+                       kv_transfer_params: Optional[dict] = None
                        ) -> AsyncIterator[RequestOutput]:
         if self.dead is not None:
             raise EngineDeadError(self.dead)
         q: asyncio.Queue = asyncio.Queue()
         self.queues[req_id] = q
         try:
-            self.engine.add_request(req_id, prompt, params, prompt_ids=prompt_ids, stream=stream)
+            if kv_transfer_params and "transfer_id" in kv_transfer_params:
+                first = await self._pull_remote_kv(req_id, params, stream, kv_transfer_params)
+                if first is not None:  # first token already ended the request
+                    yield first
+                    return
+            else:
+                self.engine.add_request(req_id, prompt, params, prompt_ids=prompt_ids,
+                                        stream=stream, kv_transfer_params=kv_transfer_params)
             self._wake.set()
             while True:
                 o = await q.get()
@@ -90,6 +101,44 @@ class AsyncEngine:
             self.queues.pop(req_id, None)
             if req_id in self.engine.by_name:  # client went away: free its KV blocks
                 self.engine.abort_request(req_id)
+
+    async def _pull_remote_kv(self, req_id: str, params: SamplingParams, stream: bool,
+                              kvp: dict) -> Optional[RequestOutput]:
+        """P/D decode side: reserve blocks, ask the prefill server to push the request's
+        KV to our rank, receive it over RCCL, then let the engine decode."""
+        eng = self.engine
+        prompt_ids = [int(t) for t in kvp["prompt_token_ids"]]
+        first = int(kvp["first_token"])
+        sp = params.normalized()
+        if (not sp.ignore_eos and first == eng.mcfg.eos_id) or sp.max_tokens <= 1:
+            reason = "stop" if first == eng.mcfg.eos_id else "length"
+            text = "" if reason == "stop" else eng.tokenizer.decode([first])
+            return RequestOutput(req_id, prompt_ids, [first], [first], text, text, True,
+                                 reason)
+        if self.kv_agent is None:
+            raise RuntimeError("this server has no KV-transfer agent (start with --kv-role decode)")
+        loop = asyncio.get_running_loop()
+
+        def pull():
+            iid, blocks = eng.reserve_prefilled(req_id, prompt_ids, first, params, stream)
+            if not blocks:
+                raise RuntimeError("KV pool exhausted on the decode engine")
+            body = json.dumps({"transfer_id": kvp["transfer_id"], "dst_rank": eng.rank}).encode()
+            req = urllib.request.Request(kvp["remote_url"].rstrip("/") + "/kv/push", data=body,
+                                         headers={"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=60) as r:
+                meta = json.loads(r.read())
+            if int(meta.get("num_blocks", -1)) != len(blocks):
+                raise RuntimeError(f"KV block count mismatch {meta} vs {len(blocks)}")
+            self.kv_agent.recv_blocks(blocks, int(kvp["remote_rank"]))
+            eng.activate(iid)
+
+        await loop.run_in_executor(None, pull)
+        if stream:  # the first token was produced remotely: deliver it first
+            t = eng.tokenizer.decode_token(first)
+            self.queues[req_id].put_nowait(RequestOutput(req_id, prompt_ids, [first], [first],
+                                                         t, t, False, None))
+        return None
 
     async def abort(self, req_id: str) -> None:
         self.engine.abort_request(req_id)
