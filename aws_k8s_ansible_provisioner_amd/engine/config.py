@@ -27,6 +27,7 @@ class EngineConfig:
     chat_template: Optional[str] = None
     kv_role: str = "both"                     # "both" | "prefill" | "decode" (P/D)
     init_std: float = 0.02                    # random-init weight scale
+    shard_init: str = "per_rank"              # "per_rank" | "full" (identical logical weights for any TP)
 
     def resolved_device(self) -> str:
         if self.device != "auto":

@@ -44,7 +44,8 @@ class ModelRunner:
         self.is_gpu = self.device.type == "cuda"
         t0 = time.time()
         self.model = DecoderLM(mcfg, self.device, seed=ecfg.seed, pstate=self.ps,
-                               max_model_len=ecfg.max_model_len, init_std=ecfg.init_std)
+                               max_model_len=ecfg.max_model_len, init_std=ecfg.init_std,
+                               full_then_shard=ecfg.shard_init == "full")
         if ecfg.load_format == "safetensors" and ecfg.weights_path:
             from .weights import load_safetensors_dir
 
@@ -58,6 +59,13 @@ class ModelRunner:
         self.cap_tokens = max(ecfg.max_num_batched_tokens, self.max_seqs)
         self.cap_tiles = self.cap_tokens * self.G // 64 + self.max_seqs + 1
         self.num_blocks = ecfg.num_gpu_blocks or self._derive_num_blocks()
+        if self.ps.tp_size > 1:  # every TP rank must address the same block pool
+            import torch.distributed as dist
+
+            t = torch.tensor([self.num_blocks], dtype=torch.int64,
+                             device=self.device if self.is_gpu else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.ps.tp_group)
+            self.num_blocks = int(t.item())
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
         self.k_caches, self.v_caches = self.model.cache_views(self.kv, self.bs)
         self.log(f"[runner] KV cache: {self.num_blocks} blocks x {self.bs} tokens "

@@ -100,6 +100,21 @@ class MoEBlock:
         return out
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
+        if self.mode == "ep" and self.ps.tp_size > 1:
+            # activations are replicated across the TP group: each rank routes only its
+            # 1/tp token slice through the EP all-to-all, then the slices are all-gathered
+            T = h.shape[0]
+            tp, r = self.ps.tp_size, self.ps.tp_rank
+            per = (T + tp - 1) // tp
+            pad = per * tp - T
+            hp = torch.cat([h, h.new_zeros(pad, h.shape[1])]) if pad else h
+            mine = self._forward_tokens(hp[r * per:(r + 1) * per].contiguous())
+            parts = [torch.empty_like(mine) for _ in range(tp)]
+            torch.distributed.all_gather(parts, mine, group=self.ps.tp_group)
+            return torch.cat(parts)[:T]
+        return self._forward_tokens(h)
+
+    def _forward_tokens(self, h: torch.Tensor) -> torch.Tensor:
         T, d = h.shape
         logits = F.linear(h, self.router)
         w, ids = ops.moe_topk_softmax(logits, self.K, renormalize=True)
