@@ -1,0 +1,234 @@
+"""Provisioning layer (Ansible, CLI, manifests, OTel, exporter) validated offline:
+ansible/kubectl/kind are not installed here, so the CLI runs against a recording fake
+`ansible-playbook`, playbooks/manifests are checked structurally, and the exporter reads
+a synthetic amdgpu sysfs tree."""
+import glob
+import os
+import stat
+import subprocess
+import urllib.request
+
+import jinja2
+import pytest
+import yaml
+
+from aws_k8s_ansible_provisioner_amd.deploy import installer
+from aws_k8s_ansible_provisioner_amd.exporter import gpu_exporter, rocprof_bridge
+from aws_k8s_ansible_provisioner_amd.utils import chat_template
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PB = os.path.join(ROOT, "provision")
+SCRIPT = os.path.join(ROOT, "deploy-k8s-cluster.sh")
+ORDER = ["inventory-baremetal.yaml", "rocm-node.yaml", "kubernetes-single-node.yaml",
+         "llm-d-deploy.yaml", "llm-d-test.yaml", "otel-observability-setup.yaml"]
+
+
+class _Loader(yaml.SafeLoader):
+    pass
+
+
+def _load(path):
+    with open(path) as f:
+        return yaml.load(f, Loader=_Loader)
+
+
+@pytest.mark.parametrize("pb", ORDER + ["cleanup-instance.yaml"])
+def test_playbooks_parse_and_are_well_formed(pb):
+    plays = _load(os.path.join(PB, pb))
+    assert isinstance(plays, list) and plays
+    for play in plays:
+        assert "hosts" in play and "tasks" in play and play["tasks"], play.get("name")
+        for t in play["tasks"]:
+            assert "name" in t, t
+            mods = [k for k in t if k.startswith(("ansible.", "community.", "amazon."))]
+            assert mods or "block" in t, t["name"]
+            # every retries loop has a real until:
+            if "retries" in t:
+                assert "until" in t, t["name"]
+
+
+def test_playbook_contracts():
+    k8s = open(os.path.join(PB, "kubernetes-single-node.yaml")).read()
+    assert "amd.com/gpu" in k8s and "gpu-metrics" in k8s and "kube-prometheus-stack" in k8s
+    assert "helm install --generate-name" not in k8s and "upgrade --install" in k8s  # 2H #3
+    assert "lineinfile" in k8s
+    assert "unix:///var/run/crio/crio.sock" in k8s and "local-path" in k8s
+    rocm = open(os.path.join(PB, "rocm-node.yaml")).read()
+    assert "amdgpu-install" in rocm and "rocminfo" in rocm and "{{ gpu_arch }}" in rocm
+    test = _load(os.path.join(PB, "llm-d-test.yaml"))[0]
+    text = yaml.safe_dump(test)
+    assert "/v1/models" in text and "/v1/completions" in text and "Who are you?" in text
+    assert "llm-d-inference-gateway" in text
+    inv = open(os.path.join(PB, "inventory-baremetal.yaml")).read()
+    assert "instance_id={{ instance_id }}" in inv
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "config", "cluster.yaml")))
+    assert cfg["model"] == "Qwen/Qwen3-0.6B" and cfg["llm_d_namespace"] == "llm-d"
+
+
+def _fake_ansible(tmp_path, make_inventory=True):
+    log = tmp_path / "calls.log"
+    fake = tmp_path / "ansible-playbook"
+    fake.write_text(f"""#!/usr/bin/env bash
+echo "$@" >> {log}
+pb="${{@: -1}}"
+if [[ "$pb" == *inventory-baremetal.yaml && "{int(make_inventory)}" == "1" ]]; then
+  printf '[gpu_instances]\\nnode ansible_host=10.0.0.9 ansible_user=ubuntu instance_id=mi355x-abc\\n' > gpu-inventory-mi355x-abc.ini
+  printf 'Instance ID: mi355x-abc\\nInstance Name: node\\nInstance Type: baremetal-8xMI355X\\nPublic IP: 10.0.0.9\\nPrivate IP: 10.0.0.9\\nGPUs: 8 (gfx950)\\nssh -i k ubuntu@10.0.0.9\\n' > instance-mi355x-abc-details.txt
+fi
+if [[ "$pb" == *cleanup-instance.yaml ]]; then rm -f gpu-inventory-*.ini instance-*-details.txt; fi
+exit 0
+""")
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    return str(fake), log
+
+
+def _run(tmp_path, *args, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run(["bash", SCRIPT, *args], cwd=tmp_path, env=e, capture_output=True,
+                          text=True, timeout=60)
+
+
+def test_cli_deploy_runs_playbooks_in_order(tmp_path):
+    fake, log = _fake_ansible(tmp_path)
+    r = _run(tmp_path, "deploy", env={"ANSIBLE_PLAYBOOK": fake, "AKAP_NODE_HOST": "10.0.0.9"})
+    assert r.returncode == 0, r.stderr
+    calls = log.read_text().splitlines()
+    assert [c.split()[-1].rsplit("/", 1)[-1] for c in calls] == ORDER
+    assert all("@" + os.path.join(ROOT, "config", "cluster.yaml") in c for c in calls)
+    assert "node_host=10.0.0.9" in calls[0]
+    assert all("-i gpu-inventory-mi355x-abc.ini" in c for c in calls[1:])
+    assert "Instance ID: mi355x-abc" in r.stdout and "ssh -i k ubuntu@10.0.0.9" in r.stdout
+
+
+def test_cli_no_argument_deploys_and_errors(tmp_path):
+    fake, log = _fake_ansible(tmp_path)
+    assert _run(tmp_path, env={"ANSIBLE_PLAYBOOK": fake}).returncode == 0
+    r = _run(tmp_path, "deploy", "extra", env={"ANSIBLE_PLAYBOOK": fake})
+    assert r.returncode == 1 and "doesn't accept additional arguments" in r.stderr
+    r = _run(tmp_path, "bogus", env={"ANSIBLE_PLAYBOOK": fake})
+    assert r.returncode == 1 and "Unknown command" in r.stderr
+    assert _run(tmp_path, "help").returncode == 0
+
+
+def test_cli_deploy_fails_without_inventory(tmp_path):
+    fake, _ = _fake_ansible(tmp_path, make_inventory=False)
+    r = _run(tmp_path, "deploy", env={"ANSIBLE_PLAYBOOK": fake})
+    assert r.returncode == 1 and "no gpu-inventory" in r.stderr
+
+
+def test_cli_cleanup(tmp_path):
+    fake, log = _fake_ansible(tmp_path)
+    r = _run(tmp_path, "cleanup", env={"ANSIBLE_PLAYBOOK": fake})
+    assert r.returncode == 0 and "Nothing to cleanup" in r.stdout
+    (tmp_path / "gpu-inventory-x.ini").write_text("[gpu_instances]\n")
+    r = _run(tmp_path, "cleanup", env={"ANSIBLE_PLAYBOOK": fake, "AKAP_YES": "1"})
+    assert r.returncode == 0 and "cleanup-instance.yaml" in log.read_text()
+    assert not list(tmp_path.glob("gpu-inventory-*.ini"))
+
+
+@pytest.mark.parametrize("preset", ["slim", "pd", "tp8", "moe", "kind"])
+def test_manifests_render(preset):
+    v = installer.load_values(os.path.join(ROOT, "deploy", "values", f"{preset}.yaml"))
+    out = installer.render(v, "llm-d", "local-path", "50Gi", "Qwen/Qwen3-0.6B", hf_token="t0k")
+    docs = [d for text in out.values() for d in yaml.safe_load_all(text) if d]
+    kinds = {(d["kind"], d["metadata"]["name"]) for d in docs}
+    assert ("Service", "llm-d-inference-gateway") in kinds
+    assert ("PersistentVolumeClaim", "model-pvc") in kinds
+    for n in ("phi", "opt", "default"):
+        assert ("ConfigMap", f"{n}-chat-template") in kinds
+    gw_svc = [d for d in docs if d["kind"] == "Service" and d["metadata"]["name"] ==
+              "llm-d-inference-gateway"][0]
+    assert gw_svc["metadata"]["labels"]["app.kubernetes.io/name"] == "llm-d-inference-gateway"
+    assert gw_svc["spec"]["ports"][0]["port"] == 80
+    engines = [d for d in docs if d["kind"] == "Deployment" and "gateway" not in d["metadata"]["name"]]
+    assert engines
+    for d in engines:
+        pod = d["spec"]["template"]
+        assert pod["metadata"]["annotations"]["prometheus.io/scrape"] == "true"
+        c = pod["spec"]["containers"][0]
+        assert {"containerPort": 8000, "name": "http"} in c["ports"]
+        gpus = v["engines"][0]["gpusPerPod"]
+        if gpus:
+            assert c["resources"]["limits"]["amd.com/gpu"] == str(gpus)
+        else:
+            assert "limits" not in c["resources"]
+    if preset == "tp8":
+        assert "--nproc-per-node=8" in engines[0]["spec"]["template"]["spec"]["containers"][0]["command"]
+    if preset == "pd":
+        gw = [d for d in docs if d["kind"] == "Deployment" and d["metadata"]["name"] ==
+              "llm-d-inference-gateway"][0]
+        args = " ".join(gw["spec"]["template"]["spec"]["containers"][0]["args"])
+        assert "@prefill" in args and "@decode" in args
+    cms = {d["metadata"]["name"]: d for d in docs if d["kind"] == "ConfigMap"}
+    assert cms["phi-chat-template"]["data"]["template.jinja"] == chat_template.BUILTIN["phi"]
+    if v.get("gpuExporter", True):
+        ds = [d for d in docs if d["kind"] == "DaemonSet"][0]
+        ports = ds["spec"]["template"]["spec"]["containers"][0]["ports"]
+        assert ports[0]["name"] == "gpu-metrics"
+
+
+def test_otel_templates_render():
+    ctx = yaml.safe_load(open(os.path.join(ROOT, "config", "cluster.yaml")))
+    ctx["cluster_name"] = "node-k8s"
+    env = jinja2.Environment(undefined=jinja2.StrictUndefined)
+    for name in ("collector", "otel-prometheus"):
+        text = env.from_string(open(os.path.join(ROOT, "deploy", "otel",
+                                                 f"{name}.yaml.j2")).read()).render(**ctx)
+        docs = [d for d in yaml.safe_load_all(text) if d]
+        if name == "collector":
+            col = [d for d in docs if d["kind"] == "OpenTelemetryCollector"][0]
+            jobs = {j["job_name"]: j for j in
+                    col["spec"]["config"]["receivers"]["prometheus"]["config"]["scrape_configs"]}
+            assert {"akap-engines", "amd-gpu-exporter", "kubernetes-nodes",
+                    "kubernetes-cadvisor"} <= set(jobs)
+            assert jobs["kubernetes-nodes"]["scheme"] == "https"
+            pipes = col["spec"]["config"]["service"]["pipelines"]
+            assert pipes["metrics"]["exporters"] == ["prometheusremotewrite"]
+        else:
+            cm = docs[0]["data"]["prometheus.yml"]
+            assert "remote_write" not in cm  # no self-loop
+
+
+def _fake_sysfs(root, n=2):
+    for i in range(n):
+        dev = root / "class" / "drm" / f"card{i}" / "device"
+        hw = dev / "hwmon" / "hwmon0"
+        hw.mkdir(parents=True)
+        (dev / "vendor").write_text("0x1002\n")
+        (dev / "gpu_busy_percent").write_text(f"{40 + i}\n")
+        (dev / "mem_busy_percent").write_text("12\n")
+        (dev / "mem_info_vram_used").write_text(str(100 * 2**30))
+        (dev / "mem_info_vram_total").write_text(str(288 * 2**30))
+        (hw / "temp1_input").write_text("55000")
+        (hw / "temp1_label").write_text("edge")
+        (hw / "temp2_input").write_text("71000")
+        (hw / "temp2_label").write_text("junction")
+        (hw / "power1_average").write_text("850000000")
+    (root / "class" / "drm" / "card0-DP-1").mkdir(parents=True)
+
+
+def test_gpu_exporter_sysfs_and_dcgm_aliases(tmp_path):
+    _fake_sysfs(tmp_path)
+    exp = gpu_exporter.Exporter(str(tmp_path), node="n1")
+    txt = exp.text()
+    assert 'DCGM_FI_DEV_GPU_UTIL{gpu="1"' in txt and "} 41.0" in txt
+    assert 'DCGM_FI_DEV_GPU_TEMP{gpu="0"' in txt and "71.0" in txt  # junction preferred
+    assert 'DCGM_FI_DEV_POWER_USAGE{gpu="0"' in txt and "850.0" in txt
+    assert "amd_gpu_vram_total_bytes" in txt and 'amd_gpu_exporter_gpus{Hostname="n1"} 2' in txt
+    srv = gpu_exporter.serve(exp, "127.0.0.1", 0)
+    port = srv.server_address[1]
+    body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics").read().decode()
+    assert "DCGM_FI_DEV_FB_USED" in body
+    srv.shutdown()
+
+
+def test_rocprof_bridge(tmp_path):
+    d = tmp_path / "prof" / "run"
+    d.mkdir(parents=True)
+    (d / "r_kernel_stats.csv").write_text(
+        '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+        '"akap::paged_attn_decode_kernel(akap::AttnParams)",10,2000000,200000,50,1,1,0\n')
+    txt = rocprof_bridge.render(rocprof_bridge.collect(str(tmp_path)))
+    assert 'akap_kernel_time_seconds_total{kernel="akap::paged_attn_decode_kernel' in txt
+    assert "akap_kernel_calls_total" in txt and " 10" in txt
