@@ -50,10 +50,16 @@ struct AttnParams {
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s);
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s);
 
+// ---- gemm.hip ----
+int gemm_splitk_choice(int M, int N, int K);
+void launch_gemm_bf16(const void* X, const void* W, void* Y, float* ws, int M, int N, int K,
+                      int ldx, int ldw, int ldy, int splitk, hipStream_t st);
+
 // ---- sampling.hip ----
 struct SampleParams {
-  const float* logits;  // [B, V] (row stride ld)
+  const void* logits;  // [B, V] (row stride ld), fp32 or bf16
   int ld, V;
+  int is_bf16;
   const float* temperature;  // [B] (<=0 => greedy)
   const int* top_k;          // [B] (<=0 => off)
   const float* top_p;        // [B] (>=1 => off)

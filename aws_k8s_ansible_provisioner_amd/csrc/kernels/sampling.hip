@@ -59,7 +59,23 @@ __device__ __forceinline__ float ldf(const T* p, int i) { return (float)p[i]; }
 template <typename T>
 __device__ ArgBest row_argmax(const T* x, int V, float* sv, int* si) {
   ArgBest b{-INFINITY, 0x7fffffff};
-  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+  int tail = 0;
+  if constexpr (sizeof(T) == 2) {
+    // 16-byte vector loads: 8 contiguous bf16 per lane per step
+    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+      const int nvec = V / 8;
+      for (int v = threadIdx.x; v < nvec; v += blockDim.x) {
+        const bf16x8 q = *reinterpret_cast<const bf16x8*>(x + (size_t)v * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)q[j];
+          if (f > b.v) { b.v = f; b.i = v * 8 + j; }
+        }
+      }
+      tail = nvec * 8;
+    }
+  }
+  for (int i = tail + threadIdx.x; i < V; i += blockDim.x) {
     const float v = ldf(x, i);
     if (v > b.v) { b.v = v; b.i = i; }  // strided ascending i: first max kept
   }
@@ -69,8 +85,8 @@ __device__ ArgBest row_argmax(const T* x, int V, float* sv, int* si) {
 // Radix select over keys of x (restricted to key >= floor_key).
 //  MASS=false: returns the key of the k-th largest element (k = target, integer).
 //  MASS=true : returns the largest key tau with sum_{key>=tau} exp((x-M)*invT) >= target.
-template <bool MASS>
-__device__ uint32_t radix_select(const float* x, int V, uint32_t floor_key, float target,
+template <bool MASS, typename T>
+__device__ uint32_t radix_select(const T* x, int V, uint32_t floor_key, float target,
                                  float M, float invT, int* cnt, float* mass, uint32_t* shared_u,
                                  float* shared_f) {
   uint32_t prefix = 0, mask = 0;
@@ -79,7 +95,7 @@ __device__ uint32_t radix_select(const float* x, int V, uint32_t floor_key, floa
     for (int b = threadIdx.x; b < 256; b += blockDim.x) { cnt[b] = 0; mass[b] = 0.f; }
     __syncthreads();
     for (int i = threadIdx.x; i < V; i += blockDim.x) {
-      const float v = x[i];
+      const float v = (float)x[i];
       const uint32_t k = fkey(v);
       if (k < floor_key || (k & mask) != prefix) continue;
       const int d = (k >> shift) & 255;
@@ -110,6 +126,7 @@ __device__ uint32_t radix_select(const float* x, int V, uint32_t floor_key, floa
   return prefix;
 }
 
+template <typename T>
 __global__ __launch_bounds__(kSampThreads) void sample_kernel(SampleParams p) {
   __shared__ float sv[16];
   __shared__ int si[16];
@@ -118,10 +135,10 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(SampleParams p) {
   __shared__ uint32_t su[1];
   __shared__ float sf[1];
   const int row = blockIdx.x;
-  const float* x = p.logits + (size_t)row * p.ld;
+  const T* x = reinterpret_cast<const T*>(p.logits) + (size_t)row * p.ld;
   const int V = p.V;
-  const float T = p.temperature ? p.temperature[row] : 0.f;
-  if (!(T > 0.f)) {
+  const float temp = p.temperature ? p.temperature[row] : 0.f;
+  if (!(temp > 0.f)) {
     ArgBest b = row_argmax(x, V, sv, si);
     if (threadIdx.x == 0) {
       p.out_tokens[row] = b.i;
@@ -129,13 +146,13 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(SampleParams p) {
     }
     return;
   }
-  const float invT = 1.f / T;
+  const float invT = 1.f / temp;
   // pass 1: max and partition function
   float m = -INFINITY;
-  for (int i = threadIdx.x; i < V; i += blockDim.x) m = fmaxf(m, x[i]);
+  for (int i = threadIdx.x; i < V; i += blockDim.x) m = fmaxf(m, (float)x[i]);
   const float M = block_max(m, sv);
   float z = 0.f;
-  for (int i = threadIdx.x; i < V; i += blockDim.x) z += __expf((x[i] - M) * invT);
+  for (int i = threadIdx.x; i < V; i += blockDim.x) z += __expf(((float)x[i] - M) * invT);
   const float Z = block_sum(z, sv);
 
   uint32_t thr = 0;
@@ -147,7 +164,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(SampleParams p) {
     if (tp < 1.f) {
       float zk = 0.f;
       for (int i = threadIdx.x; i < V; i += blockDim.x)
-        if (fkey(x[i]) >= thr) zk += __expf((x[i] - M) * invT);
+        if (fkey((float)x[i]) >= thr) zk += __expf(((float)x[i] - M) * invT);
       Zk = block_sum(zk, sv);
     }
   }
@@ -160,7 +177,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(SampleParams p) {
   const uint32_t step = p.steps ? (uint32_t)p.steps[row] : 0u;
   ArgBest b{-INFINITY, 0x7fffffff};
   for (int i = threadIdx.x; i < V; i += blockDim.x) {
-    const float v = x[i];
+    const float v = (float)x[i];
     if (fkey(v) < thr) continue;
     const float u = uniform01(seed, step, (uint32_t)i);
     const float gval = v * invT - __logf(-__logf(u));
@@ -171,13 +188,16 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(SampleParams p) {
     int tok = b.i;
     if (tok < 0 || tok >= V) tok = 0;
     p.out_tokens[row] = tok;
-    if (p.out_logprobs) p.out_logprobs[row] = (x[tok] - M) * invT - __logf(Z);
+    if (p.out_logprobs) p.out_logprobs[row] = ((float)x[tok] - M) * invT - __logf(Z);
   }
 }
 
 void launch_sample(const SampleParams& p, int B, hipStream_t s) {
   if (B == 0) return;
-  sample_kernel<<<B, kSampThreads, 0, s>>>(p);
+  if (p.is_bf16)
+    sample_kernel<bf16><<<B, kSampThreads, 0, s>>>(p);
+  else
+    sample_kernel<float><<<B, kSampThreads, 0, s>>>(p);
 }
 
 // Greedy fast path straight on bf16 or fp32 logits.

@@ -163,10 +163,33 @@ void paged_attention_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache
   akap::launch_paged_attn_decode(p, B, cur_stream());
 }
 
+int64_t gemm_splitk(int64_t M, int64_t N, int64_t K) {
+  return akap::gemm_splitk_choice(M, N, K);
+}
+
+void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D tensors");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm: shape mismatch");
+  TORCH_CHECK(K % 8 == 0 && N % 4 == 0, "gemm: K % 8, N % 4");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm: 16-byte aligned rows");
+  if (splitk > 1) {
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= splitk * M * N,
+                "gemm: fp32 workspace of splitk*M*N");
+  }
+  const c10::DeviceGuard g(x.device());
+  akap::launch_gemm_bf16(x.data_ptr(), w.data_ptr(), out.data_ptr(),
+                         splitk > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, x.stride(0),
+                         w.stride(0), out.stride(0), splitk, cur_stream());
+}
+
 void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
             Tensor steps, Tensor out_tokens, Tensor out_logprobs) {
   CHECK_GPU(logits);
-  TORCH_CHECK(logits.scalar_type() == at::kFloat, "sampler expects fp32 logits");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16,
+              "sampler expects fp32 or bf16 logits");
   CHECK_LAST_CONTIG(logits);
   TORCH_CHECK(temperature.scalar_type() == at::kFloat && top_p.scalar_type() == at::kFloat,
               "temperature/top_p fp32");
@@ -174,7 +197,8 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tenso
   TORCH_CHECK(seeds.scalar_type() == at::kLong && out_tokens.scalar_type() == at::kLong, "int64");
   const int B = logits.size(0);
   akap::SampleParams p{};
-  p.logits = logits.data_ptr<float>();
+  p.logits = logits.data_ptr();
+  p.is_bf16 = logits.scalar_type() == at::kBFloat16;
   p.ld = logits.stride(0);
   p.V = logits.size(1);
   p.temperature = temperature.data_ptr<float>();
@@ -276,6 +300,8 @@ TORCH_LIBRARY(akap, m) {
       "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
       "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs) -> ()");
   m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
+  m.def("gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int splitk) -> ()");
+  m.def("gemm_splitk(int M, int N, int K) -> int");
   m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def(
       "moe_align(Tensor topk_ids, int E, int block, Tensor(a!) sorted_ids, Tensor(b!) offsets, "
@@ -283,6 +309,10 @@ TORCH_LIBRARY(akap, m) {
   m.def("kv_gather(Tensor cache, Tensor block_ids, Tensor(a!) out) -> ()");
   m.def("kv_scatter(Tensor buf, Tensor(a!) cache, Tensor block_ids) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start, int vocab_end) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
+  m.impl("gemm_splitk", &gemm_splitk);
 }
 
 TORCH_LIBRARY_IMPL(akap, CUDA, m) {
@@ -295,6 +325,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("paged_attention_decode", &paged_attention_decode);
   m.impl("sample", &sample);
   m.impl("argmax", &argmax);
+  m.impl("gemm", &gemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
   m.impl("kv_gather", &kv_gather);

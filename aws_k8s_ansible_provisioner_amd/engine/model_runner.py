@@ -179,7 +179,8 @@ class ModelRunner:
                           self.d["seq_lens"][:n], self.d["q_start"][:n + 1], None, None,
                           parts, ps, self.workspace)
         h = self.model.forward(self.d["input_ids"][:n], batch, self.k_caches, self.v_caches)
-        logits = self.model.compute_logits(h).float()
+        # sampler reads bf16 logits directly (no [n, V] fp32 cast pass)
+        logits = self.model.compute_logits(h)
         self._sample(logits, n)
 
     def _pad_host(self, B: int, n: int) -> None:

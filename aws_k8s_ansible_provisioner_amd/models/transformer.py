@@ -258,25 +258,25 @@ class DecoderLM:
         for li, lw in enumerate(self.layers):
             if li > 0:
                 h, residual = ops.fused_add_rms_norm(x, residual, lw.ln1, eps)
-            qkv = F.linear(h, lw.w_qkv)
+            qkv = ops.linear(h, lw.w_qkv)
             q = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
             ops.qk_norm_rope_cache(qkv, q, k_caches[li], v_caches[li], batch.positions,
                                    batch.slots, self.cos_sin, lw.q_norm, lw.k_norm, self.hq,
                                    self.hkv, eps, True)
             attn = torch.empty_like(q)
             self._attention(q, batch, k_caches[li], v_caches[li], attn)
-            o = comm.tp_all_reduce(F.linear(attn.view(T, self.hq * self.D), lw.w_o))
+            o = comm.tp_all_reduce(ops.linear(attn.view(T, self.hq * self.D), lw.w_o))
             h, residual = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             if lw.moe is not None:
                 x = lw.moe.forward(h)
             else:
-                gu = F.linear(h, lw.w_gate_up)
-                x = comm.tp_all_reduce(F.linear(ops.silu_and_mul(gu), lw.w_down))
+                gu = ops.linear(h, lw.w_gate_up)
+                x = comm.tp_all_reduce(ops.linear(ops.silu_and_mul(gu), lw.w_down))
         h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
         return h
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(h, self.lm_head)
+        logits = ops.linear(h, self.lm_head)
         if self.ps.tp_size > 1:
             logits = comm.tp_all_gather_last(logits)
         return logits[:, : self.cfg.vocab_size]

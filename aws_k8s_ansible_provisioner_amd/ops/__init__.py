@@ -149,6 +149,52 @@ def decode_workspace(max_seqs: int, num_kv_heads: int, gqa_group: int, num_parts
     return pm, pl, po
 
 
+# ----------------------------------------------------------------------------- GEMM
+_GEMM_MODE = os.environ.get("AKAP_GEMM", "torch")  # torch (hipBLASLt) | auto | hip
+GEMM_MAX_M = int(os.environ.get("AKAP_GEMM_MAX_M", "512"))
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T.  Decode-sized M on the GPU -> the hand-written MFMA GEMM (small tiles +
+    split-K to fill 256 CUs); large M (prefill) -> hipBLASLt via torch."""
+    M = x.shape[0]
+    use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
+               and (M <= GEMM_MAX_M or _GEMM_MODE == "hip") and x.shape[1] % 8 == 0
+               and w.shape[0] % 4 == 0)
+    if not use_hip:
+        y = torch.nn.functional.linear(x, w)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    load_native(required=True)
+    N, K = w.shape
+    if out is None:
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    s = gemm_splitk(M, N, K)
+    if s > 1:
+        ws = torch.empty(s * M * N, dtype=torch.float32, device=x.device)
+    else:
+        ws = _EMPTY_F32.get(x.device)
+        if ws is None:
+            ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
+    torch.ops.akap.gemm(out, x, w, ws, s)
+    return out
+
+
+_EMPTY_F32: dict = {}
+
+
+def gemm_splitk(M: int, N: int, K: int) -> int:
+    """Split-K factor for the decode GEMM: enough 64x64 tiles x splits to cover 256 CUs,
+    each split keeping >= 256 of K (mirrors gemm_splitk_choice in gemm.hip)."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    s = 1
+    while tiles * s < 256 and K // (s * 2) >= 256:
+        s *= 2
+    return s
+
+
 # ----------------------------------------------------------------------------- sampling
 def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out_logprobs=None):
     B = logits.shape[0]

@@ -260,3 +260,28 @@ def test_kv_gather_scatter_roundtrip():
     ids2 = torch.tensor([1, 2, 5, 19], dtype=torch.int32, device=DEV)
     ops.kv_scatter(buf, dst, ids2)
     assert torch.equal(dst.view(planes, NB, -1)[:, ids2.long()], buf.view(planes, 4, -1))
+
+
+@pytest.mark.parametrize("M", [1, 7, 64, 100, 256, 512])
+@pytest.mark.parametrize("N,K", [(4096, 1024), (1024, 2048), (6144, 1024), (1024, 3072),
+                                 (1000, 520), (64, 64)])
+def test_decode_gemm(M, N, K):
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    s = ops.gemm_splitk(M, N, K)
+    ws = torch.empty(max(1, s * M * N), device=DEV, dtype=torch.float32)
+    torch.ops.akap.gemm(y, x, w, ws, s)
+    ref_ = (x.float() @ w.float().t())
+    err = (y.float() - ref_).abs().max().item()
+    assert err <= 2e-2 * ref_.abs().max().item() + 1e-2, err
+
+
+def test_decode_gemm_strided_input():
+    x = torch.randn(64, 2048, device=DEV, dtype=torch.bfloat16)[:, :1024]
+    w = torch.randn(512, 1024, device=DEV, dtype=torch.bfloat16) * 0.05
+    ref_ = x.float() @ w.float().t()
+    y = torch.empty(64, 512, device=DEV, dtype=torch.bfloat16)
+    torch.ops.akap.gemm(y, x, w, torch.empty(1, device=DEV), 1)
+    assert (y.float() - ref_).abs().max().item() < 3e-2 * ref_.abs().max().item()
