@@ -10,7 +10,8 @@
 //    score registers are directly the B operand of the next MFMA.
 //  * Rows of the two 16-token S tiles map to tokens 8*(r>>2) + 4*tile + (r&3), which
 //    makes lane group g hold tokens 8g..8g+7 contiguous -> O^T = V^T . P^T takes V^T
-//    straight from the dim-major V cache ([blk, Hkv, D, BS]) with 16-byte loads:
+//    straight from the V cache ([blk, Hkv, BS/8, D, 8]: 8-token groups, dim-major) with
+//    one 16-byte load per (dim, 8 tokens), 256 contiguous bytes per 16 lanes:
 //    no LDS transpose, no ds_bpermute.  O^T keeps the query row on the lane, so the
 //    softmax rescale is lane-local.
 //  * K operand: K cache [blk, Hkv, BS, D]; each lane loads 16 B per MFMA k-chunk.
@@ -67,9 +68,9 @@ __device__ __forceinline__ void load_chunk(ChunkRegs& c, const bf16* __restrict_
   vt = min(vt, (kv_len - 1) & ~7);
   const int vblk = bt[vt / BS];
   const int voff = vt % BS;
-  const bf16* vp = v_cache + ((size_t)vblk * Hkv + kvh) * kD * BS + voff + (size_t)r * BS;
+  const bf16* vp = v_cache + ((size_t)vblk * Hkv + kvh) * kD * BS + (voff >> 3) * kD * 8 + r * 8;
 #pragma unroll
-  for (int n = 0; n < kND; ++n) c.vb[n] = *reinterpret_cast<const bf16x8*>(vp + (size_t)16 * n * BS);
+  for (int n = 0; n < kND; ++n) c.vb[n] = *reinterpret_cast<const bf16x8*>(vp + 16 * n * 8);
 }
 
 // Scores, online softmax and P.V for one staged chunk.

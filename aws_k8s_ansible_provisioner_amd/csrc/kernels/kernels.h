@@ -29,7 +29,7 @@ void launch_silu_and_mul(void* out, const void* in, long T, int F, int in_stride
 struct AttnParams {
   const __bf16* q;        // [T, Hq, D]
   const __bf16* k_cache;  // [NB, Hkv, BS, D]
-  const __bf16* v_cache;  // [NB, Hkv, D, BS]
+  const __bf16* v_cache;  // [NB, Hkv, BS/8, D, 8]
   __bf16* out;            // [T, Hq, D]
   const int* block_tables;  // [B, bt_stride]
   int bt_stride;

@@ -59,7 +59,9 @@ void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache
   const int D = k_cache.size(3);
   const int BS = k_cache.size(2);
   TORCH_CHECK(D == 128 || D == 64, "head_dim must be 64 or 128");
-  TORCH_CHECK(v_cache.size(2) == D && v_cache.size(3) == BS, "v_cache must be [NB,Hkv,D,BS]");
+  TORCH_CHECK(v_cache.dim() == 5 && v_cache.size(2) * 8 == BS && v_cache.size(3) == D &&
+                  v_cache.size(4) == 8,
+              "v_cache must be [NB,Hkv,BS/8,D,8]");
   TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D, "qkv too narrow");
   TORCH_CHECK(positions.numel() >= T && slots.numel() >= T, "positions/slots too short");
   const c10::DeviceGuard g(qkv.device());
@@ -119,6 +121,7 @@ akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_
   p.G = G;
   p.BS = k_cache.size(2);
   TORCH_CHECK(q.size(2) == 128 && k_cache.size(3) == 128, "attention kernels need head_dim 128");
+  TORCH_CHECK(v_cache.dim() == 5 && v_cache.size(4) == 8, "v_cache must be [NB,Hkv,BS/8,D,8]");
   TORCH_CHECK(p.Hq == p.Hkv * G, "Hq must equal Hkv * G");
   TORCH_CHECK(p.BS % 8 == 0 && (p.BS % 32 == 0 || 32 % p.BS == 0), "block size must be 8/16/32/64..");
   p.scale_log2 = (float)(scale * 1.4426950408889634);

@@ -218,7 +218,7 @@ class DecoderLM:
 
     # ------------------------------------------------------------------ kv cache
     def allocate_kv_cache(self, num_blocks: int, block_size: int) -> torch.Tensor:
-        """One allocation [L, 2, NB, Hkv*BS*D] (K block = [Hkv,BS,D], V block = [Hkv,D,BS]),
+        """One allocation [L, 2, NB, Hkv*BS*D] (K block = [Hkv,BS,D], V block = [Hkv,BS/8,D,8]),
         zero-filled so never-written slots read as finite zeros."""
         per_block = self.hkv * block_size * self.D
         return torch.zeros(self.cfg.num_layers, 2, num_blocks, per_block, dtype=self.dtype,
@@ -227,7 +227,7 @@ class DecoderLM:
     def cache_views(self, kv: torch.Tensor, block_size: int):
         NB = kv.shape[2]
         ks = [kv[l, 0].view(NB, self.hkv, block_size, self.D) for l in range(kv.shape[0])]
-        vs = [kv[l, 1].view(NB, self.hkv, self.D, block_size) for l in range(kv.shape[0])]
+        vs = [kv[l, 1].view(NB, self.hkv, block_size // 8, self.D, 8) for l in range(kv.shape[0])]
         return ks, vs
 
     # ------------------------------------------------------------------ forward

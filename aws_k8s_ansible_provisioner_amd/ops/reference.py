@@ -1,7 +1,7 @@
 """Plain-PyTorch (fp32-accumulating) reference implementations of every kernel.
 
 They define the semantics the HIP kernels are tested against and serve the CPU
-engine path.  Cache layouts: K [NB, Hkv, BS, D], V [NB, Hkv, D, BS].
+engine path.  Cache layouts: K [NB, Hkv, BS, D], V [NB, Hkv, BS/8, D, 8].
 """
 from __future__ import annotations
 
@@ -63,7 +63,7 @@ def write_cache(k: torch.Tensor, v: torch.Tensor, k_cache, v_cache, slots) -> No
             continue
         b, o = divmod(s, BS)
         k_cache[b, :, o, :] = k[t].to(k_cache.dtype)
-        v_cache[b, :, :, o] = v[t].to(v_cache.dtype)
+        v_cache[b, :, o // 8, :, o % 8] = v[t].to(v_cache.dtype)
 
 
 def qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w, Hq,
@@ -95,7 +95,8 @@ def gather_kv(k_cache, v_cache, block_table, kv_len: int):
     nb = (kv_len + BS - 1) // BS
     blocks = block_table[:nb].long()
     K = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * BS, k_cache.shape[1], -1)[:kv_len]
-    V = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * BS, v_cache.shape[1], -1)[:kv_len]
+    # [nb, Hkv, BS/8, D, 8] -> [nb, BS/8, 8, Hkv, D] -> tokens
+    V = v_cache[blocks].permute(0, 2, 4, 1, 3).reshape(nb * BS, v_cache.shape[1], -1)[:kv_len]
     return K, V
 
 

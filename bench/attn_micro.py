@@ -36,7 +36,7 @@ def main():
         bt[s, :n] = perm[i:i + n].to(torch.int32)
         i += n
     kc = torch.randn(NB, a.hkv, bs, D, dtype=torch.bfloat16, device=dev)
-    vc = torch.randn(NB, a.hkv, D, bs, dtype=torch.bfloat16, device=dev)
+    vc = torch.randn(NB, a.hkv, bs // 8, D, 8, dtype=torch.bfloat16, device=dev)
     q = torch.randn(B, a.hq, D, dtype=torch.bfloat16, device=dev)
     out = torch.empty_like(q)
     bt, lens_d = bt.to(dev), lens.to(dev)

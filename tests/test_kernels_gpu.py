@@ -57,7 +57,7 @@ def test_silu_and_mul(T, F):
 def _rand_cache(nb, hkv, bs, d=128, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     k = torch.randn(nb, hkv, bs, d, generator=g).bfloat16()
-    v = torch.randn(nb, hkv, d, bs, generator=g).bfloat16()
+    v = torch.randn(nb, hkv, bs // 8, d, 8, generator=g).bfloat16()
     return k, v
 
 
@@ -73,7 +73,7 @@ def test_qk_norm_rope_cache(qk_norm, hq, hkv):
     cs = ref.rope_cos_sin(4096, D, 1e6)
     qw = torch.randn(D).bfloat16() if qk_norm else None
     kw = torch.randn(D).bfloat16() if qk_norm else None
-    kc, vc = torch.zeros(NB, hkv, BS, D).bfloat16(), torch.zeros(NB, hkv, D, BS).bfloat16()
+    kc, vc = torch.zeros(NB, hkv, BS, D).bfloat16(), torch.zeros(NB, hkv, BS // 8, D, 8).bfloat16()
     q_ref = torch.empty(T, hq, D).bfloat16()
     ref.qk_norm_rope_cache(qkv, q_ref, kc, vc, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
     kg, vg = kc.zero_().to(DEV), vc.zero_().to(DEV)
