@@ -201,8 +201,8 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
 // Decode: one new token per sequence, rows = the G q-heads of one kv head.
 // grid = (num_seqs, Hkv, num_parts); 4 waves split the partition's chunks.
 // ----------------------------------------------------------------------------------
-template <bool PREFETCH>
-__global__ __launch_bounds__(256) void paged_attn_decode_kernel(AttnParams p) {
+template <bool PREFETCH, int MINW>
+__global__ __launch_bounds__(256, MINW) void paged_attn_decode_kernel(AttnParams p) {
   const int seq = blockIdx.x;
   const int kvh = blockIdx.y;
   const int part = blockIdx.z;
@@ -218,10 +218,13 @@ __global__ __launch_bounds__(256) void paged_attn_decode_kernel(AttnParams p) {
   const int q_tok = p.q_start ? p.q_start[seq] : seq;
   const bf16* qptr = p.q + ((size_t)q_tok * p.Hq + kvh * G + qr) * kD;
 
-  __shared__ float o_s[4][16][kD + 4];
-  __shared__ float m_s[4][16];
-  __shared__ float l_s[4][16];
-
+  // combine buffer sized by G (dynamic LDS: 4 x G x (D+4) floats + stats), so small G
+  // keeps LDS from limiting occupancy (G=2: ~4 KiB instead of 34 KiB)
+  extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
+  float* o_s = dyn_lds;                       // [4][G][kD + 4]
+  float* m_s = dyn_lds + 4 * G * (kD + 4);    // [4][G]
+  float* l_s = m_s + 4 * G;                   // [4][G]
+#define OS(w_, r_, d_) o_s[((w_) * G + (r_)) * (kD + 4) + (d_)]
   WaveState st;
   wave_state_init(st);
   if (pstart < pend) {
@@ -260,13 +263,15 @@ __global__ __launch_bounds__(256) void paged_attn_decode_kernel(AttnParams p) {
   float l = st.l;
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
+  if (qr < G) {
 #pragma unroll
-  for (int n = 0; n < kND; ++n)
+    for (int n = 0; n < kND; ++n)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o_s[w][qr][16 * n + 4 * g + i] = st.o[n][i];
-  if (g == 0) {
-    m_s[w][qr] = st.m;
-    l_s[w][qr] = l;
+      for (int i = 0; i < 4; ++i) OS(w, qr, 16 * n + 4 * g + i) = st.o[n][i];
+    if (g == 0) {
+      m_s[w * G + qr] = st.m;
+      l_s[w * G + qr] = l;
+    }
   }
   __syncthreads();
   // combine: thread -> (row, 8 dims)
@@ -275,16 +280,17 @@ __global__ __launch_bounds__(256) void paged_attn_decode_kernel(AttnParams p) {
   if (row >= G) return;
   float M = -1e30f;
 #pragma unroll
-  for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, m_s[ww][row]);
+  for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, m_s[ww * G + row]);
   float L = 0.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int ww = 0; ww < 4; ++ww) {
-    const float f = exp2f(m_s[ww][row] - M);
-    L += f * l_s[ww][row];
+    const float f = exp2f(m_s[ww * G + row] - M);
+    L += f * l_s[ww * G + row];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += f * o_s[ww][row][d0 + j];
+    for (int j = 0; j < 8; ++j) acc[j] += f * OS(ww, row, d0 + j);
   }
+#undef OS
   const float inv = L > 0.f ? 1.f / L : 0.f;
   if (p.num_parts == 1) {
     bf16* op = p.out + ((size_t)q_tok * p.Hq + kvh * G + row) * kD + d0;
@@ -347,10 +353,16 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s
 
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) {
   if (num_seqs == 0) return;
+  const dim3 grid(num_seqs, p.Hkv, p.num_parts);
+  const size_t smem = (size_t)(4 * p.G * (kD + 4) + 8 * p.G) * sizeof(float);
   if (p.flags & 1)
-    paged_attn_decode_kernel<true><<<dim3(num_seqs, p.Hkv, p.num_parts), 256, 0, s>>>(p);
+    paged_attn_decode_kernel<true, 1><<<grid, 256, smem, s>>>(p);
+  else if (p.flags & 2)
+    paged_attn_decode_kernel<false, 5><<<grid, 256, smem, s>>>(p);
+  else if (p.flags & 4)
+    paged_attn_decode_kernel<false, 6><<<grid, 256, smem, s>>>(p);
   else
-    paged_attn_decode_kernel<false><<<dim3(num_seqs, p.Hkv, p.num_parts), 256, 0, s>>>(p);
+    paged_attn_decode_kernel<false, 1><<<grid, 256, smem, s>>>(p);
   if (p.num_parts > 1) paged_attn_reduce_kernel<<<dim3(num_seqs, p.Hkv), 256, 0, s>>>(p);
 }
 

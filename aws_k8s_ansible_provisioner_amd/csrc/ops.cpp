@@ -95,8 +95,9 @@ void silu_and_mul(Tensor out, Tensor x) {
 
 int attn_flags() {
   static int f = [] {
+    // bit0 (default on): register double-buffered K/V prefetch in decode (+1-2% measured)
     const char* e = std::getenv("AKAP_ATTN_FLAGS");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 1;
   }();
   return f;
 }
