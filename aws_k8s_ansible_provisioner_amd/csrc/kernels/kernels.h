@@ -76,7 +76,13 @@ void launch_argmax(const void* logits, int ld, int V, int is_bf16, int64_t* out,
 void launch_moe_topk_softmax(const void* logits, int ld, int E, int K, float* topk_w,
                              int32_t* topk_ids, int T, int renormalize, hipStream_t s);
 void launch_moe_align(const int32_t* topk_ids, int n, int E, int block, int32_t* sorted_ids,
-                      int32_t* expert_offsets, int32_t* num_padded, hipStream_t s);
+                      int32_t* expert_offsets, int32_t* num_padded, int32_t* inv,
+                      int32_t* tile_expert, int max_tiles, hipStream_t s);
+void launch_moe_gemm(const void* A, const void* W, void* Y, const int32_t* sorted_ids,
+                     const int32_t* tile_expert, int max_tiles, int n_flat, int topk, int N,
+                     int K, int lda, int gather, hipStream_t s);
+void launch_moe_combine(const void* Y, const float* wts, const int32_t* inv, void* out, int T,
+                        int topk, int d, hipStream_t s);
 
 // ---- kv_transfer.hip ----
 // The paged cache is `planes` planes (layer x {K,V}) of [NB, block_elems] bf16.

@@ -58,11 +58,16 @@ void launch_moe_topk_softmax(const void* logits, int ld, int E, int K, float* to
 }
 
 // sorted_ids: [n + E*(block-1)] rounded, filled with n (sentinel) for padding.
+// inv[i] = position of flat (token, k) index i in the sorted list (for the combine);
+// tile_expert[t] = expert of row tile t (block rows each), -1 past the last tile.
 __global__ __launch_bounds__(1024) void moe_align_kernel(const int32_t* __restrict__ ids, int n,
                                                          int E, int block,
                                                          int32_t* __restrict__ sorted_ids,
                                                          int32_t* __restrict__ offsets,
-                                                         int32_t* __restrict__ num_padded) {
+                                                         int32_t* __restrict__ num_padded,
+                                                         int32_t* __restrict__ inv,
+                                                         int32_t* __restrict__ tile_expert,
+                                                         int max_tiles) {
   extern __shared__ int sm[];
   int* cnt = sm;          // [E]
   int* cursor = sm + E;   // [E]
@@ -83,17 +88,174 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int32_t* __restri
   __syncthreads();
   const int total = offsets[E];
   for (int i = threadIdx.x; i < total; i += blockDim.x) sorted_ids[i] = n;
+  if (tile_expert != nullptr) {
+    for (int t = threadIdx.x; t < max_tiles; t += blockDim.x) {
+      const int r0 = t * block;
+      int e = -1;
+      if (r0 < total) {
+        e = 0;
+        while (e + 1 < E && offsets[e + 1] <= r0) ++e;
+      }
+      tile_expert[t] = e;
+    }
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int pos = atomicAdd(&cursor[ids[i]], 1);
     sorted_ids[pos] = i;
+    if (inv != nullptr) inv[i] = pos;
   }
 }
 
+// Grouped GEMM over expert-sorted rows:  Y[r] = A[row(r)] . W[e(tile)]^T
+// A_GATHER: row(r) = sorted_ids[r] / topk (token rows of the hidden state; padding rows
+// read as zeros); else row(r) = r (the previous grouped GEMM's output).  Same 64x64x64
+// MFMA tile as gemm.hip, weights per expert [E, N, K] K-major.
+template <bool A_GATHER>
+__global__ __launch_bounds__(256) void moe_gemm_kernel(const bf16* __restrict__ A,
+                                                       const bf16* __restrict__ W,
+                                                       bf16* __restrict__ Y,
+                                                       const int32_t* __restrict__ sorted_ids,
+                                                       const int32_t* __restrict__ tile_expert,
+                                                       int n_flat, int topk, int N, int K,
+                                                       int lda) {
+  __shared__ bf16x8 lds[2][2][64 * 8];
+  const int tile = blockIdx.x;
+  const int e = tile_expert[tile];
+  if (e < 0) return;  // beyond the padded row count (graph-safe fixed grid)
+  const int n0 = blockIdx.y * 64;
+  const int m0 = tile * 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int s_row = tid >> 2, s_ch = (tid & 3) * 2;
+  int arow;
+  bool a_ok;
+  if (A_GATHER) {
+    const int sid = sorted_ids[m0 + s_row];
+    a_ok = sid < n_flat;
+    arow = a_ok ? sid / topk : 0;
+  } else {
+    arow = m0 + s_row;
+    a_ok = true;
+  }
+  const bool b_ok = n0 + s_row < N;
+  const bf16* xa = A + (size_t)arow * lda;
+  const bf16* wb = W + ((size_t)e * N + (b_ok ? n0 + s_row : 0)) * K;
+  const bf16x8 zero8 = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  bf16x8 ra[2], rb[2];
+  auto sw = [](int row, int ch) { return row * 8 + (ch ^ (row & 7)); };
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int kk = k0 + (s_ch + c) * 8;
+      ra[c] = (a_ok && kk < K) ? *reinterpret_cast<const bf16x8*>(xa + kk) : zero8;
+      rb[c] = (b_ok && kk < K) ? *reinterpret_cast<const bf16x8*>(wb + kk) : zero8;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      lds[buf][0][sw(s_row, s_ch + c)] = ra[c];
+      lds[buf][1][sw(s_row, s_ch + c)] = rb[c];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (K + 63) / 64;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nk) gload((it + 1) * 64);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = lds[cur][0][sw(wm * 32 + i * 16 + fr, ks * 4 + fg)];
+        bfr[i] = lds[cur][1][sw(wn * 32 + i * 16 + fr, ks * 4 + fg)];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (it + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 32 + j * 16 + fr;
+      if (col >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + fg * 4 + r;
+        Y[(size_t)row * N + col] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+// out[t] = sum_k w[t,k] * Y[inv[t*K+k]]   (deterministic gather-combine, fp32 sum)
+__global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict__ Y,
+                                                          const float* __restrict__ wts,
+                                                          const int32_t* __restrict__ inv,
+                                                          bf16* __restrict__ out, int T,
+                                                          int topk, int d) {
+  const int vpr = d / 8;
+  const long total = (long)T * vpr;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int t = (int)(i / vpr);
+    const int c = (int)(i % vpr) * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < topk; ++k) {
+      const float wk = wts[(size_t)t * topk + k];
+      const bf16x8 y = *reinterpret_cast<const bf16x8*>(Y + (size_t)inv[(size_t)t * topk + k] * d + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += wk * bf2f(y[j]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+    *reinterpret_cast<bf16x8*>(out + (size_t)t * d + c) = o;
+  }
+}
+
+void launch_moe_gemm(const void* A, const void* W, void* Y, const int32_t* sorted_ids,
+                     const int32_t* tile_expert, int max_tiles, int n_flat, int topk, int N,
+                     int K, int lda, int gather, hipStream_t s) {
+  if (max_tiles == 0) return;
+  dim3 grid(max_tiles, (N + 63) / 64);
+  if (gather)
+    moe_gemm_kernel<true><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)W, (bf16*)Y,
+                                               sorted_ids, tile_expert, n_flat, topk, N, K, lda);
+  else
+    moe_gemm_kernel<false><<<grid, 256, 0, s>>>((const bf16*)A, (const bf16*)W, (bf16*)Y,
+                                                sorted_ids, tile_expert, n_flat, topk, N, K, lda);
+}
+
+void launch_moe_combine(const void* Y, const float* wts, const int32_t* inv, void* out, int T,
+                        int topk, int d, hipStream_t s) {
+  if (T == 0) return;
+  long blocks = ((long)T * (d / 8) + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  moe_combine_kernel<<<(int)blocks, 256, 0, s>>>((const bf16*)Y, wts, inv, (bf16*)out, T, topk,
+                                                 d);
+}
+
 void launch_moe_align(const int32_t* topk_ids, int n, int E, int block, int32_t* sorted_ids,
-                      int32_t* expert_offsets, int32_t* num_padded, hipStream_t s) {
+                      int32_t* expert_offsets, int32_t* num_padded, int32_t* inv,
+                      int32_t* tile_expert, int max_tiles, hipStream_t s) {
   moe_align_kernel<<<1, 1024, 2 * E * sizeof(int), s>>>(topk_ids, n, E, block, sorted_ids,
-                                                        expert_offsets, num_padded);
+                                                        expert_offsets, num_padded, inv,
+                                                        tile_expert, max_tiles);
 }
 
 }  // namespace akap

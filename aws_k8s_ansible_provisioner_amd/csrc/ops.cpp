@@ -238,14 +238,48 @@ void moe_topk_softmax(Tensor logits, Tensor topk_w, Tensor topk_ids, bool renorm
 }
 
 void moe_align(Tensor topk_ids, int64_t E, int64_t block, Tensor sorted_ids, Tensor offsets,
-               Tensor num_padded) {
+               Tensor num_padded, Tensor inv, Tensor tile_expert) {
   CHECK_GPU(topk_ids); CHECK_CONTIG(topk_ids);
   const int n = topk_ids.numel();
   TORCH_CHECK(sorted_ids.numel() >= n + E * (block - 1), "sorted_ids too small");
+  TORCH_CHECK(inv.numel() == 0 || inv.numel() >= n, "inv too small");
+  const int max_tiles = tile_expert.numel();
+  TORCH_CHECK(max_tiles == 0 || (int64_t)max_tiles * block >= sorted_ids.numel(),
+              "tile_expert must cover sorted_ids");
   const c10::DeviceGuard g(topk_ids.device());
   akap::launch_moe_align(topk_ids.data_ptr<int32_t>(), n, E, block,
                          sorted_ids.data_ptr<int32_t>(), offsets.data_ptr<int32_t>(),
-                         num_padded.data_ptr<int32_t>(), cur_stream());
+                         num_padded.data_ptr<int32_t>(),
+                         inv.numel() ? inv.data_ptr<int32_t>() : nullptr,
+                         max_tiles ? tile_expert.data_ptr<int32_t>() : nullptr, max_tiles,
+                         cur_stream());
+}
+
+void moe_gemm(Tensor out, Tensor a, Tensor w, Tensor sorted_ids, Tensor tile_expert,
+              int64_t n_flat, int64_t topk, bool gather) {
+  CHECK_GPU(a); CHECK_BF16(a); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
+  CHECK_LAST_CONTIG(a);
+  TORCH_CHECK(w.dim() == 3, "expert weights [E, N, K]");
+  const int N = w.size(1), K = w.size(2);
+  TORCH_CHECK(a.size(1) == K && out.size(1) == N, "moe_gemm shape mismatch");
+  TORCH_CHECK(K % 8 == 0, "K % 8");
+  const int max_tiles = tile_expert.numel();
+  TORCH_CHECK(out.size(0) >= (int64_t)max_tiles * 64, "out rows must cover all tiles");
+  if (!gather) TORCH_CHECK(a.size(0) >= (int64_t)max_tiles * 64, "a rows must cover all tiles");
+  const c10::DeviceGuard g(a.device());
+  akap::launch_moe_gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), sorted_ids.data_ptr<int32_t>(),
+                        tile_expert.data_ptr<int32_t>(), max_tiles, n_flat, topk, N, K,
+                        a.stride(0), gather ? 1 : 0, cur_stream());
+}
+
+void moe_combine(Tensor y, Tensor wts, Tensor inv, Tensor out) {
+  CHECK_GPU(y); CHECK_BF16(y); CHECK_CONTIG(y); CHECK_CONTIG(out);
+  TORCH_CHECK(wts.scalar_type() == at::kFloat && inv.scalar_type() == at::kInt, "dtypes");
+  const int T = out.size(0), d = out.size(1), topk = wts.size(1);
+  TORCH_CHECK(d % 8 == 0, "d % 8");
+  const c10::DeviceGuard g(y.device());
+  akap::launch_moe_combine(y.data_ptr(), wts.data_ptr<float>(), inv.data_ptr<int32_t>(),
+                           out.data_ptr(), T, topk, d, cur_stream());
 }
 
 void kv_gather(Tensor cache, Tensor block_ids, Tensor out) {
@@ -309,7 +343,11 @@ TORCH_LIBRARY(akap, m) {
   m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def(
       "moe_align(Tensor topk_ids, int E, int block, Tensor(a!) sorted_ids, Tensor(b!) offsets, "
-      "Tensor(c!) num_padded) -> ()");
+      "Tensor(c!) num_padded, Tensor(d!) inv, Tensor(e!) tile_expert) -> ()");
+  m.def(
+      "moe_gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor sorted_ids, Tensor tile_expert, "
+      "int n_flat, int topk, bool gather) -> ()");
+  m.def("moe_combine(Tensor y, Tensor wts, Tensor inv, Tensor(a!) out) -> ()");
   m.def("kv_gather(Tensor cache, Tensor block_ids, Tensor(a!) out) -> ()");
   m.def("kv_scatter(Tensor buf, Tensor(a!) cache, Tensor block_ids) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start, int vocab_end) -> ()");
@@ -332,6 +370,8 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
+  m.impl("moe_gemm", &moe_gemm);
+  m.impl("moe_combine", &moe_combine);
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);
   m.impl("embedding", &embedding);

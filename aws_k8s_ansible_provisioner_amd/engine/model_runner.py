@@ -76,7 +76,7 @@ class ModelRunner:
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.buckets: list[int] = []
-        if self.is_gpu and not ecfg.enforce_eager:
+        if self.is_gpu and not ecfg.enforce_eager and self.model.graph_safe:
             self.capture_graphs()
 
     # ------------------------------------------------------------------ sizing

@@ -6,7 +6,10 @@ sorted, tile-padded index list).  Two placements:
     like a dense layer) -- best at small batch on a single xGMI node;
   * "ep": rank e holds experts [e*E/ep, (e+1)*E/ep) whole; tokens are dispatched and
     combined with two RCCL all_to_all_single calls over the EP (=dp x tp) group.
-Expert GEMMs run per expert on the grouped, contiguous token slices (hipBLASLt).
+Expert GEMMs, "tp" mode on the GPU at decode sizes: `ops.fused_moe` -- device-side
+sort + grouped MFMA GEMMs + gather-combine, no host sync, so decode captures in a
+hipGraph.  Large (prefill) batches and "ep" mode run per expert on the grouped token
+slices (hipBLASLt), which needs the per-expert counts on the host.
 """
 from __future__ import annotations
 
@@ -114,10 +117,21 @@ class MoEBlock:
             return torch.cat(parts)[:T]
         return self._forward_tokens(h)
 
+    graph_safe_max_tokens = int(os.environ.get("AKAP_FUSED_MOE_MAX_T", "1024"))
+
+    @property
+    def graph_safe(self) -> bool:
+        return self.mode != "ep"
+
     def _forward_tokens(self, h: torch.Tensor) -> torch.Tensor:
         T, d = h.shape
         logits = F.linear(h, self.router)
         w, ids = ops.moe_topk_softmax(logits, self.K, renormalize=True)
+        if self.mode != "ep" and h.is_cuda and (T <= self.graph_safe_max_tokens or
+                                                  torch.cuda.is_current_stream_capturing()):
+            out = ops.fused_moe(h, self.w13, self.w2, w, ids)
+            comm.tp_all_reduce(out)
+            return out
         flat = ids.reshape(-1).long()
         order = torch.argsort(flat, stable=True)
         tok_of = order // self.K

@@ -171,6 +171,11 @@ class DecoderLM:
         h = r // (tp // H)
         return h, h + 1
 
+    @property
+    def graph_safe(self) -> bool:
+        """Decode step free of host syncs (capturable in a hipGraph)."""
+        return all(l.moe is None or l.moe.graph_safe for l in self.layers)
+
     def weight_bytes(self) -> int:
         n = self.embed.numel() + self.final_norm.numel()
         if self.lm_head is not self.embed:

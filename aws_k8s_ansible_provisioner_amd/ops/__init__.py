@@ -8,7 +8,7 @@ Every op dispatches on the device of its inputs:
     suite, the CPU mock engine and as the numerics oracle of the GPU tests).
 
 Layouts shared with the kernels (see csrc/kernels/rope_cache.hip):
-  K cache [num_blocks, Hkv, BS, D], V cache [num_blocks, Hkv, D, BS] (V^T per block).
+  K cache [num_blocks, Hkv, BS, D], V cache [num_blocks, Hkv, BS/8, D, 8] (8-token groups).
 """
 from __future__ import annotations
 
@@ -248,23 +248,68 @@ def moe_topk_softmax(router_logits, top_k: int, renormalize: bool = True):
     return w, ids
 
 
-def moe_align(topk_ids, num_experts: int, block: int):
-    n = topk_ids.numel()
+def moe_capacity(n: int, num_experts: int, block: int) -> int:
     cap = n + num_experts * (block - 1)
-    cap = (cap + block - 1) // block * block
+    return (cap + block - 1) // block * block
+
+
+def moe_align(topk_ids, num_experts: int, block: int, inv=None, tile_expert=None):
+    """Expert-sorted, block-padded index list.  Optional outputs (GPU): inv[i] = sorted
+    position of flat index i; tile_expert[t] = expert of row tile t (-1 past the end)."""
+    n = topk_ids.numel()
+    cap = moe_capacity(n, num_experts, block)
     dev = topk_ids.device
     sorted_ids = torch.empty(cap, dtype=torch.int32, device=dev)
     offsets = torch.empty(num_experts + 1, dtype=torch.int32, device=dev)
     num_padded = torch.empty(1, dtype=torch.int32, device=dev)
     if _native(topk_ids):
+        e32 = _EMPTY_I32.get(dev)
+        if e32 is None:
+            e32 = _EMPTY_I32[dev] = torch.empty(0, dtype=torch.int32, device=dev)
         torch.ops.akap.moe_align(topk_ids.contiguous(), num_experts, block, sorted_ids, offsets,
-                                 num_padded)
+                                 num_padded, e32 if inv is None else inv,
+                                 e32 if tile_expert is None else tile_expert)
         return sorted_ids, offsets, num_padded
     s, o, npad = ref.moe_align(topk_ids, num_experts, block, cap)
     sorted_ids.copy_(s)
     offsets.copy_(o)
     num_padded.fill_(npad)
     return sorted_ids, offsets, num_padded
+
+
+_EMPTY_I32: dict = {}
+MOE_BLOCK = 64
+
+
+def fused_moe(h, w13, w2, topk_w, topk_ids, out=None):
+    """Graph-safe fused expert FFN: out[t] = sum_k w[t,k] * W2_e . silu_mul(W13_e . h[t]).
+
+    GPU: moe_align (device-side sort + tile->expert map) -> grouped MFMA GEMM gathering
+    token rows -> silu_and_mul -> grouped GEMM -> deterministic gather-combine.  All
+    buffer shapes depend only on (T, top_k, E), so the whole block captures in a hipGraph.
+    w13 [E, 2F, d], w2 [E, d, F]."""
+    T, d = h.shape
+    K = topk_ids.shape[1]
+    E = w13.shape[0]
+    if out is None:
+        out = torch.empty(T, d, dtype=h.dtype, device=h.device)
+    if not _native(h):
+        out.copy_(ref.fused_moe(h, w13, w2, topk_w, topk_ids))
+        return out
+    n = T * K
+    cap = moe_capacity(n, E, MOE_BLOCK)
+    tiles = cap // MOE_BLOCK
+    dev = h.device
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    tile_expert = torch.empty(tiles, dtype=torch.int32, device=dev)
+    sorted_ids, _, _ = moe_align(topk_ids, E, MOE_BLOCK, inv=inv, tile_expert=tile_expert)
+    y1 = torch.empty(cap, w13.shape[1], dtype=h.dtype, device=dev)
+    torch.ops.akap.moe_gemm(y1, h, w13, sorted_ids, tile_expert, n, K, True)
+    a = silu_and_mul(y1)
+    y2 = torch.empty(cap, d, dtype=h.dtype, device=dev)
+    torch.ops.akap.moe_gemm(y2, a, w2, sorted_ids, tile_expert, n, K, False)
+    torch.ops.akap.moe_combine(y2, topk_w.contiguous(), inv, out)
+    return out
 
 
 def kv_gather(cache_planes, block_ids, out=None):

@@ -196,3 +196,18 @@ def moe_align(topk_ids, E, block, cap):
         acc += (idx.numel() + block - 1) // block * block
     offsets[E] = acc
     return sorted_ids.to(topk_ids.device), offsets.to(topk_ids.device), acc
+
+
+def fused_moe(h, w13, w2, topk_w, topk_ids):
+    """fp32 reference of the fused expert FFN (bf16 rounding at the same points as the
+    kernels: after each GEMM and after silu_and_mul)."""
+    T, d = h.shape
+    out = torch.zeros(T, d, dtype=torch.float32, device=h.device)
+    for t in range(T):
+        for k in range(topk_ids.shape[1]):
+            e = int(topk_ids[t, k])
+            y1 = (h[t].float() @ w13[e].float().t()).to(h.dtype)
+            a = silu_and_mul(y1[None])[0]
+            y2 = (a.float() @ w2[e].float().t()).to(h.dtype)
+            out[t] += float(topk_w[t, k]) * y2.float()
+    return out.to(h.dtype)

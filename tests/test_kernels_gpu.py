@@ -250,6 +250,68 @@ def test_moe_routing():
     assert int(npad) == int(off[-1])
 
 
+def test_moe_align_inv_and_tiles():
+    torch.manual_seed(9)
+    T, E, K = 77, 8, 2
+    ids = torch.randint(0, E, (T, K), dtype=torch.int32, device=DEV)
+    n = T * K
+    cap = ops.moe_capacity(n, E, 64)
+    inv = torch.empty(n, dtype=torch.int32, device=DEV)
+    te = torch.empty(cap // 64, dtype=torch.int32, device=DEV)
+    s, off, npad = ops.moe_align(ids, E, 64, inv=inv, tile_expert=te)
+    s, off, inv, te = s.cpu(), off.cpu(), inv.cpu(), te.cpu()
+    assert torch.equal(s[inv.long()], torch.arange(n, dtype=torch.int32))
+    for t in range(cap // 64):
+        if t * 64 >= int(off[-1]):
+            assert int(te[t]) == -1
+        else:
+            e = int(te[t])
+            assert off[e] <= t * 64 < off[e + 1]
+
+
+@pytest.mark.parametrize("T,E,K,d,F", [(1, 8, 2, 256, 512), (37, 8, 2, 512, 384),
+                                       (256, 8, 2, 256, 256), (64, 16, 4, 128, 192)])
+def test_fused_moe(T, E, K, d, F):
+    torch.manual_seed(T + E)
+    h = torch.randn(T, d, dtype=torch.bfloat16)
+    w13 = torch.randn(E, 2 * F, d, dtype=torch.bfloat16) * d ** -0.5
+    w2 = torch.randn(E, d, F, dtype=torch.bfloat16) * F ** -0.5
+    logits = torch.randn(T, E, dtype=torch.bfloat16)
+    w, ids = ref.moe_topk_softmax(logits, K)
+    exp = ref.fused_moe(h, w13, w2, w, ids)
+    out = ops.fused_moe(h.to(DEV), w13.to(DEV), w2.to(DEV), w.to(DEV), ids.to(DEV))
+    _close(out, exp, atol=3e-2, rtol=3e-2)
+
+
+def test_fused_moe_graph_capture():
+    torch.manual_seed(3)
+    T, E, K, d, F = 48, 8, 2, 256, 256
+    h = torch.randn(T, d, dtype=torch.bfloat16, device=DEV)
+    w13 = torch.randn(E, 2 * F, d, dtype=torch.bfloat16, device=DEV) * 0.06
+    w2 = torch.randn(E, d, F, dtype=torch.bfloat16, device=DEV) * 0.06
+    logits = torch.randn(T, E, dtype=torch.bfloat16, device=DEV)
+    out = torch.empty(T, d, dtype=torch.bfloat16, device=DEV)
+
+    def run():
+        w, ids = ops.moe_topk_softmax(logits, K)
+        ops.fused_moe(h, w13, w2, w, ids, out=out)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    logits.copy_(torch.randn(T, E, dtype=torch.bfloat16, device=DEV))
+    g.replay()
+    torch.cuda.synchronize()
+    w, ids = ref.moe_topk_softmax(logits.cpu(), K)
+    exp = ref.fused_moe(h.cpu(), w13.cpu(), w2.cpu(), w, ids)
+    _close(out, exp, atol=3e-2, rtol=3e-2)
+
+
 def test_kv_gather_scatter_roundtrip():
     planes, NB = 6, 20
     cache = torch.randn(planes, NB, 8, 32, 128, dtype=torch.bfloat16, device=DEV)

@@ -1,0 +1,131 @@
+"""CPU checks of the op references (the semantics every HIP kernel is tested against)
+and of the Python-side glue around them.  The GPU kernels are compared against these
+same references in tests/test_kernels_gpu.py."""
+import math
+
+import torch
+
+from aws_k8s_ansible_provisioner_amd import ops
+from aws_k8s_ansible_provisioner_amd.ops import reference as ref
+
+
+def _moe_dense(h, w13, w2, w, ids):
+    """Dense fp32 formulation: every token through every expert, masked by routing."""
+    T, d = h.shape
+    E = w13.shape[0]
+    F = w13.shape[1] // 2
+    out = torch.zeros(T, d)
+    for e in range(E):
+        y = h.float() @ w13[e].float().t()
+        a = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
+        y2 = a @ w2[e].float().t()
+        gate = ((ids == e).float() * w).sum(-1, keepdim=True)
+        out += gate * y2
+    return out
+
+
+def test_fused_moe_reference_matches_dense():
+    torch.manual_seed(0)
+    T, E, K, d, F = 9, 4, 2, 32, 24
+    h = torch.randn(T, d, dtype=torch.bfloat16)
+    w13 = (torch.randn(E, 2 * F, d) * 0.2).bfloat16()
+    w2 = (torch.randn(E, d, F) * 0.2).bfloat16()
+    w, ids = ref.moe_topk_softmax(torch.randn(T, E), K)
+    got = ops.fused_moe(h, w13, w2, w, ids).float()
+    exp = _moe_dense(h, w13, w2, w, ids)
+    assert torch.allclose(got, exp, atol=3e-2, rtol=3e-2)
+
+
+def test_moe_align_reference_layout():
+    ids = torch.tensor([[0, 2], [2, 1], [0, 2]], dtype=torch.int32)
+    s, off, npad = ops.moe_align(ids, 4, 4)
+    assert off.tolist() == [0, 4, 8, 12, 12]
+    assert int(npad) == 12
+    flat = ids.reshape(-1)
+    for e in range(4):
+        seg = s[off[e]:off[e + 1]]
+        real = seg[seg < flat.numel()]
+        assert sorted(real.tolist()) == (flat == e).nonzero().flatten().tolist()
+
+
+def test_moe_capacity_covers_worst_case():
+    for n, E, b in [(1, 8, 64), (512, 8, 64), (7, 64, 16)]:
+        cap = ops.moe_capacity(n, E, b)
+        assert cap % b == 0 and cap >= n + E * (b - 1)
+
+
+def test_paged_attention_reference_vs_dense_causal():
+    torch.manual_seed(1)
+    Hq, Hkv, D, BS = 4, 2, 64, 16
+    lens = [5, 23]
+    nb = 8
+    kc = torch.zeros(nb, Hkv, BS, D)
+    vc = torch.zeros(nb, Hkv, BS // 8, D, 8)
+    tables = torch.tensor([[3, 5, 0, 0], [1, 6, 0, 0]], dtype=torch.int32)
+    ks, vs = [], []
+    for b, L in enumerate(lens):
+        k = torch.randn(L, Hkv, D)
+        v = torch.randn(L, Hkv, D)
+        slots = torch.tensor([int(tables[b, t // BS]) * BS + t % BS for t in range(L)])
+        ref.write_cache(k, v, kc, vc, slots)
+        ks.append(k)
+        vs.append(v)
+    q = torch.randn(sum(lens), Hq, D)
+    q_start = torch.tensor([0, lens[0], sum(lens)], dtype=torch.int32)
+    out = ref.paged_attention(q, kc, vc, tables, torch.tensor(lens), q_start, D ** -0.5)
+    G = Hq // Hkv
+    for b, L in enumerate(lens):
+        qb = q[q_start[b]:q_start[b + 1]]
+        K = ks[b].repeat_interleave(G, 1)
+        V = vs[b].repeat_interleave(G, 1)
+        s = torch.einsum("qhd,khd->hqk", qb, K) * D ** -0.5
+        s = s.masked_fill(torch.ones(L, L).triu(1).bool()[None], -math.inf)
+        o = torch.einsum("hqk,khd->qhd", s.softmax(-1), V)
+        assert torch.allclose(out[q_start[b]:q_start[b + 1]], o, atol=1e-5)
+
+
+def test_v_cache_group_layout_roundtrip():
+    BS, D, Hkv = 32, 16, 2
+    kc = torch.zeros(4, Hkv, BS, D)
+    vc = torch.zeros(4, Hkv, BS // 8, D, 8)
+    k = torch.randn(40, Hkv, D)
+    v = torch.randn(40, Hkv, D)
+    slots = torch.arange(40) + 32
+    ref.write_cache(k, v, kc, vc, slots)
+    K, V = ref.gather_kv(kc, vc, torch.tensor([1, 2], dtype=torch.int32), 40)
+    assert torch.equal(K, k) and torch.equal(V, v)
+    # token o of block b sits at v_cache[b, h, o // 8, :, o % 8]
+    assert torch.equal(vc[1, 0, 1, :, 3], v[11, 0])
+
+
+def test_sampler_reference_topk_topp_support():
+    torch.manual_seed(2)
+    V = 50
+    logits = torch.randn(64, V)
+    temp = torch.full((64,), 0.8)
+    top_k = torch.full((64,), 5, dtype=torch.int32)
+    top_p = torch.full((64,), 1.0)
+    toks, lps = ref.sample(logits, temp, top_k, top_p, torch.arange(64), torch.zeros(64))
+    for i in range(64):
+        assert int(toks[i]) in torch.topk(logits[i], 5).indices.tolist()
+        assert float(lps[i]) <= 0.0
+    greedy, _ = ref.sample(logits, torch.zeros(64), top_k, top_p, torch.arange(64),
+                           torch.zeros(64))
+    assert torch.equal(greedy, logits.argmax(-1))
+
+
+def test_rope_llama3_scaling_keeps_high_freqs():
+    plain = ref.rope_cos_sin(20000, 128, 500000.0)
+    sc = ref.rope_cos_sin(20000, 128, 500000.0, {"rope_type": "llama3", "factor": 8.0,
+                                              "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                              "original_max_position_embeddings": 8192})
+    # highest frequencies (first dims) are unscaled, lowest are divided by the factor
+    assert torch.allclose(plain[:, :4], sc[:, :4])
+    assert not torch.allclose(plain[:, 124:128], sc[:, 124:128], atol=1e-3)
+
+
+def test_gemm_splitk_fills_chip():
+    for M, N, K in [(64, 1024, 4096), (256, 4096, 1024), (512, 151936, 1024)]:
+        s = ops.gemm_splitk(M, N, K)
+        tiles = ((M + 63) // 64) * ((N + 63) // 64)
+        assert tiles * s >= 256 or K // (s * 2) < 256
