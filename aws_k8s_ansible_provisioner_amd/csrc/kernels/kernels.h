@@ -95,4 +95,24 @@ void launch_kv_scatter(const void* in, void* cache, long plane_stride, int plane
 void launch_embedding(const int64_t* ids, const void* table, void* out, int T, int d,
                       int vocab_start, int vocab_end, hipStream_t s);
 
+// ---- custom_allreduce.hip ----
+struct CarArgs {
+  __bf16* bufs[8];       // per-rank IPC-mapped buffers [4 * half_elems] (staging x2, result x2)
+  uint32_t* sigs[8];     // per-rank IPC-mapped flag arrays
+  uint32_t* counter;     // local per-block epoch counters
+  uint32_t* err;         // local error flag (spin-wait timeout)
+  int rank, world;
+  size_t half_elems;     // capacity in elements of one staging half
+};
+void launch_custom_allreduce(const CarArgs& a, const void* in, void* out, long n, int two_shot,
+                             hipStream_t s);
+size_t custom_allreduce_signal_bytes();
+struct CarMulti {  // test-only: every rank of a simulated group in one launch
+  CarArgs args[8];
+  const void* in[8];
+  void* out[8];
+};
+void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two_shot,
+                                   hipStream_t s);
+
 }  // namespace akap

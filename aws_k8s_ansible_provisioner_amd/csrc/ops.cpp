@@ -4,6 +4,8 @@
 // never synchronises, so all of them are hipGraph-capturable (engine decode path).
 // PyTorch on ROCm names the GPU dispatch key "CUDA"; kernels are HIP/CDNA4 only.
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -317,6 +319,167 @@ void embedding(Tensor ids, Tensor table, Tensor out, int64_t vocab_start, int64_
 
 }  // namespace
 
+
+// ---------------------------------------------------------------- custom all-reduce (K13)
+// Per-communicator state lives here (C++), indexed by a small integer handle that the
+// Python wrapper (parallel/custom_allreduce.py) keeps.  IPC handles are exchanged by the
+// caller over torch.distributed.
+namespace {
+struct CarComm {
+  int device = 0;
+  akap::CarArgs args{};
+  void* buf = nullptr;
+  void* sig = nullptr;
+  std::vector<void*> opened;
+};
+std::vector<CarComm*>& car_table() {
+  static std::vector<CarComm*> t;
+  return t;
+}
+CarComm* car_get(int64_t h) {
+  auto& t = car_table();
+  TORCH_CHECK(h >= 0 && h < (int64_t)t.size() && t[h] != nullptr, "bad custom all-reduce handle");
+  return t[h];
+}
+#define HIP_OK(x)                                                                     \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    TORCH_CHECK(e_ == hipSuccess, #x " failed: ", hipGetErrorString(e_));             \
+  } while (0)
+}  // namespace
+
+int64_t car_create(int64_t device, int64_t rank, int64_t world, int64_t max_elems) {
+  TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "world must be 1..8");
+  TORCH_CHECK(max_elems % 8 == 0, "max_elems % 8");
+  const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (int)device));
+  auto* c = new CarComm();
+  c->device = (int)device;
+  const size_t buf_bytes = (size_t)4 * max_elems * sizeof(uint16_t);
+  const size_t sig_bytes = akap::custom_allreduce_signal_bytes();
+  HIP_OK(hipExtMallocWithFlags(&c->buf, buf_bytes, hipDeviceMallocUncached));
+  HIP_OK(hipExtMallocWithFlags(&c->sig, sig_bytes, hipDeviceMallocUncached));
+  HIP_OK(hipMemset(c->sig, 0, sig_bytes));
+  void* local = nullptr;
+  HIP_OK(hipMalloc(&local, 4096));
+  HIP_OK(hipMemset(local, 0, 4096));
+  HIP_OK(hipDeviceSynchronize());
+  c->args.counter = reinterpret_cast<uint32_t*>(local);
+  c->args.err = reinterpret_cast<uint32_t*>(local) + 1023;
+  c->args.rank = (int)rank;
+  c->args.world = (int)world;
+  c->args.half_elems = (size_t)max_elems;
+  for (int p = 0; p < 8; ++p) { c->args.bufs[p] = nullptr; c->args.sigs[p] = nullptr; }
+  c->args.bufs[rank] = reinterpret_cast<__bf16*>(c->buf);
+  c->args.sigs[rank] = reinterpret_cast<uint32_t*>(c->sig);
+  car_table().push_back(c);
+  return (int64_t)car_table().size() - 1;
+}
+
+Tensor car_ipc_handles(int64_t h) {
+  CarComm* c = car_get(h);
+  const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c->device));
+  auto out = at::empty({2, (int64_t)sizeof(hipIpcMemHandle_t)}, at::kByte);
+  hipIpcMemHandle_t hb, hs;
+  HIP_OK(hipIpcGetMemHandle(&hb, c->buf));
+  HIP_OK(hipIpcGetMemHandle(&hs, c->sig));
+  std::memcpy(out.data_ptr<uint8_t>(), &hb, sizeof(hb));
+  std::memcpy(out.data_ptr<uint8_t>() + sizeof(hb), &hs, sizeof(hs));
+  return out;
+}
+
+void car_open(int64_t h, Tensor all_handles) {
+  CarComm* c = car_get(h);
+  TORCH_CHECK(all_handles.device().is_cpu() && all_handles.scalar_type() == at::kByte, "cpu uint8");
+  TORCH_CHECK(all_handles.size(0) == c->args.world, "one handle pair per rank");
+  const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c->device));
+  auto hc = all_handles.contiguous();
+  const uint8_t* base = hc.data_ptr<uint8_t>();
+  const size_t hs = sizeof(hipIpcMemHandle_t);
+  for (int p = 0; p < c->args.world; ++p) {
+    if (p == c->args.rank) continue;
+    hipIpcMemHandle_t hb, hg;
+    std::memcpy(&hb, base + (size_t)p * 2 * hs, hs);
+    std::memcpy(&hg, base + (size_t)p * 2 * hs + hs, hs);
+    void* pb = nullptr;
+    void* pg = nullptr;
+    HIP_OK(hipIpcOpenMemHandle(&pb, hb, hipIpcMemLazyEnablePeerAccess));
+    HIP_OK(hipIpcOpenMemHandle(&pg, hg, hipIpcMemLazyEnablePeerAccess));
+    c->opened.push_back(pb);
+    c->opened.push_back(pg);
+    c->args.bufs[p] = reinterpret_cast<__bf16*>(pb);
+    c->args.sigs[p] = reinterpret_cast<uint32_t*>(pg);
+  }
+}
+
+void car_all_reduce(int64_t h, Tensor inp, Tensor out, bool two_shot) {
+  CarComm* c = car_get(h);
+  CHECK_GPU(inp); CHECK_BF16(inp); CHECK_CONTIG(inp); CHECK_CONTIG(out); CHECK_BF16(out);
+  TORCH_CHECK(inp.numel() == out.numel(), "size mismatch");
+  TORCH_CHECK(inp.numel() % 8 == 0, "numel % 8");
+  TORCH_CHECK((size_t)inp.numel() <= c->args.half_elems, "message larger than the buffer");
+  for (int p = 0; p < c->args.world; ++p)
+    TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
+  const c10::DeviceGuard g(inp.device());
+  akap::launch_custom_allreduce(c->args, inp.data_ptr(), out.data_ptr(), inp.numel(),
+                                two_shot ? 1 : 0, cur_stream());
+}
+
+// Test hook: wire communicators created in THIS process (one per simulated rank, all on
+// one GPU) to each other without IPC, so the kernel protocol can be exercised on 1 GPU.
+void car_link_local(int64_t h, std::vector<int64_t> peers) {
+  CarComm* c = car_get(h);
+  TORCH_CHECK((int)peers.size() == c->args.world, "one handle per rank");
+  for (int p = 0; p < c->args.world; ++p) {
+    CarComm* o = car_get(peers[p]);
+    c->args.bufs[p] = reinterpret_cast<__bf16*>(o->buf);
+    c->args.sigs[p] = reinterpret_cast<uint32_t*>(o->sig);
+  }
+}
+
+// Test hook: run the all-reduce of every simulated rank (communicators linked with
+// car_link_local) in ONE grid, blockIdx.y = rank, so all ranks are co-resident regardless
+// of how streams map to hardware queues.
+void car_all_reduce_multi(std::vector<int64_t> hs, std::vector<Tensor> ins,
+                          std::vector<Tensor> outs, bool two_shot) {
+  const int W = hs.size();
+  TORCH_CHECK(W >= 1 && W <= 8 && (int)ins.size() == W && (int)outs.size() == W, "W ranks");
+  akap::CarMulti m{};
+  const int64_t n = ins[0].numel();
+  for (int r = 0; r < W; ++r) {
+    CarComm* c = car_get(hs[r]);
+    TORCH_CHECK(c->args.world == W && c->args.rank == r, "handles must be ranks 0..W-1");
+    CHECK_GPU(ins[r]); CHECK_BF16(ins[r]); CHECK_CONTIG(ins[r]); CHECK_CONTIG(outs[r]);
+    TORCH_CHECK(ins[r].numel() == n && outs[r].numel() == n && n % 8 == 0, "sizes");
+    TORCH_CHECK((size_t)n <= c->args.half_elems, "message larger than the buffer");
+    m.args[r] = c->args;
+    m.in[r] = ins[r].data_ptr();
+    m.out[r] = outs[r].data_ptr();
+  }
+  const c10::DeviceGuard g(ins[0].device());
+  akap::launch_custom_allreduce_multi(m, W, n, two_shot ? 1 : 0, cur_stream());
+}
+
+int64_t car_error(int64_t h) {
+  CarComm* c = car_get(h);
+  const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c->device));
+  uint32_t v = 0;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(&v, c->args.err, sizeof(v), hipMemcpyDeviceToHost));
+  return (int64_t)v;
+}
+
+void car_destroy(int64_t h) {
+  CarComm* c = car_get(h);
+  const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c->device));
+  (void)hipDeviceSynchronize();
+  for (void* p : c->opened) (void)hipIpcCloseMemHandle(p);
+  (void)hipFree(c->buf);
+  (void)hipFree(c->sig);
+  (void)hipFree(c->args.counter);
+  delete c;
+  car_table()[h] = nullptr;
+}
+
 TORCH_LIBRARY(akap, m) {
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
@@ -340,6 +503,14 @@ TORCH_LIBRARY(akap, m) {
   m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
   m.def("gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int splitk) -> ()");
   m.def("gemm_splitk(int M, int N, int K) -> int");
+  m.def("car_create(int device, int rank, int world, int max_elems) -> int");
+  m.def("car_ipc_handles(int h) -> Tensor");
+  m.def("car_open(int h, Tensor handles) -> ()");
+  m.def("car_all_reduce(int h, Tensor inp, Tensor(a!) out, bool two_shot) -> ()");
+  m.def("car_error(int h) -> int");
+  m.def("car_link_local(int h, int[] peers) -> ()");
+  m.def("car_all_reduce_multi(int[] hs, Tensor[] ins, Tensor(a!)[] outs, bool two_shot) -> ()");
+  m.def("car_destroy(int h) -> ()");
   m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def(
       "moe_align(Tensor topk_ids, int E, int block, Tensor(a!) sorted_ids, Tensor(b!) offsets, "
@@ -355,6 +526,12 @@ TORCH_LIBRARY(akap, m) {
 
 TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("gemm_splitk", &gemm_splitk);
+  m.impl("car_create", &car_create);
+  m.impl("car_ipc_handles", &car_ipc_handles);
+  m.impl("car_open", &car_open);
+  m.impl("car_error", &car_error);
+  m.impl("car_link_local", &car_link_local);
+  m.impl("car_destroy", &car_destroy);
 }
 
 TORCH_LIBRARY_IMPL(akap, CUDA, m) {
@@ -372,6 +549,8 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
+  m.impl("car_all_reduce", &car_all_reduce);
+  m.impl("car_all_reduce_multi", &car_all_reduce_multi);
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);
   m.impl("embedding", &embedding);

@@ -2,8 +2,9 @@
 
 MI355X nodes are a fully-connected xGMI mesh (7 links x ~153 GB/s per GPU), not a
 switch: a ring all-reduce is bound by one link per hop.  The policy here:
-  * small decode-time all-reduces (a few KB-MB per layer) -> one RCCL all_reduce
-    call in-place on the activation (RCCL picks its LL/LL128 protocols for these);
+  * decode-time all-reduces (a few KB-MB per layer) -> the custom one-/two-shot xGMI
+    kernel (parallel/custom_allreduce.py, one launch, graph-capturable); larger ones
+    (prefill) -> one RCCL all_reduce in place;
   * vocab-parallel logits -> all_gather into a pre-allocated buffer;
   * MoE token dispatch/combine -> all_to_all_single with explicit split sizes;
   * KV hand-off (P/D) -> one packed send/recv per request (see parallel/kv_transfer.py).
@@ -23,6 +24,8 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     st = get_state()
     if st.tp_size == 1:
         return x
+    if st.car is not None and st.car.should_use(x):
+        return st.car.all_reduce(x)
     dist.all_reduce(x, group=st.tp_group)
     return x
 

@@ -1,0 +1,71 @@
+"""Custom intra-node all-reduce over xGMI peer mappings.
+
+Wraps the one-shot / two-shot HIP kernels of csrc/kernels/custom_allreduce.hip.  Each
+TP rank allocates an uncached staging buffer + flag array, exports hipIpc handles, the
+handles are all-gathered over torch.distributed, and every rank maps its peers' buffers.
+Decode-sized activations (<= ``max_bytes``) then take one kernel launch instead of an
+RCCL ring; larger messages (prefill) fall back to RCCL.  The kernels keep their epochs
+on the device, so they replay correctly inside captured hipGraphs.
+
+Policy (xGMI mesh, W ranks): one-shot reads (W-1) x the message over W-1 links at once
+and has one flag exchange -- best while the message is small; two-shot moves 2(W-1)/W x
+the message with two flag exchanges -- better once link bandwidth, not latency, binds.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+DEFAULT_MAX_BYTES = int(os.environ.get("AKAP_CAR_MAX_BYTES", str(8 << 20)))
+
+
+def oneshot_limit(world: int) -> int:
+    env = os.environ.get("AKAP_CAR_ONESHOT_BYTES")
+    if env:
+        return int(env)
+    return (512 << 10) if world <= 4 else (256 << 10)
+
+
+class CustomAllReduce:
+    def __init__(self, group=None, device: Optional[torch.device] = None,
+                 max_bytes: int = DEFAULT_MAX_BYTES):
+        ops.load_native(required=True)
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.max_bytes = max_bytes
+        self.oneshot_bytes = oneshot_limit(self.world)
+        max_elems = (max_bytes // 2 + 7) // 8 * 8
+        self.h = torch.ops.akap.car_create(self.device.index, self.rank, self.world, max_elems)
+        mine = torch.ops.akap.car_ipc_handles(self.h)
+        allh: list = [None] * self.world
+        dist.all_gather_object(allh, mine.numpy().tobytes(), group=group)
+        handles = torch.stack([torch.frombuffer(bytearray(b), dtype=torch.uint8).view(2, -1)
+                               for b in allh])
+        torch.ops.akap.car_open(self.h, handles)
+        dist.barrier(group=group)
+
+    def should_use(self, x: torch.Tensor) -> bool:
+        nbytes = x.numel() * x.element_size()
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
+                and x.numel() % 8 == 0 and nbytes <= self.max_bytes)
+
+    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        out = x if out is None else out
+        two = x.numel() * 2 > self.oneshot_bytes and self.world > 2
+        torch.ops.akap.car_all_reduce(self.h, x, out, two)
+        return out
+
+    def error(self) -> int:
+        return int(torch.ops.akap.car_error(self.h))
+
+    def close(self) -> None:
+        if self.h is not None:
+            torch.ops.akap.car_destroy(self.h)
+            self.h = None

@@ -30,6 +30,7 @@ class ParallelState:
     tp_group: Optional[object] = None
     dp_group: Optional[object] = None
     backend: str = "none"
+    car: Optional[object] = None   # CustomAllReduce over the TP group (xGMI peer mappings)
 
     @property
     def is_distributed(self) -> bool:
@@ -88,6 +89,10 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
             grp = dist.new_group(ranks)
             if rank in ranks:
                 st.dp_group = grp
+    if (world > 1 and tp_size > 1 and backend == "nccl"
+            and os.environ.get("AKAP_CUSTOM_AR", "1") != "0"):
+        from .custom_allreduce import CustomAllReduce
+        st.car = CustomAllReduce(group=st.tp_group, device=torch.device("cuda", local))
     _STATE = st
     return st
 
@@ -99,6 +104,8 @@ def set_state(st: ParallelState) -> None:
 
 def destroy() -> None:
     global _STATE
+    if _STATE.car is not None:
+        _STATE.car.close()
     if dist.is_initialized():
         dist.destroy_process_group()
     _STATE = ParallelState()

@@ -1,0 +1,188 @@
+"""Custom xGMI all-reduce kernels (K13) on one MI355X.
+
+* in-process: W communicators in one process (one per simulated rank) wired together
+  without IPC, all ranks in one grid (blockIdx.y = rank, so co-residency does not depend
+  on the stream -> hardware-queue mapping) or, for W=2, on two HIP streams -- exercises
+  the flag protocol, epoch parity, slice ownership and graph replay;
+* multi-process: 2 processes on the same GPU exchange real hipIpc handles over gloo.
+Results are checked against an fp32 sum of the inputs (PyTorch reference)."""
+import socket
+
+import pytest
+import torch
+
+from aws_k8s_ansible_provisioner_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref_sum(xs):
+    acc = torch.zeros_like(xs[0], dtype=torch.float32)
+    for x in xs:
+        acc += x.float()
+    return acc.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("two_shot", [False, True])
+@pytest.mark.parametrize("n", [8, 4096, 8 * 1000 + 8 * 3, 1 << 19])
+def test_custom_allreduce_in_process(world, two_shot, n):
+    """All simulated ranks in one grid (blockIdx.y = rank): protocol, parity, ownership."""
+    ops.load_native(required=True)
+    max_elems = 1 << 20
+    hs = [torch.ops.akap.car_create(0, r, world, max_elems) for r in range(world)]
+    try:
+        for h in hs:
+            torch.ops.akap.car_link_local(h, hs)
+        for it in range(3):  # several epochs: both parities, reused flags
+            torch.manual_seed(100 * it + world + n)
+            xs = [torch.randn(n, dtype=torch.bfloat16, device=DEV) for _ in range(world)]
+            outs = [torch.empty_like(x) for x in xs]
+            torch.ops.akap.car_all_reduce_multi(hs, xs, outs, two_shot)
+            torch.cuda.synchronize()
+            for h in hs:
+                assert torch.ops.akap.car_error(h) == 0, "flag wait timed out"
+            exp = _ref_sum(xs)
+            for r in range(world):
+                assert torch.equal(outs[r], outs[0]), "ranks disagree"
+            err = (outs[0].float() - exp.float()).abs().max().item()
+            assert err <= 0.02 * world, err
+    finally:
+        torch.cuda.synchronize()
+        for h in hs:
+            torch.ops.akap.car_destroy(h)
+
+
+def test_custom_allreduce_two_streams():
+    """Two ranks as separate launches on separate HIP streams (the production launch)."""
+    ops.load_native(required=True)
+    world, n = 2, 40000
+    hs = [torch.ops.akap.car_create(0, r, world, 1 << 16) for r in range(world)]
+    try:
+        for h in hs:
+            torch.ops.akap.car_link_local(h, hs)
+        streams = [torch.cuda.Stream() for _ in range(world)]
+        for it in range(3):
+            xs = [torch.randn(n, dtype=torch.bfloat16, device=DEV) for _ in range(world)]
+            outs = [torch.empty_like(x) for x in xs]
+            torch.cuda.synchronize()
+            for r in range(world):
+                with torch.cuda.stream(streams[r]):
+                    torch.ops.akap.car_all_reduce(hs[r], xs[r], outs[r], False)
+            torch.cuda.synchronize()
+            assert all(torch.ops.akap.car_error(h) == 0 for h in hs)
+            assert torch.equal(outs[0], outs[1])
+            assert (outs[0].float() - _ref_sum(xs).float()).abs().max().item() <= 0.05
+    finally:
+        torch.cuda.synchronize()
+        for h in hs:
+            torch.ops.akap.car_destroy(h)
+
+
+def test_custom_allreduce_graph_replay():
+    """Captured once, replayed several times: the device-side epochs must advance."""
+    ops.load_native(required=True)
+    world, n = 4, 8192
+    hs = [torch.ops.akap.car_create(0, r, world, 1 << 14) for r in range(world)]
+    try:
+        for h in hs:
+            torch.ops.akap.car_link_local(h, hs)
+        xs = [torch.randn(n, dtype=torch.bfloat16, device=DEV) for _ in range(world)]
+        outs = [torch.empty_like(x) for x in xs]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            torch.ops.akap.car_all_reduce_multi(hs, xs, outs, True)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            torch.ops.akap.car_all_reduce_multi(hs, xs, outs, True)
+        for it in range(4):
+            for x in xs:
+                x.copy_(torch.randn(n, dtype=torch.bfloat16, device=DEV))
+            g.replay()
+            torch.cuda.synchronize()
+            assert all(torch.ops.akap.car_error(h) == 0 for h in hs)
+            assert (outs[2].float() - _ref_sum(xs).float()).abs().max().item() <= 0.1
+    finally:
+        torch.cuda.synchronize()
+        for h in hs:
+            torch.ops.akap.car_destroy(h)
+
+
+def test_custom_allreduce_in_place():
+    ops.load_native(required=True)
+    world, n = 2, 2048
+    hs = [torch.ops.akap.car_create(0, r, world, 4096) for r in range(world)]
+    try:
+        for h in hs:
+            torch.ops.akap.car_link_local(h, hs)
+        xs = [torch.randn(n, dtype=torch.bfloat16, device=DEV) for _ in range(world)]
+        exp = _ref_sum(xs)
+        torch.ops.akap.car_all_reduce_multi(hs, xs, xs, False)
+        torch.cuda.synchronize()
+        assert torch.ops.akap.car_error(hs[0]) == 0
+        assert (xs[0].float() - exp.float()).abs().max().item() <= 0.05
+        assert torch.equal(xs[0], xs[1])
+    finally:
+        for h in hs:
+            torch.ops.akap.car_destroy(h)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ipc_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from aws_k8s_ansible_provisioner_amd.parallel.custom_allreduce import CustomAllReduce
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        car = CustomAllReduce(group=None, device=torch.device("cuda", 0), max_bytes=1 << 20)
+        res = []
+        for it in range(3):
+            g = torch.Generator().manual_seed(10 * it + rank)
+            x = torch.randn(20000, generator=g).to(torch.bfloat16)
+            y = car.all_reduce(x.to(DEV).contiguous())
+            torch.cuda.synchronize()
+            res.append(y.cpu())
+        err = car.error()
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+        q.put((rank, err, [r.float().numpy() for r in res]))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e), None))
+
+
+def test_custom_allreduce_ipc_two_processes():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        rank, err, res = q.get(timeout=240)
+        out[rank] = (err, res)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert out[r][0] == 0, out[r][0]
+    for it in range(3):
+        xs = [torch.randn(20000, generator=torch.Generator().manual_seed(10 * it + r))
+              .to(torch.bfloat16) for r in range(2)]
+        exp = _ref_sum(xs).float().numpy()
+        import numpy as np
+        assert np.array_equal(out[0][1][it], out[1][1][it])
+        assert np.abs(out[0][1][it] - exp).max() <= 0.05
