@@ -27,6 +27,8 @@ from ..utils import chat_template
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 TEMPLATES = os.path.join(ROOT, "deploy", "templates")
+OTEL_TRACES_ENDPOINT = ("http://otel-metrics-collector-collector.observability.svc"
+                        ".cluster.local:4318")
 ORDER = ["base.yaml.j2", "engines.yaml.j2", "gateway.yaml.j2", "gpu-exporter.yaml.j2"]
 
 
@@ -36,6 +38,8 @@ def load_values(path: str) -> dict:
     v.setdefault("engines", [{"role": "both", "replicas": 1, "gpusPerPod": 1,
                               "tensorParallel": 1}])
     v.setdefault("gateway", {"replicas": 1, "pdThresholdChars": 2048})
+    # OTLP/HTTP traces -> the OTel collector DaemonSet of otel-observability-setup.yaml
+    v.setdefault("tracing", {"endpoint": OTEL_TRACES_ENDPOINT})
     return v
 
 

@@ -15,6 +15,7 @@ import numpy as np
 
 from .. import _runtime_loader
 from ..models.config import ModelConfig, get_config
+from ..utils import tracing
 from ..utils.metrics import EngineMetrics
 from ..utils.tokenizer import get_tokenizer
 from .config import EngineConfig, SamplingParams
@@ -40,6 +41,7 @@ class RequestState:
     text: str = ""
     stream: bool = False
     hold_kv: bool = False
+    traceparent: Optional[str] = None
 
 
 @dataclasses.dataclass
@@ -93,7 +95,8 @@ class LLMEngine:
     def add_request(self, req_id: Optional[str], prompt: Union[str, list, None],
                     params: Optional[SamplingParams] = None,
                     prompt_ids: Optional[list] = None, stream: bool = False,
-                    kv_transfer_params: Optional[dict] = None) -> str:
+                    kv_transfer_params: Optional[dict] = None,
+                    traceparent: Optional[str] = None) -> str:
         """Queue a request.  stream=True reports every token (server SSE); otherwise the
         engine reports only the first token (TTFT) and the finished output."""
         params = (params or SamplingParams()).normalized()
@@ -119,6 +122,7 @@ class LLMEngine:
                           params, time.time())
         st.stream = stream or bool(params.stop)
         st.hold_kv = hold
+        st.traceparent = traceparent
         with self._lock:
             self.sched.add_request(iid, prompt_ids, max_tokens, params.min_tokens,
                                    params.ignore_eos, list(params.stop_token_ids),
@@ -271,6 +275,15 @@ class LLMEngine:
                     m.tpot.observe((now - st.first_token_time) / (n - 1), model_name=name)
                 info_r = self.sched.request_info(iid)
                 cached = info_r["num_cached"] if info_r else 0
+                tr = tracing.get_tracer()
+                if tr is not None:
+                    tracing.record_request(
+                        tr, req_id=st.req_id, model=name, arrival=st.arrival,
+                        first_token=st.first_token_time, finish=now,
+                        prompt_tokens=len(st.prompt_ids), completion_tokens=n,
+                        finish_reason=reason, max_tokens=st.params.max_tokens,
+                        temperature=st.params.temperature, top_p=st.params.top_p,
+                        traceparent=st.traceparent, cached_tokens=cached)
                 with self._lock:
                     self.sched.release(iid)
                     self.reqs.pop(iid, None)

@@ -19,6 +19,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from ..utils import profiling
 from .. import ops
 from ..models.config import ModelConfig
 from ..models.transformer import AttnBatch, DecoderLM
@@ -219,7 +220,12 @@ class ModelRunner:
         return self.out_tokens[:B]
 
     def execute(self, info: dict) -> np.ndarray:
-        toks = self.execute_prefill(info) if info["is_prefill"] else self.execute_decode(info)
+        if info["is_prefill"]:
+            with profiling.phase("akap.prefill"):
+                toks = self.execute_prefill(info)
+        else:
+            with profiling.phase("akap.decode"):
+                toks = self.execute_decode(info)
         return toks.to("cpu").numpy()
 
     # ------------------------------------------------------------------ graphs

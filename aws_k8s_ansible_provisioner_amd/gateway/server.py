@@ -19,6 +19,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import os
 import socket
 import time
 from typing import Optional
@@ -27,6 +28,7 @@ from urllib.parse import urlparse
 import aiohttp
 from aiohttp import web
 
+from ..utils import tracing
 from ..utils.metrics import Counter, Gauge, Histogram, LAT_BUCKETS, Registry
 from .picker import Endpoint, EndpointPicker, PickerConfig, parse_prometheus
 
@@ -117,10 +119,10 @@ class Gateway:
         return p if isinstance(p, str) else json.dumps(p)
 
     async def _forward(self, request: web.Request, ep: Endpoint, path: str, body: dict,
-                       stream: bool) -> web.StreamResponse:
+                       stream: bool, headers: Optional[dict] = None) -> web.StreamResponse:
         ep.inflight += 1
         try:
-            async with self.session.post(ep.url + path, json=body) as up:
+            async with self.session.post(ep.url + path, json=body, headers=headers) as up:
                 if not stream or up.status != 200:
                     data = await up.read()
                     return web.Response(body=data, status=up.status,
@@ -136,6 +138,14 @@ class Gateway:
             ep.inflight -= 1
 
     async def handle_generate(self, request: web.Request) -> web.StreamResponse:
+        with tracing.Span("gateway.route", request.headers.get("traceparent"),
+                          attributes={"http.route": request.path}) as span:
+            resp = await self._route(request, span)
+            span.attributes["http.status_code"] = resp.status
+            span.error = resp.status >= 500
+            return resp
+
+    async def _route(self, request: web.Request, span) -> web.StreamResponse:
         t0 = time.time()
         path = request.path
         try:
@@ -144,6 +154,7 @@ class Gateway:
             return web.json_response({"object": "error", "message": "invalid JSON"}, status=400)
         stream = bool(body.get("stream"))
         text = self._prompt_text(body)
+        headers = {"traceparent": span.traceparent}
         tried: set[str] = set()
         for attempt in range(2):
             pre, dec = self.picker.pick_pd(text)
@@ -153,11 +164,14 @@ class Gateway:
                 if not cands:
                     break
                 dec = cands[0]
+            span.attributes["akap.endpoint"] = dec.url
+            span.attributes["akap.attempt"] = attempt
             try:
                 if pre is not None:
-                    body = await self._prefill_remote(pre, path, body)
+                    span.attributes["akap.prefill_endpoint"] = pre.url
+                    body = await self._prefill_remote(pre, path, body, headers)
                     self.m_pd.inc()
-                resp = await self._forward(request, dec, path, body, stream)
+                resp = await self._forward(request, dec, path, body, stream, headers)
                 self.m_req.inc(endpoint=dec.url, code=str(resp.status), route=path)
                 self.m_lat.observe(time.time() - t0, route=path)
                 return resp
@@ -168,7 +182,8 @@ class Gateway:
         return web.json_response({"object": "error", "message": "no healthy model server",
                                   "type": "ServiceUnavailable"}, status=503)
 
-    async def _prefill_remote(self, pre: Endpoint, path: str, body: dict) -> dict:
+    async def _prefill_remote(self, pre: Endpoint, path: str, body: dict,
+                              headers: Optional[dict] = None) -> dict:
         """P/D step 1: prefill on `pre` (1 token), keep its KV for the decode pod."""
         pbody = dict(body)
         pbody["max_tokens"] = 1
@@ -177,7 +192,7 @@ class Gateway:
         pbody["kv_transfer_params"] = {"do_remote_decode": True}
         pre.inflight += 1
         try:
-            async with self.session.post(pre.url + path, json=pbody) as r:
+            async with self.session.post(pre.url + path, json=pbody, headers=headers) as r:
                 j = await r.json()
         finally:
             pre.inflight -= 1
@@ -256,7 +271,10 @@ def main(argv=None) -> None:
     ap.add_argument("--scrape-interval", type=float, default=1.0)
     ap.add_argument("--pd-threshold-chars", type=int, default=512)
     ap.add_argument("--w-prefix", type=float, default=2.0)
+    ap.add_argument("--otlp-traces-endpoint", default=None)
     a = ap.parse_args(argv)
+    tracing.configure(a.otlp_traces_endpoint, service_name=os.environ.get(
+        "OTEL_SERVICE_NAME", "akap-gateway"))
     cfg = PickerConfig(pd_threshold_chars=a.pd_threshold_chars, w_prefix=a.w_prefix)
     gw = Gateway(_parse_targets(a.endpoints), _parse_dns(a.dns), cfg, a.scrape_interval)
     web.run_app(gw.app(), host=a.host, port=a.port, access_log=None)

@@ -24,7 +24,7 @@ from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 
 from .. import __version__
 from ..engine.config import EngineConfig, SamplingParams
-from ..utils import chat_template
+from ..utils import chat_template, tracing
 from .async_engine import AsyncEngine, EngineDeadError
 
 
@@ -80,10 +80,11 @@ class OpenAIServer:
             return _err(404, f"The model `{m}` does not exist.", "NotFoundError")
         return None
 
-    async def _collect(self, prompt, sp: SamplingParams, rid: str, prompt_ids=None, kvp=None):
+    async def _collect(self, prompt, sp: SamplingParams, rid: str, prompt_ids=None, kvp=None,
+                       tp=None):
         final = None
         async for o in self.ae.generate(prompt, sp, rid, prompt_ids=prompt_ids, stream=False,
-                                        kv_transfer_params=kvp):
+                                        kv_transfer_params=kvp, traceparent=tp):
             final = o
         return final
 
@@ -172,11 +173,13 @@ class OpenAIServer:
                 return _err(400, str(e))
             cid = f"cmpl-{uuid.uuid4().hex}"
             created = int(time.time())
+            tp = req.headers.get("traceparent")
             if body.get("stream"):
                 if len(prompts) != 1 or sp.n != 1:
                     return _err(400, "streaming supports a single prompt with n=1")
                 return StreamingResponse(self._stream_completion(cid, created, prompts[0], sp,
-                                                                 body), media_type="text/event-stream")
+                                                                 body, tp),
+                                         media_type="text/event-stream")
             try:
                 jobs = []
                 for i, p in enumerate(prompts):
@@ -184,7 +187,7 @@ class OpenAIServer:
                         pid = p if isinstance(p, list) else None
                         jobs.append(self._collect(p if isinstance(p, str) else None, sp,
                                                   f"{cid}-{i}-{j}", prompt_ids=pid,
-                                                  kvp=body.get("kv_transfer_params")))
+                                                  kvp=body.get("kv_transfer_params"), tp=tp))
                 outs = await asyncio.gather(*jobs)
             except EngineDeadError as e:
                 return _err(500, "engine failure: " + str(e)[:200], "InternalServerError")
@@ -235,12 +238,14 @@ class OpenAIServer:
                 return _err(400, f"chat template error: {e}")
             cid = f"chatcmpl-{uuid.uuid4().hex}"
             created = int(time.time())
+            tp = req.headers.get("traceparent")
             if body.get("stream"):
-                return StreamingResponse(self._stream_chat(cid, created, prompt, sp, body),
+                return StreamingResponse(self._stream_chat(cid, created, prompt, sp, body, tp),
                                          media_type="text/event-stream")
             try:
                 outs = await asyncio.gather(*[self._collect(prompt, sp, f"{cid}-{j}",
-                                                            kvp=body.get("kv_transfer_params"))
+                                                            kvp=body.get("kv_transfer_params"),
+                                                            tp=tp)
                                               for j in range(sp.n)])
             except EngineDeadError as e:
                 return _err(500, "engine failure: " + str(e)[:200], "InternalServerError")
@@ -264,13 +269,14 @@ class OpenAIServer:
         return app
 
     # ------------------------------------------------------------------ SSE
-    async def _stream_completion(self, cid, created, prompt, sp, body):
+    async def _stream_completion(self, cid, created, prompt, sp, body, tp=None):
         pid = prompt if isinstance(prompt, list) else None
         ptext = prompt if isinstance(prompt, str) else None
         n_out, n_prompt = 0, 0
         try:
             async for o in self.ae.generate(ptext, sp, cid, prompt_ids=pid, stream=True,
-                                            kv_transfer_params=body.get("kv_transfer_params")):
+                                            kv_transfer_params=body.get("kv_transfer_params"),
+                                            traceparent=tp):
                 n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
                 chunk = {"id": cid, "object": "text_completion", "created": created,
                          "model": self.name, "choices": [{
@@ -286,7 +292,7 @@ class OpenAIServer:
             yield f"data: {json.dumps(u)}\n\n"
         yield "data: [DONE]\n\n"
 
-    async def _stream_chat(self, cid, created, prompt, sp, body):
+    async def _stream_chat(self, cid, created, prompt, sp, body, tp=None):
         first = {"id": cid, "object": "chat.completion.chunk", "created": created,
                  "model": self.name, "choices": [{"index": 0, "delta": {"role": "assistant",
                                                                         "content": ""},
@@ -295,7 +301,8 @@ class OpenAIServer:
         n_out, n_prompt = 0, 0
         try:
             async for o in self.ae.generate(prompt, sp, cid, stream=True,
-                                            kv_transfer_params=body.get("kv_transfer_params")):
+                                            kv_transfer_params=body.get("kv_transfer_params"),
+                                            traceparent=tp):
                 n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
                 chunk = {"id": cid, "object": "chat.completion.chunk", "created": created,
                          "model": self.name, "choices": [{
@@ -334,6 +341,9 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--load-format", default="random", choices=["random", "safetensors"])
     ap.add_argument("--weights-path", default=None)
     ap.add_argument("--kv-role", default="both", choices=["both", "prefill", "decode"])
+    ap.add_argument("--otlp-traces-endpoint", default=None,
+                    help="OTLP/HTTP collector (e.g. http://otel-collector:4318); also read "
+                         "from OTEL_EXPORTER_OTLP_TRACES_ENDPOINT")
     return ap
 
 
@@ -366,6 +376,8 @@ def main(argv: Optional[list] = None) -> None:
 
     a = make_parser().parse_args(argv)
     ecfg = engine_config_from_args(a)
+    tracing.configure(a.otlp_traces_endpoint, service_name=os.environ.get(
+        "OTEL_SERVICE_NAME", f"akap-engine-{a.kv_role}"))
     if a.tensor_parallel_size > 1:
         from ..parallel.tp_worker import serve_tp
 

@@ -74,8 +74,8 @@ class AsyncEngine:
 
     async def generate(self, prompt, params: SamplingParams, req_id: str,
                        prompt_ids: Optional[list] = None, stream: bool = False,
-                       kv_transfer_params: Optional[dict] = None
-                       ) -> AsyncIterator[RequestOutput]:
+                       kv_transfer_params: Optional[dict] = None,
+                       traceparent: Optional[str] = None) -> AsyncIterator[RequestOutput]:
         if self.dead is not None:
             raise EngineDeadError(self.dead)
         q: asyncio.Queue = asyncio.Queue()
@@ -88,7 +88,8 @@ class AsyncEngine:
                     return
             else:
                 self.engine.add_request(req_id, prompt, params, prompt_ids=prompt_ids,
-                                        stream=stream, kv_transfer_params=kv_transfer_params)
+                                        stream=stream, kv_transfer_params=kv_transfer_params,
+                                        traceparent=traceparent)
             self._wake.set()
             while True:
                 o = await q.get()
