@@ -23,6 +23,12 @@ class EngineDeadError(RuntimeError):
     pass
 
 
+class KVTransferError(RuntimeError):
+    """P/D: the prefill pod could not hand the request's KV over (pod gone, timeout,
+    block-count mismatch).  The decode side frees its reserved blocks and fails the
+    request; the gateway may retry it monolithically."""
+
+
 class AsyncEngine:
     def __init__(self, engine: LLMEngine, step_hook=None):
         self.engine = engine
@@ -67,8 +73,10 @@ class AsyncEngine:
                     self.step_hook(outs)
                 if outs:
                     self._deliver(outs)
-        except Exception:  # engine failure: fail every waiter, mark unhealthy
-            self.dead = traceback.format_exc()
+        except Exception as e:  # engine failure: fail every waiter, mark unhealthy
+            self.dead_traceback = traceback.format_exc()
+            self.dead = f"{type(e).__name__}: {e}"
+            print("[engine] step loop died:\n" + self.dead_traceback, flush=True)
             for q in list(self.queues.values()):
                 self.loop.call_soon_threadsafe(q.put_nowait, EngineDeadError(self.dead))
 
@@ -134,7 +142,10 @@ class AsyncEngine:
             self.kv_agent.recv_blocks(blocks, int(kvp["remote_rank"]))
             eng.activate(iid)
 
-        await loop.run_in_executor(None, pull)
+        try:
+            await loop.run_in_executor(None, pull)
+        except (OSError, ValueError, KeyError, RuntimeError) as e:
+            raise KVTransferError(f"KV transfer from {kvp.get('remote_url')} failed: {e}") from e
         if stream:  # the first token was produced remotely: deliver it first
             t = eng.tokenizer.decode_token(first)
             self.queues[req_id].put_nowait(RequestOutput(req_id, prompt_ids, [first], [first],
