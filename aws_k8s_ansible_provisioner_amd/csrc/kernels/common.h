@@ -90,4 +90,18 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint32_t a, uint32_t b
   return ((hash3(seed, a, b) >> 8) + 1) * (1.0f / 16777216.0f);
 }
 
+// ---- paged K cache layout (D = 128) --------------------------------------------------
+// Within one (block, kv head) of BS tokens (BS % 32 == 0), each 32-token chunk is stored as
+// [tile tt (2)][k-step cc (4)][row r (16)][32 dims]: the exact operand order of the
+// attention kernels' S^T = K.Q^T MFMA tiles, whose row r of tile tt is chunk token
+// 8*(r>>2) + 4*tt + (r&3).  Element offset of (token `off`, dim 0) within the block-head;
+// dim d lives at + (d/32)*512 + d%32.
+__host__ __device__ __forceinline__ int k_swz_offset(int off) {
+  const int o = off & 31;
+  const int tt = (o >> 2) & 1;
+  const int r = ((o >> 3) << 2) | (o & 3);
+  return (off >> 5) * 32 * 128 + tt * 16 * 128 + r * 32;
+}
+__host__ __device__ __forceinline__ int k_dim_offset(int d) { return (d >> 5) * 512 + (d & 31); }
+
 }  // namespace akap

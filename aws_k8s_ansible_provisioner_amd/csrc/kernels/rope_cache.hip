@@ -8,8 +8,9 @@
 // from a host-precomputed fp32 table [max_pos, D] (cos | sin), no on-device trig.
 //
 // Paged cache layouts (MI355X-first, chosen so the attention kernels can issue
-// 16-byte MFMA-operand loads with no transpose):
-//   K cache: [num_blocks, Hkv, BS, D]   (token-major inside a block)
+// 16-byte MFMA-operand loads with no transpose, 1 KiB contiguous per load instruction):
+//   K cache: [num_blocks, Hkv, BS, D] shape, MFMA-fragment order inside each 32-token
+//            chunk (k_swz_offset in common.h)
 //   V cache: [num_blocks, Hkv, BS/8, D, 8] (8-token groups, dim-major inside a group):
 //            the attention kernel's V^T operand (one dim, 8 consecutive tokens) is one
 //            16-byte load, and a token's 128 dims land in 16-byte-strided slots of one
@@ -88,9 +89,9 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
   const int off = (int)(slot % BS);
   if (is_k) {
     const int kh = h - Hq;
-    bf16* dst = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D;
-    *reinterpret_cast<bf16x4*>(dst + 4 * li) = oa;
-    *reinterpret_cast<bf16x4*>(dst + HALF + 4 * li) = ob;
+    bf16* dst = k_cache + ((size_t)blk * Hkv + kh) * BS * D + k_swz_offset(off);
+    *reinterpret_cast<bf16x4*>(dst + k_dim_offset(4 * li)) = oa;
+    *reinterpret_cast<bf16x4*>(dst + k_dim_offset(HALF + 4 * li)) = ob;
   } else {
     const int vh = h - Hq - Hkv;
     bf16* dst = v_cache + ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + (off & 7);
@@ -116,10 +117,6 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
     qk_norm_rope_cache_kernel<128><<<grid, 256, 0, s>>>(
         (const bf16*)qkv, qkv_stride, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions,
         slots, cos_sin, (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope);
-  } else if (D == 64) {
-    qk_norm_rope_cache_kernel<64><<<grid, 256, 0, s>>>(
-        (const bf16*)qkv, qkv_stride, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions,
-        slots, cos_sin, (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope);
   }
 }
 
@@ -140,7 +137,8 @@ __global__ __launch_bounds__(256) void reshape_and_cache_kernel(
   const int off = (int)(slot % BS);
   bf16x8 kv = *reinterpret_cast<const bf16x8*>(k + ((size_t)t * Hkv + h) * D + 8 * li);
   bf16x8 vv = *reinterpret_cast<const bf16x8*>(v + ((size_t)t * Hkv + h) * D + 8 * li);
-  *reinterpret_cast<bf16x8*>(k_cache + (((size_t)blk * Hkv + h) * BS + off) * D + 8 * li) = kv;
+  *reinterpret_cast<bf16x8*>(k_cache + ((size_t)blk * Hkv + h) * BS * D + k_swz_offset(off) +
+                             k_dim_offset(8 * li)) = kv;
   bf16* vd = v_cache + ((size_t)blk * Hkv + h) * D * BS + (off >> 3) * D * 8 + (off & 7);
 #pragma unroll
   for (int j = 0; j < 8; ++j) vd[(size_t)(8 * li + j) * 8] = vv[j];
@@ -155,10 +153,6 @@ void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void*
     reshape_and_cache_kernel<128><<<grid, 256, 0, s>>>((const bf16*)k, (const bf16*)v,
                                                       (bf16*)k_cache, (bf16*)v_cache, slots, T,
                                                       Hkv, BS);
-  else if (D == 64)
-    reshape_and_cache_kernel<64><<<grid, 256, 0, s>>>((const bf16*)k, (const bf16*)v,
-                                                     (bf16*)k_cache, (bf16*)v_cache, slots, T,
-                                                     Hkv, BS);
 }
 
 }  // namespace akap

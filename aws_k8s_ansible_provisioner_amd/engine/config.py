@@ -29,6 +29,11 @@ class EngineConfig:
     init_std: float = 0.02                    # random-init weight scale
     shard_init: str = "per_rank"              # "per_rank" | "full" (identical logical weights for any TP)
 
+    def __post_init__(self) -> None:
+        # the K cache stores each 32-token chunk in MFMA-fragment order (ops/reference.py)
+        if self.block_size <= 0 or self.block_size % 32:
+            raise ValueError(f"block_size must be a multiple of 32, got {self.block_size}")
+
     def resolved_device(self) -> str:
         if self.device != "auto":
             return self.device

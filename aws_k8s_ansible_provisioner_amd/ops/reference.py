@@ -1,7 +1,11 @@
 """Plain-PyTorch (fp32-accumulating) reference implementations of every kernel.
 
 They define the semantics the HIP kernels are tested against and serve the CPU
-engine path.  Cache layouts: K [NB, Hkv, BS, D], V [NB, Hkv, BS/8, D, 8].
+engine path.  Cache layouts (BS % 32 == 0, D = 128 on the GPU path):
+  K [NB, Hkv, BS, D] shape, stored MFMA-fragment ordered inside each 32-token chunk:
+    [BS/32][tile tt 2][k-step D/32][row r 16][32 dims], chunk token o = 8*(r>>2)+4*tt+(r&3)
+    (csrc/kernels/common.h k_swz_offset) -- use k_tokens()/write_k() to index it;
+  V [NB, Hkv, BS/8, D, 8] (8-token groups, dim-major).
 """
 from __future__ import annotations
 
@@ -55,6 +59,39 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
     return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
 
 
+def k_swz(o: int) -> tuple[int, int, int]:
+    """Token offset within a block -> (32-token chunk, tile tt, row r) of the K layout."""
+    c, oo = divmod(o, 32)
+    return c, (oo >> 2) & 1, ((oo >> 3) << 2) | (oo & 3)
+
+
+# position (tt * 16 + r) of chunk token o, for o = 0..31
+K_CHUNK_POS = [k_swz(o)[1] * 16 + k_swz(o)[2] for o in range(32)]
+
+
+def k_blocks_view(k_cache: torch.Tensor) -> torch.Tensor:
+    NB, H, BS, D = k_cache.shape
+    assert BS % 32 == 0 and D % 32 == 0, "K cache layout needs BS % 32 == 0"
+    return k_cache.view(NB, H, BS // 32, 2, D // 32, 16, 32)
+
+
+def write_k(k_cache: torch.Tensor, b: int, o: int, val: torch.Tensor) -> None:
+    """k_cache[block b, :, token o, :] = val [Hkv, D] in the swizzled layout."""
+    c, tt, r = k_swz(o)
+    H, D = val.shape
+    k_blocks_view(k_cache)[b, :, c, tt, :, r, :] = val.to(k_cache.dtype).view(H, D // 32, 32)
+
+
+def k_tokens(k_cache: torch.Tensor, blocks: torch.Tensor) -> torch.Tensor:
+    """Logical K of `blocks` in token order: [len(blocks) * BS, Hkv, D]."""
+    NB, H, BS, D = k_cache.shape
+    v = k_blocks_view(k_cache)[blocks]                       # [nb, H, C, 2, D/32, 16, 32]
+    nb = v.shape[0]
+    t = v.permute(0, 2, 3, 5, 1, 4, 6).reshape(nb, BS // 32, 32, H, D)  # pos = tt*16 + r
+    t = t[:, :, K_CHUNK_POS]
+    return t.reshape(nb * BS, H, D)
+
+
 def write_cache(k: torch.Tensor, v: torch.Tensor, k_cache, v_cache, slots) -> None:
     BS = k_cache.shape[2]
     for t in range(k.shape[0]):
@@ -62,7 +99,7 @@ def write_cache(k: torch.Tensor, v: torch.Tensor, k_cache, v_cache, slots) -> No
         if s < 0:
             continue
         b, o = divmod(s, BS)
-        k_cache[b, :, o, :] = k[t].to(k_cache.dtype)
+        write_k(k_cache, b, o, k[t])
         v_cache[b, :, o // 8, :, o % 8] = v[t].to(v_cache.dtype)
 
 
@@ -94,7 +131,7 @@ def gather_kv(k_cache, v_cache, block_table, kv_len: int):
     BS = k_cache.shape[2]
     nb = (kv_len + BS - 1) // BS
     blocks = block_table[:nb].long()
-    K = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * BS, k_cache.shape[1], -1)[:kv_len]
+    K = k_tokens(k_cache, blocks)[:kv_len]
     # [nb, Hkv, BS/8, D, 8] -> [nb, BS/8, 8, Hkv, D] -> tokens
     V = v_cache[blocks].permute(0, 2, 4, 1, 3).reshape(nb * BS, v_cache.shape[1], -1)[:kv_len]
     return K, V

@@ -21,11 +21,13 @@ def main():
     ap.add_argument("--hkv", type=int, default=8)
     ap.add_argument("--bs", type=int, default=32)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--spread", type=int, default=128)
+    ap.add_argument("--parts", default="1,2,4,8,16")
     a = ap.parse_args()
     ops.load_native(required=True)
     dev = "cuda"
     B, D, bs = a.B, 128, a.bs
-    lens = torch.randint(a.ctx - 128, a.ctx + 129, (B,), dtype=torch.int32)
+    lens = torch.randint(a.ctx - a.spread, a.ctx + a.spread + 1, (B,), dtype=torch.int32)
     nb = [math.ceil(int(x) / bs) for x in lens]
     NB = sum(nb) + 8
     perm = torch.randperm(NB)
@@ -42,8 +44,9 @@ def main():
     bt, lens_d = bt.to(dev), lens.to(dev)
     G = a.hq // a.hkv
     kv_bytes = int(lens.sum()) * a.hkv * D * 2 * 2
-    flags = os.environ.get("AKAP_ATTN_FLAGS", "0")
-    for parts, ps in [(1, 4096), (2, 2048), (4, 1024), (8, 512), (16, 256)]:
+    flags = os.environ.get("AKAP_ATTN_FLAGS", "default")
+    for parts in [int(x) for x in a.parts.split(",")]:
+        ps = 4096 // parts
         ws = ops.decode_workspace(B, a.hkv, G, parts, dev)
         f = lambda: ops.paged_attention_decode(out, q, kc, vc, bt, lens_d, G, 1 / math.sqrt(D),  # noqa
                                                workspace=ws, num_parts=parts, part_size=ps)

@@ -11,7 +11,7 @@ from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logit
 
 def _engine(model, **kw):
     cfg = dict(model=model, device="cpu", max_model_len=256, max_num_seqs=8,
-               max_num_batched_tokens=32, block_size=16, num_gpu_blocks=96, init_std=0.15)
+               max_num_batched_tokens=32, block_size=32, num_gpu_blocks=96, init_std=0.15)
     cfg.update(kw)
     return LLMEngine(EngineConfig(**cfg), log=lambda *a: None)
 
@@ -28,7 +28,7 @@ def _near_argmax(eng, prompt, out, tol=0.1):
 @pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama", "tiny-mixtral"])
 def test_engine_vs_dense_reference(model):
     eng = _engine(model)
-    prompts = [list(range(5, 24)), [100, 101], [7, 8, 9] * 14, list(range(5, 24))]
+    prompts = [list(range(5, 45)), [100, 101], [7, 8, 9] * 14, list(range(5, 45))]
     outs = eng.generate(None, SamplingParams(max_tokens=8, temperature=0, ignore_eos=True),
                         prompt_ids=prompts)
     assert [len(o.output_ids) for o in outs] == [8] * 4

@@ -19,7 +19,7 @@ from aws_k8s_ansible_provisioner_amd.server.api_server import build_app
 
 def _cfg(**kw):
     base = dict(model="tiny-qwen3", served_model_name="m", device="cpu", max_model_len=128,
-                max_num_seqs=4, max_num_batched_tokens=64, block_size=16, num_gpu_blocks=64)
+                max_num_seqs=4, max_num_batched_tokens=64, block_size=32, num_gpu_blocks=64)
     base.update(kw)
     return EngineConfig(**base)
 

@@ -87,7 +87,7 @@ def two_engines():
     for i in range(2):
         ecfg = EngineConfig(model="tiny-qwen3", served_model_name=MODEL, device="cpu",
                             max_model_len=256, max_num_seqs=8, max_num_batched_tokens=64,
-                            block_size=16, num_gpu_blocks=128, seed=i)
+                            block_size=32, num_gpu_blocks=128, seed=i)
         app, _ = build_app(ecfg)
         port = _free_port()
         t = _Uvicorn(app, port)

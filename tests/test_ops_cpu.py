@@ -3,6 +3,7 @@ and of the Python-side glue around them.  The GPU kernels are compared against t
 same references in tests/test_kernels_gpu.py."""
 import math
 
+import pytest
 import torch
 
 from aws_k8s_ansible_provisioner_amd import ops
@@ -56,8 +57,8 @@ def test_moe_capacity_covers_worst_case():
 
 def test_paged_attention_reference_vs_dense_causal():
     torch.manual_seed(1)
-    Hq, Hkv, D, BS = 4, 2, 64, 16
-    lens = [5, 23]
+    Hq, Hkv, D, BS = 4, 2, 64, 32
+    lens = [5, 53]
     nb = 8
     kc = torch.zeros(nb, Hkv, BS, D)
     vc = torch.zeros(nb, Hkv, BS // 8, D, 8)
@@ -85,7 +86,7 @@ def test_paged_attention_reference_vs_dense_causal():
 
 
 def test_v_cache_group_layout_roundtrip():
-    BS, D, Hkv = 32, 16, 2
+    BS, D, Hkv = 32, 32, 2
     kc = torch.zeros(4, Hkv, BS, D)
     vc = torch.zeros(4, Hkv, BS // 8, D, 8)
     k = torch.randn(40, Hkv, D)
@@ -96,6 +97,33 @@ def test_v_cache_group_layout_roundtrip():
     assert torch.equal(K, k) and torch.equal(V, v)
     # token o of block b sits at v_cache[b, h, o // 8, :, o % 8]
     assert torch.equal(vc[1, 0, 1, :, 3], v[11, 0])
+
+
+def test_k_cache_fragment_layout():
+    """K is stored [chunk][tile tt][k-step][row r][32 dims] per 32-token chunk, with chunk
+    token o = 8*(r>>2) + 4*tt + (r&3) (the decode kernel's MFMA operand order)."""
+    BS, D, H = 64, 128, 2
+    kc = torch.zeros(3, H, BS, D)
+    vals = torch.randn(BS, H, D)
+    for o in range(BS):
+        ref.write_k(kc, 1, o, vals[o])
+    flat = kc[1].reshape(H, -1)
+    for o in [0, 3, 4, 5, 9, 31, 32, 45, 63]:
+        c, oo = divmod(o, 32)
+        tt, r = (oo >> 2) & 1, ((oo >> 3) << 2) | (oo & 3)
+        for d in [0, 31, 32, 100, 127]:
+            off = c * 32 * 128 + tt * 2048 + (d // 32) * 512 + r * 32 + d % 32
+            assert flat[0, off] == vals[o, 0, d]
+    assert torch.equal(ref.k_tokens(kc, torch.tensor([1])), vals)
+    # the permutation is a bijection over each chunk
+    assert sorted(ref.K_CHUNK_POS) == list(range(32))
+
+
+def test_block_size_must_be_multiple_of_32():
+    from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig
+    with pytest.raises(ValueError):
+        EngineConfig(block_size=16)
+    EngineConfig(block_size=64)
 
 
 def test_sampler_reference_topk_topp_support():

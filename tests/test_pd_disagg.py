@@ -21,7 +21,7 @@ from aws_k8s_ansible_provisioner_amd.gateway.server import Gateway
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 COMMON = ["--model", "tiny-qwen3", "--device", "cpu", "--max-model-len", "256",
-          "--max-num-seqs", "8", "--max-num-batched-tokens", "64", "--block-size", "16",
+          "--max-num-seqs", "8", "--max-num-batched-tokens", "64", "--block-size", "32",
           "--num-gpu-blocks", "128", "--served-model-name", "Qwen/Qwen3-0.6B"]
 
 
@@ -70,7 +70,7 @@ def test_pd_generation_matches_monolithic(pd_servers):
     pre_url, dec_url = pd_servers
     prompt = "disaggregated prefill and decode over RCCL " * 3
     ref = LLMEngine(EngineConfig(model="tiny-qwen3", device="cpu", max_model_len=256,
-                                 max_num_seqs=8, max_num_batched_tokens=64, block_size=16,
+                                 max_num_seqs=8, max_num_batched_tokens=64, block_size=32,
                                  num_gpu_blocks=128), log=lambda *a: None)
     expect = ref.generate([prompt], SamplingParams(max_tokens=12, temperature=0,
                                                    ignore_eos=True))[0]

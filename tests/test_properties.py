@@ -154,11 +154,11 @@ def test_moe_align_reference_properties(T, E, K, block, seed):
 
 @FAST
 @given(st.integers(1, 6), st.sampled_from([(2, 1), (4, 2), (4, 4), (8, 1)]),
-       st.sampled_from([8, 16, 32]), st.integers(0, 10 ** 6))
+       st.sampled_from([32, 64]), st.integers(0, 10 ** 6))
 def test_paged_attention_reference_block_table_invariance(B, heads, BS, seed):
     """Permuting physical blocks (and the tables with them) must not change the output."""
     Hq, Hkv = heads
-    D = 16
+    D = 32
     g = torch.Generator().manual_seed(seed)
     lens = torch.randint(1, 3 * BS, (B,), generator=g)
     mb = 3

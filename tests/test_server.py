@@ -16,7 +16,7 @@ MODEL = "Qwen/Qwen3-0.6B"
 def client():
     ecfg = EngineConfig(model="tiny-qwen3", served_model_name=MODEL, device="cpu",
                         max_model_len=256, max_num_seqs=8, max_num_batched_tokens=64,
-                        block_size=16, num_gpu_blocks=128, chat_template="default")
+                        block_size=32, num_gpu_blocks=128, chat_template="default")
     app, ae = build_app(ecfg)
     with TestClient(app) as c:
         yield c

@@ -20,7 +20,7 @@ from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, Sampling
 from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
 model = os.environ["MODEL"]
 ecfg = EngineConfig(model=model, device="cpu", max_model_len=256, max_num_seqs=8,
-                    max_num_batched_tokens=32, block_size=16, num_gpu_blocks=96,
+                    max_num_batched_tokens=32, block_size=32, num_gpu_blocks=96,
                     tensor_parallel_size=2, shard_init="full", init_std=0.15)
 eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
 if eng is not None:
@@ -58,7 +58,7 @@ def test_tp2_matches_tp1(model, moe_mode):
     line = [l for l in outs[0][0].splitlines() if l.startswith("RESULT ")][0]
     tp_out = json.loads(line[7:])
     ref = LLMEngine(EngineConfig(model=model, device="cpu", max_model_len=256, max_num_seqs=8,
-                                 max_num_batched_tokens=32, block_size=16, num_gpu_blocks=96,
+                                 max_num_batched_tokens=32, block_size=32, num_gpu_blocks=96,
                                  shard_init="full", init_std=0.15), log=lambda *a: None)
     from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logits
 

@@ -87,7 +87,7 @@ def test_export_batches_and_drops_when_collector_down():
 
 def _engine():
     return LLMEngine(EngineConfig(model="tiny-qwen3", device="cpu", max_model_len=128,
-                                  max_num_seqs=4, max_num_batched_tokens=64, block_size=16,
+                                  max_num_seqs=4, max_num_batched_tokens=64, block_size=32,
                                   num_gpu_blocks=64), log=lambda *a: None)
 
 
@@ -141,7 +141,7 @@ def test_gateway_propagates_trace_to_engine(collector):
 
     ecfg = EngineConfig(model="tiny-qwen3", served_model_name="m", device="cpu",
                         max_model_len=128, max_num_seqs=4, max_num_batched_tokens=64,
-                        block_size=16, num_gpu_blocks=64)
+                        block_size=32, num_gpu_blocks=64)
     app, _ = build_app(ecfg)
     eport = free_port()
     server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=eport, log_level="error"))
