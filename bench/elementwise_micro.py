@@ -24,7 +24,26 @@ slots = torch.randperm(NB * BS, device=dev)[:T]
 cs = ref.rope_cos_sin(4096, D, 1e6, device=dev)
 qw = torch.ones(D, device=dev, dtype=torch.bfloat16)
 gu = torch.randn(T, 6144, device=dev, dtype=torch.bfloat16)
+noslots = torch.full_like(slots, -1)
+# engine-like: 28 layers' caches, each written once per "step" (cold in L2)
+L = 28
+caches = [(torch.zeros(NB, hkv, BS, D, device=dev, dtype=torch.bfloat16),
+           torch.zeros(NB, hkv, BS // 8, D, 8, device=dev, dtype=torch.bfloat16))
+          for _ in range(L)]
+qkvs = [torch.randn(T, (hq + 2 * hkv) * D, device=dev, dtype=torch.bfloat16) for _ in range(L)]
+_layer = [0]
+
+
+def layered():
+    i = _layer[0] = (_layer[0] + 1) % L
+    ops.qk_norm_rope_cache(qkvs[i], q, caches[i][0], caches[i][1], pos, slots, cs, qw, qw, hq,
+                           hkv, 1e-6)
+
+
 fns = {
+    "qk_rope_no_cache_write": lambda: ops.qk_norm_rope_cache(qkv, q, kc, vc, pos, noslots, cs,
+                                                             qw, qw, hq, hkv, 1e-6),
+    "qk_rope_28_layer_caches": layered,
     "rmsnorm": lambda: ops.rms_norm(x, w, 1e-6),
     "fused_add_rmsnorm": lambda: ops.fused_add_rms_norm(x, r, w, 1e-6),
     "qk_norm_rope_cache": lambda: ops.qk_norm_rope_cache(qkv, q, kc, vc, pos, slots, cs, qw, qw,

@@ -1,18 +1,37 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --kernel-trace --stats CSV into markdown (for profiles/)."""
+"""Summarise rocprofv3 --kernel-trace --stats output into markdown (for profiles/).
+
+Accepts either the CSV stats file (``--output-format csv``: *_kernel_stats.csv) or the
+default rocpd SQLite database (*_results.db; per-kernel totals plus VGPR/LDS use)."""
 import csv
+import sqlite3
 import sys
 
 
+def _rows_csv(path):
+    for r in csv.DictReader(open(path)):
+        yield (r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]), None, None)
+
+
+def _rows_db(path):
+    c = sqlite3.connect(path)
+    q = ("select name, count(*), sum(duration), max(vgpr_count + accum_vgpr_count), "
+         "max(lds_size) from kernels group by name order by sum(duration) desc")
+    yield from c.execute(q)
+
+
 def main(path, out=None, title="kernel stats", top=30):
-    rows = list(csv.DictReader(open(path)))
-    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    rows = list(_rows_db(path) if path.endswith(".db") else _rows_csv(path))
+    rows.sort(key=lambda r: -r[2])
+    tot = sum(r[2] for r in rows)
     lines = [f"# {title}", "", f"source: `{path}`  total GPU kernel time {tot/1e6:.1f} ms", "",
-             "| % | total ms | calls | avg us | kernel |", "|---:|---:|---:|---:|---|"]
-    for r in rows[:top]:
-        name = r["Name"].replace("|", "/")[:120]
-        lines.append(f"| {float(r['Percentage']):.2f} | {float(r['TotalDurationNs'])/1e6:.2f} | "
-                     f"{r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | `{name}` |")
+             "| % | total ms | calls | avg us | VGPR | LDS B | kernel |",
+             "|---:|---:|---:|---:|---:|---:|---|"]
+    for name, calls, dur, vgpr, lds in rows[:top]:
+        name = name.replace("|", "/")[:110]
+        lines.append(f"| {100 * dur / tot:.2f} | {dur / 1e6:.2f} | {calls} | "
+                     f"{dur / calls / 1e3:.2f} | {vgpr if vgpr is not None else ''} | "
+                     f"{lds if lds is not None else ''} | `{name}` |")
     text = "\n".join(lines) + "\n"
     if out:
         open(out, "w").write(text)
