@@ -1,0 +1,113 @@
+"""Decode-step anatomy: the marginal cost of each op class inside a real decode step.
+
+Builds the model (random init), a B-sequence decode batch at ~ctx tokens of context, and
+times the captured hipGraph of one decode step (forward + LM head + sampler) with op
+classes knocked out one at a time (replaced by no-ops of the same output shape).  The
+difference to the full step is what that op class really costs in context (cold weights,
+L2 state after the attention stream, clocks), which isolated micro-benchmarks miss.
+
+python bench/decode_anatomy.py [--model qwen3-0.6b] [--B 256] [--ctx 640]
+"""
+import argparse
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aws_k8s_ansible_provisioner_amd import ops  # noqa: E402
+from aws_k8s_ansible_provisioner_amd.models.config import get_config  # noqa: E402
+from aws_k8s_ansible_provisioner_amd.models.transformer import AttnBatch, DecoderLM  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="qwen3-0.6b")
+    ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--ctx", type=int, default=640)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    ops.load_native(required=True)
+    dev = torch.device("cuda", 0)
+    cfg = get_config(a.model)
+    m = DecoderLM(cfg, dev, max_model_len=4096)
+    B, BS = a.B, 32
+    lens = torch.randint(a.ctx - 128, a.ctx + 129, (B,), dtype=torch.int32)
+    nb = [math.ceil(int(x) / BS) for x in lens]
+    NB = sum(nb) + 8
+    kv = m.allocate_kv_cache(NB, BS)
+    kc, vc = m.cache_views(kv, BS)
+    perm = torch.randperm(NB)
+    bt = torch.zeros(B, 4096 // BS, dtype=torch.int32)
+    i = 0
+    for s, n in enumerate(nb):
+        bt[s, :n] = perm[i:i + n].to(torch.int32)
+        i += n
+    pos = (lens - 1).to(torch.int64)
+    slots = torch.tensor([int(bt[s, int(pos[s]) // BS]) * BS + int(pos[s]) % BS
+                          for s in range(B)], dtype=torch.int64)
+    d = lambda t: t.to(dev)  # noqa: E731
+    ws = ops.decode_workspace(B, m.hkv, m.hq // m.hkv, 1, dev)
+    batch = AttnBatch(False, d(pos), d(slots), d(bt), d(lens), d(torch.arange(B + 1,
+                      dtype=torch.int32)), None, None, 1, 4096, ws)
+    ids = torch.randint(0, cfg.vocab_size, (B,), device=dev)
+    temp = torch.zeros(B, device=dev)
+    topk = torch.zeros(B, dtype=torch.int32, device=dev)
+    topp = torch.ones(B, device=dev)
+    seeds = torch.zeros(B, dtype=torch.int64, device=dev)
+    steps = torch.zeros(B, dtype=torch.int32, device=dev)
+
+    def step():
+        h = m.forward(ids, batch, kc, vc)
+        logits = m.compute_logits(h)
+        ops.sample(logits, temp, topk, topp, seeds, steps)
+
+    orig = {k: getattr(ops, k) for k in ("paged_attention_decode", "qk_norm_rope_cache",
+                                          "rms_norm", "fused_add_rms_norm", "silu_and_mul",
+                                          "linear", "sample")}
+    noop = {
+        "attention": {"paged_attention_decode": lambda out, *a_, **k: out},
+        "qk_norm_rope_cache": {"qk_norm_rope_cache": lambda qkv, q_out, *a_, **k: q_out},
+        "norms": {"rms_norm": lambda x, w, eps, out=None: x,
+                  "fused_add_rms_norm": lambda x, r, w, eps, out=None: (x, r)},
+        "silu_and_mul": {"silu_and_mul": lambda x, out=None: x[..., : x.shape[-1] // 2]},
+        "gemms (incl. LM head)": {"linear": lambda x, w, out=None: x.new_empty(x.shape[0],
+                                                                               w.shape[0])},
+        "sampler": {"sample": lambda logits, *a_, **k: (None, None)},
+    }
+
+    def run(name, patch):
+        for k, f in patch.items():
+            setattr(ops, k, f)
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                step()
+            s.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                step()
+            g.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+            e0.record()
+            for _ in range(a.iters):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / a.iters
+        finally:
+            for k, f in orig.items():
+                setattr(ops, k, f)
+
+    full = run("full", {})
+    print(f"{a.model} B={B} ctx~{a.ctx}: full decode step {full * 1000:8.1f} us")
+    for name, patch in noop.items():
+        t = run(name, patch)
+        print(f"  without {name:22s} {t * 1000:8.1f} us   -> costs {(full - t) * 1000:7.1f} us "
+              f"({100 * (full - t) / full:4.1f} %)")
+
+
+if __name__ == "__main__":
+    main()
