@@ -215,9 +215,82 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
 // Decode: one new token per sequence, rows = the G q-heads of one kv head.
 // grid = (num_seqs, Hkv, num_parts); 4 waves split the partition's chunks.
 // ----------------------------------------------------------------------------------
+// Fused decode prologue: rows 0..G-1 = this kv head's G query heads, row G = its key head,
+// row G+1 = its value head; 16 threads per row, 8 dims each.  q rows -> per-head RMSNorm
+// (bf16-rounded, like the standalone kernel) -> NeoX RoPE -> LDS; the new token's k / v
+// (only when write_kv) -> paged cache.  Rotary pairs (d, d+64) sit in threads j and j^8.
+__device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq, int kvh,
+                                                   bool write_kv, bf16* q_s) {
+  const int G = p.G;
+  const int rr = threadIdx.x >> 4;
+  const int j = threadIdx.x & 15;
+  if (rr < G + 2) {
+    int head;
+    if (rr < G) head = kvh * G + rr;
+    else if (rr == G) head = p.Hq + kvh;
+    else head = p.Hq + p.Hkv + kvh;
+    const bf16x8 raw =
+        *reinterpret_cast<const bf16x8*>(p.qkv + (size_t)seq * p.qkv_stride + head * kD + 8 * j);
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = bf2f(raw[i]);
+    if (rr <= G) {
+      const bf16* nw = rr < G ? p.q_w : p.k_w;
+      if (nw != nullptr) {
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ss += x[i] * x[i];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+        const float inv = rsqrtf(ss / (float)kD + p.eps);
+        const bf16x8 w8 = *reinterpret_cast<const bf16x8*>(nw + 8 * j);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = bf2f(f2bf(x[i] * inv * bf2f(w8[i])));
+      }
+      const float* cs = p.cos_sin + (size_t)p.positions[seq] * kD;
+      const int i0 = 8 * (j & 7);
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + i0);
+      const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + i0 + 4);
+      const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + 64 + i0);
+      const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + 64 + i0 + 4);
+      const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float other = __shfl_xor(x[i], 8, 16);
+        x[i] = j < 8 ? x[i] * cv[i] - other * sv[i] : x[i] * cv[i] + other * sv[i];
+      }
+    }
+    bf16x8 o8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o8[i] = f2bf(x[i]);
+    if (rr < G) {
+      *reinterpret_cast<bf16x8*>(q_s + rr * kD + 8 * j) = o8;
+    } else if (write_kv) {
+      const int64_t slot = p.slots[seq];
+      if (slot >= 0) {
+        const int64_t blk = slot / p.BS;
+        const int off = (int)(slot % p.BS);
+        if (rr == G) {
+          bf16* dst = const_cast<bf16*>(p.k_cache) + ((size_t)blk * p.Hkv + kvh) * p.BS * kD +
+                      k_swz_offset(off) + k_dim_offset(8 * j);
+          *reinterpret_cast<bf16x8*>(dst) = o8;
+        } else {
+          bf16* dst = const_cast<bf16*>(p.v_cache) + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
+                      (off >> 3) * kD * 8 + (off & 7);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dst[(size_t)(8 * j + i) * 8] = o8[i];
+        }
+      }
+    }
+  }
+  // q rows visible in LDS and the new K/V visible to every wave of this workgroup
+  __syncthreads();
+}
+
 // One (seq, kv head, partition) work item.  Ends with the LDS combine; callers that run
 // several items per workgroup must __syncthreads() before the next item's LDS writes.
-template <bool PREFETCH, bool NT = false>
+template <bool PREFETCH, bool NT = false, bool FUSED = false>
 __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
                                             float* dyn_lds) {
   const int lane = threadIdx.x & 63;
@@ -230,7 +303,7 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
   const int qr = lane & 15;
   const bool valid = qr < G && kv_len > 0;
   const int q_tok = p.q_start ? p.q_start[seq] : seq;
-  const bf16* qptr = p.q + ((size_t)q_tok * p.Hq + kvh * G + qr) * kD;
+  const bf16* qptr = FUSED ? nullptr : p.q + ((size_t)q_tok * p.Hq + kvh * G + qr) * kD;
 
   // combine buffer sized by G (dynamic LDS: 4 x G x (D+4) floats + stats), so small G
   // keeps LDS from limiting occupancy (G=2: ~4 KiB instead of 34 KiB)
@@ -238,19 +311,37 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
   float* m_s = dyn_lds + 4 * G * (kD + 4);    // [4][G]
   float* l_s = m_s + 4 * G;                   // [4][G]
 #define OS(w_, r_, d_) o_s[((w_) * G + (r_)) * (kD + 4) + (d_)]
+  bf16* q_s = reinterpret_cast<bf16*>(l_s + 4 * G);  // [G][kD] (fused only)
+  const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
+  const int limit = kv_len - 1;
+  const bool writes_kv = kv_len > 0 && pstart <= kv_len - 1 && kv_len - 1 < pend;
+  // PREFETCH: this wave's first chunk is issued before anything else (in the fused kernel,
+  // before the q/k prologue, so its HBM latency overlaps the prologue's)
+  int t0 = pstart + 32 * w;
+  ChunkRegs cur;
+  if (PREFETCH && t0 < pend)
+    load_chunk<NT>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+  if constexpr (FUSED) {
+    fused_qkv_prologue(p, seq, kvh, writes_kv, q_s);
+    // the chunk holding the token the prologue just wrote is re-read after the barrier
+    if (PREFETCH && writes_kv && t0 < pend && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
+      load_chunk<NT>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+  }
   WaveState st;
   wave_state_init(st);
   if (pstart < pend) {
     bf16x8 qb[kNC];
-    load_q(qb, qptr, valid);
-    const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
-    const int limit = kv_len - 1;
+    if constexpr (FUSED) {
+#pragma unroll
+      for (int c = 0; c < kNC; ++c)
+        qb[c] = valid ? *reinterpret_cast<const bf16x8*>(q_s + qr * kD + 32 * c + 8 * g)
+                      : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    } else {
+      load_q(qb, qptr, valid);
+    }
     if constexpr (PREFETCH) {
       // register double buffer: chunk i+1's loads are in flight during chunk i's MFMAs
-      int t0 = pstart + 32 * w;
       if (t0 < pend) {
-        ChunkRegs cur;
-        load_chunk<NT>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
         for (; t0 < pend; t0 += 128) {
           ChunkRegs nxt;
           const bool more = t0 + 128 < pend;
@@ -264,7 +355,7 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
         }
       }
     } else {
-      for (int t0 = pstart + 32 * w; t0 < pend; t0 += 128) {
+      for (; t0 < pend; t0 += 128) {
         if (t0 + 31 < kv_len)
           attn_chunk<false, NT>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
                                 t0, limit, p.scale_log2);
@@ -326,10 +417,10 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
 }
 
 // grid = (num_seqs, Hkv, num_parts): one work item per workgroup.
-template <bool PREFETCH, int MINW, bool NT = false>
+template <bool PREFETCH, int MINW, bool NT = false, bool FUSED = false>
 __global__ __launch_bounds__(256, MINW) void paged_attn_decode_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
-  decode_item<PREFETCH, NT>(p, blockIdx.x, blockIdx.y, blockIdx.z, dyn_lds);
+  decode_item<PREFETCH, NT, FUSED>(p, blockIdx.x, blockIdx.y, blockIdx.z, dyn_lds);
 }
 
 // Persistent variant: a fixed grid (a few workgroups per CU) strides over all work items
@@ -402,9 +493,16 @@ static int num_cus() {
 
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) {
   if (num_seqs == 0) return;
-  const size_t smem = (size_t)(4 * p.G * (kD + 4) + 8 * p.G) * sizeof(float);
+  const size_t smem = (size_t)(4 * p.G * (kD + 4) + 8 * p.G) * sizeof(float) +
+                      (p.qkv ? (size_t)p.G * kD * sizeof(bf16) : 0);
   const int per_cu = (p.flags >> 3) & 7;  // flags bits 3..5: persistent, WGs per CU
-  if (per_cu > 0) {
+  if (p.qkv != nullptr) {  // fused q/k-norm + RoPE + KV write (default flags path)
+    const dim3 grid(num_seqs, p.Hkv, p.num_parts);
+    if (p.flags & 1)
+      paged_attn_decode_kernel<true, 1, true, true><<<grid, 256, smem, s>>>(p);
+    else
+      paged_attn_decode_kernel<false, 1, true, true><<<grid, 256, smem, s>>>(p);
+  } else if (per_cu > 0) {
     const int items = num_seqs * p.Hkv * p.num_parts;
     const int grid = min(items, num_cus() * per_cu);
     const bool nt = p.flags & 64;

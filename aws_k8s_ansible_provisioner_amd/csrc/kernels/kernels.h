@@ -46,6 +46,16 @@ struct AttnParams {
   float* part_l;
   float* part_o;  // [B, Hkv, parts, G, D]
   int flags;      // bit0: register double-buffered K/V prefetch in decode
+  // fused decode (qkv != nullptr): the kernel itself applies per-head q/k RMSNorm + RoPE to
+  // the raw QKV projection row and writes the new token's K/V into the paged cache
+  const __bf16* qkv;      // [B, qkv_stride]: q heads | k heads | v heads
+  int qkv_stride;
+  const int64_t* positions;  // [B]
+  const int64_t* slots;      // [B] (-1: no write)
+  const float* cos_sin;      // [max_pos, D] = cos | sin
+  const __bf16* q_w;         // [D] or nullptr
+  const __bf16* k_w;
+  float eps;
 };
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s);
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s);

@@ -174,6 +174,49 @@ void paged_attention_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache
   akap::launch_paged_attn_decode(p, B, cur_stream());
 }
 
+// Decode attention fused with the per-head q/k RMSNorm + RoPE + new-token K/V cache write:
+// reads the raw QKV projection rows, so the standalone qk_norm_rope_cache launch (and its
+// q round trip) disappears from every decode layer.
+void paged_attention_decode_fused(Tensor out, Tensor qkv, Tensor k_cache, Tensor v_cache,
+                                  Tensor block_tables, Tensor seq_lens, Tensor positions,
+                                  Tensor slots, Tensor cos_sin, std::optional<Tensor> q_w,
+                                  std::optional<Tensor> k_w, Tensor part_m, Tensor part_l,
+                                  Tensor part_o, int64_t num_parts, int64_t part_size, int64_t G,
+                                  double scale, double eps) {
+  auto p = attn_params(out, out, k_cache, v_cache, block_tables, seq_lens, G, scale);
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv);
+  TORCH_CHECK(G + 2 <= 16, "fused decode supports up to 14 q heads per kv head");
+  TORCH_CHECK(part_size % 128 == 0 && part_size > 0, "part_size must be a multiple of 128");
+  const int B = seq_lens.numel();
+  TORCH_CHECK(qkv.size(0) >= B && qkv.size(1) >= (p.Hq + 2 * p.Hkv) * 128, "qkv shape");
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong,
+              "positions / slots must be int64");
+  TORCH_CHECK(positions.numel() >= B && slots.numel() >= B, "positions / slots too short");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == 128, "cos_sin [P, 128]");
+  p.q = nullptr;
+  p.qkv = (const __bf16*)qkv.data_ptr();
+  p.qkv_stride = qkv.stride(0);
+  p.positions = positions.data_ptr<int64_t>();
+  p.slots = slots.data_ptr<int64_t>();
+  p.cos_sin = cos_sin.data_ptr<float>();
+  p.q_w = q_w ? (const __bf16*)q_w->data_ptr() : nullptr;
+  p.k_w = k_w ? (const __bf16*)k_w->data_ptr() : nullptr;
+  p.eps = (float)eps;
+  p.q_start = nullptr;
+  p.num_parts = num_parts;
+  p.part_size = part_size;
+  if (num_parts > 1) {
+    TORCH_CHECK(part_o.numel() >= (int64_t)B * p.Hkv * num_parts * G * 128,
+                "part_o workspace too small");
+    TORCH_CHECK(part_m.numel() >= (int64_t)B * p.Hkv * num_parts * G, "part_m too small");
+    p.part_m = part_m.data_ptr<float>();
+    p.part_l = part_l.data_ptr<float>();
+    p.part_o = part_o.data_ptr<float>();
+  }
+  const c10::DeviceGuard g(qkv.device());
+  akap::launch_paged_attn_decode(p, B, cur_stream());
+}
+
 int64_t gemm_splitk(int64_t M, int64_t N, int64_t K) {
   return akap::gemm_splitk_choice(M, N, K);
 }
@@ -503,6 +546,11 @@ TORCH_LIBRARY(akap, m) {
       "Tensor block_tables, Tensor seq_lens, Tensor? q_start, Tensor(b!) part_m, Tensor(c!) part_l, "
       "Tensor(d!) part_o, int num_parts, int part_size, int G, float scale) -> ()");
   m.def(
+      "paged_attention_decode_fused(Tensor(a!) out, Tensor qkv, Tensor(b!) k_cache, "
+      "Tensor(c!) v_cache, Tensor block_tables, Tensor seq_lens, Tensor positions, Tensor slots, "
+      "Tensor cos_sin, Tensor? q_w, Tensor? k_w, Tensor(d!) part_m, Tensor(e!) part_l, "
+      "Tensor(f!) part_o, int num_parts, int part_size, int G, float scale, float eps) -> ()");
+  m.def(
       "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
       "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs) -> ()");
   m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
@@ -547,6 +595,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("silu_and_mul", &silu_and_mul);
   m.impl("paged_attention_prefill", &paged_attention_prefill);
   m.impl("paged_attention_decode", &paged_attention_decode);
+  m.impl("paged_attention_decode_fused", &paged_attention_decode_fused);
   m.impl("sample", &sample);
   m.impl("argmax", &argmax);
   m.impl("gemm", &gemm);

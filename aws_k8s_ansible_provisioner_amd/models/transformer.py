@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import Optional
 
 import torch
@@ -25,6 +26,8 @@ from ..parallel import comm
 from ..parallel.state import ParallelState, get_state
 from .config import ModelConfig
 from .moe import MoEBlock
+
+FUSED_DECODE = os.environ.get("AKAP_FUSED_DECODE", "1") != "0"
 
 
 @dataclasses.dataclass
@@ -264,12 +267,20 @@ class DecoderLM:
             if li > 0:
                 h, residual = ops.fused_add_rms_norm(x, residual, lw.ln1, eps)
             qkv = ops.linear(h, lw.w_qkv)
-            q = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
-            ops.qk_norm_rope_cache(qkv, q, k_caches[li], v_caches[li], batch.positions,
-                                   batch.slots, self.cos_sin, lw.q_norm, lw.k_norm, self.hq,
-                                   self.hkv, eps, True)
-            attn = torch.empty_like(q)
-            self._attention(q, batch, k_caches[li], v_caches[li], attn)
+            attn = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+            if not batch.is_prefill and FUSED_DECODE:
+                # q/k-norm + RoPE + KV-cache write fused into the decode attention kernel
+                ops.paged_attention_decode_fused(
+                    attn, qkv, k_caches[li], v_caches[li], batch.block_tables, batch.seq_lens,
+                    batch.positions, batch.slots, self.cos_sin, lw.q_norm, lw.k_norm,
+                    self.hq // self.hkv, self.scale, eps, workspace=batch.workspace,
+                    num_parts=batch.num_parts, part_size=batch.part_size)
+            else:
+                q = torch.empty_like(attn)
+                ops.qk_norm_rope_cache(qkv, q, k_caches[li], v_caches[li], batch.positions,
+                                       batch.slots, self.cos_sin, lw.q_norm, lw.k_norm, self.hq,
+                                       self.hkv, eps, True)
+                self._attention(q, batch, k_caches[li], v_caches[li], attn)
             o = comm.tp_all_reduce(ops.linear(attn.view(T, self.hq * self.D), lw.w_o))
             h, residual = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             if lw.moe is not None:

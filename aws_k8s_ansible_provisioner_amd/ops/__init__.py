@@ -140,6 +140,32 @@ def paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens, gqa
     return out
 
 
+def paged_attention_decode_fused(out, qkv, k_cache, v_cache, block_tables, seq_lens, positions,
+                                 slots, cos_sin, q_w, k_w, gqa_group: int, scale: float,
+                                 eps: float, workspace=None, num_parts: int = 1,
+                                 part_size: int = 512):
+    """Decode attention that consumes the raw QKV projection: per-head q/k RMSNorm + RoPE
+    and the new token's K/V cache write happen inside the attention kernel.
+    out [B, Hq, D]; qkv [B, (Hq + 2 Hkv) * D]."""
+    if _native(qkv):
+        if workspace is None:
+            workspace = decode_workspace(seq_lens.numel(), k_cache.shape[1], gqa_group,
+                                         num_parts, qkv.device)
+        pm, pl, po = workspace
+        torch.ops.akap.paged_attention_decode_fused(out, qkv, k_cache, v_cache, block_tables,
+                                                    seq_lens, positions, slots, cos_sin, q_w, k_w,
+                                                    pm, pl, po, num_parts, part_size, gqa_group,
+                                                    scale, eps)
+        return out
+    B, Hq = out.shape[0], out.shape[1]
+    q = torch.empty_like(out)
+    ref.qk_norm_rope_cache(qkv[:B], q, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w, Hq,
+                           k_cache.shape[1], eps, True)
+    q_start = torch.arange(B + 1, dtype=torch.int32)
+    out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale))
+    return out
+
+
 def decode_workspace(max_seqs: int, num_kv_heads: int, gqa_group: int, num_parts: int,
                      device) -> tuple:
     n = max(1, max_seqs * num_kv_heads * max(num_parts, 1) * gqa_group)

@@ -63,11 +63,14 @@ def main():
         logits = m.compute_logits(h)
         ops.sample(logits, temp, topk, topp, seeds, steps)
 
-    orig = {k: getattr(ops, k) for k in ("paged_attention_decode", "qk_norm_rope_cache",
+    orig = {k: getattr(ops, k) for k in ("paged_attention_decode", "paged_attention_decode_fused",
+                                          "qk_norm_rope_cache",
                                           "rms_norm", "fused_add_rms_norm", "silu_and_mul",
                                           "linear", "sample")}
     noop = {
-        "attention": {"paged_attention_decode": lambda out, *a_, **k: out},
+        "attention (fused: +qk-norm/rope/kv-write)": {
+            "paged_attention_decode": lambda out, *a_, **k: out,
+            "paged_attention_decode_fused": lambda out, *a_, **k: out},
         "qk_norm_rope_cache": {"qk_norm_rope_cache": lambda qkv, q_out, *a_, **k: q_out},
         "norms": {"rms_norm": lambda x, w, eps, out=None: x,
                   "fused_add_rms_norm": lambda x, r, w, eps, out=None: (x, r)},
@@ -105,7 +108,7 @@ def main():
     print(f"{a.model} B={B} ctx~{a.ctx}: full decode step {full * 1000:8.1f} us")
     for name, patch in noop.items():
         t = run(name, patch)
-        print(f"  without {name:22s} {t * 1000:8.1f} us   -> costs {(full - t) * 1000:7.1f} us "
+        print(f"  without {name:40s} {t * 1000:8.1f} us   -> costs {(full - t) * 1000:7.1f} us "
               f"({100 * (full - t) / full:4.1f} %)")
 
 

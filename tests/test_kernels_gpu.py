@@ -152,6 +152,43 @@ def test_paged_attention_decode(num_parts, part_size, hq, hkv):
     _close(out, exp, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (64, 8)])
+@pytest.mark.parametrize("qk_norm", [True, False])
+@pytest.mark.parametrize("num_parts,part_size", [(1, 4096), (3, 512)])
+def test_paged_attention_decode_fused(hq, hkv, qk_norm, num_parts, part_size):
+    """Fused q/k-norm + RoPE + KV write + decode attention vs the reference pipeline."""
+    lens = [1, 31, 32, 33, 200, 777, 1500]
+    seqs = [(kv, 1) for kv in lens]
+    _, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=hq + num_parts)
+    B, D = len(lens), 128
+    g = torch.Generator().manual_seed(11)
+    qkv = torch.randn(B, (hq + 2 * hkv) * D, generator=g).bfloat16()
+    pos = (sl - 1).to(torch.int64)
+    slots = torch.tensor([int(bt[s, int(pos[s]) // 32]) * 32 + int(pos[s]) % 32
+                          for s in range(B)], dtype=torch.int64)
+    slots[2] = -1  # padding row: no cache write
+    cs = ref.rope_cos_sin(4096, D, 1e6)
+    qw = torch.randn(D, generator=g).bfloat16() if qk_norm else None
+    kw = torch.randn(D, generator=g).bfloat16() if qk_norm else None
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    q_ref = torch.empty(B, hq, D).bfloat16()
+    ref.qk_norm_rope_cache(qkv, q_ref, kc_ref, vc_ref, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
+    scale = 1 / math.sqrt(D)
+    exp = ref.paged_attention(q_ref, kc_ref, vc_ref, bt, sl, qs, scale)
+    kg, vg = kc.to(DEV), vc.to(DEV)
+    out = torch.empty(B, hq, D, dtype=torch.bfloat16, device=DEV)
+    G = hq // hkv
+    ws = ops.decode_workspace(B, hkv, G, num_parts, DEV)
+    ops.paged_attention_decode_fused(out, qkv.to(DEV), kg, vg, bt.to(DEV), sl.to(DEV),
+                                     pos.to(DEV), slots.to(DEV), cs.to(DEV),
+                                     None if qw is None else qw.to(DEV),
+                                     None if kw is None else kw.to(DEV), G, scale, 1e-6,
+                                     workspace=ws, num_parts=num_parts, part_size=part_size)
+    _close(out, exp, atol=3e-2, rtol=3e-2)
+    _close(kg, kc_ref, atol=3e-2, rtol=2e-2)
+    _close(vg, vc_ref, atol=0)
+
+
 def test_decode_attention_large_score_spike():
     """Force the online-softmax rescale branch: a single huge-score key late in the sequence."""
     seqs = [(900, 1)]
