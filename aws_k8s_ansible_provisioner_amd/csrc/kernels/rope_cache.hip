@@ -20,6 +20,18 @@
 
 namespace akap {
 
+// True when batch token t belongs to an 8-token V slot group whose 8 tokens are all in the
+// batch, consecutive (slots s0..s0+7, s0 % 8 == 0).  Written slots are never shared between
+// sequences (shared prefix blocks are full and read-only), so consecutive slots imply one
+// sequence's consecutive positions.
+__device__ __forceinline__ bool v_group_complete(const int64_t* __restrict__ slots, int t, int T,
+                                                 int64_t slot) {
+  const int r = (int)(slot & 7);
+  const int g0 = t - r;
+  if (g0 < 0 || g0 + 7 >= T) return false;
+  return slots[g0] == slot - r && slots[g0 + 7] == slot - r + 7;
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
     const bf16* __restrict__ qkv, int qkv_stride, bf16* __restrict__ q_out,
@@ -93,6 +105,9 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
     *reinterpret_cast<bf16x4*>(dst + k_dim_offset(4 * li)) = oa;
     *reinterpret_cast<bf16x4*>(dst + k_dim_offset(HALF + 4 * li)) = ob;
   } else {
+    // tokens of a complete 8-token slot group are written by v_group_write_kernel as
+    // 16-byte vectors; only stragglers (chunk edges, decode tokens) scatter 2-byte stores
+    if (v_group_complete(slots, t, T, slot)) return;
     const int vh = h - Hq - Hkv;
     bf16* dst = v_cache + ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + (off & 7);
 #pragma unroll
@@ -100,6 +115,33 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
       dst[(size_t)(4 * li + j) * 8] = oa[j];
       dst[(size_t)(HALF + 4 * li + j) * 8] = ob[j];
     }
+  }
+}
+
+// V cache groups are [D][8 tokens]: a token alone can only be written as D scattered
+// 2-byte stores.  When the batch holds all 8 tokens of a slot group (prefill chunks), a
+// thread per dim gathers the 8 values (each read coalesced across the wave) and writes one
+// 16-byte vector.  grid = (ceil(T / 64), Hkv), 128 threads = one per dim.
+__global__ __launch_bounds__(128) void v_group_write_kernel(const bf16* __restrict__ qkv,
+                                                            int qkv_stride,
+                                                            bf16* __restrict__ v_cache,
+                                                            const int64_t* __restrict__ slots,
+                                                            int T, int Hq, int Hkv, int BS) {
+  constexpr int D = 128;
+  const int vh = blockIdx.y;
+  const int d = threadIdx.x;
+  const int t_end = min(T, (int)(blockIdx.x + 1) * 64);
+  for (int t = blockIdx.x * 64; t < t_end; ++t) {
+    const int64_t slot = slots[t];
+    if (slot < 0 || (slot & 7) != 0 || !v_group_complete(slots, t, T, slot)) continue;
+    const bf16* src = qkv + (size_t)t * qkv_stride + (Hq + Hkv + vh) * D + d;
+    bf16x8 g8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g8[i] = src[(size_t)i * qkv_stride];
+    const int64_t blk = slot / BS;
+    const int off = (int)(slot % BS);
+    *reinterpret_cast<bf16x8*>(v_cache + ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 +
+                               d * 8) = g8;
   }
 }
 
@@ -117,6 +159,9 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
     qk_norm_rope_cache_kernel<128><<<grid, 256, 0, s>>>(
         (const bf16*)qkv, qkv_stride, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions,
         slots, cos_sin, (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope);
+    if (T >= 8)
+      v_group_write_kernel<<<dim3((T + 63) / 64, Hkv), 128, 0, s>>>(
+          (const bf16*)qkv, qkv_stride, (bf16*)v_cache, slots, T, Hq, Hkv, BS);
   }
 }
 

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--ctx", type=int, default=640)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--prefill", type=int, default=0,
+                    help="instead: a prefill step of B sequences x this many new tokens")
     a = ap.parse_args()
     ops.load_native(required=True)
     dev = torch.device("cuda", 0)
@@ -51,7 +53,32 @@ def main():
     ws = ops.decode_workspace(B, m.hkv, m.hq // m.hkv, 1, dev)
     batch = AttnBatch(False, d(pos), d(slots), d(bt), d(lens), d(torch.arange(B + 1,
                       dtype=torch.int32)), None, None, 1, 4096, ws)
-    ids = torch.randint(0, cfg.vocab_size, (B,), device=dev)
+    if a.prefill:
+        P = a.prefill
+        lens = torch.full((B,), P, dtype=torch.int32)
+        NB2 = B * math.ceil(P / BS) + 8
+        kv = m.allocate_kv_cache(NB2, BS)
+        kc, vc = m.cache_views(kv, BS)
+        bt = torch.zeros(B, 4096 // BS, dtype=torch.int32)
+        perm = torch.randperm(NB2)
+        nbp = math.ceil(P / BS)
+        for s_ in range(B):
+            bt[s_, :nbp] = perm[s_ * nbp:(s_ + 1) * nbp].to(torch.int32)
+        pos = torch.arange(P, dtype=torch.int64).repeat(B)
+        slots = torch.cat([bt[s_, torch.arange(P) // BS].to(torch.int64) * BS + torch.arange(P) % BS
+                           for s_ in range(B)])
+        q_start = torch.arange(0, B * P + 1, P, dtype=torch.int32)
+        G = m.hq // m.hkv
+        ts, tr = [], []
+        for s_ in range(B):
+            for r in range(0, P * G, 64):
+                ts.append(s_)
+                tr.append(r)
+        batch = AttnBatch(True, d(pos), d(slots), d(bt), d(lens), d(q_start),
+                          d(torch.tensor(ts, dtype=torch.int32)),
+                          d(torch.tensor(tr, dtype=torch.int32)))
+        lidx = d(q_start[1:].to(torch.int64) - 1)
+    ids = torch.randint(0, cfg.vocab_size, (B * (a.prefill or 1),), device=dev)
     temp = torch.zeros(B, device=dev)
     topk = torch.zeros(B, dtype=torch.int32, device=dev)
     topp = torch.ones(B, device=dev)
@@ -60,17 +87,21 @@ def main():
 
     def step():
         h = m.forward(ids, batch, kc, vc)
+        if a.prefill:
+            h = h.index_select(0, lidx)
         logits = m.compute_logits(h)
         ops.sample(logits, temp, topk, topp, seeds, steps)
 
     orig = {k: getattr(ops, k) for k in ("paged_attention_decode", "paged_attention_decode_fused",
+                                          "paged_attention_prefill",
                                           "qk_norm_rope_cache",
                                           "rms_norm", "fused_add_rms_norm", "silu_and_mul",
                                           "linear", "sample")}
     noop = {
         "attention (fused: +qk-norm/rope/kv-write)": {
             "paged_attention_decode": lambda out, *a_, **k: out,
-            "paged_attention_decode_fused": lambda out, *a_, **k: out},
+            "paged_attention_decode_fused": lambda out, *a_, **k: out,
+            "paged_attention_prefill": lambda out, *a_, **k: out},
         "qk_norm_rope_cache": {"qk_norm_rope_cache": lambda qkv, q_out, *a_, **k: q_out},
         "norms": {"rms_norm": lambda x, w, eps, out=None: x,
                   "fused_add_rms_norm": lambda x, r, w, eps, out=None: (x, r)},
@@ -105,7 +136,8 @@ def main():
                 setattr(ops, k, f)
 
     full = run("full", {})
-    print(f"{a.model} B={B} ctx~{a.ctx}: full decode step {full * 1000:8.1f} us")
+    what = f"prefill {B}x{a.prefill}" if a.prefill else f"decode B={B} ctx~{a.ctx}"
+    print(f"{a.model} {what}: full step {full * 1000:8.1f} us")
     for name, patch in noop.items():
         t = run(name, patch)
         print(f"  without {name:40s} {t * 1000:8.1f} us   -> costs {(full - t) * 1000:7.1f} us "

@@ -63,12 +63,17 @@ def _rand_cache(nb, hkv, bs, d=128, seed=0):
 
 @pytest.mark.parametrize("qk_norm", [True, False])
 @pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8)])
-def test_qk_norm_rope_cache(qk_norm, hq, hkv):
+@pytest.mark.parametrize("layout", ["random", "prefill"])
+def test_qk_norm_rope_cache(qk_norm, hq, hkv, layout):
     torch.manual_seed(2)
     T, D, BS, NB = 45, 128, 32, 16
     qkv = torch.randn(T, (hq + 2 * hkv) * D, dtype=torch.bfloat16)
     pos = torch.randint(0, 4000, (T,), dtype=torch.int64)
-    slots = torch.randperm(NB * BS)[:T].to(torch.int64)
+    if layout == "random":
+        slots = torch.randperm(NB * BS)[:T].to(torch.int64)
+    else:  # two sequences' prefill chunks: complete 8-token V groups + ragged edges
+        slots = torch.cat([torch.arange(3 * BS + 5, 3 * BS + 5 + 30),
+                           torch.arange(9 * BS + 16, 9 * BS + 16 + 15)]).to(torch.int64)
     slots[3] = -1
     cs = ref.rope_cos_sin(4096, D, 1e6)
     qw = torch.randn(D).bfloat16() if qk_norm else None
