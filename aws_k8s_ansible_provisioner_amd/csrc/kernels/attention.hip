@@ -439,6 +439,204 @@ __global__ __launch_bounds__(256) void paged_attn_decode_persistent_kernel(AttnP
   }
 }
 
+
+// ----------------------------------------------------------------------------------
+// Flash-style prefill: 128 flattened q rows (token x GQA head) per workgroup, 4 waves x 32
+// rows, 64-key K/V tiles staged once per workgroup in LDS (double-buffered, next tile's
+// global loads in flight during the current tile's MFMAs), v_mfma_f32_32x32x16_bf16.
+//   S^T = K . Q^T : K fragments from an XOR-swizzled LDS image (A), Q^T from registers (B);
+//                   each lane owns one q row (column) -> softmax is lane-local + one xor-32.
+//   O^T = V^T . P^T: P^T straight from the S^T accumulators (bf16), V^T fragments are two
+//                   8-byte reads of the V-group image ([group][d][8 tokens], copied verbatim
+//                   from the paged cache); O^T's column is again the lane's q row, so the
+//                   online-softmax rescale needs no cross-lane traffic.
+// ----------------------------------------------------------------------------------
+constexpr int kFaRows = 128;
+constexpr int kFaKeys = 64;
+
+__global__ __launch_bounds__(256) void paged_attn_prefill_fa_kernel(AttnParams p) {
+  // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB, one __shared__ object
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 2 * kFaKeys * kD];
+  const int tile = blockIdx.x;
+  const int kvh = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int seq = p.tile_seq[tile];
+  const int q0 = p.q_start[seq];
+  const int q_len = p.q_start[seq + 1] - q0;
+  const int kv_len = p.seq_lens[seq];
+  const int G = p.G;
+  const int row0 = p.tile_row[tile];
+  const int R = row0 + 32 * w + r;
+  const int pos = R / G;
+  const int hig = R % G;
+  const bool valid = pos < q_len;
+  const int ctx0 = kv_len - q_len;  // keys before this chunk's first query token
+  const int limit = valid ? ctx0 + pos : -1;
+
+  // Q^T fragments (B operand): lane (r, h) holds Q[row][16 s + 8 h + j]
+  bf16x8 qf[8];
+  const bf16* qrow = p.q + ((size_t)(q0 + (valid ? pos : 0)) * p.Hq + kvh * G + hig) * kD;
+#pragma unroll
+  for (int s8 = 0; s8 < 8; ++s8)
+    qf[s8] = valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * s8 + 8 * h)
+                   : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+
+  const int wg_last_pos = min(q_len - 1, (row0 + kFaRows - 1) / G);
+  const int wg_limit = ctx0 + wg_last_pos;
+  const int ntiles = wg_limit / kFaKeys + 1;
+  const int w_first_pos = (row0 + 32 * w) / G;
+  const int w_last_pos = min(q_len - 1, (row0 + 32 * w + 31) / G);
+  const bool wave_active = w_first_pos < q_len;
+  const int w_limit = ctx0 + w_last_pos;       // last key any row of this wave sees
+  const int w_min_limit = ctx0 + w_first_pos;  // every row of this wave sees keys <= this
+  const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
+  const int BS = p.BS;
+  const int last_chunk = (kv_len - 1) >> 5;
+
+  // staging: 1024 16-B pieces of K and 1024 of V per tile, 4 + 4 per thread
+  bf16x8 kst[4], vst[4];
+  auto stage_load = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pc = tid + 256 * i;   // 0..1023
+      const int c = pc >> 9;           // 32-key chunk of the tile
+      const int within = pc & 511;
+      const int chunk = min(t * 2 + c, last_chunk);
+      const int tok = chunk * 32;
+      const int blk = bt[tok / BS];
+      const int off = tok % BS;
+      const size_t base = ((size_t)blk * p.Hkv + kvh) * BS * kD;
+      kst[i] = *reinterpret_cast<const bf16x8*>(p.k_cache + base + (size_t)off * kD + within * 8);
+      vst[i] = *reinterpret_cast<const bf16x8*>(p.v_cache + base + (size_t)(off >> 3) * kD * 8 +
+                                                within * 8);
+    }
+  };
+  auto stage_store = [&](int buf) {
+    bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
+    bf16* vl = kl + kFaKeys * kD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pc = tid + 256 * i;
+      const int c = pc >> 9;
+      const int within = pc & 511;
+      // K cache chunk order: ((tt * 4 + cc) * 16 + r16) * 4 + q  (16-B pieces)
+      const int q4 = within & 3;
+      const int r16 = (within >> 2) & 15;
+      const int cc = (within >> 6) & 3;
+      const int tt = within >> 8;
+      const int key = 32 * c + 8 * (r16 >> 2) + 4 * tt + (r16 & 3);
+      const int dc = 4 * cc + q4;  // 16-B column of the 256-B key row
+      *reinterpret_cast<bf16x8*>(kl + key * kD + ((dc ^ (key & 15)) * 8)) = kst[i];
+      *reinterpret_cast<bf16x8*>(vl + c * 32 * kD + within * 8) = vst[i];
+    }
+  };
+
+  f32x16 oacc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+
+  stage_load(0);
+  stage_store(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) stage_load(t + 1);
+    const int key0 = t * kFaKeys;
+    if (wave_active && key0 <= w_limit) {
+      const bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
+      const bf16* vl = kl + kFaKeys * kD;
+      f32x16 sacc[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sacc[k][j] = 0.f;
+        const int key = 32 * k + r;
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(
+              kl + key * kD + (((2 * s8 + h) ^ (key & 15)) * 8));
+          sacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s8], sacc[k], 0, 0, 0);
+        }
+      }
+      // scale (log2 domain), causal mask, running max
+      const bool need_mask = key0 + kFaKeys - 1 > w_min_limit;
+      float mx = -1e30f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          float v = sacc[k][j] * p.scale_log2;
+          if (need_mask) {
+            const int kk = key0 + 32 * k + (j & 3) + 8 * (j >> 2) + 4 * h;
+            if (kk > limit) v = -INFINITY;
+          }
+          sacc[k][j] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2f(m_run - m_new);
+      float rs = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float e = exp2f(sacc[k][j] - m_new);
+          sacc[k][j] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
+      // O^T += V^T . P^T
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[k][8 * s2 + j]);
+          const int g = 4 * k + 2 * s2;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const int d = 32 * dt + r;
+            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vl + (g * kD + d) * 8 + 4 * h);
+            const bf16x4 hi =
+                *reinterpret_cast<const bf16x4*>(vl + ((g + 1) * kD + d) * 8 + 4 * h);
+            const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, oacc[dt], 0, 0, 0);
+          }
+        }
+    }
+    if (more) stage_store(buf ^ 1);
+    __syncthreads();
+  }
+  if (!valid) return;
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  bf16* orow = p.out + ((size_t)(q0 + pos) * p.Hq + kvh * G + hig) * kD;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = f2bf(oacc[dt][4 * j4 + i] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * j4 + 4 * h) = o;
+    }
+}
+
 // Combine split-KV partitions: grid (num_seqs, Hkv), 256 threads = (16 rows x 16 lanes x 8 dims).
 __global__ __launch_bounds__(256) void paged_attn_reduce_kernel(AttnParams p) {
   const int seq = blockIdx.x;
@@ -475,9 +673,13 @@ __global__ __launch_bounds__(256) void paged_attn_reduce_kernel(AttnParams p) {
   *reinterpret_cast<bf16x8*>(op) = o8;
 }
 
-void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s) {
+void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows,
+                               hipStream_t s) {
   if (num_tiles == 0) return;
-  paged_attn_prefill_kernel<<<dim3(num_tiles, p.Hkv), 256, 0, s>>>(p);
+  if (tile_rows == kFaRows)
+    paged_attn_prefill_fa_kernel<<<dim3(num_tiles, p.Hkv), 256, 0, s>>>(p);
+  else
+    paged_attn_prefill_kernel<<<dim3(num_tiles, p.Hkv), 256, 0, s>>>(p);
 }
 
 static int num_cus() {

@@ -57,7 +57,8 @@ struct AttnParams {
   const __bf16* k_w;
   float eps;
 };
-void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, hipStream_t s);
+// tile_rows: 64 -> per-wave 16-row kernel, 128 -> flash-style LDS-tiled kernel
+void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows, hipStream_t s);
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s);
 
 // ---- gemm.hip ----

@@ -139,8 +139,10 @@ akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_
 
 void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache,
                              Tensor block_tables, Tensor seq_lens, Tensor q_start,
-                             Tensor tile_seq, Tensor tile_row, int64_t G, double scale) {
+                             Tensor tile_seq, Tensor tile_row, int64_t G, double scale,
+                             int64_t tile_rows) {
   auto p = attn_params(out, q, k_cache, v_cache, block_tables, seq_lens, G, scale);
+  TORCH_CHECK(tile_rows == 64 || tile_rows == 128, "tile_rows must be 64 or 128");
   TORCH_CHECK(q_start.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
                   tile_row.scalar_type() == at::kInt,
               "q_start/tile maps must be int32");
@@ -148,7 +150,7 @@ void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cach
   p.tile_seq = tile_seq.data_ptr<int>();
   p.tile_row = tile_row.data_ptr<int>();
   const c10::DeviceGuard g(q.device());
-  akap::launch_paged_attn_prefill(p, tile_seq.numel(), cur_stream());
+  akap::launch_paged_attn_prefill(p, tile_seq.numel(), (int)tile_rows, cur_stream());
 }
 
 void paged_attention_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache,
@@ -540,7 +542,7 @@ TORCH_LIBRARY(akap, m) {
   m.def(
       "paged_attention_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_lens, Tensor q_start, Tensor tile_seq, Tensor tile_row, "
-      "int G, float scale) -> ()");
+      "int G, float scale, int tile_rows=64) -> ()");
   m.def(
       "paged_attention_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_lens, Tensor? q_start, Tensor(b!) part_m, Tensor(c!) part_l, "

@@ -74,7 +74,7 @@ class LLMEngine:
         sc.max_model_len = ecfg.max_model_len
         sc.block_size = ecfg.block_size
         sc.gqa_group = self.runner.G
-        sc.tile_rows = 64
+        sc.tile_rows = self.runner.tile_rows
         sc.eos_id = self.mcfg.eos_id
         sc.max_blocks_per_seq = self.runner.max_blocks
         self.sched = rt.Scheduler(sc, self.runner.num_blocks, ecfg.enable_prefix_caching)

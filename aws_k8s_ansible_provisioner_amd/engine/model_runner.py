@@ -58,6 +58,10 @@ class ModelRunner:
         self.G = self.model.hq // self.model.hkv
         self.max_seqs = ecfg.max_num_seqs
         self.cap_tokens = max(ecfg.max_num_batched_tokens, self.max_seqs)
+        # prefill tile map granularity: 128 flattened q rows per workgroup for the flash-style
+        # GPU kernel (AKAP_PREFILL_FA=0: the 64-row per-wave kernel)
+        self.tile_rows = 128 if (dev == "cuda" and
+                                 os.environ.get("AKAP_PREFILL_FA", "1") != "0") else 64
         self.cap_tiles = self.cap_tokens * self.G // 64 + self.max_seqs + 1
         self.num_blocks = ecfg.num_gpu_blocks or self._derive_num_blocks()
         if self.ps.tp_size > 1:  # every TP rank must address the same block pool
@@ -151,7 +155,8 @@ class ModelRunner:
         lidx = self._h2d("logits_idx", ns)
         for k in ("temperature", "top_p", "top_k", "seeds", "steps"):
             self._h2d(k, ns)
-        batch = AttnBatch(True, pos, slots, self.d_bt[:B], sl, qs, ts, tr)
+        batch = AttnBatch(True, pos, slots, self.d_bt[:B], sl, qs, ts, tr,
+                          tile_rows=self.tile_rows)
         h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
         if ns == 0:
             return self.out_tokens[:0]

@@ -41,6 +41,7 @@ class AttnBatch:
     q_start: torch.Tensor        # [B+1] int32
     tile_seq: Optional[torch.Tensor] = None  # prefill tile map
     tile_row: Optional[torch.Tensor] = None
+    tile_rows: int = 64          # q rows per tile of the map (128: flash-style kernel)
     num_parts: int = 1           # decode split-KV partitions
     part_size: int = 512
     workspace: Optional[tuple] = None
@@ -247,7 +248,8 @@ class DecoderLM:
         if batch.is_prefill:
             ops.paged_attention_prefill(out, q, kc, vc, batch.block_tables, batch.seq_lens,
                                         batch.q_start, batch.tile_seq, batch.tile_row,
-                                        self.hq // self.hkv, self.scale)
+                                        self.hq // self.hkv, self.scale,
+                                        tile_rows=batch.tile_rows)
         else:
             ops.paged_attention_decode(out, q, kc, vc, batch.block_tables, batch.seq_lens,
                                        self.hq // self.hkv, self.scale, workspace=batch.workspace,

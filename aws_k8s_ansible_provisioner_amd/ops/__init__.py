@@ -112,10 +112,13 @@ def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
 
 # ----------------------------------------------------------------------------- attention
 def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_start, tile_seq,
-                            tile_row, gqa_group: int, scale: float):
+                            tile_row, gqa_group: int, scale: float, tile_rows: int = 64):
+    """tile_rows = flattened q rows per tile of the host tile map: 128 selects the flash-style
+    LDS-tiled kernel (32x32x16 MFMA), 64 the per-wave 16-row kernel."""
     if _native(q):
         torch.ops.akap.paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens,
-                                               q_start, tile_seq, tile_row, gqa_group, scale)
+                                               q_start, tile_seq, tile_row, gqa_group, scale,
+                                               tile_rows)
         return out
     out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale))
     return out

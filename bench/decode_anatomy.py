@@ -69,14 +69,15 @@ def main():
                            for s_ in range(B)])
         q_start = torch.arange(0, B * P + 1, P, dtype=torch.int32)
         G = m.hq // m.hkv
+        TR = 128 if os.environ.get("AKAP_PREFILL_FA", "1") != "0" else 64
         ts, tr = [], []
         for s_ in range(B):
-            for r in range(0, P * G, 64):
+            for r in range(0, P * G, TR):
                 ts.append(s_)
                 tr.append(r)
         batch = AttnBatch(True, d(pos), d(slots), d(bt), d(lens), d(q_start),
                           d(torch.tensor(ts, dtype=torch.int32)),
-                          d(torch.tensor(tr, dtype=torch.int32)))
+                          d(torch.tensor(tr, dtype=torch.int32)), tile_rows=TR)
         lidx = d(q_start[1:].to(torch.int64) - 1)
     ids = torch.randint(0, cfg.vocab_size, (B * (a.prefill or 1),), device=dev)
     temp = torch.zeros(B, device=dev)

@@ -116,26 +116,28 @@ def _setup_attn(seqs, hq, hkv, bs, seed=0):
     return q, kc, vc, bt, seq_lens, q_start
 
 
-def _tiles(seqs, G):
+def _tiles(seqs, G, rows=64):
     ts, tr = [], []
     for s, (_, ql) in enumerate(seqs):
-        for r in range(0, ql * G, 64):
+        for r in range(0, ql * G, rows):
             ts.append(s)
             tr.append(r)
     return torch.tensor(ts, dtype=torch.int32), torch.tensor(tr, dtype=torch.int32)
 
 
 @pytest.mark.parametrize("bs", [32, 64])
-@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (8, 8)])
-def test_paged_attention_prefill(bs, hq, hkv):
-    seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (520, 7), (64, 1)]
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (8, 8), (64, 8)])
+@pytest.mark.parametrize("tile_rows", [64, 128])
+def test_paged_attention_prefill(bs, hq, hkv, tile_rows):
+    seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (520, 7), (64, 1), (700, 650)]
     q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, bs, seed=bs + hq)
     scale = 1 / math.sqrt(128)
     exp = ref.paged_attention(q, kc, vc, bt, sl, qs, scale)
-    ts, tr = _tiles(seqs, hq // hkv)
+    ts, tr = _tiles(seqs, hq // hkv, tile_rows)
     out = torch.empty_like(q).to(DEV)
     ops.paged_attention_prefill(out, q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV),
-                                qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv, scale)
+                                qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv, scale,
+                                tile_rows=tile_rows)
     _close(out, exp, atol=2e-2, rtol=2e-2)
 
 
