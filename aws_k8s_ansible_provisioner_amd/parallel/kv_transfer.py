@@ -43,6 +43,10 @@ class KVTransferAgent:
         self._thread.start()
         self.bytes_sent = 0
         self.bytes_recv = 0
+        # gloo moves host tensors only: GPU caches on a gloo group (single-GPU rehearsal of
+        # the P/D path) stage through pinned host memory
+        self.host_staging = self.is_gpu and dist.is_initialized() and \
+            dist.get_backend(group) == "gloo"
 
     def nbytes(self, nblk: int) -> int:
         return self.planes.shape[0] * nblk * self.block_elems * self.kv.element_size()
@@ -87,7 +91,11 @@ class KVTransferAgent:
             with self._ctx():
                 ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
                 buf = ops.kv_gather(self.planes, ids)
-                dist.send(buf, dst, group=self.group)
+                if self.host_staging:
+                    self.stream.synchronize()
+                    dist.send(buf.cpu(), dst, group=self.group)
+                else:
+                    dist.send(buf, dst, group=self.group)
                 if self.is_gpu:
                     self.stream.synchronize()
             self.bytes_sent += buf.numel() * buf.element_size()
@@ -105,7 +113,12 @@ class KVTransferAgent:
                 n = len(block_ids)
                 buf = torch.empty(self.planes.shape[0], n, self.block_elems, dtype=self.kv.dtype,
                                   device=self.device)
-                dist.recv(buf, src, group=self.group)
+                if self.host_staging:
+                    hb = torch.empty(buf.shape, dtype=buf.dtype)
+                    dist.recv(hb, src, group=self.group)
+                    buf.copy_(hb)
+                else:
+                    dist.recv(buf, src, group=self.group)
                 ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
                 ops.kv_scatter(buf, self.planes, ids)
                 if self.is_gpu:

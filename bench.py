@@ -12,6 +12,10 @@ GPU -- a data-parallel replica, exactly how the gateway scales the deployment (w
 scaling: per-GPU work is fixed).  Ranks are synchronised with barriers around the K
 timed waves; value = total output tokens of all ranks / max rank wall time.
 
+--mode pd (even WORLD_SIZE): disaggregated prefill/decode -- ranks [0, W/2) prefill,
+[W/2, W) decode, each request's KV moved prefill->decode with one RCCL send/recv
+(parallel/pd_driver.py); TTFT is measured on the decode side (includes the hand-off).
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -42,6 +46,11 @@ def parse():
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--enforce-eager", action="store_true")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--mode", default="mono", choices=["mono", "pd"],
+                    help="mono: every rank a monolithic replica (DP); pd: ranks [0,W/2) prefill, "
+                         "[W/2,W) decode, KV handed over RCCL (Llama-3-8B disagg config)")
+    ap.add_argument("--dist-backend", default=None,
+                    help="override (gloo = single-GPU rehearsal of the multi-rank paths)")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra untimed waves run after timing (for rocprofv3 captures)")
     return ap.parse_args()
@@ -63,27 +72,51 @@ def main() -> int:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
     gpu = torch.cuda.is_available() and a.device != "cpu"
     if gpu:
+        # more ranks than GPUs only in the single-GPU gloo rehearsal: share the device
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if gpu else "gloo"
-        kw = {"device_id": torch.device("cuda", local)} if gpu else {}
+        backend = a.dist_backend or ("nccl" if gpu else "gloo")
+        kw = {"device_id": torch.device("cuda", local)} if (gpu and backend == "nccl") else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    pd = a.mode == "pd"
+    if pd and (world < 2 or world % 2):
+        print("error: --mode pd needs an even WORLD_SIZE >= 2", file=sys.stderr)
+        return 2
+    is_prefill = pd and rank < world // 2
 
     mcfg = get_config(a.model)
     ecfg = EngineConfig(model=a.model, max_model_len=a.max_model_len,
                         max_num_seqs=a.max_num_seqs,
                         max_num_batched_tokens=a.max_num_batched_tokens,
                         block_size=a.block_size, enforce_eager=a.enforce_eager,
-                        device="cuda" if gpu else "cpu", seed=1234 + rank,
-                        num_gpu_blocks=None if gpu else 512)
+                        device="cuda" if gpu else "cpu",
+                        seed=1234 + (rank % (world // 2) if pd else rank),  # P/D pair: same weights
+                        num_gpu_blocks=None if gpu else 512,
+                        kv_role=("prefill" if is_prefill else "decode") if pd else "both",
+                        gpu_memory_utilization=0.45 if (pd and a.dist_backend == "gloo")
+                        else 0.90)
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if rank == 0 else (lambda *x: None)
     eng = LLMEngine(ecfg, mcfg, log=log)
     sp = SamplingParams(max_tokens=a.output_len, temperature=a.temperature, ignore_eos=True)
     rng = np.random.default_rng(1000 + rank)
     vocab_hi = min(mcfg.vocab_size, 150000)
+    pair = None
+    if pd:
+        from aws_k8s_ansible_provisioner_amd.parallel.pd_driver import PDPair
+
+        ctrl = dist.new_group(backend="gloo")  # small metadata messages on the host
+        pair = PDPair(eng, rank, world, ctrl_group=ctrl, data_group=None)
 
     def wave():
+        if pd:
+            if is_prefill:
+                prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
+                pair.run_prefill(prompts, sp)
+                return 0, []
+            r = pair.run_decode(sp, time.time())
+            return r["output_tokens"], r["ttft"]
         prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
         outs = eng.generate(None, sp, prompt_ids=prompts)
         ntok = sum(len(o.output_ids) for o in outs)
@@ -99,6 +132,7 @@ def main() -> int:
             torch.cuda.synchronize()
 
     for i in range(a.warmup):
+        barrier()
         t = time.time()
         wave()
         log(f"[bench] warmup wave {i} {time.time() - t:.2f}s")
@@ -106,6 +140,8 @@ def main() -> int:
     t0 = time.perf_counter()
     total, ttfts = 0, []
     for i in range(a.steps):
+        if pd and i:
+            barrier()  # P/D: every wave starts together on both sides (TTFT clock)
         n, tt = wave()
         total += n
         ttfts += tt
@@ -125,8 +161,10 @@ def main() -> int:
         dist.all_reduce(t_tok)
         dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
         dist.all_gather(t_all, torch.tensor([p50_local], dtype=torch.float64, device=dev))
-        stats = torch.tensor([t_tok.item(), t_el.item(),
-                              statistics.median([x.item() for x in t_all])])
+        p50s = [x.item() for x in t_all]
+        if pd:  # TTFT is observed on the decode ranks
+            p50s = p50s[world // 2:]
+        stats = torch.tensor([t_tok.item(), t_el.item(), statistics.median(p50s)])
     tok, el, p50 = float(stats[0]), float(stats[1]), float(stats[2])
     if rank == 0:
         res = {
@@ -145,18 +183,20 @@ def main() -> int:
             "p50_ttft_ms": round(p50 * 1000, 2),
             "config": {
                 "model": mcfg.hf_id,
-                "global_batch": a.num_requests * max(world, 1),
+                "global_batch": a.num_requests * (world // 2 if pd else max(world, 1)),
                 "seq_len": a.input_len + a.output_len,
                 "input_len": a.input_len,
                 "output_len": a.output_len,
-                "requests_per_gpu": a.num_requests,
-                "parallelism": f"dp{max(world, 1)}",
+                ("requests_per_pd_pair" if pd else "requests_per_gpu"): a.num_requests,
+                "parallelism": (f"pd{world // 2}x{world // 2}" if pd else f"dp{max(world, 1)}"),
                 "max_num_seqs": a.max_num_seqs,
                 "sampling": "greedy" if a.temperature <= 0 else f"T={a.temperature}",
                 "hipgraph_decode": not a.enforce_eager,
             },
         }
         print(json.dumps(res), flush=True)
+    if pair is not None:
+        pair.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

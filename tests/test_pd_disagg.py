@@ -109,3 +109,74 @@ def test_pd_generation_matches_monolithic(pd_servers):
     # the prefill server released the held blocks after the push
     m = urllib.request.urlopen(pre_url + "/metrics").read().decode()
     assert "vllm:gpu_cache_usage_perc" in m
+
+
+_PD_WORKER = r"""
+import json, os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"])
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
+from aws_k8s_ansible_provisioner_amd.parallel.pd_driver import PDPair
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo", rank=rank, world_size=2)
+eng = LLMEngine(EngineConfig(model="tiny-qwen3", device="cpu", max_model_len=256, max_num_seqs=8,
+                             max_num_batched_tokens=64, block_size=32, num_gpu_blocks=128,
+                             kv_role="prefill" if rank == 0 else "decode"), log=lambda *a: None)
+pair = PDPair(eng, rank, 2, ctrl_group=dist.new_group(backend="gloo"))
+prompts = [list(range(5, 5 + 30 + 7 * i)) for i in range(5)]
+sp = SamplingParams(max_tokens=9, temperature=0, ignore_eos=True)
+outs = {}
+if rank == 0:
+    pair.run_prefill(prompts, sp)
+else:
+    orig = eng.step
+    def step():
+        res = orig()
+        for o in res:
+            if o.finished:
+                outs[len(o.prompt_ids)] = o.output_ids
+        return res
+    eng.step = step
+    r = pair.run_decode(sp)
+    assert r["finished"] == 5 and r["output_tokens"] == 45, r
+    print("PD_OUT " + json.dumps({str(k): v for k, v in outs.items()}), flush=True)
+pair.close()
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def test_pd_driver_matches_monolithic(tmp_path):
+    """bench.py --mode pd's in-process P/D data path (gloo, 2 ranks) == monolithic greedy."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    script = tmp_path / "pd_worker.py"
+    script.write_text(_PD_WORKER)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), REPO=repo)
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e.decode()[-3000:]
+    line = [ln for ln in outs[1][0].decode().splitlines() if ln.startswith("PD_OUT ")][0]
+    got = json.loads(line[len("PD_OUT "):])
+    ref = LLMEngine(EngineConfig(model="tiny-qwen3", device="cpu", max_model_len=256,
+                                 max_num_seqs=8, max_num_batched_tokens=64, block_size=32,
+                                 num_gpu_blocks=128), log=lambda *a: None)
+    prompts = [list(range(5, 5 + 30 + 7 * i)) for i in range(5)]
+    exp = ref.generate(None, SamplingParams(max_tokens=9, temperature=0, ignore_eos=True),
+                       prompt_ids=prompts)
+    for p_, o in zip(prompts, exp):
+        assert got[str(len(p_))] == o.output_ids
