@@ -208,7 +208,16 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     const int remaining = (int)r->tokens.size() - r->num_computed;
     const int q = std::min(remaining, budget);
     // keep a small reserve so admitted sequences can decode a few steps
-    if (!ensure_blocks(*r, r->num_computed + q)) break;
+    if (!ensure_blocks(*r, r->num_computed + q)) {
+      if (running_.empty() && sched.empty()) {
+        // nothing holds blocks and it still does not fit: it never will
+        waiting_.pop_front();
+        finish(*r, FINISH_ABORT);
+        sched_finished_.emplace_back(r->id, FINISH_ABORT);
+        continue;
+      }
+      break;
+    }
     waiting_.pop_front();
     r->status = RUNNING;
     running_.push_back(r);
@@ -232,8 +241,11 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
       }
       // out of blocks (or seq too long): preempt the youngest other sequence
       Request* victim = running_.back();
-      if ((int)r->blocks.size() >= mb) {
+      if ((int)r->blocks.size() >= mb || (victim == r && i == 0)) {
+        // too long, or alone and the whole pool still cannot hold its next token:
+        // end it here (length-capped) instead of preempting it forever
         finish(*r, FINISH_LENGTH);
+        sched_finished_.emplace_back(r->id, FINISH_LENGTH);
         running_.erase(running_.begin() + i);
         continue;
       }
@@ -299,6 +311,13 @@ void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_i
                        std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish,
                        std::vector<int32_t>& out_first) {
   if (n != (int)last_sampled_.size()) throw std::invalid_argument("sample count mismatch");
+  for (const auto& f : sched_finished_) {
+    out_ids.push_back(f.first);
+    out_tokens.push_back(-1);
+    out_finish.push_back(f.second);
+    out_first.push_back(0);
+  }
+  sched_finished_.clear();
   for (Request* r : running_) publish_full_blocks(*r);
   for (int i = 0; i < n; ++i) {
     Request* r = last_sampled_[i];

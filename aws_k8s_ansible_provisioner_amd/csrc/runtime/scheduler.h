@@ -110,7 +110,9 @@ class Scheduler {
 
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
-  bool has_work() const { return !waiting_.empty() || !running_.empty(); }
+  bool has_work() const {
+    return !waiting_.empty() || !running_.empty() || !sched_finished_.empty();
+  }
   const BlockManager& blocks() const { return bm_; }
   BlockManager& blocks_mut() { return bm_; }
   const Request* get(int64_t id) const;
@@ -149,6 +151,9 @@ class Scheduler {
   std::deque<Request*> waiting_;
   std::vector<Request*> running_;
   std::vector<Request*> last_sampled_;  // order of samples in the last step
+  // requests the scheduler itself had to finish (KV pool can never hold them); reported by
+  // the next update() as events with token -1
+  std::vector<std::pair<int64_t, int>> sched_finished_;
   std::unordered_map<int64_t, std::vector<int32_t>> held_;
   int64_t preemptions_ = 0;
 };

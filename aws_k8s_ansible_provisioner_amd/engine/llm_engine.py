@@ -213,12 +213,16 @@ class LLMEngine:
             self._apply_aborts()
         with self._lock:
             info = self.sched.schedule(self.runner.host_buffers())
-        if info["num_seqs"] == 0:
-            return []
         if info["num_preempted"]:
             self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
         t1 = time.time()
-        toks = self.runner.execute(info)
+        if info["num_seqs"] == 0:
+            # nothing runnable; still flush requests the scheduler had to end (token -1)
+            if not self.sched.has_work():
+                return []
+            toks = np.zeros(0, dtype=np.int64)
+        else:
+            toks = self.runner.execute(info)
         now = time.time()
         self.timers["schedule"] += t1 - t0
         self.timers["execute"] += now - t1
@@ -239,7 +243,9 @@ class LLMEngine:
                 st.first_token_time = now
                 m.ttft.observe(now - st.arrival, model_name=name)
             reason = FINISH_REASONS.get(f)
-            if st.stream:
+            if tok < 0:  # ended by the scheduler (KV pool can never hold it): no new token
+                delta = ""
+            elif st.stream:
                 st.output_ids.append(tok)
                 delta = "" if (reason == "stop" and tok == self.mcfg.eos_id) else \
                     self.tokenizer.decode_token(tok)

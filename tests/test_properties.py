@@ -117,18 +117,17 @@ def test_scheduler_random_workload_invariants(seed, prefix, nblocks):
             if s.abort_request(victim):
                 aborted.add(victim)
         i = s.schedule(b)
-        if i["num_seqs"] == 0:
-            continue
-        _check_batch(i, b, cfg)
+        if i["num_seqs"]:
+            _check_batch(i, b, cfg)
         toks = rng.integers(2, 50, size=i["num_samples"]).astype(np.int64)
-        ids, new, fin, first = s.update(toks)
+        ids, new, fin, first = s.update(toks)  # also flushes scheduler-ended requests
         for rid, f in zip(ids, fin):
             if f:
                 outs[rid] = s.output_tokens(rid)
                 s.release(rid)
     assert not s.has_work()
     for rid, o in outs.items():
-        assert 1 <= len(o) <= max_tok[rid]
+        assert len(o) <= max_tok[rid]
     assert s.num_free_blocks() == nblocks
 
 
