@@ -453,11 +453,16 @@ __global__ __launch_bounds__(256) void paged_attn_decode_persistent_kernel(AttnP
 // ----------------------------------------------------------------------------------
 constexpr int kFaRows = 128;
 constexpr int kFaKeys = 64;
+constexpr int kFaBtCache = 1024;  // chunk -> block id cache in LDS (32768 keys)
 
-__global__ __launch_bounds__(256) void paged_attn_prefill_fa_kernel(AttnParams p) {
-  // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB, one __shared__ object
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 2 * kFaKeys * kD];
-  const int tile = blockIdx.x;
+__global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParams p) {
+  // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
+  // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 2 * kFaKeys * kD + 2 * kFaBtCache];
+  int* bt_s = reinterpret_cast<int*>(lds + 2 * 2 * kFaKeys * kD);
+  // causal work grows with a tile's position: dispatch the map back to front so the
+  // longest tiles start first and the grid's tail is made of short ones
+  const int tile = gridDim.x - 1 - blockIdx.x;
   const int kvh = blockIdx.y;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -500,19 +505,22 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_fa_kernel(AttnParams p
   // staging: 1024 16-B pieces of K and 1024 of V per tile, 4 + 4 per thread
   bf16x8 kst[4], vst[4];
   auto stage_load = [&](int t) {
+    // block ids first (LDS), then all 8 global loads back to back: no wait between them
+    int blk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = (tid + 256 * i) >> 9;
+      blk[i] = bt_s[min(t * 2 + c, last_chunk)];
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int pc = tid + 256 * i;   // 0..1023
       const int c = pc >> 9;           // 32-key chunk of the tile
       const int within = pc & 511;
-      const int chunk = min(t * 2 + c, last_chunk);
-      const int tok = chunk * 32;
-      const int blk = bt[tok / BS];
-      const int off = tok % BS;
-      const size_t base = ((size_t)blk * p.Hkv + kvh) * BS * kD;
-      kst[i] = *reinterpret_cast<const bf16x8*>(p.k_cache + base + (size_t)off * kD + within * 8);
-      vst[i] = *reinterpret_cast<const bf16x8*>(p.v_cache + base + (size_t)(off >> 3) * kD * 8 +
-                                                within * 8);
+      const int off = (min(t * 2 + c, last_chunk) * 32) % BS;
+      const size_t base = ((size_t)blk[i] * p.Hkv + kvh) * BS * kD + (size_t)off * kD;
+      kst[i] = *reinterpret_cast<const bf16x8*>(p.k_cache + base + within * 8);
+      vst[i] = *reinterpret_cast<const bf16x8*>(p.v_cache + base + within * 8);
     }
   };
   auto stage_store = [&](int buf) {
@@ -542,30 +550,35 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_fa_kernel(AttnParams p
     for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
 
+  for (int c = tid; c <= last_chunk; c += 256) bt_s[c] = bt[c * 32 / BS];
+  __syncthreads();
   stage_load(0);
   stage_store(0);
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     const bool more = t + 1 < ntiles;
-    if (more) stage_load(t + 1);
+    // timing experiments (wrong numerics): flags 256 = no K/V reloads, 512 = no compute
+    if (more && !(p.flags & 256)) stage_load(t + 1);
     const int key0 = t * kFaKeys;
-    if (wave_active && key0 <= w_limit) {
+    if (wave_active && key0 <= w_limit && !(p.flags & 512)) {
       const bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
       const bf16* vl = kl + kFaKeys * kD;
+      // S^T = K . Q^T for the two 32-key sub-tiles (interleaved: independent chains)
       f32x16 sacc[2];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
+      for (int k = 0; k < 2; ++k)
 #pragma unroll
         for (int j = 0; j < 16; ++j) sacc[k][j] = 0.f;
-        const int key = 32 * k + r;
 #pragma unroll
-        for (int s8 = 0; s8 < 8; ++s8) {
+      for (int s8 = 0; s8 < 8; ++s8)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int key = 32 * k + r;
           const bf16x8 a = *reinterpret_cast<const bf16x8*>(
               kl + key * kD + (((2 * s8 + h) ^ (key & 15)) * 8));
           sacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s8], sacc[k], 0, 0, 0);
         }
-      }
       // scale (log2 domain), causal mask, running max
       const bool need_mask = key0 + kFaKeys - 1 > w_min_limit;
       float mx = -1e30f;
@@ -583,13 +596,14 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_fa_kernel(AttnParams p
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run, mx);
-      const float alpha = exp2f(m_run - m_new);
+      // raw v_exp_f32 (no denormal range fix-up: arguments are <= 0, tiny results flush)
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       float rs = 0.f;
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float e = exp2f(sacc[k][j] - m_new);
+          const float e = __builtin_amdgcn_exp2f(sacc[k][j] - m_new);
           sacc[k][j] = e;
           rs += e;
         }
@@ -600,7 +614,8 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_fa_kernel(AttnParams p
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
-      // O^T += V^T . P^T
+      // O^T += V^T . P^T: P^T from the S^T accumulators; V^T fragments loaded per (k, s2)
+      // pair ahead of their 4 independent (per d-tile) MFMAs
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -609,15 +624,18 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_fa_kernel(AttnParams p
 #pragma unroll
           for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[k][8 * s2 + j]);
           const int g = 4 * k + 2 * s2;
+          bf16x8 va[4];
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) {
             const int d = 32 * dt + r;
             const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vl + (g * kD + d) * 8 + 4 * h);
             const bf16x4 hi =
                 *reinterpret_cast<const bf16x4*>(vl + ((g + 1) * kD + d) * 8 + 4 * h);
-            const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, oacc[dt], 0, 0, 0);
+            va[dt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[dt], pb, oacc[dt], 0, 0, 0);
         }
     }
     if (more) stage_store(buf ^ 1);

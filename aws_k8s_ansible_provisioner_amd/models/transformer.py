@@ -41,10 +41,10 @@ class AttnBatch:
     q_start: torch.Tensor        # [B+1] int32
     tile_seq: Optional[torch.Tensor] = None  # prefill tile map
     tile_row: Optional[torch.Tensor] = None
-    tile_rows: int = 64          # q rows per tile of the map (128: flash-style kernel)
     num_parts: int = 1           # decode split-KV partitions
     part_size: int = 512
     workspace: Optional[tuple] = None
+    tile_rows: int = 64          # q rows per prefill tile of the map (128: flash-style kernel)
 
 
 @dataclasses.dataclass
