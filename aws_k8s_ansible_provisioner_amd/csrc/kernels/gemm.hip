@@ -22,14 +22,17 @@ constexpr int GBM = 64, GBN = 64, GBK = 64;
 // LDS tile [64 rows][64 k] bf16 = 8 chunks of 16 B per row; chunk' = chunk ^ (row & 7).
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
-template <bool SPLIT, bool CHECK>
+template <bool SPLIT, bool CHECK, bool INREDUCE = false>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ X,
                                                         const bf16* __restrict__ W,
                                                         bf16* __restrict__ Y,
                                                         float* __restrict__ ws, int M, int N,
                                                         int K, int ldx, int ldw, int ldy,
-                                                        int k_per_split) {
-  __shared__ bf16x8 lds[2][2][GBM * 8];  // [buf][A|B][row*8+chunk]
+                                                        int k_per_split,
+                                                        int* __restrict__ counters) {
+  // [buf][A|B][row*8+chunk]; the last element doubles as the split-K "last arriver" flag
+  // (one __shared__ object: a second one makes hipcc drain vmcnt in the k-loop)
+  __shared__ bf16x8 lds[2][2][GBM * 8];
   const int tiles_n = (N + GBN - 1) / GBN;
   const int tiles_m = (M + GBM - 1) / GBM;
   const int ntiles = tiles_n * tiles_m;
@@ -126,6 +129,48 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
           Y[(size_t)row * ldy + col] = f2bf(acc[i][j][r]);
       }
     }
+  if constexpr (SPLIT && INREDUCE) {
+    // In-launch split-K combine (cdna_hip_programming.md §5 "Projection GEMM at M = 256"
+    // item 2): publish this slice's slab with an agent-scope release, take a ticket; the
+    // slice drawing the last ticket acquires and sums all slabs of the tile into Y, then
+    // re-arms the counter for the next call (graph-replay safe).  No reduce launch.
+    const int S = gridDim.y;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(&lds[1][1][GBM * 8 - 1]);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(&counters[lt], 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      *flag = old == S - 1;
+    }
+    __syncthreads();
+    if (*flag) {
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        counters[lt] = 0;
+      }
+      __syncthreads();
+      // 64x64 tile, 256 threads: each thread 4 rows x 4 consecutive columns
+      const int cc = (tid & 15) * 4;
+      const int rr = tid >> 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + rr + 16 * q;
+        const int col = n0 + cc;
+        if (row >= M || col >= N) continue;
+        f32x4 acc4 = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int z = 0; z < S; ++z)
+          acc4 += *reinterpret_cast<const f32x4*>(ws + ((size_t)z * M + row) * N + col);
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = f2bf(acc4[j]);
+        *reinterpret_cast<bf16x4*>(Y + (size_t)row * ldy + col) = o;
+      }
+    }
+  }
 }
 
 // sum S fp32 partial slabs [S, M, N] -> bf16 Y
@@ -153,7 +198,7 @@ int gemm_splitk_choice(int M, int N, int K) {
 }
 
 void launch_gemm_bf16(const void* X, const void* W, void* Y, float* ws, int M, int N, int K,
-                      int ldx, int ldw, int ldy, int splitk, hipStream_t st) {
+                      int ldx, int ldw, int ldy, int splitk, hipStream_t st, int* counters) {
   if (M == 0 || N == 0) return;
   const int tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   int kps = (K + splitk - 1) / splitk;
@@ -161,18 +206,22 @@ void launch_gemm_bf16(const void* X, const void* W, void* Y, float* ws, int M, i
   const int S = (K + kps - 1) / kps;
   dim3 grid(tiles, S);
   const bool full = M % GBM == 0 && N % GBN == 0 && K % kps == 0 && kps % GBK == 0;
-#define GEMM_LAUNCH(SPL, CHK)                                                                 \
-  gemm_bf16_kernel<SPL, CHK><<<grid, 256, 0, st>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, \
-                                                   ws, M, N, K, ldx, ldw, ldy, kps)
+#define GEMM_LAUNCH(SPL, CHK, RED)                                                            \
+  gemm_bf16_kernel<SPL, CHK, RED><<<grid, 256, 0, st>>>((const bf16*)X, (const bf16*)W,         \
+                                                        (bf16*)Y, ws, M, N, K, ldx, ldw, ldy,  \
+                                                        kps, counters)
   if (S == 1) {
-    if (full) GEMM_LAUNCH(false, false); else GEMM_LAUNCH(false, true);
+    if (full) GEMM_LAUNCH(false, false, false); else GEMM_LAUNCH(false, true, false);
+  } else if (counters != nullptr && N % 4 == 0) {
+    // split-K combined inside the launch by each tile's last-arriving slice
+    if (full) GEMM_LAUNCH(true, false, true); else GEMM_LAUNCH(true, true, true);
   } else {
-    if (full) GEMM_LAUNCH(true, false); else GEMM_LAUNCH(true, true);
-#undef GEMM_LAUNCH
+    if (full) GEMM_LAUNCH(true, false, false); else GEMM_LAUNCH(true, true, false);
     long blocks = ((long)M * N / 4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_kernel<<<(int)blocks, 256, 0, st>>>(ws, (bf16*)Y, S, M, N, ldy);
   }
+#undef GEMM_LAUNCH
 }
 
 }  // namespace akap

@@ -63,8 +63,11 @@ void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s);
 
 // ---- gemm.hip ----
 int gemm_splitk_choice(int M, int N, int K);
+// counters: zero-initialised int32 per-tile tickets (>= tiles) -> split-K partials are
+// combined inside the launch by the last-arriving slice; nullptr -> separate reduce pass
 void launch_gemm_bf16(const void* X, const void* W, void* Y, float* ws, int M, int N, int K,
-                      int ldx, int ldw, int ldy, int splitk, hipStream_t st);
+                      int ldx, int ldw, int ldy, int splitk, hipStream_t st,
+                      int* counters = nullptr);
 
 // ---- sampling.hip ----
 struct SampleParams {

@@ -559,7 +559,9 @@ TORCH_LIBRARY(akap, m) {
       "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
       "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs) -> ()");
   m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
-  m.def("gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int splitk) -> ()");
+  m.def(
+      "gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int splitk, "
+      "Tensor(c!)? counters=None) -> ()");
   m.def("gemm_splitk(int M, int N, int K) -> int");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");
   m.def("car_ipc_handles(int h) -> Tensor");

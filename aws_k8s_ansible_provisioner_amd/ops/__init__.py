@@ -207,8 +207,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
         ws = _EMPTY_F32.get(x.device)
         if ws is None:
             ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
-    torch.ops.akap.gemm(out, x, w, ws, s)
+    torch.ops.akap.gemm(out, x, w, ws, s, gemm_counters(x.device) if s > 1 else None)
     return out
+
+
+_COUNTERS: dict = {}
+
+
+def gemm_counters(device) -> torch.Tensor:
+    """Zeroed per-tile split-K tickets shared by every custom-GEMM launch on `device`
+    (launches on one stream are ordered; each tile's last arriver re-arms its counter)."""
+    c = _COUNTERS.get(device)
+    if c is None:
+        c = _COUNTERS[device] = torch.zeros(1 << 16, dtype=torch.int32, device=device)
+    return c
 
 
 _EMPTY_F32: dict = {}

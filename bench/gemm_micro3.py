@@ -57,9 +57,11 @@ for M in Ms:
             torch.nn.functional.linear(x, ws[0])
             torch.cuda.synchronize()
         t_bl = timed(lambda i: torch.nn.functional.linear(x, ws[i % copies]), iters)
-        t_hip = timed(lambda i: torch.ops.akap.gemm(y, x, ws[i % copies], wsp, s), iters)
+        cnt = ops.gemm_counters(x.device)
+        t_hip = timed(lambda i: torch.ops.akap.gemm(y, x, ws[i % copies], wsp, s, cnt), iters)
+        t_hip2 = timed(lambda i: torch.ops.akap.gemm(y, x, ws[i % copies], wsp, s), iters)
         print(f"M={M:4d} {name:16s} N={N:6d} K={K:5d}  blaslt {t_bl:8.2f} us "
               f"({wbytes / t_bl / 1e6:5.2f} TB/s)   hip(splitk={s}) {t_hip:8.2f} us "
-              f"({wbytes / t_hip / 1e6:5.2f} TB/s)", flush=True)
+              f"({wbytes / t_hip / 1e6:5.2f} TB/s)  [separate reduce: {t_hip2:7.2f} us]", flush=True)
         del ws
         torch.cuda.empty_cache()

@@ -371,17 +371,22 @@ def test_kv_gather_scatter_roundtrip():
 @pytest.mark.parametrize("M", [1, 7, 64, 100, 256, 512])
 @pytest.mark.parametrize("N,K", [(4096, 1024), (1024, 2048), (6144, 1024), (1024, 3072),
                                  (1000, 520), (64, 64)])
-def test_decode_gemm(M, N, K):
+@pytest.mark.parametrize("inlaunch", [False, True])
+def test_decode_gemm(M, N, K, inlaunch):
     torch.manual_seed(M + N + K)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
-    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ref_ = (x.float() @ w.float().t())
     s = ops.gemm_splitk(M, N, K)
     ws = torch.empty(max(1, s * M * N), device=DEV, dtype=torch.float32)
-    torch.ops.akap.gemm(y, x, w, ws, s)
-    ref_ = (x.float() @ w.float().t())
-    err = (y.float() - ref_).abs().max().item()
-    assert err <= 2e-2 * ref_.abs().max().item() + 1e-2, err
+    cnt = ops.gemm_counters(x.device) if inlaunch else None
+    for _ in range(3):  # repeated calls: the in-launch tickets must re-arm
+        y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        torch.ops.akap.gemm(y, x, w, ws, s, cnt)
+        err = (y.float() - ref_).abs().max().item()
+        assert err <= 2e-2 * ref_.abs().max().item() + 1e-2, err
+    if cnt is not None:
+        assert int(cnt.abs().sum()) == 0  # every ticket re-armed
 
 
 def test_decode_gemm_strided_input():
