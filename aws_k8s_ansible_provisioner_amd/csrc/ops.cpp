@@ -226,7 +226,8 @@ int64_t gemm_splitk(int64_t M, int64_t N, int64_t K) {
   return akap::gemm_splitk_choice(M, N, K);
 }
 
-void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk) {
+void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk,
+          std::optional<Tensor> counters) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D tensors");
@@ -238,10 +239,17 @@ void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk) {
     TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= splitk * M * N,
                 "gemm: fp32 workspace of splitk*M*N");
   }
+  int* cnt = nullptr;
+  if (counters && splitk > 1) {
+    TORCH_CHECK(counters->scalar_type() == at::kInt && counters->is_cuda(), "counters int32");
+    TORCH_CHECK(counters->numel() >= (int64_t)((M + 63) / 64) * ((N + 63) / 64),
+                "counters: one per 64x64 tile");
+    cnt = counters->data_ptr<int>();
+  }
   const c10::DeviceGuard g(x.device());
   akap::launch_gemm_bf16(x.data_ptr(), w.data_ptr(), out.data_ptr(),
                          splitk > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, x.stride(0),
-                         w.stride(0), out.stride(0), splitk, cur_stream());
+                         w.stride(0), out.stride(0), splitk, cur_stream(), cnt);
 }
 
 void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,

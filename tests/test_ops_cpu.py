@@ -157,3 +157,16 @@ def test_gemm_splitk_fills_chip():
         s = ops.gemm_splitk(M, N, K)
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
         assert tiles * s >= 256 or K // (s * 2) < 256
+
+
+def test_native_library_registers_all_ops():
+    """_C.so must load on a CPU host too (op schemas are checked at registration: a C++/
+    schema mismatch aborts the process at import on the GPU box)."""
+    import os
+    if not os.path.exists(ops._LIB):
+        pytest.skip("extension not built")
+    assert ops.load_native(), ops._load_error
+    for name in ("rmsnorm", "fused_add_rmsnorm", "qk_norm_rope_cache", "paged_attention_prefill",
+                 "paged_attention_decode", "paged_attention_decode_fused", "sample", "gemm",
+                 "moe_gemm", "moe_combine", "car_all_reduce", "kv_gather", "embedding"):
+        assert hasattr(torch.ops.akap, name), name
