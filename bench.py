@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--enforce-eager", action="store_true")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree: with --tp WORLD_SIZE the whole job is ONE "
+                         "engine replica (Llama-3-70B TP=8 config; Mixtral EP with "
+                         "AKAP_MOE_MODE=ep)")
     ap.add_argument("--mode", default="mono", choices=["mono", "pd"],
                     help="mono: every rank a monolithic replica (DP); pd: ranks [0,W/2) prefill, "
                          "[W/2,W) decode, KV handed over RCCL (Llama-3-8B disagg config)")
@@ -98,7 +102,21 @@ def main() -> int:
                         gpu_memory_utilization=0.45 if (pd and a.dist_backend == "gloo")
                         else 0.90)
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if rank == 0 else (lambda *x: None)
-    eng = LLMEngine(ecfg, mcfg, log=log)
+    tp_bc = None
+    if a.tp > 1:
+        if a.tp != world or pd:
+            print("error: --tp must equal WORLD_SIZE (one TP replica per job), no --mode pd",
+                  file=sys.stderr)
+            return 2
+        from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
+
+        ecfg.tensor_parallel_size = a.tp
+        ecfg.seed = 1234
+        eng, tp_bc = make_tp_engine(ecfg, log=log)
+        if eng is None:  # ranks != 0 mirrored every step until rank 0 shut the group down
+            return 0
+    else:
+        eng = LLMEngine(ecfg, mcfg, log=log)
     sp = SamplingParams(max_tokens=a.output_len, temperature=a.temperature, ignore_eos=True)
     rng = np.random.default_rng(1000 + rank)
     vocab_hi = min(mcfg.vocab_size, 150000)
@@ -126,7 +144,7 @@ def main() -> int:
     def barrier():
         if gpu:
             torch.cuda.synchronize()
-        if world > 1:
+        if world > 1 and tp_bc is None:  # TP ranks run in lock-step with rank 0 already
             dist.barrier()
         if gpu:
             torch.cuda.synchronize()
@@ -153,7 +171,7 @@ def main() -> int:
 
     p50_local = statistics.median(ttfts) if ttfts else 0.0
     stats = torch.tensor([float(total), el, p50_local], dtype=torch.float64)
-    if world > 1:
+    if world > 1 and tp_bc is None:
         dev = torch.device("cuda", local) if gpu else torch.device("cpu")
         t_tok = torch.tensor([float(total)], dtype=torch.float64, device=dev)
         t_el = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -176,19 +194,21 @@ def main() -> int:
             "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1000, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.tp > 1 else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic random token-id prompts, random-init weights",
             "p50_ttft_ms": round(p50 * 1000, 2),
             "config": {
                 "model": mcfg.hf_id,
-                "global_batch": a.num_requests * (world // 2 if pd else max(world, 1)),
+                "global_batch": a.num_requests * (world // 2 if pd else
+                                                  1 if a.tp > 1 else max(world, 1)),
                 "seq_len": a.input_len + a.output_len,
                 "input_len": a.input_len,
                 "output_len": a.output_len,
                 ("requests_per_pd_pair" if pd else "requests_per_gpu"): a.num_requests,
-                "parallelism": (f"pd{world // 2}x{world // 2}" if pd else f"dp{max(world, 1)}"),
+                "parallelism": (f"pd{world // 2}x{world // 2}" if pd else
+                                f"tp{a.tp}" if a.tp > 1 else f"dp{max(world, 1)}"),
                 "max_num_seqs": a.max_num_seqs,
                 "sampling": "greedy" if a.temperature <= 0 else f"T={a.temperature}",
                 "hipgraph_decode": not a.enforce_eager,
@@ -197,6 +217,9 @@ def main() -> int:
         print(json.dumps(res), flush=True)
     if pair is not None:
         pair.close()
+    if tp_bc is not None:
+        tp_bc.shutdown()  # releases the mirroring ranks, destroys the process group
+        return 0
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -1,0 +1,61 @@
+"""bench.py contract on CPU (tiny models): one JSON line with the driver's keys, for the
+monolithic (DP), tensor-parallel (--tp, also Mixtral EP) and disaggregated (--mode pd)
+layouts; multi-rank runs go through torch.distributed.run on 127.0.0.1 with gloo."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+        "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"}
+SMALL = ["--num-requests", "6", "--input-len", "40", "--output-len", "8", "--device", "cpu",
+         "--max-model-len", "256", "--steps", "1", "--warmup", "1"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, nproc=1, env=None):
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(REPO, "bench.py")] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
+               f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
+               "--gpus", str(nproc)] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd="/tmp",
+                       env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert KEYS <= set(res), set(res) ^ KEYS
+    assert res["value"] > 0 and res["dtype"] == "bf16" and res["higher_is_better"] is True
+    return res
+
+
+def test_bench_mono_single_process():
+    res = _run(["--model", "tiny-qwen3"] + SMALL)
+    assert res["n_gpus"] == 1 and res["config"]["parallelism"] == "dp1"
+    assert res["scaling"] == "weak"
+
+
+@pytest.mark.parametrize("model,env", [("tiny-llama", {}), ("tiny-mixtral", {"AKAP_MOE_MODE": "ep"})])
+def test_bench_tensor_parallel(model, env):
+    res = _run(["--tp", "2", "--model", model] + SMALL, nproc=2, env=env)
+    assert res["config"]["parallelism"] == "tp2" and res["scaling"] == "strong"
+
+
+def test_bench_pd_disaggregated():
+    res = _run(["--mode", "pd", "--model", "tiny-qwen3"] + SMALL, nproc=2)
+    assert res["config"]["parallelism"] == "pd1x1"
+    assert res["p50_ttft_ms"] > 0
