@@ -59,6 +59,9 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
     """
     global _STATE
     rank, world, local = env_rank_info()
+    if torch.cuda.is_available():
+        # more ranks than devices only in single-GPU rehearsals (gloo): share the device
+        local = local % max(1, torch.cuda.device_count())
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if world > 1 and not dist.is_initialized():

@@ -75,9 +75,12 @@ def main() -> int:
     if world != a.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
     gpu = torch.cuda.is_available() and a.device != "cpu"
+    shared_ranks = 1
     if gpu:
         # more ranks than GPUs only in the single-GPU gloo rehearsal: share the device
-        local = local % max(1, torch.cuda.device_count())
+        ndev = max(1, torch.cuda.device_count())
+        shared_ranks = max(1, -(-world // ndev)) if world > ndev else 1
+        local = local % ndev
         torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -99,8 +102,8 @@ def main() -> int:
                         seed=1234 + (rank % (world // 2) if pd else rank),  # P/D pair: same weights
                         num_gpu_blocks=None if gpu else 512,
                         kv_role=("prefill" if is_prefill else "decode") if pd else "both",
-                        gpu_memory_utilization=0.45 if (pd and a.dist_backend == "gloo")
-                        else 0.90)
+                        # ranks sharing one GPU (single-GPU gloo rehearsal) split its memory
+                        gpu_memory_utilization=0.90 / max(1, shared_ranks))
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if rank == 0 else (lambda *x: None)
     tp_bc = None
     if a.tp > 1:
