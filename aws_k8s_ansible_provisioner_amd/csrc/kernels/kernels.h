@@ -81,8 +81,16 @@ struct SampleParams {
   const int* steps;          // [B] per-request step counter mixed into the RNG
   int64_t* out_tokens;       // [B]
   float* out_logprobs;       // [B] log-prob of the sampled token (may be null)
+  int greedy_logprobs;       // also compute log-probs for greedy rows (one extra pass)
 };
 void launch_sample(const SampleParams& p, int B, hipStream_t s);
+// OpenAI/vLLM penalties on logits in place, for unique (row, token) entries:
+// repetition (prompt + output tokens, divide positive / multiply negative logits),
+// frequency * count and presence * [count > 0] (output tokens; count 0 = prompt-only)
+void launch_apply_penalties(void* logits, int ld, int is_bf16, const int32_t* rows,
+                            const int32_t* toks, const int32_t* counts, const float* presence,
+                            const float* frequency, const float* repetition, int n,
+                            hipStream_t s);
 void launch_argmax(const void* logits, int ld, int V, int is_bf16, int64_t* out, int B,
                    hipStream_t s);
 

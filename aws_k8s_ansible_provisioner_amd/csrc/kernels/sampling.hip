@@ -140,9 +140,15 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(SampleParams p) {
   const float temp = p.temperature ? p.temperature[row] : 0.f;
   if (!(temp > 0.f)) {
     ArgBest b = row_argmax(x, V, sv, si);
+    float lp = 0.f;
+    if (p.greedy_logprobs && p.out_logprobs) {  // log-softmax of the argmax: -log sum exp(x-M)
+      float z = 0.f;
+      for (int i = threadIdx.x; i < V; i += blockDim.x) z += __expf((float)x[i] - b.v);
+      lp = -__logf(block_sum(z, sv));
+    }
     if (threadIdx.x == 0) {
       p.out_tokens[row] = b.i;
-      if (p.out_logprobs) p.out_logprobs[row] = 0.f;
+      if (p.out_logprobs) p.out_logprobs[row] = lp;
     }
     return;
   }
@@ -198,6 +204,38 @@ void launch_sample(const SampleParams& p, int B, hipStream_t s) {
     sample_kernel<bf16><<<B, kSampThreads, 0, s>>>(p);
   else
     sample_kernel<float><<<B, kSampThreads, 0, s>>>(p);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void apply_penalties_kernel(
+    T* __restrict__ logits, int ld, const int32_t* __restrict__ rows,
+    const int32_t* __restrict__ toks, const int32_t* __restrict__ counts,
+    const float* __restrict__ presence, const float* __restrict__ frequency,
+    const float* __restrict__ repetition, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int r = rows[i];
+  const int c = counts[i];
+  T* px = logits + (size_t)r * ld + toks[i];
+  float x = (float)*px;
+  const float rep = repetition[r];
+  if (rep != 1.f) x = x > 0.f ? x / rep : x * rep;
+  x -= frequency[r] * (float)c + (c > 0 ? presence[r] : 0.f);
+  *px = (T)x;
+}
+
+void launch_apply_penalties(void* logits, int ld, int is_bf16, const int32_t* rows,
+                            const int32_t* toks, const int32_t* counts, const float* presence,
+                            const float* frequency, const float* repetition, int n,
+                            hipStream_t s) {
+  if (n == 0) return;
+  const int blocks = (n + 255) / 256;
+  if (is_bf16)
+    apply_penalties_kernel<bf16><<<blocks, 256, 0, s>>>((bf16*)logits, ld, rows, toks, counts,
+                                                       presence, frequency, repetition, n);
+  else
+    apply_penalties_kernel<float><<<blocks, 256, 0, s>>>((float*)logits, ld, rows, toks, counts,
+                                                        presence, frequency, repetition, n);
 }
 
 // Greedy fast path straight on bf16 or fp32 logits.

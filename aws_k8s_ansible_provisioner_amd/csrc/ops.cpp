@@ -253,7 +253,7 @@ void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk,
 }
 
 void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
-            Tensor steps, Tensor out_tokens, Tensor out_logprobs) {
+            Tensor steps, Tensor out_tokens, Tensor out_logprobs, bool greedy_logprobs) {
   CHECK_GPU(logits);
   TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16,
               "sampler expects fp32 or bf16 logits");
@@ -275,8 +275,28 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tenso
   p.steps = steps.data_ptr<int>();
   p.out_tokens = out_tokens.data_ptr<int64_t>();
   p.out_logprobs = out_logprobs.numel() ? out_logprobs.data_ptr<float>() : nullptr;
+  p.greedy_logprobs = greedy_logprobs ? 1 : 0;
   const c10::DeviceGuard g(logits.device());
   akap::launch_sample(p, B, cur_stream());
+}
+
+void apply_penalties(Tensor logits, Tensor rows, Tensor toks, Tensor counts, Tensor presence,
+                     Tensor frequency, Tensor repetition) {
+  CHECK_GPU(logits); CHECK_LAST_CONTIG(logits);
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16,
+              "fp32 or bf16 logits");
+  TORCH_CHECK(rows.scalar_type() == at::kInt && toks.scalar_type() == at::kInt &&
+                  counts.scalar_type() == at::kInt, "rows/toks/counts int32");
+  TORCH_CHECK(presence.scalar_type() == at::kFloat && frequency.scalar_type() == at::kFloat &&
+                  repetition.scalar_type() == at::kFloat, "penalties fp32");
+  const int n = rows.numel();
+  TORCH_CHECK(toks.numel() == n && counts.numel() == n, "COO length mismatch");
+  const c10::DeviceGuard g(logits.device());
+  akap::launch_apply_penalties(logits.data_ptr(), logits.stride(0),
+                               logits.scalar_type() == at::kBFloat16, rows.data_ptr<int>(),
+                               toks.data_ptr<int>(), counts.data_ptr<int>(),
+                               presence.data_ptr<float>(), frequency.data_ptr<float>(),
+                               repetition.data_ptr<float>(), n, cur_stream());
 }
 
 void argmax(Tensor logits, Tensor out) {
@@ -565,7 +585,11 @@ TORCH_LIBRARY(akap, m) {
       "Tensor(f!) part_o, int num_parts, int part_size, int G, float scale, float eps) -> ()");
   m.def(
       "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
-      "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs) -> ()");
+      "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs, "
+      "bool greedy_logprobs=False) -> ()");
+  m.def(
+      "apply_penalties(Tensor(a!) logits, Tensor rows, Tensor toks, Tensor counts, "
+      "Tensor presence, Tensor frequency, Tensor repetition) -> ()");
   m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
   m.def(
       "gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int splitk, "
@@ -612,6 +636,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("paged_attention_decode", &paged_attention_decode);
   m.impl("paged_attention_decode_fused", &paged_attention_decode_fused);
   m.impl("sample", &sample);
+  m.impl("apply_penalties", &apply_penalties);
   m.impl("argmax", &argmax);
   m.impl("gemm", &gemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);

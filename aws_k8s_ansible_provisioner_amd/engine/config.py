@@ -53,8 +53,16 @@ class SamplingParams:
     stop_token_ids: list = dataclasses.field(default_factory=list)
     stop: list = dataclasses.field(default_factory=list)  # stop strings (post-detokenize)
     ignore_eos: bool = False
-    logprobs: Optional[int] = None
+    logprobs: Optional[int] = None           # return the sampled token's log-prob
     n: int = 1
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    repetition_penalty: float = 1.0
+
+    @property
+    def has_penalties(self) -> bool:
+        return (self.presence_penalty != 0.0 or self.frequency_penalty != 0.0
+                or self.repetition_penalty != 1.0)
 
     def normalized(self) -> "SamplingParams":
         p = dataclasses.replace(self)
@@ -66,4 +74,8 @@ class SamplingParams:
             p.temperature = 1.0
         if p.temperature < 1e-5:
             p.temperature = 0.0
+        if p.repetition_penalty is None or p.repetition_penalty <= 0:
+            p.repetition_penalty = 1.0
+        p.presence_penalty = float(p.presence_penalty or 0.0)
+        p.frequency_penalty = float(p.frequency_penalty or 0.0)
         return p

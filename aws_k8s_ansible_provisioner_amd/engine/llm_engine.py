@@ -57,6 +57,7 @@ class RequestOutput:
     ttft: Optional[float] = None
     num_cached_tokens: int = 0
     kv_transfer_params: Optional[dict] = None
+    logprobs: Optional[list] = None  # per output token (when the request asked for them)
 
 
 class LLMEngine:
@@ -89,6 +90,7 @@ class LLMEngine:
         self.steps = 0
         self.last_prefix = (0, 0)
         self.timers = {"schedule": 0.0, "execute": 0.0, "post": 0.0}
+        self._n_extra = 0  # live requests that need penalties or log-probs
         self.rank = self.runner.ps.rank
 
     # ------------------------------------------------------------------ requests
@@ -120,7 +122,9 @@ class LLMEngine:
         seed = params.seed if params.seed is not None else (iid * 7919 + self.ecfg.seed)
         st = RequestState(req_id, iid, prompt if isinstance(prompt, str) else None, prompt_ids,
                           params, time.time())
-        st.stream = stream or bool(params.stop)
+        # penalties / log-probs need every token on the host: per-token events
+        st.stream = stream or bool(params.stop) or params.has_penalties or \
+            params.logprobs is not None
         st.hold_kv = hold
         st.traceparent = traceparent
         with self._lock:
@@ -132,6 +136,8 @@ class LLMEngine:
                 self.sched.set_hold_kv(iid, True)
             self.reqs[iid] = st
             self.by_name[req_id] = iid
+            if params.has_penalties or params.logprobs is not None:
+                self._n_extra += 1
         self.metrics.req_total.inc(model_name=self.model_name)
         return req_id
 
@@ -195,6 +201,8 @@ class LLMEngine:
                     self.by_name.pop(st.req_id, None)
                     st.finished, st.finish_reason = True, "abort"
                     self.metrics.success.inc(model_name=self.model_name, finished_reason="abort")
+                    if st.params.has_penalties or st.params.logprobs is not None:
+                        self._n_extra -= 1
                 self.sched.release(iid)
 
     def has_unfinished(self) -> bool:
@@ -216,12 +224,15 @@ class LLMEngine:
         if info["num_preempted"]:
             self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
         t1 = time.time()
+        sample_pos: dict = {}
         if info["num_seqs"] == 0:
             # nothing runnable; still flush requests the scheduler had to end (token -1)
             if not self.sched.has_work():
                 return []
             toks = np.zeros(0, dtype=np.int64)
         else:
+            if self._n_extra:
+                info["extras"], sample_pos = self._step_extras(info)
             toks = self.runner.execute(info)
         now = time.time()
         self.timers["schedule"] += t1 - t0
@@ -243,6 +254,9 @@ class LLMEngine:
                 st.first_token_time = now
                 m.ttft.observe(now - st.arrival, model_name=name)
             reason = FINISH_REASONS.get(f)
+            if tok >= 0 and st.params.logprobs is not None and iid in sample_pos:
+                lps = self.runner.last_logprobs
+                st.logprobs.append(float(lps[sample_pos[iid]]) if lps is not None else 0.0)
             if tok < 0:  # ended by the scheduler (KV pool can never hold it): no new token
                 delta = ""
             elif st.stream:
@@ -294,6 +308,8 @@ class LLMEngine:
                     self.sched.release(iid)
                     self.reqs.pop(iid, None)
                     self.by_name.pop(st.req_id, None)
+                    if st.params.has_penalties or st.params.logprobs is not None:
+                        self._n_extra -= 1
             elif not st.stream:
                 continue  # first-token event of a non-streaming request: metrics only
             kvp = None
@@ -304,11 +320,55 @@ class LLMEngine:
             outs.append(RequestOutput(st.req_id, st.prompt_ids, st.output_ids, [tok], st.text,
                                       delta, st.finished, st.finish_reason,
                                       (st.first_token_time - st.arrival)
-                                      if st.first_token_time else None, cached, kvp))
+                                      if st.first_token_time else None, cached, kvp,
+                                      list(st.logprobs) if st.params.logprobs is not None
+                                      else None))
         self.steps += 1
         self._update_gauges()
         self.timers["post"] += time.time() - now
         return outs
+
+    def _step_extras(self, info: dict):
+        """Penalty COO + log-prob flag for the sampled rows of this step (host side; only
+        called while some live request uses penalties or log-probs)."""
+        npb = self.runner.np
+        rows, toks, counts = [], [], []
+        B = info["num_seqs"]
+        ns = info["num_samples"]
+        pres = np.zeros(max(ns, 1), np.float32)
+        freq = np.zeros(max(ns, 1), np.float32)
+        rep = np.ones(max(ns, 1), np.float32)
+        want_lp = False
+        pos: dict = {}
+        k = 0
+        for s_ in range(B):
+            if not npb["sample_mask"][s_]:
+                continue
+            iid = int(npb["req_ids"][s_])
+            pos[iid] = k
+            st = self.reqs.get(iid)
+            if st is not None:
+                p = st.params
+                want_lp |= p.logprobs is not None
+                if p.has_penalties:
+                    pres[k], freq[k], rep[k] = (p.presence_penalty, p.frequency_penalty,
+                                                p.repetition_penalty)
+                    cnt: dict = {}
+                    for t in st.output_ids:
+                        cnt[t] = cnt.get(t, 0) + 1
+                    if p.repetition_penalty != 1.0:
+                        for t in st.prompt_ids:
+                            cnt.setdefault(t, 0)
+                    for t, c in cnt.items():
+                        rows.append(k)
+                        toks.append(t)
+                        counts.append(c)
+            k += 1
+        extras = {"logprobs": want_lp}
+        if rows:
+            extras["penalties"] = (np.asarray(rows, np.int32), np.asarray(toks, np.int32),
+                                   np.asarray(counts, np.int32), pres, freq, rep)
+        return extras, pos
 
     def _update_gauges(self) -> None:
         m, name = self.metrics, self.model_name

@@ -78,6 +78,7 @@ class ModelRunner:
         # workspace sized for the finest split any bucket uses (256-token partitions)
         self.num_parts = max(1, math.ceil(ecfg.max_model_len / 128))
         self._alloc_buffers()
+        self.last_logprobs: Optional[np.ndarray] = None
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.buckets: list[int] = []
@@ -136,10 +137,25 @@ class ModelRunner:
         return dst
 
     # ------------------------------------------------------------------ execution
-    def _sample(self, logits: torch.Tensor, n: int):
+    def _sample(self, logits: torch.Tensor, n: int, extras: Optional[dict] = None):
+        """extras (from the engine, only when some request in the step asks for them):
+        "penalties": (rows, toks, counts, presence, frequency, repetition) numpy COO over
+        the sampled rows; "logprobs": True -> log-probs also for greedy picks."""
+        lp = False
+        if extras:
+            pen = extras.get("penalties")
+            if pen is not None:
+                dev = logits.device
+                rows, toks, counts, pres, freq, rep = pen
+                ops.apply_penalties(
+                    logits, torch.from_numpy(rows).to(dev), torch.from_numpy(toks).to(dev),
+                    torch.from_numpy(counts).to(dev), torch.from_numpy(pres).to(dev),
+                    torch.from_numpy(freq).to(dev), torch.from_numpy(rep).to(dev))
+            lp = bool(extras.get("logprobs"))
         return ops.sample(logits, self.d["temperature"][:n], self.d["top_k"][:n],
                           self.d["top_p"][:n], self.d["seeds"][:n], self.d["steps"][:n],
-                          out_tokens=self.out_tokens[:n], out_logprobs=self.out_logprobs[:n])
+                          out_tokens=self.out_tokens[:n], out_logprobs=self.out_logprobs[:n],
+                          greedy_logprobs=lp)
 
     def execute_prefill(self, info: dict) -> torch.Tensor:
         T, B, nt, ns = info["num_tokens"], info["num_seqs"], info["num_tiles"], info["num_samples"]
@@ -161,7 +177,7 @@ class ModelRunner:
         if ns == 0:
             return self.out_tokens[:0]
         logits = self.model.compute_logits(h.index_select(0, lidx)).float()
-        toks, _ = self._sample(logits, ns)
+        toks, _ = self._sample(logits, ns, info.get("extras"))
         return toks
 
     def decode_partitions(self, n: int) -> tuple[int, int]:
@@ -179,7 +195,7 @@ class ModelRunner:
         parts = math.ceil(max_len / ps)
         return parts, ps
 
-    def _decode_body(self, n: int) -> None:
+    def _decode_body(self, n: int, extras: Optional[dict] = None) -> None:
         parts, ps = self.decode_partitions(n)
         batch = AttnBatch(False, self.d["positions"][:n], self.d["slots"][:n], self.d_bt[:n],
                           self.d["seq_lens"][:n], self.d["q_start"][:n + 1], None, None,
@@ -187,7 +203,7 @@ class ModelRunner:
         h = self.model.forward(self.d["input_ids"][:n], batch, self.k_caches, self.v_caches)
         # sampler reads bf16 logits directly (no [n, V] fp32 cast pass)
         logits = self.model.compute_logits(h)
-        self._sample(logits, n)
+        self._sample(logits, n, extras)
 
     def _pad_host(self, B: int, n: int) -> None:
         if n <= B:
@@ -218,10 +234,13 @@ class ModelRunner:
                   "seeds", "steps"):
             self._h2d(k, n)
         self._h2d("block_tables", n * mb)
-        if graph is not None:
+        extras = info.get("extras")
+        if graph is not None and not extras:
             graph.replay()
         else:
-            self._decode_body(n)
+            # penalties / log-probs requested: the same padded batch (n rows, so TP peers
+            # replaying their graphs issue identical collectives), eagerly
+            self._decode_body(n, extras)
         return self.out_tokens[:B]
 
     def execute(self, info: dict) -> np.ndarray:
@@ -231,6 +250,9 @@ class ModelRunner:
         else:
             with profiling.phase("akap.decode"):
                 toks = self.execute_decode(info)
+        extras = info.get("extras")
+        if extras and extras.get("logprobs"):
+            self.last_logprobs = self.out_logprobs[:toks.shape[0]].to("cpu").numpy()
         return toks.to("cpu").numpy()
 
     # ------------------------------------------------------------------ graphs

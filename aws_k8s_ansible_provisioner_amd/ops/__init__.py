@@ -237,7 +237,9 @@ def gemm_splitk(M: int, N: int, K: int) -> int:
 
 
 # ----------------------------------------------------------------------------- sampling
-def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out_logprobs=None):
+def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out_logprobs=None,
+           greedy_logprobs: bool = False):
+    """greedy_logprobs: also return the log-prob of greedy (temperature 0) picks."""
     B = logits.shape[0]
     if out_tokens is None:
         out_tokens = torch.empty(B, dtype=torch.int64, device=logits.device)
@@ -245,12 +247,26 @@ def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out
         out_logprobs = torch.empty(B, dtype=torch.float32, device=logits.device)
     if _native(logits):
         torch.ops.akap.sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens,
-                              out_logprobs)
+                              out_logprobs, greedy_logprobs)
         return out_tokens, out_logprobs
-    t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps)
+    t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps, greedy_logprobs)
     out_tokens.copy_(t)
     out_logprobs.copy_(lp)
     return out_tokens, out_logprobs
+
+
+def apply_penalties(logits, rows, toks, counts, presence, frequency, repetition):
+    """In-place presence / frequency / repetition penalties on `logits` [B, V] for the
+    unique (row, token, output-count) entries given in COO form."""
+    if rows.numel() == 0:
+        return logits
+    if _native(logits):
+        torch.ops.akap.apply_penalties(logits, rows, toks, counts, presence, frequency,
+                                       repetition)
+        return logits
+    logits.copy_(ref.apply_penalties(logits, rows, toks, counts, presence, frequency,
+                                     repetition))
+    return logits
 
 
 def argmax(logits, out=None):

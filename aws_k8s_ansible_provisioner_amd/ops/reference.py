@@ -165,7 +165,7 @@ def paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale)
     return out
 
 
-def sample(logits, temperature, top_k, top_p, seeds, steps):
+def sample(logits, temperature, top_k, top_p, seeds, steps, greedy_logprobs=False):
     """Reference sampler: greedy for T<=0; else top-k, then top-p (on the top-k
     renormalised distribution), then a draw.  Draws use torch's RNG seeded per row,
     so only the distribution (not the exact token) matches the kernel."""
@@ -177,7 +177,7 @@ def sample(logits, temperature, top_k, top_p, seeds, steps):
         T = float(temperature[i])
         if T <= 0:
             toks[i] = int(x.argmax())
-            lps[i] = 0.0
+            lps[i] = float(torch.log_softmax(x, -1)[toks[i]]) if greedy_logprobs else 0.0
             continue
         z = x / T
         logp = torch.log_softmax(z, dim=-1)
@@ -248,3 +248,15 @@ def fused_moe(h, w13, w2, topk_w, topk_ids):
             y2 = (a.float() @ w2[e].float().t()).to(h.dtype)
             out[t] += float(topk_w[t, k]) * y2.float()
     return out.to(h.dtype)
+
+
+def apply_penalties(logits, rows, toks, counts, presence, frequency, repetition):
+    out = logits.clone()
+    for r, t, c in zip(rows.tolist(), toks.tolist(), counts.tolist()):
+        x = float(out[r, t])
+        rep = float(repetition[r])
+        if rep != 1.0:
+            x = x / rep if x > 0 else x * rep
+        x -= float(frequency[r]) * c + (float(presence[r]) if c > 0 else 0.0)
+        out[r, t] = x
+    return out

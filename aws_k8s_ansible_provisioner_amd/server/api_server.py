@@ -49,7 +49,42 @@ def _sampling_from(body: dict, default_max: int = 16) -> SamplingParams:
         stop_token_ids=list(body.get("stop_token_ids") or []),
         ignore_eos=bool(body.get("ignore_eos", False)),
         n=int(body.get("n", 1) or 1),
+        presence_penalty=float(body.get("presence_penalty") or 0.0),
+        frequency_penalty=float(body.get("frequency_penalty") or 0.0),
+        repetition_penalty=float(body.get("repetition_penalty") or 1.0),
+        logprobs=_logprobs_of(body),
     )
+
+
+def _logprobs_of(body: dict) -> Optional[int]:
+    """completions: "logprobs": int; chat: "logprobs": bool (+ "top_logprobs": int).  Only
+    the sampled token's log-prob is produced (top-N alternatives are not computed)."""
+    lp = body.get("logprobs")
+    if lp is None or lp is False:
+        return None
+    if lp is True:
+        return int(body.get("top_logprobs") or 0)
+    return int(lp)
+
+
+def _completion_logprobs(tokenizer, ids: list, lps: list, offset0: int = 0) -> dict:
+    toks = [tokenizer.decode_token(t) for t in ids]
+    offs, o = [], offset0
+    for t in toks:
+        offs.append(o)
+        o += len(t)
+    return {"tokens": toks, "token_logprobs": lps,
+            "top_logprobs": [{t: lp} for t, lp in zip(toks, lps)], "text_offset": offs}
+
+
+def _chat_logprobs(tokenizer, ids: list, lps: list) -> dict:
+    out = []
+    for t, lp in zip(ids, lps):
+        s = tokenizer.decode_token(t)
+        out.append({"token": s, "logprob": lp, "bytes": list(s.encode("utf-8")),
+                    "top_logprobs": [{"token": s, "logprob": lp,
+                                      "bytes": list(s.encode("utf-8"))}]})
+    return {"content": out}
 
 
 def _prompts_of(prompt) -> list:
@@ -200,7 +235,11 @@ class OpenAIServer:
                 text = o.text
                 if body.get("echo") and isinstance(prompts[k // sp.n], str):
                     text = prompts[k // sp.n] + text
-                choices.append({"index": k, "text": text, "logprobs": None,
+                lpd = None
+                if sp.logprobs is not None and o.logprobs is not None:
+                    lpd = _completion_logprobs(self.ae.engine.tokenizer, o.output_ids,
+                                               o.logprobs)
+                choices.append({"index": k, "text": text, "logprobs": lpd,
                                 "finish_reason": o.finish_reason, "stop_reason": None})
                 ctok += len(o.output_ids)
                 if k % sp.n == 0:
@@ -253,8 +292,12 @@ class OpenAIServer:
                 return _err(400, str(e))
             except RuntimeError as e:
                 return _err(503, str(e), "ServiceUnavailable")
+            tok = self.ae.engine.tokenizer
             choices = [{"index": j, "message": {"role": "assistant", "content": o.text},
-                        "logprobs": None, "finish_reason": o.finish_reason}
+                        "logprobs": (_chat_logprobs(tok, o.output_ids, o.logprobs)
+                                     if sp.logprobs is not None and o.logprobs is not None
+                                     else None),
+                        "finish_reason": o.finish_reason}
                        for j, o in enumerate(outs)]
             ptok = len(outs[0].prompt_ids)
             ctok = sum(len(o.output_ids) for o in outs)

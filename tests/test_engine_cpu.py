@@ -90,3 +90,30 @@ def test_model_registry_shapes():
     assert 45e9 < get_config("mixtral-8x7b").num_params() < 48e9
     assert "qwen3-0.6b" in list_models()
     assert get_config("llama-3-70b").kv_bytes_per_token(tp=8) == 80 * 2 * 1 * 128 * 2
+
+
+def test_logprobs_match_dense_reference():
+    eng = _engine("tiny-qwen3")
+    prompt = list(range(7, 30))
+    out = eng.generate(None, SamplingParams(max_tokens=6, temperature=0, ignore_eos=True,
+                                            logprobs=1), prompt_ids=[prompt])[0]
+    assert out.logprobs is not None and len(out.logprobs) == len(out.output_ids) == 6
+    logits = dense_logits(eng.runner.model, prompt + out.output_ids).float()
+    for i, (tok, lp) in enumerate(zip(out.output_ids, out.logprobs)):
+        ref = torch.log_softmax(logits[len(prompt) - 1 + i], -1)[tok].item()
+        assert abs(lp - ref) < 0.05, (i, lp, ref)
+
+
+def test_frequency_penalty_prevents_repeats():
+    eng = _engine("tiny-llama")
+    prompts = [[5, 6, 7] * 6, [9] * 20]
+    base = eng.generate(None, SamplingParams(max_tokens=12, temperature=0, ignore_eos=True),
+                        prompt_ids=prompts)
+    pen = eng.generate(None, SamplingParams(max_tokens=12, temperature=0, ignore_eos=True,
+                                            frequency_penalty=1e4), prompt_ids=prompts)
+    for o in pen:
+        assert len(set(o.output_ids)) == len(o.output_ids), o.output_ids
+    # untouched requests are unaffected (penalty state is per request)
+    again = eng.generate(None, SamplingParams(max_tokens=12, temperature=0, ignore_eos=True),
+                         prompt_ids=prompts)
+    assert [o.output_ids for o in again] == [o.output_ids for o in base]

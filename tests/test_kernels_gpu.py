@@ -396,3 +396,35 @@ def test_decode_gemm_strided_input():
     y = torch.empty(64, 512, device=DEV, dtype=torch.bfloat16)
     torch.ops.akap.gemm(y, x, w, torch.empty(1, device=DEV), 1)
     assert (y.float() - ref_).abs().max().item() < 3e-2 * ref_.abs().max().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_apply_penalties(dtype):
+    torch.manual_seed(12)
+    B, V = 5, 1000
+    logits = (torch.randn(B, V) * 3).to(dtype)
+    rows = torch.tensor([0, 0, 1, 3, 3, 3, 4], dtype=torch.int32)
+    toks = torch.tensor([3, 999, 3, 0, 1, 500, 7], dtype=torch.int32)
+    counts = torch.tensor([2, 0, 1, 5, 0, 1, 3], dtype=torch.int32)
+    pres = torch.tensor([0.5, 0.0, 1.0, 0.2, 0.0])
+    freq = torch.tensor([0.1, 0.0, 0.3, 0.7, 0.0])
+    rep = torch.tensor([1.3, 1.0, 1.0, 2.0, 1.1])
+    exp = ref.apply_penalties(logits.float(), rows, toks, counts, pres, freq, rep)
+    got = logits.to(DEV)
+    ops.apply_penalties(got, rows.to(DEV), toks.to(DEV), counts.to(DEV), pres.to(DEV),
+                        freq.to(DEV), rep.to(DEV))
+    _close(got, exp, atol=5e-2 if dtype == torch.bfloat16 else 1e-5, rtol=1e-2)
+
+
+def test_greedy_logprobs():
+    torch.manual_seed(13)
+    B, V = 6, 151936
+    logits = torch.randn(B, V, device=DEV).bfloat16()
+    z = torch.zeros(B, device=DEV)
+    tok, lp = ops.sample(logits, z, torch.zeros(B, dtype=torch.int32, device=DEV),
+                         torch.ones(B, device=DEV), torch.arange(B, device=DEV),
+                         torch.zeros(B, dtype=torch.int32, device=DEV), greedy_logprobs=True)
+    ls = torch.log_softmax(logits.float(), -1)
+    exp = ls.gather(1, tok.view(-1, 1)).view(-1)
+    assert torch.equal(tok, logits.float().argmax(-1))
+    _close(lp, exp, atol=2e-3)

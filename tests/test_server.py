@@ -103,3 +103,20 @@ def test_health_and_metrics(client):
                  "vllm:gpu_cache_usage_perc", "vllm_request_total", "vllm_active_requests",
                  "vllm_request_duration_seconds_bucket"]:
         assert name in m, name
+
+
+def test_logprobs_and_penalties_in_api(client):
+    r = client.post("/v1/completions", json={"model": MODEL, "prompt": "hello there",
+                                             "max_tokens": 5, "logprobs": 1, "ignore_eos": True,
+                                             "temperature": 0})
+    assert r.status_code == 200, r.text
+    lp = r.json()["choices"][0]["logprobs"]
+    assert len(lp["tokens"]) == len(lp["token_logprobs"]) == 5
+    assert all(x <= 1e-6 for x in lp["token_logprobs"])
+    r = client.post("/v1/chat/completions", json={
+        "messages": [{"role": "user", "content": "hi"}], "max_tokens": 4, "logprobs": True,
+        "ignore_eos": True, "presence_penalty": 1.5, "frequency_penalty": 0.5,
+        "repetition_penalty": 1.2})
+    assert r.status_code == 200, r.text
+    content = r.json()["choices"][0]["logprobs"]["content"]
+    assert len(content) == 4 and all("logprob" in c for c in content)
