@@ -273,6 +273,14 @@ class ModelRunner:
                 "AKAP_TUNABLEOP_FILE", os.path.join(os.getcwd(), "tunableop_results.csv")))
         # safe static contents: every row is padding
         self._pad_host(0, self.max_seqs)
+        if os.environ.get("AKAP_GEMM_TUNE", "1") != "0" and not self.mcfg.is_moe:
+            # per-(M, N, K) hipBLASLt vs MFMA-kernel choice on the real, cold layer weights
+            from ..ops import gemm_tuner
+
+            t1 = time.time()
+            gemm_tuner.tune_model(self.model, [b for b in self.buckets if b >= 16],
+                                  log=self.log)
+            self.log(f"[runner] GEMM tuning {time.time() - t1:.1f}s")
         for k in ("input_ids", "positions", "slots", "seq_lens", "temperature", "top_p", "top_k",
                   "seeds", "steps"):
             self._h2d(k, self.max_seqs)

@@ -187,9 +187,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     """y = x @ w.T.  Decode-sized M on the GPU -> the hand-written MFMA GEMM (small tiles +
     split-K to fill 256 CUs); large M (prefill) -> hipBLASLt via torch."""
     M = x.shape[0]
-    use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
-               and (M <= GEMM_MAX_M or _GEMM_MODE == "hip") and x.shape[1] % 8 == 0
-               and w.shape[0] % 4 == 0)
+    split = None
+    if x.is_cuda and x.dim() == 2:
+        from . import gemm_tuner
+
+        choice = gemm_tuner.lookup(M, w.shape[0], w.shape[1])
+        if choice is not None:  # measured at engine start (cold weights, real layers)
+            split = choice[1] if choice[0] == "hip" else 0
+    if split is None:
+        use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
+                   and (M <= GEMM_MAX_M or _GEMM_MODE == "hip") and x.shape[1] % 8 == 0
+                   and w.shape[0] % 4 == 0)
+    else:
+        use_hip = split > 0 and x.stride(-1) == 1
     if not use_hip:
         y = torch.nn.functional.linear(x, w)
         if out is not None:
@@ -200,14 +210,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     N, K = w.shape
     if out is None:
         out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-    s = gemm_splitk(M, N, K)
+    s = split or gemm_splitk(M, N, K)
     if s > 1:
         ws = torch.empty(s * M * N, dtype=torch.float32, device=x.device)
     else:
         ws = _EMPTY_F32.get(x.device)
         if ws is None:
             ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
-    torch.ops.akap.gemm(out, x, w, ws, s, gemm_counters(x.device) if s > 1 else None)
+    torch.ops.akap.gemm(out, x, w, ws, s)
     return out
 
 

@@ -428,3 +428,22 @@ def test_greedy_logprobs():
     exp = ls.gather(1, tok.view(-1, 1)).view(-1)
     assert torch.equal(tok, logits.float().argmax(-1))
     _close(lp, exp, atol=2e-3)
+
+
+def test_gemm_tuner_plan_is_used_and_correct():
+    from aws_k8s_ansible_provisioner_amd.ops import gemm_tuner
+
+    torch.manual_seed(21)
+    ws = [torch.randn(1024, 3072, device=DEV, dtype=torch.bfloat16) * 0.02 for _ in range(4)]
+    choice = gemm_tuner.tune(128, ws)
+    assert choice[0] in ("torch", "hip")
+    assert gemm_tuner.lookup(128, 1024, 3072) == choice
+    x = torch.randn(128, 3072, device=DEV, dtype=torch.bfloat16)
+    y = ops.linear(x, ws[1])
+    ref_ = x.float() @ ws[1].float().t()
+    assert (y.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
+    # force the MFMA path through the plan and check it too
+    gemm_tuner.plan()[(128, 1024, 3072)] = ("hip", 4)
+    y2 = ops.linear(x, ws[1])
+    assert (y2.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
+    gemm_tuner.plan().pop((128, 1024, 3072))
