@@ -137,4 +137,12 @@ struct CarMulti {  // test-only: every rank of a simulated group in one launch
 void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two_shot,
                                    hipStream_t s);
 
+// ---- prefetch.hip ----
+struct PrefetchList {
+  const void* ptr[8];
+  long bytes[8];
+  int n;
+};
+void launch_l2_prefetch(const PrefetchList& L, uint32_t* sink, hipStream_t s);
+
 }  // namespace akap

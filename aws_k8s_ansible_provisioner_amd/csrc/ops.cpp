@@ -222,6 +222,19 @@ void paged_attention_decode_fused(Tensor out, Tensor qkv, Tensor k_cache, Tensor
   akap::launch_paged_attn_decode(p, B, cur_stream());
 }
 
+void l2_prefetch(std::vector<Tensor> ts, Tensor sink) {
+  TORCH_CHECK(ts.size() <= 8, "at most 8 tensors");
+  akap::PrefetchList L{};
+  for (size_t i = 0; i < ts.size(); ++i) {
+    CHECK_GPU(ts[i]); CHECK_CONTIG(ts[i]);
+    L.ptr[i] = ts[i].data_ptr();
+    L.bytes[i] = (long)ts[i].numel() * ts[i].element_size();
+  }
+  L.n = ts.size();
+  const c10::DeviceGuard g(sink.device());
+  akap::launch_l2_prefetch(L, reinterpret_cast<uint32_t*>(sink.data_ptr<int>()), cur_stream());
+}
+
 int64_t gemm_splitk(int64_t M, int64_t N, int64_t K) {
   return akap::gemm_splitk_choice(M, N, K);
 }
@@ -595,6 +608,7 @@ TORCH_LIBRARY(akap, m) {
       "gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int splitk, "
       "Tensor(c!)? counters=None) -> ()");
   m.def("gemm_splitk(int M, int N, int K) -> int");
+  m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");
   m.def("car_ipc_handles(int h) -> Tensor");
   m.def("car_open(int h, Tensor handles) -> ()");
@@ -644,6 +658,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
   m.impl("car_all_reduce", &car_all_reduce);
+  m.impl("l2_prefetch", &l2_prefetch);
   m.impl("car_all_reduce_multi", &car_all_reduce_multi);
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);

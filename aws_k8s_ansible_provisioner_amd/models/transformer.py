@@ -28,6 +28,7 @@ from .config import ModelConfig
 from .moe import MoEBlock
 
 FUSED_DECODE = os.environ.get("AKAP_FUSED_DECODE", "1") != "0"
+PREFETCH_WEIGHTS = os.environ.get("AKAP_PREFETCH_WEIGHTS", "0") == "1"
 
 
 @dataclasses.dataclass
@@ -270,6 +271,11 @@ class DecoderLM:
                 h, residual = ops.fused_add_rms_norm(x, residual, lw.ln1, eps)
             qkv = ops.linear(h, lw.w_qkv)
             attn = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+            if not batch.is_prefill and PREFETCH_WEIGHTS:
+                # warm this layer's remaining GEMM weights (+ the next QKV) in MALL before
+                # the HBM-bound attention stream; the latency-bound GEMMs then hit cache
+                nxt = self.layers[li + 1].w_qkv if li + 1 < len(self.layers) else None
+                ops.l2_prefetch([lw.w_o, lw.w_gate_up, lw.w_down, nxt])
             if not batch.is_prefill and FUSED_DECODE:
                 # q/k-norm + RoPE + KV-cache write fused into the decode attention kernel
                 ops.paged_attention_decode_fused(

@@ -345,7 +345,23 @@ def moe_align(topk_ids, num_experts: int, block: int, inv=None, tile_expert=None
 
 
 _EMPTY_I32: dict = {}
+_SINK: dict = {}
 MOE_BLOCK = 64
+
+
+def l2_prefetch(tensors) -> None:
+    """Warm the cache hierarchy with `tensors` (e.g. the next decode GEMMs' weights).
+    No-op on CPU."""
+    ts = [t for t in tensors if t is not None]
+    if not ts or not ts[0].is_cuda:
+        return
+    load_native(required=True)
+    dev = ts[0].device
+    sink = _SINK.get(dev)
+    if sink is None:
+        sink = _SINK[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    for i in range(0, len(ts), 8):
+        torch.ops.akap.l2_prefetch(ts[i:i + 8], sink)
 
 
 def fused_moe(h, w13, w2, topk_w, topk_ids, out=None):
