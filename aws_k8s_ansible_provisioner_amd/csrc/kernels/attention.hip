@@ -40,29 +40,43 @@ __device__ __forceinline__ void wave_state_init(WaveState& st) {
   st.l = 0.f;
 }
 
-// Register-staged operands of one 32-token KV chunk.
-struct ChunkRegs {
+// Register-staged operands of one 32-token KV chunk.  For an fp8 cache the raw bytes are
+// staged (half the VGPRs, so the double-buffered prefetch keeps 2 waves/SIMD) and widened
+// to bf16 right at the MFMA.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <bool F8>
+struct ChunkT {
   bf16x8 ka[2][kNC];  // K tile rows (A operand of S^T = K . Q^T)
   bf16x8 vb[kND];     // V^T tiles (A operand of O^T = V^T . P^T)
 };
+template <>
+struct ChunkT<true> {
+  u32x2 ka[2][kNC];
+  u32x2 vb[kND];
+};
+using ChunkRegs = ChunkT<false>;
+__device__ __forceinline__ bf16x8 widen(const bf16x8& v) { return v; }
+__device__ __forceinline__ bf16x8 widen(const u32x2& v) { return fp8x8_to_bf16x8(v[0], v[1]); }
 
-template <bool NT>
-__device__ __forceinline__ bf16x8 ldkv(const bf16* p) {
-  if constexpr (NT)
-    return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
-  else
-    return *reinterpret_cast<const bf16x8*>(p);
+template <bool F8, bool NT>
+__device__ __forceinline__ auto ld_raw8(const void* base, size_t off) {
+  if constexpr (F8) {
+    const u32x2* p = reinterpret_cast<const u32x2*>(reinterpret_cast<const uint8_t*>(base) + off);
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+  } else {
+    return ld_kv8<false, NT>(base, off);
+  }
 }
 
-// Issue the loads of the 32-token chunk at absolute kv position t0.
 // Issue the loads of the 32-token chunk at absolute kv position t0.
 // K cache layout inside a (block, kv head) is MFMA-fragment ordered (see k_swz_offset in
 // common.h): for each 32-token chunk, [tile tt][k-step cc][row r][32 dims], so one load
 // instruction (fixed tt, cc) reads 16 rows x 64 B = 1 KiB contiguous (a row-major K gives
 // 16 scattered 64-B segments per instruction: -10% decode attention time measured).
-template <bool NT = false>
-__device__ __forceinline__ void load_chunk(ChunkRegs& c, const bf16* __restrict__ k_cache,
-                                           const bf16* __restrict__ v_cache,
+template <bool NT = false, bool F8 = false>
+__device__ __forceinline__ void load_chunk(ChunkT<F8>& c, const void* __restrict__ k_cache,
+                                           const void* __restrict__ v_cache,
                                            const int* __restrict__ bt, int kv_len, int kvh,
                                            int Hkv, int BS, int t0) {
   const int lane = threadIdx.x & 63;
@@ -74,31 +88,31 @@ __device__ __forceinline__ void load_chunk(ChunkRegs& c, const bf16* __restrict_
     tok = min(tok, kv_len - 1);  // clamped lanes re-read a valid row (masked later)
     const int blk = bt[tok / BS];
     const int off = tok % BS;
-    const bf16* kp = k_cache + ((size_t)blk * Hkv + kvh) * BS * kD + k_swz_offset(off) + 8 * g;
+    const size_t kp = ((size_t)blk * Hkv + kvh) * BS * kD + k_swz_offset(off) + 8 * g;
 #pragma unroll
-    for (int cc = 0; cc < kNC; ++cc) c.ka[tt][cc] = ldkv<NT>(kp + cc * 512);
+    for (int cc = 0; cc < kNC; ++cc) c.ka[tt][cc] = ld_raw8<F8, NT>(k_cache, kp + cc * 512);
   }
   int vt = t0 + 8 * g;
   vt = min(vt, (kv_len - 1) & ~7);
   const int vblk = bt[vt / BS];
   const int voff = vt % BS;
-  const bf16* vp = v_cache + ((size_t)vblk * Hkv + kvh) * kD * BS + (voff >> 3) * kD * 8 + r * 8;
+  const size_t vp = ((size_t)vblk * Hkv + kvh) * kD * BS + (voff >> 3) * kD * 8 + r * 8;
 #pragma unroll
-  for (int n = 0; n < kND; ++n) c.vb[n] = ldkv<NT>(vp + 16 * n * 8);
+  for (int n = 0; n < kND; ++n) c.vb[n] = ld_raw8<F8, NT>(v_cache, vp + 16 * n * 8);
 }
 
 // Scores, online softmax and P.V for one staged chunk.
 // limit: last kv position this lane's query row may attend to (-1 => none).
-template <bool MASK>
+template <bool MASK, typename CT>
 __device__ __forceinline__ void compute_chunk(WaveState& st, const bf16x8 (&qb)[kNC],
-                                              const ChunkRegs& c, int t0, int limit,
+                                              const CT& c, int t0, int limit,
                                               float scale_log2) {
   const int g = (threadIdx.x & 63) >> 4;
   f32x4 s[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int cc = 0; cc < kNC; ++cc) {
-    s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.ka[0][cc], qb[cc], s[0], 0, 0, 0);
-    s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.ka[1][cc], qb[cc], s[1], 0, 0, 0);
+    s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(widen(c.ka[0][cc]), qb[cc], s[0], 0, 0, 0);
+    s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(widen(c.ka[1][cc]), qb[cc], s[1], 0, 0, 0);
   }
   float sv[8];
   float cmax = -INFINITY;
@@ -131,18 +145,18 @@ __device__ __forceinline__ void compute_chunk(WaveState& st, const bf16x8 (&qb)[
 #pragma unroll
   for (int n = 0; n < kND; ++n) {
     st.o[n] *= alpha;
-    st.o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.vb[n], pb, st.o[n], 0, 0, 0);
+    st.o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(widen(c.vb[n]), pb, st.o[n], 0, 0, 0);
   }
 }
 
-template <bool MASK, bool NT = false>
+template <bool MASK, bool NT = false, bool F8 = false>
 __device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC],
-                                           const bf16* __restrict__ k_cache,
-                                           const bf16* __restrict__ v_cache,
+                                           const void* __restrict__ k_cache,
+                                           const void* __restrict__ v_cache,
                                            const int* __restrict__ bt, int kv_len, int kvh,
                                            int Hkv, int BS, int t0, int limit, float scale_log2) {
-  ChunkRegs c;
-  load_chunk<NT>(c, k_cache, v_cache, bt, kv_len, kvh, Hkv, BS, t0);
+  ChunkT<F8> c;
+  load_chunk<NT, F8>(c, k_cache, v_cache, bt, kv_len, kvh, Hkv, BS, t0);
   compute_chunk<MASK>(st, qb, c, t0, limit, scale_log2);
 }
 
@@ -162,6 +176,7 @@ __device__ __forceinline__ void load_q(bf16x8 (&qb)[kNC], const bf16* qrow_ptr, 
 // Prefill / chunked-prefill / prefix-cached attention.
 // grid.x = q tiles (64 flattened rows each: 4 waves x 16), grid.y = kv heads.
 // ----------------------------------------------------------------------------------
+template <bool F8>
 __global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
   const int tile = blockIdx.x;
   const int kvh = blockIdx.y;
@@ -189,10 +204,12 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
     int t0 = 0;
     // chunks fully inside every row's causal window need no mask
     for (; t0 + 31 <= wave_min; t0 += 32)
-      attn_chunk<false>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
+      attn_chunk<false, false, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0,
+                                   limit,
                         p.scale_log2);
     for (; t0 <= wave_limit; t0 += 32)
-      attn_chunk<true>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0, limit,
+      attn_chunk<true, false, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0,
+                                  limit,
                        p.scale_log2);
   }
   float l = st.l;
@@ -219,6 +236,7 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
 // row G+1 = its value head; 16 threads per row, 8 dims each.  q rows -> per-head RMSNorm
 // (bf16-rounded, like the standalone kernel) -> NeoX RoPE -> LDS; the new token's k / v
 // (only when write_kv) -> paged cache.  Rotary pairs (d, d+64) sit in threads j and j^8.
+template <bool F8>
 __device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq, int kvh,
                                                    bool write_kv, bf16* q_s) {
   const int G = p.G;
@@ -272,14 +290,24 @@ __device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq,
         const int64_t blk = slot / p.BS;
         const int off = (int)(slot % p.BS);
         if (rr == G) {
-          bf16* dst = const_cast<bf16*>(p.k_cache) + ((size_t)blk * p.Hkv + kvh) * p.BS * kD +
-                      k_swz_offset(off) + k_dim_offset(8 * j);
-          *reinterpret_cast<bf16x8*>(dst) = o8;
+          const size_t e = ((size_t)blk * p.Hkv + kvh) * p.BS * kD + k_swz_offset(off) +
+                           k_dim_offset(8 * j);
+          if constexpr (F8) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>((uint8_t*)p.k_cache + e);
+            dst[0] = f32x4_to_fp8x4((float)o8[0], (float)o8[1], (float)o8[2], (float)o8[3]);
+            dst[1] = f32x4_to_fp8x4((float)o8[4], (float)o8[5], (float)o8[6], (float)o8[7]);
+          } else {
+            *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
+          }
         } else {
-          bf16* dst = const_cast<bf16*>(p.v_cache) + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
-                      (off >> 3) * kD * 8 + (off & 7);
+          const size_t e = ((size_t)blk * p.Hkv + kvh) * kD * p.BS + (off >> 3) * kD * 8 + (off & 7);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) dst[(size_t)(8 * j + i) * 8] = o8[i];
+          for (int i = 0; i < 8; ++i) {
+            if constexpr (F8)
+              ((uint8_t*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = f32_to_fp8((float)o8[i]);
+            else
+              ((bf16*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = o8[i];
+          }
         }
       }
     }
@@ -290,7 +318,7 @@ __device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq,
 
 // One (seq, kv head, partition) work item.  Ends with the LDS combine; callers that run
 // several items per workgroup must __syncthreads() before the next item's LDS writes.
-template <bool PREFETCH, bool NT = false, bool FUSED = false>
+template <bool PREFETCH, bool NT = false, bool FUSED = false, bool F8 = false>
 __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
                                             float* dyn_lds) {
   const int lane = threadIdx.x & 63;
@@ -318,14 +346,14 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
   // PREFETCH: this wave's first chunk is issued before anything else (in the fused kernel,
   // before the q/k prologue, so its HBM latency overlaps the prologue's)
   int t0 = pstart + 32 * w;
-  ChunkRegs cur;
+  ChunkT<F8> cur;
   if (PREFETCH && t0 < pend)
-    load_chunk<NT>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+    load_chunk<NT, F8>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
   if constexpr (FUSED) {
-    fused_qkv_prologue(p, seq, kvh, writes_kv, q_s);
+    fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s);
     // the chunk holding the token the prologue just wrote is re-read after the barrier
     if (PREFETCH && writes_kv && t0 < pend && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
-      load_chunk<NT>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+      load_chunk<NT, F8>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
   }
   WaveState st;
   wave_state_init(st);
@@ -343,10 +371,11 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
       // register double buffer: chunk i+1's loads are in flight during chunk i's MFMAs
       if (t0 < pend) {
         for (; t0 < pend; t0 += 128) {
-          ChunkRegs nxt;
+          ChunkT<F8> nxt;
           const bool more = t0 + 128 < pend;
           if (more)
-            load_chunk<NT>(nxt, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0 + 128);
+            load_chunk<NT, F8>(nxt, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
+                               t0 + 128);
           if (t0 + 31 < kv_len)
             compute_chunk<false>(st, qb, cur, t0, limit, p.scale_log2);
           else
@@ -357,11 +386,11 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
     } else {
       for (; t0 < pend; t0 += 128) {
         if (t0 + 31 < kv_len)
-          attn_chunk<false, NT>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
-                                t0, limit, p.scale_log2);
+          attn_chunk<false, NT, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
+                                    t0, limit, p.scale_log2);
         else
-          attn_chunk<true, NT>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0,
-                               limit, p.scale_log2);
+          attn_chunk<true, NT, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
+                                   t0, limit, p.scale_log2);
       }
     }
   }
@@ -417,10 +446,10 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
 }
 
 // grid = (num_seqs, Hkv, num_parts): one work item per workgroup.
-template <bool PREFETCH, int MINW, bool NT = false, bool FUSED = false>
+template <bool PREFETCH, int MINW, bool NT = false, bool FUSED = false, bool F8 = false>
 __global__ __launch_bounds__(256, MINW) void paged_attn_decode_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
-  decode_item<PREFETCH, NT, FUSED>(p, blockIdx.x, blockIdx.y, blockIdx.z, dyn_lds);
+  decode_item<PREFETCH, NT, FUSED, F8>(p, blockIdx.x, blockIdx.y, blockIdx.z, dyn_lds);
 }
 
 // Persistent variant: a fixed grid (a few workgroups per CU) strides over all work items
@@ -455,6 +484,7 @@ constexpr int kFaRows = 128;
 constexpr int kFaKeys = 64;
 constexpr int kFaBtCache = 1024;  // chunk -> block id cache in LDS (32768 keys)
 
+template <bool F8>
 __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParams p) {
   // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
   // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
@@ -519,8 +549,9 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
       const int within = pc & 511;
       const int off = (min(t * 2 + c, last_chunk) * 32) % BS;
       const size_t base = ((size_t)blk[i] * p.Hkv + kvh) * BS * kD + (size_t)off * kD;
-      kst[i] = *reinterpret_cast<const bf16x8*>(p.k_cache + base + within * 8);
-      vst[i] = *reinterpret_cast<const bf16x8*>(p.v_cache + base + within * 8);
+      // fp8 caches: 8-byte loads widened to bf16 here, so the LDS images are the same
+      kst[i] = ld_kv8<F8, false>(p.k_cache, base + within * 8);
+      vst[i] = ld_kv8<F8, false>(p.v_cache, base + within * 8);
     }
   };
   auto stage_store = [&](int buf) {
@@ -694,10 +725,14 @@ __global__ __launch_bounds__(256) void paged_attn_reduce_kernel(AttnParams p) {
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows,
                                hipStream_t s) {
   if (num_tiles == 0) return;
-  if (tile_rows == kFaRows)
-    paged_attn_prefill_fa_kernel<<<dim3(num_tiles, p.Hkv), 256, 0, s>>>(p);
-  else
-    paged_attn_prefill_kernel<<<dim3(num_tiles, p.Hkv), 256, 0, s>>>(p);
+  const dim3 grid(num_tiles, p.Hkv);
+  if (tile_rows == kFaRows) {
+    if (p.kv_fp8) paged_attn_prefill_fa_kernel<true><<<grid, 256, 0, s>>>(p);
+    else paged_attn_prefill_fa_kernel<false><<<grid, 256, 0, s>>>(p);
+  } else {
+    if (p.kv_fp8) paged_attn_prefill_kernel<true><<<grid, 256, 0, s>>>(p);
+    else paged_attn_prefill_kernel<false><<<grid, 256, 0, s>>>(p);
+  }
 }
 
 static int num_cus() {
@@ -716,7 +751,13 @@ void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) 
   const size_t smem = (size_t)(4 * p.G * (kD + 4) + 8 * p.G) * sizeof(float) +
                       (p.qkv ? (size_t)p.G * kD * sizeof(bf16) : 0);
   const int per_cu = (p.flags >> 3) & 7;  // flags bits 3..5: persistent, WGs per CU
-  if (p.qkv != nullptr) {  // fused q/k-norm + RoPE + KV write (default flags path)
+  if (p.kv_fp8) {  // fp8 KV cache: prefetching + non-temporal variants only
+    const dim3 grid(num_seqs, p.Hkv, p.num_parts);
+    if (p.qkv != nullptr)
+      paged_attn_decode_kernel<true, 1, true, true, true><<<grid, 256, smem, s>>>(p);
+    else
+      paged_attn_decode_kernel<true, 1, true, false, true><<<grid, 256, smem, s>>>(p);
+  } else if (p.qkv != nullptr) {  // fused q/k-norm + RoPE + KV write (default flags path)
     const dim3 grid(num_seqs, p.Hkv, p.num_parts);
     if (p.flags & 1)
       paged_attn_decode_kernel<true, 1, true, true><<<grid, 256, smem, s>>>(p);

@@ -104,4 +104,49 @@ __host__ __device__ __forceinline__ int k_swz_offset(int off) {
 }
 __host__ __device__ __forceinline__ int k_dim_offset(int d) { return (d >> 5) * 512 + (d & 31); }
 
+// ---- FP8 (OCP e4m3fn) KV-cache storage ---------------------------------------------------
+// Optional 1-byte KV cache (--kv-cache-dtype fp8, per-tensor scale 1.0): halves the bytes
+// the HBM-bound decode attention streams.  Values are clamped to +-448 (e4m3fn max) and
+// rounded to nearest even on store; loads widen 8 bytes to 8 bf16 (exact: every e4m3 value
+// is representable in bf16) right before the bf16 MFMAs.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16x8(uint32_t lo, uint32_t hi) {
+  const bf16x2_t a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, false);
+  const bf16x2_t b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, true);
+  const bf16x2_t c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, false);
+  const bf16x2_t d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, true);
+  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+__device__ __forceinline__ float fp8_clamp(float x) { return fminf(fmaxf(x, -448.f), 448.f); }
+
+// 4 floats -> 4 fp8 bytes (little-endian element order) in one 32-bit word
+__device__ __forceinline__ uint32_t f32x4_to_fp8x4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_clamp(a), fp8_clamp(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_clamp(c), fp8_clamp(d), w, true);
+  return (uint32_t)w;
+}
+
+__device__ __forceinline__ uint8_t f32_to_fp8(float a) {
+  return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(fp8_clamp(a), 0.f, 0, false) & 0xff);
+}
+
+// 8 consecutive cache elements starting at element `off` -> bf16x8
+template <bool F8, bool NT>
+__device__ __forceinline__ bf16x8 ld_kv8(const void* base, size_t off) {
+  if constexpr (F8) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2* p = reinterpret_cast<const u32x2*>(reinterpret_cast<const uint8_t*>(base) + off);
+    u32x2 v;
+    if constexpr (NT) v = __builtin_nontemporal_load(p);
+    else v = *p;
+    return fp8x8_to_bf16x8(v[0], v[1]);
+  } else {
+    const bf16x8* p = reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(base) + off);
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+  }
+}
+
 }  // namespace akap

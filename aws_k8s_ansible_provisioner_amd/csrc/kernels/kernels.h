@@ -18,9 +18,10 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                void* v_cache, const int64_t* positions, const int64_t* slots,
                                const float* cos_sin, const void* q_w, const void* k_w, int T,
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
-                               hipStream_t s);
+                               hipStream_t s, int kv_fp8 = 0);
 void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void* v_cache,
-                              const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s);
+                              const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s,
+                              int kv_fp8 = 0);
 
 // ---- activation.hip ----
 void launch_silu_and_mul(void* out, const void* in, long T, int F, int in_stride, hipStream_t s);
@@ -28,8 +29,8 @@ void launch_silu_and_mul(void* out, const void* in, long T, int F, int in_stride
 // ---- attention.hip ----
 struct AttnParams {
   const __bf16* q;        // [T, Hq, D]
-  const __bf16* k_cache;  // [NB, Hkv, BS, D]
-  const __bf16* v_cache;  // [NB, Hkv, BS/8, D, 8]
+  const void* k_cache;    // [NB, Hkv, BS, D]        bf16, or fp8 bytes when kv_fp8
+  const void* v_cache;    // [NB, Hkv, BS/8, D, 8]
   __bf16* out;            // [T, Hq, D]
   const int* block_tables;  // [B, bt_stride]
   int bt_stride;
@@ -46,6 +47,7 @@ struct AttnParams {
   float* part_l;
   float* part_o;  // [B, Hkv, parts, G, D]
   int flags;      // bit0: register double-buffered K/V prefetch in decode
+  int kv_fp8;     // caches hold OCP e4m3fn bytes (scale 1) instead of bf16
   // fused decode (qkv != nullptr): the kernel itself applies per-head q/k RMSNorm + RoPE to
   // the raw QKV projection row and writes the new token's K/V into the paged cache
   const __bf16* qkv;      // [B, qkv_stride]: q heads | k heads | v heads

@@ -32,10 +32,10 @@ __device__ __forceinline__ bool v_group_complete(const int64_t* __restrict__ slo
   return slots[g0] == slot - r && slots[g0 + 7] == slot - r + 7;
 }
 
-template <int D>
+template <int D, bool F8>
 __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
     const bf16* __restrict__ qkv, int qkv_stride, bf16* __restrict__ q_out,
-    bf16* __restrict__ k_cache, bf16* __restrict__ v_cache, const int64_t* __restrict__ positions,
+    void* __restrict__ k_cache, void* __restrict__ v_cache, const int64_t* __restrict__ positions,
     const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
     const bf16* __restrict__ q_w, const bf16* __restrict__ k_w, int T, int Hq, int Hkv, int BS,
     float eps, int apply_rope) {
@@ -101,19 +101,36 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
   const int off = (int)(slot % BS);
   if (is_k) {
     const int kh = h - Hq;
-    bf16* dst = k_cache + ((size_t)blk * Hkv + kh) * BS * D + k_swz_offset(off);
-    *reinterpret_cast<bf16x4*>(dst + k_dim_offset(4 * li)) = oa;
-    *reinterpret_cast<bf16x4*>(dst + k_dim_offset(HALF + 4 * li)) = ob;
+    const size_t e = ((size_t)blk * Hkv + kh) * BS * D + k_swz_offset(off);
+    if constexpr (F8) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e;
+      // from the bf16-rounded values (same rounding chain as the bf16 cache + reference)
+      *reinterpret_cast<uint32_t*>(dst + k_dim_offset(4 * li)) =
+          f32x4_to_fp8x4((float)oa[0], (float)oa[1], (float)oa[2], (float)oa[3]);
+      *reinterpret_cast<uint32_t*>(dst + k_dim_offset(HALF + 4 * li)) =
+          f32x4_to_fp8x4((float)ob[0], (float)ob[1], (float)ob[2], (float)ob[3]);
+    } else {
+      bf16* dst = reinterpret_cast<bf16*>(k_cache) + e;
+      *reinterpret_cast<bf16x4*>(dst + k_dim_offset(4 * li)) = oa;
+      *reinterpret_cast<bf16x4*>(dst + k_dim_offset(HALF + 4 * li)) = ob;
+    }
   } else {
     // tokens of a complete 8-token slot group are written by v_group_write_kernel as
     // 16-byte vectors; only stragglers (chunk edges, decode tokens) scatter 2-byte stores
     if (v_group_complete(slots, t, T, slot)) return;
     const int vh = h - Hq - Hkv;
-    bf16* dst = v_cache + ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + (off & 7);
+    const size_t e = ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + (off & 7);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      dst[(size_t)(4 * li + j) * 8] = oa[j];
-      dst[(size_t)(HALF + 4 * li + j) * 8] = ob[j];
+      if constexpr (F8) {
+        uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e;
+        dst[(size_t)(4 * li + j) * 8] = f32_to_fp8((float)oa[j]);
+        dst[(size_t)(HALF + 4 * li + j) * 8] = f32_to_fp8((float)ob[j]);
+      } else {
+        bf16* dst = reinterpret_cast<bf16*>(v_cache) + e;
+        dst[(size_t)(4 * li + j) * 8] = oa[j];
+        dst[(size_t)(HALF + 4 * li + j) * 8] = ob[j];
+      }
     }
   }
 }
@@ -122,9 +139,10 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
 // 2-byte stores.  When the batch holds all 8 tokens of a slot group (prefill chunks), a
 // thread per dim gathers the 8 values (each read coalesced across the wave) and writes one
 // 16-byte vector.  grid = (ceil(T / 64), Hkv), 128 threads = one per dim.
+template <bool F8>
 __global__ __launch_bounds__(128) void v_group_write_kernel(const bf16* __restrict__ qkv,
                                                             int qkv_stride,
-                                                            bf16* __restrict__ v_cache,
+                                                            void* __restrict__ v_cache,
                                                             const int64_t* __restrict__ slots,
                                                             int T, int Hq, int Hkv, int BS) {
   constexpr int D = 128;
@@ -140,8 +158,14 @@ __global__ __launch_bounds__(128) void v_group_write_kernel(const bf16* __restri
     for (int i = 0; i < 8; ++i) g8[i] = src[(size_t)i * qkv_stride];
     const int64_t blk = slot / BS;
     const int off = (int)(slot % BS);
-    *reinterpret_cast<bf16x8*>(v_cache + ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 +
-                               d * 8) = g8;
+    const size_t e = ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + d * 8;
+    if constexpr (F8) {
+      uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(v_cache) + e);
+      dst[0] = f32x4_to_fp8x4((float)g8[0], (float)g8[1], (float)g8[2], (float)g8[3]);
+      dst[1] = f32x4_to_fp8x4((float)g8[4], (float)g8[5], (float)g8[6], (float)g8[7]);
+    } else {
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(v_cache) + e) = g8;
+    }
   }
 }
 
@@ -149,28 +173,34 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                void* v_cache, const int64_t* positions, const int64_t* slots,
                                const float* cos_sin, const void* q_w, const void* k_w, int T,
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
-                               hipStream_t s) {
-  if (T == 0) return;
+                               hipStream_t s, int kv_fp8) {
+  if (T == 0 || D != 128) return;
   const long items = (long)T * (Hq + 2 * Hkv);
-  const int lph = D / 8;
-  const long threads = items * lph;
+  const long threads = items * (D / 8);
   dim3 grid((threads + 255) / 256);
-  if (D == 128) {
-    qk_norm_rope_cache_kernel<128><<<grid, 256, 0, s>>>(
-        (const bf16*)qkv, qkv_stride, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions,
-        slots, cos_sin, (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope);
-    if (T >= 8)
-      v_group_write_kernel<<<dim3((T + 63) / 64, Hkv), 128, 0, s>>>(
-          (const bf16*)qkv, qkv_stride, (bf16*)v_cache, slots, T, Hq, Hkv, BS);
+#define QKR(F8)                                                                                 \
+  qk_norm_rope_cache_kernel<128, F8><<<grid, 256, 0, s>>>(                                      \
+      (const bf16*)qkv, qkv_stride, (bf16*)q_out, k_cache, v_cache, positions, slots, cos_sin, \
+      (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope)
+  if (kv_fp8) QKR(true); else QKR(false);
+#undef QKR
+  if (T >= 8) {
+    const dim3 g2((T + 63) / 64, Hkv);
+    if (kv_fp8)
+      v_group_write_kernel<true><<<g2, 128, 0, s>>>((const bf16*)qkv, qkv_stride, v_cache, slots,
+                                                     T, Hq, Hkv, BS);
+    else
+      v_group_write_kernel<false><<<g2, 128, 0, s>>>((const bf16*)qkv, qkv_stride, v_cache,
+                                                      slots, T, Hq, Hkv, BS);
   }
 }
 
 // Plain scatter of already-final K/V rows into the paged cache (used by the
 // P/D KV receiver and by tests).  k, v: [T, Hkv, D].
-template <int D>
+template <int D, bool F8>
 __global__ __launch_bounds__(256) void reshape_and_cache_kernel(
-    const bf16* __restrict__ k, const bf16* __restrict__ v, bf16* __restrict__ k_cache,
-    bf16* __restrict__ v_cache, const int64_t* __restrict__ slots, int T, int Hkv, int BS) {
+    const bf16* __restrict__ k, const bf16* __restrict__ v, void* __restrict__ k_cache,
+    void* __restrict__ v_cache, const int64_t* __restrict__ slots, int T, int Hkv, int BS) {
   constexpr int LPH = D / 8;
   const int item = (blockIdx.x * 256 + threadIdx.x) / LPH;
   const int li = threadIdx.x % LPH;
@@ -182,22 +212,35 @@ __global__ __launch_bounds__(256) void reshape_and_cache_kernel(
   const int off = (int)(slot % BS);
   bf16x8 kv = *reinterpret_cast<const bf16x8*>(k + ((size_t)t * Hkv + h) * D + 8 * li);
   bf16x8 vv = *reinterpret_cast<const bf16x8*>(v + ((size_t)t * Hkv + h) * D + 8 * li);
-  *reinterpret_cast<bf16x8*>(k_cache + ((size_t)blk * Hkv + h) * BS * D + k_swz_offset(off) +
-                             k_dim_offset(8 * li)) = kv;
-  bf16* vd = v_cache + ((size_t)blk * Hkv + h) * D * BS + (off >> 3) * D * 8 + (off & 7);
+  const size_t ke = ((size_t)blk * Hkv + h) * BS * D + k_swz_offset(off) + k_dim_offset(8 * li);
+  const size_t ve = ((size_t)blk * Hkv + h) * D * BS + (off >> 3) * D * 8 + (off & 7);
+  if constexpr (F8) {
+    uint32_t* kd = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(k_cache) + ke);
+    kd[0] = f32x4_to_fp8x4((float)kv[0], (float)kv[1], (float)kv[2], (float)kv[3]);
+    kd[1] = f32x4_to_fp8x4((float)kv[4], (float)kv[5], (float)kv[6], (float)kv[7]);
+    uint8_t* vd = reinterpret_cast<uint8_t*>(v_cache) + ve;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) vd[(size_t)(8 * li + j) * 8] = vv[j];
+    for (int j = 0; j < 8; ++j) vd[(size_t)(8 * li + j) * 8] = f32_to_fp8((float)vv[j]);
+  } else {
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(k_cache) + ke) = kv;
+    bf16* vd = reinterpret_cast<bf16*>(v_cache) + ve;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vd[(size_t)(8 * li + j) * 8] = vv[j];
+  }
 }
 
 void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void* v_cache,
-                              const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s) {
-  if (T == 0) return;
+                              const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s,
+                              int kv_fp8) {
+  if (T == 0 || D != 128) return;
   const long threads = (long)T * Hkv * (D / 8);
   dim3 grid((threads + 255) / 256);
-  if (D == 128)
-    reshape_and_cache_kernel<128><<<grid, 256, 0, s>>>((const bf16*)k, (const bf16*)v,
-                                                      (bf16*)k_cache, (bf16*)v_cache, slots, T,
-                                                      Hkv, BS);
+  if (kv_fp8)
+    reshape_and_cache_kernel<128, true><<<grid, 256, 0, s>>>((const bf16*)k, (const bf16*)v,
+                                                            k_cache, v_cache, slots, T, Hkv, BS);
+  else
+    reshape_and_cache_kernel<128, false><<<grid, 256, 0, s>>>((const bf16*)k, (const bf16*)v,
+                                                             k_cache, v_cache, slots, T, Hkv, BS);
 }
 
 }  // namespace akap

@@ -19,6 +19,14 @@ using at::Tensor;
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// KV caches are bf16, or uint8 holding OCP e4m3fn bytes (--kv-cache-dtype fp8)
+int kv_fp8_of(const Tensor& k_cache, const Tensor& v_cache) {
+  const bool f8 = k_cache.scalar_type() == at::kByte;
+  TORCH_CHECK(f8 || k_cache.scalar_type() == at::kBFloat16, "KV cache must be bf16 or uint8 (fp8)");
+  TORCH_CHECK(v_cache.scalar_type() == k_cache.scalar_type(), "K and V cache dtypes differ");
+  return f8 ? 1 : 0;
+}
+
 #define CHECK_GPU(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
 #define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
 #define CHECK_LAST_CONTIG(x) TORCH_CHECK((x).stride(-1) == 1, #x " must have unit last stride")
@@ -72,7 +80,7 @@ void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache
       qkv.data_ptr(), qkv.stride(0), q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
       positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
       q_w ? q_w->data_ptr() : nullptr, k_w ? k_w->data_ptr() : nullptr, T, Hq, Hkv, D, BS,
-      (float)eps, apply_rope ? 1 : 0, cur_stream());
+      (float)eps, apply_rope ? 1 : 0, cur_stream(), kv_fp8_of(k_cache, v_cache));
 }
 
 void reshape_and_cache(Tensor k, Tensor v, Tensor k_cache, Tensor v_cache, Tensor slots) {
@@ -84,7 +92,7 @@ void reshape_and_cache(Tensor k, Tensor v, Tensor k_cache, Tensor v_cache, Tenso
   const c10::DeviceGuard g(k.device());
   akap::launch_reshape_and_cache(k.data_ptr(), v.data_ptr(), k_cache.data_ptr(),
                                  v_cache.data_ptr(), slots.data_ptr<int64_t>(), T, Hkv, D, BS,
-                                 cur_stream());
+                                 cur_stream(), kv_fp8_of(k_cache, v_cache));
 }
 
 void silu_and_mul(Tensor out, Tensor x) {
@@ -118,8 +126,9 @@ akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_
   TORCH_CHECK(block_tables.stride(1) == 1, "block_tables rows must be contiguous");
   akap::AttnParams p{};
   p.q = (const __bf16*)q.data_ptr();
-  p.k_cache = (const __bf16*)k_cache.data_ptr();
-  p.v_cache = (const __bf16*)v_cache.data_ptr();
+  p.kv_fp8 = kv_fp8_of(k_cache, v_cache);
+  p.k_cache = k_cache.data_ptr();
+  p.v_cache = v_cache.data_ptr();
   p.out = (__bf16*)out.data_ptr();
   p.block_tables = block_tables.data_ptr<int>();
   p.bt_stride = block_tables.stride(0);

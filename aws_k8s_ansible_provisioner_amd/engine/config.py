@@ -26,6 +26,7 @@ class EngineConfig:
     weights_path: Optional[str] = None
     chat_template: Optional[str] = None
     kv_role: str = "both"                     # "both" | "prefill" | "decode" (P/D)
+    kv_cache_dtype: str = "auto"              # "auto" (model dtype, bf16) | "fp8" (e4m3fn)
     init_std: float = 0.02                    # random-init weight scale
     shard_init: str = "per_rank"              # "per_rank" | "full" (identical logical weights for any TP)
 
@@ -33,6 +34,8 @@ class EngineConfig:
         # the K cache stores each 32-token chunk in MFMA-fragment order (ops/reference.py)
         if self.block_size <= 0 or self.block_size % 32:
             raise ValueError(f"block_size must be a multiple of 32, got {self.block_size}")
+        if self.kv_cache_dtype not in ("auto", "bf16", "bfloat16", "fp8", "fp8_e4m3"):
+            raise ValueError(f"kv_cache_dtype must be auto or fp8, got {self.kv_cache_dtype}")
 
     def resolved_device(self) -> str:
         if self.device != "auto":

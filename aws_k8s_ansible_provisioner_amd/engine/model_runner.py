@@ -71,10 +71,11 @@ class ModelRunner:
                              device=self.device if self.is_gpu else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.ps.tp_group)
             self.num_blocks = int(t.item())
-        self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
+        self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs, ecfg.kv_cache_dtype)
         self.k_caches, self.v_caches = self.model.cache_views(self.kv, self.bs)
         self.log(f"[runner] KV cache: {self.num_blocks} blocks x {self.bs} tokens "
-                 f"({self.kv.numel() * 2 / 2**30:.1f} GiB)")
+                 f"({self.kv.numel() * self.kv.element_size() / 2**30:.1f} GiB, "
+                 f"{'fp8 e4m3' if self.kv.dtype == torch.uint8 else 'bf16'})")
         # workspace sized for the finest split any bucket uses (256-token partitions)
         self.num_parts = max(1, math.ceil(ecfg.max_model_len / 128))
         self._alloc_buffers()
@@ -87,7 +88,8 @@ class ModelRunner:
 
     # ------------------------------------------------------------------ sizing
     def _derive_num_blocks(self) -> int:
-        per_block = self.mcfg.num_layers * 2 * self.model.hkv * self.bs * self.model.D * 2
+        elem = 1 if self.ecfg.kv_cache_dtype.startswith("fp8") else 2
+        per_block = self.mcfg.num_layers * 2 * self.model.hkv * self.bs * self.model.D * elem
         if not self.is_gpu:
             return max(64, min(4096, (self.max_seqs * self.ecfg.max_model_len) // self.bs + 8))
         torch.cuda.synchronize()

@@ -227,11 +227,14 @@ class DecoderLM:
             cp(self.lm_head[:n], sd["lm_head.weight"][self.vocab_start:self.vocab_end])
 
     # ------------------------------------------------------------------ kv cache
-    def allocate_kv_cache(self, num_blocks: int, block_size: int) -> torch.Tensor:
+    def allocate_kv_cache(self, num_blocks: int, block_size: int,
+                          kv_dtype: str = "auto") -> torch.Tensor:
         """One allocation [L, 2, NB, Hkv*BS*D] (K block = [Hkv,BS,D], V block = [Hkv,BS/8,D,8]),
-        zero-filled so never-written slots read as finite zeros."""
+        zero-filled so never-written slots read as finite zeros.  kv_dtype "fp8": uint8
+        storage of OCP e4m3fn values (half the bytes of bf16)."""
         per_block = self.hkv * block_size * self.D
-        return torch.zeros(self.cfg.num_layers, 2, num_blocks, per_block, dtype=self.dtype,
+        dt = torch.uint8 if kv_dtype.startswith("fp8") else self.dtype
+        return torch.zeros(self.cfg.num_layers, 2, num_blocks, per_block, dtype=dt,
                            device=self.device)
 
     def cache_views(self, kv: torch.Tensor, block_size: int):

@@ -59,6 +59,25 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
     return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
 
 
+FP8_MAX = 448.0  # OCP e4m3fn
+
+
+def to_cache(vals: torch.Tensor, cache: torch.Tensor) -> torch.Tensor:
+    """Values -> the cache's storage: bf16, or OCP e4m3fn bytes (uint8 cache, scale 1,
+    clamped to +-448, round-to-nearest-even like the kernels)."""
+    if cache.dtype == torch.uint8:
+        f8 = vals.float().clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+        return f8.view(torch.uint8)
+    return vals.to(cache.dtype)
+
+
+def from_cache(t: torch.Tensor) -> torch.Tensor:
+    """Cache storage -> values (fp8 bytes widen exactly to bf16)."""
+    if t.dtype == torch.uint8:
+        return t.view(torch.float8_e4m3fn).to(torch.bfloat16)
+    return t
+
+
 def k_swz(o: int) -> tuple[int, int, int]:
     """Token offset within a block -> (32-token chunk, tile tt, row r) of the K layout."""
     c, oo = divmod(o, 32)
@@ -79,7 +98,7 @@ def write_k(k_cache: torch.Tensor, b: int, o: int, val: torch.Tensor) -> None:
     """k_cache[block b, :, token o, :] = val [Hkv, D] in the swizzled layout."""
     c, tt, r = k_swz(o)
     H, D = val.shape
-    k_blocks_view(k_cache)[b, :, c, tt, :, r, :] = val.to(k_cache.dtype).view(H, D // 32, 32)
+    k_blocks_view(k_cache)[b, :, c, tt, :, r, :] = to_cache(val, k_cache).view(H, D // 32, 32)
 
 
 def k_tokens(k_cache: torch.Tensor, blocks: torch.Tensor) -> torch.Tensor:
@@ -89,7 +108,7 @@ def k_tokens(k_cache: torch.Tensor, blocks: torch.Tensor) -> torch.Tensor:
     nb = v.shape[0]
     t = v.permute(0, 2, 3, 5, 1, 4, 6).reshape(nb, BS // 32, 32, H, D)  # pos = tt*16 + r
     t = t[:, :, K_CHUNK_POS]
-    return t.reshape(nb * BS, H, D)
+    return from_cache(t.reshape(nb * BS, H, D))
 
 
 def write_cache(k: torch.Tensor, v: torch.Tensor, k_cache, v_cache, slots) -> None:
@@ -100,7 +119,7 @@ def write_cache(k: torch.Tensor, v: torch.Tensor, k_cache, v_cache, slots) -> No
             continue
         b, o = divmod(s, BS)
         write_k(k_cache, b, o, k[t])
-        v_cache[b, :, o // 8, :, o % 8] = v[t].to(v_cache.dtype)
+        v_cache[b, :, o // 8, :, o % 8] = to_cache(v[t], v_cache)
 
 
 def qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w, Hq,
@@ -134,7 +153,7 @@ def gather_kv(k_cache, v_cache, block_table, kv_len: int):
     K = k_tokens(k_cache, blocks)[:kv_len]
     # [nb, Hkv, BS/8, D, 8] -> [nb, BS/8, 8, Hkv, D] -> tokens
     V = v_cache[blocks].permute(0, 2, 4, 1, 3).reshape(nb * BS, v_cache.shape[1], -1)[:kv_len]
-    return K, V
+    return K, from_cache(V)
 
 
 def paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale):

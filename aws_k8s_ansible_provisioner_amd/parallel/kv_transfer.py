@@ -29,7 +29,10 @@ from .. import ops
 
 class KVTransferAgent:
     def __init__(self, kv_cache: torch.Tensor, group=None):
-        """kv_cache: the engine's [L, 2, NB, block_elems] cache tensor."""
+        """kv_cache: the engine's [L, 2, NB, block_elems] cache tensor (bf16, or uint8 fp8
+        bytes -- moved as bf16 pairs: the copy kernels are dtype-agnostic 16-byte moves)."""
+        if kv_cache.dtype == torch.uint8:
+            kv_cache = kv_cache.view(torch.bfloat16)
         self.kv = kv_cache
         L, two, NB, be = kv_cache.shape
         self.planes = kv_cache.view(L * two, NB, be)

@@ -384,6 +384,9 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--load-format", default="random", choices=["random", "safetensors"])
     ap.add_argument("--weights-path", default=None)
     ap.add_argument("--kv-role", default="both", choices=["both", "prefill", "decode"])
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8", "fp8_e4m3"],
+                    help="fp8: OCP e4m3 KV cache (half the bytes; decode attention streams "
+                         "half as much)")
     ap.add_argument("--otlp-traces-endpoint", default=None,
                     help="OTLP/HTTP collector (e.g. http://otel-collector:4318); also read "
                          "from OTEL_EXPORTER_OTLP_TRACES_ENDPOINT")
@@ -398,7 +401,7 @@ def engine_config_from_args(a) -> EngineConfig:
         num_gpu_blocks=a.num_gpu_blocks, enable_prefix_caching=not a.no_enable_prefix_caching,
         enforce_eager=a.enforce_eager, tensor_parallel_size=a.tensor_parallel_size, seed=a.seed,
         device=a.device, load_format=a.load_format, weights_path=a.weights_path,
-        chat_template=a.chat_template, kv_role=a.kv_role)
+        chat_template=a.chat_template, kv_role=a.kv_role, kv_cache_dtype=a.kv_cache_dtype)
 
 
 def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:

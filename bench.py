@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--max-model-len", type=int, default=2048)
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
+                    help="fp8 = e4m3 KV cache (NOT the headline config: bf16 KV like the "
+                         "reference's vLLM default)")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree: with --tp WORLD_SIZE the whole job is ONE "
@@ -102,6 +105,7 @@ def main() -> int:
                         seed=1234 + (rank % (world // 2) if pd else rank),  # P/D pair: same weights
                         num_gpu_blocks=None if gpu else 512,
                         kv_role=("prefill" if is_prefill else "decode") if pd else "both",
+                        kv_cache_dtype=a.kv_cache_dtype,
                         # ranks sharing one GPU (single-GPU gloo rehearsal) split its memory
                         gpu_memory_utilization=0.90 / max(1, shared_ranks))
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if rank == 0 else (lambda *x: None)
@@ -215,6 +219,7 @@ def main() -> int:
                 "max_num_seqs": a.max_num_seqs,
                 "sampling": "greedy" if a.temperature <= 0 else f"T={a.temperature}",
                 "hipgraph_decode": not a.enforce_eager,
+                "kv_cache_dtype": "bf16" if a.kv_cache_dtype == "auto" else "fp8_e4m3",
             },
         }
         print(json.dumps(res), flush=True)

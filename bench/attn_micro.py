@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--spread", type=int, default=128)
     ap.add_argument("--parts", default="1,2,4,8,16")
+    ap.add_argument("--fp8", action="store_true", help="e4m3 KV cache")
     a = ap.parse_args()
     ops.load_native(required=True)
     dev = "cuda"
@@ -39,11 +40,14 @@ def main():
         i += n
     kc = torch.randn(NB, a.hkv, bs, D, dtype=torch.bfloat16, device=dev)
     vc = torch.randn(NB, a.hkv, bs // 8, D, 8, dtype=torch.bfloat16, device=dev)
+    if a.fp8:
+        kc = kc.to(torch.float8_e4m3fn).view(torch.uint8)
+        vc = vc.to(torch.float8_e4m3fn).view(torch.uint8)
     q = torch.randn(B, a.hq, D, dtype=torch.bfloat16, device=dev)
     out = torch.empty_like(q)
     bt, lens_d = bt.to(dev), lens.to(dev)
     G = a.hq // a.hkv
-    kv_bytes = int(lens.sum()) * a.hkv * D * 2 * 2
+    kv_bytes = int(lens.sum()) * a.hkv * D * 2 * (1 if a.fp8 else 2)
     flags = os.environ.get("AKAP_ATTN_FLAGS", "default")
     for parts in [int(x) for x in a.parts.split(",")]:
         ps = 4096 // parts

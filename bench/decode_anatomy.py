@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--ctx", type=int, default=640)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--fp8", action="store_true", help="e4m3 KV cache")
     ap.add_argument("--prefill", type=int, default=0,
                     help="instead: a prefill step of B sequences x this many new tokens")
     a = ap.parse_args()
@@ -38,7 +39,8 @@ def main():
     lens = torch.randint(a.ctx - 128, a.ctx + 129, (B,), dtype=torch.int32)
     nb = [math.ceil(int(x) / BS) for x in lens]
     NB = sum(nb) + 8
-    kv = m.allocate_kv_cache(NB, BS)
+    kvd = "fp8" if a.fp8 else "auto"
+    kv = m.allocate_kv_cache(NB, BS, kvd)
     kc, vc = m.cache_views(kv, BS)
     perm = torch.randperm(NB)
     bt = torch.zeros(B, 4096 // BS, dtype=torch.int32)
@@ -57,7 +59,7 @@ def main():
         P = a.prefill
         lens = torch.full((B,), P, dtype=torch.int32)
         NB2 = B * math.ceil(P / BS) + 8
-        kv = m.allocate_kv_cache(NB2, BS)
+        kv = m.allocate_kv_cache(NB2, BS, kvd)
         kc, vc = m.cache_views(kv, BS)
         bt = torch.zeros(B, 4096 // BS, dtype=torch.int32)
         perm = torch.randperm(NB2)

@@ -117,3 +117,15 @@ def test_frequency_penalty_prevents_repeats():
     again = eng.generate(None, SamplingParams(max_tokens=12, temperature=0, ignore_eos=True),
                          prompt_ids=prompts)
     assert [o.output_ids for o in again] == [o.output_ids for o in base]
+
+
+def test_fp8_kv_cache_engine_close_to_bf16():
+    """--kv-cache-dtype fp8: e4m3 bytes in the paged cache; greedy tokens stay near-argmax
+    of the dense (full precision) reference."""
+    eng = _engine("tiny-qwen3", kv_cache_dtype="fp8")
+    assert eng.runner.kv.dtype == torch.uint8
+    prompts = [list(range(5, 45)), [7, 8, 9] * 14]
+    outs = eng.generate(None, SamplingParams(max_tokens=8, temperature=0, ignore_eos=True),
+                        prompt_ids=prompts)
+    for p, o in zip(prompts, outs):
+        _near_argmax(eng, p, o.output_ids, tol=0.5)

@@ -63,3 +63,16 @@ def test_sampled_generation_runs_with_topk_topp():
     b = eng.generate(None, sp, prompt_ids=[[5, 6, 7]])[0].output_ids
     assert a == b  # seeded requests are reproducible
     assert len(a) == 16
+
+
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama"])
+def test_engine_fp8_kv_cache(model):
+    """--kv-cache-dtype fp8 end to end (fused decode + flash prefill read e4m3 bytes)."""
+    eng = _engine(model, kv_cache_dtype="fp8")
+    assert eng.runner.kv.dtype == torch.uint8
+    prompts = [list(range(3, 80)), [17] * 33 + [5, 6, 7]]
+    outs = eng.generate(None, SamplingParams(max_tokens=10, temperature=0, ignore_eos=True),
+                        prompt_ids=prompts)
+    for p, o in zip(prompts, outs):
+        assert len(o.output_ids) == 10
+        _check_teacher_forced(eng, p, o.output_ids, tol=0.6)

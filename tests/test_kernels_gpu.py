@@ -447,3 +447,90 @@ def test_gemm_tuner_plan_is_used_and_correct():
     y2 = ops.linear(x, ws[1])
     assert (y2.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
     gemm_tuner.plan().pop((128, 1024, 3072))
+
+
+
+def _to_fp8_cache(kc, vc):
+    """bf16 test caches -> uint8 e4m3 caches (same values the kernels will read)."""
+    f = lambda t: t.float().clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)  # noqa
+    return f(kc), f(vc)
+
+
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8)])
+@pytest.mark.parametrize("layout", ["random", "prefill"])
+def test_qk_norm_rope_cache_fp8(hq, hkv, layout):
+    torch.manual_seed(31)
+    T, D, BS, NB = 45, 128, 32, 16
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int64)
+    slots = (torch.randperm(NB * BS)[:T] if layout == "random" else
+             torch.cat([torch.arange(3 * BS + 5, 3 * BS + 35), torch.arange(9 * BS + 16,
+                                                                          9 * BS + 31)]))
+    slots = slots.to(torch.int64)
+    cs = ref.rope_cos_sin(4096, D, 1e6)
+    qw, kw = torch.randn(D).bfloat16(), torch.randn(D).bfloat16()
+    kc = torch.zeros(NB, hkv, BS, D, dtype=torch.uint8)
+    vc = torch.zeros(NB, hkv, BS // 8, D, 8, dtype=torch.uint8)
+    q_ref = torch.empty(T, hq, D).bfloat16()
+    ref.qk_norm_rope_cache(qkv, q_ref, kc, vc, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
+    kg, vg = torch.zeros_like(kc).to(DEV), torch.zeros_like(vc).to(DEV)
+    q_out = torch.empty(T, hq, D, device=DEV, dtype=torch.bfloat16)
+    ops.qk_norm_rope_cache(qkv.to(DEV), q_out, kg, vg, pos.to(DEV), slots.to(DEV), cs.to(DEV),
+                           qw.to(DEV), kw.to(DEV), hq, hkv, 1e-6)
+    dq = lambda t: t.cpu().view(torch.float8_e4m3fn).float()  # noqa
+    # K passes through fp32 norm+rope on both sides: allow one fp8 ulp on rare ties
+    _close(dq(kg), dq(kc), atol=1e-2, rtol=0.13)
+    assert torch.equal(vg.cpu(), vc)  # V is exact: bf16 -> e4m3 on both sides
+
+
+@pytest.mark.parametrize("num_parts,part_size", [(1, 4096), (3, 512)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_paged_attention_decode_fp8(num_parts, part_size, fused):
+    lens = [1, 31, 33, 200, 777, 1500]
+    seqs = [(kv, 1) for kv in lens]
+    hq, hkv = 16, 8
+    q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=41)
+    kc8, vc8 = _to_fp8_cache(kc, vc)
+    scale = 1 / math.sqrt(128)
+    B, G = len(lens), hq // hkv
+    ws = ops.decode_workspace(B, hkv, G, num_parts, DEV)
+    out = torch.empty(B, hq, 128, dtype=torch.bfloat16, device=DEV)
+    if not fused:
+        exp = ref.paged_attention(q, kc8, vc8, bt, sl, qs, scale)
+        ops.paged_attention_decode(out, q.to(DEV), kc8.to(DEV), vc8.to(DEV), bt.to(DEV),
+                                   sl.to(DEV), G, scale, workspace=ws, num_parts=num_parts,
+                                   part_size=part_size)
+        _close(out, exp, atol=3e-2, rtol=3e-2)
+        return
+    g = torch.Generator().manual_seed(5)
+    qkv = torch.randn(B, (hq + 2 * hkv) * 128, generator=g).bfloat16()
+    pos = (sl - 1).to(torch.int64)
+    slots = torch.tensor([int(bt[s, int(pos[s]) // 32]) * 32 + int(pos[s]) % 32
+                          for s in range(B)], dtype=torch.int64)
+    cs = ref.rope_cos_sin(4096, 128, 1e6)
+    kr, vr = kc8.clone(), vc8.clone()
+    q_ref = torch.empty(B, hq, 128).bfloat16()
+    ref.qk_norm_rope_cache(qkv, q_ref, kr, vr, pos, slots, cs, None, None, hq, hkv, 1e-6)
+    exp = ref.paged_attention(q_ref, kr, vr, bt, sl, qs, scale)
+    kg, vg = kc8.to(DEV), vc8.to(DEV)
+    ops.paged_attention_decode_fused(out, qkv.to(DEV), kg, vg, bt.to(DEV), sl.to(DEV),
+                                     pos.to(DEV), slots.to(DEV), cs.to(DEV), None, None, G,
+                                     scale, 1e-6, workspace=ws, num_parts=num_parts,
+                                     part_size=part_size)
+    _close(out, exp, atol=4e-2, rtol=4e-2)
+
+
+@pytest.mark.parametrize("tile_rows", [64, 128])
+def test_paged_attention_prefill_fp8(tile_rows):
+    seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (700, 650)]
+    hq, hkv = 16, 8
+    q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=43)
+    kc8, vc8 = _to_fp8_cache(kc, vc)
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, kc8, vc8, bt, sl, qs, scale)
+    ts, tr = _tiles(seqs, hq // hkv, tile_rows)
+    out = torch.empty_like(q).to(DEV)
+    ops.paged_attention_prefill(out, q.to(DEV), kc8.to(DEV), vc8.to(DEV), bt.to(DEV), sl.to(DEV),
+                                qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv, scale,
+                                tile_rows=tile_rows)
+    _close(out, exp, atol=2e-2, rtol=2e-2)

@@ -170,3 +170,20 @@ def test_native_library_registers_all_ops():
                  "paged_attention_decode", "paged_attention_decode_fused", "sample", "gemm",
                  "moe_gemm", "moe_combine", "car_all_reduce", "kv_gather", "embedding"):
         assert hasattr(torch.ops.akap, name), name
+
+
+def test_fp8_cache_roundtrip_reference():
+    BS, D, H = 32, 128, 2
+    kc = torch.zeros(3, H, BS, D, dtype=torch.uint8)
+    vc = torch.zeros(3, H, BS // 8, D, 8, dtype=torch.uint8)
+    k = torch.randn(40, H, D) * 3
+    v = torch.randn(40, H, D) * 3
+    k[0, 0, 0] = 1000.0  # saturates to 448
+    slots = torch.arange(40) + 32
+    ref.write_cache(k, v, kc, vc, slots)
+    K, V = ref.gather_kv(kc, vc, torch.tensor([1, 2], dtype=torch.int32), 40)
+    assert K.dtype == torch.bfloat16
+    assert float(K[0, 0, 0]) == 448.0
+    rel = ((K.float() - k).abs() / (k.abs() + 1e-2))[1:]
+    assert float(rel.median()) < 0.07  # e4m3: 3 mantissa bits
+    assert torch.equal(V.float(), v.float().to(torch.float8_e4m3fn).float())
