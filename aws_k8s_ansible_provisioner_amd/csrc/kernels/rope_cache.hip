@@ -2,9 +2,8 @@
 //   per-head RMSNorm on q and k (Qwen3; optional)  ->  NeoX rotary on q and k
 //   -> q written contiguous [T, Hq, D]; k, v scattered into the paged KV cache.
 //
-// One pass over the QKV activations instead of three (norm, rope, cache write).
-// D/8 lanes own one head: lane i holds dims [4i, 4i+4) and their rotary partners
-// [D/2 + 4i, D/2 + 4i + 4) so the rotate-half pairing is lane-local.  cos/sin come
+// One pass over the QKV activations instead of three (norm, rope, cache write), one
+// launch: q/k heads and V spans are distinct workgroup roles of the same grid.  cos/sin come
 // from a host-precomputed fp32 table [max_pos, D] (cos | sin), no on-device trig.
 //
 // Paged cache layouts (MI355X-first, chosen so the attention kernels can issue
@@ -20,153 +19,192 @@
 
 namespace akap {
 
-// True when batch token t belongs to an 8-token V slot group whose 8 tokens are all in the
-// batch, consecutive (slots s0..s0+7, s0 % 8 == 0).  Written slots are never shared between
-// sequences (shared prefix blocks are full and read-only), so consecutive slots imply one
-// sequence's consecutive positions.
-__device__ __forceinline__ bool v_group_complete(const int64_t* __restrict__ slots, int t, int T,
-                                                 int64_t slot) {
-  const int r = (int)(slot & 7);
-  const int g0 = t - r;
-  if (g0 < 0 || g0 + 7 >= T) return false;
-  return slots[g0] == slot - r && slots[g0 + 7] == slot - r + 7;
+// q/k role: 16 lanes own one (token, head); lane i holds the 8 contiguous dims [8i, 8i+8)
+// (one 16-byte load / store), its rotate-half partner dims live in lane i ^ 8 and are
+// fetched with one DPP row-rotate per packed pair.  The K row goes to the cache as 16-byte
+// stores (8 dims never straddle a 32-dim fragment group).
+__device__ __forceinline__ uint32_t dpp_xor8(uint32_t v) {
+  // row_ror:8 inside a 16-lane DPP row == lane ^ 8
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);
 }
 
-template <int D, bool F8>
-__global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
-    const bf16* __restrict__ qkv, int qkv_stride, bf16* __restrict__ q_out,
-    void* __restrict__ k_cache, void* __restrict__ v_cache, const int64_t* __restrict__ positions,
-    const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
-    const bf16* __restrict__ q_w, const bf16* __restrict__ k_w, int T, int Hq, int Hkv, int BS,
-    float eps, int apply_rope) {
-  constexpr int LPH = D / 8;  // lanes per head
-  constexpr int HALF = D / 2;
-  const int heads_total = Hq + 2 * Hkv;
-  const int item = (blockIdx.x * 256 + threadIdx.x) / LPH;
-  const int li = threadIdx.x % LPH;
-  if (item >= T * heads_total) return;
-  const int t = item / heads_total;
-  const int h = item % heads_total;
-  const bf16* src = qkv + (size_t)t * qkv_stride + h * D;
-  bf16x4 a = *reinterpret_cast<const bf16x4*>(src + 4 * li);
-  bf16x4 b = *reinterpret_cast<const bf16x4*>(src + HALF + 4 * li);
-  float xa[4], xb[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { xa[j] = bf2f(a[j]); xb[j] = bf2f(b[j]); }
-
+template <bool F8>
+__device__ __forceinline__ void qk_item(const bf16* __restrict__ qkv, int qkv_stride,
+                                        bf16* __restrict__ q_out, void* __restrict__ k_cache,
+                                        const int64_t* __restrict__ positions,
+                                        const int64_t* __restrict__ slots,
+                                        const float* __restrict__ cos_sin,
+                                        const bf16* __restrict__ q_w, const bf16* __restrict__ k_w,
+                                        int T, int Hq, int Hkv, int BS, float eps, int apply_rope) {
+  constexpr int D = 128, HALF = 64;
+  const int item = (blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int li = threadIdx.x & 15;
+  // every lane of a 16-lane row shares the item, so rows exit together (DPP stays valid)
+  if (item >= T * (Hq + Hkv)) return;
+  const int t = item / (Hq + Hkv);
+  const int h = item % (Hq + Hkv);
   const bool is_q = h < Hq;
-  const bool is_k = !is_q && h < Hq + Hkv;
-  if (is_q || is_k) {
-    const bf16* nw = is_q ? q_w : k_w;
-    if (nw != nullptr) {
-      float ss = 0.f;
+  const bf16x8 raw = *reinterpret_cast<const bf16x8*>(qkv + (size_t)t * qkv_stride + h * D +
+                                                      8 * li);
+  float x[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
+  for (int j = 0; j < 8; ++j) x[j] = bf2f(raw[j]);
+  const bf16* nw = is_q ? q_w : k_w;
+  if (nw != nullptr) {
+    float ss = 0.f;
 #pragma unroll
-      for (int o = LPH / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, LPH);
-      const float inv = rsqrtf(ss / (float)D + eps);
-      bf16x4 wa = *reinterpret_cast<const bf16x4*>(nw + 4 * li);
-      bf16x4 wb = *reinterpret_cast<const bf16x4*>(nw + HALF + 4 * li);
+    for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        // round-trip through bf16 like the reference module (norm output is bf16)
-        xa[j] = bf2f(f2bf(xa[j] * inv * bf2f(wa[j])));
-        xb[j] = bf2f(f2bf(xb[j] * inv * bf2f(wb[j])));
-      }
+    for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+    const float inv = rsqrtf(ss / (float)D + eps);
+    const bf16x8 w = *reinterpret_cast<const bf16x8*>(nw + 8 * li);
+    // round-trip through bf16 like the reference module (norm output is bf16)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = bf2f(f2bf(x[j] * inv * bf2f(w[j])));
+  }
+  if (apply_rope) {
+    // partner values are exactly representable in bf16 here (raw input or bf16-rounded
+    // norm output), so they travel packed: 4 DPP moves for 8 values
+    uint32_t pk[4], pp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x2 v2 = {f2bf(x[2 * j]), f2bf(x[2 * j + 1])};
+      pk[j] = __builtin_bit_cast(uint32_t, v2);
+      pp[j] = dpp_xor8(pk[j]);
     }
-    if (apply_rope) {
-      const float* cs = cos_sin + (size_t)positions[t] * D;
-      f32x4 c = *reinterpret_cast<const f32x4*>(cs + 4 * li);
-      f32x4 s = *reinterpret_cast<const f32x4*>(cs + HALF + 4 * li);
+    const float* cs = cos_sin + (size_t)positions[t] * D + 8 * (li & 7);
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs);
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + 4);
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + HALF);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + HALF + 4);
+    const float sg = li < 8 ? -1.f : 1.f;  // first half: x1 c - x2 s; second: x2 c + x1 s
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float x1 = xa[j], x2 = xb[j];
-        xa[j] = x1 * c[j] - x2 * s[j];
-        xb[j] = x2 * c[j] + x1 * s[j];
-      }
+    for (int j = 0; j < 8; ++j) {
+      const bf16x2 p2 = __builtin_bit_cast(bf16x2, pp[j >> 1]);
+      const float p = bf2f(p2[j & 1]);
+      const float c = j < 4 ? c0[j] : c1[j - 4];
+      const float s = j < 4 ? s0[j] : s1[j - 4];
+      x[j] = x[j] * c + sg * p * s;
     }
   }
-  bf16x4 oa, ob;
+  bf16x8 o;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) { oa[j] = f2bf(xa[j]); ob[j] = f2bf(xb[j]); }
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(x[j]);
   if (is_q) {
-    bf16* dst = q_out + ((size_t)t * Hq + h) * D;
-    *reinterpret_cast<bf16x4*>(dst + 4 * li) = oa;
-    *reinterpret_cast<bf16x4*>(dst + HALF + 4 * li) = ob;
+    *reinterpret_cast<bf16x8*>(q_out + ((size_t)t * Hq + h) * D + 8 * li) = o;
     return;
   }
   const int64_t slot = slots[t];
   if (slot < 0) return;
   const int64_t blk = slot / BS;
   const int off = (int)(slot % BS);
-  if (is_k) {
-    const int kh = h - Hq;
-    const size_t e = ((size_t)blk * Hkv + kh) * BS * D + k_swz_offset(off);
-    if constexpr (F8) {
-      uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e;
-      // from the bf16-rounded values (same rounding chain as the bf16 cache + reference)
-      *reinterpret_cast<uint32_t*>(dst + k_dim_offset(4 * li)) =
-          f32x4_to_fp8x4((float)oa[0], (float)oa[1], (float)oa[2], (float)oa[3]);
-      *reinterpret_cast<uint32_t*>(dst + k_dim_offset(HALF + 4 * li)) =
-          f32x4_to_fp8x4((float)ob[0], (float)ob[1], (float)ob[2], (float)ob[3]);
-    } else {
-      bf16* dst = reinterpret_cast<bf16*>(k_cache) + e;
-      *reinterpret_cast<bf16x4*>(dst + k_dim_offset(4 * li)) = oa;
-      *reinterpret_cast<bf16x4*>(dst + k_dim_offset(HALF + 4 * li)) = ob;
-    }
+  const size_t e = ((size_t)blk * Hkv + (h - Hq)) * BS * D + k_swz_offset(off) +
+                   k_dim_offset(8 * li);
+  if constexpr (F8) {
+    // from the bf16-rounded values (same rounding chain as the bf16 cache + reference)
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 w;
+    w[0] = f32x4_to_fp8x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]);
+    w[1] = f32x4_to_fp8x4((float)o[4], (float)o[5], (float)o[6], (float)o[7]);
+    *reinterpret_cast<u32x2*>(reinterpret_cast<uint8_t*>(k_cache) + e) = w;
   } else {
-    // tokens of a complete 8-token slot group are written by v_group_write_kernel as
-    // 16-byte vectors; only stragglers (chunk edges, decode tokens) scatter 2-byte stores
-    if (v_group_complete(slots, t, T, slot)) return;
-    const int vh = h - Hq - Hkv;
-    const size_t e = ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + (off & 7);
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(k_cache) + e) = o;
+  }
+}
+
+// v role: one workgroup per (64-token span of the batch, kv head).  V rows are staged
+// through LDS with 16-byte loads; each run of batch tokens that falls into one 8-token
+// slot group (its "leader" is the run's first token) is written by the span holding the
+// leader: a complete group as one 16-byte [D][8] vector per dim, a partial group (chunk
+// edges, decode tokens) as 2-byte scatters.  Written slots are never shared between
+// sequences (shared prefix blocks are full and read-only), so a run of consecutive slots
+// is one sequence's consecutive positions.
+constexpr int V_SPAN = 64;
+constexpr int V_ROWS = V_SPAN + 7;  // a run starting in the span may end 7 tokens past it
+
+template <bool F8>
+__device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_stride,
+                                       void* __restrict__ v_cache,
+                                       const int64_t* __restrict__ slots, int T, int Hq, int Hkv,
+                                       int BS, int span_id) {
+  constexpr int D = 128;
+  __shared__ bf16 tile[V_ROWS][D];
+  __shared__ int lead_n[V_SPAN];  // run length if the token leads a run, else 0
+  __shared__ int lead_list[V_SPAN];
+  __shared__ int n_leads;
+  const int vh = span_id % Hkv;
+  const int t0 = (span_id / Hkv) * V_SPAN;
+  const int rows = min(V_ROWS, T - t0);
+  const int tid = threadIdx.x;
+  const bf16* src = qkv + (size_t)t0 * qkv_stride + (Hq + Hkv + vh) * D;
+  for (int i = tid; i < rows * (D / 8); i += 256) {
+    const int r = i >> 4, c = (i & 15) * 8;
+    *reinterpret_cast<bf16x8*>(&tile[r][c]) =
+        *reinterpret_cast<const bf16x8*>(src + (size_t)r * qkv_stride + c);
+  }
+  if (tid < V_SPAN) {
+    const int t = t0 + tid;
+    int n = 0;
+    if (t < T) {
+      const int64_t s = slots[t];
+      if (s >= 0 && (t == 0 || (s & 7) == 0 || slots[t - 1] != s - 1)) {
+        n = 1;
+        const int lim = 8 - (int)(s & 7);
+        while (n < lim && t + n < T && slots[t + n] == s + n) ++n;
+      }
+    }
+    lead_n[tid] = n;
+    // wave 0 holds the 64 span tokens: compact the leaders with a ballot
+    const uint64_t m = __ballot(n > 0);
+    if (n > 0) lead_list[__popcll(m & ((1ull << tid) - 1))] = tid;
+    if (tid == 0) n_leads = __popcll(m);
+  }
+  __syncthreads();
+  const int half = tid >> 7, d = tid & 127;
+  for (int j = half; j < n_leads; j += 2) {
+    const int i = lead_list[j];
+    const int n = lead_n[i];
+    const int64_t s = slots[t0 + i];
+    const int64_t blk = s / BS;
+    const int off = (int)(s % BS);
+    const size_t g = ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + d * 8;
+    if (n == 8) {
+      bf16x8 v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+      for (int k = 0; k < 8; ++k) v[k] = tile[i + k][d];
       if constexpr (F8) {
-        uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e;
-        dst[(size_t)(4 * li + j) * 8] = f32_to_fp8((float)oa[j]);
-        dst[(size_t)(HALF + 4 * li + j) * 8] = f32_to_fp8((float)ob[j]);
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 w;
+        w[0] = f32x4_to_fp8x4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+        w[1] = f32x4_to_fp8x4((float)v[4], (float)v[5], (float)v[6], (float)v[7]);
+        *reinterpret_cast<u32x2*>(reinterpret_cast<uint8_t*>(v_cache) + g) = w;
       } else {
-        bf16* dst = reinterpret_cast<bf16*>(v_cache) + e;
-        dst[(size_t)(4 * li + j) * 8] = oa[j];
-        dst[(size_t)(HALF + 4 * li + j) * 8] = ob[j];
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(v_cache) + g) = v;
+      }
+    } else {
+      for (int k = 0; k < n; ++k) {
+        const size_t e = g + (off & 7) + k;
+        if constexpr (F8)
+          reinterpret_cast<uint8_t*>(v_cache)[e] = f32_to_fp8((float)tile[i + k][d]);
+        else
+          reinterpret_cast<bf16*>(v_cache)[e] = tile[i + k][d];
       }
     }
   }
 }
 
-// V cache groups are [D][8 tokens]: a token alone can only be written as D scattered
-// 2-byte stores.  When the batch holds all 8 tokens of a slot group (prefill chunks), a
-// thread per dim gathers the 8 values (each read coalesced across the wave) and writes one
-// 16-byte vector.  grid = (ceil(T / 64), Hkv), 128 threads = one per dim.
 template <bool F8>
-__global__ __launch_bounds__(128) void v_group_write_kernel(const bf16* __restrict__ qkv,
-                                                            int qkv_stride,
-                                                            void* __restrict__ v_cache,
-                                                            const int64_t* __restrict__ slots,
-                                                            int T, int Hq, int Hkv, int BS) {
-  constexpr int D = 128;
-  const int vh = blockIdx.y;
-  const int d = threadIdx.x;
-  const int t_end = min(T, (int)(blockIdx.x + 1) * 64);
-  for (int t = blockIdx.x * 64; t < t_end; ++t) {
-    const int64_t slot = slots[t];
-    if (slot < 0 || (slot & 7) != 0 || !v_group_complete(slots, t, T, slot)) continue;
-    const bf16* src = qkv + (size_t)t * qkv_stride + (Hq + Hkv + vh) * D + d;
-    bf16x8 g8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) g8[i] = src[(size_t)i * qkv_stride];
-    const int64_t blk = slot / BS;
-    const int off = (int)(slot % BS);
-    const size_t e = ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + d * 8;
-    if constexpr (F8) {
-      uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(v_cache) + e);
-      dst[0] = f32x4_to_fp8x4((float)g8[0], (float)g8[1], (float)g8[2], (float)g8[3]);
-      dst[1] = f32x4_to_fp8x4((float)g8[4], (float)g8[5], (float)g8[6], (float)g8[7]);
-    } else {
-      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(v_cache) + e) = g8;
-    }
-  }
+__global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
+    const bf16* __restrict__ qkv, int qkv_stride, bf16* __restrict__ q_out,
+    void* __restrict__ k_cache, void* __restrict__ v_cache, const int64_t* __restrict__ positions,
+    const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
+    const bf16* __restrict__ q_w, const bf16* __restrict__ k_w, int T, int Hq, int Hkv, int BS,
+    float eps, int apply_rope, int qk_blocks) {
+  if ((int)blockIdx.x < qk_blocks)
+    qk_item<F8>(qkv, qkv_stride, q_out, k_cache, positions, slots, cos_sin, q_w, k_w, T, Hq, Hkv,
+                BS, eps, apply_rope);
+  else
+    v_span<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks);
 }
 
 void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, void* k_cache,
@@ -175,24 +213,16 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
                                hipStream_t s, int kv_fp8) {
   if (T == 0 || D != 128) return;
-  const long items = (long)T * (Hq + 2 * Hkv);
-  const long threads = items * (D / 8);
-  dim3 grid((threads + 255) / 256);
+  const long qk_threads = (long)T * (Hq + Hkv) * 16;
+  const int qk_blocks = (int)((qk_threads + 255) / 256);
+  const int v_blocks = ((T + V_SPAN - 1) / V_SPAN) * Hkv;
+  const dim3 grid(qk_blocks + v_blocks);
 #define QKR(F8)                                                                                 \
-  qk_norm_rope_cache_kernel<128, F8><<<grid, 256, 0, s>>>(                                      \
+  qk_norm_rope_cache_kernel<F8><<<grid, 256, 0, s>>>(                                           \
       (const bf16*)qkv, qkv_stride, (bf16*)q_out, k_cache, v_cache, positions, slots, cos_sin, \
-      (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope)
+      (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope, qk_blocks)
   if (kv_fp8) QKR(true); else QKR(false);
 #undef QKR
-  if (T >= 8) {
-    const dim3 g2((T + 63) / 64, Hkv);
-    if (kv_fp8)
-      v_group_write_kernel<true><<<g2, 128, 0, s>>>((const bf16*)qkv, qkv_stride, v_cache, slots,
-                                                     T, Hq, Hkv, BS);
-    else
-      v_group_write_kernel<false><<<g2, 128, 0, s>>>((const bf16*)qkv, qkv_stride, v_cache,
-                                                      slots, T, Hq, Hkv, BS);
-  }
 }
 
 // Plain scatter of already-final K/V rows into the paged cache (used by the

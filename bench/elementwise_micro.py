@@ -25,6 +25,10 @@ cs = ref.rope_cos_sin(4096, D, 1e6, device=dev)
 qw = torch.ones(D, device=dev, dtype=torch.bfloat16)
 gu = torch.randn(T, 6144, device=dev, dtype=torch.bfloat16)
 noslots = torch.full_like(slots, -1)
+# engine-like prefill slots: 512-token sequences, each in its own randomly placed blocks
+_blocks = torch.randperm(NB, device=dev)
+_tok = torch.arange(T, device=dev)
+pslots = _blocks[_tok // BS] * BS + _tok % BS
 # engine-like: 28 layers' caches, each written once per "step" (cold in L2)
 L = 28
 caches = [(torch.zeros(NB, hkv, BS, D, device=dev, dtype=torch.bfloat16),
@@ -36,7 +40,7 @@ _layer = [0]
 
 def layered():
     i = _layer[0] = (_layer[0] + 1) % L
-    ops.qk_norm_rope_cache(qkvs[i], q, caches[i][0], caches[i][1], pos, slots, cs, qw, qw, hq,
+    ops.qk_norm_rope_cache(qkvs[i], q, caches[i][0], caches[i][1], pos, pslots, cs, qw, qw, hq,
                            hkv, 1e-6)
 
 
@@ -44,6 +48,8 @@ fns = {
     "qk_rope_no_cache_write": lambda: ops.qk_norm_rope_cache(qkv, q, kc, vc, pos, noslots, cs,
                                                              qw, qw, hq, hkv, 1e-6),
     "qk_rope_28_layer_caches": layered,
+    "qk_norm_rope_cache_prefill_slots": lambda: ops.qk_norm_rope_cache(
+        qkv, q, kc, vc, pos, pslots, cs, qw, qw, hq, hkv, 1e-6),
     "rmsnorm": lambda: ops.rms_norm(x, w, 1e-6),
     "fused_add_rmsnorm": lambda: ops.fused_add_rms_norm(x, r, w, 1e-6),
     "qk_norm_rope_cache": lambda: ops.qk_norm_rope_cache(qkv, q, kc, vc, pos, slots, cs, qw, qw,

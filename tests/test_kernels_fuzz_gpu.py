@@ -137,3 +137,46 @@ def test_fuzz_embedding(T, shape, seed):
     ids = torch.randint(0, V, (T,), generator=g)
     table = torch.randn(V, d, generator=g).bfloat16()
     _close(ops.embedding(ids.to(DEV), table.to(DEV)), ref.embedding(ids, table, 0, V), atol=0)
+
+
+@FUZZ
+@given(st.lists(st.tuples(st.integers(0, 40), st.integers(1, 150)), min_size=1, max_size=5),
+       st.booleans(), st.booleans(), st.integers(0, 1000))
+def test_fuzz_qk_norm_rope_cache(runs, qk_norm, fp8, seed):
+    """Batches made of runs of consecutive slots at arbitrary offsets (prefill chunks,
+    chunk edges, decode tokens, padding -1): every 8-token V group is either complete,
+    partial or split across the kernel's 64-token spans."""
+    hq, hkv, D, BS = 16, 8, 128, 32
+    g = torch.Generator().manual_seed(seed)
+    slots, base = [], 0
+    for start, n in runs:
+        if start == 0 and slots:
+            slots.append(-1)
+        base = (base + BS * 2 + start)  # disjoint slot ranges per run
+        slots += list(range(base, base + n))
+        base += n
+    T = len(slots)
+    NB = base // BS + 2
+    slots = torch.tensor(slots, dtype=torch.int64)
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, generator=g).bfloat16()
+    pos = torch.randint(0, 4000, (T,), generator=g)
+    cs = ref.rope_cos_sin(4096, D, 1e6)
+    qw = torch.randn(D, generator=g).bfloat16() if qk_norm else None
+    kw = torch.randn(D, generator=g).bfloat16() if qk_norm else None
+    dt = torch.uint8 if fp8 else torch.bfloat16
+    kc = torch.zeros(NB, hkv, BS, D, dtype=dt)
+    vc = torch.zeros(NB, hkv, BS // 8, D, 8, dtype=dt)
+    q_ref = torch.empty(T, hq, D).bfloat16()
+    kg, vg = kc.to(DEV), vc.to(DEV)
+    ref.qk_norm_rope_cache(qkv, q_ref, kc, vc, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
+    q_out = torch.empty(T, hq, D, device=DEV, dtype=torch.bfloat16)
+    ops.qk_norm_rope_cache(qkv.to(DEV), q_out, kg, vg, pos.to(DEV), slots.to(DEV), cs.to(DEV),
+                           None if qw is None else qw.to(DEV), None if kw is None else kw.to(DEV),
+                           hq, hkv, 1e-6)
+    _close(q_out, q_ref, atol=3e-2, rtol=2e-2)
+    if fp8:
+        _close(ref.from_cache(kg.cpu()), ref.from_cache(kc), atol=1e-2, rtol=0.13)
+        assert torch.equal(vg.cpu(), vc)
+    else:
+        _close(kg, kc, atol=3e-2, rtol=2e-2)
+        assert torch.equal(vg.cpu(), vc)
