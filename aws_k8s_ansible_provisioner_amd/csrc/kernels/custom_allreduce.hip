@@ -38,8 +38,14 @@ __device__ __forceinline__ bool car_wait(const uint32_t* flag, uint32_t v) {
 }
 
 // All ranks' blocks meet at phase `ph` (0 or 1) of epoch ep.
+// Publish: EVERY storing wave drains its own stores with an explicit s_waitcnt AFTER the
+// release fence (ROCm 7.2 can drop the fence's own wait -- cdna_hip_programming.md §6
+// Guideline 16, Pitfalls 12 and 14: a rare stale peer read under load otherwise) before the
+// barrier that lets one lane raise the flags.  Consume: the polling lanes' acquire (buffer_inv)
+// is likewise drained before the barrier that releases the other waves' peer loads.
 __device__ __forceinline__ void car_barrier(const CarArgs& a, int bid, uint32_t ep, int ph) {
   __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int t = threadIdx.x;
   const size_t slot = ((size_t)ph * kCarMaxRanks + a.rank) * kCarMaxBlocks + bid;
@@ -47,6 +53,8 @@ __device__ __forceinline__ void car_barrier(const CarArgs& a, int bid, uint32_t 
   if (t < a.world) {
     const size_t mine = ((size_t)ph * kCarMaxRanks + t) * kCarMaxBlocks + bid;
     if (!car_wait(a.sigs[a.rank] + mine, ep)) atomicOr(a.err, 1u);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 }

@@ -71,6 +71,32 @@ void launch_gemm_bf16(const void* X, const void* W, void* Y, float* ws, int M, i
                       int ldx, int ldw, int ldy, int splitk, hipStream_t st,
                       int* counters = nullptr);
 
+// ---- dgemm.hip ----
+// Fused decode GEMM: A-operand prologue (PRO_*) folded into the MFMA GEMM's staging, and an
+// epilogue (EPI_*) doing a decode layer's residual add + next-norm elementwise half, or SwiGLU.
+// Split-K partials (+ per-row sums of squares) are reduced by a second pass with the same epilogue.
+enum { PRO_PLAIN = 0, PRO_ADDNORM = 1, PRO_SILU = 2 };
+enum { EPI_STORE = 0, EPI_RESNORM = 1, EPI_SILU = 2 };
+struct DGemmArgs {
+  // bf16 tensors (void* so this header stays free of device types)
+  const void* X;     // A source: [M, K] (PLAIN/ADDNORM) or [M, 2K] = [gate | up] (SILU)
+  const void* R;     // ADDNORM: residual in [M, K] (row stride K)
+  void* Rout;        // ADDNORM: residual out = X + R (must not alias R)
+  const void* ln;    // ADDNORM: RMSNorm weight [K]
+  const void* W;     // [N, K] (row stride ldw)
+  void* Y;           // [M, N] (row stride ldy); EPI_RESNORM: residual in/out; EPI_SILU: [M, N/2]
+  float* ws;         // split-K: fp32 [S, M, N] (+ [S, M] sums of squares for ADDNORM)
+  const float* ss_in;  // PLAIN: optional per-row sum of squares -> rows scaled by rsqrt(ss/K+eps)
+  float* ss_out;       // EPI_RESNORM: per-row sum of squares of the new residual (+= atomics)
+  void* Aout;          // EPI_RESNORM: bf16(residual * ln_out) [M, N] dense
+  const void* ln_out;  // EPI_RESNORM: next RMSNorm weight [N]
+  int M, N, K, ldx, ldw, ldy, kps, epi;
+  float eps;
+};
+bool dgemm_supported(int M, int N, int K, int splitk, int pf);
+bool dgemm_epi_supported(int N, int epi, int splitk);
+void launch_dgemm(const DGemmArgs& a, int pro, int splitk, int pf, hipStream_t st);
+
 // ---- sampling.hip ----
 struct SampleParams {
   const void* logits;  // [B, V] (row stride ld), fp32 or bf16

@@ -274,6 +274,80 @@ void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk,
                          w.stride(0), out.stride(0), splitk, cur_stream(), cnt);
 }
 
+// Fused decode GEMM: out = prologue(x, ...) @ w^T, then an epilogue.
+// pro 0 plain (optional ss_in row scale), 1 residual-add + RMSNorm (r = residual in,
+// rout = x + r out, ln = norm weight), 2 SiLU(gate) * up over x = [gate|up].
+// epi 0 store, 1 residual/next-norm (out = residual in/out, aout = bf16(out * ln_out),
+// ss_out += row sums of squares), 2 SwiGLU over gate/up-interleaved rows (out [M, N/2]).
+void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t splitk, int64_t pf,
+           std::optional<Tensor> r, std::optional<Tensor> rout, std::optional<Tensor> ln,
+           double eps, int64_t epi, std::optional<Tensor> ss_in, std::optional<Tensor> ss_out,
+           std::optional<Tensor> aout, std::optional<Tensor> ln_out) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "dgemm: 2-D tensors");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(pro >= 0 && pro <= 2, "dgemm: prologue 0|1|2");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "dgemm: epilogue 0|1|2");
+  TORCH_CHECK(epi == 0 || pro == 0, "dgemm: epilogues 1|2 need the plain prologue");
+  TORCH_CHECK(x.size(1) == (pro == akap::PRO_SILU ? 2 * K : K), "dgemm: x width");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == akap::EPI_SILU ? N / 2 : N),
+              "dgemm: out shape");
+  TORCH_CHECK(akap::dgemm_supported(M, N, K, splitk, pf), "dgemm: unsupported M/N/K/splitk/pf");
+  TORCH_CHECK(akap::dgemm_epi_supported(N, epi, splitk), "dgemm: unsupported epilogue/N/splitk");
+  TORCH_CHECK((int64_t)N * K * 2 >= (int64_t)M * 4, "dgemm: W smaller than M floats");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
+              "dgemm: 16-byte aligned rows");
+  if (splitk > 1) {
+    const int64_t need = splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= need,
+                "dgemm: fp32 workspace of splitk*M*N (+ splitk*M for the norm)");
+    TORCH_CHECK(out.stride(0) == N, "dgemm: split-K output must be dense");
+  }
+  akap::DGemmArgs a{};
+  a.X = x.data_ptr();
+  a.W = w.data_ptr();
+  a.Y = out.data_ptr();
+  a.ws = splitk > 1 ? ws.data_ptr<float>() : nullptr;
+  a.M = M; a.N = N; a.K = K;
+  a.ldx = x.stride(0); a.ldw = w.stride(0); a.ldy = out.stride(0);
+  a.eps = (float)eps;
+  a.epi = (int)epi;
+  if (pro == akap::PRO_ADDNORM) {
+    TORCH_CHECK(r && rout && ln, "dgemm addnorm: residual, residual-out and norm weight");
+    CHECK_BF16(*r); CHECK_BF16(*rout); CHECK_BF16(*ln);
+    CHECK_CONTIG(*r); CHECK_CONTIG(*rout); CHECK_CONTIG(*ln);
+    TORCH_CHECK(r->numel() == (int64_t)M * K && rout->numel() == (int64_t)M * K &&
+                ln->numel() == K, "dgemm addnorm: residual [M, K], norm weight [K]");
+    TORCH_CHECK(r->data_ptr() != rout->data_ptr(), "dgemm addnorm: rout must not alias r");
+    a.R = r->data_ptr();
+    a.Rout = rout->data_ptr();
+    a.ln = ln->data_ptr();
+  }
+  if (pro == akap::PRO_PLAIN && ss_in) {
+    TORCH_CHECK(ss_in->scalar_type() == at::kFloat && ss_in->is_cuda() && ss_in->numel() >= M,
+                "dgemm: ss_in fp32 [M]");
+    a.ss_in = ss_in->data_ptr<float>();
+  }
+  if (epi == akap::EPI_RESNORM) {
+    TORCH_CHECK(ss_out && aout && ln_out, "dgemm resnorm epilogue: ss_out, aout, ln_out");
+    TORCH_CHECK(ss_out->scalar_type() == at::kFloat && ss_out->numel() >= M, "ss_out fp32 [M]");
+    CHECK_BF16(*aout); CHECK_CONTIG(*aout); CHECK_BF16(*ln_out);
+    TORCH_CHECK(aout->numel() == (int64_t)M * N && ln_out->numel() == N,
+                "dgemm resnorm: aout [M, N], ln_out [N]");
+    TORCH_CHECK(out.stride(0) == N, "dgemm resnorm: residual must be dense");
+    a.ss_out = ss_out->data_ptr<float>();
+    a.Aout = aout->data_ptr();
+    a.ln_out = ln_out->data_ptr();
+  }
+  const c10::DeviceGuard g(x.device());
+  akap::launch_dgemm(a, (int)pro, (int)splitk, (int)pf, cur_stream());
+}
+
+bool dgemm_ok(int64_t M, int64_t N, int64_t K, int64_t splitk, int64_t pf) {
+  return akap::dgemm_supported(M, N, K, splitk, pf);
+}
+
 void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
             Tensor steps, Tensor out_tokens, Tensor out_logprobs, bool greedy_logprobs) {
   CHECK_GPU(logits);
@@ -617,6 +691,12 @@ TORCH_LIBRARY(akap, m) {
       "gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int splitk, "
       "Tensor(c!)? counters=None) -> ()");
   m.def("gemm_splitk(int M, int N, int K) -> int");
+  m.def(
+      "dgemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int pro, int splitk, int pf, "
+      "Tensor? r=None, Tensor(c!)? rout=None, Tensor? ln=None, float eps=1e-6, int epi=0, "
+      "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
+      "Tensor? ln_out=None) -> ()");
+  m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
   m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");
   m.def("car_ipc_handles(int h) -> Tensor");
@@ -641,6 +721,7 @@ TORCH_LIBRARY(akap, m) {
 
 TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("gemm_splitk", &gemm_splitk);
+  m.impl("dgemm_ok", &dgemm_ok);
   m.impl("car_create", &car_create);
   m.impl("car_ipc_handles", &car_ipc_handles);
   m.impl("car_open", &car_open);
@@ -662,6 +743,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("apply_penalties", &apply_penalties);
   m.impl("argmax", &argmax);
   m.impl("gemm", &gemm);
+  m.impl("dgemm", &dgemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

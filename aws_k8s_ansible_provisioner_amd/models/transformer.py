@@ -29,6 +29,7 @@ from .moe import MoEBlock
 
 FUSED_DECODE = os.environ.get("AKAP_FUSED_DECODE", "1") != "0"
 PREFETCH_WEIGHTS = os.environ.get("AKAP_PREFETCH_WEIGHTS", "0") == "1"
+FUSED_GEMM = os.environ.get("AKAP_FUSED_GEMM", "1") != "0"
 
 
 @dataclasses.dataclass
@@ -265,6 +266,13 @@ class DecoderLM:
         cfg = self.cfg
         T = input_ids.shape[0]
         eps = cfg.rms_eps
+        if (not batch.is_prefill and FUSED_DECODE and FUSED_GEMM and self.ps.tp_size == 1
+                and self.device.type == "cuda"):
+            from ..ops import gemm_tuner
+
+            plan = gemm_tuner.fused_plan(T)
+            if plan is not None:
+                return self._forward_fused_decode(input_ids, batch, k_caches, v_caches, plan)
         x = self.embed_tokens(input_ids)
         residual = x
         h = ops.rms_norm(x, self.layers[0].ln1, eps)
@@ -299,6 +307,51 @@ class DecoderLM:
             else:
                 gu = ops.linear(h, lw.w_gate_up)
                 x = comm.tp_all_reduce(ops.linear(ops.silu_and_mul(gu), lw.w_down))
+        h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
+        return h
+
+    def _forward_fused_decode(self, input_ids, batch: AttnBatch, k_caches, v_caches, plan: dict
+                              ) -> torch.Tensor:
+        """Dense decode step as 4 fused GEMM launches + 1 attention launch per layer
+        (csrc/kernels/dgemm.hip): the residual add and the elementwise half of the next
+        RMSNorm run in the O / down projections' epilogues (which also accumulate the
+        per-row sum of squares), the norm's row scale in the consumer GEMM's epilogue, and
+        SwiGLU in the gate|up projection's epilogue -- no separate norm / activation kernels.
+        Single rank (no all-reduce between GEMM and residual add); plan from
+        gemm_tuner.tune_fused: projection -> (split-K, prefetch depth)."""
+        T = input_ids.shape[0]
+        eps = self.cfg.rms_eps
+        L = len(self.layers)
+        residual = self.embed_tokens(input_ids)
+        ss = torch.zeros(2 * L, T, dtype=torch.float32, device=self.device)
+        a1 = ops.rms_norm(residual, self.layers[0].ln1, eps)
+        ss_in = None
+        for li, lw in enumerate(self.layers):
+            s_, p_ = plan["w_qkv"]
+            qkv = ops.dgemm(a1, lw.w_qkv, splitk=s_, pf=p_, eps=eps, ss_in=ss_in)
+            attn = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+            ops.paged_attention_decode_fused(
+                attn, qkv, k_caches[li], v_caches[li], batch.block_tables, batch.seq_lens,
+                batch.positions, batch.slots, self.cos_sin, lw.q_norm, lw.k_norm,
+                self.hq // self.hkv, self.scale, eps, workspace=batch.workspace,
+                num_parts=batch.num_parts, part_size=batch.part_size)
+            a2 = torch.empty_like(residual)
+            s_, p_ = plan["w_o"]
+            ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, splitk=s_, pf=p_, eps=eps,
+                      out=residual, epi=ops.EPI_RESNORM, ss_out=ss[2 * li], a_out=a2,
+                      ln_out=lw.ln2)
+            s_, p_ = plan["w_gate_up"]
+            act = ops.dgemm(a2, lw.w_gate_up, splitk=s_, pf=p_, eps=eps, ss_in=ss[2 * li],
+                            epi=ops.EPI_SILU)
+            s_, p_ = plan["w_down"]
+            if li + 1 < L:
+                a1 = torch.empty_like(residual)
+                ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps, out=residual,
+                          epi=ops.EPI_RESNORM, ss_out=ss[2 * li + 1], a_out=a1,
+                          ln_out=self.layers[li + 1].ln1)
+                ss_in = ss[2 * li + 1]
+            else:
+                x = ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps)
         h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
         return h
 

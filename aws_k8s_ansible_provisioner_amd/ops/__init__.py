@@ -193,6 +193,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
 
         choice = gemm_tuner.lookup(M, w.shape[0], w.shape[1])
         if choice is not None:  # measured at engine start (cold weights, real layers)
+            if choice[0] == "dgemm" and x.stride(-1) == 1:
+                return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out)
             split = choice[1] if choice[0] == "hip" else 0
     if split is None:
         use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
@@ -219,6 +221,84 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
             ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
     torch.ops.akap.gemm(out, x, w, ws, s)
     return out
+
+
+PRO_PLAIN, PRO_ADDNORM, PRO_SILU = 0, 1, 2
+EPI_STORE, EPI_RESNORM, EPI_SILU = 0, 1, 2
+
+
+def silu_interleave_perm(F: int) -> torch.Tensor:
+    """Row order in which EPI_SILU reads a [gate (F rows); up (F rows)] weight: 16-row groups
+    alternate gate / up of the same 16 features (virtual column v -> this row)."""
+    v = torch.arange(2 * F)
+    return ((v >> 4) & 1) * F + (v >> 5) * 16 + (v & 15)
+
+
+def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 1, pf: int = 2,
+          residual: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None,
+          ln: Optional[torch.Tensor] = None, eps: float = 1e-6,
+          out: Optional[torch.Tensor] = None, epi: int = EPI_STORE,
+          ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
+          a_out: Optional[torch.Tensor] = None, ln_out: Optional[torch.Tensor] = None
+          ) -> torch.Tensor:
+    """Fused decode GEMM (csrc/kernels/dgemm.hip): y = A @ w.T where A is produced from x by
+    the prologue inside the GEMM's operand staging --
+      PRO_PLAIN    A = x; with ss_in, rows of y are scaled by rsqrt(ss_in / K + eps)
+      PRO_ADDNORM  s = x + residual (written to residual_out), A = rmsnorm(s) * ln
+      PRO_SILU     x = [gate | up] ([M, 2K]), A = silu(gate) * up
+    and an epilogue --
+      EPI_STORE    out = bf16(y)
+      EPI_RESNORM  out is the residual stream [M, N] (in/out): out = bf16(bf16(y) + out);
+                   a_out = bf16(out * ln_out); ss_out += per-row sum of out^2 (caller zeroes)
+      EPI_SILU     w = [gate; up] rows, out [M, N/2] = silu(y_gate) * y_up
+    replacing the separate fused_add_rms_norm / silu_and_mul launches of a decode layer."""
+    M = x.shape[0]
+    N, K = w.shape
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == EPI_SILU else N, dtype=x.dtype, device=x.device)
+    if not _native(x):
+        if pro == PRO_ADDNORM:
+            s = (x.float() + residual.float()).to(x.dtype)
+            residual_out.copy_(s)
+            a = ref.rms_norm(s, ln, eps)
+        elif pro == PRO_SILU:
+            a = ref.silu_and_mul(x)
+        else:
+            a = x
+        y = torch.nn.functional.linear(a.float(), w.float())
+        if pro == PRO_PLAIN and ss_in is not None:
+            y = y * torch.rsqrt(ss_in[:M].float() / K + eps)[:, None]
+        if epi == EPI_RESNORM:
+            r = (y.to(x.dtype).float() + out.float()).to(x.dtype)
+            out.copy_(r)
+            a_out.copy_((r.float() * ln_out.float()).to(x.dtype))
+            ss_out[:M] += r.float().pow(2).sum(-1)
+        elif epi == EPI_SILU:
+            out.copy_(ref.silu_and_mul(y.to(x.dtype)))
+        else:
+            out.copy_(y.to(out.dtype))
+        return out
+    if splitk > 1:
+        n = splitk * M * N + (splitk * M if pro == PRO_ADDNORM else 0)
+        ws = torch.empty(n, dtype=torch.float32, device=x.device)
+    else:
+        ws = _EMPTY_F32.get(x.device)
+        if ws is None:
+            ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
+    torch.ops.akap.dgemm(out, x, w, ws, pro, splitk, pf, residual, residual_out, ln, eps, epi,
+                         ss_in, ss_out, a_out, ln_out)
+    return out
+
+
+def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI_STORE) -> bool:
+    """Mirror of dgemm_supported / dgemm_epi_supported in dgemm.hip (host-side, no GPU)."""
+    if epi == EPI_SILU and (splitk != 1 or N % 32):
+        return False
+    if epi == EPI_RESNORM and splitk > 1 and N % 256:
+        return False
+    if M <= 0 or N <= 0 or K <= 0 or splitk < 1 or N % 4 or pf not in (1, 2, 4, 8) or K % splitk:
+        return False
+    return (K // splitk) % (64 * pf) == 0
 
 
 _COUNTERS: dict = {}

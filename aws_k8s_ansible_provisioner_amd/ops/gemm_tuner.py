@@ -11,7 +11,11 @@ weights.
 
 The tuner times each candidate on the model's REAL per-layer weights, rotating through
 all layers inside one captured hipGraph (so every call sees cold weights, as in a decode
-step), and records the winner in the plan `ops.linear` consults.
+step), and records the winner in the plan `ops.linear` consults.  Candidates: hipBLASLt, the
+MFMA GEMM at each split-K, and the k-pipelined decode GEMM (csrc/kernels/dgemm.hip, plain
+prologue) at each (split-K, prefetch depth) -- the latter wins the narrow-N projections
+(o-proj, N = d) where a block's K loop is a chain of round trips
+(`profiles/r1_dgemm_micro.log`).
 """
 from __future__ import annotations
 
@@ -19,7 +23,7 @@ from typing import Optional, Sequence
 
 import torch
 
-Choice = tuple  # ("torch",) | ("hip", splitk)
+Choice = tuple  # ("torch",) | ("hip", splitk) | ("dgemm", splitk, prefetch_depth)
 _PLAN: dict = {}
 
 
@@ -56,7 +60,7 @@ def _timed(fn, n: int) -> float:
 
 
 def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
-         margin: float = 0.03) -> Choice:
+         margin: float = 0.03, pfs=(2, 4, 8)) -> Choice:
     """Pick the fastest way to compute x[M, K] @ w.T for these same-shape weights.
     hipBLASLt is kept unless the MFMA kernel is more than `margin` faster."""
     from . import gemm_counters  # noqa: F401  (ensures the native library is loaded)
@@ -77,7 +81,16 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
         t = _timed(lambda i: torch.ops.akap.gemm(y, x, weights[i % n], ws, s), n)
         if t < t_best:
             best, t_best = ("hip", s), t
-    if best[0] == "hip" and t_best > t_torch * (1.0 - margin):
+    from . import dgemm_supported
+    for s in splits:
+        for pf in pfs:
+            if not dgemm_supported(M, N, K, s, pf) or (s > 1 and K // s < 256):
+                continue
+            ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
+            t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, pf), n)
+            if t < t_best:
+                best, t_best = ("dgemm", s, pf), t
+    if best[0] != "torch" and t_best > t_torch * (1.0 - margin):
         best = ("torch",)
     _PLAN[(M, N, K)] = best
     return best
@@ -95,7 +108,117 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
     for M in Ms:
         for (name, shape), ws in groups.items():
             summary[(M, name)] = tune(M, ws)
-    wins = {k: v for k, v in summary.items() if v[0] == "hip"}
-    log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, MFMA kernel chosen for "
-        f"{len(wins)}: " + ", ".join(f"M={m} {n} s{c[1]}" for (m, n), c in sorted(wins.items())))
+    wins = {k: v for k, v in summary.items() if v[0] != "torch"}
+    log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, HIP kernel chosen for "
+        f"{len(wins)}: " + ", ".join(
+            f"M={m} {n} {c[0]} s{c[1]}" + (f"p{c[2]}" if len(c) > 2 else "")
+            for (m, n), c in sorted(wins.items())))
     return summary
+
+
+# ----------------------------------------------------------------------------- fused decode chain
+# A dense decode layer as 4 fused GEMM launches (csrc/kernels/dgemm.hip epilogues):
+#   qkv      plain, rows scaled by the input norm's rsqrt       (ss_in)
+#   o        residual += y; a2 = residual * ln2; ss2 += row sum  (EPI_RESNORM)
+#   gate_up  plain with ss2 row scale, SwiGLU epilogue           (EPI_SILU)
+#   down     residual += y; a1' = residual * ln1'; ss1' += ...   (EPI_RESNORM)
+# vs the unfused 7 launches (2 fused_add_rms_norm + silu_and_mul + 4 GEMMs at their tuned
+# best).  Chosen per M when the fused chain measures faster.
+_FUSED: dict = {}
+_FUSED_ROLES = (("w_qkv", 0), ("w_o", 1), ("w_gate_up", 2), ("w_down", 1))  # (weight, epi)
+
+
+def fused_plan(M: int) -> Optional[dict]:
+    return _FUSED.get(M)
+
+
+def _time_unfused(M: int, model) -> float:
+    lw0 = model.layers[0]
+    d = lw0.w_o.shape[0]
+    F = lw0.w_down.shape[1]
+    dev = lw0.w_o.device
+    x = torch.randn(M, d, device=dev, dtype=lw0.w_o.dtype) * 0.1
+    res = torch.randn(M, d, device=dev, dtype=lw0.w_o.dtype)
+    h = torch.empty_like(x)
+    gu = torch.randn(M, 2 * F, device=dev, dtype=lw0.w_o.dtype)
+    act = torch.empty(M, F, device=dev, dtype=lw0.w_o.dtype)
+    n = 8
+    t_norm = _timed(lambda i: torch.ops.akap.fused_add_rmsnorm(h, res, x, lw0.ln1, 1e-6), n)
+    t_silu = _timed(lambda i: torch.ops.akap.silu_and_mul(act, gu), n)
+    return 2 * t_norm + t_silu
+
+
+def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(1, 2, 4, 8),
+               verbose: bool = False) -> dict:
+    """Pick (split-K, prefetch) for each fused-chain GEMM at each M and keep the fused chain
+    for the M where it beats the unfused chain (both timed on the real cold layer weights)."""
+    from . import EPI_SILU, dgemm_supported
+
+    if not model.layers or any(getattr(l, "moe", None) is not None for l in model.layers):
+        return {}
+    L = len(model.layers)
+    dev = model.layers[0].w_o.device
+    dt = model.layers[0].w_o.dtype
+    chosen = {}
+    for M in Ms:
+        t_unfused = _time_unfused(M, model)
+        plan_m, t_fused = {}, 0.0
+        detail = []
+        for name, epi in _FUSED_ROLES:
+            ws_ = [getattr(l, name) for l in model.layers]
+            N, K = ws_[0].shape
+            t_plain = _time_best_plain(M, name, ws_)
+            t_unfused += t_plain
+            x = torch.randn(M, K, device=dev, dtype=dt) * 0.1
+            out = (torch.randn(M, N, device=dev, dtype=dt) if epi == 1 else
+                   torch.empty(M, N // 2 if epi == EPI_SILU else N, device=dev, dtype=dt))
+            ss = torch.full((M,), float(K), device=dev, dtype=torch.float32)
+            ss_o = torch.zeros(M, device=dev, dtype=torch.float32)
+            a_o = torch.empty(M, N, device=dev, dtype=dt)
+            ln = model.layers[0].ln2 if N == model.layers[0].ln2.numel() else None
+            best = None
+            for s in splits:
+                for pf in pfs:
+                    if not dgemm_supported(M, N, K, s, pf, epi) or (s > 1 and K // s < 256):
+                        continue
+                    wsp = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
+                    t = _timed(lambda i, s=s, pf=pf, wsp=wsp: torch.ops.akap.dgemm(
+                        out, x, ws_[i % L], wsp, 0, s, pf, None, None, None, 1e-6, epi,
+                        None if epi == 1 else ss, ss_o if epi == 1 else None,
+                        a_o if epi == 1 else None, ln if epi == 1 else None), L)
+                    if best is None or t < best[0]:
+                        best = (t, s, pf)
+            if best is None:
+                plan_m = None
+                break
+            plan_m[name] = (best[1], best[2])
+            t_fused += best[0]
+            detail.append(f"{name} {best[0]:.1f}/{t_plain:.1f}")
+        if plan_m is not None and t_fused < t_unfused:
+            _FUSED[M] = plan_m
+        chosen[M] = (t_fused, t_unfused, plan_m)
+        if verbose:
+            log(f"[gemm-tuner] M={M} fused/plain us: " + ", ".join(detail))
+    used = [m for m in Ms if m in _FUSED]
+    log("[gemm-tuner] fused decode layer chain (us/layer fused vs unfused): " + ", ".join(
+        f"M={m} {c[0]:.1f}/{c[1]:.1f}" + ("*" if m in _FUSED else "")
+        for m, c in chosen.items()) + f"  -> fused for {len(used)} of {len(Ms)} batch sizes")
+    return chosen
+
+
+def _time_best_plain(M: int, name: str, weights) -> float:
+    """us of the plan's choice for this projection (hipBLASLt unless tuned otherwise)."""
+    w0 = weights[0]
+    N, K = w0.shape
+    x = torch.randn(M, K, device=w0.device, dtype=w0.dtype) * 0.1
+    c = _PLAN.get((M, N, K), ("torch",))
+    n = len(weights)
+    if c[0] == "dgemm":
+        ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
+        y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)
+        return _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, c[1], c[2]), n)
+    if c[0] == "hip":
+        ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
+        y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)
+        return _timed(lambda i: torch.ops.akap.gemm(y, x, weights[i % n], ws, c[1]), n)
+    return _timed(lambda i: torch.nn.functional.linear(x, weights[i % n]), n)

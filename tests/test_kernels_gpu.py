@@ -443,9 +443,10 @@ def test_gemm_tuner_plan_is_used_and_correct():
     ref_ = x.float() @ ws[1].float().t()
     assert (y.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
     # force the MFMA path through the plan and check it too
-    gemm_tuner.plan()[(128, 1024, 3072)] = ("hip", 4)
-    y2 = ops.linear(x, ws[1])
-    assert (y2.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
+    for forced in (("hip", 4), ("dgemm", 4, 2), ("dgemm", 1, 4)):
+        gemm_tuner.plan()[(128, 1024, 3072)] = forced
+        y2 = ops.linear(x, ws[1])
+        assert (y2.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
     gemm_tuner.plan().pop((128, 1024, 3072))
 
 
@@ -534,3 +535,63 @@ def test_paged_attention_prefill_fp8(tile_rows):
                                 qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv, scale,
                                 tile_rows=tile_rows)
     _close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+def _dgemm_ref(pro, x, w, r, ln, eps):
+    """fp32 reference of the fused decode GEMM's prologue + GEMM (+ residual out)."""
+    x, w = x.float().cpu(), w.float().cpu()
+    s = None
+    if pro == ops.PRO_ADDNORM:
+        s = (x + r.float().cpu()).to(torch.bfloat16)
+        a = ref.rms_norm(s, ln.cpu(), eps).float()
+    elif pro == ops.PRO_SILU:
+        a = ref.silu_and_mul(x.to(torch.bfloat16)).float()
+    else:
+        a = x
+    return a @ w.t(), s
+
+
+@pytest.mark.parametrize("pro", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 1024), (37, 1024, 2048), (256, 4096, 1024),
+                                   (130, 3072, 512)])
+@pytest.mark.parametrize("splitk,pf", [(1, 1), (1, 2), (2, 4), (4, 1), (8, 2)])
+def test_fused_decode_gemm(pro, M, N, K, splitk, pf):
+    if not ops.dgemm_supported(M, N, K, splitk, pf):
+        pytest.skip("unsupported split/prefetch for this K")
+    torch.manual_seed(M * 7 + N + pro)
+    eps = 1e-6
+    x = torch.randn(M, 2 * K if pro == ops.PRO_SILU else K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    r = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    ln = torch.rand(K, device=DEV, dtype=torch.bfloat16) + 0.5
+    rout = torch.full_like(r, float("nan"))
+    y = ops.dgemm(x, w, pro, splitk, pf, residual=r, residual_out=rout, ln=ln, eps=eps)
+    torch.cuda.synchronize()
+    want, s = _dgemm_ref(pro, x, w, r, ln, eps)
+    scale = want.abs().max().item()
+    _close(y, want, atol=2e-2 * scale)
+    if pro == ops.PRO_ADDNORM:
+        _close(rout, s, atol=0.0)
+
+
+def test_fused_decode_gemm_in_graph():
+    """Graph-captured split-K fused GEMM replays to the same result as eager."""
+    torch.manual_seed(3)
+    M, N, K = 64, 2048, 1024
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    rout = torch.empty_like(r)
+    ln = torch.rand(K, device=DEV, dtype=torch.bfloat16) + 0.5
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    eager = ops.dgemm(x, w, ops.PRO_ADDNORM, 4, 2, residual=r, residual_out=rout, ln=ln).clone()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.dgemm(x, w, ops.PRO_ADDNORM, 4, 2, residual=r, residual_out=rout, ln=ln)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        y = ops.dgemm(x, w, ops.PRO_ADDNORM, 4, 2, residual=r, residual_out=rout, ln=ln)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y, eager)

@@ -187,3 +187,38 @@ def test_fp8_cache_roundtrip_reference():
     rel = ((K.float() - k).abs() / (k.abs() + 1e-2))[1:]
     assert float(rel.median()) < 0.07  # e4m3: 3 mantissa bits
     assert torch.equal(V.float(), v.float().to(torch.float8_e4m3fn).float())
+
+
+def test_fused_decode_gemm_reference_semantics():
+    """CPU path of ops.dgemm: prologue (plain / add+RMSNorm / SiLU*up) then GEMM."""
+    import torch
+    from aws_k8s_ansible_provisioner_amd import ops
+    from aws_k8s_ansible_provisioner_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    M, N, K = 5, 48, 64
+    w = torch.randn(N, K, dtype=torch.bfloat16)
+    x = torch.randn(M, K, dtype=torch.bfloat16)
+    r = torch.randn(M, K, dtype=torch.bfloat16)
+    ln = torch.rand(K, dtype=torch.bfloat16) + 0.5
+    rout = torch.empty_like(r)
+    y = ops.dgemm(x, w, ops.PRO_ADDNORM, residual=r, residual_out=rout, ln=ln, eps=1e-6)
+    s = (x.float() + r.float()).to(torch.bfloat16)
+    assert torch.equal(rout, s)
+    want = ref.rms_norm(s, ln, 1e-6).float() @ w.float().t()
+    assert torch.allclose(y.float(), want, atol=0.1, rtol=0.02)
+    g = torch.randn(M, 2 * K, dtype=torch.bfloat16)
+    y2 = ops.dgemm(g, w, ops.PRO_SILU)
+    want2 = ref.silu_and_mul(g).float() @ w.float().t()
+    assert torch.allclose(y2.float(), want2, atol=0.1, rtol=0.02)
+    assert torch.allclose(ops.dgemm(x, w).float(), x.float() @ w.float().t(), atol=0.1, rtol=0.02)
+
+
+def test_fused_decode_gemm_support_rules():
+    from aws_k8s_ansible_provisioner_amd import ops
+
+    assert ops.dgemm_supported(256, 4096, 1024, 1, 2)
+    assert ops.dgemm_supported(256, 1024, 2048, 4, 4)
+    assert not ops.dgemm_supported(256, 1024, 2048, 4, 3)    # prefetch depth 1|2|4
+    assert not ops.dgemm_supported(256, 1022, 1024, 1, 1)    # N % 4
+    assert not ops.dgemm_supported(256, 1024, 1024, 8, 4)    # K/split not a multiple of 64*pf
