@@ -64,43 +64,53 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
   const int wm = w >> 1, wn = w & 1;
   const int fr = lane & 15, fg = lane >> 4;  // MFMA fragment column / row group of this lane
 
-  // staging: thread -> (row tid/4, chunks 2*(tid%4) + {0,1}) of both 64x64 tiles.
+  // staging: thread -> chunk tid%8 of rows tid/8 and tid/8 + 32 of both 64x64 tiles, so
+  // each load instruction reads 8 whole 128-B lines (full-line staging:
+  // cdna_hip_programming.md "Projection GEMM at M = 256" x-operand row).
   // Rows past M / N are clamped to row 0 (valid memory, results never stored).
-  const int s_row = tid >> 2;
-  const int s_ch = (tid & 3) * 2;
-  const bool a_ok = (m0 + s_row) < p.M;
-  const int v = n0 + s_row;  // virtual output column staged by this thread
-  const bool b_ok = v < p.N;
-  int wrow = b_ok ? v : 0;
-  if constexpr (EPI == EPI_SILU)
-    wrow = b_ok ? ((v >> 4) & 1) * (p.N >> 1) + (v >> 5) * 16 + (v & 15) : 0;
-  const size_t arow = (size_t)(a_ok ? m0 + s_row : 0);
+  const int s_ch = tid & 7;
   const bf16* X = static_cast<const bf16*>(p.X);
   const bf16* W = static_cast<const bf16*>(p.W);
   const bf16* LN = static_cast<const bf16*>(p.ln);
   bf16* Y = static_cast<bf16*>(p.Y);
-  const bf16* xa = X + arow * p.ldx;
-  const bf16* wb = W + (size_t)wrow * p.ldw;
-  const bf16* rr = PRO == PRO_ADDNORM ? static_cast<const bf16*>(p.R) + arow * p.K : nullptr;
-  bf16* ro = PRO == PRO_ADDNORM ? static_cast<bf16*>(p.Rout) + arow * p.K : nullptr;
-  const bool write_res = PRO == PRO_ADDNORM && tn == 0 && a_ok;
+  int s_row[2];
+  bool a_ok[2];
+  const bf16* xa[2];
+  const bf16* wb[2];
+  const bf16* rr[2];
+  bf16* ro[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    s_row[c] = (tid >> 3) + 32 * c;
+    a_ok[c] = (m0 + s_row[c]) < p.M;
+    const int v = n0 + s_row[c];  // virtual output column staged by this thread
+    const bool b_ok = v < p.N;
+    int wrow = b_ok ? v : 0;
+    if constexpr (EPI == EPI_SILU)
+      wrow = b_ok ? ((v >> 4) & 1) * (p.N >> 1) + (v >> 5) * 16 + (v & 15) : 0;
+    const size_t arow = (size_t)(a_ok[c] ? m0 + s_row[c] : 0);
+    xa[c] = X + arow * p.ldx;
+    wb[c] = W + (size_t)wrow * p.ldw;
+    rr[c] = PRO == PRO_ADDNORM ? static_cast<const bf16*>(p.R) + arow * p.K : nullptr;
+    ro[c] = PRO == PRO_ADDNORM ? static_cast<bf16*>(p.Rout) + arow * p.K : nullptr;
+  }
 
-  bf16x8 sa[PF][2], sb[PF][2], sx[PF][2], sg[PF][2];
-  float ss = 0.f;
+  bf16x8 sa[PF][2], sb[PF][2], sx[PF][2], sg[PF];
+  float ss[2] = {0.f, 0.f};
 
   auto gload = [&](int q, int k0) {
+    const int kk = k0 + s_ch * 8;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const int kk = k0 + (s_ch + c) * 8;
-      sa[q][c] = *reinterpret_cast<const bf16x8*>(xa + kk);
+      sa[q][c] = *reinterpret_cast<const bf16x8*>(xa[c] + kk);
       if constexpr (PRO == PRO_ADDNORM) {
-        sx[q][c] = *reinterpret_cast<const bf16x8*>(rr + kk);
-        sg[q][c] = *reinterpret_cast<const bf16x8*>(LN + kk);
+        sx[q][c] = *reinterpret_cast<const bf16x8*>(rr[c] + kk);
       } else if constexpr (PRO == PRO_SILU) {
-        sx[q][c] = *reinterpret_cast<const bf16x8*>(xa + p.K + kk);
+        sx[q][c] = *reinterpret_cast<const bf16x8*>(xa[c] + p.K + kk);
       }
-      sb[q][c] = *reinterpret_cast<const bf16x8*>(wb + kk);
+      sb[q][c] = *reinterpret_cast<const bf16x8*>(wb[c] + kk);
     }
+    if constexpr (PRO == PRO_ADDNORM) sg[q] = *reinterpret_cast<const bf16x8*>(LN + kk);
   };
   auto sstore = [&](int q, int buf, int k0) {
 #pragma unroll
@@ -114,16 +124,16 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
         for (int j = 0; j < 8; ++j) {
           s[j] = f2bf(bf2f(sa[q][c][j]) + bf2f(sx[q][c][j]));
           const float f = bf2f(s[j]);
-          ss += f * f;
-          av[j] = f2bf(f * bf2f(sg[q][c][j]));
+          ss[c] += f * f;
+          av[j] = f2bf(f * bf2f(sg[q][j]));
         }
-        if (write_res) *reinterpret_cast<bf16x8*>(ro + k0 + (s_ch + c) * 8) = s;
+        if (tn == 0 && a_ok[c]) *reinterpret_cast<bf16x8*>(ro[c] + k0 + s_ch * 8) = s;
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) av[j] = f2bf(silu_bf(bf2f(sa[q][c][j])) * bf2f(sx[q][c][j]));
       }
-      lds[buf * 1024 + dswz(s_row, s_ch + c)] = av;
-      lds[buf * 1024 + 512 + dswz(s_row, s_ch + c)] = sb[q][c];
+      lds[buf * 1024 + dswz(s_row[c], s_ch)] = av;
+      lds[buf * 1024 + 512 + dswz(s_row[c], s_ch)] = sb[q][c];
     }
   };
 
@@ -209,12 +219,18 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
   }
 
   if constexpr (PRO == PRO_ADDNORM) {
-    // 4 consecutive lanes share a staging row: wave-local butterfly, then one LDS slot/row
-    ss += __shfl_xor(ss, 1, kWave);
-    ss += __shfl_xor(ss, 2, kWave);
-    if ((tid & 3) == 0) {
-      rowss[s_row] = ss;
-      if (SPLIT && tn == 0 && a_ok) p.ws[(size_t)gridDim.y * p.M * p.N + (size_t)kz * p.M + m0 + s_row] = ss;
+    // 8 consecutive lanes share a staging row: wave-local butterfly, then one LDS slot/row
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float v = ss[c];
+      v += __shfl_xor(v, 1, kWave);
+      v += __shfl_xor(v, 2, kWave);
+      v += __shfl_xor(v, 4, kWave);
+      if ((tid & 7) == 0) {
+        rowss[s_row[c]] = v;
+        if (SPLIT && tn == 0 && a_ok[c])
+          p.ws[(size_t)gridDim.y * p.M * p.N + (size_t)kz * p.M + m0 + s_row[c]] = v;
+      }
     }
     __syncthreads();
   }
