@@ -122,6 +122,18 @@ void launch_apply_penalties(void* logits, int ld, int is_bf16, const int32_t* ro
 void launch_argmax(const void* logits, int ld, int V, int is_bf16, int64_t* out, int B,
                    hipStream_t s);
 
+// ---- moe_dgemm.hip ----
+// Grouped expert GEMM for MoE decode: 32|64-row x 128-col tiles, k-pipelined, optional
+// activation-row gather and SwiGLU epilogue over gate/up-interleaved weight rows.
+bool moe_dgemm_supported(int N, int K, int pf, int silu, int splitk);
+void launch_moe_dgemm(const void* A, const void* W, void* Y, const int32_t* sorted_ids,
+                      const int32_t* tile_expert, int max_tiles, int n_flat, int topk, int N,
+                      int K, int lda, int ldy, int gather, int silu, int pf, int bm, int splitk,
+                      float* partials, hipStream_t s);
+// out[t] = sum_k w[t,k] * sum_z P[z, inv[t*K+k], :]  (split-K fp32 partials of the down GEMM)
+void launch_moe_combine_split(const float* P, const float* wts, const int32_t* inv, void* out,
+                              int T, int topk, int d, int S, int rows, hipStream_t s);
+
 // ---- moe.hip ----
 void launch_moe_topk_softmax(const void* logits, int ld, int E, int K, float* topk_w,
                              int32_t* topk_ids, int T, int renormalize, hipStream_t s);

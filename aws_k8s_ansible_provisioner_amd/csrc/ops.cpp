@@ -451,6 +451,56 @@ void moe_gemm(Tensor out, Tensor a, Tensor w, Tensor sorted_ids, Tensor tile_exp
                         a.stride(0), gather ? 1 : 0, cur_stream());
 }
 
+// out: bf16 [rows, N] (or [rows, N/2] with silu); splitk > 1: out is an fp32 partials buffer
+// [splitk, rows, N] consumed by moe_combine_split.
+void moe_dgemm(Tensor out, Tensor a, Tensor w, Tensor sorted_ids, Tensor tile_expert,
+               int64_t n_flat, int64_t topk, bool gather, bool silu, int64_t pf, int64_t bm,
+               int64_t splitk) {
+  CHECK_GPU(a); CHECK_BF16(a); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
+  CHECK_LAST_CONTIG(a);
+  TORCH_CHECK(w.dim() == 3, "expert weights [E, N, K]");
+  const int N = w.size(1), K = w.size(2);
+  TORCH_CHECK(a.size(1) == K, "moe_dgemm: a width != K");
+  TORCH_CHECK(akap::moe_dgemm_supported(N, K, pf, silu, splitk), "moe_dgemm: unsupported N/K/pf/split");
+  TORCH_CHECK(a.stride(0) % 8 == 0, "moe_dgemm: 16-byte aligned rows");
+  TORCH_CHECK(sorted_ids.scalar_type() == at::kInt && tile_expert.scalar_type() == at::kInt,
+              "moe_dgemm: int32 index tensors");
+  TORCH_CHECK(bm == 32 || bm == 64, "moe_dgemm: tile rows 32 | 64");
+  const int max_tiles = tile_expert.numel();
+  const int64_t rows = (int64_t)max_tiles * bm;
+  if (splitk > 1) {
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= splitk * rows * N,
+                "moe_dgemm: fp32 partials [splitk, rows, N]");
+  } else {
+    CHECK_BF16(out);
+    TORCH_CHECK(out.size(1) == (silu ? N / 2 : N), "moe_dgemm: out width");
+    TORCH_CHECK(out.size(0) >= rows, "moe_dgemm: out rows must cover all tiles");
+  }
+  TORCH_CHECK(sorted_ids.numel() >= rows, "moe_dgemm: sorted_ids too short");
+  if (!gather) TORCH_CHECK(a.size(0) >= rows, "moe_dgemm: a rows must cover all tiles");
+  const c10::DeviceGuard g(a.device());
+  akap::launch_moe_dgemm(a.data_ptr(), w.data_ptr(), splitk > 1 ? nullptr : out.data_ptr(),
+                         sorted_ids.data_ptr<int32_t>(), tile_expert.data_ptr<int32_t>(),
+                         max_tiles, n_flat, topk, N, K, a.stride(0),
+                         splitk > 1 ? N : out.stride(0), gather ? 1 : 0, silu ? 1 : 0, (int)pf,
+                         (int)bm, (int)splitk, splitk > 1 ? out.data_ptr<float>() : nullptr,
+                         cur_stream());
+}
+
+void moe_combine_split(Tensor partials, Tensor wts, Tensor inv, Tensor out, int64_t splitk,
+                       int64_t rows) {
+  CHECK_GPU(partials); CHECK_CONTIG(partials); CHECK_CONTIG(out); CHECK_BF16(out);
+  TORCH_CHECK(partials.scalar_type() == at::kFloat, "partials fp32");
+  TORCH_CHECK(wts.scalar_type() == at::kFloat && inv.scalar_type() == at::kInt, "dtypes");
+  const int T = out.size(0), d = out.size(1), topk = wts.size(1);
+  TORCH_CHECK(d % 8 == 0, "d % 8");
+  TORCH_CHECK(partials.numel() >= splitk * rows * d, "partials [splitk, rows, d]");
+  const c10::DeviceGuard g(out.device());
+  akap::launch_moe_combine_split(partials.data_ptr<float>(), wts.data_ptr<float>(),
+                                 inv.data_ptr<int32_t>(), out.data_ptr(), T, topk, d,
+                                 (int)splitk, (int)rows, cur_stream());
+}
+
 void moe_combine(Tensor y, Tensor wts, Tensor inv, Tensor out) {
   CHECK_GPU(y); CHECK_BF16(y); CHECK_CONTIG(y); CHECK_CONTIG(out);
   TORCH_CHECK(wts.scalar_type() == at::kFloat && inv.scalar_type() == at::kInt, "dtypes");
@@ -714,6 +764,12 @@ TORCH_LIBRARY(akap, m) {
       "moe_gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor sorted_ids, Tensor tile_expert, "
       "int n_flat, int topk, bool gather) -> ()");
   m.def("moe_combine(Tensor y, Tensor wts, Tensor inv, Tensor(a!) out) -> ()");
+  m.def(
+      "moe_dgemm(Tensor(a!) out, Tensor a, Tensor w, Tensor sorted_ids, Tensor tile_expert, "
+      "int n_flat, int topk, bool gather, bool silu, int pf, int bm=32, int splitk=1) -> ()");
+  m.def(
+      "moe_combine_split(Tensor partials, Tensor wts, Tensor inv, Tensor(a!) out, int splitk, "
+      "int rows) -> ()");
   m.def("kv_gather(Tensor cache, Tensor block_ids, Tensor(a!) out) -> ()");
   m.def("kv_scatter(Tensor buf, Tensor(a!) cache, Tensor block_ids) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start, int vocab_end) -> ()");
@@ -748,6 +804,8 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
+  m.impl("moe_dgemm", &moe_dgemm);
+  m.impl("moe_combine_split", &moe_combine_split);
   m.impl("car_all_reduce", &car_all_reduce);
   m.impl("l2_prefetch", &l2_prefetch);
   m.impl("car_all_reduce_multi", &car_all_reduce_multi);

@@ -447,32 +447,68 @@ def l2_prefetch(tensors) -> None:
 def fused_moe(h, w13, w2, topk_w, topk_ids, out=None):
     """Graph-safe fused expert FFN: out[t] = sum_k w[t,k] * W2_e . silu_mul(W13_e . h[t]).
 
-    GPU: moe_align (device-side sort + tile->expert map) -> grouped MFMA GEMM gathering
-    token rows -> silu_and_mul -> grouped GEMM -> deterministic gather-combine.  All
-    buffer shapes depend only on (T, top_k, E), so the whole block captures in a hipGraph.
+    GPU: moe_align (device-side sort + tile->expert map, 32-row tiles) -> grouped k-pipelined
+    MFMA GEMM gathering token rows with the SwiGLU in its epilogue (csrc/kernels/
+    moe_dgemm.hip) -> grouped GEMM -> deterministic gather-combine.  All buffer shapes depend
+    only on (T, top_k, E), so the whole block captures in a hipGraph.
     w13 [E, 2F, d], w2 [E, d, F]."""
     T, d = h.shape
     K = topk_ids.shape[1]
     E = w13.shape[0]
+    F = w2.shape[2]
     if out is None:
         out = torch.empty(T, d, dtype=h.dtype, device=h.device)
     if not _native(h):
         out.copy_(ref.fused_moe(h, w13, w2, topk_w, topk_ids))
         return out
     n = T * K
-    cap = moe_capacity(n, E, MOE_BLOCK)
-    tiles = cap // MOE_BLOCK
+    bm = moe_tile_rows(n, E)
+    cap = moe_capacity(n, E, bm)
+    tiles = cap // bm
     dev = h.device
     inv = torch.empty(n, dtype=torch.int32, device=dev)
     tile_expert = torch.empty(tiles, dtype=torch.int32, device=dev)
-    sorted_ids, _, _ = moe_align(topk_ids, E, MOE_BLOCK, inv=inv, tile_expert=tile_expert)
-    y1 = torch.empty(cap, w13.shape[1], dtype=h.dtype, device=dev)
-    torch.ops.akap.moe_gemm(y1, h, w13, sorted_ids, tile_expert, n, K, True)
-    a = silu_and_mul(y1)
+    sorted_ids, _, _ = moe_align(topk_ids, E, bm, inv=inv, tile_expert=tile_expert)
+    act = torch.empty(cap, F, dtype=h.dtype, device=dev)
+    torch.ops.akap.moe_dgemm(act, h, w13, sorted_ids, tile_expert, n, K, True, True,
+                             _moe_pf(d), bm)
+    S = moe_down_splitk(n, E, bm, F)
+    if S > 1:
+        # fp32 K-slices of the down projection, summed by the combine (no extra launch)
+        P = torch.empty(S * cap * d, dtype=torch.float32, device=dev)
+        torch.ops.akap.moe_dgemm(P, act, w2, sorted_ids, tile_expert, n, K, False, False,
+                                 _moe_pf(F // S), bm, S)
+        torch.ops.akap.moe_combine_split(P, topk_w.contiguous(), inv, out, S, cap)
+        return out
     y2 = torch.empty(cap, d, dtype=h.dtype, device=dev)
-    torch.ops.akap.moe_gemm(y2, a, w2, sorted_ids, tile_expert, n, K, False)
+    torch.ops.akap.moe_dgemm(y2, act, w2, sorted_ids, tile_expert, n, K, False, False,
+                             _moe_pf(F), bm)
     torch.ops.akap.moe_combine(y2, topk_w.contiguous(), inv, out)
     return out
+
+
+def moe_down_splitk(n: int, num_experts: int, bm: int, F: int) -> int:
+    """K-split of the expert down projection (K = F): with few row tiles the grid has one
+    block per CU or less and each block walks all of F (measured, bench/moe_gemm_micro.py:
+    Mixtral T=128 258 -> 221 us at 4 slices, T=32 271 -> 204 us at 2; none at T=256)."""
+    S = 4 if (bm == 64 and n <= 40 * num_experts) else (2 if bm == 32 else 1)
+    while S > 1 and (F % S or (F // S) % 64):
+        S //= 2
+    return S
+
+
+def moe_tile_rows(n: int, num_experts: int) -> int:
+    """Rows per grouped-GEMM tile: 64 once experts average more than ~20 rows (a second
+    32-row tile of an expert re-streams all its weights), else 32 (less padding)."""
+    return 64 if n > 20 * num_experts else 32
+
+
+def _moe_pf(K: int) -> int:
+    """Deepest load ring (k-tiles in flight) the reduction depth allows."""
+    for pf in (4, 2, 1):
+        if K % (64 * pf) == 0:
+            return pf
+    raise ValueError(f"MoE GEMM needs K % 64 == 0, got {K}")
 
 
 def kv_gather(cache_planes, block_ids, out=None):

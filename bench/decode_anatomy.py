@@ -99,7 +99,7 @@ def main():
                                           "paged_attention_prefill",
                                           "qk_norm_rope_cache",
                                           "rms_norm", "fused_add_rms_norm", "silu_and_mul",
-                                          "linear", "sample")}
+                                          "linear", "sample", "fused_moe")}
     noop = {
         "attention (fused: +qk-norm/rope/kv-write)": {
             "paged_attention_decode": lambda out, *a_, **k: out,
@@ -112,6 +112,7 @@ def main():
         "gemms (incl. LM head)": {"linear": lambda x, w, out=None: x.new_empty(x.shape[0],
                                                                                w.shape[0])},
         "sampler": {"sample": lambda logits, *a_, **k: (None, None)},
+        "fused MoE experts": {"fused_moe": lambda h, *a_, **k: h},
     }
 
     def run(name, patch):

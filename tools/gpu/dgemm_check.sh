@@ -1,2 +1,3 @@
-OVERLAP_GROUP=7 timeout -k 10 200 python -X faulthandler -u bench/overlap_micro.py > gpurun_out/overlap_g7.log 2>&1 && \
-OVERLAP_GROUP=4 timeout -k 10 200 python -X faulthandler -u bench/overlap_micro.py > gpurun_out/overlap_g4.log 2>&1
+set -o pipefail
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_engine_gpu.py -k "moe or mixtral" > gpurun_out/moe_tests.log 2>&1 && \
+timeout -k 10 600 python -u bench.py --model mixtral-8x7b --num-requests 128 --steps 1 > gpurun_out/bench_mixtral.log 2>&1
