@@ -383,28 +383,36 @@ static void dgemm_main(const DGemmArgs& p, dim3 grid, int pro, int epi, int pf, 
   }
 }
 
+void launch_dgemm_reduce(const DGemmArgs& p, int pro, int splitk, hipStream_t st) {
+  long blocks = ((long)p.M * p.N / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  const int scale = pro == PRO_ADDNORM ? 1 : (pro == PRO_PLAIN && p.ss_in ? 2 : 0);
+  if (p.epi == EPI_RESNORM) {
+    if (scale == 2) dgemm_reduce_kernel<2, EPI_RESNORM><<<(int)blocks, 256, 0, st>>>(p, splitk);
+    else dgemm_reduce_kernel<0, EPI_RESNORM><<<(int)blocks, 256, 0, st>>>(p, splitk);
+  } else if (scale == 1) {
+    dgemm_reduce_kernel<1, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
+  } else if (scale == 2) {
+    dgemm_reduce_kernel<2, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
+  } else {
+    dgemm_reduce_kernel<0, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
+  }
+}
+
 void launch_dgemm(const DGemmArgs& a, int pro, int splitk, int pf, hipStream_t st) {
   if (a.M == 0 || a.N == 0) return;
   DGemmArgs p = a;
   p.kps = a.K / splitk;
   if (pro != PRO_PLAIN) p.epi = EPI_STORE;  // prologue forms have the plain store epilogue
+  if (pro == PRO_PLAIN && p.bn > 0) {        // LDS-DMA (global_load_lds) ring variant
+    launch_gdgemm(p, splitk, st);
+    return;
+  }
   const int tiles = ((a.M + DBM - 1) / DBM) * ((a.N + DBN - 1) / DBN);
   dim3 grid(tiles, splitk);
   if (splitk > 1) {
     dgemm_main<true>(p, grid, pro, p.epi, pf, st);
-    long blocks = ((long)a.M * a.N / 4 + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    const int scale = pro == PRO_ADDNORM ? 1 : (pro == PRO_PLAIN && p.ss_in ? 2 : 0);
-    if (p.epi == EPI_RESNORM) {
-      if (scale == 2) dgemm_reduce_kernel<2, EPI_RESNORM><<<(int)blocks, 256, 0, st>>>(p, splitk);
-      else dgemm_reduce_kernel<0, EPI_RESNORM><<<(int)blocks, 256, 0, st>>>(p, splitk);
-    } else if (scale == 1) {
-      dgemm_reduce_kernel<1, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
-    } else if (scale == 2) {
-      dgemm_reduce_kernel<2, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
-    } else {
-      dgemm_reduce_kernel<0, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
-    }
+    launch_dgemm_reduce(p, pro, splitk, st);
   } else {
     dgemm_main<false>(p, grid, pro, p.epi, pf, st);
   }

@@ -92,10 +92,15 @@ struct DGemmArgs {
   const void* ln_out;  // EPI_RESNORM: next RMSNorm weight [N]
   int M, N, K, ldx, ldw, ldy, kps, epi;
   float eps;
+  int bn;  // 0: register-ring kernel (dgemm.hip); 64 | 128: LDS-DMA ring kernel (gdgemm.hip)
 };
 bool dgemm_supported(int M, int N, int K, int splitk, int pf);
 bool dgemm_epi_supported(int N, int epi, int splitk);
 void launch_dgemm(const DGemmArgs& a, int pro, int splitk, int pf, hipStream_t st);
+void launch_dgemm_reduce(const DGemmArgs& p, int pro, int splitk, hipStream_t st);
+// gdgemm.hip: the same plain-prologue GEMM + epilogues with operands staged by global_load_lds
+bool gdgemm_supported(int M, int N, int K, int splitk, int bn);
+void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st);
 
 // ---- sampling.hip ----
 struct SampleParams {

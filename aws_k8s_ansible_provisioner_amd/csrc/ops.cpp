@@ -282,7 +282,7 @@ void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk,
 void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t splitk, int64_t pf,
            std::optional<Tensor> r, std::optional<Tensor> rout, std::optional<Tensor> ln,
            double eps, int64_t epi, std::optional<Tensor> ss_in, std::optional<Tensor> ss_out,
-           std::optional<Tensor> aout, std::optional<Tensor> ln_out) {
+           std::optional<Tensor> aout, std::optional<Tensor> ln_out, int64_t bn) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "dgemm: 2-D tensors");
@@ -293,7 +293,10 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   TORCH_CHECK(x.size(1) == (pro == akap::PRO_SILU ? 2 * K : K), "dgemm: x width");
   TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == akap::EPI_SILU ? N / 2 : N),
               "dgemm: out shape");
-  TORCH_CHECK(akap::dgemm_supported(M, N, K, splitk, pf), "dgemm: unsupported M/N/K/splitk/pf");
+  TORCH_CHECK(bn == 0 || pro == akap::PRO_PLAIN, "dgemm: the LDS-DMA variant has the plain prologue");
+  TORCH_CHECK(bn > 0 ? akap::gdgemm_supported(M, N, K, splitk, bn)
+                     : akap::dgemm_supported(M, N, K, splitk, pf),
+              "dgemm: unsupported M/N/K/splitk/pf/bn");
   TORCH_CHECK(akap::dgemm_epi_supported(N, epi, splitk), "dgemm: unsupported epilogue/N/splitk");
   TORCH_CHECK((int64_t)N * K * 2 >= (int64_t)M * 4, "dgemm: W smaller than M floats");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
@@ -313,6 +316,7 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   a.ldx = x.stride(0); a.ldw = w.stride(0); a.ldy = out.stride(0);
   a.eps = (float)eps;
   a.epi = (int)epi;
+  a.bn = (int)bn;
   if (pro == akap::PRO_ADDNORM) {
     TORCH_CHECK(r && rout && ln, "dgemm addnorm: residual, residual-out and norm weight");
     CHECK_BF16(*r); CHECK_BF16(*rout); CHECK_BF16(*ln);
@@ -745,7 +749,7 @@ TORCH_LIBRARY(akap, m) {
       "dgemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int pro, int splitk, int pf, "
       "Tensor? r=None, Tensor(c!)? rout=None, Tensor? ln=None, float eps=1e-6, int epi=0, "
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
-      "Tensor? ln_out=None) -> ()");
+      "Tensor? ln_out=None, int bn=0) -> ()");
   m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
   m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");

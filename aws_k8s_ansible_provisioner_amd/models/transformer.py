@@ -318,7 +318,7 @@ class DecoderLM:
         per-row sum of squares), the norm's row scale in the consumer GEMM's epilogue, and
         SwiGLU in the gate|up projection's epilogue -- no separate norm / activation kernels.
         Single rank (no all-reduce between GEMM and residual add); plan from
-        gemm_tuner.tune_fused: projection -> (split-K, prefetch depth)."""
+        gemm_tuner.tune_fused: projection -> (split-K, prefetch depth, LDS-DMA tile width)."""
         T = input_ids.shape[0]
         eps = self.cfg.rms_eps
         L = len(self.layers)
@@ -327,8 +327,8 @@ class DecoderLM:
         a1 = ops.rms_norm(residual, self.layers[0].ln1, eps)
         ss_in = None
         for li, lw in enumerate(self.layers):
-            s_, p_ = plan["w_qkv"]
-            qkv = ops.dgemm(a1, lw.w_qkv, splitk=s_, pf=p_, eps=eps, ss_in=ss_in)
+            s_, p_, b_ = plan["w_qkv"]
+            qkv = ops.dgemm(a1, lw.w_qkv, splitk=s_, pf=p_, eps=eps, ss_in=ss_in, bn=b_)
             attn = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
             ops.paged_attention_decode_fused(
                 attn, qkv, k_caches[li], v_caches[li], batch.block_tables, batch.seq_lens,
@@ -336,22 +336,22 @@ class DecoderLM:
                 self.hq // self.hkv, self.scale, eps, workspace=batch.workspace,
                 num_parts=batch.num_parts, part_size=batch.part_size)
             a2 = torch.empty_like(residual)
-            s_, p_ = plan["w_o"]
+            s_, p_, b_ = plan["w_o"]
             ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, splitk=s_, pf=p_, eps=eps,
                       out=residual, epi=ops.EPI_RESNORM, ss_out=ss[2 * li], a_out=a2,
-                      ln_out=lw.ln2)
-            s_, p_ = plan["w_gate_up"]
+                      ln_out=lw.ln2, bn=b_)
+            s_, p_, b_ = plan["w_gate_up"]
             act = ops.dgemm(a2, lw.w_gate_up, splitk=s_, pf=p_, eps=eps, ss_in=ss[2 * li],
-                            epi=ops.EPI_SILU)
-            s_, p_ = plan["w_down"]
+                            epi=ops.EPI_SILU, bn=b_)
+            s_, p_, b_ = plan["w_down"]
             if li + 1 < L:
                 a1 = torch.empty_like(residual)
                 ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps, out=residual,
                           epi=ops.EPI_RESNORM, ss_out=ss[2 * li + 1], a_out=a1,
-                          ln_out=self.layers[li + 1].ln1)
+                          ln_out=self.layers[li + 1].ln1, bn=b_)
                 ss_in = ss[2 * li + 1]
             else:
-                x = ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps)
+                x = ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps, bn=b_)
         h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
         return h
 

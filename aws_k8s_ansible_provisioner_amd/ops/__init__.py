@@ -194,7 +194,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
         choice = gemm_tuner.lookup(M, w.shape[0], w.shape[1])
         if choice is not None:  # measured at engine start (cold weights, real layers)
             if choice[0] == "dgemm" and x.stride(-1) == 1:
-                return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out)
+                return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out,
+                             bn=choice[3] if len(choice) > 3 else 0)
             split = choice[1] if choice[0] == "hip" else 0
     if split is None:
         use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
@@ -239,8 +240,8 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
           ln: Optional[torch.Tensor] = None, eps: float = 1e-6,
           out: Optional[torch.Tensor] = None, epi: int = EPI_STORE,
           ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
-          a_out: Optional[torch.Tensor] = None, ln_out: Optional[torch.Tensor] = None
-          ) -> torch.Tensor:
+          a_out: Optional[torch.Tensor] = None, ln_out: Optional[torch.Tensor] = None,
+          bn: int = 0) -> torch.Tensor:
     """Fused decode GEMM (csrc/kernels/dgemm.hip): y = A @ w.T where A is produced from x by
     the prologue inside the GEMM's operand staging --
       PRO_PLAIN    A = x; with ss_in, rows of y are scaled by rsqrt(ss_in / K + eps)
@@ -251,7 +252,9 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
       EPI_RESNORM  out is the residual stream [M, N] (in/out): out = bf16(bf16(y) + out);
                    a_out = bf16(out * ln_out); ss_out += per-row sum of out^2 (caller zeroes)
       EPI_SILU     w = [gate; up] rows, out [M, N/2] = silu(y_gate) * y_up
-    replacing the separate fused_add_rms_norm / silu_and_mul launches of a decode layer."""
+    replacing the separate fused_add_rms_norm / silu_and_mul launches of a decode layer.
+    bn = 64 | 128 selects the LDS-DMA staged variant (csrc/kernels/gdgemm.hip, 64 x bn tiles,
+    plain prologue only); 0 the register-ring kernel (prefetch depth pf)."""
     M = x.shape[0]
     N, K = w.shape
     if out is None:
@@ -286,16 +289,21 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
         if ws is None:
             ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
     torch.ops.akap.dgemm(out, x, w, ws, pro, splitk, pf, residual, residual_out, ln, eps, epi,
-                         ss_in, ss_out, a_out, ln_out)
+                         ss_in, ss_out, a_out, ln_out, bn)
     return out
 
 
-def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI_STORE) -> bool:
-    """Mirror of dgemm_supported / dgemm_epi_supported in dgemm.hip (host-side, no GPU)."""
+def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI_STORE,
+                    bn: int = 0) -> bool:
+    """Mirror of dgemm_supported / gdgemm_supported / dgemm_epi_supported (host-side)."""
     if epi == EPI_SILU and (splitk != 1 or N % 32):
         return False
     if epi == EPI_RESNORM and splitk > 1 and N % 256:
         return False
+    if bn:
+        if bn not in (64, 128) or M <= 0 or N % 4 or splitk < 1 or K % splitk:
+            return False
+        return (K // splitk) % 64 == 0 and (K // splitk) // 64 >= 3
     if M <= 0 or N <= 0 or K <= 0 or splitk < 1 or N % 4 or pf not in (1, 2, 4, 8) or K % splitk:
         return False
     return (K // splitk) % (64 * pf) == 0

@@ -23,7 +23,7 @@ from typing import Optional, Sequence
 
 import torch
 
-Choice = tuple  # ("torch",) | ("hip", splitk) | ("dgemm", splitk, prefetch_depth)
+Choice = tuple  # ("torch",) | ("hip", splitk) | ("dgemm", splitk, prefetch_depth[, lds_dma_bn])
 _PLAN: dict = {}
 
 
@@ -60,7 +60,7 @@ def _timed(fn, n: int) -> float:
 
 
 def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
-         margin: float = 0.03, pfs=(2, 4, 8)) -> Choice:
+         margin: float = 0.03, pfs=(2, 4, 8), bns=(64, 128)) -> Choice:
     """Pick the fastest way to compute x[M, K] @ w.T for these same-shape weights.
     hipBLASLt is kept unless the MFMA kernel is more than `margin` faster."""
     from . import gemm_counters  # noqa: F401  (ensures the native library is loaded)
@@ -90,6 +90,15 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
             t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, pf), n)
             if t < t_best:
                 best, t_best = ("dgemm", s, pf), t
+        for bn in bns:  # LDS-DMA staged variant (gdgemm.hip)
+            if not dgemm_supported(M, N, K, s, 1, bn=bn) or (s > 1 and K // s < 256):
+                continue
+            ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
+            t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, 1, None,
+                                                      None, None, 1e-6, 0, None, None, None,
+                                                      None, bn), n)
+            if t < t_best:
+                best, t_best = ("dgemm", s, 1, bn), t
     if best[0] != "torch" and t_best > t_torch * (1.0 - margin):
         best = ("torch",)
     _PLAN[(M, N, K)] = best
@@ -111,7 +120,8 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
     wins = {k: v for k, v in summary.items() if v[0] != "torch"}
     log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, HIP kernel chosen for "
         f"{len(wins)}: " + ", ".join(
-            f"M={m} {n} {c[0]} s{c[1]}" + (f"p{c[2]}" if len(c) > 2 else "")
+            f"M={m} {n} {c[0]} s{c[1]}" + (f"p{c[2]}" if len(c) == 3 else "") +
+            (f"g{c[3]}" if len(c) > 3 else "")
             for (m, n), c in sorted(wins.items())))
     return summary
 
@@ -149,7 +159,7 @@ def _time_unfused(M: int, model) -> float:
 
 
 def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(1, 2, 4, 8),
-               verbose: bool = False) -> dict:
+               verbose: bool = False, bns=(64, 128)) -> dict:
     """Pick (split-K, prefetch) for each fused-chain GEMM at each M and keep the fused chain
     for the M where it beats the unfused chain (both timed on the real cold layer weights)."""
     from . import EPI_SILU, dgemm_supported
@@ -178,20 +188,21 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(1,
             ln = model.layers[0].ln2 if N == model.layers[0].ln2.numel() else None
             best = None
             for s in splits:
-                for pf in pfs:
-                    if not dgemm_supported(M, N, K, s, pf, epi) or (s > 1 and K // s < 256):
+                for pf, bn in [(p_, 0) for p_ in pfs] + [(1, b_) for b_ in bns]:
+                    if (not dgemm_supported(M, N, K, s, pf, epi, bn=bn)
+                            or (s > 1 and K // s < 256)):
                         continue
                     wsp = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
-                    t = _timed(lambda i, s=s, pf=pf, wsp=wsp: torch.ops.akap.dgemm(
+                    t = _timed(lambda i, s=s, pf=pf, bn=bn, wsp=wsp: torch.ops.akap.dgemm(
                         out, x, ws_[i % L], wsp, 0, s, pf, None, None, None, 1e-6, epi,
                         None if epi == 1 else ss, ss_o if epi == 1 else None,
-                        a_o if epi == 1 else None, ln if epi == 1 else None), L)
+                        a_o if epi == 1 else None, ln if epi == 1 else None, bn), L)
                     if best is None or t < best[0]:
-                        best = (t, s, pf)
+                        best = (t, s, pf, bn)
             if best is None:
                 plan_m = None
                 break
-            plan_m[name] = (best[1], best[2])
+            plan_m[name] = (best[1], best[2], best[3])
             t_fused += best[0]
             detail.append(f"{name} {best[0]:.1f}/{t_plain:.1f}")
         if plan_m is not None and t_fused < t_unfused:
@@ -216,7 +227,10 @@ def _time_best_plain(M: int, name: str, weights) -> float:
     if c[0] == "dgemm":
         ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)
-        return _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, c[1], c[2]), n)
+        bn = c[3] if len(c) > 3 else 0
+        return _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, c[1], c[2],
+                                                     None, None, None, 1e-6, 0, None, None,
+                                                     None, None, bn), n)
     if c[0] == "hip":
         ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)

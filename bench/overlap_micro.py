@@ -62,7 +62,7 @@ class Half:
 
     def pre(self, li):
         m, lw = self.m, self.m.layers[li]
-        s_, p_ = self.plan["w_qkv"]
+        s_, p_ = self.plan["w_qkv"][:2]
         self.qkv = ops.dgemm(self.a1, lw.w_qkv, splitk=s_, pf=p_, eps=m.cfg.rms_eps,
                              ss_in=self.ss_in)
 
@@ -77,14 +77,14 @@ class Half:
     def post(self, li):
         m, lw, eps, T = self.m, self.m.layers[li], self.m.cfg.rms_eps, self.T
         a2 = torch.empty_like(self.residual)
-        s_, p_ = self.plan["w_o"]
+        s_, p_ = self.plan["w_o"][:2]
         ops.dgemm(self.at.view(T, m.hq * m.D), lw.w_o, splitk=s_, pf=p_, eps=eps,
                   out=self.residual, epi=ops.EPI_RESNORM, ss_out=self.ss[2 * li], a_out=a2,
                   ln_out=lw.ln2)
-        s_, p_ = self.plan["w_gate_up"]
+        s_, p_ = self.plan["w_gate_up"][:2]
         act = ops.dgemm(a2, lw.w_gate_up, splitk=s_, pf=p_, eps=eps, ss_in=self.ss[2 * li],
                         epi=ops.EPI_SILU)
-        s_, p_ = self.plan["w_down"]
+        s_, p_ = self.plan["w_down"][:2]
         if li + 1 < len(m.layers):
             self.a1 = torch.empty_like(self.residual)
             ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps, out=self.residual,

@@ -46,7 +46,7 @@ def _compare(name, device, plan):
     assert agree >= 0.75, f"greedy agreement {agree}"
 
 
-PLAIN_PLAN = {"w_qkv": (1, 1), "w_o": (1, 1), "w_gate_up": (1, 1), "w_down": (1, 1)}
+PLAIN_PLAN = {"w_qkv": (1, 1, 0), "w_o": (1, 1, 0), "w_gate_up": (1, 1, 0), "w_down": (1, 1, 0)}
 
 
 @pytest.mark.parametrize("name", ["tiny-qwen3", "tiny-llama"])
@@ -58,8 +58,9 @@ def test_fused_decode_chain_cpu(name):
 @pytest.mark.parametrize("name", ["tiny-qwen3", "tiny-llama"])
 @pytest.mark.parametrize("plan", [
     PLAIN_PLAN,
-    {"w_qkv": (1, 4), "w_o": (2, 2), "w_gate_up": (1, 2), "w_down": (2, 2)},
-    {"w_qkv": (2, 2), "w_o": (1, 4), "w_gate_up": (1, 4), "w_down": (1, 4)},
+    {"w_qkv": (1, 4, 0), "w_o": (2, 2, 0), "w_gate_up": (1, 2, 0), "w_down": (2, 2, 0)},
+    {"w_qkv": (2, 2, 0), "w_o": (1, 4, 0), "w_gate_up": (1, 4, 0), "w_down": (1, 4, 0)},
+    {"w_qkv": (1, 1, 128), "w_o": (1, 1, 64), "w_gate_up": (1, 1, 128), "w_down": (2, 1, 64)},
 ])
 def test_fused_decode_chain_gpu(name, plan):
     ops.load_native(required=True)

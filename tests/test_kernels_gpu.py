@@ -595,3 +595,39 @@ def test_fused_decode_gemm_in_graph():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(y, eager)
+
+
+@pytest.mark.parametrize("bn", [64, 128])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K,splitk", [(1, 256, 1024, 1), (37, 1024, 2048, 2),
+                                          (256, 4096, 1024, 1), (130, 1024, 768, 1),
+                                          (64, 1024, 2048, 4)])
+def test_lds_dma_decode_gemm(bn, epi, M, N, K, splitk):
+    """gdgemm.hip (global_load_lds ring) with each epilogue vs fp32 references."""
+    if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=bn):
+        pytest.skip("unsupported combination")
+    torch.manual_seed(M + N + K + epi + bn)
+    eps = 1e-6
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    ssi = torch.rand(M, device=DEV) * K + 1.0
+    y = (x.float() @ w.float().t()) * torch.rsqrt(ssi / K + eps)[:, None]
+    if epi == ops.EPI_STORE:
+        out = ops.dgemm(x, w, splitk=splitk, bn=bn, ss_in=ssi, eps=eps)
+        _close(out, y, atol=2e-2 * y.abs().max().item())
+    elif epi == ops.EPI_RESNORM:
+        res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        res0 = res.clone()
+        ln = torch.rand(N, device=DEV, dtype=torch.bfloat16) + 0.5
+        ss = torch.zeros(M, device=DEV)
+        a = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.dgemm(x, w, splitk=splitk, bn=bn, out=res, epi=epi, ss_out=ss, a_out=a, ln_out=ln,
+                  ss_in=ssi, eps=eps)
+        want = y.to(torch.bfloat16).float() + res0.float()
+        _close(res, want, atol=2e-2 * want.abs().max().item())
+        _close(a, res.float() * ln.float(), atol=1e-2 * a.float().abs().max().item())
+        assert torch.allclose(ss, res.float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
+    else:
+        out = ops.dgemm(x, w, splitk=splitk, bn=bn, epi=epi, ss_in=ssi, eps=eps)
+        want = ref.silu_and_mul(y.to(torch.bfloat16)).float()
+        _close(out, want, atol=2e-2 * want.abs().max().item())
