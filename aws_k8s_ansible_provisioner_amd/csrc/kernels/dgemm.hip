@@ -295,8 +295,11 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
 // Sum the S fp32 partial slabs [S, M, N] -> bf16, then the same epilogue as the main kernel.
 // SCALE: 0 none, 1 ADDNORM (slabs followed by [S, M] partial sums of squares), 2 ss_in[m].
 // EPI_RESNORM needs N % 256 == 0 so one wave's 256 consecutive elements share a row.
-template <int SCALE, int EPI>
-__global__ __launch_bounds__(256) void dgemm_reduce_kernel(DGemmArgs p, int S) {
+// S is a template parameter so the S slab loads of an element issue back to back: with a
+// runtime trip count hipcc waited on each load before the next (S dependent L2/HBM round
+// trips, ~4.5 us at S = 4 in profiles/r1_qwen3_bench_v6_kernel_stats.md).
+template <int SCALE, int EPI, int S>
+__global__ __launch_bounds__(256) void dgemm_reduce_kernel(DGemmArgs p) {
   const int M = p.M, N = p.N;
   const long total = (long)M * N / 4;
   const float* ws = p.ws;
@@ -304,17 +307,25 @@ __global__ __launch_bounds__(256) void dgemm_reduce_kernel(DGemmArgs p, int S) {
   bf16* Y = static_cast<bf16*>(p.Y);
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long e = i * 4;
-    f32x4 s = *reinterpret_cast<const f32x4*>(ws + e);
-    for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(ws + (size_t)z * M * N + e);
+    f32x4 part[S];
+#pragma unroll
+    for (int z = 0; z < S; ++z) part[z] = *reinterpret_cast<const f32x4*>(ws + (size_t)z * M * N + e);
     const int row = (int)(e / N), col = (int)(e % N);
     float scale = 1.f;
     if constexpr (SCALE == 1) {
-      float q = 0.f;
-      for (int z = 0; z < S; ++z) q += ssw[(size_t)z * M + row];
-      scale = rsqrtf(q / (float)p.K + p.eps);
+      float q[S];
+#pragma unroll
+      for (int z = 0; z < S; ++z) q[z] = ssw[(size_t)z * M + row];
+      float qs = 0.f;
+#pragma unroll
+      for (int z = 0; z < S; ++z) qs += q[z];
+      scale = rsqrtf(qs / (float)p.K + p.eps);
     } else if constexpr (SCALE == 2) {
       scale = rsqrtf(p.ss_in[row] / (float)p.K + p.eps);
     }
+    f32x4 s = part[0];
+#pragma unroll
+    for (int z = 1; z < S; ++z) s += part[z];
     bf16x4* yp = reinterpret_cast<bf16x4*>(Y + (size_t)row * p.ldy + col);
     if constexpr (EPI == EPI_STORE) {
       bf16x4 o;
@@ -342,7 +353,7 @@ __global__ __launch_bounds__(256) void dgemm_reduce_kernel(DGemmArgs p, int S) {
 }
 
 bool dgemm_supported(int M, int N, int K, int splitk, int pf) {
-  if (M <= 0 || N <= 0 || K <= 0 || splitk < 1 || N % 4) return false;
+  if (M <= 0 || N <= 0 || K <= 0 || !dgemm_splitk_ok(splitk) || N % 4) return false;
   if (pf != 1 && pf != 2 && pf != 4 && pf != 8) return false;
   if (K % splitk) return false;
   const int kps = K / splitk;
@@ -383,19 +394,34 @@ static void dgemm_main(const DGemmArgs& p, dim3 grid, int pro, int epi, int pf, 
   }
 }
 
+template <int SCALE, int EPI>
+static void reduce_s(const DGemmArgs& p, int splitk, int blocks, hipStream_t st) {
+  switch (splitk) {
+    case 2: dgemm_reduce_kernel<SCALE, EPI, 2><<<blocks, 256, 0, st>>>(p); break;
+    case 4: dgemm_reduce_kernel<SCALE, EPI, 4><<<blocks, 256, 0, st>>>(p); break;
+    case 8: dgemm_reduce_kernel<SCALE, EPI, 8><<<blocks, 256, 0, st>>>(p); break;
+    default: dgemm_reduce_kernel<SCALE, EPI, 16><<<blocks, 256, 0, st>>>(p); break;
+  }
+}
+
+bool dgemm_splitk_ok(int splitk) {
+  return splitk == 1 || splitk == 2 || splitk == 4 || splitk == 8 || splitk == 16;
+}
+
 void launch_dgemm_reduce(const DGemmArgs& p, int pro, int splitk, hipStream_t st) {
   long blocks = ((long)p.M * p.N / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
+  const int b = (int)blocks;
   const int scale = pro == PRO_ADDNORM ? 1 : (pro == PRO_PLAIN && p.ss_in ? 2 : 0);
   if (p.epi == EPI_RESNORM) {
-    if (scale == 2) dgemm_reduce_kernel<2, EPI_RESNORM><<<(int)blocks, 256, 0, st>>>(p, splitk);
-    else dgemm_reduce_kernel<0, EPI_RESNORM><<<(int)blocks, 256, 0, st>>>(p, splitk);
+    if (scale == 2) reduce_s<2, EPI_RESNORM>(p, splitk, b, st);
+    else reduce_s<0, EPI_RESNORM>(p, splitk, b, st);
   } else if (scale == 1) {
-    dgemm_reduce_kernel<1, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
+    reduce_s<1, EPI_STORE>(p, splitk, b, st);
   } else if (scale == 2) {
-    dgemm_reduce_kernel<2, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
+    reduce_s<2, EPI_STORE>(p, splitk, b, st);
   } else {
-    dgemm_reduce_kernel<0, EPI_STORE><<<(int)blocks, 256, 0, st>>>(p, splitk);
+    reduce_s<0, EPI_STORE>(p, splitk, b, st);
   }
 }
 

@@ -1,19 +1,34 @@
 // Decode GEMM with LDS-DMA operand staging for gfx950:  Y[M,N] = X[M,K] . W[N,K]^T
 // (plain prologue + the dgemm.hip epilogues: store / residual+next-norm / SwiGLU, optional
-// ss_in row scale, split-K partials reduced by dgemm.hip's reduce pass).
+// ss_in row scale).
 //
-// Why: at decode sizes these GEMMs are bound by how many bytes per second each CU can pull
-// through its vector-load path; register staging (dgemm.hip) tops out at ~30-36 GB/s per CU,
-// while global_load_lds writes LDS directly (no VGPR round trip, no ds_write pass) and a CU
-// can take in far more (MI355X_MICROARCH.md price table rows ldsdma-fill / ring-gemm).
+// Why: at decode sizes (M <= 256) these GEMMs are latency bound -- every block walks its K
+// range as a chain of HBM/L2 round trips, and a CU only streams as fast as the bytes it
+// keeps in flight allow (in-flight bytes / load latency; MI355X_MICROARCH.md price-table rows
+// ldsdma-fill / ring-gemm).  global_load_lds writes LDS directly (no VGPR round trip, no
+// ds_write pass), so the ring depth is bounded by LDS, not registers:
+//   shallow ring: NS = 4 (64-col) / 3 (128-col) slots, two blocks per CU;
+//   deep ring:    NS = 8 (64-col, 128 KB) / 6 (128-col, 144 KB), one block per CU and
+//                 NS-1 k-steps (112-120 KB) in flight -- for grids of <= 256 tiles.
 //
-// Structure: 64 x BN output tile (BN 64 | 128), 4 waves as 2 (M) x 2 (N), BK = 64.  An LDS
-// ring of NS k-step slots [A 64 rows | W BN rows] x 128 B; NS-1 k-steps of global_load_lds
-// in flight.  Per k-step: counted `s_waitcnt vmcnt` for this step's DMAs, raw s_barrier (never
-// __syncthreads: its fence would drain every DMA in flight), refill the slot consumed one
-// step earlier, then ds_read fragments + MFMA.  LDS image: linear DMA destination, XOR swizzle
-// applied to the per-lane SOURCE address and to the fragment reads (the same involution,
-// cdna_hip_programming.md rule 21).
+// Structure: 64 x BN output tile (BN 64 | 128), 4 waves as 2 (M) x 2 (N), BK = 64.  Per
+// k-step: counted `s_waitcnt vmcnt` for this step's DMAs, raw s_barrier (never
+// __syncthreads: its fence would drain every DMA in flight), refill the slot consumed one step
+// earlier, then ds_read fragments + MFMA 16x16x32.  LDS image: linear DMA destination, XOR
+// swizzle applied to the per-lane SOURCE address and to the fragment reads (the same
+// involution, cdna_hip_programming.md rule 21).
+//
+// Split-K (gridDim.y = S slices):
+//   SPL 1: fp32 partial slabs [S, M, N], reduced (with the epilogue) by dgemm.hip's reduce pass;
+//   SPL 2: in-launch combine.  Every slice stores its accumulators as a fragment-native slab
+//          (16 B per lane per MFMA tile, fully coalesced), then publishes with the counter form
+//          of the agent-scope release/acquire hand-off (cdna_hip_programming.md "Projection
+//          GEMM at M = 256" item 2 / Guideline 16): every wave `s_waitcnt vmcnt(0)` ->
+//          barrier -> lane 0 release fence -> asm vmcnt(0) -> relaxed agent fetch_add on the
+//          tile's ticket.  The slice that draws S-1 re-arms the ticket, acquires (one lane,
+//          then vmcnt(0) + barrier), sums the S slabs and runs the epilogue.  No second
+//          launch, so the GEMM -> reduce kernel boundary (~1.5 us) and the reduce body go away,
+//          and split-K becomes legal for the SwiGLU epilogue too.
 #include "common.h"
 #include "kernels.h"
 
@@ -35,17 +50,21 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BN, int NS, int EPI, bool SPLIT>
-__global__ __launch_bounds__(256, 2) void gdgemm_kernel(DGemmArgs p) {
+template <int BN, int NS, int EPI, int SPL, int OCC, int S>
+__global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
   constexpr int SU = (GBM + BN) * 8;      // slot size in 16-B units
   constexpr int JN = BN / 32;             // 16-col MFMA tiles per wave (wave tile 32 x BN/2)
   constexpr int GA = 2, GW = BN / 32;     // DMA instructions per wave per k-step (A / W)
   constexpr int G = GA + GW;
-  __shared__ bf16x8 lds[NS * SU];
+  // ONE __shared__ object (a second one makes hipcc drain vmcnt inside the k-loop,
+  // cdna_hip_programming.md "Projection GEMM at M = 256" item 4a); the last element is the
+  // split-K "this block combines" flag
+  __shared__ bf16x8 lds[NS * SU + 1];
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + GBM - 1) / GBM;
-  const int lt = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+  const int ntiles = tiles_n * tiles_m;
+  const int lt = xcd_remap(blockIdx.x, ntiles);
   const int tn = lt / tiles_m, tm = lt % tiles_m;
   const int m0 = tm * GBM, n0 = tn * BN;
   const int kz = blockIdx.y;
@@ -87,11 +106,12 @@ __global__ __launch_bounds__(256, 2) void gdgemm_kernel(DGemmArgs p) {
   };
 
   // epilogue operands from the previous launch: load before the loop (hidden under it)
+  constexpr bool EPI_HERE = SPL != 1;  // this launch runs the epilogue (no separate reduce)
   float rsc[2][4];
   bf16 rold[2][4][JN];
   bf16 lnv[JN];
   const float* ssp = p.ss_in != nullptr ? p.ss_in : static_cast<const float*>(p.W);
-  if constexpr (!SPLIT) {
+  if constexpr (EPI_HERE) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -123,9 +143,12 @@ __global__ __launch_bounds__(256, 2) void gdgemm_kernel(DGemmArgs p) {
 #pragma unroll
     for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: NS-1 k-steps in flight (host: nk >= NS - 1)
+  // prologue: up to NS-1 k-steps in flight.  At step t the wait below leaves the NS-2 later
+  // steps in flight only when all of them exist (t + NS - 2 < nk), else drains to 0, so a
+  // short K range (nk < NS - 1) is handled by the same counts.
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue(s);
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s);
   for (int t = 0; t < nk; ++t) {
     // retire this thread's DMAs of step t: the later steps issued so far stay in flight
     if (t + NS - 2 < nk) wait_vm<G * (NS - 2)>();
@@ -150,6 +173,46 @@ __global__ __launch_bounds__(256, 2) void gdgemm_kernel(DGemmArgs p) {
     }
   }
 
+  if constexpr (SPL == 2) {
+    // ---- in-launch split-K combine (see header) ----
+    constexpr int NF = 2 * JN;  // f32x4 fragments per lane
+    f32x4* slabs = reinterpret_cast<f32x4*>(p.ws);
+    const size_t tile_stride = (size_t)NF * 256;
+    f32x4* mine = slabs + ((size_t)kz * ntiles + lt) * tile_stride + tid;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j) mine[(i * JN + j) * 256] = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(&lds[NS * SU]);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int prev = __hip_atomic_fetch_add(p.counters + lt, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == S - 1;
+      if (last) {
+        __hip_atomic_store(p.counters + lt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+    // the combining block sums all S slabs (its own included: one code path, every load
+    // issued back to back -- no per-slice runtime condition around a load)
+    const f32x4* t0 = slabs + (size_t)lt * tile_stride + tid;
+    const size_t zs = (size_t)ntiles * tile_stride;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] = t0[f * 256];
+#pragma unroll
+    for (int z = 1; z < S; ++z)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] += t0[z * zs + f * 256];
+  }
+
   // epilogue: lane holds rows wm*32 + i*16 + fg*4 + r, column fr of each 16-col sub-tile
   const float inv_k = 1.f / (float)p.K;
 #pragma unroll
@@ -158,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void gdgemm_kernel(DGemmArgs p) {
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wm * 32 + i * 16 + fg * 4 + r;
       const bool row_ok = row < p.M;
-      if constexpr (SPLIT) {
+      if constexpr (SPL == 1) {
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
           const int col = n0 + wn * (BN / 2) + j * 16 + fr;
@@ -210,30 +273,61 @@ __global__ __launch_bounds__(256, 2) void gdgemm_kernel(DGemmArgs p) {
 
 bool gdgemm_supported(int M, int N, int K, int splitk, int bn) {
   if (bn != 64 && bn != 128) return false;
-  if (M <= 0 || N <= 0 || K <= 0 || splitk < 1 || N % 4 || K % splitk) return false;
+  if (M <= 0 || N <= 0 || K <= 0 || !dgemm_splitk_ok(splitk) || N % 4 || K % splitk) return false;
   const int kps = K / splitk;
-  return kps % GBK == 0 && kps / GBK >= 3;  // ring prologue keeps up to 3 k-steps in flight
+  return kps % GBK == 0 && kps >= GBK;
 }
 
-template <int BN, int NS, bool SPL>
+long gdgemm_ws_floats(int M, int N, int splitk, int bn) {
+  const long tm = (M + GBM - 1) / GBM, tn = (N + bn - 1) / bn;
+  const long slabs = (long)splitk * tm * tn * GBM * bn;
+  const long dense = (long)splitk * M * N;
+  return slabs > dense ? slabs : dense;
+}
+
+template <int BN, int NS, int OCC, int SPL, int S>
 static void gdgemm_epi(const DGemmArgs& p, dim3 grid, hipStream_t st) {
-  if (p.epi == EPI_RESNORM) gdgemm_kernel<BN, NS, EPI_RESNORM, SPL><<<grid, 256, 0, st>>>(p);
-  else if (p.epi == EPI_SILU) {
-    if constexpr (!SPL) gdgemm_kernel<BN, NS, EPI_SILU, false><<<grid, 256, 0, st>>>(p);
-  } else gdgemm_kernel<BN, NS, EPI_STORE, SPL><<<grid, 256, 0, st>>>(p);
+  if (p.epi == EPI_RESNORM) {
+    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S><<<grid, 256, 0, st>>>(p);
+  } else if (p.epi == EPI_SILU) {
+    if constexpr (SPL != 1) gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S><<<grid, 256, 0, st>>>(p);
+  } else {
+    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S><<<grid, 256, 0, st>>>(p);
+  }
+}
+
+template <int BN, int NS, int OCC>
+static void gdgemm_ring(const DGemmArgs& p, dim3 grid, int splitk, hipStream_t st) {
+  if (splitk == 1) {
+    gdgemm_epi<BN, NS, OCC, 0, 1>(p, grid, st);
+  } else if (p.counters == nullptr) {
+    gdgemm_epi<BN, NS, OCC, 1, 1>(p, grid, st);
+    launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
+  } else {
+    switch (splitk) {
+      case 2: gdgemm_epi<BN, NS, OCC, 2, 2>(p, grid, st); break;
+      case 4: gdgemm_epi<BN, NS, OCC, 2, 4>(p, grid, st); break;
+      case 8: gdgemm_epi<BN, NS, OCC, 2, 8>(p, grid, st); break;
+      default:  // 16 slices: slabs + the separate reduce pass
+        gdgemm_epi<BN, NS, OCC, 1, 1>(p, grid, st);
+        launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
+        break;
+    }
+  }
 }
 
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st) {
   const int tiles = ((p.M + GBM - 1) / GBM) * ((p.N + p.bn - 1) / p.bn);
   dim3 grid(tiles, splitk);
-  // NS = 4 (64-col: 4 x 16 KB) / 3 (128-col: 3 x 24 KB): two blocks fit a CU's 160 KB LDS
-  if (splitk > 1) {
-    if (p.bn == 128) gdgemm_epi<128, 3, true>(p, grid, st);
-    else gdgemm_epi<64, 4, true>(p, grid, st);
-    launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
+  const bool deep = p.ns >= 6;
+  // shallow: NS = 4 (64-col: 4 x 16 KB) / 3 (128-col: 3 x 24 KB) -> two blocks per CU;
+  // deep: 8 x 16 KB / 6 x 24 KB -> one block per CU
+  if (p.bn == 128) {
+    if (deep) gdgemm_ring<128, 6, 1>(p, grid, splitk, st);
+    else gdgemm_ring<128, 3, 2>(p, grid, splitk, st);
   } else {
-    if (p.bn == 128) gdgemm_epi<128, 3, false>(p, grid, st);
-    else gdgemm_epi<64, 4, false>(p, grid, st);
+    if (deep) gdgemm_ring<64, 8, 1>(p, grid, splitk, st);
+    else gdgemm_ring<64, 4, 2>(p, grid, splitk, st);
   }
 }
 

@@ -93,13 +93,19 @@ struct DGemmArgs {
   int M, N, K, ldx, ldw, ldy, kps, epi;
   float eps;
   int bn;  // 0: register-ring kernel (dgemm.hip); 64 | 128: LDS-DMA ring kernel (gdgemm.hip)
+  int ns;  // gdgemm ring depth: 0 = shallow (2 blocks/CU), >= 6 = deep ring (1 block/CU)
+  int* counters;  // gdgemm split-K: zeroed per-tile tickets -> in-launch last-arriver combine
 };
 bool dgemm_supported(int M, int N, int K, int splitk, int pf);
+// split-K factors with a compiled reduce (1, 2, 4, 8, 16)
+bool dgemm_splitk_ok(int splitk);
 bool dgemm_epi_supported(int N, int epi, int splitk);
 void launch_dgemm(const DGemmArgs& a, int pro, int splitk, int pf, hipStream_t st);
 void launch_dgemm_reduce(const DGemmArgs& p, int pro, int splitk, hipStream_t st);
 // gdgemm.hip: the same plain-prologue GEMM + epilogues with operands staged by global_load_lds
 bool gdgemm_supported(int M, int N, int K, int splitk, int bn);
+// fp32 workspace floats a gdgemm split-K launch needs (tile-padded slabs)
+long gdgemm_ws_floats(int M, int N, int splitk, int bn);
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st);
 
 // ---- sampling.hip ----

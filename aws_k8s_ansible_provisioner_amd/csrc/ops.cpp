@@ -282,7 +282,8 @@ void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk,
 void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t splitk, int64_t pf,
            std::optional<Tensor> r, std::optional<Tensor> rout, std::optional<Tensor> ln,
            double eps, int64_t epi, std::optional<Tensor> ss_in, std::optional<Tensor> ss_out,
-           std::optional<Tensor> aout, std::optional<Tensor> ln_out, int64_t bn) {
+           std::optional<Tensor> aout, std::optional<Tensor> ln_out, int64_t bn, int64_t ns,
+           std::optional<Tensor> counters) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "dgemm: 2-D tensors");
@@ -297,15 +298,20 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   TORCH_CHECK(bn > 0 ? akap::gdgemm_supported(M, N, K, splitk, bn)
                      : akap::dgemm_supported(M, N, K, splitk, pf),
               "dgemm: unsupported M/N/K/splitk/pf/bn");
-  TORCH_CHECK(akap::dgemm_epi_supported(N, epi, splitk), "dgemm: unsupported epilogue/N/splitk");
+  const bool inlaunch = counters.has_value() && splitk > 1 && bn > 0;
+  TORCH_CHECK(inlaunch ? (epi != akap::EPI_SILU || N % 32 == 0)
+                       : akap::dgemm_epi_supported(N, epi, splitk),
+              "dgemm: unsupported epilogue/N/splitk");
   TORCH_CHECK((int64_t)N * K * 2 >= (int64_t)M * 4, "dgemm: W smaller than M floats");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
               "dgemm: 16-byte aligned rows");
   if (splitk > 1) {
-    const int64_t need = splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
+    const int64_t need = bn > 0 ? akap::gdgemm_ws_floats(M, N, (int)splitk, (int)bn)
+                                : splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
     TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= need,
                 "dgemm: fp32 workspace of splitk*M*N (+ splitk*M for the norm)");
-    TORCH_CHECK(out.stride(0) == N, "dgemm: split-K output must be dense");
+    TORCH_CHECK(out.stride(0) == N || (counters.has_value() && bn > 0),
+                "dgemm: split-K output must be dense (separate reduce pass)");
   }
   akap::DGemmArgs a{};
   a.X = x.data_ptr();
@@ -317,6 +323,14 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   a.eps = (float)eps;
   a.epi = (int)epi;
   a.bn = (int)bn;
+  a.ns = (int)ns;
+  if (counters && splitk > 1 && bn > 0) {
+    // in-launch split-K combine: one zeroed int32 ticket per output tile
+    TORCH_CHECK(counters->scalar_type() == at::kInt && counters->is_cuda() &&
+                    counters->numel() >= (int64_t)((M + 63) / 64) * ((N + bn - 1) / bn),
+                "dgemm: counters int32, one per output tile");
+    a.counters = counters->data_ptr<int>();
+  }
   if (pro == akap::PRO_ADDNORM) {
     TORCH_CHECK(r && rout && ln, "dgemm addnorm: residual, residual-out and norm weight");
     CHECK_BF16(*r); CHECK_BF16(*rout); CHECK_BF16(*ln);
@@ -749,7 +763,7 @@ TORCH_LIBRARY(akap, m) {
       "dgemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int pro, int splitk, int pf, "
       "Tensor? r=None, Tensor(c!)? rout=None, Tensor? ln=None, float eps=1e-6, int epi=0, "
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
-      "Tensor? ln_out=None, int bn=0) -> ()");
+      "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None) -> ()");
   m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
   m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");

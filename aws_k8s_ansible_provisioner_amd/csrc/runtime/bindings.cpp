@@ -56,7 +56,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readwrite("gqa_group", &SchedConfig::gqa_group)
       .def_readwrite("tile_rows", &SchedConfig::tile_rows)
       .def_readwrite("eos_id", &SchedConfig::eos_id)
-      .def_readwrite("max_blocks_per_seq", &SchedConfig::max_blocks_per_seq);
+      .def_readwrite("max_blocks_per_seq", &SchedConfig::max_blocks_per_seq)
+      .def_readwrite("mixed_batching", &SchedConfig::mixed_batching)
+      .def_readwrite("held_kv_ttl_s", &SchedConfig::held_kv_ttl_s);
 
   py::class_<Scheduler>(m, "Scheduler")
       .def(py::init<const SchedConfig&, int, bool>(), py::arg("config"), py::arg("num_blocks"),
@@ -104,6 +106,7 @@ PYBIND11_MODULE(_runtime, m) {
              d["num_samples"] = i.num_samples;
              d["max_seq_len"] = i.max_seq_len;
              d["num_preempted"] = i.num_preempted;
+             d["num_decode"] = i.num_decode;
              return d;
            })
       .def("update",
@@ -133,6 +136,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def("held_blocks", &Scheduler::held_blocks)
       .def("free_held", &Scheduler::free_held)
       .def_property_readonly("num_held", &Scheduler::num_held)
+      .def("expire_held", &Scheduler::expire_held, py::arg("now_s"))
+      .def_static("now_s", &Scheduler::now_s)
+      .def_property_readonly("held_expired_total", &Scheduler::held_expired_total)
       .def("reserve_prefilled", &Scheduler::reserve_prefilled, py::arg("id"), py::arg("tokens"),
            py::arg("num_prompt"), py::arg("max_tokens"), py::arg("min_tokens") = 0,
            py::arg("ignore_eos") = false, py::arg("stop_ids") = std::vector<int32_t>{},

@@ -1,6 +1,7 @@
 #include "scheduler.h"
 
 #include <algorithm>
+#include <chrono>
 #include <stdexcept>
 
 namespace akap_rt {
@@ -58,14 +59,34 @@ void Scheduler::set_hold_kv(int64_t id, bool hold) {
 
 std::vector<int32_t> Scheduler::held_blocks(int64_t id) const {
   auto it = held_.find(id);
-  return it == held_.end() ? std::vector<int32_t>{} : it->second;
+  return it == held_.end() ? std::vector<int32_t>{} : it->second.blocks;
 }
 
 void Scheduler::free_held(int64_t id) {
   auto it = held_.find(id);
   if (it == held_.end()) return;
-  bm_.free_blocks(it->second);
+  bm_.free_blocks(it->second.blocks);
   held_.erase(it);
+}
+
+double Scheduler::now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+int Scheduler::expire_held(double now) {
+  int n = 0;
+  for (auto it = held_.begin(); it != held_.end();) {
+    if (it->second.deadline <= now) {
+      bm_.free_blocks(it->second.blocks);
+      it = held_.erase(it);
+      ++n;
+    } else {
+      ++it;
+    }
+  }
+  held_expired_ += n;
+  return n;
 }
 
 std::vector<int32_t> Scheduler::reserve_prefilled(
@@ -128,7 +149,9 @@ bool Scheduler::abort_request(int64_t id) {
 
 void Scheduler::finish(Request& r, int reason) {
   if (r.hold_kv && reason != FINISH_ABORT && !r.blocks.empty()) {
-    held_[r.id] = r.blocks;  // P/D: ownership moves to the transfer agent
+    // P/D: ownership moves to the transfer agent until a decode engine pulls the KV
+    // (/kv/push -> free_held), releases it (/kv/release), or the TTL runs out
+    held_[r.id] = HeldKV{r.blocks, now_s() + cfg_.held_kv_ttl_s};
   } else if (!r.blocks.empty()) {
     bm_.free_blocks(r.blocks);
   }
@@ -174,15 +197,8 @@ void Scheduler::preempt(Request& r) {
   waiting_.push_front(&r);
 }
 
-StepInfo Scheduler::schedule(BatchBuffers& buf) {
-  StepInfo info;
-  last_sampled_.clear();
-  const int bs = cfg_.block_size;
-  const int mb = cfg_.max_blocks_per_seq;
-  std::vector<std::pair<Request*, int>> sched;  // (request, q_len)
-
-  // ---------------- prefill (chunked) ----------------
-  int budget = std::min(cfg_.max_num_batched_tokens, buf.cap_tokens);
+void Scheduler::schedule_prefills(std::vector<std::pair<Request*, int>>& sched, int& budget) {
+  // running sequences with more than one uncomputed token: the next chunk of their prompt
   for (Request* r : running_) {
     const int remaining = (int)r->tokens.size() - r->num_computed;
     if (remaining <= 1 || budget <= 0) continue;
@@ -192,6 +208,7 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     sched.emplace_back(r, q);
     budget -= q;
   }
+  // admit waiting requests (FCFS) while budget, sequence slots and KV blocks last
   while (!waiting_.empty() && budget > 0 &&
          (int)running_.size() < cfg_.max_num_seqs && (int)sched.size() < cfg_.max_num_seqs) {
     Request* r = waiting_.front();
@@ -207,7 +224,6 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     }
     const int remaining = (int)r->tokens.size() - r->num_computed;
     const int q = std::min(remaining, budget);
-    // keep a small reserve so admitted sequences can decode a few steps
     if (!ensure_blocks(*r, r->num_computed + q)) {
       if (running_.empty() && sched.empty()) {
         // nothing holds blocks and it still does not fit: it never will
@@ -224,36 +240,73 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     sched.emplace_back(r, q);
     budget -= q;
   }
+}
 
-  if (!sched.empty()) {
-    info.is_prefill = 1;
-  } else {
-    // ---------------- decode ----------------
-    // oldest first; preempt from the young end when the pool runs dry
-    size_t i = 0;
-    while (i < running_.size()) {
-      Request* r = running_[i];
-      if ((int)sched.size() >= cfg_.max_num_seqs) break;
-      if (ensure_blocks(*r, r->num_computed + 1)) {
-        sched.emplace_back(r, 1);
-        ++i;
-        continue;
-      }
-      // out of blocks (or seq too long): preempt the youngest other sequence
-      Request* victim = running_.back();
-      if ((int)r->blocks.size() >= mb || (victim == r && i == 0)) {
-        // too long, or alone and the whole pool still cannot hold its next token:
-        // end it here (length-capped) instead of preempting it forever
-        finish(*r, FINISH_LENGTH);
-        sched_finished_.emplace_back(r->id, FINISH_LENGTH);
-        running_.erase(running_.begin() + i);
-        continue;
-      }
-      preempt(*victim);
-      ++info.num_preempted;
-      if (victim == r) break;
+void Scheduler::schedule_decodes(std::vector<std::pair<Request*, int>>& sched, StepInfo& info,
+                                 int& budget) {
+  // one token for every running sequence whose prompt is fully computed; oldest first,
+  // preempt from the young end when the pool runs dry
+  const int mb = cfg_.max_blocks_per_seq;
+  size_t i = 0;
+  while (i < running_.size()) {
+    Request* r = running_[i];
+    if ((int)sched.size() >= cfg_.max_num_seqs || budget <= 0) break;
+    if ((int)r->tokens.size() - r->num_computed != 1) {  // still prefilling
+      ++i;
+      continue;
     }
+    if (ensure_blocks(*r, r->num_computed + 1)) {
+      sched.emplace_back(r, 1);
+      --budget;
+      ++i;
+      continue;
+    }
+    // out of blocks (or seq too long): preempt the youngest other sequence
+    Request* victim = running_.back();
+    if ((int)r->blocks.size() >= mb || (victim == r && i == 0)) {
+      // too long, or alone and the whole pool still cannot hold its next token:
+      // end it here (length-capped) instead of preempting it forever
+      finish(*r, FINISH_LENGTH);
+      sched_finished_.emplace_back(r->id, FINISH_LENGTH);
+      running_.erase(running_.begin() + i);
+      continue;
+    }
+    // a victim already scheduled in this step is not preempted (its rows are written)
+    bool scheduled = false;
+    for (auto& e : sched) scheduled |= e.first == victim;
+    if (scheduled) break;
+    preempt(*victim);
+    ++info.num_preempted;
+    if (victim == r) break;
   }
+}
+
+StepInfo Scheduler::schedule(BatchBuffers& buf) {
+  StepInfo info;
+  last_sampled_.clear();
+  if (!held_.empty()) expire_held(now_s());
+  const int bs = cfg_.block_size;
+  const int mb = cfg_.max_blocks_per_seq;
+  std::vector<std::pair<Request*, int>> sched;  // (request, q_len)
+  int budget = std::min(cfg_.max_num_batched_tokens, buf.cap_tokens);
+
+  bool pending_prefill = !waiting_.empty();
+  for (Request* r : running_)
+    pending_prefill |= (int)r->tokens.size() - r->num_computed > 1;
+  if (pending_prefill && cfg_.mixed_batching) {
+    // mixed step: decodes first (they never stall behind a prefill), then prefill chunks
+    schedule_decodes(sched, info, budget);
+    info.num_decode = (int)sched.size();
+    schedule_prefills(sched, budget);
+  } else if (pending_prefill) {
+    schedule_prefills(sched, budget);  // prefill-first policy
+  }
+  if (sched.empty()) {
+    budget = std::min(cfg_.max_num_batched_tokens, buf.cap_tokens);
+    schedule_decodes(sched, info, budget);
+    info.num_decode = (int)sched.size();
+  }
+  info.is_prefill = (int)sched.size() > info.num_decode ? 1 : 0;
 
   // ---------------- flatten ----------------
   int T = 0, tiles = 0, ns = 0;
@@ -276,7 +329,7 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     const int nb = (int)r->blocks.size();
     for (int b = 0; b < mb; ++b) row[b] = b < nb ? r->blocks[b] : 0;
     buf.req_ids[s] = r->id;
-    if (info.is_prefill) {
+    if (info.is_prefill && (int)s >= info.num_decode) {  // decode rows: decode kernel
       const int rows = q * cfg_.gqa_group;
       for (int t0 = 0; t0 < rows; t0 += cfg_.tile_rows) {
         if (tiles >= buf.cap_tiles) throw std::runtime_error("tile buffer too small");

@@ -4,9 +4,13 @@
 // batch description (token ids, positions, paged-cache slots, block tables, cu-seqlens,
 // attention tile map, logits rows) straight into caller-owned pinned buffers, so the
 // Python engine loop does no per-token work.  Policy:
-//   * chunked prefill under a token budget (prefill-first: best TTFT / throughput);
-//   * otherwise one decode token for every running sequence;
-//   * out of KV blocks -> preempt the youngest running sequence (recompute later).
+//   * mixed batching (default): every running decode gets its token first, the rest of the
+//     step's token budget is filled with prefill chunks, so a running decode never stalls
+//     behind a prefill (the decode rows lead the flattened batch: [0, num_decode));
+//   * mixed_batching = false: prefill-first (a step is pure prefill while any is pending);
+//   * a step with no prefill work is a pure decode step (hipGraph replay);
+//   * out of KV blocks -> preempt the youngest running sequence (recompute later);
+//   * P/D prefill side: KV blocks held for a transfer expire after held_kv_ttl_s.
 #pragma once
 
 #include <cstdint>
@@ -58,6 +62,8 @@ struct SchedConfig {
   int tile_rows = 64;     // flattened query rows per prefill attention workgroup
   int eos_id = -1;
   int max_blocks_per_seq = 128;
+  bool mixed_batching = true;
+  double held_kv_ttl_s = 120.0;  // P/D: held KV never pulled by a decode engine is freed
 };
 
 // Views into caller buffers (numpy, pinned).  Sizes are checked by the binding.
@@ -90,6 +96,7 @@ struct StepInfo {
   int num_samples = 0;
   int max_seq_len = 0;
   int num_preempted = 0;
+  int num_decode = 0;  // leading single-token decode rows (all rows of a pure decode step)
 };
 
 class Scheduler {
@@ -138,9 +145,17 @@ class Scheduler {
                                          int64_t seed, bool stream);
   void activate(int64_t id);
   size_t num_held() const { return held_.size(); }
+  // free every held-KV entry whose deadline passed (schedule() calls it with the steady
+  // clock); returns the number expired
+  int expire_held(double now_s);
+  int64_t held_expired_total() const { return held_expired_; }
+  static double now_s();
 
  private:
   bool ensure_blocks(Request& r, int num_tokens);
+  void schedule_decodes(std::vector<std::pair<Request*, int>>& sched, StepInfo& info,
+                        int& budget);
+  void schedule_prefills(std::vector<std::pair<Request*, int>>& sched, int& budget);
   void publish_full_blocks(Request& r);
   void preempt(Request& r);
   void finish(Request& r, int reason);
@@ -154,8 +169,13 @@ class Scheduler {
   // requests the scheduler itself had to finish (KV pool can never hold them); reported by
   // the next update() as events with token -1
   std::vector<std::pair<int64_t, int>> sched_finished_;
-  std::unordered_map<int64_t, std::vector<int32_t>> held_;
+  struct HeldKV {
+    std::vector<int32_t> blocks;
+    double deadline;
+  };
+  std::unordered_map<int64_t, HeldKV> held_;
   int64_t preemptions_ = 0;
+  int64_t held_expired_ = 0;
 };
 
 }  // namespace akap_rt

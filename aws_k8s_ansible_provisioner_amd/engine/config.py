@@ -29,6 +29,8 @@ class EngineConfig:
     kv_cache_dtype: str = "auto"              # "auto" (model dtype, bf16) | "fp8" (e4m3fn)
     init_std: float = 0.02                    # random-init weight scale
     shard_init: str = "per_rank"              # "per_rank" | "full" (identical logical weights for any TP)
+    mixed_batching: bool = True               # decodes + prefill chunks in one step
+    held_kv_ttl_s: float = 120.0              # P/D prefill: free un-pulled held KV after this
 
     def __post_init__(self) -> None:
         # the K cache stores each 32-token chunk in MFMA-fragment order (ops/reference.py)

@@ -78,6 +78,8 @@ class LLMEngine:
         sc.tile_rows = self.runner.tile_rows
         sc.eos_id = self.mcfg.eos_id
         sc.max_blocks_per_seq = self.runner.max_blocks
+        sc.mixed_batching = ecfg.mixed_batching
+        sc.held_kv_ttl_s = ecfg.held_kv_ttl_s
         self.sched = rt.Scheduler(sc, self.runner.num_blocks, ecfg.enable_prefix_caching)
         self.tokenizer = get_tokenizer(ecfg.weights_path, self.mcfg.vocab_size, self.mcfg.bos_id,
                                        self.mcfg.eos_id)
@@ -241,7 +243,7 @@ class LLMEngine:
             ids, new, fin, first = self.sched.update(np.ascontiguousarray(toks, dtype=np.int64))
         m, name = self.metrics, self.model_name
         if info["is_prefill"]:
-            m.prompt_tokens.inc(info["num_tokens"], model_name=name)
+            m.prompt_tokens.inc(info["num_tokens"] - info.get("num_decode", 0), model_name=name)
         m.gen_tokens.inc(info["num_samples"], model_name=name)
         m.step_time.observe(now - t0, model_name=name,
                             phase="prefill" if info["is_prefill"] else "decode")

@@ -193,6 +193,8 @@ class ModelRunner:
                           greedy_logprobs=lp)
 
     def execute_prefill(self, info: dict) -> torch.Tensor:
+        """A step with prefill chunks; under mixed batching its leading `num_decode` rows are
+        running sequences' decode tokens (eager, same forward)."""
         T, B, nt, ns = info["num_tokens"], info["num_seqs"], info["num_tiles"], info["num_samples"]
         mb = self.max_blocks
         ids = self._h2d("input_ids", T)
@@ -206,8 +208,10 @@ class ModelRunner:
         lidx = self._h2d("logits_idx", ns)
         for k in ("temperature", "top_p", "top_k", "seeds", "steps"):
             self._h2d(k, ns)
-        batch = AttnBatch(True, pos, slots, self.d_bt[:B], sl, qs, ts, tr,
-                          tile_rows=self.tile_rows)
+        nd = info.get("num_decode", 0)
+        parts, ps = self.decode_partitions(nd) if nd else (1, 512)
+        batch = AttnBatch(True, pos, slots, self.d_bt[:B], sl, qs, ts, tr, parts, ps,
+                          self.workspace, tile_rows=self.tile_rows, num_decode=nd)
         h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
         if ns == 0:
             return self.out_tokens[:0]

@@ -47,6 +47,7 @@ class AttnBatch:
     part_size: int = 512
     workspace: Optional[tuple] = None
     tile_rows: int = 64          # q rows per prefill tile of the map (128: flash-style kernel)
+    num_decode: int = 0          # mixed step: leading single-token decode rows [0, num_decode)
 
 
 @dataclasses.dataclass
@@ -251,6 +252,16 @@ class DecoderLM:
 
     def _attention(self, q, batch: AttnBatch, kc, vc, out):
         if batch.is_prefill:
+            nd = batch.num_decode
+            if nd and q.is_cuda:
+                # mixed step: the decode rows lead the batch and run the split-KV decode
+                # kernel; the prefill tile map covers only the prefill rows after them
+                # (on CPU the reference attention handles every row at once)
+                ops.paged_attention_decode(out[:nd], q[:nd], kc, vc, batch.block_tables[:nd],
+                                           batch.seq_lens[:nd], self.hq // self.hkv,
+                                           self.scale, workspace=batch.workspace,
+                                           num_parts=batch.num_parts,
+                                           part_size=batch.part_size)
             ops.paged_attention_prefill(out, q, kc, vc, batch.block_tables, batch.seq_lens,
                                         batch.q_start, batch.tile_seq, batch.tile_row,
                                         self.hq // self.hkv, self.scale,
@@ -322,13 +333,18 @@ class DecoderLM:
         T = input_ids.shape[0]
         eps = self.cfg.rms_eps
         L = len(self.layers)
+
+        def cfg_(name):  # plan entry (split-K, prefetch, tile width[, ring, in-launch combine])
+            s_, p_, b_, n_, i_ = (tuple(plan[name]) + (0, False))[:5]
+            return dict(splitk=s_, pf=p_, bn=b_, ns=n_, inlaunch=bool(i_))
+
+        c_qkv, c_o, c_gu, c_d = (cfg_(n) for n in ("w_qkv", "w_o", "w_gate_up", "w_down"))
         residual = self.embed_tokens(input_ids)
         ss = torch.zeros(2 * L, T, dtype=torch.float32, device=self.device)
         a1 = ops.rms_norm(residual, self.layers[0].ln1, eps)
         ss_in = None
         for li, lw in enumerate(self.layers):
-            s_, p_, b_ = plan["w_qkv"]
-            qkv = ops.dgemm(a1, lw.w_qkv, splitk=s_, pf=p_, eps=eps, ss_in=ss_in, bn=b_)
+            qkv = ops.dgemm(a1, lw.w_qkv, eps=eps, ss_in=ss_in, **c_qkv)
             attn = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
             ops.paged_attention_decode_fused(
                 attn, qkv, k_caches[li], v_caches[li], batch.block_tables, batch.seq_lens,
@@ -336,22 +352,18 @@ class DecoderLM:
                 self.hq // self.hkv, self.scale, eps, workspace=batch.workspace,
                 num_parts=batch.num_parts, part_size=batch.part_size)
             a2 = torch.empty_like(residual)
-            s_, p_, b_ = plan["w_o"]
-            ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, splitk=s_, pf=p_, eps=eps,
-                      out=residual, epi=ops.EPI_RESNORM, ss_out=ss[2 * li], a_out=a2,
-                      ln_out=lw.ln2, bn=b_)
-            s_, p_, b_ = plan["w_gate_up"]
-            act = ops.dgemm(a2, lw.w_gate_up, splitk=s_, pf=p_, eps=eps, ss_in=ss[2 * li],
-                            epi=ops.EPI_SILU, bn=b_)
-            s_, p_, b_ = plan["w_down"]
+            ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, eps=eps, out=residual,
+                      epi=ops.EPI_RESNORM, ss_out=ss[2 * li], a_out=a2, ln_out=lw.ln2, **c_o)
+            act = ops.dgemm(a2, lw.w_gate_up, eps=eps, ss_in=ss[2 * li], epi=ops.EPI_SILU,
+                            **c_gu)
             if li + 1 < L:
                 a1 = torch.empty_like(residual)
-                ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps, out=residual,
-                          epi=ops.EPI_RESNORM, ss_out=ss[2 * li + 1], a_out=a1,
-                          ln_out=self.layers[li + 1].ln1, bn=b_)
+                ops.dgemm(act, lw.w_down, eps=eps, out=residual, epi=ops.EPI_RESNORM,
+                          ss_out=ss[2 * li + 1], a_out=a1, ln_out=self.layers[li + 1].ln1,
+                          **c_d)
                 ss_in = ss[2 * li + 1]
             else:
-                x = ops.dgemm(act, lw.w_down, splitk=s_, pf=p_, eps=eps, bn=b_)
+                x = ops.dgemm(act, lw.w_down, eps=eps, **c_d)
         h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
         return h
 

@@ -194,8 +194,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
         choice = gemm_tuner.lookup(M, w.shape[0], w.shape[1])
         if choice is not None:  # measured at engine start (cold weights, real layers)
             if choice[0] == "dgemm" and x.stride(-1) == 1:
-                return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out,
-                             bn=choice[3] if len(choice) > 3 else 0)
+                bn, ns, inl = (tuple(choice[3:]) + (0, 0, False))[:3]
+                return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out, bn=bn, ns=ns,
+                             inlaunch=inl)
             split = choice[1] if choice[0] == "hip" else 0
     if split is None:
         use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
@@ -241,7 +242,7 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
           out: Optional[torch.Tensor] = None, epi: int = EPI_STORE,
           ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
           a_out: Optional[torch.Tensor] = None, ln_out: Optional[torch.Tensor] = None,
-          bn: int = 0) -> torch.Tensor:
+          bn: int = 0, ns: int = 0, inlaunch: bool = False) -> torch.Tensor:
     """Fused decode GEMM (csrc/kernels/dgemm.hip): y = A @ w.T where A is produced from x by
     the prologue inside the GEMM's operand staging --
       PRO_PLAIN    A = x; with ss_in, rows of y are scaled by rsqrt(ss_in / K + eps)
@@ -254,7 +255,10 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
       EPI_SILU     w = [gate; up] rows, out [M, N/2] = silu(y_gate) * y_up
     replacing the separate fused_add_rms_norm / silu_and_mul launches of a decode layer.
     bn = 64 | 128 selects the LDS-DMA staged variant (csrc/kernels/gdgemm.hip, 64 x bn tiles,
-    plain prologue only); 0 the register-ring kernel (prefetch depth pf)."""
+    plain prologue only); 0 the register-ring kernel (prefetch depth pf).  For bn > 0:
+    ns >= 6 selects the deep LDS ring (one block per CU, ~7 k-steps in flight), and with
+    splitk > 1 inlaunch=True combines the K slices inside the launch (last-arriver ticket,
+    no separate reduce kernel; also allows split-K with the SwiGLU epilogue)."""
     M = x.shape[0]
     N, K = w.shape
     if out is None:
@@ -281,32 +285,45 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
         else:
             out.copy_(y.to(out.dtype))
         return out
+    counters = None
     if splitk > 1:
-        n = splitk * M * N + (splitk * M if pro == PRO_ADDNORM else 0)
+        n = (gdgemm_ws_floats(M, N, splitk, bn) if bn else
+             splitk * M * N + (splitk * M if pro == PRO_ADDNORM else 0))
         ws = torch.empty(n, dtype=torch.float32, device=x.device)
+        if inlaunch and bn:
+            counters = gemm_counters(x.device)
     else:
         ws = _EMPTY_F32.get(x.device)
         if ws is None:
             ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
     torch.ops.akap.dgemm(out, x, w, ws, pro, splitk, pf, residual, residual_out, ln, eps, epi,
-                         ss_in, ss_out, a_out, ln_out, bn)
+                         ss_in, ss_out, a_out, ln_out, bn, ns, counters)
     return out
 
 
 def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI_STORE,
-                    bn: int = 0) -> bool:
+                    bn: int = 0, inlaunch: bool = False) -> bool:
     """Mirror of dgemm_supported / gdgemm_supported / dgemm_epi_supported (host-side)."""
-    if epi == EPI_SILU and (splitk != 1 or N % 32):
+    if splitk not in (1, 2, 4, 8, 16):
         return False
-    if epi == EPI_RESNORM and splitk > 1 and N % 256:
+    inl = inlaunch and bn and splitk > 1
+    if epi == EPI_SILU and ((splitk != 1 and not inl) or N % 32):
+        return False
+    if epi == EPI_RESNORM and splitk > 1 and N % 256 and not inl:
         return False
     if bn:
-        if bn not in (64, 128) or M <= 0 or N % 4 or splitk < 1 or K % splitk:
+        if bn not in (64, 128) or M <= 0 or N % 4 or K % splitk:
             return False
-        return (K // splitk) % 64 == 0 and (K // splitk) // 64 >= 3
-    if M <= 0 or N <= 0 or K <= 0 or splitk < 1 or N % 4 or pf not in (1, 2, 4, 8) or K % splitk:
+        return (K // splitk) % 64 == 0
+    if M <= 0 or N <= 0 or K <= 0 or N % 4 or pf not in (1, 2, 4, 8) or K % splitk:
         return False
     return (K // splitk) % (64 * pf) == 0
+
+
+def gdgemm_ws_floats(M: int, N: int, splitk: int, bn: int) -> int:
+    """fp32 workspace of a split-K LDS-DMA GEMM (tile-padded slabs; mirrors gdgemm.hip)."""
+    slabs = splitk * -(-M // 64) * -(-N // bn) * 64 * bn
+    return max(slabs, splitk * M * N)
 
 
 _COUNTERS: dict = {}

@@ -23,7 +23,8 @@ from typing import Optional, Sequence
 
 import torch
 
-Choice = tuple  # ("torch",) | ("hip", splitk) | ("dgemm", splitk, prefetch_depth[, lds_dma_bn])
+Choice = tuple  # ("torch",) | ("hip", splitk) | ("dgemm", splitk, prefetch_depth[, lds_dma_bn,
+#                 ring_slots, in_launch_combine])
 _PLAN: dict = {}
 
 
@@ -59,6 +60,28 @@ def _timed(fn, n: int) -> float:
     return e0.elapsed_time(e1) * 1000.0 / (2 * n)
 
 
+def _gd_variants(s: int, bns):
+    """gdgemm.hip variants at split s: (tile width, ring depth, in-launch split-K combine).
+    Depth 0 = shallow ring (two blocks per CU), 8 = deep ring (one block per CU)."""
+    for bn in bns:
+        for ns in (0, 8):
+            for inl in ((False, True) if s > 1 else (False,)):
+                yield bn, ns, inl
+
+
+def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out, ln_out):
+    """fn(i) launching one gdgemm variant on weights[i % len] (workspace/tickets bound)."""
+    from . import gdgemm_ws_floats, gemm_counters
+
+    dev = x.device
+    ws = torch.empty(max(1, gdgemm_ws_floats(M, N, s, bn) if s > 1 else 1), device=dev,
+                     dtype=torch.float32)
+    cnt = gemm_counters(dev) if (inl and s > 1) else None
+    n = len(weights)
+    return lambda i: torch.ops.akap.dgemm(out, x, weights[i % n], ws, 0, s, 1, None, None, None,
+                                          1e-6, epi, ss_in, ss_out, a_out, ln_out, bn, ns, cnt)
+
+
 def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
          margin: float = 0.03, pfs=(2, 4, 8), bns=(64, 128)) -> Choice:
     """Pick the fastest way to compute x[M, K] @ w.T for these same-shape weights.
@@ -90,19 +113,22 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
             t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, pf), n)
             if t < t_best:
                 best, t_best = ("dgemm", s, pf), t
-        for bn in bns:  # LDS-DMA staged variant (gdgemm.hip)
-            if not dgemm_supported(M, N, K, s, 1, bn=bn) or (s > 1 and K // s < 256):
+        for bn, ns, inl in _gd_variants(s, bns):  # LDS-DMA staged variants (gdgemm.hip)
+            if not dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl) or (s > 1 and K // s < 256):
                 continue
-            ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
-            t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, 1, None,
-                                                      None, None, 1e-6, 0, None, None, None,
-                                                      None, bn), n)
+            t = _timed(_gd_call(M, N, K, s, bn, ns, inl, y, x, weights, 0, None, None, None,
+                                None), n)
             if t < t_best:
-                best, t_best = ("dgemm", s, 1, bn), t
+                best, t_best = ("dgemm", s, 1, bn, ns, inl), t
     if best[0] != "torch" and t_best > t_torch * (1.0 - margin):
         best = ("torch",)
     _PLAN[(M, N, K)] = best
     return best
+
+
+def _gd_name(v) -> str:
+    bn, ns, inl = (tuple(v) + (0, False))[:3]
+    return f"g{bn}" + ("d" if ns >= 6 else "") + ("i" if inl else "")
 
 
 def tune_model(model, Ms: Sequence[int], log=print) -> dict:
@@ -121,7 +147,7 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
     log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, HIP kernel chosen for "
         f"{len(wins)}: " + ", ".join(
             f"M={m} {n} {c[0]} s{c[1]}" + (f"p{c[2]}" if len(c) == 3 else "") +
-            (f"g{c[3]}" if len(c) > 3 else "")
+            (_gd_name(c[3:]) if len(c) > 3 else "")
             for (m, n), c in sorted(wins.items())))
     return summary
 
@@ -158,7 +184,7 @@ def _time_unfused(M: int, model) -> float:
     return 2 * t_norm + t_silu
 
 
-def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(1, 2, 4, 8),
+def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2, 4, 8),
                verbose: bool = False, bns=(64, 128)) -> dict:
     """Pick (split-K, prefetch) for each fused-chain GEMM at each M and keep the fused chain
     for the M where it beats the unfused chain (both timed on the real cold layer weights)."""
@@ -187,24 +213,33 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(1,
             a_o = torch.empty(M, N, device=dev, dtype=dt)
             ln = model.layers[0].ln2 if N == model.layers[0].ln2.numel() else None
             best = None
+            ss_in_, ss_out_ = (None if epi == 1 else ss), (ss_o if epi == 1 else None)
+            a_o_, ln_ = (a_o if epi == 1 else None), (ln if epi == 1 else None)
             for s in splits:
-                for pf, bn in [(p_, 0) for p_ in pfs] + [(1, b_) for b_ in bns]:
-                    if (not dgemm_supported(M, N, K, s, pf, epi, bn=bn)
+                cands = [(pf, 0, 0, False) for pf in pfs] + \
+                    [(1, bn, ns, inl) for bn, ns, inl in _gd_variants(s, bns)]
+                for pf, bn, ns, inl in cands:
+                    if (not dgemm_supported(M, N, K, s, pf, epi, bn=bn, inlaunch=inl)
                             or (s > 1 and K // s < 256)):
                         continue
-                    wsp = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
-                    t = _timed(lambda i, s=s, pf=pf, bn=bn, wsp=wsp: torch.ops.akap.dgemm(
-                        out, x, ws_[i % L], wsp, 0, s, pf, None, None, None, 1e-6, epi,
-                        None if epi == 1 else ss, ss_o if epi == 1 else None,
-                        a_o if epi == 1 else None, ln if epi == 1 else None, bn), L)
+                    if bn:
+                        fn = _gd_call(M, N, K, s, bn, ns, inl, out, x, ws_, epi, ss_in_,
+                                      ss_out_, a_o_, ln_)
+                    else:
+                        wsp = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
+                        fn = (lambda i, s=s, pf=pf, wsp=wsp: torch.ops.akap.dgemm(
+                            out, x, ws_[i % L], wsp, 0, s, pf, None, None, None, 1e-6, epi,
+                            ss_in_, ss_out_, a_o_, ln_, 0))
+                    t = _timed(fn, L)
                     if best is None or t < best[0]:
-                        best = (t, s, pf, bn)
+                        best = (t, s, pf, bn, ns, inl)
             if best is None:
                 plan_m = None
                 break
-            plan_m[name] = (best[1], best[2], best[3])
+            plan_m[name] = best[1:]
             t_fused += best[0]
-            detail.append(f"{name} {best[0]:.1f}/{t_plain:.1f}")
+            detail.append(f"{name} {best[0]:.1f}/{t_plain:.1f} (s{best[1]}"
+                          + (_gd_name(best[3:]) if best[3] else f"p{best[2]}") + ")")
         if plan_m is not None and t_fused < t_unfused:
             _FUSED[M] = plan_m
         chosen[M] = (t_fused, t_unfused, plan_m)
@@ -225,12 +260,15 @@ def _time_best_plain(M: int, name: str, weights) -> float:
     c = _PLAN.get((M, N, K), ("torch",))
     n = len(weights)
     if c[0] == "dgemm":
-        ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)
-        bn = c[3] if len(c) > 3 else 0
+        if len(c) > 3 and c[3]:
+            bn, ns, inl = (tuple(c[3:]) + (0, False))[:3]
+            return _timed(_gd_call(M, N, K, c[1], bn, ns, inl, y, x, weights, 0, None, None,
+                                   None, None), n)
+        ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         return _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, c[1], c[2],
                                                      None, None, None, 1e-6, 0, None, None,
-                                                     None, None, bn), n)
+                                                     None, None, 0), n)
     if c[0] == "hip":
         ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)

@@ -27,7 +27,7 @@ _STEP_KEYS = ["input_ids", "positions", "slots", "seq_lens", "q_start", "block_t
               "tile_seq", "tile_row", "logits_idx", "temperature", "top_p", "top_k", "seeds",
               "steps"]
 _INFO_KEYS = ["is_prefill", "num_seqs", "num_tokens", "num_tiles", "num_samples",
-              "max_seq_len", "num_preempted"]
+              "max_seq_len", "num_preempted", "num_decode"]
 STOP = -1
 
 

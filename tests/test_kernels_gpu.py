@@ -597,15 +597,23 @@ def test_fused_decode_gemm_in_graph():
     assert torch.equal(y, eager)
 
 
+@pytest.mark.parametrize("ring", ["shallow", "deep", "deep-inlaunch", "shallow-inlaunch"])
 @pytest.mark.parametrize("bn", [64, 128])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K,splitk", [(1, 256, 1024, 1), (37, 1024, 2048, 2),
                                           (256, 4096, 1024, 1), (130, 1024, 768, 1),
-                                          (64, 1024, 2048, 4)])
-def test_lds_dma_decode_gemm(bn, epi, M, N, K, splitk):
-    """gdgemm.hip (global_load_lds ring) with each epilogue vs fp32 references."""
-    if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=bn):
+                                          (64, 1024, 2048, 4), (256, 1024, 3072, 8),
+                                          (200, 2048, 1024, 2), (96, 1024, 512, 4)])
+def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
+    """gdgemm.hip (global_load_lds ring) with each epilogue vs fp32 references: shallow
+    (2 blocks/CU) and deep (1 block/CU) rings, split-K reduced by the separate pass or
+    combined in-launch by the last-arriving slice (also for the SwiGLU epilogue)."""
+    inl = ring.endswith("inlaunch")
+    if inl and splitk == 1:
+        pytest.skip("in-launch combine needs split-K")
+    if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=bn, inlaunch=inl):
         pytest.skip("unsupported combination")
+    kw = dict(ns=8 if ring.startswith("deep") else 0, inlaunch=inl)
     torch.manual_seed(M + N + K + epi + bn)
     eps = 1e-6
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -613,8 +621,11 @@ def test_lds_dma_decode_gemm(bn, epi, M, N, K, splitk):
     ssi = torch.rand(M, device=DEV) * K + 1.0
     y = (x.float() @ w.float().t()) * torch.rsqrt(ssi / K + eps)[:, None]
     if epi == ops.EPI_STORE:
-        out = ops.dgemm(x, w, splitk=splitk, bn=bn, ss_in=ssi, eps=eps)
+        out = ops.dgemm(x, w, splitk=splitk, bn=bn, ss_in=ssi, eps=eps, **kw)
         _close(out, y, atol=2e-2 * y.abs().max().item())
+        if inl:  # tickets re-armed by the last arriver: a second launch reuses them
+            out2 = ops.dgemm(x, w, splitk=splitk, bn=bn, ss_in=ssi, eps=eps, **kw)
+            assert torch.equal(out, out2)
     elif epi == ops.EPI_RESNORM:
         res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
         res0 = res.clone()
@@ -622,12 +633,12 @@ def test_lds_dma_decode_gemm(bn, epi, M, N, K, splitk):
         ss = torch.zeros(M, device=DEV)
         a = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         ops.dgemm(x, w, splitk=splitk, bn=bn, out=res, epi=epi, ss_out=ss, a_out=a, ln_out=ln,
-                  ss_in=ssi, eps=eps)
+                  ss_in=ssi, eps=eps, **kw)
         want = y.to(torch.bfloat16).float() + res0.float()
         _close(res, want, atol=2e-2 * want.abs().max().item())
         _close(a, res.float() * ln.float(), atol=1e-2 * a.float().abs().max().item())
         assert torch.allclose(ss, res.float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
     else:
-        out = ops.dgemm(x, w, splitk=splitk, bn=bn, epi=epi, ss_in=ssi, eps=eps)
+        out = ops.dgemm(x, w, splitk=splitk, bn=bn, epi=epi, ss_in=ssi, eps=eps, **kw)
         want = ref.silu_and_mul(y.to(torch.bfloat16)).float()
         _close(out, want, atol=2e-2 * want.abs().max().item())
