@@ -93,6 +93,7 @@ class LLMEngine:
         self.last_prefix = (0, 0)
         self.timers = {"schedule": 0.0, "execute": 0.0, "post": 0.0}
         self._n_extra = 0  # live requests that need penalties or log-probs
+        self.last_step_mixed = False  # the last step ran decode rows beside prefill chunks
         self.rank = self.runner.ps.rank
 
     # ------------------------------------------------------------------ requests
@@ -225,6 +226,7 @@ class LLMEngine:
             info = self.sched.schedule(self.runner.host_buffers())
         if info["num_preempted"]:
             self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
+        self.last_step_mixed = bool(info["is_prefill"] and info.get("num_decode", 0))
         t1 = time.time()
         sample_pos: dict = {}
         if info["num_seqs"] == 0:

@@ -129,3 +129,31 @@ def test_fp8_kv_cache_engine_close_to_bf16():
                         prompt_ids=prompts)
     for p, o in zip(prompts, outs):
         _near_argmax(eng, p, o.output_ids, tol=0.5)
+
+
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-mixtral"])
+def test_mixed_batching_matches_prefill_first(model):
+    """Requests arriving while others decode: mixed steps (decode rows + prefill chunks in one
+    forward) give the same greedy tokens as the prefill-first policy."""
+    outs = {}
+    for mixed in (True, False):
+        eng = _engine(model, mixed_batching=mixed)
+        sp = SamplingParams(max_tokens=6, temperature=0, ignore_eos=True)
+        eng.add_request("a", None, sp, prompt_ids=list(range(5, 45)))
+        got, saw_mixed = {}, False
+        for step in range(200):
+            if step == 2:
+                eng.add_request("b", None, sp, prompt_ids=[9, 8, 7] * 15)
+            if step == 3:
+                eng.add_request("c", None, sp, prompt_ids=list(range(60, 70)))
+            info_before = eng.steps
+            for o in eng.step():
+                if o.finished:
+                    got[o.req_id] = o.output_ids
+            saw_mixed |= eng.last_step_mixed
+            assert eng.steps == info_before + 1
+            if len(got) == 3:
+                break
+        assert saw_mixed == mixed
+        outs[mixed] = got
+    assert outs[True] == outs[False]

@@ -153,3 +153,60 @@ def test_abort():
     assert not s.abort_request(1)
     i = s.schedule(b)
     assert i["num_seqs"] == 1 and b["req_ids"][0] == 2
+
+
+def test_mixed_step_runs_decodes_first_then_prefill_chunks():
+    """Mixed batching: a running decode is scheduled in the same step as a newcomer's
+    prefill chunk (decode rows lead; the tile map covers only the prefill rows)."""
+    s, b = _sched(budget=16, bs=4, max_seqs=4, G=2)
+    s.add_request(1, list(range(10, 18)), 8)
+    i = s.schedule(b)
+    assert i["is_prefill"] == 1 and i["num_decode"] == 0 and i["num_tokens"] == 8
+    s.update(np.array([5], np.int64))
+    s.add_request(2, list(range(40, 52)), 8)
+    i = s.schedule(b)
+    assert i["is_prefill"] == 1 and i["num_decode"] == 1
+    assert i["num_seqs"] == 2 and i["num_tokens"] == 1 + 12
+    assert list(b["req_ids"][:2]) == [1, 2]  # decode row first
+    assert b["q_start"][1] == 1 and b["seq_lens"][0] == 9
+    # tiles only for the prefill sequence (index 1): 12 tokens x G=2 rows / 64 -> one tile
+    assert i["num_tiles"] == 1 and b["tile_seq"][0] == 1
+    assert i["num_samples"] == 2 and list(b["logits_idx"][:2]) == [0, 12]
+    s.update(np.array([6, 7], np.int64))
+    i = s.schedule(b)  # nothing left to prefill: a pure decode step
+    assert i["is_prefill"] == 0 and i["num_decode"] == 2 and i["num_tokens"] == 2
+
+
+def test_prefill_first_policy_still_available():
+    c = rt.SchedConfig()
+    c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 4, 16, 64
+    c.block_size, c.gqa_group, c.tile_rows, c.eos_id, c.max_blocks_per_seq = 4, 2, 64, 2, 16
+    c.mixed_batching = False
+    s, b = rt.Scheduler(c, 64, True), _bufs(4, 16, 16)
+    s.add_request(1, list(range(10, 18)), 8)
+    s.schedule(b)
+    s.update(np.array([5], np.int64))
+    s.add_request(2, list(range(40, 52)), 8)
+    i = s.schedule(b)
+    assert i["is_prefill"] == 1 and i["num_decode"] == 0 and i["num_seqs"] == 1
+
+
+def test_held_kv_expires_after_ttl():
+    """P/D prefill side: KV held for a decode engine that never pulls it is freed once its
+    TTL passes (no permanent leak), and free_held after expiry is a no-op."""
+    c = rt.SchedConfig()
+    c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 4, 32, 64
+    c.block_size, c.gqa_group, c.tile_rows, c.eos_id, c.max_blocks_per_seq = 4, 2, 64, 2, 16
+    c.held_kv_ttl_s = 30.0
+    s, b = rt.Scheduler(c, 32, False), _bufs(4, 32, 16)
+    s.add_request(7, list(range(10, 22)), 1)
+    s.set_hold_kv(7, True)
+    s.schedule(b)
+    s.update(np.array([5], np.int64))
+    assert s.num_held == 1 and len(s.held_blocks(7)) == 3
+    assert s.kv_usage() > 0
+    assert s.expire_held(rt.Scheduler.now_s()) == 0  # not yet
+    assert s.expire_held(rt.Scheduler.now_s() + 31.0) == 1
+    assert s.num_held == 0 and s.kv_usage() == 0 and s.held_expired_total == 1
+    s.free_held(7)  # late release after expiry: harmless
+    assert s.kv_usage() == 0
