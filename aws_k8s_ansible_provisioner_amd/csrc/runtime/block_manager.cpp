@@ -32,7 +32,7 @@ uint64_t BlockManager::hash_block(uint64_t parent, const int32_t* toks, int n) {
 int BlockManager::match_prefix(const std::vector<int32_t>& tokens, int max_tokens,
                                std::vector<int32_t>& blocks, std::vector<uint64_t>& hashes) {
   if (!prefix_) return 0;
-  ++queries_;
+  queries_ += max_tokens;  // token counts, like vllm:prefix_cache_{queries,hits}_total
   uint64_t parent = 0;
   int matched = 0;
   const int nfull = max_tokens / block_size_;
@@ -51,7 +51,7 @@ int BlockManager::match_prefix(const std::vector<int32_t>& tokens, int max_token
     parent = h;
     matched += block_size_;
   }
-  if (matched) ++hits_;
+  hits_ += matched;
   return matched;
 }
 

@@ -288,6 +288,9 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
   const int bs = cfg_.block_size;
   const int mb = cfg_.max_blocks_per_seq;
   std::vector<std::pair<Request*, int>> sched;  // (request, q_len)
+  // prefill chunks get the whole token budget; the decode rows of a mixed step ride along
+  // on top of it (one token each, at most max_num_seqs), so mixing never shrinks the
+  // prefill chunks (TTFT) -- the token buffers hold budget + max_num_seqs rows
   int budget = std::min(cfg_.max_num_batched_tokens, buf.cap_tokens);
 
   bool pending_prefill = !waiting_.empty();
@@ -295,7 +298,8 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     pending_prefill |= (int)r->tokens.size() - r->num_computed > 1;
   if (pending_prefill && cfg_.mixed_batching) {
     // mixed step: decodes first (they never stall behind a prefill), then prefill chunks
-    schedule_decodes(sched, info, budget);
+    int dbudget = std::max(0, std::min(cfg_.max_num_seqs, buf.cap_tokens - budget));
+    schedule_decodes(sched, info, dbudget);
     info.num_decode = (int)sched.size();
     schedule_prefills(sched, budget);
   } else if (pending_prefill) {

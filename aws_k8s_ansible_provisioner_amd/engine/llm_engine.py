@@ -42,6 +42,7 @@ class RequestState:
     stream: bool = False
     hold_kv: bool = False
     traceparent: Optional[str] = None
+    first_scheduled: Optional[float] = None
 
 
 @dataclasses.dataclass
@@ -94,6 +95,8 @@ class LLMEngine:
         self.timers = {"schedule": 0.0, "execute": 0.0, "post": 0.0}
         self._n_extra = 0  # live requests that need penalties or log-probs
         self.last_step_mixed = False  # the last step ran decode rows beside prefill chunks
+        self.pd_group: Optional[str] = None  # P/D transfer-group id (stamped into kvp)
+        self.kv_agent = None  # P/D: the KVTransferAgent (metrics only)
         self.rank = self.runner.ps.rank
 
     # ------------------------------------------------------------------ requests
@@ -173,7 +176,9 @@ class LLMEngine:
         iid = next(self._ids)
         seed = params.seed if params.seed is not None else (iid * 7919 + self.ecfg.seed)
         st = RequestState(req_id, iid, None, prompt_ids, params, time.time())
-        st.stream = stream or bool(params.stop)
+        # as in add_request: penalties / log-probs need every token on the host
+        extra = params.has_penalties or params.logprobs is not None
+        st.stream = stream or bool(params.stop) or extra
         st.first_token_time = st.arrival
         st.output_ids = [int(first_token)]
         st.text = self.tokenizer.decode_token(int(first_token)) if st.stream else ""
@@ -186,6 +191,8 @@ class LLMEngine:
             if blocks:
                 self.reqs[iid] = st
                 self.by_name[req_id] = iid
+                if extra:  # paired with the decrement on finish / abort
+                    self._n_extra += 1
         if blocks:
             self.metrics.req_total.inc(model_name=self.model_name)
         return iid, list(blocks)
@@ -227,6 +234,8 @@ class LLMEngine:
         if info["num_preempted"]:
             self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
         self.last_step_mixed = bool(info["is_prefill"] and info.get("num_decode", 0))
+        if info["is_prefill"]:  # requests are admitted only in steps with prefill rows
+            self._observe_queue_time(info, t0)
         t1 = time.time()
         sample_pos: dict = {}
         if info["num_seqs"] == 0:
@@ -320,7 +329,8 @@ class LLMEngine:
             if st.hold_kv and st.finished:
                 kvp = {"transfer_id": iid, "num_prompt": len(st.prompt_ids),
                        "prompt_token_ids": st.prompt_ids, "first_token": st.output_ids[0],
-                       "remote_rank": self.rank, "num_blocks": len(self.sched.held_blocks(iid))}
+                       "remote_rank": self.rank, "num_blocks": len(self.sched.held_blocks(iid)),
+                       "group": self.pd_group}
             outs.append(RequestOutput(st.req_id, st.prompt_ids, st.output_ids, [tok], st.text,
                                       delta, st.finished, st.finish_reason,
                                       (st.first_token_time - st.arrival)
@@ -331,6 +341,16 @@ class LLMEngine:
         self._update_gauges()
         self.timers["post"] += time.time() - now
         return outs
+
+    def _observe_queue_time(self, info: dict, t_sched: float) -> None:
+        """vllm:request_queue_time_seconds: arrival -> first scheduled (prefill rows only)."""
+        ids = self.runner.np["req_ids"]
+        for s_ in range(info.get("num_decode", 0), info["num_seqs"]):
+            st = self.reqs.get(int(ids[s_]))
+            if st is not None and st.first_scheduled is None:
+                st.first_scheduled = t_sched
+                self.metrics.queue.observe(max(0.0, t_sched - st.arrival),
+                                           model_name=self.model_name)
 
     def _step_extras(self, info: dict):
         """Penalty COO + log-prob flag for the sampled rows of this step (host side; only
@@ -380,6 +400,16 @@ class LLMEngine:
         m.waiting.set(self.sched.num_waiting, model_name=name)
         m.active.set(self.sched.num_running + self.sched.num_waiting, model_name=name)
         m.kv_usage.set(self.sched.kv_usage(), model_name=name)
+        hits, queries = self.sched.prefix_stats()
+        m.prefix_hits.set_total(hits, model_name=name)
+        m.prefix_queries.set_total(queries, model_name=name)
+        m.kv_held.set(self.sched.num_held, model_name=name)
+        m.kv_held_expired.set_total(self.sched.held_expired_total, model_name=name)
+        agent = self.kv_agent
+        if agent is not None:
+            m.kv_xfer_fail.set_total(agent.failures, model_name=name)
+            m.kv_xfer_bytes.set_total(agent.bytes_sent, model_name=name, direction="send")
+            m.kv_xfer_bytes.set_total(agent.bytes_recv, model_name=name, direction="recv")
 
     # ------------------------------------------------------------------ offline API
     def generate(self, prompts: Iterable, params: Optional[SamplingParams] = None,

@@ -62,7 +62,8 @@ class ModelRunner:
         self.max_blocks = math.ceil(ecfg.max_model_len / self.bs)
         self.G = self.model.hq // self.model.hkv
         self.max_seqs = ecfg.max_num_seqs
-        self.cap_tokens = max(ecfg.max_num_batched_tokens, self.max_seqs)
+        # a mixed step holds a full prefill token budget plus one decode row per sequence
+        self.cap_tokens = ecfg.max_num_batched_tokens + self.max_seqs
         # prefill tile map granularity: 128 flattened q rows per workgroup for the flash-style
         # GPU kernel (AKAP_PREFILL_FA=0: the 64-row per-wave kernel)
         self.tile_rows = 128 if (dev == "cuda" and

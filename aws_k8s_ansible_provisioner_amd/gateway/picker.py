@@ -11,7 +11,10 @@ hashes (same chained-hash scheme as the engine's prefix cache, computed on the p
 text in fixed-size character blocks), so routing is cache-aware without asking pods.
 
 Disaggregated prefill/decode: with both roles present and a prompt of at least
-`pd_threshold` characters, `pick_pd` returns a (prefill, decode) pair.
+`pd_threshold` characters, `pick_pd` returns a (prefill, decode) pair.  A prefill and a decode
+endpoint can only be paired inside one P/D transfer group (the torch.distributed / RCCL group
+their processes share -- in the `pd` preset, the two processes of one pod), so every endpoint
+carries a `group` and the pair is the best-scoring (prefill + decode) within a group.
 """
 from __future__ import annotations
 
@@ -28,6 +31,7 @@ from typing import Optional
 class Endpoint:
     url: str
     role: str = "both"  # both | prefill | decode
+    group: str = ""     # P/D transfer group (prefill and decode pair only within one)
     healthy: bool = True
     running: float = 0.0
     waiting: float = 0.0
@@ -101,12 +105,17 @@ class EndpointPicker:
         self.lock = threading.Lock()
 
     # ---------------------------------------------------------------- membership
-    def set_endpoints(self, urls_roles: list[tuple[str, str]]) -> None:
+    def set_endpoints(self, urls_roles: list[tuple]) -> None:
+        """(url, role) or (url, role, group); the default group is the URL's host (the two
+        P/D processes of one pod share its IP)."""
         with self.lock:
             keep = {}
-            for url, role in urls_roles:
-                keep[url] = self.eps.get(url) or Endpoint(url, role)
+            for item in urls_roles:
+                url, role = item[0], item[1]
+                group = item[2] if len(item) > 2 and item[2] else default_group(url)
+                keep[url] = self.eps.get(url) or Endpoint(url, role, group)
                 keep[url].role = role
+                keep[url].group = group
             self.eps = keep
 
     def endpoints(self) -> list[Endpoint]:
@@ -163,14 +172,39 @@ class EndpointPicker:
         chosen.served += 1
         return chosen
 
-    def pick_pd(self, prompt_text: str) -> tuple[Optional[Endpoint], Optional[Endpoint]]:
+    def pick_pd(self, prompt_text: str, pd_ok: bool = True
+                ) -> tuple[Optional[Endpoint], Optional[Endpoint]]:
         """(prefill, decode) for disaggregated serving, or (None, endpoint) when the
-        request should run monolithically (short prompt or no P/D pool)."""
-        has_p = any(e.role == "prefill" and e.healthy for e in self.eps.values())
-        has_d = any(e.role == "decode" and e.healthy for e in self.eps.values())
-        if has_p and has_d and len(prompt_text) >= self.cfg.pd_threshold_chars:
-            return self.pick(prompt_text, ("prefill",)), self.pick(prompt_text, ("decode",))
+        request should run monolithically (short prompt, n > 1 / several prompts, or no
+        transfer group with a healthy prefill AND decode endpoint)."""
+        if pd_ok and len(prompt_text) >= self.cfg.pd_threshold_chars:
+            pre = self._candidates(("prefill",))
+            dec = self._candidates(("decode",))
+            if pre and dec:
+                hs = prefix_hashes(prompt_text, self.cfg.block_chars)
+                match = self.prefix.match(hs)
+                best, best_s = None, -1e30
+                for p in pre:
+                    for d in dec:
+                        if p.group != d.group:
+                            continue
+                        s = self.score(p, match, len(hs)) + self.score(d, {}, 0)
+                        if s > best_s + 1e-9 or (abs(s - best_s) <= 1e-9 and
+                                                 self.rng.random() < 0.5):
+                            best, best_s = (p, d), s
+                if best is not None:
+                    if hs:
+                        self.prefix.insert(hs, best[0].url)
+                    best[0].served += 1
+                    best[1].served += 1
+                    return best
         return None, self.pick(prompt_text, ("both", "decode"))
+
+
+def default_group(url: str) -> str:
+    from urllib.parse import urlparse
+
+    return urlparse(url).hostname or url
 
 
 def parse_prometheus(text: str) -> dict[str, float]:

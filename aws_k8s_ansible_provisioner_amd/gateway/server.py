@@ -34,12 +34,14 @@ from .picker import Endpoint, EndpointPicker, PickerConfig, parse_prometheus
 
 
 class Gateway:
-    def __init__(self, static: list[tuple[str, str]], dns: list[tuple[str, int, str]],
+    def __init__(self, static: list[tuple], dns: list[tuple[str, int, str]],
                  cfg: Optional[PickerConfig] = None, scrape_interval: float = 1.0,
                  request_timeout: float = 600.0):
+        """static: (url, role[, P/D group]) tuples; dns: (host, port, role)."""
         self.static = static
         self.dns = dns
-        self.picker = EndpointPicker([Endpoint(u, r) for u, r in static], cfg)
+        self.picker = EndpointPicker([], cfg)
+        self.picker.set_endpoints(static)
         self.scrape_interval = scrape_interval
         self.timeout = aiohttp.ClientTimeout(total=request_timeout, sock_connect=5)
         self.session: Optional[aiohttp.ClientSession] = None
@@ -50,6 +52,9 @@ class Gateway:
         self.m_lat = self.reg.add(Histogram("akap_gateway_request_seconds", "Gateway latency",
                                             LAT_BUCKETS, ("route",)))
         self.m_up = self.reg.add(Gauge("akap_gateway_endpoint_up", "Endpoint health", ("endpoint", "role")))
+        self.m_pd_fallback = self.reg.add(Counter(
+            "akap_gateway_pd_fallback_total",
+            "P/D requests served monolithically after a failed KV hand-off", ()))
         self.m_pd = self.reg.add(Counter("akap_gateway_pd_requests_total",
                                          "Requests served disaggregated", ()))
 
@@ -74,7 +79,8 @@ class Gateway:
             try:
                 infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
                 for ip in sorted({i[4][0] for i in infos}):
-                    found.append((f"http://{ip}:{port}", role))
+                    # pod IP = P/D group: a pod's prefill (:8000) and decode (:8001) ranks
+                    found.append((f"http://{ip}:{port}", role, ip))
             except OSError:
                 pass
         self.picker.set_endpoints(found)
@@ -156,8 +162,13 @@ class Gateway:
         text = self._prompt_text(body)
         headers = {"traceparent": span.traceparent}
         tried: set[str] = set()
+        # P/D hands ONE prefilled sequence to the decode pod: single prompt, n == 1
+        p_ = body.get("prompt")
+        pd_ok = (body.get("n") in (None, 1) and
+                 not (isinstance(p_, list) and p_ and not isinstance(p_[0], int)))
+        orig = body
         for attempt in range(2):
-            pre, dec = self.picker.pick_pd(text)
+            pre, dec = self.picker.pick_pd(text, pd_ok)
             if dec is None or dec.url in tried:
                 cands = [e for e in self.picker.endpoints() if e.healthy and e.url not in tried
                          and e.role in ("both", "decode")]
@@ -167,11 +178,20 @@ class Gateway:
             span.attributes["akap.endpoint"] = dec.url
             span.attributes["akap.attempt"] = attempt
             try:
+                body = orig
                 if pre is not None:
                     span.attributes["akap.prefill_endpoint"] = pre.url
-                    body = await self._prefill_remote(pre, path, body, headers)
+                    body = await self._prefill_remote(pre, path, orig, headers)
                     self.m_pd.inc()
                 resp = await self._forward(request, dec, path, body, stream, headers)
+                if (pre is not None and resp.status >= 500 and attempt == 0
+                        and isinstance(resp, web.Response)):
+                    # KV hand-off failed on the decode pod (it released the prefill's held
+                    # KV): serve this request monolithically instead
+                    self.m_pd_fallback.inc()
+                    pd_ok = False
+                    body = orig
+                    resp = await self._forward(request, dec, path, orig, stream, headers)
                 self.m_req.inc(endpoint=dec.url, code=str(resp.status), route=path)
                 self.m_lat.observe(time.time() - t0, route=path)
                 return resp
@@ -243,13 +263,15 @@ class Gateway:
         return app
 
 
-def _parse_targets(spec: str) -> list[tuple[str, str]]:
+def _parse_targets(spec: str) -> list[tuple[str, str, str]]:
+    """url[@role[:group]],...  (group: P/D transfer group; default the URL's host)."""
     out = []
     for item in filter(None, (s.strip() for s in spec.split(","))):
-        url, _, role = item.partition("@")
+        url, _, rg = item.partition("@")
+        role, _, group = rg.partition(":")
         if "://" not in url:
             url = "http://" + url
-        out.append((url.rstrip("/"), role or "both"))
+        out.append((url.rstrip("/"), role or "both", group))
     return out
 
 

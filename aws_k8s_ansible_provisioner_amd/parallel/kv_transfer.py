@@ -1,24 +1,36 @@
 """KV-cache hand-off between a prefill engine and a decode engine (disaggregated P/D).
 
 MI355X design: the prefill and decode engines are two processes (two GPUs of the same
-xGMI mesh) in one torch.distributed group (RCCL).  A request's KV cache -- all layers,
-K and V, only its own blocks -- is packed by the `kv_gather` HIP kernel into ONE
-contiguous buffer [2L, nblk, block_elems] and moved with a single RCCL send/recv (one
-large P2P transfer per request instead of 2*L*nblk small ones), then unpacked into the
-decode engine's own block ids by `kv_scatter`.  Transfers run on a dedicated stream and
-thread on each side, so they overlap both engines' compute.
+xGMI mesh) in one torch.distributed group (RCCL).  The KV cache of a BATCH of requests --
+all layers, K and V, only their own blocks -- is packed by the `kv_gather` HIP kernel into ONE
+contiguous buffer [2L, nblk, block_elems] and moved with a single RCCL send/recv (one large
+P2P transfer instead of 2*L*nblk small ones, and one per batch of requests finished in the
+same prefill step instead of one per request), then unpacked into the decode engine's own
+block ids by `kv_scatter`.  Transfers run on a dedicated stream and thread on each side, so
+they overlap both engines' compute.
 
 For Llama-3-8B (32 layers, 8 kv heads x 128, bf16) a 2048-token prompt is 256 MiB of KV:
 ~2 ms over one xGMI link pair.
 
+Failure handling (a peer that dies or never posts its half must not hang the other):
+every send/recv is posted asynchronously (isend/irecv) and waited with a deadline
+(`timeout_s`, default AKAP_KV_TIMEOUT_S = 60).  On expiry the transfer raises
+KVTransferTimeout and the agent is marked broken: an un-matched P2P op may still be posted in
+the communicator, so later transfers on this channel fail fast (the engines keep serving;
+the gateway falls back to monolithic serving) instead of pairing with stale ops.  A send's
+`on_done` (the prefill side's free_held) runs whether the send succeeded or not.
+
 Control plane: the decode side asks the prefill server (HTTP POST /kv/push) to send the
-blocks of `transfer_id` to its rank, then posts the matching recv.  The same code runs on
-CPU with the gloo backend (tests).
+blocks of one or more transfer ids to its rank, then posts the matching recv.  The same
+code runs on CPU with the gloo backend (tests).
 """
 from __future__ import annotations
 
+import datetime
+import os
 import queue
 import threading
+import time
 from typing import Callable, Optional
 
 import torch
@@ -26,9 +38,41 @@ import torch.distributed as dist
 
 from .. import ops
 
+DEFAULT_TIMEOUT_S = float(os.environ.get("AKAP_KV_TIMEOUT_S", "60"))
+
+
+class KVTransferTimeout(TimeoutError):
+    pass
+
+
+class KVChannelBroken(RuntimeError):
+    pass
+
+
+def _wait(work, timeout_s: float, what: str, gloo: bool) -> None:
+    """Bounded wait on an async P2P op.  gloo: its send/recv work completes inside wait(),
+    which takes the deadline itself.  RCCL: poll the op's completion event against the
+    deadline (wait() would only order the op on the current stream)."""
+    if gloo:
+        try:
+            work.wait(datetime.timedelta(seconds=timeout_s))
+        except RuntimeError as e:
+            if "imed out" in str(e) or "imeout" in str(e):
+                raise KVTransferTimeout(f"{what} did not complete within {timeout_s:.1f}s")
+            raise
+        return
+    deadline = time.monotonic() + timeout_s
+    sleep = 0.0001
+    while not work.is_completed():
+        if time.monotonic() > deadline:
+            raise KVTransferTimeout(f"{what} did not complete within {timeout_s:.1f}s")
+        time.sleep(sleep)
+        sleep = min(sleep * 2, 0.005)
+    work.wait()  # surfaces a failed op (raises) and orders the op on the current stream
+
 
 class KVTransferAgent:
-    def __init__(self, kv_cache: torch.Tensor, group=None):
+    def __init__(self, kv_cache: torch.Tensor, group=None, timeout_s: float = DEFAULT_TIMEOUT_S):
         """kv_cache: the engine's [L, 2, NB, block_elems] cache tensor (bf16, or uint8 fp8
         bytes -- moved as bf16 pairs: the copy kernels are dtype-agnostic 16-byte moves)."""
         if kv_cache.dtype == torch.uint8:
@@ -38,6 +82,7 @@ class KVTransferAgent:
         self.planes = kv_cache.view(L * two, NB, be)
         self.block_elems = be
         self.group = group
+        self.timeout_s = timeout_s
         self.device = kv_cache.device
         self.is_gpu = self.device.type == "cuda"
         self.stream = torch.cuda.Stream(device=self.device) if self.is_gpu else None
@@ -46,10 +91,13 @@ class KVTransferAgent:
         self._thread.start()
         self.bytes_sent = 0
         self.bytes_recv = 0
+        self.transfers = 0
+        self.failures = 0
+        self.broken: Optional[str] = None
         # gloo moves host tensors only: GPU caches on a gloo group (single-GPU rehearsal of
         # the P/D path) stage through pinned host memory
-        self.host_staging = self.is_gpu and dist.is_initialized() and \
-            dist.get_backend(group) == "gloo"
+        self.gloo = dist.is_initialized() and dist.get_backend(group) == "gloo"
+        self.host_staging = self.is_gpu and self.gloo
 
     def nbytes(self, nblk: int) -> int:
         return self.planes.shape[0] * nblk * self.block_elems * self.kv.element_size()
@@ -74,6 +122,7 @@ class KVTransferAgent:
             box["res"], box["err"] = res, err
             ev.set()
 
+        ev.box = box  # type: ignore[attr-defined]
         self._q.put((fn, done))
         if not wait:
             return ev
@@ -82,52 +131,85 @@ class KVTransferAgent:
             raise box["err"]
         return box.get("res")
 
+    def _check(self) -> None:
+        if self.broken is not None:
+            raise KVChannelBroken(f"KV channel broken: {self.broken}")
+
+    def _fail(self, e: BaseException) -> None:
+        self.failures += 1
+        if isinstance(e, KVTransferTimeout):
+            self.broken = str(e)
+
     # ---------------------------------------------------------------- ops
     def _ctx(self):
         return torch.cuda.stream(self.stream) if self.is_gpu else _Null()
 
     def send_blocks(self, block_ids: list[int], dst: int,
-                    on_done: Optional[Callable[[], None]] = None, wait: bool = False):
-        """Pack the blocks and send them to rank `dst` (async by default)."""
+                    on_done: Optional[Callable[[], None]] = None, wait: bool = False,
+                    timeout_s: Optional[float] = None):
+        """Pack the blocks (one request's, or several requests' concatenated) and send them
+        to rank `dst` (async by default).  `on_done` always runs once the send ended --
+        successfully or not -- so the sender's held blocks are never leaked."""
+        t_out = self.timeout_s if timeout_s is None else timeout_s
 
         def fn():
-            with self._ctx():
-                ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
-                buf = ops.kv_gather(self.planes, ids)
-                if self.host_staging:
-                    self.stream.synchronize()
-                    dist.send(buf.cpu(), dst, group=self.group)
-                else:
-                    dist.send(buf, dst, group=self.group)
-                if self.is_gpu:
-                    self.stream.synchronize()
-            self.bytes_sent += buf.numel() * buf.element_size()
-            if on_done:
-                on_done()
-            return True
+            try:
+                self._check()
+                with self._ctx():
+                    ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
+                    buf = ops.kv_gather(self.planes, ids)
+                    if self.host_staging or not self.is_gpu:
+                        if self.is_gpu:
+                            self.stream.synchronize()
+                        buf = buf.cpu() if self.is_gpu else buf
+                    work = dist.isend(buf, dst, group=self.group)
+                    _wait(work, t_out, f"KV send of {len(block_ids)} blocks to rank {dst}",
+                          self.gloo)
+                    if self.is_gpu:
+                        self.stream.synchronize()
+                self.bytes_sent += buf.numel() * buf.element_size()
+                self.transfers += 1
+                return True
+            except Exception as e:
+                self._fail(e)
+                print(f"[kv-transfer] send to rank {dst} failed: {e}", flush=True)
+                raise
+            finally:
+                if on_done:
+                    on_done()
 
         return self._submit(fn, wait)
 
-    def recv_blocks(self, block_ids: list[int], src: int) -> None:
-        """Receive a packed request KV from rank `src` into our `block_ids` (blocking)."""
+    def recv_blocks(self, block_ids: list[int], src: int,
+                    timeout_s: Optional[float] = None) -> None:
+        """Receive packed KV from rank `src` into our `block_ids` (blocking, bounded)."""
+        t_out = self.timeout_s if timeout_s is None else timeout_s
 
         def fn():
-            with self._ctx():
-                n = len(block_ids)
-                buf = torch.empty(self.planes.shape[0], n, self.block_elems, dtype=self.kv.dtype,
-                                  device=self.device)
-                if self.host_staging:
-                    hb = torch.empty(buf.shape, dtype=buf.dtype)
-                    dist.recv(hb, src, group=self.group)
-                    buf.copy_(hb)
-                else:
-                    dist.recv(buf, src, group=self.group)
-                ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
-                ops.kv_scatter(buf, self.planes, ids)
-                if self.is_gpu:
-                    self.stream.synchronize()
-            self.bytes_recv += buf.numel() * buf.element_size()
-            return True
+            try:
+                self._check()
+                with self._ctx():
+                    n = len(block_ids)
+                    buf = torch.empty(self.planes.shape[0], n, self.block_elems,
+                                      dtype=self.kv.dtype, device=self.device)
+                    if self.host_staging:
+                        hb = torch.empty(buf.shape, dtype=buf.dtype)
+                        _wait(dist.irecv(hb, src, group=self.group), t_out,
+                              f"KV recv of {n} blocks from rank {src}", True)
+                        buf.copy_(hb)
+                    else:
+                        _wait(dist.irecv(buf, src, group=self.group), t_out,
+                              f"KV recv of {n} blocks from rank {src}", self.gloo)
+                    ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
+                    ops.kv_scatter(buf, self.planes, ids)
+                    if self.is_gpu:
+                        self.stream.synchronize()
+                self.bytes_recv += buf.numel() * buf.element_size()
+                self.transfers += 1
+                return True
+            except Exception as e:
+                self._fail(e)
+                raise
 
         return self._submit(fn, True)
 

@@ -2,12 +2,14 @@
 `pd` deployment preset driven directly, for `bench.py --mode pd` and tests.
 
 Ranks [0, W/2) are prefill engines, ranks [W/2, W) decode engines; prefill rank i feeds
-decode rank i + W/2.  Per request:
-  prefill rank: prefill + first token (KV held in its pool, `hold_kv`) -> metadata message
-                on a gloo control group -> `KVTransferAgent.send_blocks` (kv_gather + one
-                RCCL send over xGMI) -> its blocks are freed when the send completes;
-  decode rank:  metadata -> `reserve_prefilled` (blocks + first token) -> `recv_blocks`
-                (one RCCL recv + kv_scatter) -> `activate` -> continuous-batching decode.
+decode rank i + W/2.  Per prefill STEP (every request whose prefill finished in it):
+  prefill rank: prefill + first token (KV held in its pool, `hold_kv`) -> ONE metadata
+                message for the step's requests on a gloo control group -> ONE
+                `KVTransferAgent.send_blocks` of all their blocks (kv_gather + one RCCL send
+                over xGMI) -> the blocks are freed when the send ends;
+  decode rank:  metadata -> `reserve_prefilled` per request -> ONE `recv_blocks` of the
+                concatenated block lists (one RCCL recv + kv_scatter) -> `activate` each ->
+                continuous-batching decode.
 Metadata and KV go in the same order on both sides, so the RCCL sends and recvs pair up.
 
 TTFT is taken on the decode side (when the request becomes decodable with its first
@@ -55,6 +57,7 @@ class PDPair:
         self.peer = rank + world // 2 if self.is_prefill else rank - world // 2
         self.ctrl = ctrl_group
         self.agent = KVTransferAgent(engine.runner.kv, group=data_group)
+        self.batches = 0
 
     # ------------------------------------------------------------------ prefill side
     def run_prefill(self, prompts: list[list[int]], params: SamplingParams) -> dict:
@@ -65,22 +68,27 @@ class PDPair:
         pending = []
         sent = 0
         while eng.has_unfinished():
-            for o in eng.step():
-                if not o.finished or not o.kv_transfer_params:
-                    continue
-                kvp = o.kv_transfer_params
-                tid = int(kvp["transfer_id"])
-                blocks = eng.held_blocks(tid)
-                msg = np.array([tid, len(o.prompt_ids), int(o.output_ids[0]), len(blocks)]
-                               + list(o.prompt_ids), dtype=np.int64)
-                _send_msg(msg, self.peer, self.ctrl)
-                pending.append(self.agent.send_blocks(
-                    blocks, self.peer, on_done=lambda t=tid: eng.free_held(t), wait=False))
-                sent += 1
+            batch = [o for o in eng.step() if o.finished and o.kv_transfer_params]
+            if not batch:
+                continue
+            msg, tids, blocks = [len(batch)], [], []
+            for o in batch:
+                tid = int(o.kv_transfer_params["transfer_id"])
+                b = eng.held_blocks(tid)
+                msg += [tid, len(o.prompt_ids), int(o.output_ids[0]), len(b)] + list(o.prompt_ids)
+                tids.append(tid)
+                blocks += b
+            _send_msg(np.array(msg, dtype=np.int64), self.peer, self.ctrl)
+            pending.append(self.agent.send_blocks(
+                blocks, self.peer, on_done=lambda ts=tuple(tids): [eng.free_held(t) for t in ts],
+                wait=False))
+            sent += len(batch)
         _send_msg(np.array([_END], dtype=np.int64), self.peer, self.ctrl)
         for ev in pending:
             ev.wait()
-        return {"requests": len(names), "sent": sent}
+            if ev.box.get("err") is not None:
+                raise ev.box["err"]
+        return {"requests": len(names), "sent": sent, "transfers": len(pending)}
 
     # ------------------------------------------------------------------ decode side
     def run_decode(self, params: SamplingParams, t0: Optional[float] = None) -> dict:
@@ -97,16 +105,23 @@ class PDPair:
                     msg = _recv_msg(self.peer, self.ctrl)
                     if msg[0] == _END:
                         return
-                    tid, n_prompt, first, nblk = (int(x) for x in msg[:4])
-                    prompt = [int(x) for x in msg[4:4 + n_prompt]]
-                    iid, blocks = eng.reserve_prefilled(f"pd-{self.rank}-{k}", prompt, first,
-                                                        params)
-                    if len(blocks) != nblk:
-                        raise RuntimeError(f"decode pool short: {len(blocks)} vs {nblk} blocks")
-                    self.agent.recv_blocks(blocks, self.peer)
-                    eng.activate(iid)
-                    ttft.append(time.time() - t0)
-                    k += 1
+                    off, reserved = 1, []
+                    for _ in range(int(msg[0])):
+                        tid, n_prompt, first, nblk = (int(x) for x in msg[off:off + 4])
+                        prompt = [int(x) for x in msg[off + 4:off + 4 + n_prompt]]
+                        off += 4 + n_prompt
+                        iid, blocks = eng.reserve_prefilled(f"pd-{self.rank}-{k}", prompt,
+                                                            first, params)
+                        if len(blocks) != nblk:
+                            raise RuntimeError(f"decode pool short: {len(blocks)} vs {nblk} "
+                                               "blocks")
+                        reserved.append((iid, blocks))
+                        k += 1
+                    self.agent.recv_blocks([b for _, bl in reserved for b in bl], self.peer)
+                    for iid, _ in reserved:
+                        eng.activate(iid)
+                        ttft.append(time.time() - t0)
+                    self.batches += 1
             except BaseException as e:  # surfaced to the caller
                 errors.append(e)
             finally:

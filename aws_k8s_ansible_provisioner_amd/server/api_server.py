@@ -123,6 +123,25 @@ class OpenAIServer:
             final = o
         return final
 
+    def _pd_guard(self, body: dict, n_jobs: int) -> Optional[JSONResponse]:
+        """P/D decode: one pulled transfer feeds exactly one sequence."""
+        kvp = body.get("kv_transfer_params")
+        if kvp and "transfer_id" in kvp and n_jobs != 1:
+            AsyncEngine._release_remote(kvp)
+            return _err(400, "P/D decode takes a single prompt with n=1")
+        return None
+
+    def _attach_kvp(self, resp: dict, outs: list) -> None:
+        """P/D prefill: one decode engine pulls ONE transfer per response (the gateway sends
+        n=1 single-prompt requests through P/D); the held KV of any further choice / prompt
+        is freed now instead of waiting for its TTL."""
+        kvps = [o.kv_transfer_params for o in outs if o is not None and o.kv_transfer_params]
+        if not kvps:
+            return
+        resp["kv_transfer_params"] = kvps[0]
+        for k in kvps[1:]:
+            self.ae.engine.free_held(int(k["transfer_id"]))
+
     # ------------------------------------------------------------------ routes
     def _build(self) -> FastAPI:
         @contextlib.asynccontextmanager
@@ -180,17 +199,46 @@ class OpenAIServer:
 
         @app.post("/kv/push")
         async def kv_push(req: Request):
-            """P/D prefill side: send a held request's KV to the decode rank."""
+            """P/D prefill side: send the held KV of one or more transfers to the decode rank
+            as ONE packed RCCL send (the decode side posts one matching recv)."""
             body = await req.json()
             if self.ae.kv_agent is None:
                 return _err(400, "not a P/D prefill server")
-            tid = int(body["transfer_id"])
-            blocks = eng.held_blocks(tid)
-            if not blocks:
-                return _err(404, f"no held KV for transfer {tid}")
-            self.ae.kv_agent.send_blocks(blocks, int(body["dst_rank"]),
-                                         on_done=lambda: eng.free_held(tid))
-            return {"ok": True, "num_blocks": len(blocks)}
+            grp = body.get("group")
+            if grp is not None and self.ae.pd_group is not None and grp != self.ae.pd_group:
+                return _err(409, f"P/D group mismatch: decode {grp} vs prefill "
+                                 f"{self.ae.pd_group}", "Conflict")
+            tids = [int(t) for t in (body.get("transfer_ids") or [body["transfer_id"]])]
+            per = [eng.held_blocks(t) for t in tids]
+            missing = [t for t, b in zip(tids, per) if not b]
+            if missing:
+                return _err(404, f"no held KV for transfer(s) {missing}")
+            blocks = [b for bl in per for b in bl]
+            if os.environ.get("AKAP_FAULT_KV_PUSH") == "drop":
+                # fault injection (tests): acknowledge the push, then "die" before sending --
+                # the decode side's bounded recv must fail the request, not hang
+                for t in tids:
+                    eng.free_held(t)
+                return {"ok": True, "num_blocks": [len(b) for b in per]
+                        if "transfer_ids" in body else len(per[0])}
+
+            def done(ts=tuple(tids)):
+                for t in ts:
+                    eng.free_held(t)
+
+            self.ae.kv_agent.send_blocks(blocks, int(body["dst_rank"]), on_done=done)
+            nb = [len(b) for b in per]
+            return {"ok": True, "num_blocks": nb if "transfer_ids" in body else nb[0]}
+
+        @app.post("/kv/release")
+        async def kv_release(req: Request):
+            """P/D prefill side: the decode side will not pull these transfers (first token
+            ended the request, decode failure, retry): free their held KV now."""
+            body = await req.json()
+            tids = [int(t) for t in (body.get("transfer_ids") or [body["transfer_id"]])]
+            for t in tids:
+                eng.free_held(t)
+            return {"ok": True, "released": len(tids)}
 
         @app.post("/v1/completions")
         async def completions(req: Request):
@@ -206,6 +254,9 @@ class OpenAIServer:
                 prompts = _prompts_of(body.get("prompt", ""))
             except (ValueError, TypeError) as e:
                 return _err(400, str(e))
+            bad = self._pd_guard(body, len(prompts) * sp.n)
+            if bad:
+                return bad
             cid = f"cmpl-{uuid.uuid4().hex}"
             created = int(time.time())
             tp = req.headers.get("traceparent")
@@ -248,8 +299,7 @@ class OpenAIServer:
                     "model": self.name, "choices": choices,
                     "usage": {"prompt_tokens": ptok, "completion_tokens": ctok,
                               "total_tokens": ptok + ctok}}
-            if outs and outs[0].kv_transfer_params:
-                resp["kv_transfer_params"] = outs[0].kv_transfer_params
+            self._attach_kvp(resp, outs)
             return resp
 
         @app.post("/v1/chat/completions")
@@ -275,6 +325,9 @@ class OpenAIServer:
                 sp = _sampling_from(body, default_max=max(16, self.max_model_len // 4))
             except Exception as e:
                 return _err(400, f"chat template error: {e}")
+            bad = self._pd_guard(body, sp.n)
+            if bad:
+                return bad
             cid = f"chatcmpl-{uuid.uuid4().hex}"
             created = int(time.time())
             tp = req.headers.get("traceparent")
@@ -305,8 +358,7 @@ class OpenAIServer:
                     "model": self.name, "choices": choices,
                     "usage": {"prompt_tokens": ptok, "completion_tokens": ctok,
                               "total_tokens": ptok + ctok}}
-            if outs and outs[0].kv_transfer_params:
-                resp["kv_transfer_params"] = outs[0].kv_transfer_params
+            self._attach_kvp(resp, outs)
             return resp
 
         return app
@@ -404,6 +456,20 @@ def engine_config_from_args(a) -> EngineConfig:
         chat_template=a.chat_template, kv_role=a.kv_role, kv_cache_dtype=a.kv_cache_dtype)
 
 
+def pd_group_id() -> str:
+    """Identity of this process's P/D transfer group (the torch.distributed group shared by a
+    prefill and a decode rank): AKAP_PD_GROUP, else host + rendezvous port.  The prefill side
+    stamps it into kv_transfer_params; the decode side refuses a transfer from another group
+    (its RCCL send could never pair with our recv) instead of hanging."""
+    g = os.environ.get("AKAP_PD_GROUP")
+    if g:
+        return g
+    import socket
+
+    return f"{socket.gethostname()}:{os.environ.get('MASTER_ADDR', '')}:" \
+           f"{os.environ.get('MASTER_PORT', '')}"
+
+
 def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:
     from ..engine.llm_engine import LLMEngine
 
@@ -413,6 +479,8 @@ def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:
         from ..parallel.kv_transfer import KVTransferAgent
 
         ae.kv_agent = KVTransferAgent(eng.runner.kv)
+        ae.pd_group = eng.pd_group = pd_group_id()
+        eng.kv_agent = ae.kv_agent
     srv = OpenAIServer(ae, eng.model_name, ecfg.chat_template, ecfg.max_model_len)
     return srv.app, ae
 

@@ -8,7 +8,9 @@ thread parks on an Event, so an idle pod burns no CPU.
 from __future__ import annotations
 
 import asyncio
+import dataclasses
 import json
+import queue
 import threading
 import urllib.request
 import time
@@ -29,6 +31,107 @@ class KVTransferError(RuntimeError):
     request; the gateway may retry it monolithically."""
 
 
+@dataclasses.dataclass
+class PullJob:
+    req_id: str
+    prompt_ids: list
+    first: int
+    params: SamplingParams
+    stream: bool
+    kvp: dict
+    fut: "asyncio.Future"
+    loop: "asyncio.AbstractEventLoop"
+
+
+class KVPuller:
+    """Decode-side P/D data path.  Pulls queued at the same moment from the same prefill
+    server are coalesced: blocks are reserved for each request, ONE POST /kv/push names all
+    their transfer ids, and ONE packed RCCL recv lands every request's KV (the prefill side
+    gathers all their blocks into one send), instead of one HTTP round trip + one P2P
+    transfer per request."""
+
+    MAX_BATCH = 64
+
+    def __init__(self, ae: "AsyncEngine"):
+        self.ae = ae
+        self.q: "queue.Queue[PullJob]" = queue.Queue()
+        self.batches = 0
+        self._thread = threading.Thread(target=self._run, name="kv-puller", daemon=True)
+        self._thread.start()
+
+    def submit(self, job: PullJob) -> None:
+        self.q.put(job)
+
+    @staticmethod
+    def _resolve(job: PullJob, err: Optional[BaseException]) -> None:
+        def set_():
+            if job.fut.done():
+                return
+            if err is None:
+                job.fut.set_result(True)
+            else:
+                job.fut.set_exception(err)
+
+        job.loop.call_soon_threadsafe(set_)
+
+    def _run(self) -> None:
+        while True:
+            jobs = [self.q.get()]
+            time.sleep(0.001)  # let concurrent pulls of the same moment join the batch
+            while len(jobs) < self.MAX_BATCH:
+                try:
+                    jobs.append(self.q.get_nowait())
+                except queue.Empty:
+                    break
+            groups: dict = {}
+            for j in jobs:
+                groups.setdefault((j.kvp["remote_url"], int(j.kvp["remote_rank"])),
+                                  []).append(j)
+            for (url, rank), js in groups.items():
+                self._pull_batch(url, rank, js)
+
+    def _pull_batch(self, url: str, rank: int, jobs: list) -> None:
+        eng = self.ae.engine
+        ready, reserved = [], []
+        for j in jobs:
+            try:
+                iid, blocks = eng.reserve_prefilled(j.req_id, j.prompt_ids, j.first, j.params,
+                                                    j.stream)
+                if not blocks:
+                    raise RuntimeError("KV pool exhausted on the decode engine")
+                ready.append(j)
+                reserved.append((iid, blocks))
+            except Exception as e:
+                AsyncEngine._release_remote(j.kvp)
+                self._resolve(j, e)
+        if not ready:
+            return
+        try:
+            body = json.dumps({"transfer_ids": [int(j.kvp["transfer_id"]) for j in ready],
+                               "dst_rank": eng.rank, "group": self.ae.pd_group}).encode()
+            req = urllib.request.Request(url.rstrip("/") + "/kv/push", data=body,
+                                         headers={"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=60) as r:
+                meta = json.loads(r.read())
+            counts = [int(n) for n in meta.get("num_blocks", [])]
+            if counts != [len(b) for _, b in reserved]:
+                raise RuntimeError(f"KV block count mismatch {counts} vs "
+                                   f"{[len(b) for _, b in reserved]}")
+            all_blocks = [b for _, bl in reserved for b in bl]
+            self.ae.kv_agent.recv_blocks(all_blocks, rank)
+        except Exception as e:
+            for j, (iid, _) in zip(ready, reserved):
+                eng.abort_request(j.req_id)  # frees the reserved decode blocks
+                AsyncEngine._release_remote(j.kvp)
+                self._resolve(j, e)
+            return
+        self.batches += 1
+        for j, (iid, _) in zip(ready, reserved):
+            eng.activate(iid)
+            self._resolve(j, None)
+        self.ae._wake.set()
+
+
 class AsyncEngine:
     def __init__(self, engine: LLMEngine, step_hook=None):
         self.engine = engine
@@ -39,6 +142,8 @@ class AsyncEngine:
         self.dead: Optional[str] = None
         self.step_hook = step_hook
         self.kv_agent = None  # parallel.kv_transfer.KVTransferAgent for P/D roles
+        self.pd_group: Optional[str] = None  # P/D: id of this engine's RCCL transfer group
+        self.puller: Optional["KVPuller"] = None
         self._thread = threading.Thread(target=self._run, name="engine-loop", daemon=True)
         self.started = time.time()
 
@@ -113,44 +218,62 @@ class AsyncEngine:
 
     async def _pull_remote_kv(self, req_id: str, params: SamplingParams, stream: bool,
                               kvp: dict) -> Optional[RequestOutput]:
-        """P/D decode side: reserve blocks, ask the prefill server to push the request's
-        KV to our rank, receive it over RCCL, then let the engine decode."""
+        """P/D decode side: reserve blocks, have the prefill server push the request's KV to
+        our rank (batched with other pulls queued at the same moment), receive it over RCCL,
+        then let the engine decode.  Every exit path that does not consume the prefill's held
+        KV releases it there (/kv/release), so the prefill pod never leaks blocks."""
         eng = self.engine
         prompt_ids = [int(t) for t in kvp["prompt_token_ids"]]
         first = int(kvp["first_token"])
         sp = params.normalized()
         if (not sp.ignore_eos and first == eng.mcfg.eos_id) or sp.max_tokens <= 1:
+            # the first token already ends the request: the KV is not needed here
+            self._release_remote(kvp)
             reason = "stop" if first == eng.mcfg.eos_id else "length"
             text = "" if reason == "stop" else eng.tokenizer.decode([first])
             return RequestOutput(req_id, prompt_ids, [first], [first], text, text, True,
                                  reason)
         if self.kv_agent is None:
+            self._release_remote(kvp)
             raise RuntimeError("this server has no KV-transfer agent (start with --kv-role decode)")
+        group = kvp.get("group")
+        if group is not None and self.pd_group is not None and group != self.pd_group:
+            # prefill of another RCCL group: its send could never pair with our recv
+            self._release_remote(kvp)
+            raise KVTransferError(f"P/D group mismatch: prefill {group} vs decode "
+                                  f"{self.pd_group}")
+        if self.puller is None:
+            self.puller = KVPuller(self)
         loop = asyncio.get_running_loop()
-
-        def pull():
-            iid, blocks = eng.reserve_prefilled(req_id, prompt_ids, first, params, stream)
-            if not blocks:
-                raise RuntimeError("KV pool exhausted on the decode engine")
-            body = json.dumps({"transfer_id": kvp["transfer_id"], "dst_rank": eng.rank}).encode()
-            req = urllib.request.Request(kvp["remote_url"].rstrip("/") + "/kv/push", data=body,
-                                         headers={"Content-Type": "application/json"})
-            with urllib.request.urlopen(req, timeout=60) as r:
-                meta = json.loads(r.read())
-            if int(meta.get("num_blocks", -1)) != len(blocks):
-                raise RuntimeError(f"KV block count mismatch {meta} vs {len(blocks)}")
-            self.kv_agent.recv_blocks(blocks, int(kvp["remote_rank"]))
-            eng.activate(iid)
-
+        fut = loop.create_future()
+        self.puller.submit(PullJob(req_id, prompt_ids, first, params, stream, kvp, fut, loop))
         try:
-            await loop.run_in_executor(None, pull)
-        except (OSError, ValueError, KeyError, RuntimeError) as e:
+            await fut
+        except (OSError, ValueError, KeyError, RuntimeError, TimeoutError) as e:
             raise KVTransferError(f"KV transfer from {kvp.get('remote_url')} failed: {e}") from e
         if stream:  # the first token was produced remotely: deliver it first
             t = eng.tokenizer.decode_token(first)
             self.queues[req_id].put_nowait(RequestOutput(req_id, prompt_ids, [first], [first],
                                                          t, t, False, None))
         return None
+
+    @staticmethod
+    def _release_remote(kvp: dict) -> None:
+        """Best effort: tell the prefill server to free the held KV of this transfer."""
+        url = kvp.get("remote_url")
+        if not url or "transfer_id" not in kvp:
+            return
+
+        def go():
+            try:
+                body = json.dumps({"transfer_ids": [int(kvp["transfer_id"])]}).encode()
+                req = urllib.request.Request(url.rstrip("/") + "/kv/release", data=body,
+                                             headers={"Content-Type": "application/json"})
+                urllib.request.urlopen(req, timeout=10).read()
+            except Exception as e:  # the prefill side's TTL frees it eventually
+                print(f"[pd] /kv/release to {url} failed: {e}", flush=True)
+
+        threading.Thread(target=go, name="kv-release", daemon=True).start()
 
     async def abort(self, req_id: str) -> None:
         self.engine.abort_request(req_id)

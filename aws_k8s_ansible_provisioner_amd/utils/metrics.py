@@ -49,6 +49,11 @@ class Counter(_Metric):
             key = self._key(labels)
             self._v[key] = self._v.get(key, 0.0) + amount
 
+    def set_total(self, value: float, **labels) -> None:
+        """Mirror a monotonic total kept elsewhere (e.g. the C++ block manager's counts)."""
+        with self._lock:
+            self._v[self._key(labels)] = float(value)
+
     def value(self, **labels) -> float:
         return self._v.get(self._key(labels), 0.0)
 
@@ -167,6 +172,16 @@ class EngineMetrics:
                                      LAT_BUCKETS, L))
         self.step_time = r.add(Histogram("akap:engine_step_seconds", "Engine step wall time",
                                          LAT_BUCKETS, ("model_name", "phase")))
+        # disaggregated P/D KV hand-off
+        self.kv_held = r.add(Gauge("akap:kv_held_transfers",
+                                   "Prefill side: requests whose KV is held for a decode pull", L))
+        self.kv_held_expired = r.add(Counter("akap:kv_held_expired_total",
+                                             "Held KV freed by the TTL (never pulled)", L))
+        self.kv_xfer_fail = r.add(Counter("akap:kv_transfer_failures_total",
+                                          "KV sends/receives that failed or timed out", L))
+        self.kv_xfer_bytes = r.add(Counter("akap:kv_transfer_bytes_total",
+                                           "KV bytes moved over the transfer group",
+                                           ("model_name", "direction")))
         # aliases queried by the reference's OTel verification play
         self.req_total = r.add(Counter("vllm_request_total", "Requests received (alias)", L))
         self.active = r.add(Gauge("vllm_active_requests", "Requests in flight (alias)", L))

@@ -51,14 +51,43 @@ def test_picker_pd_pairs():
     assert pre.url == "p1" and dec.url == "d1"
     pre, dec = p.pick_pd("short")
     assert pre is None and dec.url in ("m1", "d1")
+    pre, dec = p.pick_pd("y" * 200, pd_ok=False)  # n > 1 / several prompts: monolithic
+    assert pre is None
+
+
+def test_picker_pd_pairs_only_within_a_transfer_group():
+    """Two `pd` pods behind one gateway: a prefill is never paired with the other pod's
+    decode rank (its RCCL send could not pair with that recv -> both would hang)."""
+    p = EndpointPicker([], PickerConfig(pd_threshold_chars=10), seed=3)
+    p.set_endpoints([("http://10.0.0.1:8000", "prefill"), ("http://10.0.0.1:8001", "decode"),
+                     ("http://10.0.0.2:8000", "prefill"), ("http://10.0.0.2:8001", "decode")])
+    for u in [e.url for e in p.endpoints()]:
+        p.update_metrics(u, 0, 0, 0.0)
+    seen = set()
+    for i in range(40):
+        # load one pod's decode heavily: an independent pick would mix pods
+        p.update_metrics("http://10.0.0.1:8001", running=50, waiting=20, kv=0.9)
+        pre, dec = p.pick_pd(f"{i} " + "z" * 50)
+        assert pre.group == dec.group
+        assert pre.url.split(":")[1] == dec.url.split(":")[1]
+        seen.add(pre.group)
+    assert seen == {"10.0.0.2"}  # the pair on the idle pod wins on combined score
+    # a group that lost its decode endpoint cannot serve P/D; the other group still can
+    p.mark_failure("http://10.0.0.2:8001", hard=True)
+    pre, dec = p.pick_pd("q" * 50)
+    assert pre.url == "http://10.0.0.1:8000" and dec.url == "http://10.0.0.1:8001"
+    p.mark_failure("http://10.0.0.1:8000", hard=True)
+    pre, dec = p.pick_pd("q" * 50)  # no complete group: monolithic on a decode endpoint
+    assert pre is None and dec.url == "http://10.0.0.1:8001"
 
 
 def test_parsers():
     m = parse_prometheus('# HELP x\nvllm:num_requests_running{model_name="m"} 3.0\n'
                          'vllm:num_requests_running{model_name="n"} 2\nbad line\n')
     assert m["vllm:num_requests_running"] == 5.0
-    assert _parse_targets("a:8000@prefill,http://b:9/") == [("http://a:8000", "prefill"),
-                                                            ("http://b:9", "both")]
+    assert _parse_targets("a:8000@prefill,http://b:9/,c:1@decode:g7") == [
+        ("http://a:8000", "prefill", ""), ("http://b:9", "both", ""),
+        ("http://c:1", "decode", "g7")]
     assert _parse_dns("svc.ns.svc.cluster.local:8000@decode") == [
         ("svc.ns.svc.cluster.local", 8000, "decode")]
 

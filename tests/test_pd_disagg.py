@@ -180,3 +180,146 @@ def test_pd_driver_matches_monolithic(tmp_path):
                        prompt_ids=prompts)
     for p_, o in zip(prompts, exp):
         assert got[str(len(p_))] == o.output_ids
+
+
+# ---------------------------------------------------------------------------------------------
+# P/D KV lifecycle: no held-KV leak, no cross-group pairing, bounded transfers
+# ---------------------------------------------------------------------------------------------
+def _spawn_pair(extra_env=None, decode_env=None):
+    """One prefill + one decode server process (gloo, one transfer group)."""
+    master = _port()
+    procs, urls = [], []
+    for rank, role in enumerate(["prefill", "decode"]):
+        port = _port()
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master), AKAP_DIST_BACKEND="gloo",
+                   PYTHONPATH=ROOT, **(extra_env or {}))
+        if role == "decode":
+            env.update(decode_env or {})
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "aws_k8s_ansible_provisioner_amd.server", *COMMON,
+             "--kv-role", role, "--port", str(port), "--host", "127.0.0.1"],
+            env=env, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+        urls.append(f"http://127.0.0.1:{port}")
+    deadline = time.time() + 120
+    for u in urls:
+        while True:
+            try:
+                urllib.request.urlopen(u + "/health", timeout=1)
+                break
+            except Exception:
+                if time.time() > deadline or any(p.poll() is not None for p in procs):
+                    for p in procs:
+                        p.kill()
+                    raise RuntimeError("P/D servers failed to start: " + str(
+                        [p.stderr.read().decode()[-1500:] for p in procs]))
+                time.sleep(0.2)
+    return procs, urls
+
+
+def _kill(procs):
+    for p in procs:
+        p.kill()
+        p.wait()
+
+
+def _metric(url, name):
+    for ln in urllib.request.urlopen(url + "/metrics").read().decode().splitlines():
+        if ln.startswith(name + "{") or ln.startswith(name + " "):
+            return float(ln.rsplit(" ", 1)[1])
+    raise KeyError(name)
+
+
+async def _gw_post(targets, bodies, pd_threshold=32):
+    gw = Gateway(targets, [], PickerConfig(pd_threshold_chars=pd_threshold), scrape_interval=0.2)
+    runner = web.AppRunner(gw.app())
+    await runner.setup()
+    port = _port()
+    await web.TCPSite(runner, "127.0.0.1", port).start()
+    try:
+        await asyncio.sleep(0.3)
+        out = []
+        async with aiohttp.ClientSession() as s:
+            for b in bodies:
+                async with s.post(f"http://127.0.0.1:{port}/v1/completions", json=b) as r:
+                    out.append((r.status, await r.json()))
+        return out, gw
+    finally:
+        await runner.cleanup()
+
+
+def test_pd_first_token_only_requests_do_not_leak_prefill_kv(pd_servers):
+    """max_tokens=1 (and an n=2 request) through the gateway: the decode side never pulls the
+    KV, so it must release it on the prefill pod -- kv usage returns to 0, nothing held."""
+    pre_url, dec_url = pd_servers
+    prompt = "the first token ends this request " * 4
+    bodies = [{"prompt": prompt, "max_tokens": 1, "temperature": 0},
+              {"prompt": prompt + "!", "max_tokens": 1, "temperature": 0, "ignore_eos": True},
+              {"prompt": prompt + "?", "max_tokens": 3, "n": 2, "temperature": 0,
+               "ignore_eos": True}]
+    res, gw = asyncio.run(_gw_post([(pre_url, "prefill"), (dec_url, "decode")], bodies))
+    assert [st for st, _ in res] == [200, 200, 200]
+    assert res[0][1]["usage"]["completion_tokens"] == 1
+    assert len(res[2][1]["choices"]) == 2  # n > 1 served monolithically
+    deadline = time.time() + 10
+    while time.time() < deadline:
+        if _metric(pre_url, "vllm:gpu_cache_usage_perc") == 0.0 and \
+                _metric(pre_url, "akap:kv_held_transfers") == 0.0:
+            break
+        time.sleep(0.2)
+    assert _metric(pre_url, "vllm:gpu_cache_usage_perc") == 0.0
+    assert _metric(pre_url, "akap:kv_held_transfers") == 0.0
+    assert _metric(dec_url, "vllm:gpu_cache_usage_perc") == 0.0
+
+
+def test_two_pd_pairs_behind_one_gateway_never_cross_pair():
+    """Two P/D transfer groups (4 processes) behind one gateway: every request is prefilled
+    and decoded inside one group, and all of them complete (a cross-group pairing would send
+    on one RCCL group and receive on another: both sides would hang)."""
+    pa, ua = _spawn_pair(extra_env={"AKAP_PD_GROUP": "pairA"})
+    pb, ub = _spawn_pair(extra_env={"AKAP_PD_GROUP": "pairB"})
+    try:
+        targets = [(ua[0], "prefill", "pairA"), (ua[1], "decode", "pairA"),
+                   (ub[0], "prefill", "pairB"), (ub[1], "decode", "pairB")]
+        bodies = [{"prompt": f"request {i} " + "two pods one gateway " * 3, "max_tokens": 5,
+                   "temperature": 0, "ignore_eos": True} for i in range(8)]
+        res, gw = asyncio.run(_gw_post(targets, bodies))
+        assert all(st == 200 for st, _ in res)
+        assert all(j["usage"]["completion_tokens"] == 5 for _, j in res)
+        assert gw.m_pd.value() == 8 and gw.m_pd_fallback.value() == 0
+        for u in ua + ub:
+            assert _metric(u, "vllm:gpu_cache_usage_perc") == 0.0
+        # a deliberately wrong pairing (decode of pair B told it is in pair A's group) is
+        # refused by the group check on the decode side, then served monolithically
+        res2, gw2 = asyncio.run(_gw_post([(ua[0], "prefill", "x"), (ub[1], "decode", "x")],
+                                         bodies[:1]))
+        assert res2[0][0] == 200 and res2[0][1]["usage"]["completion_tokens"] == 5
+        assert gw2.m_pd_fallback.value() == 1
+        assert _metric(ua[0], "akap:kv_held_transfers") == 0.0
+    finally:
+        _kill(pa + pb)
+
+
+def test_pd_sender_dies_after_push_ack_fails_fast_and_frees_blocks():
+    """The prefill acks /kv/push and never sends: the decode's bounded recv times out, the
+    request is served monolithically by the gateway's fallback, the decode engine frees the
+    reserved blocks, stays healthy, and its broken channel fails later pulls fast."""
+    procs, (pre_url, dec_url) = _spawn_pair(extra_env={"AKAP_FAULT_KV_PUSH": "drop"},
+                                            decode_env={"AKAP_KV_TIMEOUT_S": "2"})
+    try:
+        body = {"prompt": "sender dies after the ack " * 3, "max_tokens": 4, "temperature": 0,
+                "ignore_eos": True}
+        t0 = time.time()
+        res, gw = asyncio.run(_gw_post([(pre_url, "prefill"), (dec_url, "decode")], [body]))
+        assert res[0][0] == 200 and res[0][1]["usage"]["completion_tokens"] == 4
+        assert gw.m_pd_fallback.value() == 1
+        assert time.time() - t0 < 30
+        assert urllib.request.urlopen(dec_url + "/health").status == 200
+        assert _metric(dec_url, "vllm:gpu_cache_usage_perc") == 0.0
+        assert _metric(dec_url, "akap:kv_transfer_failures_total") >= 1
+        # the channel is now marked broken: the next P/D attempt fails immediately
+        t1 = time.time()
+        res, gw = asyncio.run(_gw_post([(pre_url, "prefill"), (dec_url, "decode")], [body]))
+        assert res[0][0] == 200 and time.time() - t1 < 10
+    finally:
+        _kill(procs)

@@ -53,7 +53,7 @@ def _sched(num_blocks=64, bs=4, max_seqs=4, budget=16, max_len=64, prefix=True, 
     c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = max_seqs, budget, max_len
     c.block_size, c.gqa_group, c.tile_rows, c.eos_id = bs, G, 64, 2
     c.max_blocks_per_seq = max_len // bs
-    return rt.Scheduler(c, num_blocks, prefix), _bufs(max_seqs, max(budget, max_seqs), max_len // bs)
+    return rt.Scheduler(c, num_blocks, prefix), _bufs(max_seqs, budget + max_seqs, max_len // bs)
 
 
 def test_chunked_prefill_then_decode_and_slots():
@@ -117,7 +117,7 @@ def test_prefix_cache_hit_on_second_request():
     assert i["num_tokens"] == 1  # 16 cached tokens, only the last prompt token computed
     assert s.request_info(2)["num_cached"] == 16
     hits, queries = s.prefix_stats()
-    assert hits == 1
+    assert hits == 16 and queries == 2 * 16  # tokens (vLLM's prefix-cache metric units)
 
 
 def test_preemption_when_pool_exhausted():
@@ -182,7 +182,7 @@ def test_prefill_first_policy_still_available():
     c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 4, 16, 64
     c.block_size, c.gqa_group, c.tile_rows, c.eos_id, c.max_blocks_per_seq = 4, 2, 64, 2, 16
     c.mixed_batching = False
-    s, b = rt.Scheduler(c, 64, True), _bufs(4, 16, 16)
+    s, b = rt.Scheduler(c, 64, True), _bufs(4, 20, 16)
     s.add_request(1, list(range(10, 18)), 8)
     s.schedule(b)
     s.update(np.array([5], np.int64))
@@ -198,7 +198,7 @@ def test_held_kv_expires_after_ttl():
     c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 4, 32, 64
     c.block_size, c.gqa_group, c.tile_rows, c.eos_id, c.max_blocks_per_seq = 4, 2, 64, 2, 16
     c.held_kv_ttl_s = 30.0
-    s, b = rt.Scheduler(c, 32, False), _bufs(4, 32, 16)
+    s, b = rt.Scheduler(c, 32, False), _bufs(4, 36, 16)
     s.add_request(7, list(range(10, 22)), 1)
     s.set_hold_kv(7, True)
     s.schedule(b)

@@ -120,3 +120,31 @@ def test_logprobs_and_penalties_in_api(client):
     assert r.status_code == 200, r.text
     content = r.json()["choices"][0]["logprobs"]["content"]
     assert len(content) == 4 and all("logprob" in c for c in content)
+
+
+def test_prefix_cache_and_queue_time_metrics_are_live():
+    """vllm:prefix_cache_{hits,queries}_total (tokens) and vllm:request_queue_time_seconds
+    are fed by the engine (they read 0 forever in round 1)."""
+    from fastapi.testclient import TestClient
+
+    from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig
+    from aws_k8s_ansible_provisioner_amd.server.api_server import build_app
+
+    app, ae = build_app(EngineConfig(model="tiny-qwen3", served_model_name="m", device="cpu",
+                                     max_model_len=256, max_num_seqs=4,
+                                     max_num_batched_tokens=64, block_size=32,
+                                     num_gpu_blocks=64))
+    prompt = list(range(10, 110))
+    with TestClient(app) as c:
+        for _ in range(2):
+            r = c.post("/v1/completions", json={"prompt": prompt, "max_tokens": 2})
+            assert r.status_code == 200
+        text = c.get("/metrics").text
+    vals = {}
+    for ln in text.splitlines():
+        if ln and not ln.startswith("#"):
+            k, v = ln.rsplit(" ", 1)
+            vals[k.split("{")[0]] = vals.get(k.split("{")[0], 0.0) + float(v)
+    assert vals["vllm:prefix_cache_queries_total"] >= 2 * 99
+    assert vals["vllm:prefix_cache_hits_total"] >= 96  # 3 full 32-token blocks reused
+    assert vals["vllm:request_queue_time_seconds_count"] == 2
