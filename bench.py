@@ -12,6 +12,11 @@ GPU -- a data-parallel replica, exactly how the gateway scales the deployment (w
 scaling: per-GPU work is fixed).  Ranks are synchronised with barriers around the K
 timed waves; value = total output tokens of all ranks / max rank wall time.
 
+--arrival-rate R: online serving instead of the t=0 burst -- requests arrive as a Poisson
+process at R req/s (streaming, so every token is timestamped) and the line also reports
+p50/p99 TTFT, TPOT (per-request mean inter-token time) and p99 inter-token latency; with
+--no-mixed-batching the prefill-first policy is measured for comparison.
+
 --mode pd (even WORLD_SIZE): disaggregated prefill/decode -- ranks [0, W/2) prefill,
 [W/2, W) decode, each request's KV moved prefill->decode with one RCCL send/recv
 (parallel/pd_driver.py); TTFT is measured on the decode side (includes the hand-off).
@@ -58,6 +63,10 @@ def parse():
                          "[W/2,W) decode, KV handed over RCCL (Llama-3-8B disagg config)")
     ap.add_argument("--dist-backend", default=None,
                     help="override (gloo = single-GPU rehearsal of the multi-rank paths)")
+    ap.add_argument("--arrival-rate", type=float, default=0.0,
+                    help="Poisson arrivals at this many requests/s (0 = all at t=0)")
+    ap.add_argument("--no-mixed-batching", action="store_true",
+                    help="prefill-first scheduling (decodes stall while a prefill runs)")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra untimed waves run after timing (for rocprofv3 captures)")
     return ap.parse_args()
@@ -106,6 +115,7 @@ def main() -> int:
                         num_gpu_blocks=None if gpu else 512,
                         kv_role=("prefill" if is_prefill else "decode") if pd else "both",
                         kv_cache_dtype=a.kv_cache_dtype,
+                        mixed_batching=not a.no_mixed_batching,
                         # ranks sharing one GPU (single-GPU gloo rehearsal) split its memory
                         gpu_memory_utilization=0.90 / max(1, shared_ranks))
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if rank == 0 else (lambda *x: None)
@@ -134,7 +144,44 @@ def main() -> int:
         ctrl = dist.new_group(backend="gloo")  # small metadata messages on the host
         pair = PDPair(eng, rank, world, ctrl_group=ctrl, data_group=None)
 
+    lat = {"itl": [], "tpot": []}
+
+    def online_wave():
+        """Poisson arrivals; every token event timestamped (streaming requests)."""
+        prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
+        gaps = rng.exponential(1.0 / a.arrival_rate, size=a.num_requests)
+        t_arr = time.time() + np.cumsum(gaps) - gaps[0]
+        last, first, ttft, ntok, i = {}, {}, [], 0, 0
+        while i < a.num_requests or eng.has_unfinished():
+            now = time.time()
+            while i < a.num_requests and t_arr[i] <= now:
+                rid = f"r{i}"
+                eng.add_request(rid, None, sp, prompt_ids=prompts[i], stream=True)
+                first[rid] = t_arr[i]
+                i += 1
+            if not eng.has_unfinished():
+                time.sleep(max(0.0, min(t_arr[i] - time.time(), 0.01)))
+                continue
+            outs = eng.step()
+            now = time.time()
+            for o in outs:
+                n = len(o.new_ids) if o.new_ids and o.new_ids[0] >= 0 else 0
+                if not n:
+                    continue
+                ntok += n
+                if o.req_id not in last:
+                    ttft.append(now - first[o.req_id])
+                    first[o.req_id] = now  # from here: first-token time
+                else:
+                    lat["itl"].append(now - last[o.req_id])
+                last[o.req_id] = now
+                if o.finished and len(o.output_ids) > 1:
+                    lat["tpot"].append((now - first[o.req_id]) / (len(o.output_ids) - 1))
+        return ntok, ttft
+
     def wave():
+        if a.arrival_rate > 0 and not pd:
+            return online_wave()
         if pd:
             if is_prefill:
                 prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
@@ -177,6 +224,9 @@ def main() -> int:
         wave()
 
     p50_local = statistics.median(ttfts) if ttfts else 0.0
+
+    def pct(xs, q):
+        return float(np.percentile(np.asarray(xs), q)) if xs else 0.0
     stats = torch.tensor([float(total), el, p50_local], dtype=torch.float64)
     if world > 1 and tp_bc is None:
         dev = torch.device("cuda", local) if gpu else torch.device("cpu")
@@ -203,7 +253,8 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "strong" if a.tp > 1 else "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            # compute dtype; an fp8 KV cache (storage only, not the headline) is named too
+            "dtype": "bf16" if a.kv_cache_dtype == "auto" else "bf16+fp8kv",
             "data": "synthetic random token-id prompts, random-init weights",
             "p50_ttft_ms": round(p50 * 1000, 2),
             "config": {
@@ -220,8 +271,17 @@ def main() -> int:
                 "sampling": "greedy" if a.temperature <= 0 else f"T={a.temperature}",
                 "hipgraph_decode": not a.enforce_eager,
                 "kv_cache_dtype": "bf16" if a.kv_cache_dtype == "auto" else "fp8_e4m3",
+                "mixed_batching": not a.no_mixed_batching,
             },
         }
+        if a.arrival_rate > 0:
+            res["arrival_rate_rps"] = a.arrival_rate
+            res["p99_ttft_ms"] = round(pct(ttfts, 99) * 1000, 2)
+            res["p50_tpot_ms"] = round(pct(lat["tpot"], 50) * 1000, 3)
+            res["p99_tpot_ms"] = round(pct(lat["tpot"], 99) * 1000, 3)
+            res["p50_itl_ms"] = round(pct(lat["itl"], 50) * 1000, 3)
+            res["p99_itl_ms"] = round(pct(lat["itl"], 99) * 1000, 3)
+            res["config"]["arrivals"] = "poisson"
         print(json.dumps(res), flush=True)
     if pair is not None:
         pair.close()
