@@ -53,12 +53,18 @@ def chat_configmaps(ns: str) -> list[str]:
 
 def render(values: dict, ns: str = "llm-d", storage_class: str = "local-path",
            storage_size: str = "50Gi", download_model: Optional[str] = None,
-           hf_token: Optional[str] = None, exporter_ns: str = "kube-amd-gpu") -> dict[str, str]:
+           hf_token: Optional[str] = None, exporter_ns: str = "kube-amd-gpu",
+           gateway_api: bool = False) -> dict[str, str]:
+    """gateway_api: also emit a Gateway API `Gateway` + `HTTPRoute` named
+    llm-d-inference-gateway in front of our gateway Service (tier 1 of the reference smoke
+    test's address lookup, llm-d-test.yaml:16); the installer turns it on when the
+    gateways.gateway.networking.k8s.io CRD exists in the cluster."""
     env = jinja2.Environment(loader=jinja2.FileSystemLoader(TEMPLATES), trim_blocks=True,
                              lstrip_blocks=True, undefined=jinja2.StrictUndefined)
     ctx = dict(v=values, ns=ns, storage_class=storage_class, storage_size=storage_size,
                download_model=download_model, hf_token=hf_token,
-               chat_configmaps=chat_configmaps(ns), exporter_ns=exporter_ns)
+               chat_configmaps=chat_configmaps(ns), exporter_ns=exporter_ns,
+               gateway_api=gateway_api)
     out = {}
     for name in ORDER:
         if name == "gpu-exporter.yaml.j2" and not values.get("gpuExporter", True):
@@ -89,8 +95,12 @@ def main(argv=None) -> int:
     ap.add_argument("--wait-timeout", default="1800s")
     a = ap.parse_args(argv)
     values = load_values(a.values_file)
+    gw_api = values.get("gatewayApi", "auto")
+    if gw_api == "auto":
+        gw_api = (not a.dry_run and shutil.which("kubectl") is not None and kubectl(
+            ["get", "crd", "gateways.gateway.networking.k8s.io"], check=False).returncode == 0)
     manifests = render(values, a.namespace, a.storage_class, a.storage_size, a.download_model,
-                       os.environ.get("HF_TOKEN") or None)
+                       os.environ.get("HF_TOKEN") or None, gateway_api=bool(gw_api))
     os.makedirs(a.output_dir, exist_ok=True)
     paths = []
     for name, text in manifests.items():

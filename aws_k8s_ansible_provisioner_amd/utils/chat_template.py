@@ -119,3 +119,35 @@ def configmap_yaml(name: str, template: str, namespace: Optional[str] = None) ->
         meta["namespace"] = namespace
     return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": meta,
             "data": {"template.jinja": template}}
+
+
+def configmap_text(name: str) -> str:
+    """The ConfigMap manifest of builtin template `name` as YAML text in the reference's
+    layout (templates/<name>-chat-template.yaml: a `|-` block scalar indented 4 spaces) --
+    for phi / opt byte-identical to the reference files (pinned by tests/test_provisioning)."""
+    body = "\n".join(("    " + ln) if ln else "" for ln in BUILTIN[name].split("\n"))
+    return ("apiVersion: v1\nkind: ConfigMap\nmetadata:\n"
+            f"  name: {configmap_name(name)}\ndata:\n  template.jinja: |-\n{body}")
+
+
+def main(argv=None) -> int:
+    """python -m aws_k8s_ansible_provisioner_amd.utils.chat_template --write-configmaps DIR
+    writes <name>-chat-template.yaml for the reference-compatible phi / opt templates (and
+    the corrected default) so `kubectl apply -f DIR` installs them as the reference did."""
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--write-configmaps", metavar="DIR", required=True)
+    ap.add_argument("--names", default="phi,opt,default")
+    a = ap.parse_args(argv)
+    os.makedirs(a.write_configmaps, exist_ok=True)
+    for n in a.names.split(","):
+        path = os.path.join(a.write_configmaps, f"{configmap_name(n)}.yaml")
+        with open(path, "w") as f:
+            f.write(configmap_text(n))
+        print(path)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -232,3 +232,66 @@ def test_rocprof_bridge(tmp_path):
     txt = rocprof_bridge.render(rocprof_bridge.collect(str(tmp_path)))
     assert 'akap_kernel_time_seconds_total{kernel="akap::paged_attn_decode_kernel' in txt
     assert "akap_kernel_calls_total" in txt and " 10" in txt
+
+
+REF_TEMPLATES = "/root/reference/templates"
+
+
+@pytest.mark.parametrize("name", ["phi", "opt"])
+def test_chat_template_configmaps_byte_identical_to_reference(name):
+    """the phi/opt ConfigMaps we generate are byte-identical to the
+    reference's templates/<name>-chat-template.yaml (parity pinned against the reference's
+    own files when they are present; skipped where the reference is not mounted)."""
+    path = os.path.join(REF_TEMPLATES, f"{name}-chat-template.yaml")
+    if not os.path.exists(path):
+        pytest.skip("reference templates not mounted here")
+    ref = open(path).read()
+    assert chat_template.configmap_text(name) == ref
+    assert yaml.safe_load(ref)["data"]["template.jinja"] == chat_template.BUILTIN[name]
+
+
+def test_reference_template_rendering_quirks_pinned():
+    """SURVEY C14's verified rendering of the reference template (jinja2 3.1.6): turns are
+    concatenated without separators and the generation prompt opens a *user* turn."""
+    msgs = [{"role": "system", "content": "SYS"}, {"role": "user", "content": "Hi"},
+            {"role": "assistant", "content": "Hello"}, {"role": "user", "content": "Q2"}]
+    assert chat_template.render(msgs, chat_template.BUILTIN["phi"]) == \
+        "SYS\n\nHuman: HiAssistant: HelloHuman: Q2Human:  "
+    assert chat_template.render(msgs, chat_template.BUILTIN["opt"]) == \
+        "SYS\n\nUser: HiAssistant: HelloUser: Q2User:  "
+
+
+def test_chat_template_cli_writes_configmaps(tmp_path):
+    chat_template.main(["--write-configmaps", str(tmp_path), "--names", "phi,opt"])
+    for n in ("phi", "opt"):
+        doc = yaml.safe_load(open(tmp_path / f"{n}-chat-template.yaml"))
+        assert doc["kind"] == "ConfigMap" and doc["metadata"]["name"] == f"{n}-chat-template"
+
+
+def test_gateway_api_objects_when_crds_present():
+    """With the Gateway API CRDs, the installer also emits Gateway + HTTPRoute named
+    llm-d-inference-gateway (tier 1 of the smoke test's address lookup)."""
+    v = installer.load_values(os.path.join(ROOT, "deploy", "values", "slim.yaml"))
+    off = installer.render(v, gateway_api=False)["gateway.yaml"]
+    on = installer.render(v, gateway_api=True)["gateway.yaml"]
+    kinds = {(d["kind"], d["metadata"]["name"]) for d in yaml.safe_load_all(on) if d}
+    assert ("Gateway", "llm-d-inference-gateway") in kinds
+    assert ("HTTPRoute", "llm-d-inference-gateway") in kinds
+    assert "kind: Gateway\n" not in off
+    route = [d for d in yaml.safe_load_all(on) if d and d["kind"] == "HTTPRoute"][0]
+    assert route["spec"]["rules"][0]["backendRefs"][0] == {"name": "llm-d-inference-gateway",
+                                                           "port": 80}
+    test_play = open(os.path.join(ROOT, "provision", "llm-d-test.yaml")).read()
+    assert "get gateway llm-d-inference-gateway" in test_play
+
+
+def test_gitignore_covers_reference_local_state():
+    gi = open(os.path.join(ROOT, ".gitignore")).read().split()
+    for pat in ("gpu-inventory-*.ini", "instance-*-details.txt", "*.tmp", "*.temp",
+                "kubeconfig-*"):
+        assert pat in gi
+
+
+def test_cleanup_removes_kubeconfigs_and_records_reset():
+    play = open(os.path.join(ROOT, "provision", "cleanup-instance.yaml")).read()
+    assert 'patterns: "kubeconfig-*"' in play and "Record what was reset" in play
