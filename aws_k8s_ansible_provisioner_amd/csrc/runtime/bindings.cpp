@@ -58,6 +58,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readwrite("eos_id", &SchedConfig::eos_id)
       .def_readwrite("max_blocks_per_seq", &SchedConfig::max_blocks_per_seq)
       .def_readwrite("mixed_batching", &SchedConfig::mixed_batching)
+      .def_readwrite("mix_backlog_steps", &SchedConfig::mix_backlog_steps)
+      .def_readwrite("max_decode_stall_steps", &SchedConfig::max_decode_stall_steps)
       .def_readwrite("held_kv_ttl_s", &SchedConfig::held_kv_ttl_s);
 
   py::class_<Scheduler>(m, "Scheduler")

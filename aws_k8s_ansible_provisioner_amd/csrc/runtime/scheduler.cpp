@@ -293,10 +293,23 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
   // prefill chunks (TTFT) -- the token buffers hold budget + max_num_seqs rows
   int budget = std::min(cfg_.max_num_batched_tokens, buf.cap_tokens);
 
-  bool pending_prefill = !waiting_.empty();
-  for (Request* r : running_)
-    pending_prefill |= (int)r->tokens.size() - r->num_computed > 1;
-  if (pending_prefill && cfg_.mixed_batching) {
+  // pending prompt tokens (waiting requests not yet prefix-matched count in full) and
+  // whether any running sequence is in its decode phase
+  int64_t backlog = 0;
+  bool any_decode = false;
+  for (Request* r : waiting_) backlog += (int)r->tokens.size() - r->num_computed;
+  for (Request* r : running_) {
+    const int rem = (int)r->tokens.size() - r->num_computed;
+    if (rem > 1) backlog += rem;
+    else any_decode = true;
+  }
+  const bool pending_prefill = backlog > 0;
+  bool mix = pending_prefill && cfg_.mixed_batching && any_decode;
+  if (mix && backlog > (int64_t)budget * cfg_.mix_backlog_steps &&
+      prefill_only_run_ < cfg_.max_decode_stall_steps)
+    mix = false;  // burst: drain the prefill queue first (TTFT), decodes wait a bounded time
+  prefill_only_run_ = (pending_prefill && !mix && any_decode) ? prefill_only_run_ + 1 : 0;
+  if (mix) {
     // mixed step: decodes first (they never stall behind a prefill), then prefill chunks
     int dbudget = std::max(0, std::min(cfg_.max_num_seqs, buf.cap_tokens - budget));
     schedule_decodes(sched, info, dbudget);

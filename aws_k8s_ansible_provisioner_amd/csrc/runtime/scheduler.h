@@ -4,9 +4,12 @@
 // batch description (token ids, positions, paged-cache slots, block tables, cu-seqlens,
 // attention tile map, logits rows) straight into caller-owned pinned buffers, so the
 // Python engine loop does no per-token work.  Policy:
-//   * mixed batching (default): every running decode gets its token first, the rest of the
-//     step's token budget is filled with prefill chunks, so a running decode never stalls
-//     behind a prefill (the decode rows lead the flattened batch: [0, num_decode));
+//   * mixed batching (default): every running decode gets its token in the same step as the
+//     prefill chunks (the decode rows lead the flattened batch: [0, num_decode)), so a
+//     running decode does not stall behind prefills.  Under a prefill BACKLOG (more pending
+//     prompt tokens than `mix_backlog_steps` steps' budget -- a burst of arrivals) the step
+//     stays prefill-first, which minimises TTFT while the queue drains, but never for more
+//     than `max_decode_stall_steps` consecutive steps;
 //   * mixed_batching = false: prefill-first (a step is pure prefill while any is pending);
 //   * a step with no prefill work is a pure decode step (hipGraph replay);
 //   * out of KV blocks -> preempt the youngest running sequence (recompute later);
@@ -63,6 +66,8 @@ struct SchedConfig {
   int eos_id = -1;
   int max_blocks_per_seq = 128;
   bool mixed_batching = true;
+  int mix_backlog_steps = 1;       // mix when pending prefill <= this many steps' budget
+  int max_decode_stall_steps = 8;  // ... or after this many prefill-only steps in a row
   double held_kv_ttl_s = 120.0;  // P/D: held KV never pulled by a decode engine is freed
 };
 
@@ -176,6 +181,7 @@ class Scheduler {
   std::unordered_map<int64_t, HeldKV> held_;
   int64_t preemptions_ = 0;
   int64_t held_expired_ = 0;
+  int prefill_only_run_ = 0;  // consecutive prefill-only steps while decodes were waiting
 };
 
 }  // namespace akap_rt

@@ -30,6 +30,9 @@ class EngineConfig:
     init_std: float = 0.02                    # random-init weight scale
     shard_init: str = "per_rank"              # "per_rank" | "full" (identical logical weights for any TP)
     mixed_batching: bool = True               # decodes + prefill chunks in one step
+    mix_backlog_steps: int = 1                # ... unless more prefill is queued than this
+    max_decode_stall_steps: int = 8           #     many steps' budget (burst: TTFT first),
+    #                                           for at most this many steps in a row
     held_kv_ttl_s: float = 120.0              # P/D prefill: free un-pulled held KV after this
 
     def __post_init__(self) -> None:

@@ -80,6 +80,8 @@ class LLMEngine:
         sc.eos_id = self.mcfg.eos_id
         sc.max_blocks_per_seq = self.runner.max_blocks
         sc.mixed_batching = ecfg.mixed_batching
+        sc.mix_backlog_steps = ecfg.mix_backlog_steps
+        sc.max_decode_stall_steps = ecfg.max_decode_stall_steps
         sc.held_kv_ttl_s = ecfg.held_kv_ttl_s
         self.sched = rt.Scheduler(sc, self.runner.num_blocks, ecfg.enable_prefix_caching)
         self.tokenizer = get_tokenizer(ecfg.weights_path, self.mcfg.vocab_size, self.mcfg.bos_id,
@@ -93,6 +95,8 @@ class LLMEngine:
         self.steps = 0
         self.last_prefix = (0, 0)
         self.timers = {"schedule": 0.0, "execute": 0.0, "post": 0.0}
+        # execute wall time / step count per step kind (pure prefill, mixed, pure decode)
+        self.step_kinds = {k: [0.0, 0] for k in ("prefill", "mixed", "decode")}
         self._n_extra = 0  # live requests that need penalties or log-probs
         self.last_step_mixed = False  # the last step ran decode rows beside prefill chunks
         self.pd_group: Optional[str] = None  # P/D transfer-group id (stamped into kvp)
@@ -250,6 +254,11 @@ class LLMEngine:
         now = time.time()
         self.timers["schedule"] += t1 - t0
         self.timers["execute"] += now - t1
+        if info["num_seqs"]:
+            kind = ("mixed" if self.last_step_mixed else "prefill") if info["is_prefill"] \
+                else "decode"
+            self.step_kinds[kind][0] += now - t1
+            self.step_kinds[kind][1] += 1
         with self._lock:
             ids, new, fin, first = self.sched.update(np.ascontiguousarray(toks, dtype=np.int64))
         m, name = self.metrics, self.model_name

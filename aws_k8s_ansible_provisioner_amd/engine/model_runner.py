@@ -216,7 +216,9 @@ class ModelRunner:
         h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
         if ns == 0:
             return self.out_tokens[:0]
-        logits = self.model.compute_logits(h.index_select(0, lidx)).float()
+        logits = self.model.compute_logits(h.index_select(0, lidx))
+        if not self.is_gpu:
+            logits = logits.float()  # the GPU sampler reads bf16 logits directly
         toks, _ = self._sample(logits, ns, info.get("extras"))
         return toks
 

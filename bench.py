@@ -220,6 +220,8 @@ def main() -> int:
     barrier()
     el = time.perf_counter() - t0
     log(f"[bench] host timers (all waves): {eng.timers}  steps={eng.steps}")
+    log("[bench] execute s / steps by kind: " + ", ".join(
+        f"{k} {v[0]:.3f}/{v[1]}" for k, v in getattr(eng, "step_kinds", {}).items()))
     for _ in range(a.profile_steps):
         wave()
 

@@ -210,3 +210,33 @@ def test_held_kv_expires_after_ttl():
     assert s.num_held == 0 and s.kv_usage() == 0 and s.held_expired_total == 1
     s.free_held(7)  # late release after expiry: harmless
     assert s.kv_usage() == 0
+
+
+def test_burst_backlog_stays_prefill_first_for_a_bounded_number_of_steps():
+    """A prefill backlog larger than one step's budget (burst arrival) is drained
+    prefill-first (TTFT) -- but decodes wait at most max_decode_stall_steps steps; once the
+    backlog fits in a step, decodes and prefill chunks mix."""
+    c = rt.SchedConfig()
+    c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 8, 16, 128
+    c.block_size, c.gqa_group, c.tile_rows, c.eos_id, c.max_blocks_per_seq = 4, 2, 64, 2, 32
+    c.max_decode_stall_steps = 3
+    s, b = rt.Scheduler(c, 256, False), _bufs(8, 24, 32)
+    s.add_request(1, list(range(10, 26)), 50)   # 16 tokens: fills step 1
+    for k in range(2, 8):                        # 6 x 16 = 96 tokens queued behind it
+        s.add_request(k, list(range(100 * k, 100 * k + 16)), 50)
+    kinds = []
+    for _ in range(8):
+        i = s.schedule(b)
+        kinds.append((i["is_prefill"], i["num_decode"]))
+        s.update(np.zeros(i["num_samples"], np.int64) + 5)
+    # step 1: pure prefill (nothing decoding); steps 2-4: backlog > budget -> prefill-first
+    # while request 1 waits (3 stall steps); step 5: stall bound -> mixed; afterwards no run
+    # of decode-stalling prefill steps is longer than the bound
+    assert kinds[0] == (1, 0)
+    assert kinds[1:4] == [(1, 0)] * 3
+    assert kinds[4][0] == 1 and kinds[4][1] >= 1
+    run = longest = 0
+    for k in kinds[1:]:
+        run = run + 1 if k[1] == 0 else 0
+        longest = max(longest, run)
+    assert longest <= 3
