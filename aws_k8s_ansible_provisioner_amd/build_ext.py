@@ -78,16 +78,21 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
     return out
 
 
-def build_runtime(force: bool = False) -> str:
+def build_runtime(force: bool = False, out_dir: str = PKG, sanitize: bool = False) -> str:
+    """sanitize: -fsanitize=address,undefined build (host code only) into out_dir, for
+    tools/sanitize_runtime.sh (load it with AKAP_RUNTIME_DIR=out_dir + LD_PRELOAD libasan)."""
     import pybind11
 
     os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(out_dir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     hdrs = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
     ext = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    out = os.path.join(PKG, "_runtime" + ext)
-    if force or _newer(out, srcs + hdrs):
-        _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-fvisibility=hidden",
+    out = os.path.join(out_dir, "_runtime" + ext)
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+             "-fno-sanitize-recover=undefined"] if sanitize else ["-O3"]
+    if force or sanitize or _newer(out, srcs + hdrs):
+        _run(["g++", *flags, "-std=c++17", "-shared", "-fPIC", "-Wall", "-fvisibility=hidden",
               "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], *srcs,
               "-o", out])
     return out
@@ -103,7 +108,12 @@ def main() -> None:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 8))
     ap.add_argument("--runtime-only", action="store_true")
+    ap.add_argument("--sanitize-runtime", metavar="DIR", default=None,
+                    help="ASan+UBSan build of the host runtime into DIR")
     a = ap.parse_args()
+    if a.sanitize_runtime:
+        print(build_runtime(True, a.sanitize_runtime, sanitize=True))
+        return
     if a.runtime_only:
         print(build_runtime(a.force))
         return

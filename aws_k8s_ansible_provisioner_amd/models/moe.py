@@ -89,6 +89,19 @@ class MoEBlock:
             self.w13[j].copy_(torch.cat([w1, w3], 0))
             self.w2[j].copy_(w2)
 
+    def hf_state_dict(self, prefix: str) -> dict:
+        """HF (Mixtral) names of this unsharded block's router and experts."""
+        if self.e_local != self.E or self.f_local != self.cfg.intermediate_size:
+            raise ValueError("hf_state_dict needs the unsharded MoE block")
+        Fn = self.f_local
+        sd = {prefix + "block_sparse_moe.gate.weight": self.router.clone()}
+        for e in range(self.E):
+            p = f"{prefix}block_sparse_moe.experts.{e}."
+            sd[p + "w1.weight"] = self.w13[e, :Fn].clone()
+            sd[p + "w3.weight"] = self.w13[e, Fn:].clone()
+            sd[p + "w2.weight"] = self.w2[e].clone()
+        return sd
+
     def _experts(self, x: torch.Tensor, counts: list[int]) -> torch.Tensor:
         """x: tokens grouped by local expert (counts[j] rows for expert j)."""
         out = torch.empty(x.shape[0], x.shape[1], dtype=x.dtype, device=x.device)

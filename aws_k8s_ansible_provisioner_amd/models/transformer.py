@@ -196,6 +196,39 @@ class DecoderLM:
                 n += lw.moe.numel()
         return n * 2
 
+    def hf_state_dict(self) -> dict:
+        """This (unsharded, tp=1) model's weights under HF names, un-fusing QKV and gate|up
+        and the Mixtral experts -- the inverse of load_state_dict (checkpoint export and the
+        loader's round-trip tests)."""
+        if self.ps.tp_size != 1:
+            raise ValueError("hf_state_dict needs the unsharded (tp=1) model")
+        cfg, D = self.cfg, self.D
+        n = self.vocab_end - self.vocab_start
+        sd = {"model.embed_tokens.weight": self.embed[:n].clone(),
+              "model.norm.weight": self.final_norm.clone()}
+        if not cfg.tie_embeddings:
+            sd["lm_head.weight"] = self.lm_head[:n].clone()
+        q, kv = self.hq * D, self.hkv * D
+        for i, lw in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            sd[p + "input_layernorm.weight"] = lw.ln1.clone()
+            sd[p + "post_attention_layernorm.weight"] = lw.ln2.clone()
+            sd[p + "self_attn.q_proj.weight"] = lw.w_qkv[:q].clone()
+            sd[p + "self_attn.k_proj.weight"] = lw.w_qkv[q:q + kv].clone()
+            sd[p + "self_attn.v_proj.weight"] = lw.w_qkv[q + kv:].clone()
+            sd[p + "self_attn.o_proj.weight"] = lw.w_o.clone()
+            if lw.q_norm is not None:
+                sd[p + "self_attn.q_norm.weight"] = lw.q_norm.clone()
+                sd[p + "self_attn.k_norm.weight"] = lw.k_norm.clone()
+            if lw.moe is not None:
+                sd.update(lw.moe.hf_state_dict(p))
+            else:
+                F_ = lw.w_gate_up.shape[0] // 2
+                sd[p + "mlp.gate_proj.weight"] = lw.w_gate_up[:F_].clone()
+                sd[p + "mlp.up_proj.weight"] = lw.w_gate_up[F_:].clone()
+                sd[p + "mlp.down_proj.weight"] = lw.w_down.clone()
+        return sd
+
     def load_state_dict(self, sd: dict) -> None:
         """Load HF-named tensors (safetensors from the model PVC) into the fused layout."""
         cfg, tp, r = self.cfg, self.ps.tp_size, self.ps.tp_rank
