@@ -73,7 +73,9 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int32_t* __restri
   int* cursor = sm + E;   // [E]
   for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[ids[i]], 1);
+  // ids outside [0, E) (expert-parallel padding rows) are skipped: no slot, inv = -1
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    if ((unsigned)ids[i] < (unsigned)E) atomicAdd(&cnt[ids[i]], 1);
   __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
@@ -101,6 +103,10 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int32_t* __restri
   }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    if ((unsigned)ids[i] >= (unsigned)E) {
+      if (inv != nullptr) inv[i] = -1;
+      continue;
+    }
     const int pos = atomicAdd(&cursor[ids[i]], 1);
     sorted_ids[pos] = i;
     if (inv != nullptr) inv[i] = pos;
@@ -216,8 +222,10 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict
     const int c = (int)(i % vpr) * 8;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int k = 0; k < topk; ++k) {
+      const int pos = inv[(size_t)t * topk + k];
+      if (pos < 0) continue;  // skipped (expert-parallel padding) row: contributes nothing
       const float wk = wts[(size_t)t * topk + k];
-      const bf16x8 y = *reinterpret_cast<const bf16x8*>(Y + (size_t)inv[(size_t)t * topk + k] * d + c);
+      const bf16x8 y = *reinterpret_cast<const bf16x8*>(Y + (size_t)pos * d + c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += wk * bf2f(y[j]);
     }

@@ -187,8 +187,10 @@ __global__ __launch_bounds__(256) void moe_combine_split_kernel(const float* __r
     const int c = (int)(i % vpr) * 8;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int k = 0; k < topk; ++k) {
+      const int pos = inv[(size_t)t * topk + k];
+      if (pos < 0) continue;  // skipped (expert-parallel padding) row
       const float wk = wts[(size_t)t * topk + k];
-      const size_t r = (size_t)inv[(size_t)t * topk + k];
+      const size_t r = (size_t)pos;
       for (int z = 0; z < S; ++z) {
         const f32x4* p = reinterpret_cast<const f32x4*>(P + ((size_t)z * rows + r) * d + c);
         const f32x4 a = p[0], b = p[1];

@@ -6,10 +6,18 @@ sorted, tile-padded index list).  Two placements:
     like a dense layer) -- best at small batch on a single xGMI node;
   * "ep": rank e holds experts [e*E/ep, (e+1)*E/ep) whole; tokens are dispatched and
     combined with two RCCL all_to_all_single calls over the EP (=dp x tp) group.
-Expert GEMMs, "tp" mode on the GPU at decode sizes: `ops.fused_moe` -- device-side
-sort + grouped MFMA GEMMs + gather-combine, no host sync, so decode captures in a
-hipGraph.  Large (prefill) batches and "ep" mode run per expert on the grouped token
-slices (hipBLASLt), which needs the per-expert counts on the host.
+Expert GEMMs: `ops.fused_moe` -- device-side sort + grouped MFMA GEMMs + gather-combine,
+no host sync.  "tp" mode uses it at decode sizes (captured in the decode hipGraph); very
+large "tp" prefill batches run per expert on hipBLASLt (AKAP_FUSED_MOE_MAX_T).
+
+"ep" mode, decode sizes (T <= AKAP_EP_FIXED_MAX_T): a FIXED-CAPACITY dispatch -- every
+(token, expert) pair gets a slot (destination rank, rank-local index) computed on the device,
+the send buffer is [ep, C, d] with C = T*K (the most pairs any one rank can receive), so both
+all_to_all_single calls use equal splits and no split size ever goes to the host: the whole
+EP MoE block (route, dispatch, grouped expert GEMMs on the received rows, combine) is
+sync-free and graph-capturable.  Empty slots carry expert id -1, which moe_align skips.
+Larger (prefill) batches exchange exact split sizes (one small host sync per layer) and run
+the received rows through the same grouped GEMM.
 """
 from __future__ import annotations
 
@@ -125,52 +133,94 @@ class MoEBlock:
             pad = per * tp - T
             hp = torch.cat([h, h.new_zeros(pad, h.shape[1])]) if pad else h
             mine = self._forward_tokens(hp[r * per:(r + 1) * per].contiguous())
-            parts = [torch.empty_like(mine) for _ in range(tp)]
-            torch.distributed.all_gather(parts, mine, group=self.ps.tp_group)
-            return torch.cat(parts)[:T]
+            full = torch.empty(per * tp, h.shape[1], dtype=h.dtype, device=h.device)
+            torch.distributed.all_gather_into_tensor(full, mine, group=self.ps.tp_group)
+            return full[:T]
         return self._forward_tokens(h)
 
     graph_safe_max_tokens = int(os.environ.get("AKAP_FUSED_MOE_MAX_T", "1024"))
+    ep_fixed_max_tokens = int(os.environ.get("AKAP_EP_FIXED_MAX_T", "512"))
 
     @property
     def graph_safe(self) -> bool:
-        return self.mode != "ep"
+        """Decode steps capture in a hipGraph: tp mode (fused_moe) and ep mode (fixed-capacity
+        dispatch) are both free of host syncs at decode sizes."""
+        return True
 
     def _forward_tokens(self, h: torch.Tensor) -> torch.Tensor:
         T, d = h.shape
         logits = F.linear(h, self.router)
         w, ids = ops.moe_topk_softmax(logits, self.K, renormalize=True)
-        if self.mode != "ep" and h.is_cuda and (T <= self.graph_safe_max_tokens or
-                                                  torch.cuda.is_current_stream_capturing()):
+        capturing = h.is_cuda and torch.cuda.is_current_stream_capturing()
+        if self.mode == "ep":
+            if T <= self.ep_fixed_max_tokens or capturing:
+                return self._ep_fixed(h, w, ids)
+            return self._ep_exact(h, w, ids)
+        if h.is_cuda and (T <= self.graph_safe_max_tokens or capturing):
             out = ops.fused_moe(h, self.w13, self.w2, w, ids)
             comm.tp_all_reduce(out)
             return out
         flat = ids.reshape(-1).long()
         order = torch.argsort(flat, stable=True)
         tok_of = order // self.K
-        if self.mode == "ep":
-            owner = flat[order] // self.e_local
-            send_counts = torch.bincount(owner, minlength=self.ep)
-            recv_counts = torch.empty_like(send_counts)
-            torch.distributed.all_to_all_single(recv_counts, send_counts)
-            sc, rc = send_counts.tolist(), recv_counts.tolist()
-            x_send = h[tok_of]
-            e_send = flat[order].to(torch.int32)
-            x_recv = comm.all_to_all(x_send, rc, sc)
-            e_recv = comm.all_to_all(e_send, rc, sc).long() - self.e0
-            o2 = torch.argsort(e_recv, stable=True)
-            counts = torch.bincount(e_recv, minlength=self.e_local).tolist()
-            y_sorted = self._experts(x_recv[o2], counts)
-            y_recv = torch.empty_like(y_sorted)
-            y_recv[o2] = y_sorted
-            y_back = comm.all_to_all(y_recv, sc, rc)
-        else:
-            counts = torch.bincount(flat, minlength=self.E).tolist()
-            y_back = self._experts(h[tok_of], counts)
+        counts = torch.bincount(flat, minlength=self.E).tolist()
+        y_back = self._experts(h[tok_of], counts)
         wt = w.reshape(-1)[order].to(torch.float32)
         out = torch.zeros(T, d, dtype=torch.float32, device=h.device)
         out.index_add_(0, tok_of, y_back.float() * wt[:, None])
         out = out.to(h.dtype)
-        if self.mode != "ep":
-            comm.tp_all_reduce(out)
+        comm.tp_all_reduce(out)
         return out
+
+    def _ep_fixed(self, h: torch.Tensor, w: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+        """Sync-free, capturable EP dispatch/combine with per-peer capacity C = T*K."""
+        T, d = h.shape
+        K, ep, el = self.K, self.ep, self.e_local
+        n = T * K
+        C = n
+        flat = ids.reshape(-1).long()                       # [n] global expert ids
+        dest = flat // el                                   # owning rank
+        onehot = F.one_hot(dest, ep).to(torch.int32)        # [n, ep]
+        slot = ((torch.cumsum(onehot, 0) - onehot) * onehot).sum(1).long()  # rank-local index
+        pos = dest * C + slot                               # row in the [ep * C] send buffer
+        tok = torch.arange(n, device=h.device) // K
+        send_x = h.new_zeros(ep * C, d)
+        send_x.index_copy_(0, pos, h[tok])
+        send_e = torch.full((ep * C,), -1, dtype=torch.int32, device=h.device)
+        send_e.index_copy_(0, pos, (flat - dest * el).to(torch.int32))
+        recv_x = torch.empty_like(send_x)
+        recv_e = torch.empty_like(send_e)
+        grp = None  # the EP group is the whole job (dp x tp ranks)
+        torch.distributed.all_to_all_single(recv_x, send_x, group=grp)
+        torch.distributed.all_to_all_single(recv_e, send_e, group=grp)
+        # every received row is one (token, local expert) pair: K = 1, weight 1 (the router
+        # weight is applied by the sender at combine); empty slots (id -1) give zero rows
+        ones = torch.ones(ep * C, 1, dtype=torch.float32, device=h.device)
+        y = ops.fused_moe(recv_x, self.w13, self.w2, ones, recv_e.view(-1, 1))
+        back = torch.empty_like(y)
+        torch.distributed.all_to_all_single(back, y, group=grp)
+        mine = back.index_select(0, pos).view(T, K, d).float()
+        return (mine * w.view(T, K, 1)).sum(1).to(h.dtype)
+
+    def _ep_exact(self, h: torch.Tensor, w: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+        """Prefill-size EP: exact split sizes (one host sync for the counts), received rows
+        through the grouped expert GEMM (no per-expert host loop)."""
+        T, d = h.shape
+        flat = ids.reshape(-1).long()
+        order = torch.argsort(flat, stable=True)
+        tok_of = order // self.K
+        grp = None  # the EP group is the whole job (dp x tp ranks)
+        owner = flat[order] // self.e_local
+        send_counts = torch.bincount(owner, minlength=self.ep)
+        recv_counts = torch.empty_like(send_counts)
+        torch.distributed.all_to_all_single(recv_counts, send_counts, group=grp)
+        sc, rc = torch.stack([send_counts, recv_counts]).tolist()
+        x_recv = comm.all_to_all(h[tok_of], rc, sc, group=grp)
+        e_recv = comm.all_to_all(flat[order].to(torch.int32), rc, sc, group=grp) - self.e0
+        ones = torch.ones(x_recv.shape[0], 1, dtype=torch.float32, device=h.device)
+        y_recv = ops.fused_moe(x_recv, self.w13, self.w2, ones, e_recv.view(-1, 1))
+        y_back = comm.all_to_all(y_recv, sc, rc, group=grp)
+        wt = w.reshape(-1)[order].to(torch.float32)
+        out = torch.zeros(T, d, dtype=torch.float32, device=h.device)
+        out.index_add_(0, tok_of, y_back.float() * wt[:, None])
+        return out.to(h.dtype)

@@ -245,7 +245,7 @@ def moe_align(topk_ids, E, block, cap):
     sorted_ids = torch.full((cap,), n, dtype=torch.int32)
     offsets = torch.zeros(E + 1, dtype=torch.int32)
     acc = 0
-    for e in range(E):
+    for e in range(E):  # ids outside [0, E) are skipped
         idx = (flat == e).nonzero().flatten()
         offsets[e] = acc
         sorted_ids[acc:acc + idx.numel()] = idx.to(torch.int32)
@@ -256,16 +256,20 @@ def moe_align(topk_ids, E, block, cap):
 
 def fused_moe(h, w13, w2, topk_w, topk_ids):
     """fp32 reference of the fused expert FFN (bf16 rounding at the same points as the
-    kernels: after each GEMM and after silu_and_mul)."""
+    kernels: after each GEMM and after silu_and_mul).  Expert ids outside [0, E) -- the
+    padding rows of the expert-parallel dispatch -- contribute nothing (as in moe_align)."""
     T, d = h.shape
+    E = w13.shape[0]
     out = torch.zeros(T, d, dtype=torch.float32, device=h.device)
-    for t in range(T):
-        for k in range(topk_ids.shape[1]):
-            e = int(topk_ids[t, k])
-            y1 = (h[t].float() @ w13[e].float().t()).to(h.dtype)
-            a = silu_and_mul(y1[None])[0]
-            y2 = (a.float() @ w2[e].float().t()).to(h.dtype)
-            out[t] += float(topk_w[t, k]) * y2.float()
+    ids = topk_ids.long()
+    for e in range(E):
+        t_idx, k_idx = (ids == e).nonzero(as_tuple=True)
+        if t_idx.numel() == 0:
+            continue
+        y1 = (h[t_idx].float() @ w13[e].float().t()).to(h.dtype)
+        a = silu_and_mul(y1)
+        y2 = (a.float() @ w2[e].float().t()).to(h.dtype)
+        out.index_add_(0, t_idx, topk_w[t_idx, k_idx].float()[:, None] * y2.float())
     return out.to(h.dtype)
 
 

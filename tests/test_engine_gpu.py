@@ -106,3 +106,63 @@ def test_mixed_batching_gpu(model):
             _check_teacher_forced(eng, p, got[k])
         outs[mixed] = got
     assert outs[True] == outs[False]
+
+
+def test_qwen3_0_6b_production_decode_path():
+    """Real Qwen3-0.6B shapes with max_num_seqs=64 / graphs up to 64: the GEMM tuner and the
+    fused dgemm decode chain run inside the captured graphs (not only tiny models), and the
+    tokens are teacher-forced against the dense reference."""
+    from aws_k8s_ansible_provisioner_amd.ops import gemm_tuner
+
+    eng = _engine("qwen3-0.6b", max_model_len=512, max_num_seqs=64, cuda_graph_max_bs=64,
+                  max_num_batched_tokens=2048, num_gpu_blocks=1200, init_std=0.05)
+    assert eng.runner.graphs and max(eng.runner.buckets) == 64
+    assert any(gemm_tuner.fused_plan(b) is not None for b in eng.runner.buckets if b >= 16)
+    prompts = [list(range(1000 + 7 * i, 1000 + 7 * i + 60 + i)) for i in range(48)]
+    outs = eng.generate(None, SamplingParams(max_tokens=5, temperature=0, ignore_eos=True),
+                        prompt_ids=prompts)
+    assert len(outs) == 48
+    for p, o in list(zip(prompts, outs))[::6]:
+        _check_teacher_forced(eng, p, o.output_ids, tol=0.25)
+
+
+def test_ep_decode_step_captures_in_a_hipgraph(monkeypatch):
+    """Mixtral expert parallelism on 1 GPU with a simulated EP world of 1 (RCCL process group
+    of size one): the fixed-capacity dispatch has no host sync, so the decode step is
+    captured in hipGraphs, and the EP engine generates the tp-mode engine's tokens."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+    created = not dist.is_initialized()
+    if created:
+        dist.init_process_group("nccl", rank=0, world_size=1,
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        from aws_k8s_ansible_provisioner_amd.models import moe as moe_mod
+
+        outs = {}
+        for mode in ("ep", "tp"):
+            monkeypatch.setenv("AKAP_MOE_MODE", mode)
+            eng = _engine("tiny-mixtral")
+            blk = eng.runner.model.layers[0].moe
+            assert blk.mode == mode and blk.graph_safe
+            assert eng.runner.graphs, f"{mode}: decode not captured"
+            prompts = [list(range(5, 60)), [7, 8] * 20, list(range(200, 230))]
+            res = eng.generate(None, SamplingParams(max_tokens=8, temperature=0,
+                                                    ignore_eos=True), prompt_ids=prompts)
+            for p, o in zip(prompts, res):
+                _check_teacher_forced(eng, p, o.output_ids)
+            outs[mode] = [o.output_ids for o in res]
+        assert outs["ep"] == outs["tp"]
+        assert moe_mod.MoEBlock.ep_fixed_max_tokens >= 16
+    finally:
+        if created:
+            dist.destroy_process_group()

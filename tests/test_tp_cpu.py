@@ -21,7 +21,8 @@ from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
 model = os.environ["MODEL"]
 ecfg = EngineConfig(model=model, device="cpu", max_model_len=256, max_num_seqs=8,
                     max_num_batched_tokens=32, block_size=32, num_gpu_blocks=96,
-                    tensor_parallel_size=2, shard_init="full", init_std=0.15)
+                    tensor_parallel_size=int(os.environ["WORLD_SIZE"]), shard_init="full",
+                    init_std=0.15)
 eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
 if eng is not None:
     outs = eng.generate(None, SamplingParams(max_tokens=8, temperature=0, ignore_eos=True),
@@ -39,18 +40,22 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("model,moe_mode", [("tiny-llama", "tp"), ("tiny-qwen3", "tp"),
-                                            ("tiny-mixtral", "tp"), ("tiny-mixtral", "ep")])
-def test_tp2_matches_tp1(model, moe_mode):
+@pytest.mark.parametrize("model,moe_mode,world,ep_fixed", [
+    ("tiny-llama", "tp", 2, 512), ("tiny-qwen3", "tp", 2, 512), ("tiny-mixtral", "tp", 2, 512),
+    ("tiny-mixtral", "ep", 2, 512),
+    # 4 ranks: kv heads replicated (2 kv heads / 4 ranks), one expert per EP rank; EP with the
+    # fixed-capacity (graph-safe) dispatch and with the exact-split prefill path
+    ("tiny-llama", "tp", 4, 512), ("tiny-mixtral", "ep", 4, 512), ("tiny-mixtral", "ep", 4, 0)])
+def test_tp_matches_tp1(model, moe_mode, world, ep_fixed):
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
 
     port = _port()
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROOT=ROOT, MODEL=model,
-                   AKAP_MOE_MODE=moe_mode)
+                   AKAP_MOE_MODE=moe_mode, AKAP_EP_FIXED_MAX_T=str(ep_fixed))
         procs.append(subprocess.Popen([sys.executable, "-c", CHILD], env=env, cwd=ROOT,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=300) for p in procs]
