@@ -75,11 +75,42 @@ __device__ __forceinline__ void acc_add(float* acc, const bf16x8& v) {
   for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
 }
 
+// Store of one reduced 8-vector i: plain, or the residual + next-norm epilogue (CarEpi).
+// The epilogue's per-row sum of squares is reduced across the wave first (d % 512 == 0:
+// a wave's 64 consecutive vectors lie in one row), then one atomic per wave.
+template <bool EPI>
+__device__ __forceinline__ void car_store(bf16* __restrict__ out, const CarEpi& e, long i,
+                                          const bf16x8& sum) {
+  if constexpr (!EPI) {
+    reinterpret_cast<bf16x8*>(out)[i] = sum;
+  } else {
+    const long el = i * 8;
+    const int row = (int)(el / e.d), col = (int)(el % e.d);
+    bf16x8* rp = reinterpret_cast<bf16x8*>(e.residual) + i;
+    const bf16x8 r = *rp;
+    const bf16x8 g = *reinterpret_cast<const bf16x8*>(e.ln + col);
+    bf16x8 s8, a8;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s8[j] = f2bf(bf2f(sum[j]) + bf2f(r[j]));
+      const float f = bf2f(s8[j]);
+      a8[j] = f2bf(f * bf2f(g[j]));
+      q += f * f;
+    }
+    *rp = s8;
+    reinterpret_cast<bf16x8*>(e.aout)[i] = a8;
+    q = wave_sum(q);
+    if ((threadIdx.x & 63) == 0) atomicAdd(e.ss + row, q);
+  }
+}
+
 // Kernel bodies take the block's identity (bid of nblk) explicitly so the test launcher
 // below can run every simulated rank of one process inside one grid.
+template <bool EPI>
 __device__ __forceinline__ void car_oneshot(const CarArgs& a, int bid, int nblk,
                                             const bf16* __restrict__ in, bf16* __restrict__ out,
-                                            long n8) {
+                                            long n8, const CarEpi& epi) {
   const uint32_t ep = car_epoch(a, bid);
   const size_t par = (ep & 1) * a.half_elems;
   bf16x8* mine = reinterpret_cast<bf16x8*>(a.bufs[a.rank] + par);
@@ -96,14 +127,16 @@ __device__ __forceinline__ void car_oneshot(const CarArgs& a, int bid, int nblk,
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
-    dst[i] = o;
+    car_store<EPI>(out, epi, i, o);
   }
+  (void)dst;
 }
 
 // Two-shot: n8 split into W slices of s8 vectors (last slice may be short).
+template <bool EPI>
 __device__ __forceinline__ void car_twoshot(const CarArgs& a, int bid, int nblk,
                                             const bf16* __restrict__ in, bf16* __restrict__ out,
-                                            long n8) {
+                                            long n8, const CarEpi& epi) {
   const uint32_t ep = car_epoch(a, bid);
   const size_t par = (ep & 1) * a.half_elems;
   // staging region: [0, half) input copies; result region: [2*half, 3*half) by parity
@@ -134,7 +167,7 @@ __device__ __forceinline__ void car_twoshot(const CarArgs& a, int bid, int nblk,
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
     myres[i] = o;
-    dst[i] = o;
+    car_store<EPI>(out, epi, i, o);
   }
   car_barrier(a, bid, ep, 1);
   // all-gather the other slices
@@ -144,27 +177,35 @@ __device__ __forceinline__ void car_twoshot(const CarArgs& a, int bid, int nblk,
     const long phi = plo + s8 < n8 ? plo + s8 : n8;
     const bf16x8* pres = reinterpret_cast<const bf16x8*>(a.bufs[p] + res);
     for (long i = plo + (long)bid * 256 + threadIdx.x; i < phi; i += stride)
-      dst[i] = pres[i];
+      car_store<EPI>(out, epi, i, pres[i]);
   }
+  (void)dst;
 }
 
+template <bool EPI>
 __global__ __launch_bounds__(256) void car_oneshot_kernel(CarArgs a, const bf16* __restrict__ in,
-                                                          bf16* __restrict__ out, long n8) {
-  car_oneshot(a, blockIdx.x, gridDim.x, in, out, n8);
+                                                          bf16* __restrict__ out, long n8,
+                                                          CarEpi epi) {
+  car_oneshot<EPI>(a, blockIdx.x, gridDim.x, in, out, n8, epi);
 }
 
+template <bool EPI>
 __global__ __launch_bounds__(256) void car_twoshot_kernel(CarArgs a, const bf16* __restrict__ in,
-                                                          bf16* __restrict__ out, long n8) {
-  car_twoshot(a, blockIdx.x, gridDim.x, in, out, n8);
+                                                          bf16* __restrict__ out, long n8,
+                                                          CarEpi epi) {
+  car_twoshot<EPI>(a, blockIdx.x, gridDim.x, in, out, n8, epi);
 }
 
 // Test launcher: blockIdx.y = simulated rank (all ranks' blocks co-resident in one grid).
+template <bool EPI>
 __global__ __launch_bounds__(256) void car_multi_kernel(CarMulti m, long n8, int two_shot) {
   const int r = blockIdx.y;
   if (two_shot)
-    car_twoshot(m.args[r], blockIdx.x, gridDim.x, (const bf16*)m.in[r], (bf16*)m.out[r], n8);
+    car_twoshot<EPI>(m.args[r], blockIdx.x, gridDim.x, (const bf16*)m.in[r], (bf16*)m.out[r],
+                     n8, m.epi[r]);
   else
-    car_oneshot(m.args[r], blockIdx.x, gridDim.x, (const bf16*)m.in[r], (bf16*)m.out[r], n8);
+    car_oneshot<EPI>(m.args[r], blockIdx.x, gridDim.x, (const bf16*)m.in[r], (bf16*)m.out[r],
+                     n8, m.epi[r]);
 }
 
 // Block count for n8 vectors: the same on every rank (a pure function of n8 and world).
@@ -176,14 +217,18 @@ static int car_blocks(long n8, int world, bool two) {
 }
 
 void launch_custom_allreduce(const CarArgs& a, const void* in, void* out, long n, int two_shot,
-                             hipStream_t s) {
+                             hipStream_t s, const CarEpi* epi) {
   const long n8 = n / 8;
   if (n8 == 0) return;
   const int blocks = car_blocks(n8, a.world, two_shot != 0);
-  if (two_shot)
-    car_twoshot_kernel<<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8);
-  else
-    car_oneshot_kernel<<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8);
+  const CarEpi e = epi ? *epi : CarEpi{};
+  if (two_shot) {
+    if (epi) car_twoshot_kernel<true><<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8, e);
+    else car_twoshot_kernel<false><<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8, e);
+  } else {
+    if (epi) car_oneshot_kernel<true><<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8, e);
+    else car_oneshot_kernel<false><<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8, e);
+  }
 }
 
 void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two_shot,
@@ -191,7 +236,8 @@ void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two
   const long n8 = n / 8;
   if (n8 == 0) return;
   dim3 grid(car_blocks(n8, world, two_shot != 0), world);
-  car_multi_kernel<<<grid, 256, 0, s>>>(m, n8, two_shot);
+  if (m.use_epi) car_multi_kernel<true><<<grid, 256, 0, s>>>(m, n8, two_shot);
+  else car_multi_kernel<false><<<grid, 256, 0, s>>>(m, n8, two_shot);
 }
 
 size_t custom_allreduce_signal_bytes() {

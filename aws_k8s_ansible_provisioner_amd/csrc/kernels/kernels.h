@@ -177,13 +177,26 @@ struct CarArgs {
   int rank, world;
   size_t half_elems;     // capacity in elements of one staging half
 };
+// Optional fused epilogue of the TP decode chain (the row-parallel O / down projection's
+// partial sums are all-reduced, then): s = bf16(bf16(sum) + residual); residual = s;
+// aout = bf16(s * ln[col]); ss[row] += s^2 -- the residual add + the elementwise half of the
+// next RMSNorm, whose row scale the consumer GEMM applies (dgemm ss_in).  Rows are d wide.
+struct CarEpi {
+  __bf16* residual;  // [M, d] in/out
+  const __bf16* ln;  // [d]
+  __bf16* aout;      // [M, d]
+  float* ss;         // [M] (+=; caller zeroes)
+  int d;             // row width (multiple of 512: one wave's 64 x 8 elements share a row)
+};
 void launch_custom_allreduce(const CarArgs& a, const void* in, void* out, long n, int two_shot,
-                             hipStream_t s);
+                             hipStream_t s, const CarEpi* epi = nullptr);
 size_t custom_allreduce_signal_bytes();
 struct CarMulti {  // test-only: every rank of a simulated group in one launch
   CarArgs args[8];
   const void* in[8];
   void* out[8];
+  CarEpi epi[8];
+  int use_epi;
 };
 void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two_shot,
                                    hipStream_t s);

@@ -669,6 +669,41 @@ void car_all_reduce(int64_t h, Tensor inp, Tensor out, bool two_shot) {
                                 two_shot ? 1 : 0, cur_stream());
 }
 
+static akap::CarEpi car_epi_of(Tensor& residual, Tensor& ln, Tensor& aout, Tensor& ss,
+                               int64_t n) {
+  CHECK_BF16(residual); CHECK_CONTIG(residual); CHECK_BF16(ln); CHECK_CONTIG(ln);
+  CHECK_BF16(aout); CHECK_CONTIG(aout);
+  const int64_t d = ln.numel();
+  TORCH_CHECK(d % 512 == 0, "car resnorm: row width must be a multiple of 512");
+  TORCH_CHECK(residual.numel() == n && aout.numel() == n && n % d == 0,
+              "car resnorm: residual / aout [M, d] like the message");
+  TORCH_CHECK(ss.scalar_type() == at::kFloat && ss.is_cuda() && ss.numel() >= n / d,
+              "car resnorm: ss fp32 [M]");
+  akap::CarEpi e{};
+  e.residual = (__bf16*)residual.data_ptr();
+  e.ln = (const __bf16*)ln.data_ptr();
+  e.aout = (__bf16*)aout.data_ptr();
+  e.ss = ss.data_ptr<float>();
+  e.d = (int)d;
+  return e;
+}
+
+// All-reduce of row-parallel partial sums fused with the decode chain's residual add and the
+// elementwise half of the next RMSNorm (see CarEpi): residual += sum; aout = residual * ln;
+// ss += row sums of residual^2.  `inp` is consumed (staged), nothing else is written.
+void car_all_reduce_resnorm(int64_t h, Tensor inp, Tensor residual, Tensor ln, Tensor aout,
+                            Tensor ss, bool two_shot) {
+  CarComm* c = car_get(h);
+  CHECK_GPU(inp); CHECK_BF16(inp); CHECK_CONTIG(inp);
+  TORCH_CHECK((size_t)inp.numel() <= c->args.half_elems, "message larger than the buffer");
+  for (int p = 0; p < c->args.world; ++p)
+    TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
+  const akap::CarEpi e = car_epi_of(residual, ln, aout, ss, inp.numel());
+  const c10::DeviceGuard g(inp.device());
+  akap::launch_custom_allreduce(c->args, inp.data_ptr(), nullptr, inp.numel(),
+                                two_shot ? 1 : 0, cur_stream(), &e);
+}
+
 // Test hook: wire communicators created in THIS process (one per simulated rank, all on
 // one GPU) to each other without IPC, so the kernel protocol can be exercised on 1 GPU.
 void car_link_local(int64_t h, std::vector<int64_t> peers) {
@@ -685,7 +720,8 @@ void car_link_local(int64_t h, std::vector<int64_t> peers) {
 // car_link_local) in ONE grid, blockIdx.y = rank, so all ranks are co-resident regardless
 // of how streams map to hardware queues.
 void car_all_reduce_multi(std::vector<int64_t> hs, std::vector<Tensor> ins,
-                          std::vector<Tensor> outs, bool two_shot) {
+                          std::vector<Tensor> outs, bool two_shot,
+                          std::optional<std::vector<Tensor>> epi) {
   const int W = hs.size();
   TORCH_CHECK(W >= 1 && W <= 8 && (int)ins.size() == W && (int)outs.size() == W, "W ranks");
   akap::CarMulti m{};
@@ -699,6 +735,12 @@ void car_all_reduce_multi(std::vector<int64_t> hs, std::vector<Tensor> ins,
     m.args[r] = c->args;
     m.in[r] = ins[r].data_ptr();
     m.out[r] = outs[r].data_ptr();
+    if (epi) {  // 4 tensors per rank: residual, ln, aout, ss
+      TORCH_CHECK((int)epi->size() == 4 * W, "epi: residual, ln, aout, ss per rank");
+      m.epi[r] = car_epi_of((*epi)[4 * r], (*epi)[4 * r + 1], (*epi)[4 * r + 2],
+                            (*epi)[4 * r + 3], n);
+      m.use_epi = 1;
+    }
   }
   const c10::DeviceGuard g(ins[0].device());
   akap::launch_custom_allreduce_multi(m, W, n, two_shot ? 1 : 0, cur_stream());
@@ -772,7 +814,10 @@ TORCH_LIBRARY(akap, m) {
   m.def("car_all_reduce(int h, Tensor inp, Tensor(a!) out, bool two_shot) -> ()");
   m.def("car_error(int h) -> int");
   m.def("car_link_local(int h, int[] peers) -> ()");
-  m.def("car_all_reduce_multi(int[] hs, Tensor[] ins, Tensor(a!)[] outs, bool two_shot) -> ()");
+  m.def("car_all_reduce_multi(int[] hs, Tensor[] ins, Tensor(a!)[] outs, bool two_shot, "
+        "Tensor(b!)[]? epi=None) -> ()");
+  m.def("car_all_reduce_resnorm(int h, Tensor inp, Tensor(a!) residual, Tensor ln, "
+        "Tensor(b!) aout, Tensor(c!) ss, bool two_shot) -> ()");
   m.def("car_destroy(int h) -> ()");
   m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def(
@@ -827,6 +872,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("car_all_reduce", &car_all_reduce);
   m.impl("l2_prefetch", &l2_prefetch);
   m.impl("car_all_reduce_multi", &car_all_reduce_multi);
+  m.impl("car_all_reduce_resnorm", &car_all_reduce_resnorm);
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);
   m.impl("embedding", &embedding);

@@ -319,7 +319,7 @@ class ModelRunner:
             t1 = time.time()
             gemm_tuner.tune_model(self.model, [b for b in self.buckets if b >= 16],
                                   log=self.log)
-            if self.model.ps.tp_size == 1 and os.environ.get("AKAP_FUSED_GEMM", "1") != "0":
+            if os.environ.get("AKAP_FUSED_GEMM", "1") != "0":
                 gemm_tuner.tune_fused(self.model, [b for b in self.buckets if b >= 16],
                                       log=self.log)
             self.log(f"[runner] GEMM tuning {time.time() - t1:.1f}s")

@@ -310,8 +310,8 @@ class DecoderLM:
         cfg = self.cfg
         T = input_ids.shape[0]
         eps = cfg.rms_eps
-        if (not batch.is_prefill and FUSED_DECODE and FUSED_GEMM and self.ps.tp_size == 1
-                and self.device.type == "cuda"):
+        if (not batch.is_prefill and FUSED_DECODE and FUSED_GEMM and self.device.type == "cuda"
+                and all(l.moe is None for l in self.layers)):
             from ..ops import gemm_tuner
 
             plan = gemm_tuner.fused_plan(T)
@@ -361,8 +361,11 @@ class DecoderLM:
         RMSNorm run in the O / down projections' epilogues (which also accumulate the
         per-row sum of squares), the norm's row scale in the consumer GEMM's epilogue, and
         SwiGLU in the gate|up projection's epilogue -- no separate norm / activation kernels.
-        Single rank (no all-reduce between GEMM and residual add); plan from
-        gemm_tuner.tune_fused: projection -> (split-K, prefetch depth, LDS-DMA tile width)."""
+        Tensor parallel: the row-parallel O / down projections store their partial sums and
+        the residual epilogue moves into the all-reduce (comm.tp_all_reduce_resnorm: the
+        custom xGMI kernel applies it in its store pass), so a TP layer is still 4 GEMM
+        launches + 2 all-reduce launches + attention.  Plan from gemm_tuner.tune_fused:
+        projection -> (split-K, prefetch depth, LDS-DMA tile width[, ring, in-launch])."""
         T = input_ids.shape[0]
         eps = self.cfg.rms_eps
         L = len(self.layers)
@@ -372,6 +375,7 @@ class DecoderLM:
             return dict(splitk=s_, pf=p_, bn=b_, ns=n_, inlaunch=bool(i_))
 
         c_qkv, c_o, c_gu, c_d = (cfg_(n) for n in ("w_qkv", "w_o", "w_gate_up", "w_down"))
+        tp = self.ps.tp_size
         residual = self.embed_tokens(input_ids)
         ss = torch.zeros(2 * L, T, dtype=torch.float32, device=self.device)
         a1 = ops.rms_norm(residual, self.layers[0].ln1, eps)
@@ -385,18 +389,28 @@ class DecoderLM:
                 self.hq // self.hkv, self.scale, eps, workspace=batch.workspace,
                 num_parts=batch.num_parts, part_size=batch.part_size)
             a2 = torch.empty_like(residual)
-            ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, eps=eps, out=residual,
-                      epi=ops.EPI_RESNORM, ss_out=ss[2 * li], a_out=a2, ln_out=lw.ln2, **c_o)
+            if tp > 1:
+                part = ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, eps=eps, **c_o)
+                comm.tp_all_reduce_resnorm(part, residual, lw.ln2, a2, ss[2 * li])
+            else:
+                ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, eps=eps, out=residual,
+                          epi=ops.EPI_RESNORM, ss_out=ss[2 * li], a_out=a2, ln_out=lw.ln2,
+                          **c_o)
             act = ops.dgemm(a2, lw.w_gate_up, eps=eps, ss_in=ss[2 * li], epi=ops.EPI_SILU,
                             **c_gu)
             if li + 1 < L:
                 a1 = torch.empty_like(residual)
-                ops.dgemm(act, lw.w_down, eps=eps, out=residual, epi=ops.EPI_RESNORM,
-                          ss_out=ss[2 * li + 1], a_out=a1, ln_out=self.layers[li + 1].ln1,
-                          **c_d)
+                if tp > 1:
+                    part = ops.dgemm(act, lw.w_down, eps=eps, **c_d)
+                    comm.tp_all_reduce_resnorm(part, residual, self.layers[li + 1].ln1, a1,
+                                               ss[2 * li + 1])
+                else:
+                    ops.dgemm(act, lw.w_down, eps=eps, out=residual, epi=ops.EPI_RESNORM,
+                              ss_out=ss[2 * li + 1], a_out=a1, ln_out=self.layers[li + 1].ln1,
+                              **c_d)
                 ss_in = ss[2 * li + 1]
             else:
-                x = ops.dgemm(act, lw.w_down, eps=eps, **c_d)
+                x = comm.tp_all_reduce(ops.dgemm(act, lw.w_down, eps=eps, **c_d))
         h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
         return h
 

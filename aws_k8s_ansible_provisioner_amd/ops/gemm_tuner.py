@@ -196,11 +196,15 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
     dev = model.layers[0].w_o.device
     dt = model.layers[0].w_o.dtype
     chosen = {}
+    # tensor parallel: O / down store partial sums (their residual epilogue runs in the
+    # all-reduce, comm.tp_all_reduce_resnorm), so they are timed with the plain store
+    roles = _FUSED_ROLES if model.ps.tp_size == 1 else tuple(
+        (n, 0 if n in ("w_o", "w_down") else e) for n, e in _FUSED_ROLES)
     for M in Ms:
         t_unfused = _time_unfused(M, model)
         plan_m, t_fused = {}, 0.0
         detail = []
-        for name, epi in _FUSED_ROLES:
+        for name, epi in roles:
             ws_ = [getattr(l, name) for l in model.layers]
             N, K = ws_[0].shape
             t_plain = _time_best_plain(M, name, ws_)
@@ -245,6 +249,22 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
         chosen[M] = (t_fused, t_unfused, plan_m)
         if verbose:
             log(f"[gemm-tuner] M={M} fused/plain us: " + ", ".join(detail))
+    if model.ps.tp_size > 1:
+        # every TP rank must run the same chain (the same collectives per step): rank 0's
+        # timing decides
+        from ..parallel import comm
+
+        import torch.distributed as dist
+
+        g = model.ps.tp_group
+        plans = comm.broadcast_object({m: _FUSED.get(m) for m in Ms},
+                                      src=dist.get_global_rank(g, 0) if g is not None else 0,
+                                      group=g)
+        for m, pl in plans.items():
+            if pl is None:
+                _FUSED.pop(m, None)
+            else:
+                _FUSED[m] = pl
     used = [m for m in Ms if m in _FUSED]
     log("[gemm-tuner] fused decode layer chain (us/layer fused vs unfused): " + ", ".join(
         f"M={m} {c[0]:.1f}/{c[1]:.1f}" + ("*" if m in _FUSED else "")

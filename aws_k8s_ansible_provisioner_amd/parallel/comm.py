@@ -30,14 +30,36 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def tp_all_reduce_resnorm(partial: torch.Tensor, residual: torch.Tensor, ln: torch.Tensor,
+                          a_out: torch.Tensor, ss: torch.Tensor) -> None:
+    """Row-parallel partial sums -> the decode chain's residual epilogue on every TP rank:
+    residual += all_reduce(partial); a_out = residual * ln; ss += row sums of residual^2
+    (the next RMSNorm's row scale is applied by the consumer GEMM, dgemm ss_in).  Decode
+    sizes take the custom xGMI all-reduce with this epilogue fused into its store pass (one
+    launch); otherwise RCCL all_reduce + the same elementwise math."""
+    st = get_state()
+    if st.tp_size > 1 and st.car is not None and st.car.should_use(partial) and \
+            ln.numel() % 512 == 0:
+        st.car.all_reduce_resnorm(partial, residual, ln, a_out, ss)
+        return
+    if st.tp_size > 1:
+        dist.all_reduce(partial, group=st.tp_group)
+    r = (partial.float() + residual.float()).to(residual.dtype)
+    residual.copy_(r)
+    a_out.copy_((r.float() * ln.float()).to(a_out.dtype))
+    ss[: r.shape[0]] += r.float().pow(2).sum(-1)
+
+
 def tp_all_gather_last(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Gather shards along the last dim: [.., n] x tp -> [.., n*tp]."""
+    """Gather shards along the last dim: [.., n] x tp -> [.., n*tp].  One all_gather into a
+    single [tp, .., n] buffer (no per-rank tensor list) + one transposing copy."""
     st = get_state()
     if st.tp_size == 1:
         return x
-    parts = [torch.empty_like(x) for _ in range(st.tp_size)]
-    dist.all_gather(parts, x.contiguous(), group=st.tp_group)
-    res = torch.cat(parts, dim=-1)
+    x = x.contiguous()
+    buf = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(buf, x, group=st.tp_group)
+    res = buf.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
     if out is not None:
         out.copy_(res)
         return out

@@ -62,6 +62,14 @@ class CustomAllReduce:
         torch.ops.akap.car_all_reduce(self.h, x, out, two)
         return out
 
+    def all_reduce_resnorm(self, x: torch.Tensor, residual: torch.Tensor, ln: torch.Tensor,
+                           a_out: torch.Tensor, ss: torch.Tensor) -> None:
+        """x = this rank's row-parallel partial sums [M, d]; after the exchange every rank has
+        residual += sum, a_out = residual * ln, ss += row sums of residual^2 (the decode
+        chain's residual-add epilogue, fused into the all-reduce's store pass)."""
+        two = x.numel() * 2 > self.oneshot_bytes and self.world > 2
+        torch.ops.akap.car_all_reduce_resnorm(self.h, x, residual, ln, a_out, ss, two)
+
     def error(self) -> int:
         return int(torch.ops.akap.car_error(self.h))
 

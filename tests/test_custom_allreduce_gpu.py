@@ -186,3 +186,45 @@ def test_custom_allreduce_ipc_two_processes():
         import numpy as np
         assert np.array_equal(out[0][1][it], out[1][1][it])
         assert np.abs(out[0][1][it] - exp).max() <= 0.05
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("two_shot", [False, True])
+@pytest.mark.parametrize("M,d", [(1, 512), (37, 1024), (64, 8192)])
+def test_custom_allreduce_resnorm_epilogue(world, two_shot, M, d):
+    """All-reduce of row-parallel partial sums fused with the TP decode chain's residual
+    epilogue: residual += sum, aout = residual * ln, ss += row sums of residual^2 -- checked
+    against fp32 references, identical on every rank (fixed summation order)."""
+    ops.load_native(required=True)
+    n = M * d
+    hs = [torch.ops.akap.car_create(0, r, world, 1 << 20) for r in range(world)]
+    try:
+        for h in hs:
+            torch.ops.akap.car_link_local(h, hs)
+        for it in range(2):
+            torch.manual_seed(7 * it + world + n)
+            xs = [torch.randn(n, dtype=torch.bfloat16, device=DEV) * 0.3 for _ in range(world)]
+            res0 = torch.randn(M, d, dtype=torch.bfloat16, device=DEV)
+            ln = (torch.rand(d, device=DEV) + 0.5).to(torch.bfloat16)
+            res = [res0.clone() for _ in range(world)]
+            aout = [torch.empty(M, d, dtype=torch.bfloat16, device=DEV) for _ in range(world)]
+            ss = [torch.zeros(M, device=DEV) for _ in range(world)]
+            outs = [torch.empty_like(x) for x in xs]  # unused by the epilogue form
+            epi = []
+            for r in range(world):
+                epi += [res[r], ln, aout[r], ss[r]]
+            torch.ops.akap.car_all_reduce_multi(hs, xs, outs, two_shot, epi)
+            torch.cuda.synchronize()
+            assert all(torch.ops.akap.car_error(h) == 0 for h in hs)
+            s = (_ref_sum(xs).float().view(M, d) + res0.float()).to(torch.bfloat16)
+            for r in range(world):
+                assert torch.equal(res[r], res[0]) and torch.equal(aout[r], aout[0])
+                assert torch.allclose(ss[r], ss[0])
+            assert (res[0].float() - s.float()).abs().max().item() <= 0.05 * world
+            assert (aout[0].float() - res[0].float() * ln.float()).abs().max().item() <= \
+                0.02 * aout[0].float().abs().max().item()
+            assert torch.allclose(ss[0], res[0].float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
+    finally:
+        torch.cuda.synchronize()
+        for h in hs:
+            torch.ops.akap.car_destroy(h)
