@@ -57,9 +57,12 @@ def tp_all_gather_last(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> t
     if st.tp_size == 1:
         return x
     x = x.contiguous()
-    buf = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(buf, x, group=st.tp_group)
-    res = buf.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
+    flat = x.reshape(1, -1) if x.dim() == 1 else x.reshape(-1, x.shape[-1])
+    buf = torch.empty(st.tp_size * flat.shape[0], flat.shape[1], dtype=x.dtype,
+                      device=x.device)
+    dist.all_gather_into_tensor(buf, flat, group=st.tp_group)  # rank-major rows
+    res = buf.view(st.tp_size, flat.shape[0], flat.shape[1]).movedim(0, 1).reshape(
+        *x.shape[:-1], st.tp_size * x.shape[-1])
     if out is not None:
         out.copy_(res)
         return out
