@@ -143,7 +143,9 @@ __device__ __forceinline__ void car_twoshot(const CarArgs& a, int bid, int nblk,
   bf16x8* mine = reinterpret_cast<bf16x8*>(a.bufs[a.rank] + par);
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
   const long stride = (long)nblk * 256;
-  const long s8 = (n8 + a.world - 1) / a.world;
+  // slices are whole 64-vector groups: with the epilogue a wave's 64 lanes must stay inside one
+  // slice (and so one row, d % 512 == 0) for car_store's wave-wide row sum of squares
+  const long s8 = ((n8 + a.world - 1) / a.world + 63) / 64 * 64;
   // staged with the same slice-relative index->block map the reduce uses below, so block
   // b of a peer reads exactly what block b of this rank wrote before its flag
   for (int p = 0; p < a.world; ++p) {
