@@ -18,7 +18,7 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                void* v_cache, const int64_t* positions, const int64_t* slots,
                                const float* cos_sin, const void* q_w, const void* k_w, int T,
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
-                               hipStream_t s, int kv_fp8 = 0);
+                               hipStream_t s, int kv_fp8 = 0, int v_per_token = 0);
 void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void* v_cache,
                               const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s,
                               int kv_fp8 = 0);
@@ -107,6 +107,35 @@ bool gdgemm_supported(int M, int N, int K, int splitk, int bn);
 // fp32 workspace floats a gdgemm split-K launch needs (tile-padded slabs)
 long gdgemm_ws_floats(int M, int N, int splitk, int bn);
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st);
+
+// ---- wgemm.hip: wide-row weight-streaming GEMM (LM head) Y[M,N] = X[M,K] . W[N,K]^T ----
+struct WGemmArgs {
+  const void* X;  // bf16 [M, K] (row stride ldx)
+  const void* W;  // bf16 [N, K] (row stride ldw)
+  void* Y;        // bf16 [M, N] (row stride ldy)
+  int M, N, K, ldx, ldw, ldy;
+};
+bool wgemm_supported(int M, int N, int K, int ldx, int ldw, int ldy);
+void launch_wgemm(const WGemmArgs& p, hipStream_t st);
+
+// ---- qkvgemm.hip: QKV projection + per-head q/k RMSNorm + RoPE + K/V cache write ----
+struct QkvRopeArgs {
+  const void* X;        // bf16 [M, K] (row stride ldx): the normed layer input
+  const void* W;        // bf16 [(Hq + 2 Hkv) * 128, K] (row stride ldw)
+  const float* ss_in;   // optional [M] sums of squares -> rows scaled by rsqrt(ss/K + eps)
+  void* q_out;          // bf16 [M, Hq, 128]
+  void* k_cache;        // [NB, Hkv, BS, 128] (K-fragment order), bf16 or fp8 bytes
+  void* v_cache;        // [NB, Hkv, BS/8, 128, 8]
+  const int64_t* positions;  // [M]
+  const int64_t* slots;      // [M] (-1: no cache write)
+  const float* cos_sin;      // [max_pos, 128] = cos | sin
+  const void* q_w;           // [128] or nullptr
+  const void* k_w;
+  float eps;
+  int M, K, ldx, ldw, Hq, Hkv, BS, rope, kv_fp8;
+};
+bool qkv_rope_gemm_supported(int M, int K, int bm, int ns);
+void launch_qkv_rope_gemm(const QkvRopeArgs& p, int bm, int ns, hipStream_t st);
 
 // ---- sampling.hip ----
 struct SampleParams {

@@ -193,16 +193,46 @@ __device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_str
   }
 }
 
+// v role for decode batches (one new token per sequence: every run is a single token, so
+// the span role's leader scan degenerates into one serial scatter per token): 16 lanes per
+// (token, kv head), lane i writes dims [8i, 8i+8) of the token's slot.
+template <bool F8>
+__device__ __forceinline__ void v_item(const bf16* __restrict__ qkv, int qkv_stride,
+                                       void* __restrict__ v_cache,
+                                       const int64_t* __restrict__ slots, int T, int Hq, int Hkv,
+                                       int BS, int vblk) {
+  constexpr int D = 128;
+  const int item = (vblk * 256 + threadIdx.x) >> 4;
+  const int li = threadIdx.x & 15;
+  if (item >= T * Hkv) return;
+  const int t = item / Hkv, vh = item % Hkv;
+  const int64_t slot = slots[t];
+  if (slot < 0) return;
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(qkv + (size_t)t * qkv_stride +
+                                                    (Hq + Hkv + vh) * D + 8 * li);
+  const int64_t blk = slot / BS;
+  const int off = (int)(slot % BS);
+  const size_t e = ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + (off & 7) +
+                   (size_t)(8 * li) * 8;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if constexpr (F8) reinterpret_cast<uint8_t*>(v_cache)[e + 8 * k] = f32_to_fp8((float)v[k]);
+    else reinterpret_cast<bf16*>(v_cache)[e + 8 * k] = v[k];
+  }
+}
+
 template <bool F8>
 __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
     const bf16* __restrict__ qkv, int qkv_stride, bf16* __restrict__ q_out,
     void* __restrict__ k_cache, void* __restrict__ v_cache, const int64_t* __restrict__ positions,
     const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
     const bf16* __restrict__ q_w, const bf16* __restrict__ k_w, int T, int Hq, int Hkv, int BS,
-    float eps, int apply_rope, int qk_blocks) {
+    float eps, int apply_rope, int qk_blocks, int v_per_token) {
   if ((int)blockIdx.x < qk_blocks)
     qk_item<F8>(qkv, qkv_stride, q_out, k_cache, positions, slots, cos_sin, q_w, k_w, T, Hq, Hkv,
                 BS, eps, apply_rope);
+  else if (v_per_token)
+    v_item<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks);
   else
     v_span<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks);
 }
@@ -211,16 +241,17 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                void* v_cache, const int64_t* positions, const int64_t* slots,
                                const float* cos_sin, const void* q_w, const void* k_w, int T,
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
-                               hipStream_t s, int kv_fp8) {
+                               hipStream_t s, int kv_fp8, int v_per_token) {
   if (T == 0 || D != 128) return;
   const long qk_threads = (long)T * (Hq + Hkv) * 16;
   const int qk_blocks = (int)((qk_threads + 255) / 256);
-  const int v_blocks = ((T + V_SPAN - 1) / V_SPAN) * Hkv;
+  const int v_blocks = v_per_token ? (int)(((long)T * Hkv * 16 + 255) / 256)
+                                   : ((T + V_SPAN - 1) / V_SPAN) * Hkv;
   const dim3 grid(qk_blocks + v_blocks);
 #define QKR(F8)                                                                                 \
   qk_norm_rope_cache_kernel<F8><<<grid, 256, 0, s>>>(                                           \
       (const bf16*)qkv, qkv_stride, (bf16*)q_out, k_cache, v_cache, positions, slots, cos_sin, \
-      (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope, qk_blocks)
+      (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope, qk_blocks, v_per_token)
   if (kv_fp8) QKR(true); else QKR(false);
 #undef QKR
 }

@@ -59,7 +59,7 @@ void fused_add_rmsnorm(Tensor out, Tensor residual, Tensor x, Tensor w, double e
 void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache,
                         Tensor positions, Tensor slots, Tensor cos_sin,
                         std::optional<Tensor> q_w, std::optional<Tensor> k_w, int64_t Hq,
-                        int64_t Hkv, double eps, bool apply_rope) {
+                        int64_t Hkv, double eps, bool apply_rope, bool decode) {
   CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv); CHECK_CONTIG(q_out);
   CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
   TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong,
@@ -80,7 +80,7 @@ void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache
       qkv.data_ptr(), qkv.stride(0), q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
       positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
       q_w ? q_w->data_ptr() : nullptr, k_w ? k_w->data_ptr() : nullptr, T, Hq, Hkv, D, BS,
-      (float)eps, apply_rope ? 1 : 0, cur_stream(), kv_fp8_of(k_cache, v_cache));
+      (float)eps, apply_rope ? 1 : 0, cur_stream(), kv_fp8_of(k_cache, v_cache), decode ? 1 : 0);
 }
 
 void reshape_and_cache(Tensor k, Tensor v, Tensor k_cache, Tensor v_cache, Tensor slots) {
@@ -360,6 +360,64 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   }
   const c10::DeviceGuard g(x.device());
   akap::launch_dgemm(a, (int)pro, (int)splitk, (int)pf, cur_stream());
+}
+
+// Wide-row weight-streaming GEMM (LM head): out[M, N] = x[M, K] @ w[N, K]^T, one workgroup
+// per column tile holding all (<= 256) rows, so the weights cross HBM -> CU once.
+void wgemm(Tensor out, Tensor x, Tensor w) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "wgemm: 2-D tensors");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == N, "wgemm: shapes");
+  TORCH_CHECK(akap::wgemm_supported(M, N, K, x.stride(0), w.stride(0), out.stride(0)),
+              "wgemm: K % 64 == 0 and 16-byte aligned rows");
+  akap::WGemmArgs a{x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K,
+                    (int)x.stride(0), (int)w.stride(0), (int)out.stride(0)};
+  const c10::DeviceGuard g(x.device());
+  akap::launch_wgemm(a, cur_stream());
+}
+
+// QKV projection with the decode attention layer's per-head epilogue (csrc/kernels/
+// qkvgemm.hip): q_out = rope(norm(q)), k = rope(norm(k)) and v written to the paged caches.
+void qkv_rope_gemm(Tensor x, Tensor w, std::optional<Tensor> ss_in, Tensor q_out,
+                   Tensor k_cache, Tensor v_cache, Tensor positions, Tensor slots,
+                   Tensor cos_sin, std::optional<Tensor> q_w, std::optional<Tensor> k_w,
+                   int64_t Hq, int64_t Hkv, double eps, bool apply_rope, int64_t bm, int64_t ns) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(q_out);
+  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_CONTIG(q_out);
+  CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
+  const int M = x.size(0), K = w.size(1);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) == K, "qkv_rope_gemm: x [M, K]");
+  TORCH_CHECK(w.size(0) == (Hq + 2 * Hkv) * 128, "qkv_rope_gemm: w [(Hq + 2 Hkv) * 128, K]");
+  TORCH_CHECK(q_out.numel() >= (int64_t)M * Hq * 128, "qkv_rope_gemm: q_out [M, Hq, 128]");
+  TORCH_CHECK(k_cache.size(3) == 128 && k_cache.size(1) == Hkv, "qkv_rope_gemm: k_cache layout");
+  const int BS = k_cache.size(2);
+  TORCH_CHECK(BS % 32 == 0 && v_cache.dim() == 5 && v_cache.size(2) * 8 == BS,
+              "qkv_rope_gemm: cache block size");
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong &&
+                  positions.numel() >= M && slots.numel() >= M,
+              "qkv_rope_gemm: int64 positions / slots [M]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(-1) == 128, "cos_sin fp32");
+  TORCH_CHECK(akap::qkv_rope_gemm_supported(M, K, (int)bm, (int)ns) && x.stride(0) % 8 == 0 &&
+                  w.stride(0) % 8 == 0,
+              "qkv_rope_gemm: K % 64, bm 32|64, ns 3|6, aligned rows");
+  if (ss_in)
+    TORCH_CHECK(ss_in->scalar_type() == at::kFloat && ss_in->numel() >= M, "ss_in fp32 [M]");
+  akap::QkvRopeArgs a{};
+  a.X = x.data_ptr(); a.W = w.data_ptr();
+  a.ss_in = ss_in ? ss_in->data_ptr<float>() : nullptr;
+  a.q_out = q_out.data_ptr(); a.k_cache = k_cache.data_ptr(); a.v_cache = v_cache.data_ptr();
+  a.positions = positions.data_ptr<int64_t>(); a.slots = slots.data_ptr<int64_t>();
+  a.cos_sin = cos_sin.data_ptr<float>();
+  a.q_w = q_w ? q_w->data_ptr() : nullptr;
+  a.k_w = k_w ? k_w->data_ptr() : nullptr;
+  a.eps = (float)eps;
+  a.M = M; a.K = K; a.ldx = x.stride(0); a.ldw = w.stride(0);
+  a.Hq = Hq; a.Hkv = Hkv; a.BS = BS; a.rope = apply_rope ? 1 : 0;
+  a.kv_fp8 = kv_fp8_of(k_cache, v_cache);
+  const c10::DeviceGuard g(x.device());
+  akap::launch_qkv_rope_gemm(a, (int)bm, (int)ns, cur_stream());
 }
 
 bool dgemm_ok(int64_t M, int64_t N, int64_t K, int64_t splitk, int64_t pf) {
@@ -773,7 +831,7 @@ TORCH_LIBRARY(akap, m) {
   m.def(
       "qk_norm_rope_cache(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, "
       "Tensor positions, Tensor slots, Tensor cos_sin, Tensor? q_w, Tensor? k_w, int Hq, int Hkv, "
-      "float eps, bool apply_rope) -> ()");
+      "float eps, bool apply_rope, bool decode=False) -> ()");
   m.def("reshape_and_cache(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def(
@@ -806,6 +864,10 @@ TORCH_LIBRARY(akap, m) {
       "Tensor? r=None, Tensor(c!)? rout=None, Tensor? ln=None, float eps=1e-6, int epi=0, "
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
       "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None) -> ()");
+  m.def("wgemm(Tensor(a!) out, Tensor x, Tensor w) -> ()");
+  m.def("qkv_rope_gemm(Tensor x, Tensor w, Tensor? ss_in, Tensor(a!) q_out, Tensor(b!) k_cache, "
+        "Tensor(c!) v_cache, Tensor positions, Tensor slots, Tensor cos_sin, Tensor? q_w, "
+        "Tensor? k_w, int Hq, int Hkv, float eps, bool apply_rope, int bm, int ns) -> ()");
   m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
   m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");
@@ -863,6 +925,8 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("gemm", &gemm);
   m.impl("dgemm", &dgemm);
+  m.impl("wgemm", &wgemm);
+  m.impl("qkv_rope_gemm", &qkv_rope_gemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

@@ -81,10 +81,14 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
 
 # ----------------------------------------------------------------------------- rope/cache
 def qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
-                       num_q_heads: int, num_kv_heads: int, eps: float, apply_rope: bool = True):
+                       num_q_heads: int, num_kv_heads: int, eps: float, apply_rope: bool = True,
+                       decode: bool = False):
+    """decode=True: one new token per sequence (V written per token instead of by the
+    prefill role's 64-token span scan)."""
     if _native(qkv):
         torch.ops.akap.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin,
-                                          q_w, k_w, num_q_heads, num_kv_heads, eps, apply_rope)
+                                          q_w, k_w, num_q_heads, num_kv_heads, eps, apply_rope,
+                                          decode)
         return q_out
     ref.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
                            num_q_heads, num_kv_heads, eps, apply_rope)
@@ -192,6 +196,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
         from . import gemm_tuner
 
         choice = gemm_tuner.lookup(M, w.shape[0], w.shape[1])
+        if choice is not None and choice[0] == "wgemm" and x.stride(-1) == 1:
+            return wgemm(x, w, out=out)
         if choice is not None:  # measured at engine start (cold weights, real layers)
             if choice[0] == "dgemm" and x.stride(-1) == 1:
                 bn, ns, inl = (tuple(choice[3:]) + (0, 0, False))[:3]
@@ -223,6 +229,42 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
             ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
     torch.ops.akap.gemm(out, x, w, ws, s)
     return out
+
+
+def wgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T by the wide-row weight-streaming kernel (csrc/kernels/wgemm.hip): one
+    workgroup owns all (<= 256) rows of a column tile, so each weight byte crosses HBM -> CU
+    once -- the decode LM head.  CPU: plain matmul."""
+    M, N = x.shape[0], w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if not _native(x):
+        out.copy_(torch.nn.functional.linear(x.float(), w.float()).to(out.dtype))
+        return out
+    torch.ops.akap.wgemm(out, x, w)
+    return out
+
+
+def qkv_rope_gemm(x, w, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
+                  num_q_heads: int, num_kv_heads: int, eps: float, ss_in=None,
+                  apply_rope: bool = True, bm: int = 32, ns: int = 6):
+    """QKV projection with the decode attention layer's per-head epilogue
+    (csrc/kernels/qkvgemm.hip): qkv = x @ w.T (rows scaled by rsqrt(ss_in / K + eps) when
+    ss_in is given), then per-head q/k RMSNorm (q_w / k_w, optional) + NeoX RoPE; q goes to
+    q_out [M, Hq, 128], the new token's k / v into the paged caches at `slots`.  Equivalent
+    to dgemm(...) followed by qk_norm_rope_cache(...), in one launch."""
+    if _native(x):
+        torch.ops.akap.qkv_rope_gemm(x, w, ss_in, q_out, k_cache, v_cache, positions, slots,
+                                     cos_sin, q_w, k_w, num_q_heads, num_kv_heads, eps,
+                                     apply_rope, bm, ns)
+        return q_out
+    M, K = x.shape[0], w.shape[1]
+    y = torch.nn.functional.linear(x.float(), w.float())
+    if ss_in is not None:
+        y = y * torch.rsqrt(ss_in[:M].float() / K + eps)[:, None]
+    ref.qk_norm_rope_cache(y.to(x.dtype), q_out, k_cache, v_cache, positions, slots, cos_sin,
+                           q_w, k_w, num_q_heads, num_kv_heads, eps, apply_rope)
+    return q_out
 
 
 PRO_PLAIN, PRO_ADDNORM, PRO_SILU = 0, 1, 2

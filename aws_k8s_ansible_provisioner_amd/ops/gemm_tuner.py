@@ -24,7 +24,7 @@ from typing import Optional, Sequence
 import torch
 
 Choice = tuple  # ("torch",) | ("hip", splitk) | ("dgemm", splitk, prefetch_depth[, lds_dma_bn,
-#                 ring_slots, in_launch_combine])
+#                 ring_slots, in_launch_combine]) | ("wgemm",)
 _PLAN: dict = {}
 
 
@@ -97,6 +97,10 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
     best: Choice = ("torch",)
     t_best = _timed(lambda i: torch.nn.functional.linear(x, weights[i % n]), n)
     t_torch = t_best
+    if K % 64 == 0:  # wide-row weight-streaming kernel (csrc/kernels/wgemm.hip)
+        t = _timed(lambda i: torch.ops.akap.wgemm(y, x, weights[i % n]), n)
+        if t < t_best:
+            best, t_best = ("wgemm",), t
     for s in splits:
         if K // s < 256 or K % (64 * s):
             continue
@@ -143,10 +147,17 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
     for M in Ms:
         for (name, shape), ws in groups.items():
             summary[(M, name)] = tune(M, ws)
+    lm = getattr(model, "lm_head", None)
+    if lm is not None and lm.is_cuda:
+        # the decode LM head: hipBLASLt vs the wide-row kernel only (split-K slabs of a
+        # vocab-wide output would be GBs)
+        for M in Ms:
+            summary[(M, "lm_head")] = tune(M, [lm], splits=(), pfs=(), bns=())
     wins = {k: v for k, v in summary.items() if v[0] != "torch"}
     log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, HIP kernel chosen for "
         f"{len(wins)}: " + ", ".join(
-            f"M={m} {n} {c[0]} s{c[1]}" + (f"p{c[2]}" if len(c) == 3 else "") +
+            f"M={m} {n} {c[0]}" + (f" s{c[1]}" if len(c) > 1 else "") +
+            (f"p{c[2]}" if len(c) == 3 else "") +
             (_gd_name(c[3:]) if len(c) > 3 else "")
             for (m, n), c in sorted(wins.items())))
     return summary
@@ -289,6 +300,9 @@ def _time_best_plain(M: int, name: str, weights) -> float:
         return _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, c[1], c[2],
                                                      None, None, None, 1e-6, 0, None, None,
                                                      None, None, 0), n)
+    if c[0] == "wgemm":
+        y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)
+        return _timed(lambda i: torch.ops.akap.wgemm(y, x, weights[i % n]), n)
     if c[0] == "hip":
         ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)

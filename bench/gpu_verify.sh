@@ -11,7 +11,7 @@ echo "smoke ok"
 timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 > gpurun_out/${TAG}_bench.log 2>&1
 echo "bench ok"
 tail -1 gpurun_out/${TAG}_bench.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 1 --warmup 1 > gpurun_out/${TAG}_prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 1 --warmup 1 > gpurun_out/${TAG}_prof.log 2>&1
 echo "prof ok"
 # keep only the stats summaries (the full trace would exceed gpurun's 64 MiB pull-back)
 find gpurun_out/${TAG}_prof -type f ! -name '*stats*' -delete

@@ -642,3 +642,125 @@ def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
         out = ops.dgemm(x, w, splitk=splitk, bn=bn, epi=epi, ss_in=ssi, eps=eps, **kw)
         want = ref.silu_and_mul(y.to(torch.bfloat16)).float()
         _close(out, want, atol=2e-2 * want.abs().max().item())
+
+
+@pytest.mark.parametrize("M", [1, 16, 37, 64, 100, 128, 200, 256, 300])
+@pytest.mark.parametrize("N,K", [(1000, 64), (4100, 1024), (2056, 2048)])
+def test_wide_row_gemm(M, N, K):
+    """wgemm.hip (the decode LM head kernel): every row tile width (64/128/256 rows per
+    workgroup, and > 256 rows over several), partial column tiles (N % 8 != 0 included)
+    vs an fp32 matmul."""
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    # output rows padded to a multiple of 8 (16-byte aligned row starts); N itself need not be
+    out = torch.full((M, N + (-N) % 8), float("nan"), device=DEV, dtype=torch.bfloat16)[:, :N]
+    ops.wgemm(x, w, out=out)
+    exp = x.float() @ w.float().T
+    _close(out, exp, atol=0.02 * math.sqrt(K / 64), rtol=1e-2)
+
+
+def test_wide_row_gemm_strided_rows_in_graph():
+    """Strided input rows (a view of a larger buffer) and replay from a captured graph."""
+    torch.manual_seed(1)
+    buf = torch.randn(256, 1024 + 64, device=DEV, dtype=torch.bfloat16)
+    x = buf[:, :1024]
+    w = torch.randn(3000, 1024, device=DEV, dtype=torch.bfloat16) * 0.05
+    out = torch.empty(256, 3000, device=DEV, dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ops.wgemm(x, w, out=out)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        ops.wgemm(x, w, out=out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    _close(out, x.float() @ w.float().T, atol=0.1, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 16, 45, 64, 100, 256])
+@pytest.mark.parametrize("bm,ns", [(32, 6), (64, 3)])
+@pytest.mark.parametrize("qk_norm,ss", [(True, True), (False, False)])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_qkv_rope_gemm(M, bm, ns, qk_norm, ss, fp8):
+    """qkvgemm.hip vs the unfused pipeline (fp32 GEMM with the input norm's row scale ->
+    bf16 -> reference q/k-norm + RoPE + cache write): q rows, the written K (fragment order)
+    and V (8-token groups) slots, and untouched cache elsewhere (slot -1 rows write nothing)."""
+    torch.manual_seed(M + bm)
+    hq, hkv, D, BS, K = 16, 8, 128, 32, 1024
+    NB = (M + 1) * 2
+    x = torch.randn(M, K, dtype=torch.bfloat16)
+    w = torch.randn((hq + 2 * hkv) * D, K, dtype=torch.bfloat16) * 0.03
+    ssv = (torch.rand(M) * 2 + 0.5) * K if ss else None
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int64)
+    slots = torch.randperm(NB * BS)[:M].to(torch.int64)
+    if M > 3:
+        slots[3] = -1
+    cs = ref.rope_cos_sin(4096, D, 1e6)
+    qw = torch.randn(D).bfloat16() if qk_norm else None
+    kw = torch.randn(D).bfloat16() if qk_norm else None
+    y = x.float() @ w.float().T
+    if ss:
+        y = y * torch.rsqrt(ssv / K + 1e-6)[:, None]
+    kc_r = torch.zeros(NB, hkv, BS, D).bfloat16()
+    vc_r = torch.zeros(NB, hkv, BS // 8, D, 8).bfloat16()
+    q_r = torch.empty(M, hq, D).bfloat16()
+    ref.qk_norm_rope_cache(y.bfloat16(), q_r, kc_r, vc_r, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
+    dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
+    kg = torch.zeros(NB, hkv, BS, D, device=DEV, dtype=dt)
+    vg = torch.zeros(NB, hkv, BS // 8, D, 8, device=DEV, dtype=dt)
+    if fp8:
+        kg, vg = kg.view(torch.uint8), vg.view(torch.uint8)
+    q_out = torch.empty(M, hq, D, device=DEV, dtype=torch.bfloat16)
+    g = lambda t: None if t is None else t.to(DEV)  # noqa: E731
+    ops.qkv_rope_gemm(x.to(DEV), w.to(DEV), q_out, kg, vg, pos.to(DEV), slots.to(DEV),
+                      cs.to(DEV), g(qw), g(kw), hq, hkv, 1e-6, ss_in=g(ssv), bm=bm, ns=ns)
+    torch.cuda.synchronize()
+    _close(q_out, q_r, atol=5e-2, rtol=3e-2)
+    if fp8:
+        kg = kg.view(torch.float8_e4m3fn).float()
+        vg = vg.view(torch.float8_e4m3fn).float()
+        _close(kg, kc_r.float().to(torch.float8_e4m3fn).float(), atol=0.1, rtol=0.13)
+        _close(vg, vc_r.float().to(torch.float8_e4m3fn).float(), atol=0.05, rtol=0.13)
+    else:
+        _close(kg, kc_r, atol=5e-2, rtol=3e-2)
+        _close(vg, vc_r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("qk_norm", [True, False])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_qk_norm_rope_cache_decode_mode(qk_norm, fp8):
+    """decode=True (per-token V writes, one token per sequence) writes the same cache as the
+    reference; a slot of -1 writes nothing."""
+    torch.manual_seed(5)
+    T, hq, hkv, D, BS, NB = 77, 16, 8, 128, 32, 40
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int64)
+    slots = torch.randperm(NB * BS)[:T].to(torch.int64)
+    slots[7] = -1
+    cs = ref.rope_cos_sin(4096, D, 1e6)
+    qw = torch.randn(D).bfloat16() if qk_norm else None
+    kw = torch.randn(D).bfloat16() if qk_norm else None
+    kc, vc = torch.zeros(NB, hkv, BS, D).bfloat16(), torch.zeros(NB, hkv, BS // 8, D, 8).bfloat16()
+    q_ref = torch.empty(T, hq, D).bfloat16()
+    ref.qk_norm_rope_cache(qkv, q_ref, kc, vc, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
+    dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
+    kg = torch.zeros(NB, hkv, BS, D, device=DEV, dtype=dt)
+    vg = torch.zeros(NB, hkv, BS // 8, D, 8, device=DEV, dtype=dt)
+    if fp8:
+        kg, vg = kg.view(torch.uint8), vg.view(torch.uint8)
+    q_out = torch.empty(T, hq, D, device=DEV, dtype=torch.bfloat16)
+    ops.qk_norm_rope_cache(qkv.to(DEV), q_out, kg, vg, pos.to(DEV), slots.to(DEV), cs.to(DEV),
+                           None if qw is None else qw.to(DEV), None if kw is None else kw.to(DEV),
+                           hq, hkv, 1e-6, decode=True)
+    _close(q_out, q_ref, atol=3e-2, rtol=2e-2)
+    if fp8:
+        _close(kg.view(torch.float8_e4m3fn).float(), kc.float().to(torch.float8_e4m3fn).float(),
+               atol=0.1, rtol=0.13)
+        _close(vg.view(torch.float8_e4m3fn).float(), vc.float().to(torch.float8_e4m3fn).float(),
+               atol=0)
+    else:
+        _close(kg, kc, atol=3e-2, rtol=2e-2)
+        _close(vg, vc, atol=0)
