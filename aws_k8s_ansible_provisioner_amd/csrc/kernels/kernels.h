@@ -118,25 +118,6 @@ struct WGemmArgs {
 bool wgemm_supported(int M, int N, int K, int ldx, int ldw, int ldy);
 void launch_wgemm(const WGemmArgs& p, hipStream_t st);
 
-// ---- qkvgemm.hip: QKV projection + per-head q/k RMSNorm + RoPE + K/V cache write ----
-struct QkvRopeArgs {
-  const void* X;        // bf16 [M, K] (row stride ldx): the normed layer input
-  const void* W;        // bf16 [(Hq + 2 Hkv) * 128, K] (row stride ldw)
-  const float* ss_in;   // optional [M] sums of squares -> rows scaled by rsqrt(ss/K + eps)
-  void* q_out;          // bf16 [M, Hq, 128]
-  void* k_cache;        // [NB, Hkv, BS, 128] (K-fragment order), bf16 or fp8 bytes
-  void* v_cache;        // [NB, Hkv, BS/8, 128, 8]
-  const int64_t* positions;  // [M]
-  const int64_t* slots;      // [M] (-1: no cache write)
-  const float* cos_sin;      // [max_pos, 128] = cos | sin
-  const void* q_w;           // [128] or nullptr
-  const void* k_w;
-  float eps;
-  int M, K, ldx, ldw, Hq, Hkv, BS, rope, kv_fp8;
-};
-bool qkv_rope_gemm_supported(int M, int K, int bm, int ns);
-void launch_qkv_rope_gemm(const QkvRopeArgs& p, int bm, int ns, hipStream_t st);
-
 // ---- sampling.hip ----
 struct SampleParams {
   const void* logits;  // [B, V] (row stride ld), fp32 or bf16

@@ -378,48 +378,6 @@ void wgemm(Tensor out, Tensor x, Tensor w) {
   akap::launch_wgemm(a, cur_stream());
 }
 
-// QKV projection with the decode attention layer's per-head epilogue (csrc/kernels/
-// qkvgemm.hip): q_out = rope(norm(q)), k = rope(norm(k)) and v written to the paged caches.
-void qkv_rope_gemm(Tensor x, Tensor w, std::optional<Tensor> ss_in, Tensor q_out,
-                   Tensor k_cache, Tensor v_cache, Tensor positions, Tensor slots,
-                   Tensor cos_sin, std::optional<Tensor> q_w, std::optional<Tensor> k_w,
-                   int64_t Hq, int64_t Hkv, double eps, bool apply_rope, int64_t bm, int64_t ns) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(q_out);
-  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_CONTIG(q_out);
-  CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
-  const int M = x.size(0), K = w.size(1);
-  TORCH_CHECK(x.dim() == 2 && x.size(1) == K, "qkv_rope_gemm: x [M, K]");
-  TORCH_CHECK(w.size(0) == (Hq + 2 * Hkv) * 128, "qkv_rope_gemm: w [(Hq + 2 Hkv) * 128, K]");
-  TORCH_CHECK(q_out.numel() >= (int64_t)M * Hq * 128, "qkv_rope_gemm: q_out [M, Hq, 128]");
-  TORCH_CHECK(k_cache.size(3) == 128 && k_cache.size(1) == Hkv, "qkv_rope_gemm: k_cache layout");
-  const int BS = k_cache.size(2);
-  TORCH_CHECK(BS % 32 == 0 && v_cache.dim() == 5 && v_cache.size(2) * 8 == BS,
-              "qkv_rope_gemm: cache block size");
-  TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong &&
-                  positions.numel() >= M && slots.numel() >= M,
-              "qkv_rope_gemm: int64 positions / slots [M]");
-  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(-1) == 128, "cos_sin fp32");
-  TORCH_CHECK(akap::qkv_rope_gemm_supported(M, K, (int)bm, (int)ns) && x.stride(0) % 8 == 0 &&
-                  w.stride(0) % 8 == 0,
-              "qkv_rope_gemm: K % 64, bm 32|64, ns 3|6, aligned rows");
-  if (ss_in)
-    TORCH_CHECK(ss_in->scalar_type() == at::kFloat && ss_in->numel() >= M, "ss_in fp32 [M]");
-  akap::QkvRopeArgs a{};
-  a.X = x.data_ptr(); a.W = w.data_ptr();
-  a.ss_in = ss_in ? ss_in->data_ptr<float>() : nullptr;
-  a.q_out = q_out.data_ptr(); a.k_cache = k_cache.data_ptr(); a.v_cache = v_cache.data_ptr();
-  a.positions = positions.data_ptr<int64_t>(); a.slots = slots.data_ptr<int64_t>();
-  a.cos_sin = cos_sin.data_ptr<float>();
-  a.q_w = q_w ? q_w->data_ptr() : nullptr;
-  a.k_w = k_w ? k_w->data_ptr() : nullptr;
-  a.eps = (float)eps;
-  a.M = M; a.K = K; a.ldx = x.stride(0); a.ldw = w.stride(0);
-  a.Hq = Hq; a.Hkv = Hkv; a.BS = BS; a.rope = apply_rope ? 1 : 0;
-  a.kv_fp8 = kv_fp8_of(k_cache, v_cache);
-  const c10::DeviceGuard g(x.device());
-  akap::launch_qkv_rope_gemm(a, (int)bm, (int)ns, cur_stream());
-}
-
 bool dgemm_ok(int64_t M, int64_t N, int64_t K, int64_t splitk, int64_t pf) {
   return akap::dgemm_supported(M, N, K, splitk, pf);
 }
@@ -865,9 +823,6 @@ TORCH_LIBRARY(akap, m) {
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
       "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None) -> ()");
   m.def("wgemm(Tensor(a!) out, Tensor x, Tensor w) -> ()");
-  m.def("qkv_rope_gemm(Tensor x, Tensor w, Tensor? ss_in, Tensor(a!) q_out, Tensor(b!) k_cache, "
-        "Tensor(c!) v_cache, Tensor positions, Tensor slots, Tensor cos_sin, Tensor? q_w, "
-        "Tensor? k_w, int Hq, int Hkv, float eps, bool apply_rope, int bm, int ns) -> ()");
   m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
   m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");
@@ -926,7 +881,6 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("dgemm", &dgemm);
   m.impl("wgemm", &wgemm);
-  m.impl("qkv_rope_gemm", &qkv_rope_gemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

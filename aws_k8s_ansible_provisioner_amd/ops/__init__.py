@@ -245,28 +245,6 @@ def wgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) 
     return out
 
 
-def qkv_rope_gemm(x, w, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
-                  num_q_heads: int, num_kv_heads: int, eps: float, ss_in=None,
-                  apply_rope: bool = True, bm: int = 32, ns: int = 6):
-    """QKV projection with the decode attention layer's per-head epilogue
-    (csrc/kernels/qkvgemm.hip): qkv = x @ w.T (rows scaled by rsqrt(ss_in / K + eps) when
-    ss_in is given), then per-head q/k RMSNorm (q_w / k_w, optional) + NeoX RoPE; q goes to
-    q_out [M, Hq, 128], the new token's k / v into the paged caches at `slots`.  Equivalent
-    to dgemm(...) followed by qk_norm_rope_cache(...), in one launch."""
-    if _native(x):
-        torch.ops.akap.qkv_rope_gemm(x, w, ss_in, q_out, k_cache, v_cache, positions, slots,
-                                     cos_sin, q_w, k_w, num_q_heads, num_kv_heads, eps,
-                                     apply_rope, bm, ns)
-        return q_out
-    M, K = x.shape[0], w.shape[1]
-    y = torch.nn.functional.linear(x.float(), w.float())
-    if ss_in is not None:
-        y = y * torch.rsqrt(ss_in[:M].float() / K + eps)[:, None]
-    ref.qk_norm_rope_cache(y.to(x.dtype), q_out, k_cache, v_cache, positions, slots, cos_sin,
-                           q_w, k_w, num_q_heads, num_kv_heads, eps, apply_rope)
-    return q_out
-
-
 PRO_PLAIN, PRO_ADDNORM, PRO_SILU = 0, 1, 2
 EPI_STORE, EPI_RESNORM, EPI_SILU = 0, 1, 2
 

@@ -680,55 +680,6 @@ def test_wide_row_gemm_strided_rows_in_graph():
     _close(out, x.float() @ w.float().T, atol=0.1, rtol=1e-2)
 
 
-@pytest.mark.parametrize("M", [1, 16, 45, 64, 100, 256])
-@pytest.mark.parametrize("bm,ns", [(32, 6), (64, 3)])
-@pytest.mark.parametrize("qk_norm,ss", [(True, True), (False, False)])
-@pytest.mark.parametrize("fp8", [False, True])
-def test_qkv_rope_gemm(M, bm, ns, qk_norm, ss, fp8):
-    """qkvgemm.hip vs the unfused pipeline (fp32 GEMM with the input norm's row scale ->
-    bf16 -> reference q/k-norm + RoPE + cache write): q rows, the written K (fragment order)
-    and V (8-token groups) slots, and untouched cache elsewhere (slot -1 rows write nothing)."""
-    torch.manual_seed(M + bm)
-    hq, hkv, D, BS, K = 16, 8, 128, 32, 1024
-    NB = (M + 1) * 2
-    x = torch.randn(M, K, dtype=torch.bfloat16)
-    w = torch.randn((hq + 2 * hkv) * D, K, dtype=torch.bfloat16) * 0.03
-    ssv = (torch.rand(M) * 2 + 0.5) * K if ss else None
-    pos = torch.randint(0, 4000, (M,), dtype=torch.int64)
-    slots = torch.randperm(NB * BS)[:M].to(torch.int64)
-    if M > 3:
-        slots[3] = -1
-    cs = ref.rope_cos_sin(4096, D, 1e6)
-    qw = torch.randn(D).bfloat16() if qk_norm else None
-    kw = torch.randn(D).bfloat16() if qk_norm else None
-    y = x.float() @ w.float().T
-    if ss:
-        y = y * torch.rsqrt(ssv / K + 1e-6)[:, None]
-    kc_r = torch.zeros(NB, hkv, BS, D).bfloat16()
-    vc_r = torch.zeros(NB, hkv, BS // 8, D, 8).bfloat16()
-    q_r = torch.empty(M, hq, D).bfloat16()
-    ref.qk_norm_rope_cache(y.bfloat16(), q_r, kc_r, vc_r, pos, slots, cs, qw, kw, hq, hkv, 1e-6)
-    dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
-    kg = torch.zeros(NB, hkv, BS, D, device=DEV, dtype=dt)
-    vg = torch.zeros(NB, hkv, BS // 8, D, 8, device=DEV, dtype=dt)
-    if fp8:
-        kg, vg = kg.view(torch.uint8), vg.view(torch.uint8)
-    q_out = torch.empty(M, hq, D, device=DEV, dtype=torch.bfloat16)
-    g = lambda t: None if t is None else t.to(DEV)  # noqa: E731
-    ops.qkv_rope_gemm(x.to(DEV), w.to(DEV), q_out, kg, vg, pos.to(DEV), slots.to(DEV),
-                      cs.to(DEV), g(qw), g(kw), hq, hkv, 1e-6, ss_in=g(ssv), bm=bm, ns=ns)
-    torch.cuda.synchronize()
-    _close(q_out, q_r, atol=5e-2, rtol=3e-2)
-    if fp8:
-        kg = kg.view(torch.float8_e4m3fn).float()
-        vg = vg.view(torch.float8_e4m3fn).float()
-        _close(kg, kc_r.float().to(torch.float8_e4m3fn).float(), atol=0.1, rtol=0.13)
-        _close(vg, vc_r.float().to(torch.float8_e4m3fn).float(), atol=0.05, rtol=0.13)
-    else:
-        _close(kg, kc_r, atol=5e-2, rtol=3e-2)
-        _close(vg, vc_r, atol=2e-2, rtol=2e-2)
-
-
 @pytest.mark.parametrize("qk_norm", [True, False])
 @pytest.mark.parametrize("fp8", [False, True])
 def test_qk_norm_rope_cache_decode_mode(qk_norm, fp8):
