@@ -342,7 +342,7 @@ class DecoderLM:
                 q = torch.empty_like(attn)
                 ops.qk_norm_rope_cache(qkv, q, k_caches[li], v_caches[li], batch.positions,
                                        batch.slots, self.cos_sin, lw.q_norm, lw.k_norm, self.hq,
-                                       self.hkv, eps, True)
+                                       self.hkv, eps, True, decode=not batch.is_prefill)
                 self._attention(q, batch, k_caches[li], v_caches[li], attn)
             o = comm.tp_all_reduce(ops.linear(attn.view(T, self.hq * self.D), lw.w_o))
             h, residual = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
