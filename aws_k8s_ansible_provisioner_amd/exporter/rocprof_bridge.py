@@ -46,6 +46,34 @@ def render(agg: dict[str, tuple[float, int]]) -> str:
     return "\n".join(lines) + "\n"
 
 
+def render_windows(windows: list[str], window_s: float) -> str:
+    """kernel_profiler.py's view: cumulative counters over every kept attach window plus
+    the newest window's per-kernel share of GPU kernel time and its busy ratio."""
+    agg: dict[str, tuple[float, int]] = {}
+    for w in windows:
+        for k, (t, n) in collect(w).items():
+            t0, n0 = agg.get(k, (0.0, 0))
+            agg[k] = (t0 + t, n0 + n)
+    lines = [render(agg).rstrip("\n")]
+    last = collect(windows[-1]) if windows else {}
+    tot = sum(t for t, _ in last.values())
+
+    def esc(s):
+        return s.replace("\\", "\\\\").replace('"', '\\"').replace("\n", " ")
+
+    lines += ["# HELP akap_kernel_window_time_fraction Share of GPU kernel time in the newest "
+              "profiling window", "# TYPE akap_kernel_window_time_fraction gauge"]
+    for k, (t, _) in sorted(last.items(), key=lambda kv: -kv[1][0]):
+        lines.append(f'akap_kernel_window_time_fraction{{kernel="{esc(k)}"}} '
+                     f'{t / tot if tot else 0.0}')
+    lines += ["# HELP akap_kernel_window_busy_ratio GPU kernel time / window length (newest)",
+              "# TYPE akap_kernel_window_busy_ratio gauge",
+              f"akap_kernel_window_busy_ratio {tot / window_s if window_s and last else 0.0}",
+              "# HELP akap_kernel_windows Profiling windows kept",
+              "# TYPE akap_kernel_windows gauge", f"akap_kernel_windows {len(windows)}"]
+    return "\n".join(lines) + "\n"
+
+
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--dir", default="/prof")

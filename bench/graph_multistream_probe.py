@@ -1,8 +1,15 @@
 """Probe: hipGraph capture of fork/join and ping-pong dependencies across HIP streams.
 python bench/graph_multistream_probe.py basic|event|pingpong|pingpong_prealloc [n]"""
+import ctypes
+import faulthandler
+import os
 import sys
 
 import torch
+
+faulthandler.enable()
+if os.environ.get("AKAP_SEGV_BT"):  # native backtrace on SIGSEGV, then faulthandler's stack
+    ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "segv_bt.so"))
 
 step = sys.argv[1] if len(sys.argv) > 1 else "basic"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 30

@@ -151,8 +151,18 @@ def test_manifests_render(preset):
         gpus = v["engines"][0]["gpusPerPod"]
         if gpus:
             assert c["resources"]["limits"]["amd.com/gpu"] == str(gpus)
+            # kernel-profiler sidecar + the annotation the collector's kernel-stats job keys on
+            ann = pod["metadata"]["annotations"]
+            assert ann["akap.rocprof/port"] == "9401"
+            assert pod["spec"]["shareProcessNamespace"] is True
+            side = {x["name"]: x for x in pod["spec"]["containers"]}["kernel-profiler"]
+            assert "SYS_PTRACE" in side["securityContext"]["capabilities"]["add"]
+            assert side["command"][-1].endswith("exporter.kernel_profiler")
+            assert {"containerPort": 9401, "name": "kernel-stats"} in side["ports"]
+            assert any(vol["name"] == "prof" for vol in pod["spec"]["volumes"])
         else:
             assert "limits" not in c["resources"]
+            assert "akap.rocprof/port" not in pod["metadata"]["annotations"]
     if preset == "tp8":
         assert "--nproc-per-node=8" in engines[0]["spec"]["template"]["spec"]["containers"][0]["command"]
     if preset == "pd":
@@ -210,7 +220,7 @@ def _fake_sysfs(root, n=2):
 
 def test_gpu_exporter_sysfs_and_dcgm_aliases(tmp_path):
     _fake_sysfs(tmp_path)
-    exp = gpu_exporter.Exporter(str(tmp_path), node="n1")
+    exp = gpu_exporter.Exporter(str(tmp_path), node="n1", run=lambda args: None)
     txt = exp.text()
     assert 'DCGM_FI_DEV_GPU_UTIL{gpu="1"' in txt and "} 41.0" in txt
     assert 'DCGM_FI_DEV_GPU_TEMP{gpu="0"' in txt and "71.0" in txt  # junction preferred
@@ -221,6 +231,150 @@ def test_gpu_exporter_sysfs_and_dcgm_aliases(tmp_path):
     body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics").read().decode()
     assert "DCGM_FI_DEV_FB_USED" in body
     srv.shutdown()
+
+
+def test_kernel_profiler_windows(tmp_path):
+    """The sidecar's loop with a fake rocprofv3: it attaches to the engine PID found in
+    /proc, rotates windows (keeps the newest N) and serves cumulative + newest-window series;
+    a missing engine or a failing attach skips the window without raising."""
+    from aws_k8s_ansible_provisioner_amd.exporter import kernel_profiler as kp
+    proc = tmp_path / "proc"
+    for pid, cmd in ((41, b"python3\0-m\0aws_k8s_ansible_provisioner_amd.server\0--port\0"
+                      b"8000\0"),
+                     (7, b"python3\0-m\0aws_k8s_ansible_provisioner_amd.exporter."
+                      b"kernel_profiler\0"), (9, b"bash\0")):
+        (proc / str(pid)).mkdir(parents=True)
+        (proc / str(pid) / "cmdline").write_bytes(cmd)
+    assert kp.find_engine_pid(str(proc)) == 41
+    calls = []
+
+    def fake(cmd):
+        calls.append(cmd)
+        out = cmd[cmd.index("-d") + 1]
+        os.makedirs(os.path.join(out, "h", "41"), exist_ok=True)
+        ms = 1500000 if len(calls) == 3 else 1000000
+        with open(os.path.join(out, "h", "41", "win_kernel_stats.csv"), "w") as f:
+            f.write('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs",'
+                    '"StdDev"\n"akap::paged_attn_decode_kernel",10,' + str(ms) + ',1,1,1,1,0\n'
+                    '"akap::dgemm_kernel",20,500000,1,1,1,1,0\n')
+        return 0
+
+    prof = kp.Profiler(str(tmp_path / "prof"), window_ms=2000, keep=2, run=fake,
+                       find_pid=lambda: kp.find_engine_pid(str(proc)))
+    for _ in range(3):
+        assert prof.once()
+    assert calls[0][:3] == ["rocprofv3", "--attach", "41"]
+    assert "--attach-duration-msec" in calls[0] and "--stats" in calls[0]
+    assert len(prof.windows()) == 2  # rotated
+    txt = prof.text()
+    assert 'akap_kernel_calls_total{kernel="akap::paged_attn_decode_kernel"} 20' in txt
+    assert 'akap_kernel_window_time_fraction{kernel="akap::paged_attn_decode_kernel"} 0.75' in txt
+    assert "akap_kernel_window_busy_ratio 0.001" in txt and "akap_kernel_windows 2" in txt
+    srv = kp.serve(prof, "127.0.0.1", 0)
+    body = urllib.request.urlopen(f"http://127.0.0.1:{srv.server_address[1]}/metrics").read()
+    assert b"akap_kernel_window_time_fraction" in body
+    srv.shutdown()
+    nope = kp.Profiler(str(tmp_path / "p2"), run=fake, find_pid=lambda: None)
+    assert not nope.once() and "not found" in nope.last_error
+    bad = kp.Profiler(str(tmp_path / "p3"), run=lambda c: 1, find_pid=lambda: 41)
+    assert not bad.once() and "exited 1" in bad.last_error
+
+
+# amd-smi JSON shaped as /opt/rocm/libexec/amdsmi_cli/amdsmi_commands.py (ROCm 7.2) emits it
+_SMI_METRIC = [
+    {"gpu": 0, "usage": {"gfx_activity": {"value": 97, "unit": "%"},
+                         "umc_activity": {"value": 60, "unit": "%"}},
+     "power": {"socket_power": {"value": 1200, "unit": "W"}},
+     "clock": {"gfx_0": {"clk": {"value": 2400, "unit": "MHz"}, "min_clk": {"value": 500}},
+               "mem_0": {"clk": {"value": 1900, "unit": "MHz"}},
+               "fclk_0": {"clk": "N/A"}, "socclk_0": {"clk": {"value": 1400, "unit": "MHz"}}},
+     "temperature": {"edge": {"value": 50, "unit": "C"}, "hotspot": {"value": 80, "unit": "C"}},
+     "pcie": {"replay_count": 3},
+     "ecc": {"total_correctable_count": 5, "total_uncorrectable_count": 0,
+             "total_deferred_count": 0},
+     "ecc_blocks": {"UMC": {"correctable_count": 4, "uncorrectable_count": 0,
+                            "deferred_count": 0},
+                    "XGMI_WAFL": {"correctable_count": 1, "uncorrectable_count": 0,
+                                  "deferred_count": "N/A"}},
+     "energy": {"total_energy_consumption": {"value": 123456.5, "unit": "J"}},
+     "xgmi_err": "AMDSMI_XGMI_STATUS_NO_ERRORS",
+     "mem_usage": {"total_vram": {"value": 294912, "unit": "MB"},
+                   "used_vram": {"value": 1024, "unit": "MB"}}},
+    {"gpu": 1, "usage": {"gfx_activity": {"value": 3, "unit": "%"}}, "clock": "N/A",
+     "ecc": {"total_correctable_count": "N/A"}, "xgmi_err": "AMDSMI_XGMI_STATUS_ERROR"},
+]
+_SMI_XGMI = {"xgmi_metric": [[
+    {"gpu": 0, "bdf": "0000:05:00.0",
+     "link_metrics": {"bit_rate": {"value": 32, "unit": "Gb/s"},
+                      "max_bandwidth": {"value": 1024, "unit": "Gb/s"}, "link_type": "XGMI",
+                      "links": [{"gpu": 0, "bdf": "0000:05:00.0", "read": "N/A", "write": "N/A"},
+                                {"gpu": 1, "bdf": "0000:15:00.0",
+                                 "read": {"value": 2048, "unit": "KB"},
+                                 "write": {"value": 1024, "unit": "KB"}}]}},
+    {"gpu": 1, "bdf": "0000:15:00.0",
+     "link_metrics": {"bit_rate": "N/A", "max_bandwidth": "N/A", "link_type": "N/A",
+                      "links": []}}]]}
+
+
+def _fake_smi(args):
+    import json as _json
+    if args[0] == "metric":
+        return _json.dumps(_SMI_METRIC)
+    if args[0] == "xgmi":
+        return _json.dumps(_SMI_XGMI)
+    return None
+
+
+def test_gpu_exporter_amdsmi_clocks_ecc_xgmi():
+    """No sysfs: every series comes from amd-smi `metric` + `xgmi -m` JSON (fixture shapes
+    from the ROCm 7.2 amd-smi CLI source); N/A values are skipped, not exported as 0."""
+    exp = gpu_exporter.Exporter("/nonexistent", node="n1", run=_fake_smi)
+    txt = exp.text()
+    assert 'amd_gpu_clock_mhz{gpu="0",pci_bus_id="",modelName="AMD Instinct",Hostname="n1",' \
+           'domain="gfx"} 2400.0' in txt
+    assert 'domain="fabric"' not in txt  # "N/A"
+    assert 'DCGM_FI_DEV_SM_CLOCK{gpu="0"' in txt and 'DCGM_FI_DEV_MEM_CLOCK{gpu="0"' in txt
+    assert 'amd_gpu_ecc_errors_total{gpu="0",pci_bus_id="",modelName="AMD Instinct",' \
+           'Hostname="n1",block="umc",kind="correctable"} 4.0' in txt
+    assert 'DCGM_FI_DEV_ECC_SBE_VOL_TOTAL{gpu="0",pci_bus_id="",modelName="AMD Instinct",' \
+           'Hostname="n1"} 5.0' in txt  # UMC 4 + XGMI_WAFL 1
+    assert 'DCGM_FI_DEV_PCIE_REPLAY_COUNTER{gpu="0"' in txt
+    assert 'amd_gpu_energy_joules_total{gpu="0"' in txt and "123456.5" in txt
+    assert 'amd_gpu_xgmi_error{gpu="0",pci_bus_id="",modelName="AMD Instinct",Hostname="n1"} 0.0' \
+        in txt
+    assert 'amd_gpu_xgmi_error{gpu="1",pci_bus_id="",modelName="AMD Instinct",Hostname="n1"} 1.0' \
+        in txt
+    assert 'amd_gpu_xgmi_read_bytes_total{gpu="0",pci_bus_id="",modelName="AMD Instinct",' \
+           'Hostname="n1",peer_gpu="1"} 2097152.0' in txt
+    assert 'DCGM_FI_PROF_NVLINK_TX_BYTES{gpu="0",pci_bus_id="",modelName="AMD Instinct",' \
+           'Hostname="n1"} 1048576.0' in txt
+    assert 'amd_gpu_xgmi_link_bitrate_gbps{gpu="0"' in txt
+    assert 'amd_gpu_xgmi_link_bitrate_gbps{gpu="1"' not in txt
+
+
+def test_gpu_exporter_sysfs_clocks_ras_energy(tmp_path):
+    """sysfs: current DPM level ('*' line), RAS ue/ce counters per block, PCIe replays and
+    hwmon energy; amd-smi xGMI link counters merged in by GPU index."""
+    _fake_sysfs(tmp_path)
+    dev = tmp_path / "class" / "drm" / "card0" / "device"
+    (dev / "pp_dpm_sclk").write_text("0: 500Mhz\n1: 1800Mhz\n2: 2400Mhz *\n")
+    (dev / "pp_dpm_mclk").write_text("0: 900Mhz\n1: 1900Mhz *\n")
+    (dev / "ras").mkdir()
+    (dev / "ras" / "umc_err_count").write_text("ue: 1\nce: 7\n")
+    (dev / "ras" / "xgmi_wafl_err_count").write_text("ue: 0\nce: 2\n")
+    (dev / "pcie_replay_count").write_text("9\n")
+    (dev / "hwmon" / "hwmon0" / "energy1_input").write_text("5000000\n")
+    exp = gpu_exporter.Exporter(str(tmp_path), node="n1", run=_fake_smi)
+    txt = exp.text()
+    assert 'domain="gfx"} 2400.0' in txt and 'domain="mem"} 1900.0' in txt
+    assert 'block="umc",kind="uncorrectable"} 1.0' in txt
+    assert 'DCGM_FI_DEV_ECC_SBE_VOL_TOTAL{gpu="0"' in txt and "} 9.0" in txt
+    assert 'DCGM_FI_DEV_ECC_DBE_VOL_TOTAL{gpu="0"' in txt
+    assert 'amd_gpu_pcie_replay_total{gpu="0"' in txt
+    assert 'amd_gpu_energy_joules_total{gpu="0"' in txt and "} 5.0" in txt
+    # GPU 1 has no sysfs clocks: filled from amd-smi (clock "N/A" there -> none exported)
+    assert 'DCGM_FI_DEV_SM_CLOCK{gpu="1"' not in txt
+    assert 'peer_gpu="1"} 2097152.0' in txt
 
 
 def test_rocprof_bridge(tmp_path):
