@@ -484,7 +484,18 @@ constexpr int kFaRows = 128;
 constexpr int kFaKeys = 64;
 constexpr int kFaBtCache = 1024;  // chunk -> block id cache in LDS (32768 keys)
 
-template <bool F8>
+__device__ __forceinline__ void fa_glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
+                                   0);
+}
+
+// GL = true (bf16 caches): K/V tiles are staged by global_load_lds (LDS-DMA) straight into the
+// next LDS buffer -- no VGPR staging registers, no ds_write pass, and the only wait for the
+// next tile is the counted vmcnt at the top of the following iteration (raw s_barrier, never
+// __syncthreads, whose fence would drain the DMA early).  The K image's XOR swizzle moves to
+// the per-lane DMA source address (the LDS destination of a DMA is lane-linear).
+template <bool F8, bool GL>
 __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParams p) {
   // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
   // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
@@ -574,6 +585,35 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
     }
   };
 
+  // LDS-DMA staging of tile t into buffer buf: 16 K + 16 V instructions of 1 KiB, 4 + 4 per
+  // wave.  K: LDS 16-B slot s holds (key s/16, logical column (s%16) ^ (key&15)); the lane
+  // writing slot s loads that piece from the fragment-ordered K cache chunk.
+  auto stage_glds = [&](int t, int buf) {
+    bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
+    bf16* vl = kl + kFaKeys * kD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = w * 4 + i;
+      const int s = j * 64 + lane;
+      const int key = s >> 4;
+      const int dc = (s & 15) ^ (key & 15);
+      const int k32 = key & 31;
+      const int tt = (k32 >> 2) & 1, r16 = ((k32 >> 3) << 2) | (k32 & 3);
+      const int within = ((tt * 4 + (dc >> 2)) * 16 + r16) * 4 + (dc & 3);
+      const int chunk = min(t * 2 + (key >> 5), last_chunk);
+      const size_t base = ((size_t)bt_s[chunk] * p.Hkv + kvh) * BS * kD + (size_t)((chunk * 32) % BS) * kD;
+      fa_glds16(static_cast<const bf16*>(p.k_cache) + base + within * 8, kl + j * 512);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = w * 4 + i;
+      const int s = j * 64 + lane;
+      const int chunk = min(t * 2 + (s >> 9), last_chunk);
+      const size_t base = ((size_t)bt_s[chunk] * p.Hkv + kvh) * BS * kD + (size_t)((chunk * 32) % BS) * kD;
+      fa_glds16(static_cast<const bf16*>(p.v_cache) + base + (s & 511) * 8, vl + j * 512);
+    }
+  };
+
   f32x16 oacc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -583,14 +623,27 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
 
   for (int c = tid; c <= last_chunk; c += 256) bt_s[c] = bt[c * 32 / BS];
   __syncthreads();
-  stage_load(0);
-  stage_store(0);
-  __syncthreads();
+  if constexpr (GL) {
+    stage_glds(0, 0);
+  } else {
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+  }
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     const bool more = t + 1 < ntiles;
-    // timing experiments (wrong numerics): flags 256 = no K/V reloads, 512 = no compute
-    if (more && !(p.flags & 256)) stage_load(t + 1);
+    if constexpr (GL) {
+      // tile t (issued one iteration ago) landed for this wave; every wave's LDS reads of
+      // buffer buf^1 (tile t-1) are done -> after the barrier it may be refilled
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (more) stage_glds(t + 1, buf ^ 1);
+    } else {
+      // timing experiments (wrong numerics): flags 256 = no K/V reloads, 512 = no compute
+      if (more && !(p.flags & 256)) stage_load(t + 1);
+    }
     const int key0 = t * kFaKeys;
     if (wave_active && key0 <= w_limit && !(p.flags & 512)) {
       const bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
@@ -640,11 +693,15 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
         }
       rs += __shfl_xor(rs, 32, 64);
       l_run = l_run * alpha + rs;
+      // rescale only when some row's running max moved (alpha == 1 exactly otherwise): past
+      // the first tiles of a causal row the max rarely changes
+      if (__any(m_new != m_run)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
+      }
       m_run = m_new;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
       // O^T += V^T . P^T: P^T from the S^T accumulators; V^T fragments loaded per (k, s2)
       // pair ahead of their 4 independent (per d-tile) MFMAs
 #pragma unroll
@@ -669,8 +726,10 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
             oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[dt], pb, oacc[dt], 0, 0, 0);
         }
     }
-    if (more) stage_store(buf ^ 1);
-    __syncthreads();
+    if constexpr (!GL) {
+      if (more) stage_store(buf ^ 1);
+      __syncthreads();
+    }
   }
   if (!valid) return;
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -727,8 +786,10 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows
   if (num_tiles == 0) return;
   const dim3 grid(num_tiles, p.Hkv);
   if (tile_rows == kFaRows) {
-    if (p.kv_fp8) paged_attn_prefill_fa_kernel<true><<<grid, 256, 0, s>>>(p);
-    else paged_attn_prefill_fa_kernel<false><<<grid, 256, 0, s>>>(p);
+    // bf16 caches: LDS-DMA staging (flags bit 10 selects the register-staged form for A/B)
+    if (p.kv_fp8) paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
+    else if (p.flags & 1024) paged_attn_prefill_fa_kernel<false, false><<<grid, 256, 0, s>>>(p);
+    else paged_attn_prefill_fa_kernel<false, true><<<grid, 256, 0, s>>>(p);
   } else {
     if (p.kv_fp8) paged_attn_prefill_kernel<true><<<grid, 256, 0, s>>>(p);
     else paged_attn_prefill_kernel<false><<<grid, 256, 0, s>>>(p);

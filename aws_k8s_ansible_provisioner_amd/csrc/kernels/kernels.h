@@ -107,6 +107,10 @@ bool gdgemm_supported(int M, int N, int K, int splitk, int bn);
 // fp32 workspace floats a gdgemm split-K launch needs (tile-padded slabs)
 long gdgemm_ws_floats(int M, int N, int splitk, int bn);
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st);
+// kgemm.hip: BM (16 | 32) x 32 output tiles, K split over the workgroup's 4 waves (no global
+// partials, no reduce launch); plain prologue, EPI_STORE / EPI_RESNORM, optional ss_in
+bool kgemm_supported(int M, int N, int K, int bm);
+void launch_kgemm(const DGemmArgs& p, int bm, hipStream_t st);
 
 // ---- wgemm.hip: wide-row weight-streaming GEMM (LM head) Y[M,N] = X[M,K] . W[N,K]^T ----
 struct WGemmArgs {

@@ -378,6 +378,45 @@ void wgemm(Tensor out, Tensor x, Tensor w) {
   akap::launch_wgemm(a, cur_stream());
 }
 
+// Narrow-output decode GEMM with the K split inside the workgroup (csrc/kernels/kgemm.hip):
+// out = x @ w^T (rows scaled by rsqrt(ss_in / K + eps) when ss_in is given), epi 0 store,
+// 1 residual/next-norm (out = residual in/out, aout = bf16(out * ln_out), ss_out += row sums).
+void kgemm(Tensor out, Tensor x, Tensor w, int64_t bm, int64_t epi, double eps,
+           std::optional<Tensor> ss_in, std::optional<Tensor> ss_out, std::optional<Tensor> aout,
+           std::optional<Tensor> ln_out) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "kgemm: 2-D tensors");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == N, "kgemm: shapes");
+  TORCH_CHECK(akap::kgemm_supported(M, N, K, (int)bm), "kgemm: bm 16|32, N % 32, K % 256");
+  TORCH_CHECK(epi == 0 || epi == 1, "kgemm: epilogue 0|1");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
+              "kgemm: aligned rows");
+  akap::DGemmArgs a{};
+  a.X = x.data_ptr(); a.W = w.data_ptr(); a.Y = out.data_ptr();
+  a.M = M; a.N = N; a.K = K;
+  a.ldx = x.stride(0); a.ldw = w.stride(0); a.ldy = out.stride(0);
+  a.eps = (float)eps;
+  a.epi = (int)epi;
+  if (ss_in) {
+    TORCH_CHECK(ss_in->scalar_type() == at::kFloat && ss_in->numel() >= M, "ss_in fp32 [M]");
+    a.ss_in = ss_in->data_ptr<float>();
+  }
+  if (epi == 1) {
+    TORCH_CHECK(ss_out && aout && ln_out, "kgemm resnorm epilogue: ss_out, aout, ln_out");
+    TORCH_CHECK(ss_out->scalar_type() == at::kFloat && ss_out->numel() >= M, "ss_out fp32 [M]");
+    CHECK_BF16(*aout); CHECK_CONTIG(*aout); CHECK_BF16(*ln_out);
+    TORCH_CHECK(aout->numel() == (int64_t)M * N && ln_out->numel() == N && out.stride(0) == N,
+                "kgemm resnorm: aout [M, N], ln_out [N], dense residual");
+    a.ss_out = ss_out->data_ptr<float>();
+    a.Aout = aout->data_ptr();
+    a.ln_out = ln_out->data_ptr();
+  }
+  const c10::DeviceGuard g(x.device());
+  akap::launch_kgemm(a, (int)bm, cur_stream());
+}
+
 bool dgemm_ok(int64_t M, int64_t N, int64_t K, int64_t splitk, int64_t pf) {
   return akap::dgemm_supported(M, N, K, splitk, pf);
 }
@@ -823,6 +862,8 @@ TORCH_LIBRARY(akap, m) {
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
       "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None) -> ()");
   m.def("wgemm(Tensor(a!) out, Tensor x, Tensor w) -> ()");
+  m.def("kgemm(Tensor(a!) out, Tensor x, Tensor w, int bm, int epi, float eps, Tensor? ss_in, "
+        "Tensor(b!)? ss_out, Tensor(c!)? aout, Tensor? ln_out) -> ()");
   m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
   m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
   m.def("car_create(int device, int rank, int world, int max_elems) -> int");
@@ -881,6 +922,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("dgemm", &dgemm);
   m.impl("wgemm", &wgemm);
+  m.impl("kgemm", &kgemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

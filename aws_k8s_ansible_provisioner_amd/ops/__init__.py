@@ -200,9 +200,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
             return wgemm(x, w, out=out)
         if choice is not None:  # measured at engine start (cold weights, real layers)
             if choice[0] == "dgemm" and x.stride(-1) == 1:
-                bn, ns, inl = (tuple(choice[3:]) + (0, 0, False))[:3]
+                bn, ns, inl, km = (tuple(choice[3:]) + (0, 0, False, 0))[:4]
                 return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out, bn=bn, ns=ns,
-                             inlaunch=inl)
+                             inlaunch=inl, km=km)
             split = choice[1] if choice[0] == "hip" else 0
     if split is None:
         use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
@@ -262,7 +262,7 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
           out: Optional[torch.Tensor] = None, epi: int = EPI_STORE,
           ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
           a_out: Optional[torch.Tensor] = None, ln_out: Optional[torch.Tensor] = None,
-          bn: int = 0, ns: int = 0, inlaunch: bool = False) -> torch.Tensor:
+          bn: int = 0, ns: int = 0, inlaunch: bool = False, km: int = 0) -> torch.Tensor:
     """Fused decode GEMM (csrc/kernels/dgemm.hip): y = A @ w.T where A is produced from x by
     the prologue inside the GEMM's operand staging --
       PRO_PLAIN    A = x; with ss_in, rows of y are scaled by rsqrt(ss_in / K + eps)
@@ -278,7 +278,9 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
     plain prologue only); 0 the register-ring kernel (prefetch depth pf).  For bn > 0:
     ns >= 6 selects the deep LDS ring (one block per CU, ~7 k-steps in flight), and with
     splitk > 1 inlaunch=True combines the K slices inside the launch (last-arriver ticket,
-    no separate reduce kernel; also allows split-K with the SwiGLU epilogue)."""
+    no separate reduce kernel; also allows split-K with the SwiGLU epilogue).
+    km = 16 | 32 selects csrc/kernels/kgemm.hip instead: km x 32 output tiles with the K split
+    over the workgroup's waves (plain prologue, store / residual epilogues, no split-K)."""
     M = x.shape[0]
     N, K = w.shape
     if out is None:
@@ -304,6 +306,9 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
             out.copy_(ref.silu_and_mul(y.to(x.dtype)))
         else:
             out.copy_(y.to(out.dtype))
+        return out
+    if km:
+        torch.ops.akap.kgemm(out, x, w, km, epi, eps, ss_in, ss_out, a_out, ln_out)
         return out
     counters = None
     if splitk > 1:
@@ -338,6 +343,12 @@ def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI
     if M <= 0 or N <= 0 or K <= 0 or N % 4 or pf not in (1, 2, 4, 8) or K % splitk:
         return False
     return (K // splitk) % (64 * pf) == 0
+
+
+def kgemm_supported(M: int, N: int, K: int, km: int, epi: int = EPI_STORE, pro: int = 0) -> bool:
+    """Mirror of kgemm_supported (csrc/kernels/kgemm.hip)."""
+    return (pro == PRO_PLAIN and km in (16, 32) and M > 0 and N % 32 == 0 and K >= 256
+            and K % 256 == 0 and epi in (EPI_STORE, EPI_RESNORM))
 
 
 def gdgemm_ws_floats(M: int, N: int, splitk: int, bn: int) -> int:

@@ -83,7 +83,7 @@ def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out
 
 
 def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
-         margin: float = 0.03, pfs=(2, 4, 8), bns=(64, 128)) -> Choice:
+         margin: float = 0.03, pfs=(2, 4, 8), bns=(64, 128), kms=(16, 32)) -> Choice:
     """Pick the fastest way to compute x[M, K] @ w.T for these same-shape weights.
     hipBLASLt is kept unless the MFMA kernel is more than `margin` faster."""
     from . import gemm_counters  # noqa: F401  (ensures the native library is loaded)
@@ -124,6 +124,14 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
                                 None), n)
             if t < t_best:
                 best, t_best = ("dgemm", s, 1, bn, ns, inl), t
+    from . import kgemm_supported
+    for km in kms:  # K split inside the workgroup (csrc/kernels/kgemm.hip)
+        if not kgemm_supported(M, N, K, km):
+            continue
+        t = _timed(lambda i, km=km: torch.ops.akap.kgemm(y, x, weights[i % n], km, 0, 1e-6,
+                                                         None, None, None, None), n)
+        if t < t_best:
+            best, t_best = ("dgemm", 1, 1, 0, 0, False, km), t
     if best[0] != "torch" and t_best > t_torch * (1.0 - margin):
         best = ("torch",)
     _PLAN[(M, N, K)] = best
@@ -131,7 +139,9 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
 
 
 def _gd_name(v) -> str:
-    bn, ns, inl = (tuple(v) + (0, False))[:3]
+    bn, ns, inl, km = (tuple(v) + (0, False, 0))[:4]
+    if km:
+        return f"k{km}"
     return f"g{bn}" + ("d" if ns >= 6 else "") + ("i" if inl else "")
 
 
@@ -152,7 +162,7 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
         # the decode LM head: hipBLASLt vs the wide-row kernel only (split-K slabs of a
         # vocab-wide output would be GBs)
         for M in Ms:
-            summary[(M, "lm_head")] = tune(M, [lm], splits=(), pfs=(), bns=())
+            summary[(M, "lm_head")] = tune(M, [lm], splits=(), pfs=(), bns=(), kms=())
     wins = {k: v for k, v in summary.items() if v[0] != "torch"}
     log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, HIP kernel chosen for "
         f"{len(wins)}: " + ", ".join(
@@ -196,10 +206,10 @@ def _time_unfused(M: int, model) -> float:
 
 
 def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2, 4, 8),
-               verbose: bool = False, bns=(64, 128)) -> dict:
+               verbose: bool = False, bns=(64, 128), kms=(16, 32)) -> dict:
     """Pick (split-K, prefetch) for each fused-chain GEMM at each M and keep the fused chain
     for the M where it beats the unfused chain (both timed on the real cold layer weights)."""
-    from . import EPI_SILU, dgemm_supported
+    from . import EPI_SILU, dgemm_supported, kgemm_supported
 
     if not model.layers or any(getattr(l, "moe", None) is not None for l in model.layers):
         return {}
@@ -231,9 +241,18 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
             ss_in_, ss_out_ = (None if epi == 1 else ss), (ss_o if epi == 1 else None)
             a_o_, ln_ = (a_o if epi == 1 else None), (ln if epi == 1 else None)
             for s in splits:
-                cands = [(pf, 0, 0, False) for pf in pfs] + \
-                    [(1, bn, ns, inl) for bn, ns, inl in _gd_variants(s, bns)]
-                for pf, bn, ns, inl in cands:
+                cands = [(pf, 0, 0, False, 0) for pf in pfs] + \
+                    [(1, bn, ns, inl, 0) for bn, ns, inl in _gd_variants(s, bns)]
+                if s == 1:
+                    cands += [(1, 0, 0, False, km) for km in kms if kgemm_supported(M, N, K, km, epi)]
+                for pf, bn, ns, inl, km in cands:
+                    if km:
+                        fn = (lambda i, km=km: torch.ops.akap.kgemm(
+                            out, x, ws_[i % L], km, epi, 1e-6, ss_in_, ss_out_, a_o_, ln_))
+                        t = _timed(fn, L)
+                        if best is None or t < best[0]:
+                            best = (t, s, pf, bn, ns, inl, km)
+                        continue
                     if (not dgemm_supported(M, N, K, s, pf, epi, bn=bn, inlaunch=inl)
                             or (s > 1 and K // s < 256)):
                         continue
@@ -247,14 +266,15 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
                             ss_in_, ss_out_, a_o_, ln_, 0))
                     t = _timed(fn, L)
                     if best is None or t < best[0]:
-                        best = (t, s, pf, bn, ns, inl)
+                        best = (t, s, pf, bn, ns, inl, 0)
             if best is None:
                 plan_m = None
                 break
             plan_m[name] = best[1:]
             t_fused += best[0]
             detail.append(f"{name} {best[0]:.1f}/{t_plain:.1f} (s{best[1]}"
-                          + (_gd_name(best[3:]) if best[3] else f"p{best[2]}") + ")")
+                          + (_gd_name(best[3:]) if (best[3] or best[6]) else f"p{best[2]}")
+                          + ")")
         if plan_m is not None and t_fused < t_unfused:
             _FUSED[M] = plan_m
         chosen[M] = (t_fused, t_unfused, plan_m)
@@ -292,6 +312,9 @@ def _time_best_plain(M: int, name: str, weights) -> float:
     n = len(weights)
     if c[0] == "dgemm":
         y = torch.empty(M, N, device=w0.device, dtype=w0.dtype)
+        if len(c) > 6 and c[6]:
+            return _timed(lambda i: torch.ops.akap.kgemm(y, x, weights[i % n], c[6], 0, 1e-6, None,
+                                                         None, None, None), n)
         if len(c) > 3 and c[3]:
             bn, ns, inl = (tuple(c[3:]) + (0, False))[:3]
             return _timed(_gd_call(M, N, K, c[1], bn, ns, inl, y, x, weights, 0, None, None,

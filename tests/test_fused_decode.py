@@ -61,6 +61,9 @@ def test_fused_decode_chain_cpu(name):
     {"w_qkv": (1, 4, 0), "w_o": (2, 2, 0), "w_gate_up": (1, 2, 0), "w_down": (2, 2, 0)},
     {"w_qkv": (2, 2, 0), "w_o": (1, 4, 0), "w_gate_up": (1, 4, 0), "w_down": (1, 4, 0)},
     {"w_qkv": (1, 1, 128), "w_o": (1, 1, 64), "w_gate_up": (1, 1, 128), "w_down": (2, 1, 64)},
+    # kgemm.hip (K split inside the workgroup) for the plain qkv and the residual epilogues
+    {"w_qkv": (1, 1, 0, 0, False, 32), "w_o": (1, 1, 0, 0, False, 16), "w_gate_up": (1, 2, 0),
+     "w_down": (1, 1, 0, 0, False, 32)},
 ])
 def test_fused_decode_chain_gpu(name, plan):
     ops.load_native(required=True)

@@ -715,3 +715,35 @@ def test_qk_norm_rope_cache_decode_mode(qk_norm, fp8):
     else:
         _close(kg, kc, atol=3e-2, rtol=2e-2)
         _close(vg, vc, atol=0)
+
+
+@pytest.mark.parametrize("km", [16, 32])
+@pytest.mark.parametrize("epi", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(1, 1024, 2048), (37, 1024, 3072), (256, 1024, 2048),
+                                   (200, 4096, 1024), (300, 96, 256)])
+def test_kgemm_in_workgroup_splitk(km, epi, M, N, K):
+    """kgemm.hip (K split over the workgroup's waves, partials summed in LDS) with the store
+    and residual/next-norm epilogues and the ss_in row scale vs fp32 references; a second
+    launch gives identical bits (no cross-workgroup state)."""
+    torch.manual_seed(M + N + K + epi + km)
+    eps = 1e-6
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    ssi = torch.rand(M, device=DEV) * K + 1.0
+    y = (x.float() @ w.float().t()) * torch.rsqrt(ssi / K + eps)[:, None]
+    if epi == 0:
+        out = ops.dgemm(x, w, ss_in=ssi, eps=eps, km=km)
+        _close(out, y, atol=2e-2 * y.abs().max().item())
+        assert torch.equal(out, ops.dgemm(x, w, ss_in=ssi, eps=eps, km=km))
+    else:
+        res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        res0 = res.clone()
+        ln = torch.rand(N, device=DEV, dtype=torch.bfloat16) + 0.5
+        ss = torch.zeros(M, device=DEV)
+        a = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.dgemm(x, w, out=res, epi=epi, ss_out=ss, a_out=a, ln_out=ln, ss_in=ssi, eps=eps,
+                  km=km)
+        want = y.to(torch.bfloat16).float() + res0.float()
+        _close(res, want, atol=2e-2 * want.abs().max().item())
+        _close(a, res.float() * ln.float(), atol=1e-2 * a.float().abs().max().item())
+        assert torch.allclose(ss, res.float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
