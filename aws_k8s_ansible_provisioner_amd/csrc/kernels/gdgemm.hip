@@ -11,7 +11,10 @@
 //   deep ring:    NS = 8 (64-col, 128 KB) / 6 (128-col, 144 KB), one block per CU and
 //                 NS-1 k-steps (112-120 KB) in flight -- for grids of <= 256 tiles.
 //
-// Structure: 64 x BN output tile (BN 64 | 128), 4 waves as 2 (M) x 2 (N), BK = 64.  Per
+// Structure: BM x BN output tile (BM 64 | 128, BN 64 | 128), 4 waves as 2 (M) x 2 (N), BK = 64.
+// BM = 128 (wave tile 64 x 64) halves the weight traffic of a 256-row batch (each weight byte
+// crosses L2 -> CU twice instead of four times): the large-weight projections of Llama-3-8B
+// class models, where the decode GEMMs are weight-stream bound.  Per
 // k-step: counted `s_waitcnt vmcnt` for this step's DMAs, raw s_barrier (never
 // __syncthreads: its fence would drain every DMA in flight), refill the slot consumed one step
 // earlier, then ds_read fragments + MFMA 16x16x32.  LDS image: linear DMA destination, XOR
@@ -34,7 +37,7 @@
 
 namespace akap {
 
-constexpr int GBM = 64, GBK = 64;
+constexpr int GBK = 64;
 
 __device__ __forceinline__ int gswz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
@@ -50,11 +53,12 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BN, int NS, int EPI, int SPL, int OCC, int S>
+template <int BN, int NS, int EPI, int SPL, int OCC, int S, int GBM = 64>
 __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
   constexpr int SU = (GBM + BN) * 8;      // slot size in 16-B units
-  constexpr int JN = BN / 32;             // 16-col MFMA tiles per wave (wave tile 32 x BN/2)
-  constexpr int GA = 2, GW = BN / 32;     // DMA instructions per wave per k-step (A / W)
+  constexpr int MI = GBM / 32;            // 16-row MFMA tiles per wave (wave tile GBM/2 x BN/2)
+  constexpr int JN = BN / 32;             // 16-col MFMA tiles per wave
+  constexpr int GA = GBM / 32, GW = BN / 32;  // DMA instructions per wave per k-step (A / W)
   constexpr int G = GA + GW;
   // ONE __shared__ object (a second one makes hipcc drain vmcnt inside the k-loop,
   // cdna_hip_programming.md "Projection GEMM at M = 256" item 4a); the last element is the
@@ -107,16 +111,16 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
 
   // epilogue operands from the previous launch: load before the loop (hidden under it)
   constexpr bool EPI_HERE = SPL != 1;  // this launch runs the epilogue (no separate reduce)
-  float rsc[2][4];
-  bf16 rold[2][4][JN];
+  float rsc[MI][4];
+  bf16 rold[MI][4][JN];
   bf16 lnv[JN];
   const float* ssp = p.ss_in != nullptr ? p.ss_in : static_cast<const float*>(p.W);
   if constexpr (EPI_HERE) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 32 + i * 16 + fg * 4 + r;
+        const int row = m0 + wm * (GBM / 2) + i * 16 + fg * 4 + r;
         const int rowc = row < p.M ? row : 0;
         rsc[i][r] = ssp[rowc];
         if constexpr (EPI == EPI_RESNORM) {
@@ -137,9 +141,9 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
     }
   }
 
-  f32x4 acc[2][JN];
+  f32x4 acc[MI][JN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -159,14 +163,14 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
     const bf16x8* slot = lds + (t % NS) * SU;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[2], bfr[JN];
+      bf16x8 af[MI], bfr[JN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = slot[gswz(wm * 32 + i * 16 + fr, ks * 4 + fg)];
+      for (int i = 0; i < MI; ++i) af[i] = slot[gswz(wm * (GBM / 2) + i * 16 + fr, ks * 4 + fg)];
 #pragma unroll
       for (int j = 0; j < JN; ++j)
         bfr[j] = slot[GBM * 8 + gswz(wn * (BN / 2) + j * 16 + fr, ks * 4 + fg)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < JN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
@@ -175,12 +179,12 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
 
   if constexpr (SPL == 2) {
     // ---- in-launch split-K combine (see header) ----
-    constexpr int NF = 2 * JN;  // f32x4 fragments per lane
+    constexpr int NF = MI * JN;  // f32x4 fragments per lane
     f32x4* slabs = reinterpret_cast<f32x4*>(p.ws);
     const size_t tile_stride = (size_t)NF * 256;
     f32x4* mine = slabs + ((size_t)kz * ntiles + lt) * tile_stride + tid;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < JN; ++j) mine[(i * JN + j) * 256] = acc[i][j];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -213,13 +217,13 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
       for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] += t0[z * zs + f * 256];
   }
 
-  // epilogue: lane holds rows wm*32 + i*16 + fg*4 + r, column fr of each 16-col sub-tile
+  // epilogue: lane holds rows wm*GBM/2 + i*16 + fg*4 + r, column fr of each 16-col sub-tile
   const float inv_k = 1.f / (float)p.K;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm * 32 + i * 16 + fg * 4 + r;
+      const int row = m0 + wm * (GBM / 2) + i * 16 + fg * 4 + r;
       const bool row_ok = row < p.M;
       if constexpr (SPL == 1) {
 #pragma unroll
@@ -271,45 +275,47 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
     }
 }
 
-bool gdgemm_supported(int M, int N, int K, int splitk, int bn) {
+bool gdgemm_supported(int M, int N, int K, int splitk, int bn, int bm) {
   if (bn != 64 && bn != 128) return false;
+  if (bm != 64 && !(bm == 128 && bn == 128)) return false;
   if (M <= 0 || N <= 0 || K <= 0 || !dgemm_splitk_ok(splitk) || N % 4 || K % splitk) return false;
   const int kps = K / splitk;
   return kps % GBK == 0 && kps >= GBK;
 }
 
-long gdgemm_ws_floats(int M, int N, int splitk, int bn) {
-  const long tm = (M + GBM - 1) / GBM, tn = (N + bn - 1) / bn;
-  const long slabs = (long)splitk * tm * tn * GBM * bn;
+long gdgemm_ws_floats(int M, int N, int splitk, int bn, int bm) {
+  const long tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
+  const long slabs = (long)splitk * tm * tn * bm * bn;
   const long dense = (long)splitk * M * N;
   return slabs > dense ? slabs : dense;
 }
 
-template <int BN, int NS, int OCC, int SPL, int S>
+template <int BN, int NS, int OCC, int SPL, int S, int BM>
 static void gdgemm_epi(const DGemmArgs& p, dim3 grid, hipStream_t st) {
   if (p.epi == EPI_RESNORM) {
-    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S><<<grid, 256, 0, st>>>(p);
+    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S, BM><<<grid, 256, 0, st>>>(p);
   } else if (p.epi == EPI_SILU) {
-    if constexpr (SPL != 1) gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S><<<grid, 256, 0, st>>>(p);
+    if constexpr (SPL != 1)
+      gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S, BM><<<grid, 256, 0, st>>>(p);
   } else {
-    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S><<<grid, 256, 0, st>>>(p);
+    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S, BM><<<grid, 256, 0, st>>>(p);
   }
 }
 
-template <int BN, int NS, int OCC>
+template <int BN, int NS, int OCC, int BM = 64>
 static void gdgemm_ring(const DGemmArgs& p, dim3 grid, int splitk, hipStream_t st) {
   if (splitk == 1) {
-    gdgemm_epi<BN, NS, OCC, 0, 1>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 0, 1, BM>(p, grid, st);
   } else if (p.counters == nullptr) {
-    gdgemm_epi<BN, NS, OCC, 1, 1>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 1, 1, BM>(p, grid, st);
     launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
   } else {
     switch (splitk) {
-      case 2: gdgemm_epi<BN, NS, OCC, 2, 2>(p, grid, st); break;
-      case 4: gdgemm_epi<BN, NS, OCC, 2, 4>(p, grid, st); break;
-      case 8: gdgemm_epi<BN, NS, OCC, 2, 8>(p, grid, st); break;
+      case 2: gdgemm_epi<BN, NS, OCC, 2, 2, BM>(p, grid, st); break;
+      case 4: gdgemm_epi<BN, NS, OCC, 2, 4, BM>(p, grid, st); break;
+      case 8: gdgemm_epi<BN, NS, OCC, 2, 8, BM>(p, grid, st); break;
       default:  // 16 slices: slabs + the separate reduce pass
-        gdgemm_epi<BN, NS, OCC, 1, 1>(p, grid, st);
+        gdgemm_epi<BN, NS, OCC, 1, 1, BM>(p, grid, st);
         launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
         break;
     }
@@ -317,9 +323,14 @@ static void gdgemm_ring(const DGemmArgs& p, dim3 grid, int splitk, hipStream_t s
 }
 
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st) {
-  const int tiles = ((p.M + GBM - 1) / GBM) * ((p.N + p.bn - 1) / p.bn);
+  const int bm = p.bm == 128 ? 128 : 64;
+  const int tiles = ((p.M + bm - 1) / bm) * ((p.N + p.bn - 1) / p.bn);
   dim3 grid(tiles, splitk);
   const bool deep = p.ns >= 6;
+  if (bm == 128) {  // 128 x 128 tiles: 4 x 32 KB ring, one block per CU
+    gdgemm_ring<128, 4, 1, 128>(p, grid, splitk, st);
+    return;
+  }
   // shallow: NS = 4 (64-col: 4 x 16 KB) / 3 (128-col: 3 x 24 KB) -> two blocks per CU;
   // deep: 8 x 16 KB / 6 x 24 KB -> one block per CU
   if (p.bn == 128) {

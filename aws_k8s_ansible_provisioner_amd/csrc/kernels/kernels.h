@@ -95,6 +95,7 @@ struct DGemmArgs {
   int bn;  // 0: register-ring kernel (dgemm.hip); 64 | 128: LDS-DMA ring kernel (gdgemm.hip)
   int ns;  // gdgemm ring depth: 0 = shallow (2 blocks/CU), >= 6 = deep ring (1 block/CU)
   int* counters;  // gdgemm split-K: zeroed per-tile tickets -> in-launch last-arriver combine
+  int bm;         // gdgemm tile rows: 64 (default) | 128 (with bn = 128)
 };
 bool dgemm_supported(int M, int N, int K, int splitk, int pf);
 // split-K factors with a compiled reduce (1, 2, 4, 8, 16)
@@ -103,9 +104,9 @@ bool dgemm_epi_supported(int N, int epi, int splitk);
 void launch_dgemm(const DGemmArgs& a, int pro, int splitk, int pf, hipStream_t st);
 void launch_dgemm_reduce(const DGemmArgs& p, int pro, int splitk, hipStream_t st);
 // gdgemm.hip: the same plain-prologue GEMM + epilogues with operands staged by global_load_lds
-bool gdgemm_supported(int M, int N, int K, int splitk, int bn);
+bool gdgemm_supported(int M, int N, int K, int splitk, int bn, int bm = 64);
 // fp32 workspace floats a gdgemm split-K launch needs (tile-padded slabs)
-long gdgemm_ws_floats(int M, int N, int splitk, int bn);
+long gdgemm_ws_floats(int M, int N, int splitk, int bn, int bm = 64);
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st);
 // kgemm.hip: BM (16 | 32) x 32 output tiles, K split over the workgroup's 4 waves (no global
 // partials, no reduce launch); plain prologue, EPI_STORE / EPI_RESNORM, optional ss_in

@@ -283,7 +283,7 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
            std::optional<Tensor> r, std::optional<Tensor> rout, std::optional<Tensor> ln,
            double eps, int64_t epi, std::optional<Tensor> ss_in, std::optional<Tensor> ss_out,
            std::optional<Tensor> aout, std::optional<Tensor> ln_out, int64_t bn, int64_t ns,
-           std::optional<Tensor> counters) {
+           std::optional<Tensor> counters, int64_t bm) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "dgemm: 2-D tensors");
@@ -295,7 +295,8 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == akap::EPI_SILU ? N / 2 : N),
               "dgemm: out shape");
   TORCH_CHECK(bn == 0 || pro == akap::PRO_PLAIN, "dgemm: the LDS-DMA variant has the plain prologue");
-  TORCH_CHECK(bn > 0 ? akap::gdgemm_supported(M, N, K, splitk, bn)
+  TORCH_CHECK(bm == 64 || bn > 0, "dgemm: 128-row tiles are an LDS-DMA (bn > 0) variant");
+  TORCH_CHECK(bn > 0 ? akap::gdgemm_supported(M, N, K, splitk, bn, bm)
                      : akap::dgemm_supported(M, N, K, splitk, pf),
               "dgemm: unsupported M/N/K/splitk/pf/bn");
   const bool inlaunch = counters.has_value() && splitk > 1 && bn > 0;
@@ -306,7 +307,7 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
               "dgemm: 16-byte aligned rows");
   if (splitk > 1) {
-    const int64_t need = bn > 0 ? akap::gdgemm_ws_floats(M, N, (int)splitk, (int)bn)
+    const int64_t need = bn > 0 ? akap::gdgemm_ws_floats(M, N, (int)splitk, (int)bn, (int)bm)
                                 : splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
     TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= need,
                 "dgemm: fp32 workspace of splitk*M*N (+ splitk*M for the norm)");
@@ -324,10 +325,11 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   a.epi = (int)epi;
   a.bn = (int)bn;
   a.ns = (int)ns;
+  a.bm = (int)bm;
   if (counters && splitk > 1 && bn > 0) {
     // in-launch split-K combine: one zeroed int32 ticket per output tile
     TORCH_CHECK(counters->scalar_type() == at::kInt && counters->is_cuda() &&
-                    counters->numel() >= (int64_t)((M + 63) / 64) * ((N + bn - 1) / bn),
+                    counters->numel() >= (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn),
                 "dgemm: counters int32, one per output tile");
     a.counters = counters->data_ptr<int>();
   }
@@ -860,7 +862,7 @@ TORCH_LIBRARY(akap, m) {
       "dgemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int pro, int splitk, int pf, "
       "Tensor? r=None, Tensor(c!)? rout=None, Tensor? ln=None, float eps=1e-6, int epi=0, "
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
-      "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None) -> ()");
+      "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None, int bm=64) -> ()");
   m.def("wgemm(Tensor(a!) out, Tensor x, Tensor w) -> ()");
   m.def("kgemm(Tensor(a!) out, Tensor x, Tensor w, int bm, int epi, float eps, Tensor? ss_in, "
         "Tensor(b!)? ss_out, Tensor(c!)? aout, Tensor? ln_out) -> ()");

@@ -372,8 +372,8 @@ class DecoderLM:
 
         def cfg_(name):  # plan entry (split-K, prefetch, tile width[, ring, in-launch combine,
             #                            kgemm rows])
-            s_, p_, b_, n_, i_, k_ = (tuple(plan[name]) + (0, False, 0))[:6]
-            return dict(splitk=s_, pf=p_, bn=b_, ns=n_, inlaunch=bool(i_), km=k_)
+            s_, p_, b_, n_, i_, k_, m_ = (tuple(plan[name]) + (0, False, 0, 64))[:7]
+            return dict(splitk=s_, pf=p_, bn=b_, ns=n_, inlaunch=bool(i_), km=k_, bm=m_)
 
         c_qkv, c_o, c_gu, c_d = (cfg_(n) for n in ("w_qkv", "w_o", "w_gate_up", "w_down"))
         tp = self.ps.tp_size

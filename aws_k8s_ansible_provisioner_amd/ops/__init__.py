@@ -200,9 +200,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
             return wgemm(x, w, out=out)
         if choice is not None:  # measured at engine start (cold weights, real layers)
             if choice[0] == "dgemm" and x.stride(-1) == 1:
-                bn, ns, inl, km = (tuple(choice[3:]) + (0, 0, False, 0))[:4]
+                bn, ns, inl, km, bm = (tuple(choice[3:]) + (0, 0, False, 0, 64))[:5]
                 return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out, bn=bn, ns=ns,
-                             inlaunch=inl, km=km)
+                             inlaunch=inl, km=km, bm=bm)
             split = choice[1] if choice[0] == "hip" else 0
     if split is None:
         use_hip = (x.is_cuda and _GEMM_MODE != "torch" and x.dim() == 2 and x.stride(-1) == 1
@@ -262,7 +262,8 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
           out: Optional[torch.Tensor] = None, epi: int = EPI_STORE,
           ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
           a_out: Optional[torch.Tensor] = None, ln_out: Optional[torch.Tensor] = None,
-          bn: int = 0, ns: int = 0, inlaunch: bool = False, km: int = 0) -> torch.Tensor:
+          bn: int = 0, ns: int = 0, inlaunch: bool = False, km: int = 0,
+          bm: int = 64) -> torch.Tensor:
     """Fused decode GEMM (csrc/kernels/dgemm.hip): y = A @ w.T where A is produced from x by
     the prologue inside the GEMM's operand staging --
       PRO_PLAIN    A = x; with ss_in, rows of y are scaled by rsqrt(ss_in / K + eps)
@@ -279,6 +280,8 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
     ns >= 6 selects the deep LDS ring (one block per CU, ~7 k-steps in flight), and with
     splitk > 1 inlaunch=True combines the K slices inside the launch (last-arriver ticket,
     no separate reduce kernel; also allows split-K with the SwiGLU epilogue).
+    bm = 128 (with bn = 128): 128-row LDS-DMA tiles (weights cross L2 -> CU half as often at
+    M = 256; the large-weight projections).
     km = 16 | 32 selects csrc/kernels/kgemm.hip instead: km x 32 output tiles with the K split
     over the workgroup's waves (plain prologue, store / residual epilogues, no split-K)."""
     M = x.shape[0]
@@ -312,7 +315,7 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
         return out
     counters = None
     if splitk > 1:
-        n = (gdgemm_ws_floats(M, N, splitk, bn) if bn else
+        n = (gdgemm_ws_floats(M, N, splitk, bn, bm) if bn else
              splitk * M * N + (splitk * M if pro == PRO_ADDNORM else 0))
         ws = torch.empty(n, dtype=torch.float32, device=x.device)
         if inlaunch and bn:
@@ -322,14 +325,16 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
         if ws is None:
             ws = _EMPTY_F32[x.device] = torch.empty(1, dtype=torch.float32, device=x.device)
     torch.ops.akap.dgemm(out, x, w, ws, pro, splitk, pf, residual, residual_out, ln, eps, epi,
-                         ss_in, ss_out, a_out, ln_out, bn, ns, counters)
+                         ss_in, ss_out, a_out, ln_out, bn, ns, counters, bm)
     return out
 
 
 def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI_STORE,
-                    bn: int = 0, inlaunch: bool = False) -> bool:
+                    bn: int = 0, inlaunch: bool = False, bm: int = 64) -> bool:
     """Mirror of dgemm_supported / gdgemm_supported / dgemm_epi_supported (host-side)."""
     if splitk not in (1, 2, 4, 8, 16):
+        return False
+    if bm != 64 and not (bm == 128 and bn == 128):
         return False
     inl = inlaunch and bn and splitk > 1
     if epi == EPI_SILU and ((splitk != 1 and not inl) or N % 32):
@@ -351,9 +356,9 @@ def kgemm_supported(M: int, N: int, K: int, km: int, epi: int = EPI_STORE, pro: 
             and K % 256 == 0 and epi in (EPI_STORE, EPI_RESNORM))
 
 
-def gdgemm_ws_floats(M: int, N: int, splitk: int, bn: int) -> int:
+def gdgemm_ws_floats(M: int, N: int, splitk: int, bn: int, bm: int = 64) -> int:
     """fp32 workspace of a split-K LDS-DMA GEMM (tile-padded slabs; mirrors gdgemm.hip)."""
-    slabs = splitk * -(-M // 64) * -(-N // bn) * 64 * bn
+    slabs = splitk * -(-M // bm) * -(-N // bn) * bm * bn
     return max(slabs, splitk * M * N)
 
 

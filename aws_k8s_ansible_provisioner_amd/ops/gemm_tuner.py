@@ -61,25 +61,31 @@ def _timed(fn, n: int) -> float:
 
 
 def _gd_variants(s: int, bns):
-    """gdgemm.hip variants at split s: (tile width, ring depth, in-launch split-K combine).
-    Depth 0 = shallow ring (two blocks per CU), 8 = deep ring (one block per CU)."""
+    """gdgemm.hip variants at split s: (tile width, ring depth, in-launch split-K combine, tile
+    rows).  Depth 0 = shallow ring (two blocks per CU), 8 = deep ring (one block per CU);
+    128 x 128 tiles (rows 128) have their own 4-slot ring."""
     for bn in bns:
         for ns in (0, 8):
             for inl in ((False, True) if s > 1 else (False,)):
-                yield bn, ns, inl
+                yield bn, ns, inl, 64
+        if bn == 128:
+            for inl in ((False, True) if s > 1 else (False,)):
+                yield bn, 4, inl, 128
 
 
-def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out, ln_out):
+def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out, ln_out,
+             bm=64):
     """fn(i) launching one gdgemm variant on weights[i % len] (workspace/tickets bound)."""
     from . import gdgemm_ws_floats, gemm_counters
 
     dev = x.device
-    ws = torch.empty(max(1, gdgemm_ws_floats(M, N, s, bn) if s > 1 else 1), device=dev,
+    ws = torch.empty(max(1, gdgemm_ws_floats(M, N, s, bn, bm) if s > 1 else 1), device=dev,
                      dtype=torch.float32)
     cnt = gemm_counters(dev) if (inl and s > 1) else None
     n = len(weights)
     return lambda i: torch.ops.akap.dgemm(out, x, weights[i % n], ws, 0, s, 1, None, None, None,
-                                          1e-6, epi, ss_in, ss_out, a_out, ln_out, bn, ns, cnt)
+                                          1e-6, epi, ss_in, ss_out, a_out, ln_out, bn, ns, cnt,
+                                          bm)
 
 
 def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
@@ -117,13 +123,14 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
             t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, pf), n)
             if t < t_best:
                 best, t_best = ("dgemm", s, pf), t
-        for bn, ns, inl in _gd_variants(s, bns):  # LDS-DMA staged variants (gdgemm.hip)
-            if not dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl) or (s > 1 and K // s < 256):
+        for bn, ns, inl, bm in _gd_variants(s, bns):  # LDS-DMA staged variants (gdgemm.hip)
+            if (not dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl, bm=bm)
+                    or (s > 1 and K // s < 256)):
                 continue
             t = _timed(_gd_call(M, N, K, s, bn, ns, inl, y, x, weights, 0, None, None, None,
-                                None), n)
+                                None, bm), n)
             if t < t_best:
-                best, t_best = ("dgemm", s, 1, bn, ns, inl), t
+                best, t_best = ("dgemm", s, 1, bn, ns, inl, 0, bm), t
     from . import kgemm_supported
     for km in kms:  # K split inside the workgroup (csrc/kernels/kgemm.hip)
         if not kgemm_supported(M, N, K, km):
@@ -139,9 +146,11 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
 
 
 def _gd_name(v) -> str:
-    bn, ns, inl, km = (tuple(v) + (0, False, 0))[:4]
+    bn, ns, inl, km, bm = (tuple(v) + (0, False, 0, 64))[:5]
     if km:
         return f"k{km}"
+    if bm == 128:
+        return f"g{bn}x128" + ("i" if inl else "")
     return f"g{bn}" + ("d" if ns >= 6 else "") + ("i" if inl else "")
 
 
@@ -241,24 +250,25 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
             ss_in_, ss_out_ = (None if epi == 1 else ss), (ss_o if epi == 1 else None)
             a_o_, ln_ = (a_o if epi == 1 else None), (ln if epi == 1 else None)
             for s in splits:
-                cands = [(pf, 0, 0, False, 0) for pf in pfs] + \
-                    [(1, bn, ns, inl, 0) for bn, ns, inl in _gd_variants(s, bns)]
+                cands = [(pf, 0, 0, False, 0, 64) for pf in pfs] + \
+                    [(1, bn, ns, inl, 0, bm) for bn, ns, inl, bm in _gd_variants(s, bns)]
                 if s == 1:
-                    cands += [(1, 0, 0, False, km) for km in kms if kgemm_supported(M, N, K, km, epi)]
-                for pf, bn, ns, inl, km in cands:
+                    cands += [(1, 0, 0, False, km, 64) for km in kms
+                              if kgemm_supported(M, N, K, km, epi)]
+                for pf, bn, ns, inl, km, bm in cands:
                     if km:
                         fn = (lambda i, km=km: torch.ops.akap.kgemm(
                             out, x, ws_[i % L], km, epi, 1e-6, ss_in_, ss_out_, a_o_, ln_))
                         t = _timed(fn, L)
                         if best is None or t < best[0]:
-                            best = (t, s, pf, bn, ns, inl, km)
+                            best = (t, s, pf, bn, ns, inl, km, bm)
                         continue
-                    if (not dgemm_supported(M, N, K, s, pf, epi, bn=bn, inlaunch=inl)
+                    if (not dgemm_supported(M, N, K, s, pf, epi, bn=bn, inlaunch=inl, bm=bm)
                             or (s > 1 and K // s < 256)):
                         continue
                     if bn:
                         fn = _gd_call(M, N, K, s, bn, ns, inl, out, x, ws_, epi, ss_in_,
-                                      ss_out_, a_o_, ln_)
+                                      ss_out_, a_o_, ln_, bm)
                     else:
                         wsp = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
                         fn = (lambda i, s=s, pf=pf, wsp=wsp: torch.ops.akap.dgemm(
@@ -266,7 +276,7 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
                             ss_in_, ss_out_, a_o_, ln_, 0))
                     t = _timed(fn, L)
                     if best is None or t < best[0]:
-                        best = (t, s, pf, bn, ns, inl, 0)
+                        best = (t, s, pf, bn, ns, inl, 0, bm)
             if best is None:
                 plan_m = None
                 break
@@ -316,9 +326,9 @@ def _time_best_plain(M: int, name: str, weights) -> float:
             return _timed(lambda i: torch.ops.akap.kgemm(y, x, weights[i % n], c[6], 0, 1e-6, None,
                                                          None, None, None), n)
         if len(c) > 3 and c[3]:
-            bn, ns, inl = (tuple(c[3:]) + (0, False))[:3]
+            bn, ns, inl, _, bm = (tuple(c[3:]) + (0, False, 0, 64))[:5]
             return _timed(_gd_call(M, N, K, c[1], bn, ns, inl, y, x, weights, 0, None, None,
-                                   None, None), n)
+                                   None, None, bm), n)
         ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         return _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, c[1], c[2],
                                                      None, None, None, 1e-6, 0, None, None,

@@ -31,7 +31,8 @@ for M in [int(v) for v in a.m.split(",")]:
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16) * 0.1
         y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         gb = N * K * 2 / 1e9
-        rows = [("hipblaslt", gt._timed(lambda i: torch.nn.functional.linear(x, ws[i % L]), L))]
+        rows = [("hipblaslt", gt._timed(lambda i: torch.nn.functional.linear(x, ws[i % L]), L)),
+                ("wgemm", gt._timed(lambda i: torch.ops.akap.wgemm(y, x, ws[i % L]), L))]
         # floor: the same launch with K cut to one 64-deep step (boundary + one round trip)
         w64 = [w[:, :64].contiguous() for w in ws]
         x64 = x[:, :64].contiguous()
@@ -46,11 +47,17 @@ for M in [int(v) for v in a.m.split(",")]:
                     rows.append((f"s{s} reg p{pf}", gt._timed(
                         lambda i, s=s, pf=pf, wsp=wsp: torch.ops.akap.dgemm(
                             y, x, ws[i % L], wsp, 0, s, pf), L)))
-            for bn, ns, inl in gt._gd_variants(s, (64, 128)):
-                if ops.dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl):
-                    rows.append((f"s{s} {gt._gd_name((bn, ns, inl))}", gt._timed(
+            for bn, ns, inl, bm in gt._gd_variants(s, (64, 128)):
+                if ops.dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl, bm=bm):
+                    rows.append((f"s{s} {gt._gd_name((bn, ns, inl, 0, bm))}", gt._timed(
                         gt._gd_call(M, N, K, s, bn, ns, inl, y, x, ws, 0, None, None, None,
-                                    None), L)))
+                                    None, bm), L)))
+            if s == 1:
+                for km in (16, 32):
+                    if ops.kgemm_supported(M, N, K, km):
+                        rows.append((f"k{km}", gt._timed(
+                            lambda i, km=km: torch.ops.akap.kgemm(y, x, ws[i % L], km, 0, 1e-6,
+                                                                  None, None, None, None), L)))
         rows.sort(key=lambda r: r[1])
         print(f"M={M:4d} {name:10s} N={N:6d} K={K:6d}: " + "  ".join(
             f"{n} {t:.1f}" for n, t in rows), flush=True)

@@ -436,14 +436,15 @@ def test_gemm_tuner_plan_is_used_and_correct():
     torch.manual_seed(21)
     ws = [torch.randn(1024, 3072, device=DEV, dtype=torch.bfloat16) * 0.02 for _ in range(4)]
     choice = gemm_tuner.tune(128, ws)
-    assert choice[0] in ("torch", "hip")
+    assert choice[0] in ("torch", "hip", "dgemm", "wgemm")
     assert gemm_tuner.lookup(128, 1024, 3072) == choice
     x = torch.randn(128, 3072, device=DEV, dtype=torch.bfloat16)
     y = ops.linear(x, ws[1])
     ref_ = x.float() @ ws[1].float().t()
     assert (y.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
     # force the MFMA path through the plan and check it too
-    for forced in (("hip", 4), ("dgemm", 4, 2), ("dgemm", 1, 4)):
+    for forced in (("hip", 4), ("dgemm", 4, 2), ("dgemm", 1, 4), ("dgemm", 1, 1, 0, 0, False, 16),
+                   ("dgemm", 1, 1, 0, 0, False, 32), ("wgemm",)):
         gemm_tuner.plan()[(128, 1024, 3072)] = forced
         y2 = ops.linear(x, ws[1])
         assert (y2.float() - ref_).abs().max().item() <= 2e-2 * ref_.abs().max().item() + 1e-2
@@ -597,7 +598,8 @@ def test_fused_decode_gemm_in_graph():
     assert torch.equal(y, eager)
 
 
-@pytest.mark.parametrize("ring", ["shallow", "deep", "deep-inlaunch", "shallow-inlaunch"])
+@pytest.mark.parametrize("ring", ["shallow", "deep", "deep-inlaunch", "shallow-inlaunch",
+                                  "rows128", "rows128-inlaunch"])
 @pytest.mark.parametrize("bn", [64, 128])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K,splitk", [(1, 256, 1024, 1), (37, 1024, 2048, 2),
@@ -609,11 +611,12 @@ def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
     (2 blocks/CU) and deep (1 block/CU) rings, split-K reduced by the separate pass or
     combined in-launch by the last-arriving slice (also for the SwiGLU epilogue)."""
     inl = ring.endswith("inlaunch")
+    bm = 128 if ring.startswith("rows128") else 64
     if inl and splitk == 1:
         pytest.skip("in-launch combine needs split-K")
-    if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=bn, inlaunch=inl):
+    if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=bn, inlaunch=inl, bm=bm):
         pytest.skip("unsupported combination")
-    kw = dict(ns=8 if ring.startswith("deep") else 0, inlaunch=inl)
+    kw = dict(ns=8 if ring.startswith("deep") else 0, inlaunch=inl, bm=bm)
     torch.manual_seed(M + N + K + epi + bn)
     eps = 1e-6
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
