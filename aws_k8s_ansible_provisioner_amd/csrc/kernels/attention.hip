@@ -495,7 +495,7 @@ __device__ __forceinline__ void fa_glds16(const void* g, void* lds_wave_base) {
 // next tile is the counted vmcnt at the top of the following iteration (raw s_barrier, never
 // __syncthreads, whose fence would drain the DMA early).  The K image's XOR swizzle moves to
 // the per-lane DMA source address (the LDS destination of a DMA is lane-linear).
-template <bool F8, bool GL>
+template <bool F8, bool GL, bool VSWAP = true>
 __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParams p) {
   // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
   // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
@@ -713,13 +713,29 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
           for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[k][8 * s2 + j]);
           const int g = 4 * k + 2 * s2;
           bf16x8 va[4];
+          if (VSWAP) {
+            // one conflict-free 16-B read per lane -- group g (lanes < 32) or g+1 (lanes >= 32)
+            // of dim d, all 8 tokens -- then two v_permlane32_swap exchange the 8-byte halves
+            // between lanes i and i+32: lane i ends with tokens 0-3 of g and g+1, lane i+32
+            // with tokens 4-7 (the 2 x 8-byte reads they replace hit 2-way bank conflicts)
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            const int d = 32 * dt + r;
-            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vl + (g * kD + d) * 8 + 4 * h);
-            const bf16x4 hi =
-                *reinterpret_cast<const bf16x4*>(vl + ((g + 1) * kD + d) * 8 + 4 * h);
-            va[dt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            for (int dt = 0; dt < 4; ++dt) {
+              const u32x4 u =
+                  *reinterpret_cast<const u32x4*>(vl + ((g + h) * kD + 32 * dt + r) * 8);
+              const auto a = __builtin_amdgcn_permlane32_swap(u[0], u[2], false, false);
+              const auto b = __builtin_amdgcn_permlane32_swap(u[1], u[3], false, false);
+              const u32x4 o = {a[0], b[0], a[1], b[1]};
+              va[dt] = __builtin_bit_cast(bf16x8, o);
+            }
+          } else {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+              const int d = 32 * dt + r;
+              const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vl + (g * kD + d) * 8 + 4 * h);
+              const bf16x4 hi =
+                  *reinterpret_cast<const bf16x4*>(vl + ((g + 1) * kD + d) * 8 + 4 * h);
+              va[dt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
           }
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt)
@@ -787,8 +803,10 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows
   const dim3 grid(num_tiles, p.Hkv);
   if (tile_rows == kFaRows) {
     // bf16 caches: LDS-DMA staging (flags bit 10 selects the register-staged form for A/B)
+    // flags bit 11: the former pair-of-8-byte V fragment reads (A/B)
     if (p.kv_fp8) paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
     else if (p.flags & 1024) paged_attn_prefill_fa_kernel<false, false><<<grid, 256, 0, s>>>(p);
+    else if (p.flags & 2048) paged_attn_prefill_fa_kernel<false, true, false><<<grid, 256, 0, s>>>(p);
     else paged_attn_prefill_fa_kernel<false, true><<<grid, 256, 0, s>>>(p);
   } else {
     if (p.kv_fp8) paged_attn_prefill_kernel<true><<<grid, 256, 0, s>>>(p);
