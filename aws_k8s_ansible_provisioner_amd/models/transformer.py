@@ -366,13 +366,17 @@ class DecoderLM:
         custom xGMI kernel applies it in its store pass), so a TP layer is still 4 GEMM
         launches + 2 all-reduce launches + attention.  Plan from gemm_tuner.tune_fused:
         projection -> (split-K, prefetch depth, LDS-DMA tile width[, ring, in-launch])."""
+        from ..ops import gemm_tuner
+
         T = input_ids.shape[0]
         eps = self.cfg.rms_eps
         L = len(self.layers)
 
         def cfg_(name):  # plan entry (split-K, prefetch, tile width[, ring, in-launch combine,
             #                            kgemm rows])
-            s_, p_, b_, n_, i_, k_, m_ = (tuple(plan[name]) + (0, False, 0, 64))[:7]
+            e = tuple(plan[name])
+            s_, p_ = e[:2]
+            b_, n_, i_, k_, m_ = gemm_tuner.variant_fields(e[2:])[:5]
             return dict(splitk=s_, pf=p_, bn=b_, ns=n_, inlaunch=bool(i_), km=k_, bm=m_)
 
         c_qkv, c_o, c_gu, c_d = (cfg_(n) for n in ("w_qkv", "w_o", "w_gate_up", "w_down"))

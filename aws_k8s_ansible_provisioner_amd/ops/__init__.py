@@ -200,7 +200,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
             return wgemm(x, w, out=out)
         if choice is not None:  # measured at engine start (cold weights, real layers)
             if choice[0] == "dgemm" and x.stride(-1) == 1:
-                bn, ns, inl, km, bm = (tuple(choice[3:]) + (0, 0, False, 0, 64))[:5]
+                bn, ns, inl, km, bm = gemm_tuner.variant_fields(choice[3:])[:5]
                 return dgemm(x, w, PRO_PLAIN, choice[1], choice[2], out=out, bn=bn, ns=ns,
                              inlaunch=inl, km=km, bm=bm)
             split = choice[1] if choice[0] == "hip" else 0

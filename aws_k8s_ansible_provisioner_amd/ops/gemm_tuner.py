@@ -27,6 +27,16 @@ Choice = tuple  # ("torch",) | ("hip", splitk) | ("dgemm", splitk, prefetch_dept
 #                 ring_slots, in_launch_combine]) | ("wgemm",)
 _PLAN: dict = {}
 
+# positional defaults of a "dgemm" choice's variant fields after (split-K, prefetch):
+# (LDS-DMA tile width, ring depth, in-launch combine, kgemm rows, tile rows)
+VARIANT_DEFAULTS = (0, 0, False, 0, 64)
+
+
+def variant_fields(v) -> tuple:
+    """(bn, ns, inlaunch, km, bm) of a choice's tail, missing trailing fields defaulted."""
+    v = tuple(v)
+    return v + VARIANT_DEFAULTS[len(v):]
+
 
 def plan() -> dict:
     return _PLAN
@@ -146,7 +156,7 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
 
 
 def _gd_name(v) -> str:
-    bn, ns, inl, km, bm = (tuple(v) + (0, False, 0, 64))[:5]
+    bn, ns, inl, km, bm = variant_fields(v)[:5]
     if km:
         return f"k{km}"
     if bm == 128:
@@ -326,7 +336,7 @@ def _time_best_plain(M: int, name: str, weights) -> float:
             return _timed(lambda i: torch.ops.akap.kgemm(y, x, weights[i % n], c[6], 0, 1e-6, None,
                                                          None, None, None), n)
         if len(c) > 3 and c[3]:
-            bn, ns, inl, _, bm = (tuple(c[3:]) + (0, False, 0, 64))[:5]
+            bn, ns, inl, _, bm = variant_fields(c[3:])[:5]
             return _timed(_gd_call(M, N, K, c[1], bn, ns, inl, y, x, weights, 0, None, None,
                                    None, None, bm), n)
         ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)

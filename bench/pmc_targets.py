@@ -50,8 +50,11 @@ def decode(iters):
     B = 256
     # the tuner's M=256 choices (profiles/r2_gemm_variants.log), fixed so the profiled run
     # holds only the decode step's own dispatches: (split-K, prefetch, LDS-DMA tile width)
-    gemm_tuner._FUSED[B] = {"w_qkv": (1, 4, 0), "w_o": (4, 4, 0), "w_gate_up": (1, 1, 128),
-                            "w_down": (4, 4, 0)}
+    # (split-K, prefetch, LDS-DMA tile width, ring, in-launch, kgemm rows); the LM head on the
+    # wide-row kernel (wgemm.hip) as the tuner picks it at M=256 (profiles/r2_bench_*.log)
+    gemm_tuner._FUSED[B] = {"w_qkv": (1, 4, 0), "w_o": (1, 1, 0, 0, False, 32),
+                            "w_gate_up": (1, 1, 128, 8), "w_down": (1, 1, 0, 0, False, 32)}
+    gemm_tuner._PLAN[(B, m.lm_head.shape[0], m.lm_head.shape[1])] = ("wgemm",)
     lens = torch.full((B,), 640, dtype=torch.int32)
     kc, vc, bt = _paged(B, lens, m, 4096)
     pos = (lens - 1).to(torch.int64)
