@@ -14,10 +14,12 @@
 //
 // Staging: one K stage = (BM + 32) rows x 256 k of bf16 (24 / 32 KB) by global_load_lds
 // (LDS-DMA, 16 B per lane, lane-linear destination) into an NS = 4 slot ring -> three stages
-// in flight; counted `s_waitcnt vmcnt` + raw s_barrier per stage.  LDS row = 32 chunks of 16 B;
-// the low three chunk bits are XORed with the row (on the DMA source address and on the
-// fragment reads -- cdna_hip_programming.md rule 21), so a 16-row fragment read touches 8
-// distinct 16-B bank groups.
+// in flight; counted `s_waitcnt vmcnt` + raw s_barrier per stage.  LDS row = 32 chunks of 16 B
+// (512 B: every row starts on the same bank); the low four chunk bits are XORed with row & 15
+// (on the DMA source address and on the fragment reads -- cdna_hip_programming.md rule 21), so
+// the 16 lanes of each ds_read_b128 lane group (rows 0-3, 12-15 at chunk c, rows 4-11 at c+1)
+// land on 16 distinct 16-B bank positions: conflict-free (XOR with row & 7 measured 48 %
+// bank-conflict cycles, profiles/r2_pmc_decode_v2.md).
 #include "common.h"
 #include "kernels.h"
 
@@ -27,7 +29,7 @@ constexpr int KBN = 32;    // output columns per workgroup
 constexpr int KST = 256;   // K per stage (4 waves x 64)
 constexpr int KNS = 4;     // ring slots
 
-__device__ __forceinline__ int kswz(int row, int chunk) { return row * 32 + (chunk ^ (row & 7)); }
+__device__ __forceinline__ int kswz(int row, int chunk) { return row * 32 + (chunk ^ (row & 15)); }
 
 __device__ __forceinline__ void kglds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(256, 1) void kgemm_kernel(DGemmArgs p) {
   for (int i = 0; i < G; ++i) {
     const int u = (w * G + i) * 64 + lane;
     const int row = u >> 5;
-    const int lchunk = (u & 31) ^ (row & 7);
+    const int lchunk = (u & 31) ^ (row & 15);
     const bf16* base;
     if (row < BM) {
       const int m = m0 + row;
