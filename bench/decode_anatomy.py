@@ -30,11 +30,20 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="e4m3 KV cache")
     ap.add_argument("--prefill", type=int, default=0,
                     help="instead: a prefill step of B sequences x this many new tokens")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="one TP rank's shard, collectives stubbed (bench/tp_shard_rehearsal.py)")
     a = ap.parse_args()
     ops.load_native(required=True)
     dev = torch.device("cuda", 0)
     cfg = get_config(a.model)
-    m = DecoderLM(cfg, dev, max_model_len=4096)
+    pstate = None
+    if a.tp > 1:
+        from aws_k8s_ansible_provisioner_amd.parallel import state
+        from tp_shard_rehearsal import stub_collectives
+        pstate = state.ParallelState(rank=0, world_size=1, tp_size=a.tp, tp_rank=0)
+        state.set_state(pstate)
+        stub_collectives(a.tp)
+    m = DecoderLM(cfg, dev, max_model_len=4096, pstate=pstate)
     B, BS = a.B, 32
     lens = torch.randint(a.ctx - 128, a.ctx + 129, (B,), dtype=torch.int32)
     nb = [math.ceil(int(x) / BS) for x in lens]
@@ -52,9 +61,12 @@ def main():
     slots = torch.tensor([int(bt[s, int(pos[s]) // BS]) * BS + int(pos[s]) % BS
                           for s in range(B)], dtype=torch.int64)
     d = lambda t: t.to(dev)  # noqa: E731
-    ws = ops.decode_workspace(B, m.hkv, m.hq // m.hkv, 1, dev)
+    parts = 1 if B * m.hkv >= 2048 else min(math.ceil(2048 / (B * m.hkv)), 16)
+    psz = math.ceil(math.ceil(4096 / parts) / 128) * 128
+    parts = math.ceil(4096 / psz)
+    ws = ops.decode_workspace(B, m.hkv, m.hq // m.hkv, parts, dev)
     batch = AttnBatch(False, d(pos), d(slots), d(bt), d(lens), d(torch.arange(B + 1,
-                      dtype=torch.int32)), None, None, 1, 4096, ws)
+                      dtype=torch.int32)), None, None, parts, psz, ws)
     if a.prefill:
         P = a.prefill
         lens = torch.full((B,), P, dtype=torch.int32)
