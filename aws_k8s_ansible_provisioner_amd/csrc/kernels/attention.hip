@@ -507,7 +507,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
   const int kvh = blockIdx.y;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int w = tid >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar registers
   const int r = lane & 31;
   const int h = lane >> 5;
   const int seq = p.tile_seq[tile];
@@ -587,31 +587,33 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
 
   // LDS-DMA staging of tile t into buffer buf: 16 K + 16 V instructions of 1 KiB, 4 + 4 per
   // wave.  K: LDS 16-B slot s holds (key s/16, logical column (s%16) ^ (key&15)); the lane
-  // writing slot s loads that piece from the fragment-ordered K cache chunk.
+  // writing slot s loads that piece from the fragment-ordered K cache chunk.  Every piece a
+  // wave stages lies in 32-key chunk (w >> 1) of the tile, so the chunk base is wave-uniform
+  // (scalar) and the per-lane offsets are the same for every tile.
+  int koff[4], voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int s = (w * 4 + i) * 64 + lane;
+    const int key = s >> 4;
+    const int dc = (s & 15) ^ (key & 15);
+    const int k32 = key & 31;
+    const int tt = (k32 >> 2) & 1, r16 = ((k32 >> 3) << 2) | (k32 & 3);
+    koff[i] = (((tt * 4 + (dc >> 2)) * 16 + r16) * 4 + (dc & 3)) * 8;
+    voff[i] = (s & 511) * 8;
+  }
   auto stage_glds = [&](int t, int buf) {
     bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
     bf16* vl = kl + kFaKeys * kD;
+    const int chunk = min(t * 2 + (w >> 1), last_chunk);
+    const int blk = __builtin_amdgcn_readfirstlane(bt_s[chunk]);
+    const size_t base =
+        ((size_t)blk * p.Hkv + kvh) * BS * kD + (size_t)((chunk * 32) % BS) * kD;
+    const bf16* kb = static_cast<const bf16*>(p.k_cache) + base;
+    const bf16* vb = static_cast<const bf16*>(p.v_cache) + base;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = w * 4 + i;
-      const int s = j * 64 + lane;
-      const int key = s >> 4;
-      const int dc = (s & 15) ^ (key & 15);
-      const int k32 = key & 31;
-      const int tt = (k32 >> 2) & 1, r16 = ((k32 >> 3) << 2) | (k32 & 3);
-      const int within = ((tt * 4 + (dc >> 2)) * 16 + r16) * 4 + (dc & 3);
-      const int chunk = min(t * 2 + (key >> 5), last_chunk);
-      const size_t base = ((size_t)bt_s[chunk] * p.Hkv + kvh) * BS * kD + (size_t)((chunk * 32) % BS) * kD;
-      fa_glds16(static_cast<const bf16*>(p.k_cache) + base + within * 8, kl + j * 512);
-    }
+    for (int i = 0; i < 4; ++i) fa_glds16(kb + koff[i], kl + (w * 4 + i) * 512);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = w * 4 + i;
-      const int s = j * 64 + lane;
-      const int chunk = min(t * 2 + (s >> 9), last_chunk);
-      const size_t base = ((size_t)bt_s[chunk] * p.Hkv + kvh) * BS * kD + (size_t)((chunk * 32) % BS) * kD;
-      fa_glds16(static_cast<const bf16*>(p.v_cache) + base + (s & 511) * 8, vl + j * 512);
-    }
+    for (int i = 0; i < 4; ++i) fa_glds16(vb + voff[i], vl + (w * 4 + i) * 512);
   };
 
   f32x16 oacc[4];
@@ -663,34 +665,40 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
               kl + key * kD + (((2 * s8 + h) ^ (key & 15)) * 8));
           sacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s8], sacc[k], 0, 0, 0);
         }
-      // scale (log2 domain), causal mask, running max
+      // causal mask (wave-uniform branch: only tiles that cross this wave's diagonal pay for
+      // it) and the running max on the raw scores -- the log2-domain scale is positive, so
+      // it commutes with max and folds into the exponent's FMA below
       const bool need_mask = key0 + kFaKeys - 1 > w_min_limit;
-      float mx = -1e30f;
+      float mx = -INFINITY;
+      if (need_mask) {
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < 2; ++k)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          float v = sacc[k][j] * p.scale_log2;
-          if (need_mask) {
+          for (int j = 0; j < 16; ++j) {
             const int kk = key0 + 32 * k + (j & 3) + 8 * (j >> 2) + 4 * h;
-            if (kk > limit) v = -INFINITY;
+            if (kk > limit) sacc[k][j] = -INFINITY;
+            mx = fmaxf(mx, sacc[k][j]);
           }
-          sacc[k][j] = v;
-          mx = fmaxf(mx, v);
-        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sacc[k][j]);
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
+      const float m_new = fmaxf(m_run, mx * p.scale_log2);
       // raw v_exp_f32 (no denormal range fix-up: arguments are <= 0, tiny results flush)
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      float rs = 0.f;
+      float rsp[4] = {0.f, 0.f, 0.f, 0.f};  // four short add chains instead of one of 32
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float e = __builtin_amdgcn_exp2f(sacc[k][j] - m_new);
+          const float e = __builtin_amdgcn_exp2f(fmaf(sacc[k][j], p.scale_log2, -m_new));
           sacc[k][j] = e;
-          rs += e;
+          rsp[j & 3] += e;
         }
+      float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
       rs += __shfl_xor(rs, 32, 64);
       l_run = l_run * alpha + rs;
       // rescale only when some row's running max moved (alpha == 1 exactly otherwise): past

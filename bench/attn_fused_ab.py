@@ -29,6 +29,7 @@ def main():
     dev = "cuda"
     B, D, bs, Hq, Hkv = a.B, 128, 32, a.hq, a.hkv
     G = Hq // Hkv
+    torch.manual_seed(0)
     lens = torch.randint(a.ctx - 128, a.ctx + 129, (B,), dtype=torch.int32)
     nb = [math.ceil(int(x) / bs) for x in lens]
     NB = sum(nb) + 8
@@ -51,7 +52,7 @@ def main():
     qw = torch.ones(D, dtype=torch.bfloat16, device=dev)
     kw = torch.ones(D, dtype=torch.bfloat16, device=dev)
     bt, lens_d, pos_d, slots_d = bt.to(dev), lens.to(dev), pos.to(dev), slots.to(dev)
-    ws = ops.decode_workspace(B, Hkv, G, 1, dev)
+    ws = ops.decode_workspace(B, Hkv, G, int(os.environ.get("AB_WS_PARTS", "1")), dev)
     scale = 1 / math.sqrt(D)
     kv_bytes = int(lens.sum()) * Hkv * D * 2 * 2
     qbuf = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=dev)

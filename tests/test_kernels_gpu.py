@@ -509,6 +509,7 @@ def test_paged_attention_decode_fp8(num_parts, part_size, fused):
     pos = (sl - 1).to(torch.int64)
     slots = torch.tensor([int(bt[s, int(pos[s]) // 32]) * 32 + int(pos[s]) % 32
                           for s in range(B)], dtype=torch.int64)
+    slots[1] = -1  # padding row: no cache write, attends what the cache holds
     cs = ref.rope_cos_sin(4096, 128, 1e6)
     kr, vr = kc8.clone(), vc8.clone()
     q_ref = torch.empty(B, hq, 128).bfloat16()
@@ -520,6 +521,9 @@ def test_paged_attention_decode_fp8(num_parts, part_size, fused):
                                      scale, 1e-6, workspace=ws, num_parts=num_parts,
                                      part_size=part_size)
     _close(out, exp, atol=4e-2, rtol=4e-2)
+    dq = lambda t: t.cpu().view(torch.float8_e4m3fn).float()  # noqa: E731
+    _close(dq(kg), dq(kr), atol=1e-2, rtol=0.13)
+    assert torch.equal(vg.cpu(), vr)  # the new token's V group is stored back whole
 
 
 @pytest.mark.parametrize("tile_rows", [64, 128])
