@@ -475,11 +475,35 @@ __global__ __launch_bounds__(256) void paged_attn_decode_persistent_kernel(AttnP
 // global loads in flight during the current tile's MFMAs), v_mfma_f32_32x32x16_bf16.
 //   S^T = K . Q^T : K fragments from an XOR-swizzled LDS image (A), Q^T from registers (B);
 //                   each lane owns one q row (column) -> softmax is lane-local + one xor-32.
-//   O^T = V^T . P^T: P^T straight from the S^T accumulators (bf16), V^T fragments are two
-//                   8-byte reads of the V-group image ([group][d][8 tokens], copied verbatim
-//                   from the paged cache); O^T's column is again the lane's q row, so the
-//                   online-softmax rescale needs no cross-lane traffic.
+//   O^T = V^T . P^T: P^T straight from the S^T accumulators (bf16); the S^T rows are keys
+//                   in fa_row_key order, so each V^T fragment is one 16-B read of the V-group
+//                   image ([group][d][8 tokens], copied verbatim from the paged cache); O^T's
+//                   column is again the lane's q row, so the online-softmax rescale needs no
+//                   cross-lane traffic.
 // ----------------------------------------------------------------------------------
+// lane l <-> lane l ^ 32 reductions by one v_permlane32_swap (VALU) instead of a
+// ds_bpermute round trip through LDS: with both operands = x, result [0] holds x of lanes
+// 0..31 in every lane's upper-half view and [1] the other half, so op([0], [1]) is the pair's
+// reduction in all 64 lanes
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x),
+                                                  false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x),
+                                                  false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// MFMA row r of an S^T sub-tile holds key fa_row_key(r) of the 32.  The 32x32 accumulator
+// gives lane half h the rows 8 i + 4 h + (0..3); with this order its P^T fragment for k-slice
+// s2 (accumulator registers 8 s2 .. 8 s2 + 7) is keys 16 s2 + 8 h + 0..7 -- one whole 8-token V
+// group, so every V^T fragment is a single 16-B LDS read of the cache's group image.
+__device__ __forceinline__ int fa_row_key(int r) {
+  return 16 * (r >> 4) + 8 * ((r >> 2) & 1) + 4 * ((r >> 3) & 1) + (r & 3);
+}
+
 constexpr int kFaRows = 128;
 constexpr int kFaKeys = 64;
 constexpr int kFaBtCache = 1024;  // chunk -> block id cache in LDS (32768 keys)
@@ -495,8 +519,14 @@ __device__ __forceinline__ void fa_glds16(const void* g, void* lds_wave_base) {
 // next tile is the counted vmcnt at the top of the following iteration (raw s_barrier, never
 // __syncthreads, whose fence would drain the DMA early).  The K image's XOR swizzle moves to
 // the per-lane DMA source address (the LDS destination of a DMA is lane-linear).
-template <bool F8, bool GL, bool VSWAP = true>
-__global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParams p) {
+// NW = waves per workgroup (4: 128 q rows, two workgroups per CU; 8: 256 q rows, one
+// workgroup per CU -- every staged K/V tile feeds twice the rows).
+template <bool F8, bool GL, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(AttnParams p) {
+  constexpr int ROWS = 32 * NW;
+  constexpr int NT = 64 * NW;    // threads
+  constexpr int PW = 16 / NW;    // 1-KiB K (and V) DMA pieces per wave per tile
+  static_assert(NW == 4 || (NW == 8 && GL), "the register-staged path assumes 256 threads");
   // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
   // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * 2 * kFaKeys * kD + 2 * kFaBtCache];
@@ -531,7 +561,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
     qf[s8] = valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * s8 + 8 * h)
                    : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
 
-  const int wg_last_pos = min(q_len - 1, (row0 + kFaRows - 1) / G);
+  const int wg_last_pos = min(q_len - 1, (row0 + ROWS - 1) / G);
   const int wg_limit = ctx0 + wg_last_pos;
   const int ntiles = wg_limit / kFaKeys + 1;
   const int w_first_pos = (row0 + 32 * w) / G;
@@ -590,10 +620,10 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
   // writing slot s loads that piece from the fragment-ordered K cache chunk.  Every piece a
   // wave stages lies in 32-key chunk (w >> 1) of the tile, so the chunk base is wave-uniform
   // (scalar) and the per-lane offsets are the same for every tile.
-  int koff[4], voff[4];
+  int koff[PW], voff[PW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int s = (w * 4 + i) * 64 + lane;
+  for (int i = 0; i < PW; ++i) {
+    const int s = (w * PW + i) * 64 + lane;
     const int key = s >> 4;
     const int dc = (s & 15) ^ (key & 15);
     const int k32 = key & 31;
@@ -604,16 +634,16 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
   auto stage_glds = [&](int t, int buf) {
     bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
     bf16* vl = kl + kFaKeys * kD;
-    const int chunk = min(t * 2 + (w >> 1), last_chunk);
+    const int chunk = min(t * 2 + ((w * PW) >> 3), last_chunk);
     const int blk = __builtin_amdgcn_readfirstlane(bt_s[chunk]);
     const size_t base =
         ((size_t)blk * p.Hkv + kvh) * BS * kD + (size_t)((chunk * 32) % BS) * kD;
     const bf16* kb = static_cast<const bf16*>(p.k_cache) + base;
     const bf16* vb = static_cast<const bf16*>(p.v_cache) + base;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa_glds16(kb + koff[i], kl + (w * 4 + i) * 512);
+    for (int i = 0; i < PW; ++i) fa_glds16(kb + koff[i], kl + (w * PW + i) * 512);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa_glds16(vb + voff[i], vl + (w * 4 + i) * 512);
+    for (int i = 0; i < PW; ++i) fa_glds16(vb + voff[i], vl + (w * PW + i) * 512);
   };
 
   f32x16 oacc[4];
@@ -623,7 +653,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
     for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
 
-  for (int c = tid; c <= last_chunk; c += 256) bt_s[c] = bt[c * 32 / BS];
+  for (int c = tid; c <= last_chunk; c += NT) bt_s[c] = bt[c * 32 / BS];
   __syncthreads();
   if constexpr (GL) {
     stage_glds(0, 0);
@@ -660,7 +690,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
       for (int s8 = 0; s8 < 8; ++s8)
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          const int key = 32 * k + r;
+          const int key = 32 * k + fa_row_key(r);
           const bf16x8 a = *reinterpret_cast<const bf16x8*>(
               kl + key * kD + (((2 * s8 + h) ^ (key & 15)) * 8));
           sacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s8], sacc[k], 0, 0, 0);
@@ -675,7 +705,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
         for (int k = 0; k < 2; ++k)
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
-            const int kk = key0 + 32 * k + (j & 3) + 8 * (j >> 2) + 4 * h;
+            const int kk = key0 + 32 * k + 16 * (j >> 3) + 8 * h + (j & 7);
             if (kk > limit) sacc[k][j] = -INFINITY;
             mx = fmaxf(mx, sacc[k][j]);
           }
@@ -685,7 +715,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
 #pragma unroll
           for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sacc[k][j]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xor32_max(mx);
       const float m_new = fmaxf(m_run, mx * p.scale_log2);
       // raw v_exp_f32 (no denormal range fix-up: arguments are <= 0, tiny results flush)
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
@@ -698,8 +728,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
           sacc[k][j] = e;
           rsp[j & 3] += e;
         }
-      float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
-      rs += __shfl_xor(rs, 32, 64);
+      const float rs = xor32_sum((rsp[0] + rsp[1]) + (rsp[2] + rsp[3]));
       l_run = l_run * alpha + rs;
       // rescale only when some row's running max moved (alpha == 1 exactly otherwise): past
       // the first tiles of a causal row the max rarely changes
@@ -719,32 +748,12 @@ __global__ __launch_bounds__(256, 2) void paged_attn_prefill_fa_kernel(AttnParam
           bf16x8 pb;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[k][8 * s2 + j]);
-          const int g = 4 * k + 2 * s2;
+          // keys 16 s2 + 8 h + 0..7 of sub-tile k = V group 4 k + 2 s2 + h: one 16-B read
+          const int g = 4 * k + 2 * s2 + h;
           bf16x8 va[4];
-          if (VSWAP) {
-            // one conflict-free 16-B read per lane -- group g (lanes < 32) or g+1 (lanes >= 32)
-            // of dim d, all 8 tokens -- then two v_permlane32_swap exchange the 8-byte halves
-            // between lanes i and i+32: lane i ends with tokens 0-3 of g and g+1, lane i+32
-            // with tokens 4-7 (the 2 x 8-byte reads they replace hit 2-way bank conflicts)
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-              const u32x4 u =
-                  *reinterpret_cast<const u32x4*>(vl + ((g + h) * kD + 32 * dt + r) * 8);
-              const auto a = __builtin_amdgcn_permlane32_swap(u[0], u[2], false, false);
-              const auto b = __builtin_amdgcn_permlane32_swap(u[1], u[3], false, false);
-              const u32x4 o = {a[0], b[0], a[1], b[1]};
-              va[dt] = __builtin_bit_cast(bf16x8, o);
-            }
-          } else {
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-              const int d = 32 * dt + r;
-              const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vl + (g * kD + d) * 8 + 4 * h);
-              const bf16x4 hi =
-                  *reinterpret_cast<const bf16x4*>(vl + ((g + 1) * kD + d) * 8 + 4 * h);
-              va[dt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            }
-          }
+          for (int dt = 0; dt < 4; ++dt)
+            va[dt] = *reinterpret_cast<const bf16x8*>(vl + (g * kD + 32 * dt + r) * 8);
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt)
             oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[dt], pb, oacc[dt], 0, 0, 0);
@@ -809,12 +818,12 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows
                                hipStream_t s) {
   if (num_tiles == 0) return;
   const dim3 grid(num_tiles, p.Hkv);
-  if (tile_rows == kFaRows) {
+  if (tile_rows == 2 * kFaRows && !p.kv_fp8) {
+    paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(p);
+  } else if (tile_rows == kFaRows) {
     // bf16 caches: LDS-DMA staging (flags bit 10 selects the register-staged form for A/B)
-    // flags bit 11: the former pair-of-8-byte V fragment reads (A/B)
     if (p.kv_fp8) paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
     else if (p.flags & 1024) paged_attn_prefill_fa_kernel<false, false><<<grid, 256, 0, s>>>(p);
-    else if (p.flags & 2048) paged_attn_prefill_fa_kernel<false, true, false><<<grid, 256, 0, s>>>(p);
     else paged_attn_prefill_fa_kernel<false, true><<<grid, 256, 0, s>>>(p);
   } else {
     if (p.kv_fp8) paged_attn_prefill_kernel<true><<<grid, 256, 0, s>>>(p);

@@ -151,10 +151,13 @@ void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cach
                              Tensor tile_seq, Tensor tile_row, int64_t G, double scale,
                              int64_t tile_rows) {
   auto p = attn_params(out, q, k_cache, v_cache, block_tables, seq_lens, G, scale);
-  TORCH_CHECK(tile_rows == 64 || tile_rows == 128, "tile_rows must be 64 or 128");
+  TORCH_CHECK(tile_rows == 64 || tile_rows == 128 || tile_rows == 256,
+              "tile_rows must be 64, 128 or 256");
+  TORCH_CHECK(tile_rows != 256 || k_cache.scalar_type() == at::kBFloat16,
+              "tile_rows=256 needs a bf16 KV cache");
   // the flash-style kernel caches a sequence's block ids in LDS: <= 32768 keys
   TORCH_CHECK(tile_rows == 64 || block_tables.size(1) * k_cache.size(2) <= 32768,
-              "tile_rows=128 supports contexts up to 32768 tokens");
+              "tile_rows=128/256 support contexts up to 32768 tokens");
   TORCH_CHECK(q_start.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
                   tile_row.scalar_type() == at::kInt,
               "q_start/tile maps must be int32");

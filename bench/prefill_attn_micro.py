@@ -36,7 +36,7 @@ def main():
     sl = torch.full((B,), L, dtype=torch.int32, device=dev)
     qs = torch.arange(0, B * L + 1, L, dtype=torch.int32, device=dev)
     flops = B * a.hq * L * L / 2 * D * 4
-    for rows in (64, 128):
+    for rows in (64, 128, 256):
         ts, tr = [], []
         for s in range(B):
             for r in range(0, L * G, rows):

@@ -127,7 +127,7 @@ def _tiles(seqs, G, rows=64):
 
 @pytest.mark.parametrize("bs", [32, 64])
 @pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (8, 8), (64, 8)])
-@pytest.mark.parametrize("tile_rows", [64, 128])
+@pytest.mark.parametrize("tile_rows", [64, 128, 256])
 def test_paged_attention_prefill(bs, hq, hkv, tile_rows):
     seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (520, 7), (64, 1), (700, 650)]
     q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, bs, seed=bs + hq)
