@@ -686,15 +686,32 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
       for (int k = 0; k < 2; ++k)
 #pragma unroll
         for (int j = 0; j < 16; ++j) sacc[k][j] = 0.f;
+      // every K fragment of the tile is requested before the first MFMA, so the LDS latency
+      // is paid once per tile, not once per MFMA
+      bf16x8 kf[8][2];
 #pragma unroll
       for (int s8 = 0; s8 < 8; ++s8)
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const int key = 32 * k + fa_row_key(r);
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(
+          kf[s8][k] = *reinterpret_cast<const bf16x8*>(
               kl + key * kD + (((2 * s8 + h) ^ (key & 15)) * 8));
-          sacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s8], sacc[k], 0, 0, 0);
         }
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          sacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s8][k], qf[s8], sacc[k], 0, 0, 0);
+      // likewise the V^T fragments: requested now, their latency hides under the softmax
+      bf16x8 vf[2][2][4];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            vf[k][s2][dt] = *reinterpret_cast<const bf16x8*>(
+                vl + ((4 * k + 2 * s2 + h) * kD + 32 * dt + r) * 8);
       // causal mask (wave-uniform branch: only tiles that cross this wave's diagonal pay for
       // it) and the running max on the raw scores -- the log2-domain scale is positive, so
       // it commutes with max and folds into the exponent's FMA below
@@ -748,15 +765,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
           bf16x8 pb;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[k][8 * s2 + j]);
-          // keys 16 s2 + 8 h + 0..7 of sub-tile k = V group 4 k + 2 s2 + h: one 16-B read
-          const int g = 4 * k + 2 * s2 + h;
-          bf16x8 va[4];
+          // keys 16 s2 + 8 h + 0..7 of sub-tile k = V group 4 k + 2 s2 + h (vf above)
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt)
-            va[dt] = *reinterpret_cast<const bf16x8*>(vl + (g * kD + 32 * dt + r) * 8);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt)
-            oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[dt], pb, oacc[dt], 0, 0, 0);
+            oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[k][s2][dt], pb, oacc[dt], 0,
+                                                               0, 0);
         }
     }
     if constexpr (!GL) {
