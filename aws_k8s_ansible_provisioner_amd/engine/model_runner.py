@@ -317,11 +317,19 @@ class ModelRunner:
             from ..ops import gemm_tuner
 
             t1 = time.time()
-            gemm_tuner.tune_model(self.model, [b for b in self.buckets if b >= 16],
-                                  log=self.log)
-            if os.environ.get("AKAP_FUSED_GEMM", "1") != "0":
-                gemm_tuner.tune_fused(self.model, [b for b in self.buckets if b >= 16],
-                                      log=self.log)
+            tune_ms = [b for b in self.buckets if b >= 16]
+            cache = os.environ.get("AKAP_GEMM_TUNE_CACHE")
+            if cache and self.model.ps.world_size > 1:
+                cache = f"{cache}.rank{self.model.ps.rank}"
+            if cache and gemm_tuner.load_cache(cache, self.model, tune_ms):
+                self.log(f"[runner] GEMM plan loaded from {cache} "
+                         f"({len(gemm_tuner.plan())} shapes)")
+            else:
+                gemm_tuner.tune_model(self.model, tune_ms, log=self.log)
+                if os.environ.get("AKAP_FUSED_GEMM", "1") != "0":
+                    gemm_tuner.tune_fused(self.model, tune_ms, log=self.log)
+                if cache:
+                    gemm_tuner.save_cache(cache, self.model, tune_ms)
             self.log(f"[runner] GEMM tuning {time.time() - t1:.1f}s")
         self._stage_decode(self.max_seqs)
         torch.cuda.synchronize()

@@ -323,6 +323,73 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
     return chosen
 
 
+# ----------------------------------------------------------------------------- tuning cache
+# The plan is a pure function of (GPU, kernel library, model shapes, TP layout, batch
+# buckets): a JSON file keyed on those lets a restarted engine skip the ~3-10 s of timing
+# (AKAP_GEMM_TUNE_CACHE=path, engine/model_runner.py), and keeps a profiled run free of the
+# tuning candidates' launches.  Any key mismatch -> retune and overwrite.
+CACHE_VERSION = 1
+
+
+def cache_key(model, Ms: Sequence[int]) -> dict:
+    import os
+
+    from . import _LIB
+
+    shapes = sorted({(name, tuple(getattr(lw, name).shape)) for lw in model.layers
+                     for name in ("w_qkv", "w_o", "w_gate_up", "w_down")
+                     if getattr(lw, name, None) is not None})
+    lm = getattr(model, "lm_head", None)
+    try:
+        arch = torch.cuda.get_device_properties(0).gcnArchName if torch.cuda.is_available() \
+            else "cpu"
+    except Exception:  # pragma: no cover - device query failures
+        arch = "unknown"
+    try:
+        st = os.stat(_LIB)
+        lib = [st.st_size, int(st.st_mtime)]
+    except OSError:
+        lib = None
+    return {"version": CACHE_VERSION, "arch": arch, "lib": lib,
+            "tp": [model.ps.tp_size, model.ps.tp_rank], "layers": len(model.layers),
+            "shapes": [[n, list(sh)] for n, sh in shapes],
+            "lm_head": list(lm.shape) if lm is not None else None, "Ms": sorted(int(m) for m in Ms)}
+
+
+def save_cache(path: str, model, Ms: Sequence[int]) -> None:
+    import json
+    import os
+
+    data = {"key": cache_key(model, Ms),
+            "plan": [[list(k), list(v)] for k, v in sorted(_PLAN.items())],
+            "fused": [[m, {n: list(t) for n, t in pl.items()}] for m, pl in sorted(_FUSED.items())]}
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump(data, f)
+    os.replace(tmp, path)  # readers never see a half-written file
+
+
+def load_cache(path: str, model, Ms: Sequence[int]) -> bool:
+    """Install the cached plan when its key matches this model/GPU/library; False otherwise."""
+    import json
+
+    try:
+        with open(path) as f:
+            data = json.load(f)
+    except (OSError, ValueError):
+        return False
+    if data.get("key") != cache_key(model, Ms):
+        return False
+    _PLAN.clear()
+    _FUSED.clear()
+    for k, v in data["plan"]:
+        _PLAN[tuple(k)] = tuple(v)
+    for m, pl in data["fused"]:
+        _FUSED[int(m)] = {n: tuple(t) for n, t in pl.items()}
+    return True
+
+
 def _time_best_plain(M: int, name: str, weights) -> float:
     """us of the plan's choice for this projection (hipBLASLt unless tuned otherwise)."""
     w0 = weights[0]

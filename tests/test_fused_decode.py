@@ -5,6 +5,8 @@ gate|up epilogue) vs the regular decode forward of the same model and inputs.
 CPU: the ops' torch reference paths (chain bookkeeping: sums of squares, residual stream,
 norm weights per position).  GPU: the HIP kernels, split-K and prefetch variants included.
 """
+import dataclasses
+
 import pytest
 import torch
 
@@ -101,3 +103,35 @@ def test_fused_epilogues_gpu():
         want2 = ops.reference.silu_and_mul(gu.to(torch.bfloat16)).float()
         assert act.shape == (M, N)
         assert (act.float() - want2).abs().max().item() <= 2e-2 * want2.abs().max().item()
+
+
+def test_gemm_tune_cache_round_trip(tmp_path):
+    """The persisted plan reloads only for the same model shapes / batch buckets / library."""
+    from aws_k8s_ansible_provisioner_amd.ops import gemm_tuner
+
+    m = DecoderLM(get_config("tiny-llama"), device="cpu", seed=0, max_model_len=64)
+    Ms = [16, 32]
+    w = m.layers[0].w_qkv
+    gemm_tuner._PLAN.clear()
+    gemm_tuner._FUSED.clear()
+    gemm_tuner._PLAN[(16,) + tuple(w.shape)] = ("dgemm", 1, 1, 128, 4, False, 0, 128)
+    gemm_tuner._PLAN[(32,) + tuple(w.shape)] = ("wgemm",)
+    gemm_tuner._FUSED[32] = {"w_qkv": (1, 4, 0, 0, False, 0, 64),
+                             "w_o": (1, 1, 0, 0, False, 32, 64)}
+    want_plan, want_fused = dict(gemm_tuner._PLAN), dict(gemm_tuner._FUSED)
+    path = str(tmp_path / "tune.json")
+    gemm_tuner.save_cache(path, m, Ms)
+    gemm_tuner._PLAN.clear()
+    gemm_tuner._FUSED.clear()
+    assert not gemm_tuner.load_cache(path, m, [16, 32, 64])  # other buckets: retune
+    assert not gemm_tuner._PLAN
+    cfg = dataclasses.replace(get_config("tiny-llama"), intermediate_size=2 * get_config(
+        "tiny-llama").intermediate_size)
+    other = DecoderLM(cfg, device="cpu", seed=0, max_model_len=64)
+    assert not gemm_tuner.load_cache(path, other, Ms)          # other shapes: retune
+    assert gemm_tuner.load_cache(path, m, Ms)
+    assert gemm_tuner._PLAN == want_plan and gemm_tuner._FUSED == want_fused
+    assert gemm_tuner.lookup(32, *w.shape) == ("wgemm",)
+    gemm_tuner._PLAN.clear()
+    gemm_tuner._FUSED.clear()
+    assert not gemm_tuner.load_cache(str(tmp_path / "missing.json"), m, Ms)
