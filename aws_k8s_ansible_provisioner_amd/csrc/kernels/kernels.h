@@ -163,6 +163,11 @@ void launch_moe_combine_split(const float* P, const float* wts, const int32_t* i
 // ---- moe.hip ----
 void launch_moe_topk_softmax(const void* logits, int ld, int E, int K, float* topk_w,
                              int32_t* topk_ids, int T, int renormalize, hipStream_t s);
+// router GEMM (h [T, d] . W[E, d]^T, bf16-rounded logits) + softmax + top-k, E <= 16
+bool moe_router_topk_supported(int E, int d);
+void launch_moe_router_topk(const void* h, int ldh, const void* W, int d, int E, int K,
+                            float* topk_w, int32_t* topk_ids, int T, int renormalize,
+                            hipStream_t s);
 void launch_moe_align(const int32_t* topk_ids, int n, int E, int block, int32_t* sorted_ids,
                       int32_t* expert_offsets, int32_t* num_padded, int32_t* inv,
                       int32_t* tile_expert, int max_tiles, hipStream_t s);

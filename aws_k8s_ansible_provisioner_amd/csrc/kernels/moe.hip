@@ -9,6 +9,43 @@
 
 namespace akap {
 
+// softmax over E logits (read through x(e)) -> top-K (ties -> lowest expert id), optional
+// renormalisation of the K weights
+template <typename F>
+__device__ __forceinline__ void topk_softmax_row(F x, int E, int K, float* __restrict__ w_out,
+                                                 int32_t* __restrict__ id_out, int renorm) {
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) mx = fmaxf(mx, x(e));
+  float z = 0.f;
+  for (int e = 0; e < E; ++e) z += __expf(x(e) - mx);
+  const float invz = 1.f / z;
+  float wsum = 0.f;
+  // selection by repeated scan (K is tiny: 1..8)
+  uint64_t taken_lo = 0, taken_hi = 0, taken_2 = 0, taken_3 = 0;
+  for (int k = 0; k < K; ++k) {
+    float best = -INFINITY;
+    int bi = 0;
+    for (int e = 0; e < E; ++e) {
+      const uint64_t bit = 1ull << (e & 63);
+      const uint64_t word = e < 64 ? taken_lo : e < 128 ? taken_hi : e < 192 ? taken_2 : taken_3;
+      if (word & bit) continue;
+      const float v = x(e);
+      if (v > best) { best = v; bi = e; }
+    }
+    const uint64_t bit = 1ull << (bi & 63);
+    if (bi < 64) taken_lo |= bit; else if (bi < 128) taken_hi |= bit;
+    else if (bi < 192) taken_2 |= bit; else taken_3 |= bit;
+    const float w = __expf(best - mx) * invz;
+    w_out[k] = w;
+    id_out[k] = bi;
+    wsum += w;
+  }
+  if (renorm) {
+    const float inv = 1.f / wsum;
+    for (int k = 0; k < K; ++k) w_out[k] *= inv;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restrict__ logits,
                                                                int ld, int E, int K,
@@ -18,36 +55,68 @@ __global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restri
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= Tn) return;
   const T* x = logits + (size_t)t * ld;
-  float mx = -INFINITY;
-  for (int e = 0; e < E; ++e) mx = fmaxf(mx, (float)x[e]);
-  float z = 0.f;
-  for (int e = 0; e < E; ++e) z += __expf((float)x[e] - mx);
-  const float invz = 1.f / z;
-  float wsum = 0.f;
-  // selection by repeated scan (K is tiny: 1..8); ties -> lowest expert id
-  uint64_t taken_lo = 0, taken_hi = 0, taken_2 = 0, taken_3 = 0;
-  for (int k = 0; k < K; ++k) {
-    float best = -INFINITY;
-    int bi = 0;
-    for (int e = 0; e < E; ++e) {
-      const uint64_t bit = 1ull << (e & 63);
-      const uint64_t word = e < 64 ? taken_lo : e < 128 ? taken_hi : e < 192 ? taken_2 : taken_3;
-      if (word & bit) continue;
-      const float v = (float)x[e];
-      if (v > best) { best = v; bi = e; }
+  topk_softmax_row([&](int e) { return (float)x[e]; }, E, K, topk_w + (size_t)t * K,
+                   topk_ids + (size_t)t * K, renorm);
+}
+
+// Router GEMM + softmax + top-k in one launch for E <= kRouterMaxE experts: one workgroup per
+// token.  Its 256 threads take 8-element slices of the hidden row and of every router row
+// (the E x d router, 64 KB for Mixtral, stays L2-resident), the E dot products are reduced
+// across the workgroup, and the logits are rounded to bf16 like the separate F.linear's
+// output before the softmax.  Replaces a hipBLASLt launch (M x 8 output: 13.5 us at M = 128)
+// plus the top-k launch (profiles/r2_mixtral_bench_kernel_stats.md).
+constexpr int kRouterMaxE = 16;
+
+__global__ __launch_bounds__(256) void moe_router_topk_kernel(const bf16* __restrict__ h, int ldh,
+                                                              const bf16* __restrict__ W, int d,
+                                                              int E, int K,
+                                                              float* __restrict__ topk_w,
+                                                              int32_t* __restrict__ topk_ids,
+                                                              int renorm) {
+  __shared__ float part[4][kRouterMaxE];
+  __shared__ float logit[kRouterMaxE];
+  const int t = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bf16* x = h + (size_t)t * ldh;
+  float acc[kRouterMaxE];
+#pragma unroll
+  for (int e = 0; e < kRouterMaxE; ++e) acc[e] = 0.f;
+  for (int c = tid; c < d / 8; c += 256) {
+    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(x + 8 * c);
+#pragma unroll
+    for (int e = 0; e < kRouterMaxE; ++e) {
+      if (e < E) {
+        const bf16x8 wv = *reinterpret_cast<const bf16x8*>(W + (size_t)e * d + 8 * c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[e] += bf2f(xv[i]) * bf2f(wv[i]);
+      }
     }
-    const uint64_t bit = 1ull << (bi & 63);
-    if (bi < 64) taken_lo |= bit; else if (bi < 128) taken_hi |= bit;
-    else if (bi < 192) taken_2 |= bit; else taken_3 |= bit;
-    const float w = __expf(best - mx) * invz;
-    topk_w[(size_t)t * K + k] = w;
-    topk_ids[(size_t)t * K + k] = bi;
-    wsum += w;
   }
-  if (renorm) {
-    const float inv = 1.f / wsum;
-    for (int k = 0; k < K; ++k) topk_w[(size_t)t * K + k] *= inv;
+#pragma unroll
+  for (int e = 0; e < kRouterMaxE; ++e) {
+    if (e < E) {
+      float v = acc[e];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) part[w][e] = v;
+    }
   }
+  __syncthreads();
+  if (tid < E) logit[tid] = bf2f(f2bf(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]));
+  __syncthreads();
+  if (tid == 0)
+    topk_softmax_row([&](int e) { return logit[e]; }, E, K, topk_w + (size_t)t * K,
+                     topk_ids + (size_t)t * K, renorm);
+}
+
+bool moe_router_topk_supported(int E, int d) { return E >= 1 && E <= kRouterMaxE && d % 8 == 0; }
+
+void launch_moe_router_topk(const void* h, int ldh, const void* W, int d, int E, int K,
+                            float* topk_w, int32_t* topk_ids, int T, int renormalize,
+                            hipStream_t s) {
+  if (T == 0) return;
+  moe_router_topk_kernel<<<T, 256, 0, s>>>((const bf16*)h, ldh, (const bf16*)W, d, E, K, topk_w,
+                                           topk_ids, renormalize);
 }
 
 void launch_moe_topk_softmax(const void* logits, int ld, int E, int K, float* topk_w,

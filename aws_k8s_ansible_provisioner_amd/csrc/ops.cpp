@@ -494,6 +494,20 @@ void moe_topk_softmax(Tensor logits, Tensor topk_w, Tensor topk_ids, bool renorm
                                 cur_stream());
 }
 
+void moe_router_topk(Tensor h, Tensor router, Tensor topk_w, Tensor topk_ids, bool renorm) {
+  CHECK_GPU(h); CHECK_BF16(h); CHECK_LAST_CONTIG(h);
+  CHECK_GPU(router); CHECK_BF16(router); CHECK_CONTIG(router);
+  const int d = h.size(1), E = router.size(0);
+  TORCH_CHECK(router.size(1) == d, "router shape");
+  TORCH_CHECK(akap::moe_router_topk_supported(E, d), "fused router supports <= 16 experts, d % 8 == 0");
+  TORCH_CHECK(topk_w.size(0) >= h.size(0) && topk_ids.size(0) >= h.size(0), "outputs too small");
+  TORCH_CHECK(((uintptr_t)h.data_ptr() % 16) == 0 && h.stride(0) % 8 == 0, "h rows 16-B aligned");
+  const c10::DeviceGuard g(h.device());
+  akap::launch_moe_router_topk(h.data_ptr(), h.stride(0), router.data_ptr(), d, E, topk_w.size(1),
+                               topk_w.data_ptr<float>(), topk_ids.data_ptr<int32_t>(), h.size(0),
+                               renorm ? 1 : 0, cur_stream());
+}
+
 void moe_align(Tensor topk_ids, int64_t E, int64_t block, Tensor sorted_ids, Tensor offsets,
                Tensor num_padded, Tensor inv, Tensor tile_expert) {
   CHECK_GPU(topk_ids); CHECK_CONTIG(topk_ids);
@@ -883,6 +897,7 @@ TORCH_LIBRARY(akap, m) {
         "Tensor(b!) aout, Tensor(c!) ss, bool two_shot) -> ()");
   m.def("car_destroy(int h) -> ()");
   m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
+  m.def("moe_router_topk(Tensor h, Tensor router, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def(
       "moe_align(Tensor topk_ids, int E, int block, Tensor(a!) sorted_ids, Tensor(b!) offsets, "
       "Tensor(c!) num_padded, Tensor(d!) inv, Tensor(e!) tile_expert) -> ()");
@@ -929,6 +944,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("wgemm", &wgemm);
   m.impl("kgemm", &kgemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
+  m.impl("moe_router_topk", &moe_router_topk);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);

@@ -312,7 +312,9 @@ class ModelRunner:
                 "AKAP_TUNABLEOP_FILE", os.path.join(os.getcwd(), "tunableop_results.csv")))
         # safe static contents: every row is padding
         self._pad_host(0, self.max_seqs)
-        if os.environ.get("AKAP_GEMM_TUNE", "1") != "0" and not self.mcfg.is_moe:
+        if os.environ.get("AKAP_GEMM_TUNE", "1") != "0":
+            # MoE models: the attention projections are tuned (the experts run the grouped
+            # GEMM; tune_fused skips MoE layers)
             # per-(M, N, K) hipBLASLt vs MFMA-kernel choice on the real, cold layer weights
             from ..ops import gemm_tuner
 

@@ -149,8 +149,7 @@ class MoEBlock:
 
     def _forward_tokens(self, h: torch.Tensor) -> torch.Tensor:
         T, d = h.shape
-        logits = F.linear(h, self.router)
-        w, ids = ops.moe_topk_softmax(logits, self.K, renormalize=True)
+        w, ids = ops.moe_router_topk(h, self.router, self.K, renormalize=True)
         capturing = h.is_cuda and torch.cuda.is_current_stream_capturing()
         if self.mode == "ep":
             if T <= self.ep_fixed_max_tokens or capturing:

@@ -456,6 +456,19 @@ def moe_topk_softmax(router_logits, top_k: int, renormalize: bool = True):
     return w, ids
 
 
+def moe_router_topk(h, router, top_k: int, renormalize: bool = True):
+    """Router logits (bf16, as F.linear(h, router)) -> softmax -> top-k in one launch on the
+    GPU for <= 16 experts (csrc/kernels/moe.hip); the two-step path otherwise."""
+    T, E = h.shape[0], router.shape[0]
+    if (_native(h) and E <= 16 and T <= 2048 and h.shape[1] % 8 == 0 and h.stride(-1) == 1
+            and h.stride(0) % 8 == 0):  # prefill-sized T: hipBLASLt + top-k is cheaper
+        w = torch.empty(T, top_k, dtype=torch.float32, device=h.device)
+        ids = torch.empty(T, top_k, dtype=torch.int32, device=h.device)
+        torch.ops.akap.moe_router_topk(h, router, w, ids, renormalize)
+        return w, ids
+    return moe_topk_softmax(torch.nn.functional.linear(h, router), top_k, renormalize)
+
+
 def moe_capacity(n: int, num_experts: int, block: int) -> int:
     cap = n + num_experts * (block - 1)
     return (cap + block - 1) // block * block

@@ -274,6 +274,28 @@ def test_embedding_vocab_parallel():
     _close(out2, exp2, atol=0)
 
 
+@pytest.mark.parametrize("T,E,K,d", [(1, 8, 2, 4096), (37, 8, 2, 4096), (128, 8, 2, 4096),
+                                     (64, 16, 4, 1024), (5, 3, 1, 256)])
+def test_moe_router_topk_fused(T, E, K, d):
+    """Router GEMM + softmax + top-k in one launch vs fp32 logits rounded to bf16 + reference."""
+    g = torch.Generator().manual_seed(T + E)
+    h = (torch.randn(T, d, generator=g) * 0.5).bfloat16()
+    router = (torch.randn(E, d, generator=g) * 0.05).bfloat16()
+    logits = (h.float() @ router.float().t()).bfloat16()
+    rw, rid = ref.moe_topk_softmax(logits, K)
+    w = torch.empty(T, K, dtype=torch.float32, device=DEV)
+    ids = torch.empty(T, K, dtype=torch.int32, device=DEV)
+    torch.ops.akap.moe_router_topk(h.to(DEV), router.to(DEV), w, ids, True)
+    # bf16 logits tie often at E = 8: compare the selected (expert, weight) sets, not the order
+    # among equal logits (ours: lowest id first; torch.topk: unspecified)
+    oi, o = ids.cpu().long().sort(dim=-1)
+    ri, r = rid.long().sort(dim=-1)
+    assert torch.equal(oi, ri)
+    _close(w.cpu().gather(1, o), rw.gather(1, r), atol=1e-3)
+    w2, ids2 = ops.moe_router_topk(h.to(DEV), router.to(DEV), K)  # the dispatching wrapper
+    assert torch.equal(ids2.cpu(), ids.cpu())
+
+
 def test_moe_routing():
     torch.manual_seed(6)
     T, E, K = 300, 8, 2
