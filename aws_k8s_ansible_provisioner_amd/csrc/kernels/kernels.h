@@ -155,7 +155,7 @@ bool moe_dgemm_supported(int N, int K, int pf, int silu, int splitk);
 void launch_moe_dgemm(const void* A, const void* W, void* Y, const int32_t* sorted_ids,
                       const int32_t* tile_expert, int max_tiles, int n_flat, int topk, int N,
                       int K, int lda, int ldy, int gather, int silu, int pf, int bm, int splitk,
-                      float* partials, hipStream_t s);
+                      float* partials, bool nt_weights, hipStream_t s);
 // out[t] = sum_k w[t,k] * sum_z P[z, inv[t*K+k], :]  (split-K fp32 partials of the down GEMM)
 void launch_moe_combine_split(const float* P, const float* wts, const int32_t* inv, void* out,
                               int T, int topk, int d, int S, int rows, hipStream_t s);

@@ -30,7 +30,7 @@ __device__ __forceinline__ int mswz(int row, int chunk) { return row * 8 + (chun
 // 32-row x (128/WN)-col sub-tile = 2 x JN 16x16 MFMA tiles.
 // SPLIT: K is split over gridDim.z; each slice writes fp32 partials P[z, row, col] (ldy = N)
 // that moe_combine_split_kernel sums while combining (no extra launch).
-template <int BM, bool GATHER, bool SILU, int PF, bool SPLIT>
+template <int BM, bool GATHER, bool SILU, int PF, bool SPLIT, bool NTW = false>
 __global__ __launch_bounds__(256, 2) void moe_dgemm_kernel(const bf16* __restrict__ A,
                                                            const bf16* __restrict__ W,
                                                            bf16* __restrict__ Y,
@@ -78,7 +78,10 @@ __global__ __launch_bounds__(256, 2) void moe_dgemm_kernel(const bf16* __restric
 #pragma unroll
     for (int c = 0; c < AR; ++c) sa[q][c] = *reinterpret_cast<const bf16x8*>(xa[c] + kk);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) sb[q][c] = *reinterpret_cast<const bf16x8*>(wb[c] + kk);
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(wb[c] + kk);
+      sb[q][c] = NTW ? __builtin_nontemporal_load(src) : *src;
+    }
   };
   constexpr int BUF = (BM + MBN) * 8;
   auto sstore = [&](int q, int buf) {
@@ -218,42 +221,42 @@ void launch_moe_combine_split(const float* P, const float* wts, const int32_t* i
 }
 
 template <int BM, bool G, bool S, bool SPL>
-static void moe_dgemm_pf(dim3 grid, int pf, hipStream_t s, const bf16* A, const bf16* W, bf16* Y,
+static void moe_dgemm_pf(dim3 grid, int pf, bool ntw, hipStream_t s, const bf16* A, const bf16* W, bf16* Y,
                          float* P, const int32_t* sid, const int32_t* te, int n_flat, int topk,
                          int N, int K, int lda, int ldy, int rows) {
-#define MOE_L(PFV) moe_dgemm_kernel<BM, G, S, PFV, SPL><<<grid, 256, 0, s>>>( \
+#define MOE_L(PFV, NT) moe_dgemm_kernel<BM, G, S, PFV, SPL, NT><<<grid, 256, 0, s>>>( \
       A, W, Y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows)
   switch (pf) {
-    case 4: MOE_L(4); break;
-    case 2: MOE_L(2); break;
-    default: MOE_L(1);
+    case 4: if (ntw) MOE_L(4, true); else MOE_L(4, false); break;
+    case 2: if (ntw) MOE_L(2, true); else MOE_L(2, false); break;
+    default: MOE_L(1, false);
   }
 #undef MOE_L
 }
 
 template <int BM>
-static void moe_dgemm_bm(dim3 grid, int gather, int silu, int pf, hipStream_t s, const bf16* a,
+static void moe_dgemm_bm(dim3 grid, int gather, int silu, int pf, bool ntw, hipStream_t s, const bf16* a,
                          const bf16* w, bf16* y, float* P, const int32_t* sid, const int32_t* te,
                          int n_flat, int topk, int N, int K, int lda, int ldy, int rows) {
   const bool spl = grid.z > 1;
   if (gather && silu)
-    moe_dgemm_pf<BM, true, true, false>(grid, pf, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_pf<BM, true, true, false>(grid, pf, ntw, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
   else if (silu)
-    moe_dgemm_pf<BM, false, true, false>(grid, pf, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_pf<BM, false, true, false>(grid, pf, ntw, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
   else if (gather && spl)
-    moe_dgemm_pf<BM, true, false, true>(grid, pf, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_pf<BM, true, false, true>(grid, pf, ntw, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
   else if (gather)
-    moe_dgemm_pf<BM, true, false, false>(grid, pf, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_pf<BM, true, false, false>(grid, pf, ntw, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
   else if (spl)
-    moe_dgemm_pf<BM, false, false, true>(grid, pf, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_pf<BM, false, false, true>(grid, pf, ntw, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
   else
-    moe_dgemm_pf<BM, false, false, false>(grid, pf, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_pf<BM, false, false, false>(grid, pf, ntw, s, a, w, y, P, sid, te, n_flat, topk, N, K, lda, ldy, rows);
 }
 
 void launch_moe_dgemm(const void* A, const void* W, void* Y, const int32_t* sorted_ids,
                       const int32_t* tile_expert, int max_tiles, int n_flat, int topk, int N,
                       int K, int lda, int ldy, int gather, int silu, int pf, int bm, int splitk,
-                      float* partials, hipStream_t s) {
+                      float* partials, bool ntw, hipStream_t s) {
   if (max_tiles == 0) return;
   dim3 grid(max_tiles, (N + MBN - 1) / MBN, splitk);
   const bf16* a = (const bf16*)A;
@@ -261,9 +264,9 @@ void launch_moe_dgemm(const void* A, const void* W, void* Y, const int32_t* sort
   bf16* y = (bf16*)Y;
   const int rows = max_tiles * bm;
   if (bm == 64)
-    moe_dgemm_bm<64>(grid, gather, silu, pf, s, a, w, y, partials, sorted_ids, tile_expert, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_bm<64>(grid, gather, silu, pf, ntw, s, a, w, y, partials, sorted_ids, tile_expert, n_flat, topk, N, K, lda, ldy, rows);
   else
-    moe_dgemm_bm<32>(grid, gather, silu, pf, s, a, w, y, partials, sorted_ids, tile_expert, n_flat, topk, N, K, lda, ldy, rows);
+    moe_dgemm_bm<32>(grid, gather, silu, pf, ntw, s, a, w, y, partials, sorted_ids, tile_expert, n_flat, topk, N, K, lda, ldy, rows);
 }
 
 }  // namespace akap

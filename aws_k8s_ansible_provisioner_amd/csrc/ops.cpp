@@ -570,12 +570,22 @@ void moe_dgemm(Tensor out, Tensor a, Tensor w, Tensor sorted_ids, Tensor tile_ex
   }
   TORCH_CHECK(sorted_ids.numel() >= rows, "moe_dgemm: sorted_ids too short");
   if (!gather) TORCH_CHECK(a.size(0) >= rows, "moe_dgemm: a rows must cover all tiles");
+  // Non-temporal expert-weight loads when each expert's weights are streamed by one row tile
+  // (64-row tiles, <= 40 rows per expert on average): measured on MI355X, Mixtral T=128,
+  // w13 345 -> 319 us, w2 (split 4) 226 -> 215 us; with 32-row tiles an expert's second tile
+  // re-reads its weights and nt loses (bench/moe_gemm_micro.py, profiles/r2_moe_nt.log).
+  // AKAP_MOE_NT=0|1 overrides.
+  static const int nt_env = [] {
+    const char* e = std::getenv("AKAP_MOE_NT");
+    return e ? std::atoi(e) : -1;
+  }();
+  const bool ntw = nt_env >= 0 ? nt_env != 0 : (bm == 64 && n_flat <= 40 * w.size(0));
   const c10::DeviceGuard g(a.device());
   akap::launch_moe_dgemm(a.data_ptr(), w.data_ptr(), splitk > 1 ? nullptr : out.data_ptr(),
                          sorted_ids.data_ptr<int32_t>(), tile_expert.data_ptr<int32_t>(),
                          max_tiles, n_flat, topk, N, K, a.stride(0),
                          splitk > 1 ? N : out.stride(0), gather ? 1 : 0, silu ? 1 : 0, (int)pf,
-                         (int)bm, (int)splitk, splitk > 1 ? out.data_ptr<float>() : nullptr,
+                         (int)bm, (int)splitk, splitk > 1 ? out.data_ptr<float>() : nullptr, ntw,
                          cur_stream());
 }
 
