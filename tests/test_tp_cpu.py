@@ -102,6 +102,11 @@ fused = m._forward_fused_decode(ids, batch, ks, vs, PLAIN_PLAN).float()
 if ps.rank == 0:
     print("RESULT " + json.dumps({"err": (fused - base).abs().max().item(),
                                   "scale": base.abs().max().item()}), flush=True)
+# orderly teardown: a rank that exits while its peer still has gloo work queued can die in
+# std::terminate from the process group's threads
+import torch.distributed as dist
+dist.barrier()
+dist.destroy_process_group()
 """
 
 
