@@ -20,6 +20,8 @@
 // Epilogue: the wave tile goes through LDS (the ring is free by then) so the bf16 output is
 // written as whole 16-byte row segments instead of 2-byte fragment scatters -- at M = 256
 // the LM head writes 78 MB of logits.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -44,10 +46,11 @@ struct WCfg {
 
 __device__ __forceinline__ int wswz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
+template <int AUX = 0>
 __device__ __forceinline__ void wglds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
-                                   0);
+                                   AUX);
 }
 
 template <int N_>
@@ -55,7 +58,9 @@ __device__ __forceinline__ void wwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int WM>
+// NTW: the weight stream's DMAs carry the non-temporal policy (aux = 2): every weight byte is
+// read by exactly one workgroup, once
+template <int WM, bool NTW = false>
 __global__ __launch_bounds__(512, 2) void wgemm_kernel(WGemmArgs p) {
   using C = WCfg<WM>;
   // ONE __shared__ object (cdna_hip_programming.md "Projection GEMM at M = 256" item 4a)
@@ -91,7 +96,8 @@ __global__ __launch_bounds__(512, 2) void wgemm_kernel(WGemmArgs p) {
 #pragma unroll
     for (int i = 0; i < C::GA; ++i) wglds16(asrc[i] + k0, slot + (w * C::GA + i) * 64);
 #pragma unroll
-    for (int i = 0; i < C::GW; ++i) wglds16(wsrc[i] + k0, slot + C::BM * 8 + (w * C::GW + i) * 64);
+    for (int i = 0; i < C::GW; ++i)
+      wglds16<NTW ? 2 : 0>(wsrc[i] + k0, slot + C::BM * 8 + (w * C::GW + i) * 64);
   };
 
   f32x4 acc[4][C::JN];
@@ -171,10 +177,17 @@ void launch_wgemm(const WGemmArgs& p, hipStream_t st) {
   const int wmr = wgemm_rows(p.M);
   const int bm = 64 * wmr, bn = wmr == 4 ? 128 : 256;
   dim3 grid((p.N + bn - 1) / bn, (p.M + bm - 1) / bm);
+  // non-temporal weight DMAs by default (AKAP_WGEMM_NT=0 disables): measured on MI355X,
+  // Qwen3 LM head M=256 111.5 -> 108.2 us, Llama-3-8B LM head M=16/128 232/257 -> 205/226 us
+  // (profiles/r2_wgemm_nt.log)
+  static const bool nt = [] {
+    const char* e = std::getenv("AKAP_WGEMM_NT");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
   switch (wmr) {
-    case 1: wgemm_kernel<1><<<grid, 512, 0, st>>>(p); break;
-    case 2: wgemm_kernel<2><<<grid, 512, 0, st>>>(p); break;
-    default: wgemm_kernel<4><<<grid, 512, 0, st>>>(p); break;
+    case 1: if (nt) wgemm_kernel<1, true><<<grid, 512, 0, st>>>(p); else wgemm_kernel<1><<<grid, 512, 0, st>>>(p); break;
+    case 2: if (nt) wgemm_kernel<2, true><<<grid, 512, 0, st>>>(p); else wgemm_kernel<2><<<grid, 512, 0, st>>>(p); break;
+    default: if (nt) wgemm_kernel<4, true><<<grid, 512, 0, st>>>(p); else wgemm_kernel<4><<<grid, 512, 0, st>>>(p); break;
   }
 }
 
