@@ -12,6 +12,8 @@ from __future__ import annotations
 import os
 from typing import Optional
 
+import numpy as np
+
 
 class ByteTokenizer:
     OFFSET = 3
@@ -27,17 +29,15 @@ class ByteTokenizer:
         return ([self.bos_token_id] + ids) if add_bos else ids
 
     def decode(self, ids, skip_special: bool = True) -> str:
-        out = bytearray()
-        for i in ids:
-            i = int(i)
-            if i in (self.bos_token_id, self.eos_token_id, 0) and skip_special:
-                continue
-            b = i - self.OFFSET
-            if 0 <= b < 256:
-                out.append(b)
-            else:
-                out.append(33 + (i % 94))  # printable ASCII placeholder
-        return out.decode("utf-8", errors="replace")
+        # vectorised: a finishing decode batch detokenises 256 x 256 ids at once (a per-id
+        # Python loop took ~40 ms of host time per such step)
+        a = np.asarray(ids, dtype=np.int64).reshape(-1)
+        if skip_special:
+            a = a[(a != self.bos_token_id) & (a != self.eos_token_id) & (a != 0)]
+        b = a - self.OFFSET
+        # ids outside the byte range -> printable ASCII placeholder 33 + (id % 94)
+        out = np.where((b >= 0) & (b < 256), b, 33 + (a % 94)).astype(np.uint8)
+        return out.tobytes().decode("utf-8", errors="replace")
 
     def decode_token(self, i: int) -> str:
         return self.decode([i])

@@ -214,3 +214,22 @@ def test_chat_templates_render_any_conversation(msgs, name):
     for m in msgs:
         if m["role"] != "system" or name == "default":
             assert m["content"] in out
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.integers(0, 151935), max_size=300), st.booleans())
+def test_byte_tokenizer_decode_matches_reference_loop(ids, skip):
+    """The vectorised ByteTokenizer.decode equals the per-id definition: specials skipped,
+    bytes [3, 259) verbatim, anything else -> the printable placeholder 33 + id % 94."""
+    from aws_k8s_ansible_provisioner_amd.utils.tokenizer import ByteTokenizer
+
+    tk = ByteTokenizer(151936, 151643, 151645)
+    ids = ids + [151643, 151645, 0][: len(ids) % 4]
+    out = bytearray()
+    for i in ids:
+        if skip and i in (151643, 151645, 0):
+            continue
+        b = i - 3
+        out.append(b if 0 <= b < 256 else 33 + i % 94)
+    assert tk.decode(ids, skip_special=skip) == out.decode("utf-8", errors="replace")
+    assert tk.decode(np.asarray(ids), skip_special=skip) == tk.decode(ids, skip_special=skip)
