@@ -34,6 +34,7 @@ class EngineConfig:
     max_decode_stall_steps: int = 8           #     many steps' budget (burst: TTFT first),
     #                                           for at most this many steps in a row
     held_kv_ttl_s: float = 120.0              # P/D prefill: free un-pulled held KV after this
+    gc_freeze: bool = True                    # gc.freeze() the start-up heap (no full-GC stalls)
 
     def __post_init__(self) -> None:
         # the K cache stores each 32-token chunk in MFMA-fragment order (ops/reference.py)
