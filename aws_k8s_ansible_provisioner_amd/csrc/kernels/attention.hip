@@ -777,17 +777,29 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
       __syncthreads();
     }
   }
-  if (!valid) return;
+  // O^T accumulator of lane (r, h): row r's dims 32 dt + 8 j4 + 4 h + (0..3).  Each pair of
+  // 8-dim groups (j4 = 2 kp, 2 kp + 1) is exchanged between the lane halves with two
+  // v_permlane32_swap, after which lane r holds dims 16 kp + 0..7 and lane r + 32 dims
+  // 16 kp + 8..15 of the same row: one 16-B store per pair instead of two 8-B stores (the
+  // epilogue is store-issue bound: 18 us of 117 at 32 x 512, profiles/r2_pmc_prefill_v2.md)
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-  bf16* orow = p.out + ((size_t)(q0 + pos) * p.Hq + kvh * G + hig) * kD;
+  bf16* orow = p.out + ((size_t)(q0 + (valid ? pos : 0)) * p.Hq + kvh * G + hig) * kD;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-      bf16x4 o;
+    for (int kp = 0; kp < 2; ++kp) {
+      bf16x4 oa, ob;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = f2bf(oacc[dt][4 * j4 + i] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * j4 + 4 * h) = o;
+      for (int i = 0; i < 4; ++i) {
+        oa[i] = f2bf(oacc[dt][8 * kp + i] * inv);
+        ob[i] = f2bf(oacc[dt][8 * kp + 4 + i] * inv);
+      }
+      const u32x2 a = __builtin_bit_cast(u32x2, oa), b = __builtin_bit_cast(u32x2, ob);
+      const auto r0 = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
+      const u32x4 o = {r0[0], r1[0], r0[1], r1[1]};
+      // every lane takes part in the swaps; only rows of this chunk store
+      if (valid) *reinterpret_cast<u32x4*>(orow + 32 * dt + 16 * kp + 8 * h) = o;
     }
 }
 
