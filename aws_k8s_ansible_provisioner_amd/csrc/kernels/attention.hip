@@ -540,7 +540,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar registers
   const int r = lane & 31;
   const int h = lane >> 5;
-  const int seq = p.tile_seq[tile];
+  const int seq = __builtin_amdgcn_readfirstlane(p.tile_seq[tile]);  // scalar: bt is uniform
   const int q0 = p.q_start[seq];
   const int q_len = p.q_start[seq + 1] - q0;
   const int kv_len = p.seq_lens[seq];
@@ -631,11 +631,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     koff[i] = (((tt * 4 + (dc >> 2)) * 16 + r16) * 4 + (dc & 3)) * 8;
     voff[i] = (s & 511) * 8;
   }
-  auto stage_glds = [&](int t, int buf) {
+  // wave-uniform chunk -> its block id by a scalar load straight from the block table (no LDS
+  // copy of the table, no workgroup barrier before the first DMA); loaded one tile ahead of
+  // its DMA, so the load is retired by the next iteration's lgkmcnt wait
+  auto chunk_of = [&](int t) {
+    return __builtin_amdgcn_readfirstlane(min(t * 2 + ((w * PW) >> 3), last_chunk));
+  };
+  // through the constant address space: a uniform load from it is a scalar (s_load) read of
+  // the block table, which this kernel never writes
+  const __attribute__((address_space(4))) int* bt_c =
+      (const __attribute__((address_space(4))) int*)bt;
+  auto blk_of = [&](int t) { return bt_c[chunk_of(t) * 32 / BS]; };
+  auto stage_glds = [&](int t, int buf, int blk) {
     bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
     bf16* vl = kl + kFaKeys * kD;
-    const int chunk = min(t * 2 + ((w * PW) >> 3), last_chunk);
-    const int blk = __builtin_amdgcn_readfirstlane(bt_s[chunk]);
+    const int chunk = chunk_of(t);
     const size_t base =
         ((size_t)blk * p.Hkv + kvh) * BS * kD + (size_t)((chunk * 32) % BS) * kD;
     const bf16* kb = static_cast<const bf16*>(p.k_cache) + base;
@@ -653,11 +663,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
 
-  for (int c = tid; c <= last_chunk; c += NT) bt_s[c] = bt[c * 32 / BS];
-  __syncthreads();
+  int blk_next = 0;
   if constexpr (GL) {
-    stage_glds(0, 0);
+    stage_glds(0, 0, blk_of(0));
+    blk_next = blk_of(1);
   } else {
+    // register-staged form: per-piece block ids come from an LDS copy of the table
+    for (int c = tid; c <= last_chunk; c += NT) bt_s[c] = bt[c * 32 / BS];
+    __syncthreads();
     stage_load(0);
     stage_store(0);
     __syncthreads();
@@ -671,7 +684,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (more) stage_glds(t + 1, buf ^ 1);
+      if (more) {
+        stage_glds(t + 1, buf ^ 1, blk_next);
+        blk_next = blk_of(t + 2);
+      }
     } else {
       // timing experiments (wrong numerics): flags 256 = no K/V reloads, 512 = no compute
       if (more && !(p.flags & 256)) stage_load(t + 1);
