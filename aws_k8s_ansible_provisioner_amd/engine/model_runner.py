@@ -23,7 +23,7 @@ from ..utils import profiling
 from .. import ops
 from ..models.config import ModelConfig
 from ..models.transformer import AttnBatch, DecoderLM
-from ..parallel.state import ParallelState, get_state
+from ..parallel.state import ParallelState, drain_pending_collectives, get_state
 from .config import EngineConfig
 
 DEFAULT_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320,
@@ -341,6 +341,7 @@ class ModelRunner:
             with torch.cuda.stream(stream):
                 self._decode_body(b)  # warm-up (hipBLASLt heuristics, allocator)
             stream.synchronize()
+            drain_pending_collectives(self.ps)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
                 self._decode_body(b)

@@ -105,6 +105,29 @@ def set_state(st: ParallelState) -> None:
     _STATE = st
 
 
+def drain_pending_collectives(st: Optional[ParallelState] = None) -> None:
+    """Block until the RCCL watchdog has retired every outstanding work of our groups.
+
+    Call before a hipGraph capture that records collectives: the watchdog polls each pending
+    work's end event, and on ROCm querying an event whose stream has since joined a capture
+    fails with hipErrorCapturedEvent, which terminates the process from the watchdog thread.
+    The warm-up collectives issued just before capture are exactly such works."""
+    if not dist.is_initialized():
+        return
+    st = st or _STATE
+    seen = set()
+    for grp in (dist.group.WORLD, st.tp_group, st.dp_group):
+        if grp is None or id(grp) in seen:
+            continue
+        seen.add(id(grp))
+        try:
+            if dist.get_backend(grp) != "nccl":
+                continue
+            grp._wait_for_pending_works()
+        except (RuntimeError, NotImplementedError, AttributeError, ValueError):
+            pass
+
+
 def destroy() -> None:
     global _STATE
     if _STATE.car is not None:
