@@ -16,6 +16,44 @@ static T* ptr_of(py::dict& d, const char* k, size_t min_elems) {
   return a.mutable_data();
 }
 
+static BatchBuffers batch_buffers(const Scheduler& s, py::dict bufs) {
+  const auto& c = s.config();
+  BatchBuffers b{};
+  b.cap_tokens = bufs["input_ids"].cast<py::array>().size();
+  b.input_ids = ptr_of<int64_t>(bufs, "input_ids", b.cap_tokens);
+  b.positions = ptr_of<int64_t>(bufs, "positions", b.cap_tokens);
+  b.slots = ptr_of<int64_t>(bufs, "slots", b.cap_tokens);
+  b.seq_lens = ptr_of<int32_t>(bufs, "seq_lens", c.max_num_seqs);
+  b.q_start = ptr_of<int32_t>(bufs, "q_start", c.max_num_seqs + 1);
+  b.block_tables =
+      ptr_of<int32_t>(bufs, "block_tables", (size_t)c.max_num_seqs * c.max_blocks_per_seq);
+  b.cap_tiles = bufs["tile_seq"].cast<py::array>().size();
+  b.tile_seq = ptr_of<int32_t>(bufs, "tile_seq", b.cap_tiles);
+  b.tile_row = ptr_of<int32_t>(bufs, "tile_row", b.cap_tiles);
+  b.logits_idx = ptr_of<int64_t>(bufs, "logits_idx", c.max_num_seqs);
+  b.req_ids = ptr_of<int64_t>(bufs, "req_ids", c.max_num_seqs);
+  b.sample_mask = ptr_of<int32_t>(bufs, "sample_mask", c.max_num_seqs);
+  b.temperature = ptr_of<float>(bufs, "temperature", c.max_num_seqs);
+  b.top_p = ptr_of<float>(bufs, "top_p", c.max_num_seqs);
+  b.top_k = ptr_of<int32_t>(bufs, "top_k", c.max_num_seqs);
+  b.seeds = ptr_of<int64_t>(bufs, "seeds", c.max_num_seqs);
+  b.steps = ptr_of<int32_t>(bufs, "steps", c.max_num_seqs);
+  return b;
+}
+
+static py::dict step_info(const StepInfo& i) {
+  py::dict d;
+  d["is_prefill"] = i.is_prefill;
+  d["num_seqs"] = i.num_seqs;
+  d["num_tokens"] = i.num_tokens;
+  d["num_tiles"] = i.num_tiles;
+  d["num_samples"] = i.num_samples;
+  d["max_seq_len"] = i.max_seq_len;
+  d["num_preempted"] = i.num_preempted;
+  d["num_decode"] = i.num_decode;
+  return d;
+}
+
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "MI355X serving engine host runtime: paged KV block manager + batch scheduler";
 
@@ -74,42 +112,24 @@ PYBIND11_MODULE(_runtime, m) {
       .def("release", &Scheduler::release)
       .def("schedule",
            [](Scheduler& s, py::dict bufs) {
-             const auto& c = s.config();
-             BatchBuffers b{};
-             b.cap_tokens = bufs["input_ids"].cast<py::array>().size();
-             b.input_ids = ptr_of<int64_t>(bufs, "input_ids", b.cap_tokens);
-             b.positions = ptr_of<int64_t>(bufs, "positions", b.cap_tokens);
-             b.slots = ptr_of<int64_t>(bufs, "slots", b.cap_tokens);
-             b.seq_lens = ptr_of<int32_t>(bufs, "seq_lens", c.max_num_seqs);
-             b.q_start = ptr_of<int32_t>(bufs, "q_start", c.max_num_seqs + 1);
-             b.block_tables = ptr_of<int32_t>(bufs, "block_tables",
-                                              (size_t)c.max_num_seqs * c.max_blocks_per_seq);
-             b.cap_tiles = bufs["tile_seq"].cast<py::array>().size();
-             b.tile_seq = ptr_of<int32_t>(bufs, "tile_seq", b.cap_tiles);
-             b.tile_row = ptr_of<int32_t>(bufs, "tile_row", b.cap_tiles);
-             b.logits_idx = ptr_of<int64_t>(bufs, "logits_idx", c.max_num_seqs);
-             b.req_ids = ptr_of<int64_t>(bufs, "req_ids", c.max_num_seqs);
-             b.sample_mask = ptr_of<int32_t>(bufs, "sample_mask", c.max_num_seqs);
-             b.temperature = ptr_of<float>(bufs, "temperature", c.max_num_seqs);
-             b.top_p = ptr_of<float>(bufs, "top_p", c.max_num_seqs);
-             b.top_k = ptr_of<int32_t>(bufs, "top_k", c.max_num_seqs);
-             b.seeds = ptr_of<int64_t>(bufs, "seeds", c.max_num_seqs);
-             b.steps = ptr_of<int32_t>(bufs, "steps", c.max_num_seqs);
+             BatchBuffers b = batch_buffers(s, bufs);
              StepInfo i;
              {
                py::gil_scoped_release nogil;
                i = s.schedule(b);
              }
-             py::dict d;
-             d["is_prefill"] = i.is_prefill;
-             d["num_seqs"] = i.num_seqs;
-             d["num_tokens"] = i.num_tokens;
-             d["num_tiles"] = i.num_tiles;
-             d["num_samples"] = i.num_samples;
-             d["max_seq_len"] = i.max_seq_len;
-             d["num_preempted"] = i.num_preempted;
-             d["num_decode"] = i.num_decode;
-             return d;
+             return step_info(i);
+           })
+      .def("schedule_lookahead",
+           [](Scheduler& s, py::dict bufs) {
+             BatchBuffers b = batch_buffers(s, bufs);
+             int64_t* src = ptr_of<int64_t>(bufs, "src_rows", s.config().max_num_seqs);
+             StepInfo i;
+             {
+               py::gil_scoped_release nogil;
+               i = s.schedule_lookahead(b, src);
+             }
+             return step_info(i);
            })
       .def("update",
            [](Scheduler& s, py::array_t<int64_t, py::array::c_style> toks) {

@@ -141,9 +141,7 @@ bool Scheduler::abort_request(int64_t id) {
   } else {
     running_.erase(std::remove(running_.begin(), running_.end(), r), running_.end());
   }
-  last_sampled_.erase(std::remove(last_sampled_.begin(), last_sampled_.end(), r),
-                      last_sampled_.end());
-  finish(*r, FINISH_ABORT);
+  finish(*r, FINISH_ABORT);  // its rows in pending steps are skipped by update()
   return true;
 }
 
@@ -174,8 +172,9 @@ bool Scheduler::ensure_blocks(Request& r, int num_tokens) {
 
 void Scheduler::publish_full_blocks(Request& r) {
   const int bs = cfg_.block_size;
-  while ((int)r.hashes.size() < (int)r.blocks.size() &&
-         ((int)r.hashes.size() + 1) * bs <= r.num_computed) {
+  // a lookahead step counts the in-flight token as computed before it is in r.tokens
+  const int done = std::min(r.num_computed, (int)r.tokens.size());
+  while ((int)r.hashes.size() < (int)r.blocks.size() && ((int)r.hashes.size() + 1) * bs <= done) {
     const int i = (int)r.hashes.size();
     const uint64_t parent = i ? r.hashes[i - 1] : 0;
     const uint64_t h = BlockManager::hash_block(parent, r.tokens.data() + i * bs, bs);
@@ -283,7 +282,8 @@ void Scheduler::schedule_decodes(std::vector<std::pair<Request*, int>>& sched, S
 
 StepInfo Scheduler::schedule(BatchBuffers& buf) {
   StepInfo info;
-  last_sampled_.clear();
+  pending_.clear();  // a normal step is only scheduled with nothing in flight
+  std::vector<int64_t> sampled;
   if (!held_.empty()) expire_held(now_s());
   const int bs = cfg_.block_size;
   const int mb = cfg_.max_blocks_per_seq;
@@ -365,7 +365,7 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
       buf.seeds[ns] = r->seed;
       buf.steps[ns] = r->num_generated();
       buf.logits_idx[ns++] = T + q - 1;
-      last_sampled_.push_back(r);
+      sampled.push_back(r->id);
     }
     T += q;
   }
@@ -374,13 +374,85 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
   info.num_tokens = T;
   info.num_tiles = tiles;
   info.num_samples = ns;
+  pending_.push_back(std::move(sampled));
+  last_pure_decode_ = !info.is_prefill && info.num_seqs > 0;
+  return info;
+}
+
+StepInfo Scheduler::schedule_lookahead(BatchBuffers& buf, int64_t* src_rows) {
+  StepInfo info;
+  if (pending_.size() != 1 || !last_pure_decode_ || !waiting_.empty() ||
+      !sched_finished_.empty())
+    return info;
+  const std::vector<int64_t>& prev = pending_.back();
+  const int bs = cfg_.block_size;
+  const int mb = cfg_.max_blocks_per_seq;
+  std::vector<std::pair<Request*, int>> rows;  // (request, in-flight row)
+  int live = 0;
+  for (int i = 0; i < (int)prev.size(); ++i) {
+    auto it = reqs_.find(prev[i]);
+    if (it == reqs_.end() || it->second->status != RUNNING) continue;
+    Request* r = it->second.get();
+    ++live;
+    // the in-flight step appends one token: does that token end r by length?
+    const int gen_after = r->num_generated() + 1;
+    const int len_after = (int)r->tokens.size() + 1;
+    if (gen_after >= r->max_tokens || len_after >= cfg_.max_model_len) continue;
+    rows.emplace_back(r, i);
+  }
+  // every running sequence must be in the in-flight batch (an activated P/D request or a
+  // still-prefilling one needs a normal step)
+  if (live != (int)running_.size() || rows.empty() || (int)rows.size() > cfg_.max_num_seqs)
+    return info;
+  for (auto& e : rows)
+    if (!ensure_blocks(*e.first, e.first->num_computed + 1)) return info;
+  int ns = 0;
+  for (auto& e : rows) {
+    Request* r = e.first;
+    const int pos = r->num_computed;  // position of the in-flight step's token
+    buf.q_start[ns] = ns;
+    buf.input_ids[ns] = -1;  // gathered on the device from the in-flight step's samples
+    src_rows[ns] = e.second;
+    buf.positions[ns] = pos;
+    buf.slots[ns] = (int64_t)r->blocks[pos / bs] * bs + pos % bs;
+    buf.seq_lens[ns] = pos + 1;
+    info.max_seq_len = std::max(info.max_seq_len, pos + 1);
+    int32_t* row = buf.block_tables + (size_t)ns * mb;
+    const int nb = (int)r->blocks.size();
+    for (int b = 0; b < mb; ++b) row[b] = b < nb ? r->blocks[b] : 0;
+    buf.req_ids[ns] = r->id;
+    buf.sample_mask[ns] = 1;
+    buf.temperature[ns] = r->temperature;
+    buf.top_p[ns] = r->top_p;
+    buf.top_k[ns] = r->top_k;
+    buf.seeds[ns] = r->seed;
+    buf.steps[ns] = r->num_generated() + 1;
+    buf.logits_idx[ns] = ns;
+    r->num_computed = pos + 1;
+    ++ns;
+  }
+  buf.q_start[ns] = ns;
+  std::vector<int64_t> sampled;
+  sampled.reserve(ns);
+  for (auto& e : rows) sampled.push_back(e.first->id);
+  pending_.push_back(std::move(sampled));
+  info.num_seqs = info.num_tokens = info.num_samples = info.num_decode = ns;
   return info;
 }
 
 void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_ids,
                        std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish,
                        std::vector<int32_t>& out_first) {
-  if (n != (int)last_sampled_.size()) throw std::invalid_argument("sample count mismatch");
+  if (pending_.empty()) {
+    if (n) throw std::invalid_argument("update() without a scheduled step");
+  } else if (n != (int)pending_.front().size()) {
+    throw std::invalid_argument("sample count mismatch");
+  }
+  std::vector<int64_t> sampled;
+  if (!pending_.empty()) {
+    sampled = std::move(pending_.front());
+    pending_.pop_front();
+  }
   for (const auto& f : sched_finished_) {
     out_ids.push_back(f.first);
     out_tokens.push_back(-1);
@@ -390,7 +462,11 @@ void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_i
   sched_finished_.clear();
   for (Request* r : running_) publish_full_blocks(*r);
   for (int i = 0; i < n; ++i) {
-    Request* r = last_sampled_[i];
+    auto it = reqs_.find(sampled[i]);
+    // finished (EOS/stop in an earlier update, aborted) or released while this step was in
+    // flight: its row was computed and is discarded
+    if (it == reqs_.end() || it->second->status != RUNNING) continue;
+    Request* r = it->second.get();
     const int32_t tok = (int32_t)tokens[i];
     r->tokens.push_back(tok);
     int reason = NOT_FINISHED;
@@ -414,7 +490,6 @@ void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_i
       finish(*r, reason);
     }
   }
-  last_sampled_.clear();
 }
 
 }  // namespace akap_rt

@@ -113,6 +113,16 @@ class Scheduler {
                    float top_p = 1.f, int top_k = 0, int64_t seed = 0, bool stream = false);
   bool abort_request(int64_t id);
   StepInfo schedule(BatchBuffers& buf);
+  // Decode lookahead (async scheduling): called while the pure decode step just scheduled
+  // (or looked ahead) is still running on the GPU and BEFORE its update().  Builds the next
+  // decode step assuming every row of the in-flight step appends its (not yet known) token:
+  // input ids are not written -- src_rows[j] names the in-flight row whose sampled token is
+  // row j's input, and the device gathers it.  Rows whose pending token finishes them by
+  // length are left out; a row that turns out to finish by EOS/stop (or is aborted) computes
+  // one discarded token (its KV lands in its own, already freed blocks before any reuse:
+  // stream order).  Returns num_seqs = 0 when the next step must be a normal one (waiting
+  // requests, a running sequence outside the in-flight batch, no KV blocks, nothing left).
+  StepInfo schedule_lookahead(BatchBuffers& buf, int64_t* src_rows);
   // tokens[i] is the sample for the i-th sampled sequence of the last step.
   // Emits (id, token, finish_reason, is_first) events only for sequences that got their
   // first token, finished, or stream -- O(events) host work per step, not O(batch).
@@ -123,7 +133,8 @@ class Scheduler {
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   bool has_work() const {
-    return !waiting_.empty() || !running_.empty() || !sched_finished_.empty();
+    return !waiting_.empty() || !running_.empty() || !sched_finished_.empty() ||
+           !pending_.empty();
   }
   const BlockManager& blocks() const { return bm_; }
   BlockManager& blocks_mut() { return bm_; }
@@ -170,7 +181,11 @@ class Scheduler {
   std::unordered_map<int64_t, std::unique_ptr<Request>> reqs_;
   std::deque<Request*> waiting_;
   std::vector<Request*> running_;
-  std::vector<Request*> last_sampled_;  // order of samples in the last step
+  // ids of the sampled rows of every scheduled step whose update() is still due, oldest
+  // first (one entry normally; two while a lookahead step is in flight).  Ids, not pointers:
+  // a request may finish, be aborted or released while a step that holds it is in flight.
+  std::deque<std::vector<int64_t>> pending_;
+  bool last_pure_decode_ = false;  // the newest pending step is a pure decode step
   // requests the scheduler itself had to finish (KV pool can never hold them); reported by
   // the next update() as events with token -1
   std::vector<std::pair<int64_t, int>> sched_finished_;

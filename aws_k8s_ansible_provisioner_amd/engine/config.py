@@ -35,6 +35,10 @@ class EngineConfig:
     #                                           for at most this many steps in a row
     held_kv_ttl_s: float = 120.0              # P/D prefill: free un-pulled held KV after this
     gc_freeze: bool = True                    # gc.freeze() the start-up heap (no full-GC stalls)
+    # decode lookahead: queue decode step N+1 (inputs gathered on the GPU from step N's
+    # samples) before waiting for step N, so host bookkeeping and the graph launch overlap
+    # the GPU (single-rank engines with hipGraphs; AKAP_ASYNC_DECODE=0 disables)
+    async_decode: bool = True
 
     def __post_init__(self) -> None:
         # the K cache stores each 32-token chunk in MFMA-fragment order (ops/reference.py)

@@ -104,6 +104,11 @@ class LLMEngine:
         self.pd_group: Optional[str] = None  # P/D transfer-group id (stamped into kvp)
         self.kv_agent = None  # P/D: the KVTransferAgent (metrics only)
         self.rank = self.runner.ps.rank
+        self._inflight = None  # (info, handle) of a launched lookahead decode step
+        self.lookahead_steps = 0
+        self._async_decode = (ecfg.async_decode and self.runner.is_gpu and
+                              bool(self.runner.graphs) and self.runner.ps.world_size == 1 and
+                              os.environ.get("AKAP_ASYNC_DECODE", "1") != "0")
         if ecfg.gc_freeze and os.environ.get("AKAP_GC_FREEZE", "1") != "0":
             # Move everything alive after start-up (model, graphs, torch/extension objects)
             # into the permanent generation: the serving loop allocates ~10^5 small objects
@@ -239,28 +244,54 @@ class LLMEngine:
         return self.sched.num_running + self.sched.num_waiting
 
     # ------------------------------------------------------------------ step
+    def _try_lookahead(self):
+        """Launch the next decode step while the current one runs (see
+        Scheduler.schedule_lookahead); None when the next step must be a normal one."""
+        if not self._async_decode or self._n_extra or self._pending_aborts:
+            return None
+        with self._lock:
+            info = self.sched.schedule_lookahead(self.runner.host_buffers())
+        if not info["num_seqs"]:
+            return None
+        self.lookahead_steps += 1
+        return info, self.runner.launch_decode(info, chained=True)
+
     def step(self) -> list[RequestOutput]:
         t0 = time.time()
         if self._pending_aborts:
             self._apply_aborts()
-        with self._lock:
-            info = self.sched.schedule(self.runner.host_buffers())
-        if info["num_preempted"]:
-            self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
-        self.last_step_mixed = bool(info["is_prefill"] and info.get("num_decode", 0))
-        if info["is_prefill"]:  # requests are admitted only in steps with prefill rows
-            self._observe_queue_time(info, t0)
-        t1 = time.time()
         sample_pos: dict = {}
-        if info["num_seqs"] == 0:
-            # nothing runnable; still flush requests the scheduler had to end (token -1)
-            if not self.sched.has_work():
-                return []
-            toks = np.zeros(0, dtype=np.int64)
+        if self._inflight is not None:
+            # a lookahead step is already queued: queue the one after it, then collect it
+            info, handle = self._inflight
+            t1 = time.time()
+            self._inflight = self._try_lookahead()
+            toks = self.runner.wait_decode(handle)
+            self.last_step_mixed = False
         else:
-            if self._n_extra:
-                info["extras"], sample_pos = self._step_extras(info)
-            toks = self.runner.execute(info)
+            with self._lock:
+                info = self.sched.schedule(self.runner.host_buffers())
+            if info["num_preempted"]:
+                self.metrics.preempt.inc(info["num_preempted"], model_name=self.model_name)
+            self.last_step_mixed = bool(info["is_prefill"] and info.get("num_decode", 0))
+            if info["is_prefill"]:  # requests are admitted only in steps with prefill rows
+                self._observe_queue_time(info, t0)
+            t1 = time.time()
+            if info["num_seqs"] == 0:
+                # nothing runnable; still flush requests the scheduler had to end (token -1)
+                if not self.sched.has_work():
+                    return []
+                toks = np.zeros(0, dtype=np.int64)
+            else:
+                if self._n_extra:
+                    info["extras"], sample_pos = self._step_extras(info)
+                if (self._async_decode and not info["is_prefill"] and "extras" not in info
+                        and info["num_seqs"] <= self.runner.buckets[-1]):
+                    handle = self.runner.launch_decode(info)
+                    self._inflight = self._try_lookahead()
+                    toks = self.runner.wait_decode(handle)
+                else:
+                    toks = self.runner.execute(info)
         now = time.time()
         self.timers["schedule"] += t1 - t0
         self.timers["execute"] += now - t1

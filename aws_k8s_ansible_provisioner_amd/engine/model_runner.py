@@ -32,7 +32,7 @@ DEFAULT_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 2
 
 # per-step decode inputs (one row per sequence), staged together: see _stage_decode
 DECODE_FIELDS = ("input_ids", "positions", "slots", "seeds", "seq_lens", "temperature", "top_p",
-                 "top_k", "steps")
+                 "top_k", "steps", "src_rows")
 
 
 class ModelRunner:
@@ -125,6 +125,8 @@ class ModelRunner:
             "req_ids": (S, torch.int64), "sample_mask": (S, torch.int32),
             "temperature": (S, torch.float32), "top_p": (S, torch.float32),
             "top_k": (S, torch.int32), "seeds": (S, torch.int64), "steps": (S, torch.int32),
+            # decode lookahead: in-flight row whose sampled token is this row's input
+            "src_rows": (S, torch.int64),
         }
         self.h = {k: self._pinned(n, dt) for k, (n, dt) in spec.items()}
         self.np = {k: v.numpy() for k, v in self.h.items()}
@@ -140,15 +142,20 @@ class ModelRunner:
         for k, dt, n in fields:
             lay[k] = (off, dt, n)
             off += -(-n * torch.empty(0, dtype=dt).element_size() // 16) * 16
-        self.hdec = self._pinned(off, torch.uint8)
+        # two pinned staging regions used alternately: with a lookahead step in flight the
+        # host stages step N+2 while step N+1's copy may still be queued behind step N
+        self.hdecs = [self._pinned(off, torch.uint8) for _ in range(2)]
         self.ddec = torch.zeros(off, dtype=torch.uint8, device=self.device)
         view = lambda buf, o, dt, n: buf[o:o + n * torch.empty(0, dtype=dt).element_size()].view(dt)  # noqa: E731
-        self.hd = {k: view(self.hdec, o, dt, n) for k, (o, dt, n) in lay.items()}
-        self.hd_np = {k: v.numpy() for k, v in self.hd.items()}
+        self.hd_nps = [{k: view(h, o, dt, n).numpy() for k, (o, dt, n) in lay.items()}
+                       for h in self.hdecs]
+        self._dslot = 0
         self.dd = {k: view(self.ddec, o, dt, n) for k, (o, dt, n) in lay.items()}
         self.dd_bt = self.dd["block_tables"].view(S, mb)
         self._dec_bt_off = lay["block_tables"][0]
         self.out_tokens = torch.zeros(S, dtype=torch.int64, device=self.device)
+        # sampled tokens of launched decode steps land here (one region per staging slot)
+        self.tok_host = [self._pinned(S, torch.int64) for _ in range(2)]
         self.out_logprobs = torch.zeros(S, dtype=torch.float32, device=self.device)
         self.workspace = ops.decode_workspace(S, self.model.hkv, self.G, self.num_parts,
                                               self.device)
@@ -156,14 +163,19 @@ class ModelRunner:
     def host_buffers(self) -> dict:
         return self.np
 
-    def _stage_decode(self, n: int) -> None:
-        """Host buffers (rows [0, n)) -> decode staging region -> device, one copy."""
+    def _stage_decode(self, n: int) -> int:
+        """Host buffers (rows [0, n)) -> decode staging region -> device, one copy.  Returns
+        the staging slot used (alternating)."""
+        slot = self._dslot
+        self._dslot ^= 1
+        hd_np = self.hd_nps[slot]
         for k in DECODE_FIELDS:
-            self.hd_np[k][:n] = self.np[k][:n]
+            hd_np[k][:n] = self.np[k][:n]
         nb = n * self.max_blocks
-        self.hd_np["block_tables"][:nb] = self.np["block_tables"][:nb]
+        hd_np["block_tables"][:nb] = self.np["block_tables"][:nb]
         end = self._dec_bt_off + nb * 4
-        self.ddec[:end].copy_(self.hdec[:end], non_blocking=True)
+        self.ddec[:end].copy_(self.hdecs[slot][:end], non_blocking=True)
+        return slot
 
     def _h2d(self, key: str, n: int) -> torch.Tensor:
         dst = self.d[key][:n]
@@ -261,6 +273,7 @@ class ModelRunner:
         npd["top_k"][B:n] = 0
         npd["seeds"][B:n] = 0
         npd["steps"][B:n] = 0
+        npd["src_rows"][B:n] = 0
 
     def execute_decode(self, info: dict) -> torch.Tensor:
         B = info["num_seqs"]
@@ -281,6 +294,38 @@ class ModelRunner:
             # replaying their graphs issue identical collectives), eagerly
             self._decode_body(n, extras)
         return self.out_tokens[:B]
+
+    def launch_decode(self, info: dict, chained: bool = False):
+        """Queue a graph-replayed decode step without waiting for it.  chained: the step was
+        built by Scheduler.schedule_lookahead while the previous decode step is still
+        queued -- its input ids are gathered on the device from that step's sampled tokens
+        (out_tokens[src_rows]) before the replay.  Returns a handle for wait_decode()."""
+        B = info["num_seqs"]
+        n, graph = B, None
+        for b in self.buckets:
+            if b >= B:
+                n, graph = b, self.graphs[b]
+                break
+        if graph is None:
+            raise RuntimeError(f"no decode graph holds {B} rows")
+        self._pad_host(B, n)
+        with profiling.phase("akap.decode"):
+            slot = self._stage_decode(n)
+            if chained:
+                torch.index_select(self.out_tokens[:self.max_seqs], 0, self.dd["src_rows"][:n],
+                                   out=self.dd["input_ids"][:n])
+            graph.replay()
+        host = self.tok_host[slot][:B]
+        host.copy_(self.out_tokens[:B], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev, host
+
+    @staticmethod
+    def wait_decode(handle) -> np.ndarray:
+        ev, host = handle
+        ev.synchronize()
+        return host.numpy()
 
     def execute(self, info: dict) -> np.ndarray:
         if info["is_prefill"]:

@@ -173,3 +173,39 @@ def test_ep_decode_step_captures_in_a_hipgraph(monkeypatch):
             gc.collect()
             torch.cuda.synchronize()
             dist.destroy_process_group()
+
+
+def test_async_decode_lookahead_matches_synchronous(monkeypatch):
+    """Decode lookahead (step N+1 queued before step N's tokens reach the host, its input ids
+    gathered on the GPU) generates exactly what the synchronous loop generates: fixed
+    lengths, seeded sampling, and a stop token that ends a request while its next step is
+    already in flight (that row is computed and discarded)."""
+    prompts = [list(range(5, 60)), [7, 8] * 20, list(range(200, 230)), [100, 101, 102],
+               list(range(400, 470))]
+
+    def run(mode, stop_tok=None):
+        monkeypatch.setenv("AKAP_ASYNC_DECODE", mode)
+        eng = _engine("tiny-qwen3")
+        params = [SamplingParams(max_tokens=m, temperature=0, ignore_eos=True)
+                  for m in (3, 7, 12, 20)]
+        params.append(SamplingParams(max_tokens=16, temperature=0.8, top_p=0.9, seed=7,
+                                     ignore_eos=True))
+        names = [eng.add_request(None, None, p, prompt_ids=q) for q, p in zip(prompts, params)]
+        if stop_tok is not None:
+            names.append(eng.add_request(None, None, SamplingParams(
+                max_tokens=20, temperature=0, stop_token_ids=[stop_tok]), prompt_ids=prompts[3]))
+        final = {}
+        while eng.has_unfinished():
+            for o in eng.step():
+                if o.finished:
+                    final[o.req_id] = o
+        assert eng.sched.kv_usage() == 0.0
+        return [final[n].output_ids for n in names], eng.lookahead_steps
+
+    ref, n0 = run("0")
+    stop_tok = ref[3][5]
+    ref, _ = run("0", stop_tok)
+    got, n1 = run("1", stop_tok)
+    assert n0 == 0 and n1 > 10
+    assert got == ref
+    assert len(ref[5]) <= 6 and ref[5][-1] == stop_tok

@@ -240,3 +240,98 @@ def test_burst_backlog_stays_prefill_first_for_a_bounded_number_of_steps():
         run = run + 1 if k[1] == 0 else 0
         longest = max(longest, run)
     assert longest <= 3
+
+
+def _fake_model(b, info, req_of_row, prev=None):
+    """Deterministic stand-in for the GPU step: the token sampled for a row depends on its
+    input id, position and request; chained (lookahead) steps gather their input ids from
+    the previous step's samples through src_rows, as the runner does on the device."""
+    n, ns = info["num_tokens"], info["num_samples"]
+    ids = b["input_ids"][:n].copy()
+    if prev is not None:
+        ids = prev[b["src_rows"][:n]]
+    rows = b["logits_idx"][:ns]
+    pos = b["positions"][:n]
+    seq = b["req_ids"][:info["num_seqs"]]
+    req = np.repeat(seq, np.diff(b["q_start"][:info["num_seqs"] + 1]))
+    toks = (ids[rows] * 31 + pos[rows] * 7 + req[rows] * 5) % 97 + 3
+    toks[(ids[rows] + pos[rows]) % 11 == 0] = 2  # EOS now and then
+    for j in range(n):
+        req_of_row.setdefault(int(req[j]), {})[int(pos[j])] = int(ids[j])
+    return toks.astype(np.int64)
+
+
+def _drive(lookahead, prompts, max_tokens, ignore_eos):
+    s, b = _sched(num_blocks=256, max_seqs=4, budget=16, max_len=64)
+    b["src_rows"] = np.zeros(4, np.int64)
+    for i, p in enumerate(prompts):
+        s.add_request(i + 1, p, max_tokens[i], 0, ignore_eos[i], [], stream=True)
+    out = {i + 1: [] for i in range(len(prompts))}
+    fed, inflight, n_look = {}, None, 0
+    for _ in range(1000):
+        if not s.has_work():
+            break
+        if inflight is None:
+            info = s.schedule(b)
+            toks = _fake_model(b, info, fed)
+            if lookahead and not info["is_prefill"] and info["num_seqs"]:
+                i2 = s.schedule_lookahead(b)
+                if i2["num_seqs"]:
+                    inflight = _fake_model(b, i2, fed, prev=toks)
+                    n_look += 1
+        else:
+            toks = inflight
+            i2 = s.schedule_lookahead(b)
+            inflight = None
+            if i2["num_seqs"]:
+                inflight = _fake_model(b, i2, fed, prev=toks)
+                n_look += 1
+        ids, new, fin, _ = s.update(toks)
+        for rid, tok, f in zip(ids, new, fin):
+            if tok >= 0:
+                out[rid].append(tok)
+            if f:
+                s.release(rid)  # what the engine does after delivering the finish
+    assert not s.has_work()
+    assert s.kv_usage() == 0.0
+    return out, fed, n_look
+
+
+def test_decode_lookahead_matches_synchronous_scheduling():
+    """Async (lookahead) decode scheduling produces exactly the synchronous token streams:
+    rows finished by EOS while their next step was in flight are discarded, rows that the
+    in-flight token ends by length are left out, and every computed row fed the model the
+    right input id at the right position."""
+    rng = np.random.default_rng(0)
+    prompts = [list(rng.integers(3, 90, size=int(k))) for k in (5, 9, 3, 12, 7, 4)]
+    max_tokens = [6, 11, 1, 9, 14, 3]
+    ignore_eos = [True, False, True, False, False, True]
+    ref, _, n0 = _drive(False, prompts, max_tokens, ignore_eos)
+    got, fed, n1 = _drive(True, prompts, max_tokens, ignore_eos)
+    assert n0 == 0 and n1 > 5
+    assert got == ref
+    for rid, toks in got.items():
+        full = list(prompts[rid - 1]) + toks
+        for pos, tok in fed[rid].items():
+            if pos < len(full) - 1:  # rows past the end were computed and discarded
+                assert tok == full[pos], (rid, pos)
+
+
+def test_decode_lookahead_declines_when_work_waits():
+    s, b = _sched(num_blocks=64, max_seqs=4, budget=16, max_len=64)
+    b["src_rows"] = np.zeros(4, np.int64)
+    s.add_request(1, [5, 6, 7], 8, 0, True, [])
+    info = s.schedule(b)
+    assert info["is_prefill"]
+    assert s.schedule_lookahead(b)["num_seqs"] == 0  # never after a prefill step
+    s.update(np.array([9], np.int64))
+    info = s.schedule(b)
+    assert not info["is_prefill"]
+    s.add_request(2, [5, 6], 8, 0, True, [])  # a waiting request needs a normal step
+    assert s.schedule_lookahead(b)["num_seqs"] == 0
+    s.update(np.array([9], np.int64))
+    s.abort_request(2)
+    s.schedule(b)
+    la = s.schedule_lookahead(b)
+    assert la["num_seqs"] == 1 and b["src_rows"][0] == 0 and b["positions"][0] == 5
+    assert s.schedule_lookahead(b)["num_seqs"] == 0  # at most one step ahead
