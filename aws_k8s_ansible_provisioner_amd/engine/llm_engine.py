@@ -36,6 +36,7 @@ class RequestState:
     arrival: float
     output_ids: list = dataclasses.field(default_factory=list)
     logprobs: list = dataclasses.field(default_factory=list)
+    top_logprobs: list = dataclasses.field(default_factory=list)  # per token: [(id, lp)]
     first_token_time: Optional[float] = None
     last_token_time: Optional[float] = None
     finish_reason: Optional[str] = None
@@ -61,6 +62,7 @@ class RequestOutput:
     num_cached_tokens: int = 0
     kv_transfer_params: Optional[dict] = None
     logprobs: Optional[list] = None  # per output token (when the request asked for them)
+    top_logprobs: Optional[list] = None  # per output token: [(token id, log-prob)] x N
 
 
 class LLMEngine:
@@ -320,6 +322,12 @@ class LLMEngine:
             if tok >= 0 and st.params.logprobs is not None and iid in sample_pos:
                 lps = self.runner.last_logprobs
                 st.logprobs.append(float(lps[sample_pos[iid]]) if lps is not None else 0.0)
+                top = self.runner.last_top
+                if st.params.logprobs > 0 and top is not None:
+                    k_ = sample_pos[iid]
+                    st.top_logprobs.append([(int(t), float(v)) for t, v in
+                                            zip(top[0][k_][:st.params.logprobs],
+                                                top[1][k_][:st.params.logprobs])])
             if tok < 0:  # ended by the scheduler (KV pool can never hold it): no new token
                 delta = ""
             elif st.stream:
@@ -386,7 +394,8 @@ class LLMEngine:
                                       (st.first_token_time - st.arrival)
                                       if st.first_token_time else None, cached, kvp,
                                       list(st.logprobs) if st.params.logprobs is not None
-                                      else None))
+                                      else None,
+                                      list(st.top_logprobs) if st.params.logprobs else None))
         self.steps += 1
         self._update_gauges()
         self.timers["post"] += time.time() - now
@@ -412,7 +421,7 @@ class LLMEngine:
         pres = np.zeros(max(ns, 1), np.float32)
         freq = np.zeros(max(ns, 1), np.float32)
         rep = np.ones(max(ns, 1), np.float32)
-        want_lp = False
+        want_lp, ntop = False, 0
         pos: dict = {}
         k = 0
         for s_ in range(B):
@@ -424,6 +433,7 @@ class LLMEngine:
             if st is not None:
                 p = st.params
                 want_lp |= p.logprobs is not None
+                ntop = max(ntop, p.logprobs or 0)
                 if p.has_penalties:
                     pres[k], freq[k], rep[k] = (p.presence_penalty, p.frequency_penalty,
                                                 p.repetition_penalty)
@@ -438,7 +448,7 @@ class LLMEngine:
                         toks.append(t)
                         counts.append(c)
             k += 1
-        extras = {"logprobs": want_lp}
+        extras = {"logprobs": want_lp, "top_logprobs": ntop}
         if rows:
             extras["penalties"] = (np.asarray(rows, np.int32), np.asarray(toks, np.int32),
                                    np.asarray(counts, np.int32), pres, freq, rep)

@@ -86,6 +86,8 @@ class ModelRunner:
         self.num_parts = max(1, math.ceil(ecfg.max_model_len / 128))
         self._alloc_buffers()
         self.last_logprobs: Optional[np.ndarray] = None
+        # top-N alternatives of the last step's sampled rows: (token ids [n, N], log-probs)
+        self.last_top: Optional[tuple] = None
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.buckets: list[int] = []
@@ -200,6 +202,16 @@ class ModelRunner:
                     torch.from_numpy(freq).to(dev), torch.from_numpy(rep).to(dev))
             lp = bool(extras.get("logprobs"))
         d = self.d if src is None else src
+        ntop = int(extras.get("top_logprobs") or 0) if extras else 0
+        if ntop > 0:
+            # OpenAI top_logprobs: the N most likely tokens under the distribution the
+            # sampler draws from (post-penalty logits, temperature-scaled when T > 0; the
+            # same convention as the sampled token's log-prob)
+            t = d["temperature"][:n].float()
+            x = logits.float() / torch.where(t > 0, t, torch.ones_like(t))[:, None]
+            vals, idx = torch.topk(x, min(ntop, x.shape[-1]), dim=-1)
+            vals = vals - torch.logsumexp(x, dim=-1, keepdim=True)
+            self.last_top = (idx.cpu().numpy(), vals.cpu().numpy())
         return ops.sample(logits, d["temperature"][:n], d["top_k"][:n],
                           d["top_p"][:n], d["seeds"][:n], d["steps"][:n],
                           out_tokens=self.out_tokens[:n], out_logprobs=self.out_logprobs[:n],

@@ -57,8 +57,8 @@ def _sampling_from(body: dict, default_max: int = 16) -> SamplingParams:
 
 
 def _logprobs_of(body: dict) -> Optional[int]:
-    """completions: "logprobs": int; chat: "logprobs": bool (+ "top_logprobs": int).  Only
-    the sampled token's log-prob is produced (top-N alternatives are not computed)."""
+    """completions: "logprobs": int; chat: "logprobs": bool (+ "top_logprobs": int).  The
+    sampled token's log-prob plus, for N > 0, the N most likely alternatives per token."""
     lp = body.get("logprobs")
     if lp is None or lp is False:
         return None
@@ -67,23 +67,31 @@ def _logprobs_of(body: dict) -> Optional[int]:
     return int(lp)
 
 
-def _completion_logprobs(tokenizer, ids: list, lps: list, offset0: int = 0) -> dict:
+def _completion_logprobs(tokenizer, ids: list, lps: list, offset0: int = 0,
+                         top: Optional[list] = None) -> dict:
     toks = [tokenizer.decode_token(t) for t in ids]
     offs, o = [], offset0
     for t in toks:
         offs.append(o)
         o += len(t)
-    return {"tokens": toks, "token_logprobs": lps,
-            "top_logprobs": [{t: lp} for t, lp in zip(toks, lps)], "text_offset": offs}
+    if top:
+        tops = [{tokenizer.decode_token(a): v for a, v in alts} for alts in top]
+    else:
+        tops = [{t: lp} for t, lp in zip(toks, lps)]
+    return {"tokens": toks, "token_logprobs": lps, "top_logprobs": tops, "text_offset": offs}
 
 
-def _chat_logprobs(tokenizer, ids: list, lps: list) -> dict:
+def _chat_logprobs(tokenizer, ids: list, lps: list, top: Optional[list] = None) -> dict:
+    def entry(tid, lp):
+        s = tokenizer.decode_token(tid)
+        return {"token": s, "logprob": lp, "bytes": list(s.encode("utf-8"))}
+
     out = []
-    for t, lp in zip(ids, lps):
-        s = tokenizer.decode_token(t)
-        out.append({"token": s, "logprob": lp, "bytes": list(s.encode("utf-8")),
-                    "top_logprobs": [{"token": s, "logprob": lp,
-                                      "bytes": list(s.encode("utf-8"))}]})
+    for i, (t, lp) in enumerate(zip(ids, lps)):
+        e = entry(t, lp)
+        alts = top[i] if top and i < len(top) else [(t, lp)]
+        e["top_logprobs"] = [entry(a, v) for a, v in alts]
+        out.append(e)
     return {"content": out}
 
 
@@ -261,9 +269,8 @@ class OpenAIServer:
             created = int(time.time())
             tp = req.headers.get("traceparent")
             if body.get("stream"):
-                if len(prompts) != 1 or sp.n != 1:
-                    return _err(400, "streaming supports a single prompt with n=1")
-                return StreamingResponse(self._stream_completion(cid, created, prompts[0], sp,
+                # every (prompt, choice) streams as its own choice index i * n + j
+                return StreamingResponse(self._stream_completion(cid, created, prompts, sp,
                                                                  body, tp),
                                          media_type="text/event-stream")
             try:
@@ -289,7 +296,7 @@ class OpenAIServer:
                 lpd = None
                 if sp.logprobs is not None and o.logprobs is not None:
                     lpd = _completion_logprobs(self.ae.engine.tokenizer, o.output_ids,
-                                               o.logprobs)
+                                               o.logprobs, top=o.top_logprobs)
                 choices.append({"index": k, "text": text, "logprobs": lpd,
                                 "finish_reason": o.finish_reason, "stop_reason": None})
                 ctok += len(o.output_ids)
@@ -347,7 +354,8 @@ class OpenAIServer:
                 return _err(503, str(e), "ServiceUnavailable")
             tok = self.ae.engine.tokenizer
             choices = [{"index": j, "message": {"role": "assistant", "content": o.text},
-                        "logprobs": (_chat_logprobs(tok, o.output_ids, o.logprobs)
+                        "logprobs": (_chat_logprobs(tok, o.output_ids, o.logprobs,
+                                                    o.top_logprobs)
                                      if sp.logprobs is not None and o.logprobs is not None
                                      else None),
                         "finish_reason": o.finish_reason}
@@ -364,53 +372,93 @@ class OpenAIServer:
         return app
 
     # ------------------------------------------------------------------ SSE
-    async def _stream_completion(self, cid, created, prompt, sp, body, tp=None):
-        pid = prompt if isinstance(prompt, list) else None
-        ptext = prompt if isinstance(prompt, str) else None
-        n_out, n_prompt = 0, 0
+    @staticmethod
+    async def _merged(gens):
+        """Interleave several engine streams as (choice index, output) in arrival order."""
+        if len(gens) == 1:  # the common single-choice stream: no task/queue hop
+            async for o in gens[0]:
+                yield 0, o
+            return
+        q: asyncio.Queue = asyncio.Queue()
+
+        async def pump(k, g):
+            try:
+                async for o in g:
+                    await q.put((k, o))
+            except Exception as e:  # noqa: BLE001 -- re-raised in the consumer
+                await q.put((k, e))
+            await q.put((k, None))
+
+        tasks = [asyncio.create_task(pump(k, g)) for k, g in enumerate(gens)]
+        live = len(tasks)
         try:
-            async for o in self.ae.generate(ptext, sp, cid, prompt_ids=pid, stream=True,
-                                            kv_transfer_params=body.get("kv_transfer_params"),
-                                            traceparent=tp):
-                n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
+            while live:
+                k, o = await q.get()
+                if o is None:
+                    live -= 1
+                elif isinstance(o, Exception):
+                    raise o
+                else:
+                    yield k, o
+        finally:
+            for t in tasks:
+                t.cancel()
+
+    async def _stream_completion(self, cid, created, prompts, sp, body, tp=None):
+        gens = []
+        for i, p in enumerate(prompts):
+            for j in range(sp.n):
+                gens.append(self.ae.generate(
+                    p if isinstance(p, str) else None, sp,
+                    cid if len(prompts) * sp.n == 1 else f"{cid}-{i}-{j}",
+                    prompt_ids=p if isinstance(p, list) else None, stream=True,
+                    kv_transfer_params=body.get("kv_transfer_params"), traceparent=tp))
+        n_out, n_prompt = {}, {}
+        try:
+            async for k, o in self._merged(gens):
+                n_out[k], n_prompt[k] = len(o.output_ids), len(o.prompt_ids)
                 chunk = {"id": cid, "object": "text_completion", "created": created,
                          "model": self.name, "choices": [{
-                             "index": 0, "text": o.delta_text, "logprobs": None,
+                             "index": k, "text": o.delta_text, "logprobs": None,
                              "finish_reason": o.finish_reason if o.finished else None}]}
                 yield f"data: {json.dumps(chunk)}\n\n"
         except Exception as e:  # surface errors in-band, as vLLM does
             yield f"data: {json.dumps({'error': {'message': str(e)[:300]}})}\n\n"
         if (body.get("stream_options") or {}).get("include_usage"):
+            pt = sum(v for k, v in n_prompt.items() if k % sp.n == 0)
+            ct = sum(n_out.values())
             u = {"id": cid, "object": "text_completion", "created": created, "model": self.name,
-                 "choices": [], "usage": {"prompt_tokens": n_prompt, "completion_tokens": n_out,
-                                          "total_tokens": n_prompt + n_out}}
+                 "choices": [], "usage": {"prompt_tokens": pt, "completion_tokens": ct,
+                                          "total_tokens": pt + ct}}
             yield f"data: {json.dumps(u)}\n\n"
         yield "data: [DONE]\n\n"
 
     async def _stream_chat(self, cid, created, prompt, sp, body, tp=None):
-        first = {"id": cid, "object": "chat.completion.chunk", "created": created,
-                 "model": self.name, "choices": [{"index": 0, "delta": {"role": "assistant",
-                                                                        "content": ""},
-                                                  "finish_reason": None}]}
-        yield f"data: {json.dumps(first)}\n\n"
-        n_out, n_prompt = 0, 0
+        for j in range(sp.n):
+            first = {"id": cid, "object": "chat.completion.chunk", "created": created,
+                     "model": self.name, "choices": [{"index": j, "delta": {
+                         "role": "assistant", "content": ""}, "finish_reason": None}]}
+            yield f"data: {json.dumps(first)}\n\n"
+        gens = [self.ae.generate(prompt, sp, cid if sp.n == 1 else f"{cid}-{j}", stream=True,
+                                 kv_transfer_params=body.get("kv_transfer_params"),
+                                 traceparent=tp) for j in range(sp.n)]
+        n_out, n_prompt = {}, 0
         try:
-            async for o in self.ae.generate(prompt, sp, cid, stream=True,
-                                            kv_transfer_params=body.get("kv_transfer_params"),
-                                            traceparent=tp):
-                n_out, n_prompt = len(o.output_ids), len(o.prompt_ids)
+            async for k, o in self._merged(gens):
+                n_out[k], n_prompt = len(o.output_ids), len(o.prompt_ids)
                 chunk = {"id": cid, "object": "chat.completion.chunk", "created": created,
                          "model": self.name, "choices": [{
-                             "index": 0, "delta": {"content": o.delta_text} if o.delta_text else {},
+                             "index": k, "delta": {"content": o.delta_text} if o.delta_text else {},
                              "finish_reason": o.finish_reason if o.finished else None}]}
                 yield f"data: {json.dumps(chunk)}\n\n"
         except Exception as e:
             yield f"data: {json.dumps({'error': {'message': str(e)[:300]}})}\n\n"
         if (body.get("stream_options") or {}).get("include_usage"):
+            ct = sum(n_out.values())
             u = {"id": cid, "object": "chat.completion.chunk", "created": created,
                  "model": self.name, "choices": [],
-                 "usage": {"prompt_tokens": n_prompt, "completion_tokens": n_out,
-                           "total_tokens": n_prompt + n_out}}
+                 "usage": {"prompt_tokens": n_prompt, "completion_tokens": ct,
+                           "total_tokens": n_prompt + ct}}
             yield f"data: {json.dumps(u)}\n\n"
         yield "data: [DONE]\n\n"
 

@@ -104,6 +104,25 @@ def test_logprobs_match_dense_reference():
         assert abs(lp - ref) < 0.05, (i, lp, ref)
 
 
+def test_top_logprobs_alternatives_match_dense_reference():
+    """logprobs=N: the N most likely tokens per step with their log-probs, equal to the dense
+    reference's top-N (greedy: the sampled token is the first alternative)."""
+    eng = _engine("tiny-qwen3")
+    prompt = list(range(40, 61))
+    out = eng.generate(None, SamplingParams(max_tokens=5, temperature=0, ignore_eos=True,
+                                            logprobs=4), prompt_ids=[prompt])[0]
+    assert out.top_logprobs is not None and len(out.top_logprobs) == 5
+    logits = dense_logits(eng.runner.model, prompt + out.output_ids).float()
+    for i, alts in enumerate(out.top_logprobs):
+        # (bf16 logits of a tiny model tie now and then: compare values, not the order)
+        assert len(alts) == 4 and out.output_ids[i] in [a for a, _ in alts]
+        assert abs(alts[0][1] - out.logprobs[i]) < 1e-3
+        ref = torch.log_softmax(logits[len(prompt) - 1 + i], -1)
+        rv = torch.topk(ref, 4).values.tolist()
+        assert max(abs(v - r) for (_, v), r in zip(alts, rv)) < 0.1  # bf16 engine vs fp32
+        assert max(abs(ref[a].item() - v) for a, v in alts) < 0.1
+
+
 def test_frequency_penalty_prevents_repeats():
     eng = _engine("tiny-llama")
     prompts = [[5, 6, 7] * 6, [9] * 20]

@@ -62,6 +62,37 @@ def test_streaming_completion_sse(client):
     assert fins[-1] == "length" and fins.count("length") == 1
 
 
+def test_streaming_multiple_prompts_and_n(client):
+    """stream with two prompts x n=2: four choice indices interleave in one SSE stream, each
+    ends once, their texts equal the non-streaming response, usage sums every choice."""
+    body = {"prompt": [[5, 6, 7], [8, 9]], "max_tokens": 4, "temperature": 0, "n": 2,
+            "ignore_eos": True}
+    ref = client.post("/v1/completions", json=body).json()["choices"]
+    with client.stream("POST", "/v1/completions",
+                       json=dict(body, stream=True,
+                                 stream_options={"include_usage": True})) as r:
+        lines = [l for l in r.iter_lines() if l.startswith("data: ")]
+    assert lines[-1] == "data: [DONE]"
+    chunks = [json.loads(l[6:]) for l in lines[:-1]]
+    text, fins = {}, {}
+    for c in chunks:
+        for ch in c["choices"]:
+            text[ch["index"]] = text.get(ch["index"], "") + ch["text"]
+            if ch["finish_reason"]:
+                fins[ch["index"]] = fins.get(ch["index"], 0) + 1
+    assert sorted(text) == [0, 1, 2, 3] and fins == {0: 1, 1: 1, 2: 1, 3: 1}
+    assert [text[k] for k in range(4)] == [c["text"] for c in ref]
+    assert chunks[-1]["usage"]["completion_tokens"] == 16
+    assert chunks[-1]["usage"]["prompt_tokens"] == 5
+    msgs = [{"role": "user", "content": "hi"}]
+    with client.stream("POST", "/v1/chat/completions",
+                       json={"messages": msgs, "max_tokens": 3, "stream": True, "n": 3,
+                             "temperature": 0, "ignore_eos": True}) as r:
+        lines = [l for l in r.iter_lines() if l.startswith("data: ")]
+    idx = {ch["index"] for l in lines[:-1] for ch in json.loads(l[6:])["choices"]}
+    assert idx == {0, 1, 2}
+
+
 def test_chat_completion_and_stream(client):
     msgs = [{"role": "system", "content": "be brief"}, {"role": "user", "content": "hi"}]
     r = client.post("/v1/chat/completions", json={"model": MODEL, "messages": msgs,
@@ -120,6 +151,19 @@ def test_logprobs_and_penalties_in_api(client):
     assert r.status_code == 200, r.text
     content = r.json()["choices"][0]["logprobs"]["content"]
     assert len(content) == 4 and all("logprob" in c for c in content)
+    # top-N alternatives (completions: logprobs=N, chat: top_logprobs=N)
+    r = client.post("/v1/completions", json={"model": MODEL, "prompt": "hello there",
+                                             "max_tokens": 3, "logprobs": 3, "ignore_eos": True,
+                                             "temperature": 0})
+    tops = r.json()["choices"][0]["logprobs"]["top_logprobs"]
+    assert len(tops) == 3 and all(1 <= len(t) <= 3 for t in tops)
+    r = client.post("/v1/chat/completions", json={
+        "messages": [{"role": "user", "content": "hi"}], "max_tokens": 2, "logprobs": True,
+        "top_logprobs": 5, "ignore_eos": True, "temperature": 0})
+    content = r.json()["choices"][0]["logprobs"]["content"]
+    assert all(len(c["top_logprobs"]) == 5 for c in content)
+    assert all(c["top_logprobs"][0]["logprob"] >= c["top_logprobs"][-1]["logprob"]
+               for c in content)
 
 
 def test_prefix_cache_and_queue_time_metrics_are_live():
