@@ -352,6 +352,14 @@ class ModelRunner:
         return toks.to("cpu").numpy()
 
     # ------------------------------------------------------------------ graphs
+    def _graph_has_collectives(self) -> bool:
+        """TP ranks and expert-parallel MoE layers issue RCCL calls inside the decode graph
+        (DP replicas and single-GPU engines do not)."""
+        if self.ps.world_size > 1:
+            return True
+        return any(getattr(getattr(layer, "moe", None), "mode", None) == "ep"
+                   for layer in getattr(self.model, "layers", []))
+
     def capture_graphs(self) -> None:
         maxbs = min(self.ecfg.cuda_graph_max_bs or self.max_seqs, self.max_seqs)
         self.buckets = [b for b in DEFAULT_BUCKETS if b <= maxbs]
@@ -398,7 +406,8 @@ class ModelRunner:
             with torch.cuda.stream(stream):
                 self._decode_body(b)  # warm-up (hipBLASLt heuristics, allocator)
             stream.synchronize()
-            drain_pending_collectives(self.ps)
+            if self._graph_has_collectives():
+                drain_pending_collectives(self.ps)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
                 self._decode_body(b)
