@@ -261,7 +261,19 @@ class ModelRunner:
         parts = math.ceil(max_len / ps)
         return parts, ps
 
+    @property
+    def _tp_bcast_inputs(self) -> bool:
+        """TP: rank 0's staged decode inputs reach the other ranks by one RCCL broadcast of
+        the staging region at the start of the decode step (captured in the graph), so a
+        decode step costs the host control channel only the small step header."""
+        return self.ps.tp_size > 1 and self.ps.tp_group is not None
+
     def _decode_body(self, n: int, extras: Optional[dict] = None) -> None:
+        if self._tp_bcast_inputs:
+            import torch.distributed as dist
+
+            dist.broadcast(self.ddec, src=self.ps.rank - self.ps.tp_rank,
+                           group=self.ps.tp_group)
         parts, ps = self.decode_partitions(n)
         dd = self.dd
         batch = AttnBatch(False, dd["positions"][:n], dd["slots"][:n], self.dd_bt[:n],
@@ -296,8 +308,9 @@ class ModelRunner:
                 if b >= B:
                     n, graph = b, self.graphs[b]
                     break
-        self._pad_host(B, n)
-        self._stage_decode(n)
+        if not (self._tp_bcast_inputs and self.ps.tp_rank != 0):
+            self._pad_host(B, n)
+            self._stage_decode(n)  # (other TP ranks receive it by the in-graph broadcast)
         extras = info.get("extras")
         if graph is not None and not extras:
             graph.replay()

@@ -2,8 +2,11 @@
 
 Rank 0 of the group owns the C++ scheduler, the HTTP server and the request state; every
 rank owns its weight shard, its KV-cache shard (its kv heads) and its hipGraphs.  Each
-engine step, rank 0 broadcasts the step description (the used prefix of the pinned batch
-buffers, ~KBs) over a gloo control group; all ranks then run the identical step.  The
+engine step, rank 0 broadcasts the step header (StepInfo, 9 int64) over a gloo control
+group -- ONE host broadcast per decode step: the decode inputs themselves travel as one
+RCCL broadcast of rank 0's device staging region at the head of the decode step (inside the
+hipGraph, ModelRunner._decode_body).  Prefill steps also send the used prefix of the pinned
+batch buffers (~KBs) as a second gloo broadcast, sized by the header.  The
 forward's all-reduces (O-proj, down-proj) and the vocab-parallel logits all-gather run on
 RCCL over xGMI (and are captured inside the decode hipGraphs).  Every rank sees the full
 logits and runs the same seeded sampler, so all ranks produce identical tokens without
@@ -28,6 +31,7 @@ _STEP_KEYS = ["input_ids", "positions", "slots", "seq_lens", "q_start", "block_t
               "steps"]
 _INFO_KEYS = ["is_prefill", "num_seqs", "num_tokens", "num_tiles", "num_samples",
               "max_seq_len", "num_preempted", "num_decode"]
+# header = info + payload bytes (0 for decode steps: inputs go by the in-graph broadcast)
 STOP = -1
 
 
@@ -57,21 +61,20 @@ class TPStepBroadcaster:
 
     def execute(self, info: dict) -> np.ndarray:
         r = self.runner
-        if not info["is_prefill"]:
-            r._pad_host(info["num_seqs"], _extent("input_ids", info, r))
-        head = torch.tensor([info[k] for k in _INFO_KEYS], dtype=torch.int64)
+        payload = None
+        if info["is_prefill"]:
+            parts = [torch.from_numpy(r.np[k][:_extent(k, info, r)].view(np.uint8).copy())
+                     for k in _STEP_KEYS]
+            payload = torch.cat(parts)
+        head = torch.tensor([info[k] for k in _INFO_KEYS] +
+                            [0 if payload is None else payload.numel()], dtype=torch.int64)
         dist.broadcast(head, 0, group=self.ctrl)
-        parts = []
-        for k in _STEP_KEYS:
-            n = _extent(k, info, r)
-            parts.append(torch.from_numpy(r.np[k][:n].view(np.uint8).copy()))
-        payload = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8)
-        dist.broadcast(torch.tensor([payload.numel()], dtype=torch.int64), 0, group=self.ctrl)
-        dist.broadcast(payload, 0, group=self.ctrl)
+        if payload is not None:
+            dist.broadcast(payload, 0, group=self.ctrl)
         return r.execute(info)
 
     def shutdown(self) -> None:
-        head = torch.full((len(_INFO_KEYS),), STOP, dtype=torch.int64)
+        head = torch.full((len(_INFO_KEYS) + 1,), STOP, dtype=torch.int64)
         dist.broadcast(head, 0, group=self.ctrl)
         dist.barrier(group=self.ctrl)
         dist.destroy_process_group()
@@ -80,22 +83,22 @@ class TPStepBroadcaster:
 def worker_loop(runner: ModelRunner, ctrl_group) -> None:
     """Ranks != 0: mirror every step rank 0 broadcasts until STOP."""
     while True:
-        head = torch.zeros(len(_INFO_KEYS), dtype=torch.int64)
+        head = torch.zeros(len(_INFO_KEYS) + 1, dtype=torch.int64)
         dist.broadcast(head, 0, group=ctrl_group)
         if int(head[0]) == STOP:
             return
-        info = {k: int(v) for k, v in zip(_INFO_KEYS, head.tolist())}
-        n = torch.zeros(1, dtype=torch.int64)
-        dist.broadcast(n, 0, group=ctrl_group)
-        payload = torch.empty(int(n), dtype=torch.uint8)
-        dist.broadcast(payload, 0, group=ctrl_group)
-        off = 0
-        for k in _STEP_KEYS:
-            cnt = _extent(k, info, runner)
-            arr = runner.np[k]
-            nbytes = cnt * arr.itemsize
-            arr[:cnt] = payload[off:off + nbytes].numpy().view(arr.dtype)
-            off += nbytes
+        vals = head.tolist()
+        info = {k: int(v) for k, v in zip(_INFO_KEYS, vals)}
+        if vals[-1]:
+            payload = torch.empty(int(vals[-1]), dtype=torch.uint8)
+            dist.broadcast(payload, 0, group=ctrl_group)
+            off = 0
+            for k in _STEP_KEYS:
+                cnt = _extent(k, info, runner)
+                arr = runner.np[k]
+                nbytes = cnt * arr.itemsize
+                arr[:cnt] = payload[off:off + nbytes].numpy().view(arr.dtype)
+                off += nbytes
         runner.execute(info)
 
 

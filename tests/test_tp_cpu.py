@@ -126,3 +126,34 @@ def test_tp2_fused_decode_chain_matches_unfused(model):
     assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
     res = json.loads([l for l in outs[0][0].splitlines() if l.startswith("RESULT ")][0][7:])
     assert res["err"] <= 3e-2 * res["scale"] + 3e-2, res
+
+
+def test_tp_decode_step_is_one_host_broadcast(monkeypatch):
+    """Rank 0 sends a decode step to the other TP ranks with ONE gloo broadcast (the header);
+    the inputs go by the in-graph RCCL broadcast of the staging region.  Prefill steps add
+    one payload broadcast sized by the header."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from aws_k8s_ansible_provisioner_amd.parallel import tp_worker
+
+    sent = []
+    monkeypatch.setattr(dist, "broadcast", lambda t, src, group=None: sent.append(t.clone()))
+
+    class FakeRunner:
+        buckets = [1, 2, 4]
+        max_blocks = 2
+        np = {k: np.zeros(64, np.int64) for k in tp_worker._STEP_KEYS}
+
+        def execute(self, info):
+            return "ran"
+
+    bc = tp_worker.TPStepBroadcaster(FakeRunner(), ctrl_group=None)
+    dec = {"is_prefill": 0, "num_seqs": 3, "num_tokens": 3, "num_tiles": 0,
+           "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3}
+    assert bc.execute(dec) == "ran"
+    assert len(sent) == 1 and sent[0].tolist()[-1] == 0
+    sent.clear()
+    pre = dict(dec, is_prefill=1, num_tokens=20, num_tiles=2, num_decode=0)
+    bc.execute(pre)
+    assert len(sent) == 2 and sent[0].tolist()[-1] == sent[1].numel() > 0
