@@ -22,6 +22,8 @@ def dense_logits(model, ids: list[int]) -> torch.Tensor:
     D, hq, hkv = model.D, model.hq, model.hkv
     G = hq // hkv
     cs = model.cos_sin
+    if T > cs.shape[0]:
+        raise ValueError(f"{T} tokens exceed the model's rotary table ({cs.shape[0]} positions)")
     mask = torch.triu(torch.ones(T, T, dtype=torch.bool, device=dev), 1)
 
     def norm(v, w):

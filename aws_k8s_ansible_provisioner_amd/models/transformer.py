@@ -97,6 +97,10 @@ class DecoderLM:
         self.vocab_start = r * self.vocab_per
         self.vocab_end = min(cfg.vocab_size, self.vocab_start + self.vocab_per)
         self.scale = 1.0 / math.sqrt(self.D)
+        if max_model_len > cfg.max_position:
+            # the rotary table (and the kernels that index it by position) end there
+            raise ValueError(f"max_model_len {max_model_len} exceeds {cfg.name}'s "
+                             f"max_position_embeddings {cfg.max_position}")
         self._init_weights(seed, full_then_shard)
         self.cos_sin = ref.rope_cos_sin(min(cfg.max_position, max(max_model_len, 16)), self.D,
                                         cfg.rope_theta, cfg.rope_scaling, device=self.device)

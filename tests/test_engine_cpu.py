@@ -176,3 +176,10 @@ def test_mixed_batching_matches_prefill_first(model):
         assert saw_mixed == mixed
         outs[mixed] = got
     assert outs[True] == outs[False]
+
+
+def test_max_model_len_beyond_the_rotary_table_is_rejected():
+    """The engine refuses a context longer than the model's max_position_embeddings (the
+    rotary table, which the kernels index by position, ends there)."""
+    with pytest.raises(ValueError, match="max_position_embeddings"):
+        _engine("tiny-qwen3", max_model_len=8192)

@@ -209,3 +209,18 @@ def test_async_decode_lookahead_matches_synchronous(monkeypatch):
     assert n0 == 0 and n1 > 10
     assert got == ref
     assert len(ref[5]) <= 6 and ref[5][-1] == stop_tok
+
+
+def test_long_prompt_chunked_prefill_and_split_kv_decode():
+    """Qwen3-0.6B shapes, an 8k-token prompt in 1k-token prefill chunks (each chunk's causal window reaches back
+    over the cached prefix), then decode with the adaptive split-KV plan (one sequence: many
+    partitions + combine), teacher-forced against the dense reference."""
+    eng = _engine("qwen3-0.6b", max_model_len=16384, max_num_seqs=4, cuda_graph_max_bs=4,
+                  max_num_batched_tokens=1024, num_gpu_blocks=600, init_std=0.05)
+    assert eng.runner.decode_partitions(1)[0] > 1
+    prompt = [int(x) for x in torch.randint(5, 1000, (8000,),
+                                            generator=torch.Generator().manual_seed(0))]
+    out = eng.generate(None, SamplingParams(max_tokens=6, temperature=0, ignore_eos=True),
+                       prompt_ids=[prompt])[0]
+    assert len(out.output_ids) == 6
+    _check_teacher_forced(eng, prompt, out.output_ids, tol=0.25)

@@ -776,3 +776,38 @@ def test_kgemm_in_workgroup_splitk(km, epi, M, N, K):
         _close(res, want, atol=2e-2 * want.abs().max().item())
         _close(a, res.float() * ln.float(), atol=1e-2 * a.float().abs().max().item())
         assert torch.allclose(ss, res.float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("num_parts,part_size", [(1, 32768), (32, 1024), (128, 256)])
+def test_paged_attention_decode_long_context(num_parts, part_size):
+    """Long-context decode (up to 32k cached tokens per sequence, Llama-3-70B's 64/8 heads
+    per rank shape): unsplit, and split-KV with the partition combine (the engine's adaptive
+    split picks partitions like these when few sequences carry long contexts)."""
+    lens = [32768, 20001, 9000, 4097, 1]
+    seqs = [(kv, 1) for kv in lens]
+    hq, hkv = 64, 8
+    q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=num_parts)
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, kc, vc, bt, sl, qs, scale)
+    out = torch.empty_like(q).to(DEV)
+    ws = ops.decode_workspace(len(seqs), hkv, hq // hkv, num_parts, DEV)
+    ops.paged_attention_decode(out, q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV),
+                               hq // hkv, scale, workspace=ws, num_parts=num_parts,
+                               part_size=part_size)
+    _close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+def test_paged_attention_prefill_deep_context():
+    """Chunked prefill deep into a long prompt: 512-token chunks whose causal window reaches
+    back over 16k cached tokens (plus a short fresh prompt in the same launch)."""
+    seqs = [(16384, 512), (12000, 300), (700, 700)]
+    hq, hkv = 16, 8
+    q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=3)
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, kc, vc, bt, sl, qs, scale)
+    ts, tr = _tiles(seqs, hq // hkv, 128)
+    out = torch.empty_like(q).to(DEV)
+    ops.paged_attention_prefill(out, q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV),
+                                qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv, scale,
+                                tile_rows=128)
+    _close(out, exp, atol=2e-2, rtol=2e-2)
