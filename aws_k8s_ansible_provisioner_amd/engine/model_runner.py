@@ -239,6 +239,13 @@ class ModelRunner:
                           self.workspace, tile_rows=self.tile_rows, num_decode=nd)
         h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
         if ns == 0:
+            # a chunk that samples nothing (a long prompt's inner chunk): the caller's
+            # device->host copy of zero tokens does not wait for the GPU, but the H2D copies
+            # above read the pinned host buffers when they EXECUTE -- finish them before the
+            # scheduler rewrites those buffers for the next step (else the next step's ids /
+            # slots leak into this chunk's KV)
+            if self.is_gpu:
+                torch.cuda.current_stream().synchronize()
             return self.out_tokens[:0]
         logits = self.model.compute_logits(h.index_select(0, lidx))
         if not self.is_gpu:

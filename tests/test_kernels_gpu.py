@@ -162,9 +162,9 @@ def test_paged_attention_decode(num_parts, part_size, hq, hkv):
 @pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (64, 8)])
 @pytest.mark.parametrize("qk_norm", [True, False])
 @pytest.mark.parametrize("num_parts,part_size", [(1, 4096), (3, 512)])
-def test_paged_attention_decode_fused(hq, hkv, qk_norm, num_parts, part_size):
+def test_paged_attention_decode_fused(hq, hkv, qk_norm, num_parts, part_size, lens=None):
     """Fused q/k-norm + RoPE + KV write + decode attention vs the reference pipeline."""
-    lens = [1, 31, 32, 33, 200, 777, 1500]
+    lens = lens or [1, 31, 32, 33, 200, 777, 1500]
     seqs = [(kv, 1) for kv in lens]
     _, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=hq + num_parts)
     B, D = len(lens), 128
@@ -174,7 +174,7 @@ def test_paged_attention_decode_fused(hq, hkv, qk_norm, num_parts, part_size):
     slots = torch.tensor([int(bt[s, int(pos[s]) // 32]) * 32 + int(pos[s]) % 32
                           for s in range(B)], dtype=torch.int64)
     slots[2] = -1  # padding row: no cache write
-    cs = ref.rope_cos_sin(4096, D, 1e6)
+    cs = ref.rope_cos_sin(max(4096, max(lens)), D, 1e6)
     qw = torch.randn(D, generator=g).bfloat16() if qk_norm else None
     kw = torch.randn(D, generator=g).bfloat16() if qk_norm else None
     kc_ref, vc_ref = kc.clone(), vc.clone()
@@ -795,6 +795,20 @@ def test_paged_attention_decode_long_context(num_parts, part_size):
                                hq // hkv, scale, workspace=ws, num_parts=num_parts,
                                part_size=part_size)
     _close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("num_parts,part_size", [(1, 32768), (64, 512), (128, 256), (32, 1024)])
+def test_paged_attention_decode_fused_long_context(num_parts, part_size):
+    """The engine's decode kernel (fused prologue) at long context with split-KV partitions."""
+    test_paged_attention_decode_fused(16, 8, True, num_parts, part_size,
+                                      lens=[8001, 1, 20001, 32768, 4095])
+
+
+@pytest.mark.parametrize("num_parts,part_size", [(32, 256), (64, 256)])
+def test_paged_attention_decode_fused_engine_split_plans(num_parts, part_size):
+    """The split-KV plans the engine picks for one 8k-16k sequence (qwen3-0.6b shapes)."""
+    test_paged_attention_decode_fused(16, 8, True, num_parts, part_size,
+                                      lens=[8001, 6501, 8192, 1, 7000])
 
 
 def test_paged_attention_prefill_deep_context():
