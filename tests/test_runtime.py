@@ -261,9 +261,9 @@ def _fake_model(b, info, req_of_row, prev=None):
     return toks.astype(np.int64)
 
 
-def _drive(lookahead, prompts, max_tokens, ignore_eos):
-    s, b = _sched(num_blocks=256, max_seqs=4, budget=16, max_len=64)
-    b["src_rows"] = np.zeros(4, np.int64)
+def _drive(lookahead, prompts, max_tokens, ignore_eos, num_blocks=256, max_seqs=4):
+    s, b = _sched(num_blocks=num_blocks, max_seqs=max_seqs, budget=16, max_len=64)
+    b["src_rows"] = np.zeros(max_seqs, np.int64)
     for i, p in enumerate(prompts):
         s.add_request(i + 1, p, max_tokens[i], 0, ignore_eos[i], [], stream=True)
     out = {i + 1: [] for i in range(len(prompts))}
@@ -335,3 +335,27 @@ def test_decode_lookahead_declines_when_work_waits():
     la = s.schedule_lookahead(b)
     assert la["num_seqs"] == 1 and b["src_rows"][0] == 0 and b["positions"][0] == 5
     assert s.schedule_lookahead(b)["num_seqs"] == 0  # at most one step ahead
+
+
+try:
+    from hypothesis import given, settings
+    from hypothesis import strategies as st_
+except ImportError:  # pragma: no cover
+    given = None
+
+if given is not None:
+    @settings(max_examples=60, deadline=None)
+    @given(st_.lists(st_.tuples(st_.integers(1, 20), st_.integers(1, 16), st_.booleans()),
+                     min_size=1, max_size=9),
+           st_.integers(0, 10 ** 6), st_.sampled_from([2, 4, 8]), st_.sampled_from([24, 48, 256]))
+    def test_decode_lookahead_property(reqs, seed, max_seqs, num_blocks):
+        """Random request mixes (queueing behind max_num_seqs, KV pools small enough to
+        preempt, EOS finishes while a lookahead step is in flight): the lookahead loop emits
+        exactly the synchronous loop's token streams and frees every block."""
+        rng = np.random.default_rng(seed)
+        prompts = [list(rng.integers(3, 90, size=n)) for n, _, _ in reqs]
+        mt = [m for _, m, _ in reqs]
+        ie = [e for _, _, e in reqs]
+        ref_out, _, _ = _drive(False, prompts, mt, ie, num_blocks, max_seqs)
+        got, _, _ = _drive(True, prompts, mt, ie, num_blocks, max_seqs)
+        assert got == ref_out
