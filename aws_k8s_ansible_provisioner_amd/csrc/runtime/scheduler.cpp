@@ -381,9 +381,11 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
 
 StepInfo Scheduler::schedule_lookahead(BatchBuffers& buf, int64_t* src_rows) {
   StepInfo info;
-  if (pending_.size() != 1 || !last_pure_decode_ || !waiting_.empty() ||
-      !sched_finished_.empty())
-    return info;
+  if (pending_.size() != 1 || !last_pure_decode_ || !sched_finished_.empty()) return info;
+  // waiting requests: only while every sequence slot is taken (a normal step could not admit
+  // them either); a length finish in the in-flight step frees a slot -> normal step
+  const bool queued = !waiting_.empty();
+  if (queued && (int)running_.size() < cfg_.max_num_seqs) return info;
   const std::vector<int64_t>& prev = pending_.back();
   const int bs = cfg_.block_size;
   const int mb = cfg_.max_blocks_per_seq;
@@ -404,6 +406,7 @@ StepInfo Scheduler::schedule_lookahead(BatchBuffers& buf, int64_t* src_rows) {
   // still-prefilling one needs a normal step)
   if (live != (int)running_.size() || rows.empty() || (int)rows.size() > cfg_.max_num_seqs)
     return info;
+  if (queued && (int)rows.size() != live) return info;
   for (auto& e : rows)
     if (!ensure_blocks(*e.first, e.first->num_computed + 1)) return info;
   int ns = 0;

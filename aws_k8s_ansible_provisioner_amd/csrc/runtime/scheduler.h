@@ -121,7 +121,8 @@ class Scheduler {
   // length are left out; a row that turns out to finish by EOS/stop (or is aborted) computes
   // one discarded token (its KV lands in its own, already freed blocks before any reuse:
   // stream order).  Returns num_seqs = 0 when the next step must be a normal one (waiting
-  // requests, a running sequence outside the in-flight batch, no KV blocks, nothing left).
+  // requests that a free sequence slot could admit, a running sequence outside the in-flight
+  // batch, no KV blocks, nothing left).
   StepInfo schedule_lookahead(BatchBuffers& buf, int64_t* src_rows);
   // tokens[i] is the sample for the i-th sampled sequence of the last step.
   // Emits (id, token, finish_reason, is_first) events only for sequences that got their

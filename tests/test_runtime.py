@@ -328,13 +328,31 @@ def test_decode_lookahead_declines_when_work_waits():
     info = s.schedule(b)
     assert not info["is_prefill"]
     s.add_request(2, [5, 6], 8, 0, True, [])  # a waiting request needs a normal step
-    assert s.schedule_lookahead(b)["num_seqs"] == 0
+    assert s.schedule_lookahead(b)["num_seqs"] == 0  # (a free sequence slot could admit it)
     s.update(np.array([9], np.int64))
     s.abort_request(2)
     s.schedule(b)
     la = s.schedule_lookahead(b)
     assert la["num_seqs"] == 1 and b["src_rows"][0] == 0 and b["positions"][0] == 5
     assert s.schedule_lookahead(b)["num_seqs"] == 0  # at most one step ahead
+
+
+def test_decode_lookahead_continues_while_the_queue_cannot_be_admitted():
+    """Every sequence slot taken: waiting requests could not be admitted by a normal step
+    either, so lookahead continues -- until the in-flight step ends a row by length."""
+    s, b = _sched(num_blocks=64, max_seqs=2, budget=16, max_len=64)
+    b["src_rows"] = np.zeros(2, np.int64)
+    s.add_request(1, [5, 6, 7], 3, 0, True, [])
+    s.add_request(2, [8, 9], 8, 0, True, [])
+    s.add_request(3, [4, 4], 4, 0, True, [])  # waits: max_num_seqs = 2
+    assert s.schedule(b)["is_prefill"]
+    s.update(np.array([11, 12], np.int64))
+    assert not s.schedule(b)["is_prefill"]  # both decode; request 1 has 1 of 3 tokens
+    la = s.schedule_lookahead(b)
+    assert la["num_seqs"] == 2  # queue non-empty, but no slot is free
+    s.update(np.array([13, 14], np.int64))
+    # request 1's in-flight token is its 3rd: it ends by length -> a normal step admits 3
+    assert s.schedule_lookahead(b)["num_seqs"] == 0
 
 
 try:
