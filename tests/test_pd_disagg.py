@@ -185,8 +185,19 @@ def test_pd_driver_matches_monolithic(tmp_path):
 # ---------------------------------------------------------------------------------------------
 # P/D KV lifecycle: no held-KV leak, no cross-group pairing, bounded transfers
 # ---------------------------------------------------------------------------------------------
-def _spawn_pair(extra_env=None, decode_env=None):
-    """One prefill + one decode server process (gloo, one transfer group)."""
+def _spawn_pair(extra_env=None, decode_env=None, attempts=3):
+    """One prefill + one decode server process (gloo, one transfer group).  A port picked
+    free can be handed out as another process's ephemeral port before the server binds it
+    (seen under pytest-xdist): such a start is retried with fresh ports."""
+    for i in range(attempts):
+        try:
+            return _spawn_pair_once(extra_env, decode_env)
+        except RuntimeError as e:
+            if "address already in use" not in str(e) or i == attempts - 1:
+                raise
+
+
+def _spawn_pair_once(extra_env=None, decode_env=None):
     master = _port()
     procs, urls = [], []
     for rank, role in enumerate(["prefill", "decode"]):
