@@ -4,16 +4,39 @@
 // B=64: 1 MiB); RCCL's ring pays ~2(W-1) link hops of latency for these.  MI355X's xGMI
 // mesh is fully connected, so every GPU can read every peer's HBM directly:
 //   * one-shot (small messages): each rank stages its input in an IPC-shared buffer,
-//     raises a flag on every peer, waits for all peers' flags, then sums all W staged
-//     copies itself -- one exchange, all 7 links busy at once;
+//     raises a flag on every peer, waits for all peers' flags, then sums all W copies
+//     itself -- one exchange, all 7 links busy at once;
 //   * two-shot (larger messages): reduce-scatter (rank r sums slice r from all peers into
 //     its result buffer) -> flags -> all-gather (read the other slices from the peers).
 // Synchronisation is per workgroup: block b of every rank owns the same element chunks,
-// so block b only needs block b's flags (no grid-wide barrier).  Flags carry a per-block
-// epoch kept in device memory (graph-replay safe: no host-side counter baked into the
-// captured launch); staging buffers alternate by epoch parity, so a fast rank never
-// overwrites data a slow peer is still reading.  Buffers and flags are allocated
-// uncached (hipDeviceMallocUncached) so peer reads never hit stale L2 lines.
+// so block b only needs block b's flags (no grid-wide barrier).
+//
+// Ordering argument (every hand-off is {sc0 sc1 stores, sc0 sc1 loads} on both sides, the
+// system-scope form of MI355X_MICROARCH.md "Valid forms"; no step relies on a cache
+// invalidate or write-back instruction):
+//   publish  every handed-off byte (staged input, two-shot partial result) is written by a
+//            buffer_store ... sc0 sc1 (write-through: the bytes leave the CU and the XCD's L2
+//            for HBM); every storing wave then drains with an explicit `s_waitcnt vmcnt(0)`
+//            (inline asm, so no compiler pass can drop it) and reaches the workgroup barrier;
+//            only after that barrier does one lane per peer store the epoch into that peer's
+//            flag word (a system-scope atomic store, sc0 sc1).
+//   consume  one lane per peer polls its flag word with system-scope relaxed atomic loads
+//            (sc0 sc1: never served by this CU's L1) until it reads >= the epoch; the waves
+//            meet at a barrier behind an `s_waitcnt vmcnt(0)`; then EVERY load of a peer's
+//            staged bytes is a buffer_load ... sc0 sc1, which bypasses this CU's L1, and the
+//            buffers are hipDeviceMallocUncached (MTYPE UC: no XCD L2 keeps a copy), so no
+//            load can return a line cached before the peer's store -- whatever this CU or
+//            XCD read in an earlier epoch (tests/test_custom_allreduce_gpu.py pre-reads the
+//            peers' lines with plain loads to make any such stale copy present).
+//   own data a rank never reads its own staged copy back: its term of the sum comes from
+//            its input tensor (written by an earlier kernel on this stream).
+//   epochs   per-block counters in device memory, read and written by thread 0 through the
+//            vector path (an agent-scope atomic, not s_load: the scalar cache is not kept
+//            coherent with vector stores), so a captured launch replays with fresh epochs.
+//   reuse    staging / result buffers alternate by epoch parity.  A rank writes the parity of
+//            epoch e+2 only inside launch e+2; it got there after epoch e+1's flags of every
+//            peer, i.e. after every peer finished launch e (stream order), so no peer can
+//            still be reading epoch e's bytes.
 // Every spin-wait is bounded: on timeout the kernel records an error flag and exits.
 #include "common.h"
 #include "kernels.h"
@@ -22,57 +45,62 @@ namespace akap {
 
 constexpr int kCarMaxBlocks = 128;
 constexpr int kCarMaxRanks = 8;
+constexpr int kCoh = 17;  // buffer op cache bits: sc0 | sc1 (system-coherent)
 
-__device__ __forceinline__ void car_signal(uint32_t* flag, uint32_t v) {
-  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t car_rsrc(const void* base, const CarArgs& a) {
+  // buffer of 4 * half_elems bf16 (staging x2, result x2); the base is wave-uniform (kernarg)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(a.half_elems * 8), 0x00020000);
+}
+
+__device__ __forceinline__ bf16x8 car_ld(__amdgpu_buffer_rsrc_t r, size_t elem) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem * 2), 0, kCoh);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void car_st(__amdgpu_buffer_rsrc_t r, size_t elem, bf16x8 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(elem * 2), 0,
+                                         kCoh);
 }
 
 __device__ __forceinline__ bool car_wait(const uint32_t* flag, uint32_t v) {
   // bounded by the constant-rate wall clock (100 MHz on MI3xx): give up after ~2 s
   const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
     if (wall_clock64() - t0 > 200000000ull) return false;
     __builtin_amdgcn_s_sleep(1);
   }
   return true;
 }
 
-// All ranks' blocks meet at phase `ph` (0 or 1) of epoch ep.
-// Publish: EVERY storing wave drains its own stores with an explicit s_waitcnt AFTER the
-// release fence (ROCm 7.2 can drop the fence's own wait -- cdna_hip_programming.md §6
-// Guideline 16, Pitfalls 12 and 14: a rare stale peer read under load otherwise) before the
-// barrier that lets one lane raise the flags.  Consume: the polling lanes' acquire (buffer_inv)
-// is likewise drained before the barrier that releases the other waves' peer loads.
+// All ranks' blocks `bid` meet at phase `ph` (0 or 1) of epoch ep (see the header).
 __device__ __forceinline__ void car_barrier(const CarArgs& a, int bid, uint32_t ep, int ph) {
-  __threadfence_system();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
   __syncthreads();
   const int t = threadIdx.x;
-  const size_t slot = ((size_t)ph * kCarMaxRanks + a.rank) * kCarMaxBlocks + bid;
-  if (t < a.world) car_signal(a.sigs[t] + slot, ep);
   if (t < a.world) {
+    const size_t slot = ((size_t)ph * kCarMaxRanks + a.rank) * kCarMaxBlocks + bid;
+    __hip_atomic_store(a.sigs[t] + slot, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const size_t mine = ((size_t)ph * kCarMaxRanks + t) * kCarMaxBlocks + bid;
-    if (!car_wait(a.sigs[a.rank] + mine, ep)) atomicOr(a.err, 1u);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!car_wait(a.sigs[a.rank] + mine, ep))
+      __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // compiler-only ordering: no peer load may be hoisted above the poll
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 }
 
 __device__ __forceinline__ uint32_t car_epoch(const CarArgs& a, int bid) {
   __shared__ uint32_t s_ep;
   if (threadIdx.x == 0) {
-    const uint32_t ep = a.counter[bid] + 1;
-    a.counter[bid] = ep;
+    const uint32_t ep =
+        __hip_atomic_load(a.counter + bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    __hip_atomic_store(a.counter + bid, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_ep = ep;
   }
   __syncthreads();
   return s_ep;
-}
-
-__device__ __forceinline__ void acc_add(float* acc, const bf16x8& v) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
 }
 
 // Store of one reduced 8-vector i: plain, or the residual + next-norm epilogue (CarEpi).
@@ -105,70 +133,95 @@ __device__ __forceinline__ void car_store(bf16* __restrict__ out, const CarEpi& 
   }
 }
 
+// Sum of the W ranks' copies of vector i (staged at element offset base + 8i in every peer's
+// buffer), in fixed rank order -> identical bits on every rank.  This rank's term is `own`.
+__device__ __forceinline__ bf16x8 car_sum(const CarArgs& a, size_t base, long i,
+                                          const bf16x8& own) {
+  bf16x8 v[kCarMaxRanks];
+#pragma unroll
+  for (int p = 0; p < kCarMaxRanks; ++p)  // every peer load issued before the first add
+    if (p < a.world && p != a.rank) v[p] = car_ld(car_rsrc(a.bufs[p], a), base + (size_t)i * 8);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < kCarMaxRanks; ++p) {
+    if (p >= a.world) break;
+    const bf16x8 x = p == a.rank ? own : v[p];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf2f(x[j]);
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+  return o;
+}
+
+// Test stress (CarMulti::warm): pull the peers' staging lines of this block's vectors into
+// this CU's caches with PLAIN loads before the exchange, so a protocol that depended on an
+// invalidate would read them stale.  The sink store never happens for finite inputs.
+__device__ __forceinline__ void car_prewarm(const CarArgs& a, int bid, int nblk, long n8,
+                                            size_t base, bf16* sink) {
+  const long stride = (long)nblk * 256;
+  float s = 0.f;
+  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride)
+    for (int p = 0; p < a.world; ++p) {
+      const bf16x8 x = reinterpret_cast<const bf16x8*>(a.bufs[p] + base)[i];
+      s += bf2f(x[0]);
+    }
+  if (s == 12345.678f) sink[0] = f2bf(s);
+}
+
 // Kernel bodies take the block's identity (bid of nblk) explicitly so the test launcher
 // below can run every simulated rank of one process inside one grid.
 template <bool EPI>
 __device__ __forceinline__ void car_oneshot(const CarArgs& a, int bid, int nblk,
                                             const bf16* __restrict__ in, bf16* __restrict__ out,
-                                            long n8, const CarEpi& epi) {
+                                            long n8, const CarEpi& epi, bool warm) {
   const uint32_t ep = car_epoch(a, bid);
   const size_t par = (ep & 1) * a.half_elems;
-  bf16x8* mine = reinterpret_cast<bf16x8*>(a.bufs[a.rank] + par);
+  if (warm) car_prewarm(a, bid, nblk, n8, par, out);
+  const __amdgpu_buffer_rsrc_t mine = car_rsrc(a.bufs[a.rank], a);
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
   const long stride = (long)nblk * 256;
-  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride) mine[i] = src[i];
+  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride)
+    car_st(mine, par + (size_t)i * 8, src[i]);
   car_barrier(a, bid, ep, 0);
-  bf16x8* dst = reinterpret_cast<bf16x8*>(out);
-  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // fixed rank order -> identical result bits on every rank
-    for (int p = 0; p < a.world; ++p)
-      acc_add(acc, reinterpret_cast<const bf16x8*>(a.bufs[p] + par)[i]);
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
-    car_store<EPI>(out, epi, i, o);
-  }
-  (void)dst;
+  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride)
+    car_store<EPI>(out, epi, i, car_sum(a, par, i, src[i]));
 }
 
 // Two-shot: n8 split into W slices of s8 vectors (last slice may be short).
 template <bool EPI>
 __device__ __forceinline__ void car_twoshot(const CarArgs& a, int bid, int nblk,
                                             const bf16* __restrict__ in, bf16* __restrict__ out,
-                                            long n8, const CarEpi& epi) {
+                                            long n8, const CarEpi& epi, bool warm) {
   const uint32_t ep = car_epoch(a, bid);
   const size_t par = (ep & 1) * a.half_elems;
-  // staging region: [0, half) input copies; result region: [2*half, 3*half) by parity
-  bf16x8* mine = reinterpret_cast<bf16x8*>(a.bufs[a.rank] + par);
+  if (warm) car_prewarm(a, bid, nblk, n8, par, out);
+  // staging region: [0, 2*half) input copies by parity; result region: [2*half, 4*half)
+  const __amdgpu_buffer_rsrc_t mine = car_rsrc(a.bufs[a.rank], a);
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
   const long stride = (long)nblk * 256;
   // slices are whole 64-vector groups: with the epilogue a wave's 64 lanes must stay inside one
   // slice (and so one row, d % 512 == 0) for car_store's wave-wide row sum of squares
   const long s8 = ((n8 + a.world - 1) / a.world + 63) / 64 * 64;
   // staged with the same slice-relative index->block map the reduce uses below, so block
-  // b of a peer reads exactly what block b of this rank wrote before its flag
+  // b of a peer reads exactly what block b of this rank wrote before its flag (this rank's
+  // own slice is not staged: its reduce reads it from `in`)
   for (int p = 0; p < a.world; ++p) {
+    if (p == a.rank) continue;
     const long plo = (long)p * s8;
     const long phi = plo + s8 < n8 ? plo + s8 : n8;
     for (long i = plo + (long)bid * 256 + threadIdx.x; i < phi; i += stride)
-      mine[i] = src[i];
+      car_st(mine, par + (size_t)i * 8, src[i]);
   }
   car_barrier(a, bid, ep, 0);
   const size_t res = 2 * a.half_elems + par;
-  bf16x8* dst = reinterpret_cast<bf16x8*>(out);
   // reduce-scatter: my slice [r*s8, min(n8,(r+1)*s8))
   const long lo = (long)a.rank * s8;
   const long hi = lo + s8 < n8 ? lo + s8 : n8;
-  bf16x8* myres = reinterpret_cast<bf16x8*>(a.bufs[a.rank] + res);
   for (long i = lo + (long)bid * 256 + threadIdx.x; i < hi; i += stride) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int p = 0; p < a.world; ++p)
-      acc_add(acc, reinterpret_cast<const bf16x8*>(a.bufs[p] + par)[i]);
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
-    myres[i] = o;
+    const bf16x8 o = car_sum(a, par, i, src[i]);
+    car_st(mine, res + (size_t)i * 8, o);
     car_store<EPI>(out, epi, i, o);
   }
   car_barrier(a, bid, ep, 1);
@@ -177,25 +230,24 @@ __device__ __forceinline__ void car_twoshot(const CarArgs& a, int bid, int nblk,
     const int p = (a.rank + q) % a.world;
     const long plo = (long)p * s8;
     const long phi = plo + s8 < n8 ? plo + s8 : n8;
-    const bf16x8* pres = reinterpret_cast<const bf16x8*>(a.bufs[p] + res);
+    const __amdgpu_buffer_rsrc_t pr = car_rsrc(a.bufs[p], a);
     for (long i = plo + (long)bid * 256 + threadIdx.x; i < phi; i += stride)
-      car_store<EPI>(out, epi, i, pres[i]);
+      car_store<EPI>(out, epi, i, car_ld(pr, res + (size_t)i * 8));
   }
-  (void)dst;
 }
 
 template <bool EPI>
 __global__ __launch_bounds__(256) void car_oneshot_kernel(CarArgs a, const bf16* __restrict__ in,
                                                           bf16* __restrict__ out, long n8,
                                                           CarEpi epi) {
-  car_oneshot<EPI>(a, blockIdx.x, gridDim.x, in, out, n8, epi);
+  car_oneshot<EPI>(a, blockIdx.x, gridDim.x, in, out, n8, epi, false);
 }
 
 template <bool EPI>
 __global__ __launch_bounds__(256) void car_twoshot_kernel(CarArgs a, const bf16* __restrict__ in,
                                                           bf16* __restrict__ out, long n8,
                                                           CarEpi epi) {
-  car_twoshot<EPI>(a, blockIdx.x, gridDim.x, in, out, n8, epi);
+  car_twoshot<EPI>(a, blockIdx.x, gridDim.x, in, out, n8, epi, false);
 }
 
 // Test launcher: blockIdx.y = simulated rank (all ranks' blocks co-resident in one grid).
@@ -204,10 +256,10 @@ __global__ __launch_bounds__(256) void car_multi_kernel(CarMulti m, long n8, int
   const int r = blockIdx.y;
   if (two_shot)
     car_twoshot<EPI>(m.args[r], blockIdx.x, gridDim.x, (const bf16*)m.in[r], (bf16*)m.out[r],
-                     n8, m.epi[r]);
+                     n8, m.epi[r], m.warm != 0);
   else
     car_oneshot<EPI>(m.args[r], blockIdx.x, gridDim.x, (const bf16*)m.in[r], (bf16*)m.out[r],
-                     n8, m.epi[r]);
+                     n8, m.epi[r], m.warm != 0);
 }
 
 // Block count for n8 vectors: the same on every rank (a pure function of n8 and world).

@@ -217,6 +217,7 @@ struct CarMulti {  // test-only: every rank of a simulated group in one launch
   void* out[8];
   CarEpi epi[8];
   int use_epi;
+  int warm;  // stress: pre-read peers' staging lines with plain loads (L1-warm consumer)
 };
 void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two_shot,
                                    hipStream_t s);

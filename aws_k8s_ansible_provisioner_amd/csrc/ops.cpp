@@ -805,10 +805,11 @@ void car_link_local(int64_t h, std::vector<int64_t> peers) {
 // of how streams map to hardware queues.
 void car_all_reduce_multi(std::vector<int64_t> hs, std::vector<Tensor> ins,
                           std::vector<Tensor> outs, bool two_shot,
-                          std::optional<std::vector<Tensor>> epi) {
+                          std::optional<std::vector<Tensor>> epi, bool warm) {
   const int W = hs.size();
   TORCH_CHECK(W >= 1 && W <= 8 && (int)ins.size() == W && (int)outs.size() == W, "W ranks");
   akap::CarMulti m{};
+  m.warm = warm ? 1 : 0;
   const int64_t n = ins[0].numel();
   for (int r = 0; r < W; ++r) {
     CarComm* c = car_get(hs[r]);
@@ -902,7 +903,7 @@ TORCH_LIBRARY(akap, m) {
   m.def("car_error(int h) -> int");
   m.def("car_link_local(int h, int[] peers) -> ()");
   m.def("car_all_reduce_multi(int[] hs, Tensor[] ins, Tensor(a!)[] outs, bool two_shot, "
-        "Tensor(b!)[]? epi=None) -> ()");
+        "Tensor(b!)[]? epi=None, bool warm=False) -> ()");
   m.def("car_all_reduce_resnorm(int h, Tensor inp, Tensor(a!) residual, Tensor ln, "
         "Tensor(b!) aout, Tensor(c!) ss, bool two_shot) -> ()");
   m.def("car_destroy(int h) -> ()");

@@ -157,6 +157,10 @@ PYBIND11_MODULE(_runtime, m) {
       .def("set_hold_kv", &Scheduler::set_hold_kv)
       .def("held_blocks", &Scheduler::held_blocks)
       .def("free_held", &Scheduler::free_held)
+      .def("take_held", &Scheduler::take_held)
+      .def("finish_transfer", &Scheduler::finish_transfer)
+      .def_property_readonly("num_in_transfer", &Scheduler::num_in_transfer)
+      .def_property_readonly("last_appended", &Scheduler::last_appended)
       .def_property_readonly("num_held", &Scheduler::num_held)
       .def("expire_held", &Scheduler::expire_held, py::arg("now_s"))
       .def_static("now_s", &Scheduler::now_s)

@@ -69,6 +69,24 @@ void Scheduler::free_held(int64_t id) {
   held_.erase(it);
 }
 
+std::vector<int32_t> Scheduler::take_held(int64_t id) {
+  auto it = held_.find(id);
+  if (it == held_.end()) return {};
+  std::vector<int32_t> b = std::move(it->second.blocks);
+  held_.erase(it);
+  auto& slot = in_transfer_[id];
+  if (!slot.empty()) bm_.free_blocks(slot);  // defensive: an id is never sent twice
+  slot = b;
+  return b;
+}
+
+void Scheduler::finish_transfer(int64_t id) {
+  auto it = in_transfer_.find(id);
+  if (it == in_transfer_.end()) return;
+  bm_.free_blocks(it->second);
+  in_transfer_.erase(it);
+}
+
 double Scheduler::now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -308,7 +326,6 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
   if (mix && backlog > (int64_t)budget * cfg_.mix_backlog_steps &&
       prefill_only_run_ < cfg_.max_decode_stall_steps)
     mix = false;  // burst: drain the prefill queue first (TTFT), decodes wait a bounded time
-  prefill_only_run_ = (pending_prefill && !mix && any_decode) ? prefill_only_run_ + 1 : 0;
   if (mix) {
     // mixed step: decodes first (they never stall behind a prefill), then prefill chunks
     int dbudget = std::max(0, std::min(cfg_.max_num_seqs, buf.cap_tokens - budget));
@@ -324,6 +341,10 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     info.num_decode = (int)sched.size();
   }
   info.is_prefill = (int)sched.size() > info.num_decode ? 1 : 0;
+  // bounded decode stall: count steps that actually ran prefill rows while decodes waited
+  // (a prefill-first step that fit no chunk fell back to pure decode: not a stall)
+  prefill_only_run_ = (info.is_prefill && info.num_decode == 0 && any_decode)
+                          ? prefill_only_run_ + 1 : 0;
 
   // ---------------- flatten ----------------
   int T = 0, tiles = 0, ns = 0;
@@ -463,6 +484,7 @@ void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_i
     out_first.push_back(0);
   }
   sched_finished_.clear();
+  last_appended_ = 0;
   for (Request* r : running_) publish_full_blocks(*r);
   for (int i = 0; i < n; ++i) {
     auto it = reqs_.find(sampled[i]);
@@ -472,6 +494,7 @@ void Scheduler::update(const int64_t* tokens, int n, std::vector<int64_t>& out_i
     Request* r = it->second.get();
     const int32_t tok = (int32_t)tokens[i];
     r->tokens.push_back(tok);
+    ++last_appended_;
     int reason = NOT_FINISHED;
     const int gen = r->num_generated();
     if (!r->ignore_eos && gen > r->min_tokens - 1 && tok == cfg_.eos_id) reason = FINISH_STOP;

@@ -131,6 +131,9 @@ class Scheduler {
               std::vector<int32_t>& out_tokens, std::vector<int32_t>& out_finish,
               std::vector<int32_t>& out_first);
 
+  // tokens the last update() appended to live sequences (rows of requests that finished or
+  // were aborted while the step was in flight are computed but not counted)
+  int last_appended() const { return last_appended_; }
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   bool has_work() const {
@@ -151,6 +154,13 @@ class Scheduler {
   // prefill side: blocks of a finished hold_kv request (kept until free_held)
   std::vector<int32_t> held_blocks(int64_t id) const;
   void free_held(int64_t id);
+  // a send of this held KV starts: the entry leaves the TTL-tracked held set (expire_held and
+  // free_held -- a /kv/release from a decode side that gave up -- no longer touch it) and its
+  // blocks stay owned until finish_transfer(), which the send's completion calls.  Returns the
+  // blocks (empty: nothing held under this id, e.g. already expired)
+  std::vector<int32_t> take_held(int64_t id);
+  void finish_transfer(int64_t id);
+  size_t num_in_transfer() const { return in_transfer_.size(); }
   // decode side: register a request whose prompt KV arrives from a prefill engine.
   // tokens = prompt + first generated token.  Allocates the prompt's blocks and
   // returns them (empty if the pool is short); the request is not scheduled until
@@ -195,9 +205,11 @@ class Scheduler {
     double deadline;
   };
   std::unordered_map<int64_t, HeldKV> held_;
+  std::unordered_map<int64_t, std::vector<int32_t>> in_transfer_;  // held KV being sent
   int64_t preemptions_ = 0;
   int64_t held_expired_ = 0;
-  int prefill_only_run_ = 0;  // consecutive prefill-only steps while decodes were waiting
+  int prefill_only_run_ = 0;
+  int last_appended_ = 0;  // consecutive prefill-only steps while decodes were waiting
 };
 
 }  // namespace akap_rt

@@ -187,6 +187,17 @@ class LLMEngine:
         with self._lock:
             self.sched.free_held(int(transfer_id))
 
+    def take_held(self, transfer_id: int) -> list:
+        """A send of this transfer's KV starts: its blocks leave the TTL / release path and
+        stay owned until finish_transfer() (the send's completion), so neither the TTL sweep
+        nor a decode side's /kv/release can recycle blocks that are still being packed."""
+        with self._lock:
+            return list(self.sched.take_held(int(transfer_id)))
+
+    def finish_transfer(self, transfer_id: int) -> None:
+        with self._lock:
+            self.sched.finish_transfer(int(transfer_id))
+
     def reserve_prefilled(self, req_id: str, prompt_ids: list, first_token: int,
                           params: SamplingParams, stream: bool = False):
         """Decode side of P/D: allocate blocks for a remotely prefilled prompt.
@@ -307,7 +318,9 @@ class LLMEngine:
         m, name = self.metrics, self.model_name
         if info["is_prefill"]:
             m.prompt_tokens.inc(info["num_tokens"] - info.get("num_decode", 0), model_name=name)
-        m.gen_tokens.inc(info["num_samples"], model_name=name)
+        # tokens actually appended: rows of requests that ended while the step was in flight
+        # (lookahead) are computed but discarded
+        m.gen_tokens.inc(self.sched.last_appended, model_name=name)
         m.step_time.observe(now - t0, model_name=name,
                             phase="prefill" if info["is_prefill"] else "decode")
         outs = []

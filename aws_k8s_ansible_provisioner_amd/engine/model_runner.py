@@ -21,6 +21,7 @@ import torch
 
 from ..utils import profiling
 from .. import ops
+from ..models import moe as moe_mod
 from ..models.config import ModelConfig
 from ..models.transformer import AttnBatch, DecoderLM
 from ..parallel.state import ParallelState, drain_pending_collectives, get_state
@@ -89,6 +90,7 @@ class ModelRunner:
         # top-N alternatives of the last step's sampled rows: (token ids [n, N], log-probs)
         self.last_top: Optional[tuple] = None
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.ep_overflow_steps = 0  # decode steps re-run after an EP dispatch overflow
         self.graph_pool = None
         self.buckets: list[int] = []
         if self.is_gpu and not ecfg.enforce_eager and self.model.graph_safe:
@@ -286,10 +288,26 @@ class ModelRunner:
         batch = AttnBatch(False, dd["positions"][:n], dd["slots"][:n], self.dd_bt[:n],
                           dd["seq_lens"][:n], self.d["q_start"][:n + 1], None, None,
                           parts, ps, self.workspace)
+        if self._ep_moe:
+            moe_mod.ep_overflow_reset(self.device)
         h = self.model.forward(dd["input_ids"][:n], batch, self.k_caches, self.v_caches)
         # sampler reads bf16 logits directly (no [n, V] fp32 cast pass)
         logits = self.model.compute_logits(h)
         self._sample(logits, n, extras, src=dd)
+        if self._ep_moe:
+            moe_mod.ep_overflow_reduce(self.device)
+
+    @property
+    def _ep_moe(self) -> bool:
+        """Expert-parallel MoE layers over more than one rank (fixed-capacity dispatch)."""
+        return self.ps.world_size > 1 and any(
+            getattr(getattr(layer, "moe", None), "mode", None) == "ep"
+            for layer in getattr(self.model, "layers", []))
+
+    def _ep_overflowed(self) -> bool:
+        """After a replayed decode step: did a fixed-capacity EP dispatch drop a pair on any
+        rank?  (all-reduced inside the step, so every rank answers the same)"""
+        return self._ep_moe and int(moe_mod.MoEBlock.overflow_flag(self.device).item()) != 0
 
     def _pad_host(self, B: int, n: int) -> None:
         if n <= B:
@@ -321,6 +339,11 @@ class ModelRunner:
         extras = info.get("extras")
         if graph is not None and not extras:
             graph.replay()
+            if self._ep_overflowed():
+                # routing skew beyond the dispatch capacity: redo the step eagerly on the
+                # exact-split path (the same KV slots are rewritten, the tokens replaced)
+                self.ep_overflow_steps += 1
+                self._decode_body(n, extras)
         else:
             # penalties / log-probs requested: the same padded batch (n rows, so TP peers
             # replaying their graphs issue identical collectives), eagerly
@@ -408,7 +431,17 @@ class ModelRunner:
             cache = os.environ.get("AKAP_GEMM_TUNE_CACHE")
             if cache and self.model.ps.world_size > 1:
                 cache = f"{cache}.rank{self.model.ps.rank}"
-            if cache and gemm_tuner.load_cache(cache, self.model, tune_ms):
+            loaded = bool(cache) and gemm_tuner.load_cache(cache, self.model, tune_ms)
+            if self.ps.tp_size > 1:
+                # tune_fused broadcasts rank 0's plan over the TP group: every rank must take
+                # the same branch, so one rank's missing / stale cache file retunes them all
+                from ..parallel import comm
+
+                agreed = comm.tp_all_true(loaded)
+                if loaded and not agreed:
+                    gemm_tuner.reset()
+                loaded = agreed
+            if loaded:
                 self.log(f"[runner] GEMM plan loaded from {cache} "
                          f"({len(gemm_tuner.plan())} shapes)")
             else:

@@ -144,6 +144,20 @@ TINY_MIXTRAL = register(ModelConfig(
     experts_per_token=2, bos_id=1, eos_id=2))
 
 
+# the real multi-GPU layouts at world size 8: Llama-3-70B's 8 KV heads (one per TP rank, GQA
+# 8) and Mixtral's 8 experts (one per EP rank)
+TINY_LLAMA_KV8 = register(ModelConfig(
+    name="tiny-llama-kv8", hf_id="test/tiny-llama-kv8", arch="llama", vocab_size=512,
+    hidden_size=256, intermediate_size=512, num_layers=2, num_heads=16, num_kv_heads=8,
+    head_dim=128, rope_theta=500000.0, max_position=4096, bos_id=1, eos_id=2))
+
+TINY_MIXTRAL8 = register(ModelConfig(
+    name="tiny-mixtral8", hf_id="test/tiny-mixtral8", arch="mixtral", vocab_size=512,
+    hidden_size=256, intermediate_size=256, num_layers=2, num_heads=16, num_kv_heads=8,
+    head_dim=128, rope_theta=1_000_000.0, max_position=4096, num_experts=8,
+    experts_per_token=2, bos_id=1, eos_id=2))
+
+
 def get_config(name: str) -> ModelConfig:
     """Resolve a registry name, HF id, or a directory holding a HF config.json."""
     if os.path.isdir(name) and os.path.exists(os.path.join(name, "config.json")):

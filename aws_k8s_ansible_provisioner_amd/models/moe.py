@@ -7,17 +7,25 @@ sorted, tile-padded index list).  Two placements:
   * "ep": rank e holds experts [e*E/ep, (e+1)*E/ep) whole; tokens are dispatched and
     combined with two RCCL all_to_all_single calls over the EP (=dp x tp) group.
 Expert GEMMs: `ops.fused_moe` -- device-side sort + grouped MFMA GEMMs + gather-combine,
-no host sync.  "tp" mode uses it at decode sizes (captured in the decode hipGraph); very
-large "tp" prefill batches run per expert on hipBLASLt (AKAP_FUSED_MOE_MAX_T).
+no host sync, at every batch size in "tp" mode (decode steps inside the hipGraph, prefill
+chunks eagerly); the per-expert loop below serves only the CPU reference path.
 
-"ep" mode, decode sizes (T <= AKAP_EP_FIXED_MAX_T): a FIXED-CAPACITY dispatch -- every
-(token, expert) pair gets a slot (destination rank, rank-local index) computed on the device,
-the send buffer is [ep, C, d] with C = T*K (the most pairs any one rank can receive), so both
-all_to_all_single calls use equal splits and no split size ever goes to the host: the whole
-EP MoE block (route, dispatch, grouped expert GEMMs on the received rows, combine) is
-sync-free and graph-capturable.  Empty slots carry expert id -1, which moe_align skips.
-Larger (prefill) batches exchange exact split sizes (one small host sync per layer) and run
-the received rows through the same grouped GEMM.
+"ep" mode inside a captured decode step: a FIXED-CAPACITY dispatch -- every (token, expert)
+pair gets a slot (destination rank, rank-local index) computed on the device, the send buffer
+is [ep, C, d] with C = ep_capacity(n) = max(ceil(slack * n / ep), min(n, 8)) for the n = T*K
+pairs of this rank (slack 2 by default, AKAP_EP_SLACK): the exchanged bytes stay within
+slack x the exact n*d however many ranks there are, where a worst-case C = n would move
+ep*n*d.  Both all_to_all_single calls use equal splits and no split size goes to the host,
+so the whole EP MoE block (route, dispatch, grouped expert GEMMs on the received rows,
+combine) is sync-free and graph-capturable.  Empty slots carry expert id -1, which moe_align
+skips.  A pair whose destination already holds C pairs (a routing skew the capacity does not
+cover) is not sent; it raises the shared overflow flag instead, which the decode step
+all-reduces over the EP group at its end (ep_overflow_reduce): the runner then re-runs that
+step eagerly on the exact path (ModelRunner.execute_decode), so an overflow costs one extra
+step, never a wrong token.  Eager steps exchange exact split sizes (one small host sync per
+layer) and run the received rows through the same grouped GEMM; AKAP_EP_FIXED_MAX_T > 0 makes
+eager steps up to that many tokens take the fixed path too (with an immediate all-reduced
+overflow check: tests).
 """
 from __future__ import annotations
 
@@ -30,6 +38,19 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import ParallelState
+
+
+def ep_overflow_reset(device) -> None:
+    MoEBlock.overflow_flag(device).zero_()
+
+
+def ep_overflow_reduce(device) -> torch.Tensor:
+    """All-reduce (MAX) of the fixed-dispatch overflow flag over the EP group: every rank
+    sees the same value, so all of them re-run an overflowed step together."""
+    f = MoEBlock.overflow_flag(device)
+    if torch.distributed.is_initialized():
+        torch.distributed.all_reduce(f, op=torch.distributed.ReduceOp.MAX)
+    return f
 
 
 class MoEBlock:
@@ -138,8 +159,25 @@ class MoEBlock:
             return full[:T]
         return self._forward_tokens(h)
 
-    graph_safe_max_tokens = int(os.environ.get("AKAP_FUSED_MOE_MAX_T", "1024"))
-    ep_fixed_max_tokens = int(os.environ.get("AKAP_EP_FIXED_MAX_T", "512"))
+    ep_fixed_max_tokens = int(os.environ.get("AKAP_EP_FIXED_MAX_T", "0"))
+    ep_slack = float(os.environ.get("AKAP_EP_SLACK", "2.0"))
+    ep_min_cap = int(os.environ.get("AKAP_EP_MIN_CAP", "8"))
+    ep_fallbacks = 0  # eager fixed-path layers redone on the exact path after an overflow
+    _overflow: dict = {}  # device -> int32 [1]: a fixed-capacity dispatch dropped a pair
+
+    def ep_capacity(self, n: int) -> int:
+        """Rows per destination rank in the fixed-capacity dispatch of n (token, expert) pairs:
+        slack x the mean share, at least min(n, ep_min_cap = 8) (tiny decode batches), at most n."""
+        import math
+
+        return min(n, max(math.ceil(self.ep_slack * n / self.ep), min(n, self.ep_min_cap)))
+
+    @classmethod
+    def overflow_flag(cls, device) -> torch.Tensor:
+        key = str(device)
+        if key not in cls._overflow:
+            cls._overflow[key] = torch.zeros(1, dtype=torch.int32, device=device)
+        return cls._overflow[key]
 
     @property
     def graph_safe(self) -> bool:
@@ -152,10 +190,18 @@ class MoEBlock:
         w, ids = ops.moe_router_topk(h, self.router, self.K, renormalize=True)
         capturing = h.is_cuda and torch.cuda.is_current_stream_capturing()
         if self.mode == "ep":
-            if T <= self.ep_fixed_max_tokens or capturing:
+            if capturing:
                 return self._ep_fixed(h, w, ids)
+            if T <= self.ep_fixed_max_tokens:
+                flag = torch.zeros(1, dtype=torch.int32, device=h.device)
+                y = self._ep_fixed(h, w, ids, flag)
+                torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+                if int(flag.item()) == 0:
+                    return y
+                MoEBlock.ep_fallbacks += 1
             return self._ep_exact(h, w, ids)
-        if h.is_cuda and (T <= self.graph_safe_max_tokens or capturing):
+        # tp mode: device-side grouped GEMM at every size (no host sync, graph-safe)
+        if h.is_cuda:
             out = ops.fused_moe(h, self.w13, self.w2, w, ids)
             comm.tp_all_reduce(out)
             return out
@@ -171,22 +217,32 @@ class MoEBlock:
         comm.tp_all_reduce(out)
         return out
 
-    def _ep_fixed(self, h: torch.Tensor, w: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
-        """Sync-free, capturable EP dispatch/combine with per-peer capacity C = T*K."""
+    def a2a_rows(self, T: int) -> int:
+        """Rows this rank sends per all_to_all of the fixed dispatch (= rows received)."""
+        return self.ep * self.ep_capacity(T * self.K)
+
+    def _ep_fixed(self, h: torch.Tensor, w: torch.Tensor, ids: torch.Tensor,
+                  flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Sync-free, capturable EP dispatch/combine with per-peer capacity ep_capacity(T*K)."""
         T, d = h.shape
         K, ep, el = self.K, self.ep, self.e_local
         n = T * K
-        C = n
+        C = self.ep_capacity(n)
         flat = ids.reshape(-1).long()                       # [n] global expert ids
         dest = flat // el                                   # owning rank
         onehot = F.one_hot(dest, ep).to(torch.int32)        # [n, ep]
         slot = ((torch.cumsum(onehot, 0) - onehot) * onehot).sum(1).long()  # rank-local index
-        pos = dest * C + slot                               # row in the [ep * C] send buffer
+        fits = slot < C
+        # overflowing pairs go to a dump row past the send buffer (never sent)
+        pos = torch.where(fits, dest * C + slot, torch.full_like(slot, ep * C))
+        flag = self.overflow_flag(h.device) if flag is None else flag
+        torch.maximum(flag, (~fits).any().to(torch.int32).view(1), out=flag)
         tok = torch.arange(n, device=h.device) // K
-        send_x = h.new_zeros(ep * C, d)
+        send_x = h.new_zeros(ep * C + 1, d)
         send_x.index_copy_(0, pos, h[tok])
-        send_e = torch.full((ep * C,), -1, dtype=torch.int32, device=h.device)
+        send_e = torch.full((ep * C + 1,), -1, dtype=torch.int32, device=h.device)
         send_e.index_copy_(0, pos, (flat - dest * el).to(torch.int32))
+        send_x, send_e = send_x[:ep * C], send_e[:ep * C]
         recv_x = torch.empty_like(send_x)
         recv_e = torch.empty_like(send_e)
         grp = None  # the EP group is the whole job (dp x tp ranks)
@@ -196,8 +252,8 @@ class MoEBlock:
         # weight is applied by the sender at combine); empty slots (id -1) give zero rows
         ones = torch.ones(ep * C, 1, dtype=torch.float32, device=h.device)
         y = ops.fused_moe(recv_x, self.w13, self.w2, ones, recv_e.view(-1, 1))
-        back = torch.empty_like(y)
-        torch.distributed.all_to_all_single(back, y, group=grp)
+        back = h.new_zeros(ep * C + 1, d)
+        torch.distributed.all_to_all_single(back[:ep * C], y, group=grp)
         mine = back.index_select(0, pos).view(T, K, d).float()
         return (mine * w.view(T, K, 1)).sum(1).to(h.dtype)
 

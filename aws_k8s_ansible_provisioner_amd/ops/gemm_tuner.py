@@ -42,6 +42,12 @@ def plan() -> dict:
     return _PLAN
 
 
+def reset() -> None:
+    """Forget every tuned choice (per-shape plan and fused chains)."""
+    _PLAN.clear()
+    _FUSED.clear()
+
+
 def lookup(M: int, N: int, K: int) -> Optional[Choice]:
     return _PLAN.get((M, N, K))
 

@@ -76,6 +76,18 @@ def all_to_all(x: torch.Tensor, out_splits: list[int], in_splits: list[int], gro
     return out
 
 
+def tp_all_true(flag: bool) -> bool:
+    """True on every TP rank iff it is True on all of them (MIN all-reduce of a flag): for
+    per-rank decisions that must agree before a collective-issuing code path runs."""
+    st = get_state()
+    if st.tp_size == 1 or st.tp_group is None:
+        return bool(flag)
+    dev = "cuda" if dist.get_backend(st.tp_group) == "nccl" else "cpu"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=st.tp_group)
+    return bool(t.item())
+
+
 def broadcast_object(obj, src: int = 0, group=None):
     st = get_state()
     if st.world_size == 1:

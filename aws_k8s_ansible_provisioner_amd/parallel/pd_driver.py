@@ -74,13 +74,13 @@ class PDPair:
             msg, tids, blocks = [len(batch)], [], []
             for o in batch:
                 tid = int(o.kv_transfer_params["transfer_id"])
-                b = eng.held_blocks(tid)
+                b = eng.take_held(tid)
                 msg += [tid, len(o.prompt_ids), int(o.output_ids[0]), len(b)] + list(o.prompt_ids)
                 tids.append(tid)
                 blocks += b
             _send_msg(np.array(msg, dtype=np.int64), self.peer, self.ctrl)
             pending.append(self.agent.send_blocks(
-                blocks, self.peer, on_done=lambda ts=tuple(tids): [eng.free_held(t) for t in ts],
+                blocks, self.peer, on_done=lambda ts=tuple(tids): [eng.finish_transfer(t) for t in ts],
                 wait=False))
             sent += len(batch)
         _send_msg(np.array([_END], dtype=np.int64), self.peer, self.ctrl)

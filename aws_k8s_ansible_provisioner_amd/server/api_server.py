@@ -221,18 +221,25 @@ class OpenAIServer:
             missing = [t for t, b in zip(tids, per) if not b]
             if missing:
                 return _err(404, f"no held KV for transfer(s) {missing}")
+            # from here the blocks are owned by the send (not the TTL sweep, not /kv/release)
+            # until its completion frees them
+            per = [eng.take_held(t) for t in tids]
+            if any(not b for b in per):  # expired between the check and the take
+                for t in tids:
+                    eng.finish_transfer(t)
+                return _err(404, f"held KV for transfer(s) {tids} expired")
             blocks = [b for bl in per for b in bl]
             if os.environ.get("AKAP_FAULT_KV_PUSH") == "drop":
                 # fault injection (tests): acknowledge the push, then "die" before sending --
                 # the decode side's bounded recv must fail the request, not hang
                 for t in tids:
-                    eng.free_held(t)
+                    eng.finish_transfer(t)
                 return {"ok": True, "num_blocks": [len(b) for b in per]
                         if "transfer_ids" in body else len(per[0])}
 
             def done(ts=tuple(tids)):
                 for t in ts:
-                    eng.free_held(t)
+                    eng.finish_transfer(t)
 
             self.ae.kv_agent.send_blocks(blocks, int(body["dst_rank"]), on_done=done)
             nb = [len(b) for b in per]

@@ -24,30 +24,53 @@ def _ref_sum(xs):
     return acc.to(torch.bfloat16)
 
 
+def _explain(outs, exp, prev, r, world, n, two_shot):
+    """Self-explaining failure: first bad element, its block/lane, and what it equals."""
+    d = (outs[r].float() - exp.float()).abs()
+    bad = (~(d <= 0.02 * world)).nonzero().flatten()
+    i = int(bad[0])
+    v = outs[r][i].float().item()
+    n8 = n // 8
+    per = (n8 + world - 1) // world if two_shot else n8
+    nblk = max(1, min(128, (per + 255) // 256))
+    vec = i // 8
+    kind = "unwritten (NaN)" if v != v else (
+        "previous epoch's sum" if prev is not None and abs(v - prev[i].float().item()) <= 0.04
+        else "other")
+    return (f"rank {r}: {len(bad)} bad of {n}; first elem {i} (vector {vec}, block "
+            f"{(vec % (nblk * 256)) // 256}, lane {vec % 256}) = {v} vs {exp[i].item()}: {kind}")
+
+
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 @pytest.mark.parametrize("two_shot", [False, True])
 @pytest.mark.parametrize("n", [8, 4096, 8 * 1000 + 8 * 3, 1 << 19])
 def test_custom_allreduce_in_process(world, two_shot, n):
-    """All simulated ranks in one grid (blockIdx.y = rank): protocol, parity, ownership."""
+    """All simulated ranks in one grid (blockIdx.y = rank): protocol, parity, ownership.
+    Outputs are poisoned with NaN before every call (an unwritten element cannot pass), and
+    every other epoch the consumers pre-read the peers' staging lines with plain loads (an
+    L1/L2-warm consumer: a protocol relying on a cache invalidate would read them stale)."""
     ops.load_native(required=True)
     max_elems = 1 << 20
     hs = [torch.ops.akap.car_create(0, r, world, max_elems) for r in range(world)]
+    prev = None
     try:
         for h in hs:
             torch.ops.akap.car_link_local(h, hs)
-        for it in range(3):  # several epochs: both parities, reused flags
+        for it in range(6):  # several epochs: both parities, reused flags, warm and cold
             torch.manual_seed(100 * it + world + n)
             xs = [torch.randn(n, dtype=torch.bfloat16, device=DEV) for _ in range(world)]
-            outs = [torch.empty_like(x) for x in xs]
-            torch.ops.akap.car_all_reduce_multi(hs, xs, outs, two_shot)
+            outs = [torch.full_like(x, float("nan")) for x in xs]
+            torch.ops.akap.car_all_reduce_multi(hs, xs, outs, two_shot, None, it % 2 == 1)
             torch.cuda.synchronize()
             for h in hs:
                 assert torch.ops.akap.car_error(h) == 0, "flag wait timed out"
             exp = _ref_sum(xs)
             for r in range(world):
+                err = (outs[r].float() - exp.float()).abs().max().item()
+                assert err <= 0.02 * world, f"epoch {it}: " + _explain(outs, exp, prev, r, world,
+                                                                      n, two_shot)
                 assert torch.equal(outs[r], outs[0]), "ranks disagree"
-            err = (outs[0].float() - exp.float()).abs().max().item()
-            assert err <= 0.02 * world, err
+            prev = exp
     finally:
         torch.cuda.synchronize()
         for h in hs:

@@ -212,6 +212,59 @@ def test_held_kv_expires_after_ttl():
     assert s.kv_usage() == 0
 
 
+def test_held_kv_in_transfer_survives_ttl_and_release():
+    """A send that started owns its blocks: neither the TTL sweep nor a decode side's
+    /kv/release (free_held) may recycle them while they are being packed; only the send's
+    completion (finish_transfer) frees them (/kv/push vs expire_held race)."""
+    c = rt.SchedConfig()
+    c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 4, 32, 64
+    c.block_size, c.gqa_group, c.tile_rows, c.eos_id, c.max_blocks_per_seq = 4, 2, 64, 2, 16
+    c.held_kv_ttl_s = 30.0
+    s, b = rt.Scheduler(c, 32, False), _bufs(4, 36, 16)
+    s.add_request(7, list(range(10, 22)), 1)
+    s.set_hold_kv(7, True)
+    s.schedule(b)
+    s.update(np.array([5], np.int64))
+    held = list(s.held_blocks(7))
+    assert s.take_held(7) == held and s.num_held == 0 and s.num_in_transfer == 1
+    free0 = s.num_free_blocks()
+    assert s.expire_held(rt.Scheduler.now_s() + 999.0) == 0  # not TTL-tracked any more
+    s.free_held(7)  # a late /kv/release from a decode side that gave up: no effect
+    assert s.num_free_blocks() == free0 and s.kv_usage() > 0
+    # a new prefill cannot be handed the blocks still being sent
+    s.add_request(8, list(range(40, 60)), 1)
+    i = s.schedule(b)
+    assert not set(s.block_table(8)) & set(held), (s.block_table(8), held)
+    s.update(np.zeros(i["num_samples"], np.int64) + 5)
+    s.finish_transfer(7)
+    s.finish_transfer(7)  # idempotent
+    assert s.num_in_transfer == 0
+    assert s.take_held(7) == []  # nothing held any more
+
+
+def test_last_appended_counts_only_live_rows():
+    """generation_tokens_total counts tokens actually appended: a lookahead row of a request
+    that finished by EOS in the previous update is computed and discarded, not counted."""
+    c = rt.SchedConfig()
+    c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 4, 64, 64
+    c.block_size, c.gqa_group, c.tile_rows, c.eos_id, c.max_blocks_per_seq = 4, 2, 64, 2, 16
+    s, b = rt.Scheduler(c, 64, False), _bufs(4, 68, 16)
+    s.add_request(1, [10, 11, 12], 8)
+    s.add_request(2, [20, 21, 22], 8)
+    i = s.schedule(b)
+    s.update(np.array([5, 5], np.int64))
+    assert s.last_appended == 2
+    i = s.schedule(b)  # pure decode, both rows
+    assert i["num_seqs"] == 2 and not i["is_prefill"]
+    b["src_rows"] = np.zeros(4, np.int64)
+    la = s.schedule_lookahead(b)
+    assert la["num_seqs"] == 2
+    s.update(np.array([2, 5], np.int64))  # request 1 hits EOS (id 2)
+    assert s.last_appended == 2
+    s.update(np.array([7, 7], np.int64))  # lookahead: request 1's row is discarded
+    assert s.last_appended == 1
+
+
 def test_burst_backlog_stays_prefill_first_for_a_bounded_number_of_steps():
     """A prefill backlog larger than one step's budget (burst arrival) is drained
     prefill-first (TTFT) -- but decodes wait at most max_decode_stall_steps steps; once the

@@ -29,6 +29,8 @@ if eng is not None:
                         prompt_ids=[list(range(5, 40)), [100, 101], [9, 9, 9]])
     bc.shutdown()
     print("RESULT " + json.dumps([o.output_ids for o in outs]), flush=True)
+from aws_k8s_ansible_provisioner_amd.models.moe import MoEBlock
+print("FALLBACKS", MoEBlock.ep_fallbacks, flush=True)
 """
 
 
@@ -45,7 +47,12 @@ def _port():
     ("tiny-mixtral", "ep", 2, 512),
     # 4 ranks: kv heads replicated (2 kv heads / 4 ranks), one expert per EP rank; EP with the
     # fixed-capacity (graph-safe) dispatch and with the exact-split prefill path
-    ("tiny-llama", "tp", 4, 512), ("tiny-mixtral", "ep", 4, 512), ("tiny-mixtral", "ep", 4, 0)])
+    ("tiny-llama", "tp", 4, 512), ("tiny-mixtral", "ep", 4, 512), ("tiny-mixtral", "ep", 4, 0),
+    # the real world-8 layouts: Llama-3-70B's one KV head per TP rank (GQA 8 -> 2 q heads and
+    # 1 kv head per rank) and Mixtral's one expert per EP rank, fixed-capacity dispatch (slack
+    # 2) and the exact path; slack 0.3 forces dispatch overflows -> every layer falls back
+    ("tiny-llama-kv8", "tp", 8, 512), ("tiny-mixtral8", "ep", 8, 512),
+    ("tiny-mixtral8", "ep", 8, 0), ("tiny-mixtral8", "ep-slack0.3", 8, 512)])
 def test_tp_matches_tp1(model, moe_mode, world, ep_fixed):
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
@@ -53,15 +60,21 @@ def test_tp_matches_tp1(model, moe_mode, world, ep_fixed):
     port = _port()
     procs = []
     for r in range(world):
+        mode, _, slack = moe_mode.partition("-slack")
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROOT=ROOT, MODEL=model,
-                   AKAP_MOE_MODE=moe_mode, AKAP_EP_FIXED_MAX_T=str(ep_fixed))
+                   AKAP_MOE_MODE=mode, AKAP_EP_FIXED_MAX_T=str(ep_fixed),
+                   AKAP_EP_SLACK=slack or "2.0", AKAP_EP_MIN_CAP="1" if slack else "8",
+                   OMP_NUM_THREADS="1")
         procs.append(subprocess.Popen([sys.executable, "-c", CHILD], env=env, cwd=ROOT,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=300) for p in procs]
     assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
     line = [l for l in outs[0][0].splitlines() if l.startswith("RESULT ")][0]
     tp_out = json.loads(line[7:])
+    if "slack" in moe_mode:  # the undersized dispatch overflowed and fell back every time
+        fb = [l for l in outs[0][0].splitlines() if l.startswith("FALLBACKS ")][0]
+        assert int(fb.split()[1]) > 0, fb
     ref = LLMEngine(EngineConfig(model=model, device="cpu", max_model_len=256, max_num_seqs=8,
                                  max_num_batched_tokens=32, block_size=32, num_gpu_blocks=96,
                                  shard_init="full", init_std=0.15), log=lambda *a: None)
@@ -157,3 +170,57 @@ def test_tp_decode_step_is_one_host_broadcast(monkeypatch):
     pre = dict(dec, is_prefill=1, num_tokens=20, num_tiles=2, num_decode=0)
     bc.execute(pre)
     assert len(sent) == 2 and sent[0].tolist()[-1] == sent[1].numel() > 0
+
+
+AGREE_CHILD = r"""
+import os, sys
+sys.path.insert(0, os.environ["ROOT"])
+from aws_k8s_ansible_provisioner_amd.parallel.state import init_distributed
+from aws_k8s_ansible_provisioner_amd.parallel import comm
+import torch.distributed as dist
+ps = init_distributed(tp_size=2, backend="gloo")
+# rank 1's tuning-cache file is missing: every rank must take the retune branch
+mine = ps.rank != 1
+print("RESULT", int(comm.tp_all_true(mine)), int(comm.tp_all_true(True)), flush=True)
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def test_tp_ranks_agree_on_tuning_cache_load():
+    """a rank whose GEMM tuning-cache file is missing/stale retunes (tune_fused then
+    broadcasts over the TP group) -- every rank must take that branch, so the load decision is
+    a MIN all-reduce over the TP group (model_runner.capture_graphs -> comm.tp_all_true)."""
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROOT=ROOT)
+        procs.append(subprocess.Popen([sys.executable, "-c", AGREE_CHILD], env=env, cwd=ROOT,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
+    for o in outs:
+        line = [l for l in o[0].splitlines() if l.startswith("RESULT")][0]
+        assert line.split()[1:] == ["0", "1"], line
+
+
+def test_ep_dispatch_bytes_bounded():
+    """The fixed-capacity EP dispatch moves at most 2x the exact T*K*d rows per all-to-all at
+    decode sizes (a per-peer capacity of T*K moved ep x the exact traffic)."""
+    import torch
+
+    from aws_k8s_ansible_provisioner_amd.models.config import get_config
+    from aws_k8s_ansible_provisioner_amd.models.moe import MoEBlock
+    from aws_k8s_ansible_provisioner_amd.parallel.state import ParallelState
+
+    cfg = get_config("tiny-mixtral8")
+    for ep in (2, 4, 8):
+        ps = ParallelState(rank=0, world_size=ep, tp_size=ep)
+        blk = MoEBlock(cfg, ps, "cpu", torch.bfloat16, torch.Generator().manual_seed(0),
+                       full_then_shard=False, mode="ep")
+        for T in (64, 128, 256, 512):
+            exact = T * cfg.experts_per_token
+            assert blk.a2a_rows(T) <= 2 * exact, (ep, T, blk.a2a_rows(T), exact)
+        # one-token steps: capacity covers every pair (no overflow possible)
+        assert blk.ep_capacity(cfg.experts_per_token) == cfg.experts_per_token
