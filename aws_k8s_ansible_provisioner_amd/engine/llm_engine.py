@@ -108,9 +108,15 @@ class LLMEngine:
         self.rank = self.runner.ps.rank
         self._inflight = None  # (info, handle) of a launched lookahead decode step
         self.lookahead_steps = 0
-        self._async_decode = (ecfg.async_decode and self.runner.is_gpu and
-                              bool(self.runner.graphs) and self.runner.ps.world_size == 1 and
-                              os.environ.get("AKAP_ASYNC_DECODE", "1") != "0")
+        # decode lookahead: single GPU, DP replicas and TP groups (rank 0 broadcasts the
+        # lookahead step's header like any other; parallel/tp_worker); not with expert-
+        # parallel MoE (an overflowed dispatch re-runs its step, which a queued successor
+        # would already have consumed).  AKAP_ASYNC_DECODE=force: also without hipGraphs
+        # (CPU protocol tests; the step then runs eagerly inside launch_decode)
+        mode = os.environ.get("AKAP_ASYNC_DECODE", "1")
+        self._async_decode = (ecfg.async_decode and mode != "0" and
+                              ((self.runner.is_gpu and bool(self.runner.graphs))
+                               or mode == "force") and not self.runner._ep_moe)
         if ecfg.gc_freeze and os.environ.get("AKAP_GC_FREEZE", "1") != "0":
             # Move everything alive after start-up (model, graphs, torch/extension objects)
             # into the permanent generation: the serving loop allocates ~10^5 small objects
@@ -299,7 +305,8 @@ class LLMEngine:
                 if self._n_extra:
                     info["extras"], sample_pos = self._step_extras(info)
                 if (self._async_decode and not info["is_prefill"] and "extras" not in info
-                        and info["num_seqs"] <= self.runner.buckets[-1]):
+                        and (not self.runner.buckets
+                             or info["num_seqs"] <= self.runner.buckets[-1])):
                     handle = self.runner.launch_decode(info)
                     self._inflight = self._try_lookahead()
                     toks = self.runner.wait_decode(handle)
@@ -481,6 +488,8 @@ class LLMEngine:
         agent = self.kv_agent
         if agent is not None:
             m.kv_xfer_fail.set_total(agent.failures, model_name=name)
+            m.kv_broken.set(1.0 if agent.broken else 0.0, model_name=name)
+            m.kv_resets.set_total(agent.resets, model_name=name)
             m.kv_xfer_bytes.set_total(agent.bytes_sent, model_name=name, direction="send")
             m.kv_xfer_bytes.set_total(agent.bytes_recv, model_name=name, direction="recv")
 

@@ -86,6 +86,8 @@ class ModelRunner:
         # workspace sized for the finest split any bucket uses (256-token partitions)
         self.num_parts = max(1, math.ceil(ecfg.max_model_len / 128))
         self._alloc_buffers()
+        self._hpre: Optional[torch.Tensor] = None  # prefill staging (pinned) + device mirror
+        self._dpre: Optional[torch.Tensor] = None
         self.last_logprobs: Optional[np.ndarray] = None
         # top-N alternatives of the last step's sampled rows: (token ids [n, N], log-probs)
         self.last_top: Optional[tuple] = None
@@ -219,25 +221,64 @@ class ModelRunner:
                           out_tokens=self.out_tokens[:n], out_logprobs=self.out_logprobs[:n],
                           greedy_logprobs=lp)
 
+    PREFILL_FIELDS = ("input_ids", "positions", "slots", "seq_lens", "q_start", "block_tables",
+                      "tile_seq", "tile_row", "logits_idx", "temperature", "top_p", "top_k",
+                      "seeds", "steps")
+
+    def _prefill_extents(self, info: dict) -> dict:
+        T, B, nt, ns = info["num_tokens"], info["num_seqs"], info["num_tiles"], info["num_samples"]
+        return {"input_ids": T, "positions": T, "slots": T, "seq_lens": B, "q_start": B + 1,
+                "block_tables": B * self.max_blocks, "tile_seq": nt, "tile_row": nt,
+                "logits_idx": ns, "temperature": ns, "top_p": ns, "top_k": ns, "seeds": ns,
+                "steps": ns}
+
+    def _stage_prefill(self, info: dict) -> dict:
+        """The used prefix of every step buffer packed into ONE pinned region -> ONE H2D copy
+        (instead of 14 small copies, each a blit kernel + host launch); under TP that one
+        device region is then RCCL-broadcast from the group's rank 0 (over xGMI), so the
+        other ranks never receive prefill payloads over the host control channel.  Returns
+        device views per field."""
+        ext = self._prefill_extents(info)
+        lay, off = {}, 0
+        for k in self.PREFILL_FIELDS:
+            nb = ext[k] * self.h[k].element_size()
+            lay[k] = (off, ext[k])
+            off += -(-nb // 16) * 16
+        end = off
+        if self._hpre is None or self._hpre.numel() < end:
+            cap = max(end, 1 << 16)
+            self._hpre = self._pinned(cap, torch.uint8)
+            self._dpre = torch.zeros(cap, dtype=torch.uint8, device=self.device)
+        tp = self._tp_bcast_inputs
+        if not (tp and self.ps.tp_rank != 0):
+            hb = self._hpre.numpy()
+            for k in self.PREFILL_FIELDS:
+                o, n = lay[k]
+                if n:
+                    src = self.np[k][:n].view(np.uint8)
+                    hb[o:o + src.size] = src
+            self._dpre[:end].copy_(self._hpre[:end], non_blocking=True)
+        if tp:
+            import torch.distributed as dist
+
+            dist.broadcast(self._dpre[:end], src=self.ps.rank - self.ps.tp_rank,
+                           group=self.ps.tp_group)
+        return {k: self._dpre[o:o + n * self.h[k].element_size()].view(self.h[k].dtype)
+                for k, (o, n) in lay.items()}
+
     def execute_prefill(self, info: dict) -> torch.Tensor:
         """A step with prefill chunks; under mixed batching its leading `num_decode` rows are
         running sequences' decode tokens (eager, same forward)."""
         T, B, nt, ns = info["num_tokens"], info["num_seqs"], info["num_tiles"], info["num_samples"]
         mb = self.max_blocks
-        ids = self._h2d("input_ids", T)
-        pos = self._h2d("positions", T)
-        slots = self._h2d("slots", T)
-        sl = self._h2d("seq_lens", B)
-        qs = self._h2d("q_start", B + 1)
-        self._h2d("block_tables", B * mb)
-        ts = self._h2d("tile_seq", nt)
-        tr = self._h2d("tile_row", nt)
-        lidx = self._h2d("logits_idx", ns)
-        for k in ("temperature", "top_p", "top_k", "seeds", "steps"):
-            self._h2d(k, ns)
+        v = self._stage_prefill(info)
+        ids, pos, slots = v["input_ids"], v["positions"], v["slots"]
+        sl, qs, ts, tr, lidx = v["seq_lens"], v["q_start"], v["tile_seq"], v["tile_row"], \
+            v["logits_idx"]
+        bt = v["block_tables"].view(B, mb)
         nd = info.get("num_decode", 0)
         parts, ps = self.decode_partitions(nd) if nd else (1, 512)
-        batch = AttnBatch(True, pos, slots, self.d_bt[:B], sl, qs, ts, tr, parts, ps,
+        batch = AttnBatch(True, pos, slots, bt, sl, qs, ts, tr, parts, ps,
                           self.workspace, tile_rows=self.tile_rows, num_decode=nd)
         h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
         if ns == 0:
@@ -252,7 +293,7 @@ class ModelRunner:
         logits = self.model.compute_logits(h.index_select(0, lidx))
         if not self.is_gpu:
             logits = logits.float()  # the GPU sampler reads bf16 logits directly
-        toks, _ = self._sample(logits, ns, info.get("extras"))
+        toks, _ = self._sample(logits, ns, info.get("extras"), src=v)
         return toks
 
     def decode_partitions(self, n: int) -> tuple[int, int]:
@@ -354,14 +395,17 @@ class ModelRunner:
         """Queue a graph-replayed decode step without waiting for it.  chained: the step was
         built by Scheduler.schedule_lookahead while the previous decode step is still
         queued -- its input ids are gathered on the device from that step's sampled tokens
-        (out_tokens[src_rows]) before the replay.  Returns a handle for wait_decode()."""
+        (out_tokens[src_rows]) before the replay (under TP only rank 0 gathers: the replay's
+        first op broadcasts rank 0's staging region, gathered ids included, to the group).
+        Returns a handle for wait_decode().  Without graphs (CPU) the step runs eagerly and
+        the handle holds its tokens (same protocol, no overlap)."""
         B = info["num_seqs"]
         n, graph = B, None
         for b in self.buckets:
             if b >= B:
                 n, graph = b, self.graphs[b]
                 break
-        if graph is None:
+        if graph is None and self.is_gpu:
             raise RuntimeError(f"no decode graph holds {B} rows")
         self._pad_host(B, n)
         with profiling.phase("akap.decode"):
@@ -369,17 +413,39 @@ class ModelRunner:
             if chained:
                 torch.index_select(self.out_tokens[:self.max_seqs], 0, self.dd["src_rows"][:n],
                                    out=self.dd["input_ids"][:n])
-            graph.replay()
+            if graph is not None:
+                graph.replay()
+            else:
+                self._decode_body(n)
+        if not self.is_gpu:
+            return None, self.out_tokens[:B].clone()
         host = self.tok_host[slot][:B]
         host.copy_(self.out_tokens[:B], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ev, host
 
+    def replay_decode(self, info: dict) -> None:
+        """TP follower ranks: the decode step's graph replay alone -- inputs arrive by the
+        in-graph broadcast of rank 0's staging region, nobody on this rank needs the tokens,
+        so nothing is staged and the host does not wait (the next header finds the GPU
+        still busy with this step, not idle behind a host round trip)."""
+        B = info["num_seqs"]
+        n, graph = B, None
+        for b in self.buckets:
+            if b >= B:
+                n, graph = b, self.graphs[b]
+                break
+        if graph is not None:
+            graph.replay()
+        else:
+            self._decode_body(n)
+
     @staticmethod
     def wait_decode(handle) -> np.ndarray:
         ev, host = handle
-        ev.synchronize()
+        if ev is not None:
+            ev.synchronize()
         return host.numpy()
 
     def execute(self, info: dict) -> np.ndarray:

@@ -40,6 +40,7 @@ class Endpoint:
     last_scrape: float = 0.0
     failures: int = 0
     served: int = 0
+    kv_broken: bool = False  # P/D: its KV-transfer channel awaits a rebuild
 
     def load_score(self) -> float:
         return 1.0 / (1.0 + self.waiting + 0.25 * self.running + self.inflight)
@@ -121,11 +122,13 @@ class EndpointPicker:
     def endpoints(self) -> list[Endpoint]:
         return list(self.eps.values())
 
-    def update_metrics(self, url: str, running: float, waiting: float, kv: float) -> None:
+    def update_metrics(self, url: str, running: float, waiting: float, kv: float,
+                       kv_broken: bool = False) -> None:
         e = self.eps.get(url)
         if e is None:
             return
         e.running, e.waiting, e.kv_usage = running, waiting, kv
+        e.kv_broken = kv_broken
         e.last_scrape = time.time()
         e.healthy = True
         e.failures = 0
@@ -186,8 +189,8 @@ class EndpointPicker:
                 best, best_s = None, -1e30
                 for p in pre:
                     for d in dec:
-                        if p.group != d.group:
-                            continue
+                        if p.group != d.group or p.kv_broken or d.kv_broken:
+                            continue  # other transfer group, or a channel being rebuilt
                         s = self.score(p, match, len(hs)) + self.score(d, {}, 0)
                         if s > best_s + 1e-9 or (abs(s - best_s) <= 1e-9 and
                                                  self.rng.random() < 0.5):

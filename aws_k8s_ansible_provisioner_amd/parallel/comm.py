@@ -50,23 +50,39 @@ def tp_all_reduce_resnorm(partial: torch.Tensor, residual: torch.Tensor, ln: tor
     ss[: r.shape[0]] += r.float().pow(2).sum(-1)
 
 
+_GATHER_WS: dict = {}
+_GATHER_OLD: list = []  # outgrown workspaces stay alive: captured hipGraphs may address them
+
+
+def _gather_ws(key: str, rows: int, cols: int, dtype, device) -> torch.Tensor:
+    """Persistent gather workspace (grown, never shrunk): the per-step logits gather reuses
+    one allocation instead of asking the allocator for [tp*B, V/tp] + [B, V] every step."""
+    k = (key, cols, dtype, str(device))
+    buf = _GATHER_WS.get(k)
+    if buf is None or buf.shape[0] < rows:
+        if buf is not None:
+            _GATHER_OLD.append(buf)
+        buf = torch.empty(rows, cols, dtype=dtype, device=device)
+        _GATHER_WS[k] = buf
+    return buf[:rows]
+
+
 def tp_all_gather_last(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gather shards along the last dim: [.., n] x tp -> [.., n*tp].  One all_gather into a
-    single [tp, .., n] buffer (no per-rank tensor list) + one transposing copy."""
+    single preallocated [tp, .., n] buffer (no per-rank tensor list) + one transposing copy
+    into a preallocated result (or `out`)."""
     st = get_state()
     if st.tp_size == 1:
         return x
     x = x.contiguous()
     flat = x.reshape(1, -1) if x.dim() == 1 else x.reshape(-1, x.shape[-1])
-    buf = torch.empty(st.tp_size * flat.shape[0], flat.shape[1], dtype=x.dtype,
-                      device=x.device)
+    R, n = flat.shape
+    buf = _gather_ws("gather", st.tp_size * R, n, x.dtype, x.device)
     dist.all_gather_into_tensor(buf, flat, group=st.tp_group)  # rank-major rows
-    res = buf.view(st.tp_size, flat.shape[0], flat.shape[1]).movedim(0, 1).reshape(
-        *x.shape[:-1], st.tp_size * x.shape[-1])
-    if out is not None:
-        out.copy_(res)
-        return out
-    return res
+    if out is None:
+        out = _gather_ws("result", R, st.tp_size * n, x.dtype, x.device)
+    out.view(R, st.tp_size, n).copy_(buf.view(st.tp_size, R, n).transpose(0, 1))
+    return out.view(*x.shape[:-1], st.tp_size * n)
 
 
 def all_to_all(x: torch.Tensor, out_splits: list[int], in_splits: list[int], group=None

@@ -16,9 +16,13 @@ Failure handling (a peer that dies or never posts its half must not hang the oth
 every send/recv is posted asynchronously (isend/irecv) and waited with a deadline
 (`timeout_s`, default AKAP_KV_TIMEOUT_S = 60).  On expiry the transfer raises
 KVTransferTimeout and the agent is marked broken: an un-matched P2P op may still be posted in
-the communicator, so later transfers on this channel fail fast (the engines keep serving;
-the gateway falls back to monolithic serving) instead of pairing with stale ops.  A send's
-`on_done` (the prefill side's free_held) runs whether the send succeeded or not.
+the communicator, so later transfers on this channel fail fast instead of pairing with stale
+ops.  A broken channel is REBUILT, not abandoned: `reset(generation)` -- called on both sides,
+coordinated over HTTP (the decode side POSTs /kv/reset to the prefill server and resets its
+own agent at the same time) -- creates a fresh process group over the same ranks (a new RCCL
+communicator; the stale ops stay behind in the old one) and clears the broken state.
+Generations are monotonic, so a repeated or crossed reset request is a no-op.  A send's
+`on_done` (the prefill side's finish_transfer) runs whether the send succeeded or not.
 
 Control plane: the decode side asks the prefill server (HTTP POST /kv/push) to send the
 blocks of one or more transfer ids to its rank, then posts the matching recv.  The same
@@ -94,6 +98,8 @@ class KVTransferAgent:
         self.transfers = 0
         self.failures = 0
         self.broken: Optional[str] = None
+        self.generation = 0  # bumped by every rebuild of the transfer group
+        self.resets = 0
         # gloo moves host tensors only: GPU caches on a gloo group (single-GPU rehearsal of
         # the P/D path) stage through pinned host memory
         self.gloo = dist.is_initialized() and dist.get_backend(group) == "gloo"
@@ -210,6 +216,28 @@ class KVTransferAgent:
             except Exception as e:
                 self._fail(e)
                 raise
+
+        return self._submit(fn, True)
+
+    def reset(self, generation: int, timeout_s: float = 120.0) -> bool:
+        """Rebuild the transfer channel as a NEW process group over the same ranks (every rank
+        of the default group must call this with the same generation: P/D pods are 2-rank
+        jobs).  Runs on the agent thread, after any queued transfer (which fails fast while
+        broken).  Returns True if this call moved the channel to `generation`."""
+
+        def fn():
+            if generation <= self.generation:
+                return False
+            ranks = list(range(dist.get_world_size()))
+            backend = dist.get_backend(self.group)
+            self.group = dist.new_group(ranks=ranks, backend=backend,
+                                        timeout=datetime.timedelta(seconds=timeout_s))
+            self.gloo = backend == "gloo"
+            self.host_staging = self.is_gpu and self.gloo
+            self.generation = generation
+            self.broken = None
+            self.resets += 1
+            return True
 
         return self._submit(fn, True)
 

@@ -2,11 +2,13 @@
 
 Rank 0 of the group owns the C++ scheduler, the HTTP server and the request state; every
 rank owns its weight shard, its KV-cache shard (its kv heads) and its hipGraphs.  Each
-engine step, rank 0 broadcasts the step header (StepInfo, 9 int64) over a gloo control
-group -- ONE host broadcast per decode step: the decode inputs themselves travel as one
-RCCL broadcast of rank 0's device staging region at the head of the decode step (inside the
-hipGraph, ModelRunner._decode_body).  Prefill steps also send the used prefix of the pinned
-batch buffers (~KBs) as a second gloo broadcast, sized by the header.  The
+engine step, rank 0 broadcasts the step header (StepInfo + a launch mode, 9 int64) over a
+gloo control group -- ONE host broadcast per step: the step inputs themselves travel as one
+RCCL broadcast of rank 0's device staging region (decode: at the head of the step, inside
+the hipGraph, ModelRunner._decode_body; prefill: ModelRunner._stage_prefill's packed region).
+Decode lookahead works across the group: rank 0 broadcasts a lookahead step's header as it
+launches it (mode LAUNCH / CHAINED) and followers replay without waiting on the host
+(ModelRunner.replay_decode), so every rank's GPU queue holds the next step.  The
 forward's all-reduces (O-proj, down-proj) and the vocab-parallel logits all-gather run on
 RCCL over xGMI (and are captured inside the decode hipGraphs).  Every rank sees the full
 logits and runs the same seeded sampler, so all ranks produce identical tokens without
@@ -26,31 +28,15 @@ from ..engine.model_runner import ModelRunner
 from ..models.config import get_config
 from .state import ParallelState, init_distributed
 
-_STEP_KEYS = ["input_ids", "positions", "slots", "seq_lens", "q_start", "block_tables",
-              "tile_seq", "tile_row", "logits_idx", "temperature", "top_p", "top_k", "seeds",
-              "steps"]
 _INFO_KEYS = ["is_prefill", "num_seqs", "num_tokens", "num_tiles", "num_samples",
               "max_seq_len", "num_preempted", "num_decode"]
-# header = info + payload bytes (0 for decode steps: inputs go by the in-graph broadcast)
+# header = info + launch mode
+EXECUTE, LAUNCH, CHAINED = 0, 1, 2
 STOP = -1
 
 
-def _extent(key: str, info: dict, runner: ModelRunner) -> int:
-    B, T, S = info["num_seqs"], info["num_tokens"], info["num_samples"]
-    if not info["is_prefill"]:
-        B = T = S = max(B, 1)
-        for b in runner.buckets:  # decode replays pad rows up to the bucket
-            if b >= info["num_seqs"]:
-                B = T = S = b
-                break
-    return {"input_ids": T, "positions": T, "slots": T, "seq_lens": B, "q_start": B + 1,
-            "block_tables": B * runner.max_blocks, "tile_seq": info["num_tiles"],
-            "tile_row": info["num_tiles"], "logits_idx": S, "temperature": S, "top_p": S,
-            "top_k": S, "seeds": S, "steps": S}[key]
-
-
 class TPStepBroadcaster:
-    """Wraps rank 0's runner: broadcast the step, then execute it locally."""
+    """Wraps rank 0's runner: broadcast the step header, then run the step locally."""
 
     def __init__(self, runner: ModelRunner, ctrl_group):
         self.runner = runner
@@ -59,19 +45,17 @@ class TPStepBroadcaster:
     def __getattr__(self, name):
         return getattr(self.runner, name)
 
-    def execute(self, info: dict) -> np.ndarray:
-        r = self.runner
-        payload = None
-        if info["is_prefill"]:
-            parts = [torch.from_numpy(r.np[k][:_extent(k, info, r)].view(np.uint8).copy())
-                     for k in _STEP_KEYS]
-            payload = torch.cat(parts)
-        head = torch.tensor([info[k] for k in _INFO_KEYS] +
-                            [0 if payload is None else payload.numel()], dtype=torch.int64)
+    def _header(self, info: dict, mode: int) -> None:
+        head = torch.tensor([info[k] for k in _INFO_KEYS] + [mode], dtype=torch.int64)
         dist.broadcast(head, 0, group=self.ctrl)
-        if payload is not None:
-            dist.broadcast(payload, 0, group=self.ctrl)
-        return r.execute(info)
+
+    def execute(self, info: dict) -> np.ndarray:
+        self._header(info, EXECUTE)
+        return self.runner.execute(info)
+
+    def launch_decode(self, info: dict, chained: bool = False):
+        self._header(info, CHAINED if chained else LAUNCH)
+        return self.runner.launch_decode(info, chained=chained)
 
     def shutdown(self) -> None:
         head = torch.full((len(_INFO_KEYS) + 1,), STOP, dtype=torch.int64)
@@ -81,7 +65,9 @@ class TPStepBroadcaster:
 
 
 def worker_loop(runner: ModelRunner, ctrl_group) -> None:
-    """Ranks != 0: mirror every step rank 0 broadcasts until STOP."""
+    """Ranks != 0: mirror every step rank 0 broadcasts until STOP.  Decode steps replay
+    without a host wait (their tokens are rank 0's business) unless an expert-parallel
+    dispatch may need the step re-run (runner.execute checks the overflow flag)."""
     while True:
         head = torch.zeros(len(_INFO_KEYS) + 1, dtype=torch.int64)
         dist.broadcast(head, 0, group=ctrl_group)
@@ -89,17 +75,10 @@ def worker_loop(runner: ModelRunner, ctrl_group) -> None:
             return
         vals = head.tolist()
         info = {k: int(v) for k, v in zip(_INFO_KEYS, vals)}
-        if vals[-1]:
-            payload = torch.empty(int(vals[-1]), dtype=torch.uint8)
-            dist.broadcast(payload, 0, group=ctrl_group)
-            off = 0
-            for k in _STEP_KEYS:
-                cnt = _extent(k, info, runner)
-                arr = runner.np[k]
-                nbytes = cnt * arr.itemsize
-                arr[:cnt] = payload[off:off + nbytes].numpy().view(arr.dtype)
-                off += nbytes
-        runner.execute(info)
+        if not info["is_prefill"] and not runner._ep_moe:
+            runner.replay_decode(info)
+        else:
+            runner.execute(info)
 
 
 def build_tp(ecfg: EngineConfig, backend: Optional[str] = None, log=print):

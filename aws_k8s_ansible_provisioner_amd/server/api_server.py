@@ -114,6 +114,7 @@ class OpenAIServer:
         self.template = chat_template.load_template(chat_tmpl)
         self.max_model_len = max_model_len
         self.created = int(time.time())
+        self._dropped_push = False  # fault injection (AKAP_FAULT_KV_PUSH=drop_once)
         self.app = self._build()
 
     # ------------------------------------------------------------------ helpers
@@ -166,7 +167,13 @@ class OpenAIServer:
         async def health():
             if not self.ae.healthy:
                 return _err(503, "engine dead", "ServiceUnavailable")
-            return {"status": "ok"}
+            ag = self.ae.kv_agent
+            if ag is None:
+                return {"status": "ok"}
+            # P/D: a broken KV channel is rebuilt by the decode side (/kv/reset); until then
+            # the gateway's picker keeps this pair out of P/D routing
+            return {"status": "ok", "kv_channel": "broken" if ag.broken else "ok",
+                    "kv_generation": ag.generation}
 
         @app.get("/ready")
         async def ready():
@@ -216,6 +223,10 @@ class OpenAIServer:
             if grp is not None and self.ae.pd_group is not None and grp != self.ae.pd_group:
                 return _err(409, f"P/D group mismatch: decode {grp} vs prefill "
                                  f"{self.ae.pd_group}", "Conflict")
+            if self.ae.kv_agent.broken is not None:
+                # the decode side rebuilds the channel (/kv/reset) and retries later requests
+                return _err(503, f"KV channel broken: {self.ae.kv_agent.broken}",
+                            "KVChannelBroken")
             tids = [int(t) for t in (body.get("transfer_ids") or [body["transfer_id"]])]
             per = [eng.held_blocks(t) for t in tids]
             missing = [t for t, b in zip(tids, per) if not b]
@@ -229,7 +240,9 @@ class OpenAIServer:
                     eng.finish_transfer(t)
                 return _err(404, f"held KV for transfer(s) {tids} expired")
             blocks = [b for bl in per for b in bl]
-            if os.environ.get("AKAP_FAULT_KV_PUSH") == "drop":
+            fault = os.environ.get("AKAP_FAULT_KV_PUSH")
+            if fault == "drop" or (fault == "drop_once" and not self._dropped_push):
+                self._dropped_push = True
                 # fault injection (tests): acknowledge the push, then "die" before sending --
                 # the decode side's bounded recv must fail the request, not hang
                 for t in tids:
@@ -244,6 +257,23 @@ class OpenAIServer:
             self.ae.kv_agent.send_blocks(blocks, int(body["dst_rank"]), on_done=done)
             nb = [len(b) for b in per]
             return {"ok": True, "num_blocks": nb if "transfer_ids" in body else nb[0]}
+
+        @app.post("/kv/reset")
+        async def kv_reset(req: Request):
+            """P/D: rebuild the KV-transfer channel (a fresh process group over the same ranks)
+            at the given generation.  The decode side calls this while resetting its own
+            agent; both calls return once the new group is formed."""
+            body = await req.json()
+            if self.ae.kv_agent is None:
+                return _err(400, "not a P/D server")
+            gen = int(body["generation"])
+            try:
+                moved = await asyncio.get_running_loop().run_in_executor(
+                    None, self.ae.kv_agent.reset, gen)
+            except Exception as e:  # rendezvous timed out: the channel stays broken
+                return _err(503, f"KV channel reset to generation {gen} failed: {e}",
+                            "ServiceUnavailable")
+            return {"ok": True, "generation": self.ae.kv_agent.generation, "moved": moved}
 
         @app.post("/kv/release")
         async def kv_release(req: Request):

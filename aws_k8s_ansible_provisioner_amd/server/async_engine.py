@@ -124,12 +124,25 @@ class KVPuller:
                 eng.abort_request(j.req_id)  # frees the reserved decode blocks
                 AsyncEngine._release_remote(j.kvp)
                 self._resolve(j, e)
+            agent = self.ae.kv_agent
+            if agent.broken is not None or "KVChannelBroken" in _http_error_text(e):
+                # a timed-out transfer left stale ops in the channel (ours or the prefill
+                # side's): rebuild it on both sides so the NEXT request on this pair works
+                self.ae.rebuild_channel(url)
             return
         self.batches += 1
         for j, (iid, _) in zip(ready, reserved):
             eng.activate(iid)
             self._resolve(j, None)
         self.ae._wake.set()
+
+
+def _http_error_text(e: BaseException) -> str:
+    """Body of an urllib HTTPError (the server's JSON error), else the exception text."""
+    try:
+        return e.read().decode()  # type: ignore[attr-defined]
+    except Exception:
+        return str(e)
 
 
 class AsyncEngine:
@@ -256,6 +269,36 @@ class AsyncEngine:
             self.queues[req_id].put_nowait(RequestOutput(req_id, prompt_ids, [first], [first],
                                                          t, t, False, None))
         return None
+
+    def rebuild_channel(self, url: str, timeout_s: float = 120.0) -> bool:
+        """Decode side: move both ends of the KV channel to a fresh process group (the next
+        generation).  The prefill server joins through POST /kv/reset while this process's
+        agent joins here; both block in the group rendezvous until the other arrives."""
+        agent = self.kv_agent
+        gen = agent.generation + 1
+        res: dict = {}
+
+        def remote():
+            try:
+                body = json.dumps({"generation": gen}).encode()
+                req = urllib.request.Request(url.rstrip("/") + "/kv/reset", data=body,
+                                             headers={"Content-Type": "application/json"})
+                with urllib.request.urlopen(req, timeout=timeout_s) as r:
+                    res["remote"] = json.loads(r.read())
+            except Exception as e:
+                res["error"] = e
+
+        th = threading.Thread(target=remote, name="kv-reset", daemon=True)
+        th.start()
+        try:
+            agent.reset(gen, timeout_s=timeout_s)
+        except Exception as e:
+            print(f"[pd] KV channel reset to generation {gen} failed: {e}", flush=True)
+            return False
+        th.join(timeout_s)
+        ok = agent.generation == gen and "error" not in res
+        print(f"[pd] KV channel rebuilt: generation {gen} ({'ok' if ok else res})", flush=True)
+        return ok
 
     @staticmethod
     def _release_remote(kvp: dict) -> None:

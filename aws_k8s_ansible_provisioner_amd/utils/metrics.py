@@ -179,6 +179,10 @@ class EngineMetrics:
                                              "Held KV freed by the TTL (never pulled)", L))
         self.kv_xfer_fail = r.add(Counter("akap:kv_transfer_failures_total",
                                           "KV sends/receives that failed or timed out", L))
+        self.kv_broken = r.add(Gauge("akap:kv_channel_broken",
+                                     "1 while the KV-transfer channel awaits a rebuild", L))
+        self.kv_resets = r.add(Counter("akap:kv_channel_resets_total",
+                                       "KV-transfer channel rebuilds (new process group)", L))
         self.kv_xfer_bytes = r.add(Counter("akap:kv_transfer_bytes_total",
                                            "KV bytes moved over the transfer group",
                                            ("model_name", "direction")))

@@ -314,7 +314,7 @@ def test_two_pd_pairs_behind_one_gateway_never_cross_pair():
 def test_pd_sender_dies_after_push_ack_fails_fast_and_frees_blocks():
     """The prefill acks /kv/push and never sends: the decode's bounded recv times out, the
     request is served monolithically by the gateway's fallback, the decode engine frees the
-    reserved blocks, stays healthy, and its broken channel fails later pulls fast."""
+    reserved blocks and stays healthy; later pulls stay bounded."""
     procs, (pre_url, dec_url) = _spawn_pair(extra_env={"AKAP_FAULT_KV_PUSH": "drop"},
                                             decode_env={"AKAP_KV_TIMEOUT_S": "2"})
     try:
@@ -328,9 +328,55 @@ def test_pd_sender_dies_after_push_ack_fails_fast_and_frees_blocks():
         assert urllib.request.urlopen(dec_url + "/health").status == 200
         assert _metric(dec_url, "vllm:gpu_cache_usage_perc") == 0.0
         assert _metric(dec_url, "akap:kv_transfer_failures_total") >= 1
-        # the channel is now marked broken: the next P/D attempt fails immediately
+        # every push is dropped: the rebuilt channel times out again, still bounded
         t1 = time.time()
         res, gw = asyncio.run(_gw_post([(pre_url, "prefill"), (dec_url, "decode")], [body]))
         assert res[0][0] == 200 and time.time() - t1 < 10
+    finally:
+        _kill(procs)
+
+
+def _health(url):
+    import json as _json
+
+    return _json.loads(urllib.request.urlopen(url + "/health").read())
+
+
+def test_pd_channel_rebuilt_after_a_timed_out_transfer():
+    """One transfer dies mid-way (the prefill acks the push, then never sends): the decode's
+    recv times out and leaves a stale op in the channel.  The decode side rebuilds the
+    channel on BOTH ends (POST /kv/reset -> a new process group, generation 1), and the NEXT
+    P/D request on the same pair runs disaggregated again -- no pod restart, no fallback."""
+    procs, (pre_url, dec_url) = _spawn_pair(extra_env={"AKAP_FAULT_KV_PUSH": "drop_once"},
+                                            decode_env={"AKAP_KV_TIMEOUT_S": "2"})
+    try:
+        body = {"prompt": "the first transfer dies " * 3, "max_tokens": 4, "temperature": 0,
+                "ignore_eos": True}
+        res, gw = asyncio.run(_gw_post([(pre_url, "prefill"), (dec_url, "decode")], [body]))
+        assert res[0][0] == 200 and gw.m_pd_fallback.value() == 1
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            if (_health(dec_url).get("kv_generation") == 1
+                    and _health(pre_url).get("kv_generation") == 1):
+                break
+            time.sleep(0.2)
+        for u in (pre_url, dec_url):
+            h = _health(u)
+            assert h["kv_generation"] == 1 and h["kv_channel"] == "ok", (u, h)
+            assert _metric(u, "akap:kv_channel_resets_total") == 1.0
+            assert _metric(u, "akap:kv_channel_broken") == 0.0
+        def recv_bytes():
+            for ln in urllib.request.urlopen(dec_url + "/metrics").read().decode().splitlines():
+                if ln.startswith("akap:kv_transfer_bytes_total{") and 'direction="recv"' in ln:
+                    return float(ln.rsplit(" ", 1)[1])
+            return 0.0
+
+        recv0 = recv_bytes()
+        body2 = dict(body, prompt="the next request on the same pair " * 3)
+        res, gw = asyncio.run(_gw_post([(pre_url, "prefill"), (dec_url, "decode")], [body2]))
+        assert res[0][0] == 200 and res[0][1]["usage"]["completion_tokens"] == 4
+        assert gw.m_pd.value() == 1 and gw.m_pd_fallback.value() == 0
+        assert recv_bytes() > recv0
+        assert _metric(dec_url, "vllm:gpu_cache_usage_perc") == 0.0
     finally:
         _kill(procs)

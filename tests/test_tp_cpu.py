@@ -141,11 +141,10 @@ def test_tp2_fused_decode_chain_matches_unfused(model):
     assert res["err"] <= 3e-2 * res["scale"] + 3e-2, res
 
 
-def test_tp_decode_step_is_one_host_broadcast(monkeypatch):
-    """Rank 0 sends a decode step to the other TP ranks with ONE gloo broadcast (the header);
-    the inputs go by the in-graph RCCL broadcast of the staging region.  Prefill steps add
-    one payload broadcast sized by the header."""
-    import numpy as np
+def test_tp_step_is_one_host_broadcast(monkeypatch):
+    """Rank 0 sends every step to the other TP ranks with ONE gloo broadcast (the header): the
+    inputs go by RCCL broadcasts of rank 0's device staging regions (the decode graph's first
+    op; ModelRunner._stage_prefill for prefill steps).  Lookahead launches carry their mode."""
     import torch.distributed as dist
 
     from aws_k8s_ansible_provisioner_amd.parallel import tp_worker
@@ -155,21 +154,73 @@ def test_tp_decode_step_is_one_host_broadcast(monkeypatch):
 
     class FakeRunner:
         buckets = [1, 2, 4]
-        max_blocks = 2
-        np = {k: np.zeros(64, np.int64) for k in tp_worker._STEP_KEYS}
 
         def execute(self, info):
             return "ran"
+
+        def launch_decode(self, info, chained=False):
+            return ("launched", chained)
 
     bc = tp_worker.TPStepBroadcaster(FakeRunner(), ctrl_group=None)
     dec = {"is_prefill": 0, "num_seqs": 3, "num_tokens": 3, "num_tiles": 0,
            "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3}
     assert bc.execute(dec) == "ran"
-    assert len(sent) == 1 and sent[0].tolist()[-1] == 0
+    assert len(sent) == 1 and sent[0].tolist()[-1] == tp_worker.EXECUTE
     sent.clear()
     pre = dict(dec, is_prefill=1, num_tokens=20, num_tiles=2, num_decode=0)
     bc.execute(pre)
-    assert len(sent) == 2 and sent[0].tolist()[-1] == sent[1].numel() > 0
+    assert len(sent) == 1 and sent[0].tolist()[0] == 1
+    sent.clear()
+    assert bc.launch_decode(dec, chained=True) == ("launched", True)
+    assert len(sent) == 1 and sent[0].tolist()[-1] == tp_worker.CHAINED
+
+
+LOOKAHEAD_CHILD = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["ROOT"])
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
+ecfg = EngineConfig(model="tiny-llama", device="cpu", max_model_len=256, max_num_seqs=8,
+                    max_num_batched_tokens=64, block_size=32, num_gpu_blocks=96,
+                    tensor_parallel_size=2, shard_init="full", init_std=0.15)
+eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
+if eng is not None:
+    prompts = [list(range(5, 40)), [100, 101], [9, 9, 9], list(range(300, 310))]
+    params = [SamplingParams(max_tokens=m, temperature=0, ignore_eos=True) for m in (5, 9, 14)]
+    params.append(SamplingParams(max_tokens=12, temperature=0.8, top_p=0.9, seed=3,
+                                 ignore_eos=True))
+    names = [eng.add_request(None, None, p, prompt_ids=q) for q, p in zip(prompts, params)]
+    final = {}
+    while eng.has_unfinished():
+        for o in eng.step():
+            if o.finished:
+                final[o.req_id] = o.output_ids
+    bc.shutdown()
+    print("RESULT " + json.dumps({"out": [final[n] for n in names],
+                                  "lookahead": eng.lookahead_steps}), flush=True)
+"""
+
+
+def test_tp2_lookahead_matches_synchronous():
+    """Decode lookahead on a TP group (gloo): rank 0 broadcasts each lookahead step's header
+    as it launches it, followers replay it; the token streams equal the synchronous loop's."""
+    res = {}
+    for mode in ("0", "force"):
+        port = _port()
+        procs = []
+        for r in range(2):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROOT=ROOT,
+                       AKAP_ASYNC_DECODE=mode, OMP_NUM_THREADS="2")
+            procs.append(subprocess.Popen([sys.executable, "-c", LOOKAHEAD_CHILD], env=env,
+                                          cwd=ROOT, stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True))
+        outs = [p.communicate(timeout=300) for p in procs]
+        assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
+        line = [l for l in outs[0][0].splitlines() if l.startswith("RESULT ")][0]
+        res[mode] = json.loads(line[7:])
+    assert res["0"]["lookahead"] == 0 and res["force"]["lookahead"] > 0, res
+    assert res["force"]["out"] == res["0"]["out"]
 
 
 AGREE_CHILD = r"""
