@@ -171,6 +171,7 @@ PYBIND11_MODULE(_runtime, m) {
            py::arg("temperature") = 0.f, py::arg("top_p") = 1.f, py::arg("top_k") = 0,
            py::arg("seed") = 0, py::arg("stream") = false)
       .def("activate", &Scheduler::activate)
+      .def("set_first_token", &Scheduler::set_first_token)
       .def_property_readonly("total_preemptions", &Scheduler::total_preemptions)
       .def("request_info", [](const Scheduler& s, int64_t id) -> py::object {
         auto r = s.get(id);

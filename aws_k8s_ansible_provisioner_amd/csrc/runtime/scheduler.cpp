@@ -141,6 +141,12 @@ std::vector<int32_t> Scheduler::reserve_prefilled(
   return out;
 }
 
+void Scheduler::set_first_token(int64_t id, int32_t tok) {
+  auto it = reqs_.find(id);
+  if (it == reqs_.end() || it->second->status != PENDING_KV) return;
+  it->second->tokens.back() = tok;
+}
+
 void Scheduler::activate(int64_t id) {
   auto it = reqs_.find(id);
   if (it == reqs_.end() || it->second->status != PENDING_KV) return;

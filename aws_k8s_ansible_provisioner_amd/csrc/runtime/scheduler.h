@@ -171,6 +171,9 @@ class Scheduler {
                                          float temperature, float top_p, int top_k,
                                          int64_t seed, bool stream);
   void activate(int64_t id);
+  // P/D streamed hand-off: blocks are reserved (and filled chunk by chunk) before the prefill
+  // has sampled the first token; it is set here, before activate()
+  void set_first_token(int64_t id, int32_t tok);
   size_t num_held() const { return held_.size(); }
   // free every held-KV entry whose deadline passed (schedule() calls it with the steady
   // clock); returns the number expired

@@ -235,6 +235,28 @@ class LLMEngine:
             self.metrics.req_total.inc(model_name=self.model_name)
         return iid, list(blocks)
 
+    def set_first_token(self, iid: int, tok: int) -> None:
+        """P/D streamed hand-off: the first token of a request reserved before it existed."""
+        with self._lock:
+            self.sched.set_first_token(int(iid), int(tok))
+            st = self.reqs.get(int(iid))
+            if st is not None:
+                st.output_ids = [int(tok)]
+                st.text = self.tokenizer.decode_token(int(tok)) if st.stream else ""
+
+    def hold_kv_progress(self) -> list:
+        """P/D prefill side: (transfer id, block table, computed tokens) of every request
+        whose KV is being prefilled for a remote decode (for streaming finished blocks)."""
+        out = []
+        with self._lock:
+            for iid, st in self.reqs.items():
+                if st.hold_kv and not st.finished:
+                    info = self.sched.request_info(iid)
+                    if info is not None and info["status"] == 1:  # RUNNING
+                        out.append((iid, list(self.sched.block_table(iid)),
+                                    int(info["num_computed"])))
+        return out
+
     def activate(self, iid: int) -> None:
         with self._lock:
             self.sched.activate(int(iid))

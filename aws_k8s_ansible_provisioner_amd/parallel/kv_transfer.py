@@ -186,6 +186,52 @@ class KVTransferAgent:
 
         return self._submit(fn, wait)
 
+    def gather(self, block_ids: list[int]) -> tuple:
+        """Pack blocks NOW on the caller's (compute) stream: later kernels of that stream --
+        which may reuse the blocks -- are ordered after the copy, so the caller may free the
+        blocks as soon as this returns.  Returns (packed buffer, ready event) for send_packed."""
+        ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
+        buf = ops.kv_gather(self.planes, ids)
+        ev = None
+        if self.is_gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+        return buf, ev
+
+    def send_packed(self, packed: tuple, dst: int, on_done: Optional[Callable[[], None]] = None,
+                    wait: bool = False, timeout_s: Optional[float] = None):
+        """Send a buffer packed by gather() (async by default; bounded like send_blocks)."""
+        t_out = self.timeout_s if timeout_s is None else timeout_s
+        buf, ev = packed
+
+        def fn():
+            try:
+                self._check()
+                with self._ctx():
+                    b = buf
+                    if self.is_gpu:
+                        self.stream.wait_event(ev)
+                    if self.host_staging:
+                        self.stream.synchronize()
+                        b = buf.cpu()
+                    work = dist.isend(b, dst, group=self.group)
+                    _wait(work, t_out, f"KV send of {buf.shape[1]} blocks to rank {dst}",
+                          self.gloo)
+                    if self.is_gpu:
+                        self.stream.synchronize()
+                self.bytes_sent += buf.numel() * buf.element_size()
+                self.transfers += 1
+                return True
+            except Exception as e:
+                self._fail(e)
+                print(f"[kv-transfer] send to rank {dst} failed: {e}", flush=True)
+                raise
+            finally:
+                if on_done:
+                    on_done()
+
+        return self._submit(fn, wait)
+
     def recv_blocks(self, block_ids: list[int], src: int,
                     timeout_s: Optional[float] = None) -> None:
         """Receive packed KV from rank `src` into our `block_ids` (blocking, bounded)."""

@@ -127,7 +127,8 @@ prompts = [list(range(5, 5 + 30 + 7 * i)) for i in range(5)]
 sp = SamplingParams(max_tokens=9, temperature=0, ignore_eos=True)
 outs = {}
 if rank == 0:
-    pair.run_prefill(prompts, sp)
+    # longer prompts than one step's 64-token budget: chunks stream while later chunks compute
+    pair.run_prefill(prompts, sp, chunked=os.environ.get("PD_CHUNKED", "1") == "1")
 else:
     orig = eng.step
     def step():
@@ -146,8 +147,10 @@ dist.destroy_process_group()
 """
 
 
-def test_pd_driver_matches_monolithic(tmp_path):
-    """bench.py --mode pd's in-process P/D data path (gloo, 2 ranks) == monolithic greedy."""
+@pytest.mark.parametrize("chunked", ["1", "0"])
+def test_pd_driver_matches_monolithic(tmp_path, chunked):
+    """bench.py --mode pd's in-process P/D data path (gloo, 2 ranks) == monolithic greedy,
+    with the KV streamed chunk by chunk during the prefill and as one whole-prompt hand-off."""
     import json
     import os
     import socket
@@ -164,7 +167,7 @@ def test_pd_driver_matches_monolithic(tmp_path):
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), REPO=repo)
+                   MASTER_PORT=str(port), REPO=repo, PD_CHUNKED=chunked)
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE))
     outs = [p.communicate(timeout=300) for p in procs]
