@@ -194,10 +194,108 @@ def test_otel_templates_render():
                     "kubernetes-cadvisor"} <= set(jobs)
             assert jobs["kubernetes-nodes"]["scheme"] == "https"
             pipes = col["spec"]["config"]["service"]["pipelines"]
-            assert pipes["metrics"]["exporters"] == ["prometheusremotewrite"]
+            assert pipes["metrics"]["exporters"] == ["prometheusremotewrite", "debug"]
         else:
             cm = docs[0]["data"]["prometheus.yml"]
             assert "remote_write" not in cm  # no self-loop
+
+
+def _sd_name(k):
+    import re
+
+    return re.sub(r"[^a-zA-Z0-9_]", "_", k)
+
+
+def _pod_sd_targets(doc, ns, ip):
+    """Prometheus kubernetes_sd role=pod: one target per declared container port."""
+    tpl = doc["spec"]["template"]
+    meta = {"__meta_kubernetes_namespace": ns,
+            "__meta_kubernetes_pod_name": doc["metadata"]["name"] + "-0",
+            "__meta_kubernetes_pod_node_name": "node-0"}
+    for k, v in tpl["metadata"].get("labels", {}).items():
+        meta["__meta_kubernetes_pod_label_" + _sd_name(k)] = str(v)
+    for k, v in tpl["metadata"].get("annotations", {}).items():
+        meta["__meta_kubernetes_pod_annotation_" + _sd_name(k)] = str(v)
+    out = []
+    for c in tpl["spec"]["containers"]:
+        for port in c.get("ports", []):
+            t = dict(meta, __address__=f"{ip}:{port['containerPort']}",
+                     __meta_kubernetes_pod_container_port_name=port.get("name", ""),
+                     __metrics_path__="/metrics")
+            out.append(t)
+    return out
+
+
+def _relabel(target, rules):
+    """Prometheus relabel_config semantics (keep / replace / labelmap), '$$' = OTel escape."""
+    import re
+
+    t = dict(target)
+    for r in rules:
+        act = r.get("action", "replace")
+        rx = re.compile("^(?:" + str(r.get("regex", "(.*)")).replace("$$", "$") + ")$")
+        src = ";".join(t.get(x, "") for x in r.get("source_labels", []))
+        rep = str(r.get("replacement", "$1")).replace("$$", "$")
+        if act == "keep":
+            if not rx.match(src):
+                return None
+        elif act == "replace":
+            m = rx.match(src)
+            if m:
+                t[r["target_label"]] = re.sub(r"\$(\d+)", lambda g: m.group(int(g.group(1))) or "",
+                                              rep)
+        elif act == "labelmap":
+            for k in list(t):
+                m = rx.match(k)
+                if m:
+                    t[re.sub(r"\$(\d+)", lambda g: m.group(int(g.group(1))), rep)] = t[k]
+    return t
+
+
+def test_collector_scrapes_both_pd_ranks_and_labels_the_gateway_apart():
+    """pd preset: the collector's engine job yields one target per metrics port of the pd
+    pod (prefill rank :8000, decode rank :8001, labelled kv_role prefill/decode); the
+    gateway pod is NOT an engine target but its own job with its own service/job_type."""
+    ctx = yaml.safe_load(open(os.path.join(ROOT, "config", "cluster.yaml")))
+    ctx["cluster_name"] = "node-k8s"
+    env = jinja2.Environment(undefined=jinja2.StrictUndefined)
+    col_docs = yaml.safe_load_all(env.from_string(open(os.path.join(
+        ROOT, "deploy", "otel", "collector.yaml.j2")).read()).render(**ctx))
+    col = [d for d in col_docs if d and d["kind"] == "OpenTelemetryCollector"][0]
+    jobs = {j["job_name"]: j for j in
+            col["spec"]["config"]["receivers"]["prometheus"]["config"]["scrape_configs"]}
+    v = installer.load_values(os.path.join(ROOT, "deploy", "values", "pd.yaml"))
+    out = installer.render(v, "llm-d", "local-path", "50Gi", "Qwen/Qwen3-0.6B", hf_token="t")
+    docs = [d for text in out.values() for d in yaml.safe_load_all(text) if d]
+    deps = [d for d in docs if d["kind"] == "Deployment"]
+    targets = [t for i, d in enumerate(deps) for t in _pod_sd_targets(d, "llm-d", f"10.0.0.{i}")]
+
+    def scraped(job):
+        return [x for x in (_relabel(t, jobs[job]["relabel_configs"]) for t in targets) if x]
+
+    eng = scraped("akap-engines")
+    addrs = {t["__address__"]: t for t in eng}
+    pd_pod = [d for d in deps if "pd" in d["metadata"]["name"]][0]
+    ip = f"10.0.0.{deps.index(pd_pod)}"
+    assert f"{ip}:8000" in addrs and f"{ip}:8001" in addrs, sorted(addrs)
+    assert addrs[f"{ip}:8001"]["kv_role"] == "decode"
+    assert addrs[f"{ip}:8000"]["kv_role"] == "prefill"
+    assert all(t["service"] == "vllm" for t in eng)
+    assert not any(t["__address__"].endswith(":8080") for t in eng)  # no gateway target
+    assert not any(t["__address__"].endswith(":9401") for t in eng)  # no profiler sidecar
+    gw = scraped("akap-gateway")
+    assert len(gw) == 1 and gw[0]["__address__"].endswith(":8080")
+    assert gw[0]["service"] != "vllm" and gw[0]["job_type"] != "llm-inference"
+    # backup GPU-exporter job keys on the exporter pod's port name
+    exp = [d for d in docs if d["kind"] == "DaemonSet"][0]
+    et = [x for x in (_relabel(t, jobs["amd-gpu-exporter-pods"]["relabel_configs"])
+                      for t in _pod_sd_targets(exp, ctx["gpu_exporter_namespace"], "10.1.0.1"))
+          if x]
+    assert len(et) == 1 and et[0]["__address__"] == "10.1.0.1:9400" and et[0]["instance"]
+    procs = col["spec"]["config"]["processors"]
+    assert "resourcedetection" in procs and "metricstransform" in procs
+    pipe = col["spec"]["config"]["service"]["pipelines"]["metrics"]
+    assert "debug" in pipe["exporters"] and "resourcedetection" in pipe["processors"]
 
 
 def _fake_sysfs(root, n=2):
