@@ -57,6 +57,8 @@ class Gateway:
             "P/D requests served monolithically after a failed KV hand-off", ()))
         self.m_pd = self.reg.add(Counter("akap_gateway_pd_requests_total",
                                          "Requests served disaggregated", ()))
+        # Gateway API controller for our GatewayClass (gateway/k8s_controller.py), in-cluster
+        self.controller = None
 
     # ---------------------------------------------------------------- lifecycle
     async def start(self, app=None) -> None:
@@ -65,6 +67,8 @@ class Gateway:
         self._tasks.append(asyncio.create_task(self._scrape_loop()))
         if self.dns:
             self._tasks.append(asyncio.create_task(self._dns_loop()))
+        if self.controller is not None:
+            self._tasks.append(asyncio.create_task(self.controller.run()))
 
     async def stop(self, app=None) -> None:
         for t in self._tasks:
@@ -295,11 +299,22 @@ def main(argv=None) -> None:
     ap.add_argument("--pd-threshold-chars", type=int, default=512)
     ap.add_argument("--w-prefix", type=float, default=2.0)
     ap.add_argument("--otlp-traces-endpoint", default=None)
+    ap.add_argument("--gateway-controller", default="auto", choices=["auto", "on", "off"],
+                    help="reconcile Gateway/HTTPRoute status for GatewayClass --gateway-class "
+                         "(auto: when running in a cluster with a service-account token)")
+    ap.add_argument("--gateway-class", default="akap")
+    ap.add_argument("--namespace", default=os.environ.get("POD_NAMESPACE", "llm-d"))
     a = ap.parse_args(argv)
     tracing.configure(a.otlp_traces_endpoint, service_name=os.environ.get(
         "OTEL_SERVICE_NAME", "akap-gateway"))
     cfg = PickerConfig(pd_threshold_chars=a.pd_threshold_chars, w_prefix=a.w_prefix)
     gw = Gateway(_parse_targets(a.endpoints), _parse_dns(a.dns), cfg, a.scrape_interval)
+    from . import k8s_controller
+
+    if a.gateway_controller == "on" or (a.gateway_controller == "auto"
+                                         and k8s_controller.in_cluster()):
+        gw.controller = k8s_controller.GatewayController(a.namespace,
+                                                         class_name=a.gateway_class)
     web.run_app(gw.app(), host=a.host, port=a.port, access_log=None)
 
 

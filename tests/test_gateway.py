@@ -179,3 +179,96 @@ def test_gateway_end_to_end_reference_smoke(two_engines):
             await runner.cleanup()
 
     asyncio.run(run())
+
+
+def test_gateway_api_controller_programs_status():
+    """The gateway's Gateway API controller (class akap) against a fake API server: the
+    GatewayClass is accepted, the Gateway gets status.addresses[0] = its Service's ClusterIP
+    (tier 1 of /root/reference/llm-d-test.yaml:14-26's lookup) plus Accepted/Programmed, the
+    HTTPRoute's parent is accepted; a second pass writes nothing new; a class owned by
+    another controller is left alone."""
+    import asyncio
+    import json as _json
+
+    import aiohttp as _aiohttp
+    from aiohttp import web as _web
+
+    from aws_k8s_ansible_provisioner_amd.gateway.k8s_controller import (CONTROLLER_NAME,
+                                                                         GatewayController)
+
+    gw_api = "/apis/gateway.networking.k8s.io/v1"
+    state = {
+        "gc": {"metadata": {"name": "akap", "generation": 1},
+               "spec": {"controllerName": CONTROLLER_NAME}},
+        "gw": {"metadata": {"name": "llm-d-inference-gateway", "generation": 2},
+               "spec": {"gatewayClassName": "akap",
+                        "listeners": [{"name": "http", "protocol": "HTTP", "port": 80}]}},
+        "other": {"metadata": {"name": "other-gw", "generation": 1},
+                  "spec": {"gatewayClassName": "istio", "listeners": []}},
+        "rt": {"metadata": {"name": "llm-d-inference-gateway", "generation": 1},
+               "spec": {"parentRefs": [{"name": "llm-d-inference-gateway"}]}},
+    }
+    patches = []
+
+    async def gc(req):
+        return _web.json_response(state["gc"])
+
+    async def gws(req):
+        return _web.json_response({"items": [state["gw"], state["other"]]})
+
+    async def rts(req):
+        return _web.json_response({"items": [state["rt"]]})
+
+    async def svc(req):
+        if req.match_info["name"] != "llm-d-inference-gateway":
+            return _web.json_response({}, status=404)
+        return _web.json_response({"spec": {"clusterIP": "10.96.7.7"}})
+
+    async def patch(req):
+        assert req.headers["Content-Type"] == "application/merge-patch+json"
+        assert req.headers["Authorization"] == "Bearer tok"
+        body = _json.loads(await req.text())
+        patches.append((req.path, body))
+        kind = req.match_info["kind"]
+        key = {"gatewayclasses": "gc", "gateways": "gw", "httproutes": "rt"}[kind]
+        state[key]["status"] = body["status"]
+        return _web.json_response(state[key])
+
+    async def run():
+        app = _web.Application()
+        app.router.add_get(gw_api + "/gatewayclasses/akap", gc)
+        app.router.add_get(gw_api + "/namespaces/llm-d/gateways", gws)
+        app.router.add_get(gw_api + "/namespaces/llm-d/httproutes", rts)
+        app.router.add_get("/api/v1/namespaces/llm-d/services/{name}", svc)
+        app.router.add_patch(gw_api + "/{kind}/{name}/status", patch)
+        app.router.add_patch(gw_api + "/namespaces/llm-d/{kind}/{name}/status", patch)
+        runner = _web.AppRunner(app)
+        await runner.setup()
+        site = _web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        ctl = GatewayController("llm-d", api=f"http://127.0.0.1:{port}", token="tok")
+        try:
+            async with _aiohttp.ClientSession() as s:
+                first = await ctl.reconcile(s)
+                n1 = len(patches)
+                await ctl.reconcile(s)
+                n2 = len(patches)
+                state["gc"]["spec"]["controllerName"] = "example.com/other"
+                third = await ctl.reconcile(s)
+        finally:
+            await runner.cleanup()
+        return first, n1, n2, third
+
+    first, n1, n2, third = asyncio.run(run())
+    assert first["gatewayclass"] and first["gateways"] == {"llm-d-inference-gateway": "10.96.7.7"}
+    assert first["routes"] == ["llm-d-inference-gateway"]
+    st = state["gw"]["status"]
+    assert st["addresses"] == [{"type": "IPAddress", "value": "10.96.7.7"}]
+    assert {c["type"] for c in st["conditions"]} == {"Accepted", "Programmed"}
+    assert st["listeners"][0]["attachedRoutes"] == 1
+    assert "status" not in state["other"]  # another class: untouched
+    assert state["rt"]["status"]["parents"][0]["controllerName"] == CONTROLLER_NAME
+    # level-triggered and idempotent: the second pass only re-asserts the route parent
+    assert n2 - n1 == 1, patches[n1:]
+    assert third["gatewayclass"] is False and not third["gateways"]

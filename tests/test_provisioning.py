@@ -529,7 +529,12 @@ def test_gateway_api_objects_when_crds_present():
     kinds = {(d["kind"], d["metadata"]["name"]) for d in yaml.safe_load_all(on) if d}
     assert ("Gateway", "llm-d-inference-gateway") in kinds
     assert ("HTTPRoute", "llm-d-inference-gateway") in kinds
-    assert "kind: Gateway\n" not in off
+    # our own controller implements class akap: the class, its RBAC, the gateway's SA
+    assert ("GatewayClass", "akap") in kinds and ("ClusterRole", "akap-gateway-controller") in kinds
+    dep = [d for d in yaml.safe_load_all(on) if d and d["kind"] == "Deployment"][0]
+    assert dep["spec"]["template"]["spec"]["serviceAccountName"] == "llm-d-inference-gateway"
+    assert "auto" in dep["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert "kind: Gateway\n" not in off and "GatewayClass" not in off
     route = [d for d in yaml.safe_load_all(on) if d and d["kind"] == "HTTPRoute"][0]
     assert route["spec"]["rules"][0]["backendRefs"][0] == {"name": "llm-d-inference-gateway",
                                                            "port": 80}
