@@ -11,10 +11,15 @@
 //   deep ring:    NS = 8 (64-col, 128 KB) / 6 (128-col, 144 KB), one block per CU and
 //                 NS-1 k-steps (112-120 KB) in flight -- for grids of <= 256 tiles.
 //
-// Structure: BM x BN output tile (BM 64 | 128, BN 64 | 128), 4 waves as 2 (M) x 2 (N), BK = 64.
+// Structure: BM x BN output tile (BM 64 | 128 | 256, BN 64 | 128), BK = 64; 4 waves as 2 (M)
+// x 2 (N), or for BM = 256 8 waves as 4 (M) x 2 (N) (512 threads, wave tile 64 x BN/2).
 // BM = 128 (wave tile 64 x 64) halves the weight traffic of a 256-row batch (each weight byte
 // crosses L2 -> CU twice instead of four times): the large-weight projections of Llama-3-8B
-// class models, where the decode GEMMs are weight-stream bound.  Per
+// class models, where the decode GEMMs are weight-stream bound.  BM = 256 covers the whole
+// 256-row batch: every weight byte crosses L2 -> CU exactly once and each CU's load path
+// carries (256 + BN) rows per k-step for 256 x BN outputs -- 85 FLOP per staged byte at
+// BN = 128 (vs 64 for 128 x 128) -- so the 8B / 70B-shard projections at M = 256, which sit
+// at the MFMA / L2-bandwidth ridge, stream their weights once at up to the MFMA rate.  Per
 // k-step: counted `s_waitcnt vmcnt` for this step's DMAs, raw s_barrier (never
 // __syncthreads: its fence would drain every DMA in flight), refill the slot consumed one step
 // earlier, then ds_read fragments + MFMA 16x16x32.  LDS image: linear DMA destination, XOR
@@ -53,13 +58,17 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BN, int NS, int EPI, int SPL, int OCC, int S, int GBM = 64>
-__global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
+template <int BN, int NS, int EPI, int SPL, int OCC, int S, int GBM = 64, int NW = 4>
+__global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
+  constexpr int NT = 64 * NW;             // threads
+  constexpr int WMW = NW / 2;             // waves along M (2 along N)
+  constexpr int WR = GBM / WMW;           // wave tile rows (wave tile WR x BN/2)
   constexpr int SU = (GBM + BN) * 8;      // slot size in 16-B units
-  constexpr int MI = GBM / 32;            // 16-row MFMA tiles per wave (wave tile GBM/2 x BN/2)
+  constexpr int MI = WR / 16;             // 16-row MFMA tiles per wave
   constexpr int JN = BN / 32;             // 16-col MFMA tiles per wave
-  constexpr int GA = GBM / 32, GW = BN / 32;  // DMA instructions per wave per k-step (A / W)
+  constexpr int GA = GBM / (8 * NW), GW = BN / (8 * NW);  // DMA instructions per wave per k-step
   constexpr int G = GA + GW;
+  static_assert(GA * 8 * NW == GBM && GW * 8 * NW == BN, "8-row DMA pieces cover the tile");
   // ONE __shared__ object (a second one makes hipcc drain vmcnt inside the k-loop,
   // cdna_hip_programming.md "Projection GEMM at M = 256" item 4a); the last element is the
   // split-K "this block combines" flag
@@ -120,7 +129,7 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * (GBM / 2) + i * 16 + fg * 4 + r;
+        const int row = m0 + wm * WR + i * 16 + fg * 4 + r;
         const int rowc = row < p.M ? row : 0;
         rsc[i][r] = ssp[rowc];
         if constexpr (EPI == EPI_RESNORM) {
@@ -165,7 +174,7 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[MI], bfr[JN];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = slot[gswz(wm * (GBM / 2) + i * 16 + fr, ks * 4 + fg)];
+      for (int i = 0; i < MI; ++i) af[i] = slot[gswz(wm * WR + i * 16 + fr, ks * 4 + fg)];
 #pragma unroll
       for (int j = 0; j < JN; ++j)
         bfr[j] = slot[GBM * 8 + gswz(wn * (BN / 2) + j * 16 + fr, ks * 4 + fg)];
@@ -181,12 +190,12 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
     // ---- in-launch split-K combine (see header) ----
     constexpr int NF = MI * JN;  // f32x4 fragments per lane
     f32x4* slabs = reinterpret_cast<f32x4*>(p.ws);
-    const size_t tile_stride = (size_t)NF * 256;
+    const size_t tile_stride = (size_t)NF * NT;
     f32x4* mine = slabs + ((size_t)kz * ntiles + lt) * tile_stride + tid;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < JN; ++j) mine[(i * JN + j) * 256] = acc[i][j];
+      for (int j = 0; j < JN; ++j) mine[(i * JN + j) * NT] = acc[i][j];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(&lds[NS * SU]);
@@ -210,20 +219,20 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
     const f32x4* t0 = slabs + (size_t)lt * tile_stride + tid;
     const size_t zs = (size_t)ntiles * tile_stride;
 #pragma unroll
-    for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] = t0[f * 256];
+    for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] = t0[f * NT];
 #pragma unroll
     for (int z = 1; z < S; ++z)
 #pragma unroll
-      for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] += t0[z * zs + f * 256];
+      for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] += t0[z * zs + f * NT];
   }
 
-  // epilogue: lane holds rows wm*GBM/2 + i*16 + fg*4 + r, column fr of each 16-col sub-tile
+  // epilogue: lane holds rows wm*WR + i*16 + fg*4 + r, column fr of each 16-col sub-tile
   const float inv_k = 1.f / (float)p.K;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm * (GBM / 2) + i * 16 + fg * 4 + r;
+      const int row = m0 + wm * WR + i * 16 + fg * 4 + r;
       const bool row_ok = row < p.M;
       if constexpr (SPL == 1) {
 #pragma unroll
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(256, OCC) void gdgemm_kernel(DGemmArgs p) {
 
 bool gdgemm_supported(int M, int N, int K, int splitk, int bn, int bm) {
   if (bn != 64 && bn != 128) return false;
-  if (bm != 64 && !(bm == 128 && bn == 128)) return false;
+  if (bm != 64 && !(bm == 128 && bn == 128) && bm != 256) return false;
   if (M <= 0 || N <= 0 || K <= 0 || !dgemm_splitk_ok(splitk) || N % 4 || K % splitk) return false;
   const int kps = K / splitk;
   return kps % GBK == 0 && kps >= GBK;
@@ -290,32 +299,32 @@ long gdgemm_ws_floats(int M, int N, int splitk, int bn, int bm) {
   return slabs > dense ? slabs : dense;
 }
 
-template <int BN, int NS, int OCC, int SPL, int S, int BM>
+template <int BN, int NS, int OCC, int SPL, int S, int BM, int NW>
 static void gdgemm_epi(const DGemmArgs& p, dim3 grid, hipStream_t st) {
   if (p.epi == EPI_RESNORM) {
-    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S, BM><<<grid, 256, 0, st>>>(p);
+    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S, BM, NW><<<grid, 64 * NW, 0, st>>>(p);
   } else if (p.epi == EPI_SILU) {
     if constexpr (SPL != 1)
-      gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S, BM><<<grid, 256, 0, st>>>(p);
+      gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S, BM, NW><<<grid, 64 * NW, 0, st>>>(p);
   } else {
-    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S, BM><<<grid, 256, 0, st>>>(p);
+    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S, BM, NW><<<grid, 64 * NW, 0, st>>>(p);
   }
 }
 
-template <int BN, int NS, int OCC, int BM = 64>
+template <int BN, int NS, int OCC, int BM = 64, int NW = 4>
 static void gdgemm_ring(const DGemmArgs& p, dim3 grid, int splitk, hipStream_t st) {
   if (splitk == 1) {
-    gdgemm_epi<BN, NS, OCC, 0, 1, BM>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 0, 1, BM, NW>(p, grid, st);
   } else if (p.counters == nullptr) {
-    gdgemm_epi<BN, NS, OCC, 1, 1, BM>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW>(p, grid, st);
     launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
   } else {
     switch (splitk) {
-      case 2: gdgemm_epi<BN, NS, OCC, 2, 2, BM>(p, grid, st); break;
-      case 4: gdgemm_epi<BN, NS, OCC, 2, 4, BM>(p, grid, st); break;
-      case 8: gdgemm_epi<BN, NS, OCC, 2, 8, BM>(p, grid, st); break;
+      case 2: gdgemm_epi<BN, NS, OCC, 2, 2, BM, NW>(p, grid, st); break;
+      case 4: gdgemm_epi<BN, NS, OCC, 2, 4, BM, NW>(p, grid, st); break;
+      case 8: gdgemm_epi<BN, NS, OCC, 2, 8, BM, NW>(p, grid, st); break;
       default:  // 16 slices: slabs + the separate reduce pass
-        gdgemm_epi<BN, NS, OCC, 1, 1, BM>(p, grid, st);
+        gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW>(p, grid, st);
         launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
         break;
     }
@@ -323,10 +332,15 @@ static void gdgemm_ring(const DGemmArgs& p, dim3 grid, int splitk, hipStream_t s
 }
 
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st) {
-  const int bm = p.bm == 128 ? 128 : 64;
+  const int bm = (p.bm == 128 || p.bm == 256) ? p.bm : 64;
   const int tiles = ((p.M + bm - 1) / bm) * ((p.N + p.bn - 1) / p.bn);
   dim3 grid(tiles, splitk);
   const bool deep = p.ns >= 6;
+  if (bm == 256) {  // 256-row tiles, 8 waves: 3 x 48 KB (BN 128) / 3 x 40 KB (BN 64) ring
+    if (p.bn == 128) gdgemm_ring<128, 3, 1, 256, 8>(p, grid, splitk, st);
+    else gdgemm_ring<64, 3, 1, 256, 8>(p, grid, splitk, st);
+    return;
+  }
   if (bm == 128) {  // 128 x 128 tiles: 4 x 32 KB ring, one block per CU
     gdgemm_ring<128, 4, 1, 128>(p, grid, splitk, st);
     return;

@@ -24,6 +24,7 @@ from __future__ import annotations
 import argparse
 import glob
 import json
+import re
 import os
 import shutil
 import socket
@@ -137,6 +138,9 @@ def _ras_counts(dev: str) -> dict:
     return out
 
 
+_BUS = re.compile(r"^[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-7]$")
+
+
 def _run_amdsmi(args: list[str]) -> Optional[str]:
     exe = shutil.which("amd-smi")
     if not exe:
@@ -157,7 +161,29 @@ def _v(x) -> Optional[float]:
         return None
 
 
+def read_amdsmi_bdf(run=_run_amdsmi) -> dict:
+    """`amd-smi list --json` -> {amd-smi gpu index: PCI bus id}.  amd-smi numbers only the GPUs
+    visible to this process (a container granted one GPU sees "gpu 0" while sysfs lists the
+    node's eight cards), so its per-GPU data is matched to sysfs cards by bus id, never by
+    index (seen on an MI355X box: amd-smi gpu 0 = sysfs card 2, 0000:5d:00.0)."""
+    out = run(["list", "--json"])
+    if not out:
+        return {}
+    try:
+        data = json.loads(out)
+    except ValueError:
+        return {}
+    if isinstance(data, dict):
+        data = data.get("gpu_list") or data.get("gpus") or list(data.values())
+    res = {}
+    for e in data if isinstance(data, list) else []:
+        if isinstance(e, dict) and "gpu" in e and isinstance(e.get("bdf"), str):
+            res[e["gpu"]] = e["bdf"].lower()
+    return res
+
+
 def read_amdsmi(run=_run_amdsmi) -> list[dict]:
+    bdf = read_amdsmi_bdf(run)
     out = run(["metric", "--json"])
     if not out:
         return []
@@ -179,7 +205,8 @@ def read_amdsmi(run=_run_amdsmi) -> list[dict]:
                 return float(cur)
             except (TypeError, ValueError):
                 return None
-        gpus.append({"gpu": m.get("gpu", i), "card": f"gpu{i}", "pci": "", "model": "AMD Instinct",
+        gpus.append({"gpu": m.get("gpu", i), "card": f"gpu{i}", "pci": bdf.get(m.get("gpu", i), ""),
+                     "model": "AMD Instinct",
                      "util": val("usage", "gfx_activity"), "mem_busy": val("usage", "umc_activity"),
                      "vram_used": (val("mem_usage", "used_vram") or 0) * 2**20,
                      "vram_total": (val("mem_usage", "total_vram") or 0) * 2**20,
@@ -272,7 +299,8 @@ def read_xgmi(run=_run_amdsmi) -> dict:
             links[ln.get("gpu")] = (None if r is None else r * 1024,
                                     None if w is None else w * 1024)
         res[d["gpu"]] = {"bit_rate": _v(lm.get("bit_rate")),
-                         "max_bw": _v(lm.get("max_bandwidth")), "links": links}
+                         "max_bw": _v(lm.get("max_bandwidth")), "links": links,
+                         "pci": str(d.get("bdf", "")).lower()}
     return res
 
 
@@ -386,20 +414,33 @@ class Exporter:
         metric, xgmi = self._amdsmi()
         if not gpus:
             gpus = metric
-        else:  # sysfs first; amd-smi fills what the sysfs tree lacks (by GPU index)
             for g in gpus:
-                m = next((x for x in metric if x.get("gpu") == g["gpu"]), None)
-                if m is None:
-                    continue
-                for k in ("clocks", "ecc"):
-                    if not g.get(k) and m.get(k):
-                        g[k] = m[k]
-                for k in ("pcie_replay", "energy_j", "xgmi_err"):
-                    if g.get(k) is None and m.get(k) is not None:
-                        g[k] = m[k]
-        for g in gpus:
-            if g["gpu"] in xgmi:
-                g["xgmi"] = xgmi[g["gpu"]]
+                if g["gpu"] in xgmi:
+                    g["xgmi"] = xgmi[g["gpu"]]
+            return gpus
+        # sysfs first; amd-smi fills what the sysfs tree lacks, matched by PCI bus id (amd-smi
+        # numbers only the GPUs this process can see); by index only when no bus ids exist
+        by_pci = {g["pci"].lower(): g for g in gpus if _BUS.match(str(g.get("pci", "")).lower())}
+
+        def find(idx, pci):
+            if by_pci and pci:
+                return by_pci.get(pci)
+            return next((x for x in gpus if x["gpu"] == idx), None)
+
+        for m in metric:  # no `amd-smi list` mapping: the xgmi report names bus ids too
+            g = find(m["gpu"], m.get("pci") or xgmi.get(m["gpu"], {}).get("pci", ""))
+            if g is None:
+                continue
+            for k in ("clocks", "ecc"):
+                if not g.get(k) and m.get(k):
+                    g[k] = m[k]
+            for k in ("pcie_replay", "energy_j", "xgmi_err"):
+                if g.get(k) is None and m.get(k) is not None:
+                    g[k] = m[k]
+        for idx, x in xgmi.items():
+            g = find(idx, x.get("pci", ""))
+            if g is not None:
+                g["xgmi"] = x
         return gpus
 
     def text(self) -> str:

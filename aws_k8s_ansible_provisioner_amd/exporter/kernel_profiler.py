@@ -68,13 +68,21 @@ class Profiler:
         self.find_pid = find_pid
         self.n = 0
         self.last_error = ""
+        self.failures = 0
+        self.ok = 0
+        self.last_ok = False
 
-    @staticmethod
-    def _run(cmd: list[str]) -> int:
+    def _run(self, cmd: list[str]) -> int:
         exe = shutil.which(cmd[0]) or os.path.join("/opt/rocm/bin", cmd[0])
         # the attach needs no input; bounded so a wedged profiler cannot stall the loop
-        return subprocess.run([exe, *cmd[1:]], stdin=subprocess.DEVNULL,
-                              capture_output=True, timeout=60 + cmd_window_s(cmd)).returncode
+        r = subprocess.run([exe, *cmd[1:]], stdin=subprocess.DEVNULL, capture_output=True,
+                           text=True, timeout=60 + cmd_window_s(cmd))
+        if r.returncode != 0:
+            # e.g. "ptrace call failed. errno: 1 - Operation not permitted": the sidecar needs
+            # CAP_SYS_PTRACE and the engine's PID namespace (shareProcessNamespace)
+            err = [ln for ln in (r.stderr or "").splitlines() if "failed" in ln.lower()]
+            self.last_error = (err[0] if err else (r.stderr or "").strip()[-200:])[-300:]
+        return r.returncode
 
     def windows(self) -> list[str]:
         ws = [d for d in glob.glob(os.path.join(self.dir, "w[0-9]*")) if os.path.isdir(d)]
@@ -95,12 +103,26 @@ class Profiler:
             shutil.rmtree(old, ignore_errors=True)
         if rc != 0:
             self.last_error = self.last_error or f"rocprofv3 exited {rc}"
+            self.failures += 1
+            self.last_ok = False
             return False
         self.last_error = ""
+        self.ok += 1
+        self.last_ok = True
         return True
 
     def text(self) -> str:
-        return rocprof_bridge.render_windows(self.windows(), self.window_ms / 1000.0)
+        """The kept windows' akap_kernel_* series plus the sidecar's own health: whether the
+        newest window worked, and how many failed (an attach the node forbids shows up here
+        instead of as silently empty kernel series)."""
+        return rocprof_bridge.render_windows(self.windows(), self.window_ms / 1000.0) + (
+            "# HELP akap_kernel_profiler_up 1 if the newest profiling window succeeded\n"
+            "# TYPE akap_kernel_profiler_up gauge\n"
+            f"akap_kernel_profiler_up {1 if self.last_ok else 0}\n"
+            "# HELP akap_kernel_profiler_windows_total Profiling windows attempted, by result\n"
+            "# TYPE akap_kernel_profiler_windows_total counter\n"
+            f'akap_kernel_profiler_windows_total{{result="ok"}} {self.ok}\n'
+            f'akap_kernel_profiler_windows_total{{result="failed"}} {self.failures}\n')
 
 
 def cmd_window_s(cmd: list[str]) -> float:

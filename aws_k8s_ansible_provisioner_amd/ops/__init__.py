@@ -281,7 +281,8 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
     splitk > 1 inlaunch=True combines the K slices inside the launch (last-arriver ticket,
     no separate reduce kernel; also allows split-K with the SwiGLU epilogue).
     bm = 128 (with bn = 128): 128-row LDS-DMA tiles (weights cross L2 -> CU half as often at
-    M = 256; the large-weight projections).
+    M = 256; the large-weight projections); bm = 256 (bn 64 | 128, 8 waves): the whole
+    256-row batch per tile, every weight byte crosses L2 -> CU once.
     km = 16 | 32 selects csrc/kernels/kgemm.hip instead: km x 32 output tiles with the K split
     over the workgroup's waves (plain prologue, store / residual epilogues, no split-K)."""
     M = x.shape[0]
@@ -334,7 +335,7 @@ def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI
     """Mirror of dgemm_supported / gdgemm_supported / dgemm_epi_supported (host-side)."""
     if splitk not in (1, 2, 4, 8, 16):
         return False
-    if bm != 64 and not (bm == 128 and bn == 128):
+    if bm != 64 and not (bm == 128 and bn == 128) and not (bm == 256 and bn in (64, 128)):
         return False
     inl = inlaunch and bn and splitk > 1
     if epi == EPI_SILU and ((splitk != 1 and not inl) or N % 32):

@@ -76,10 +76,11 @@ def _timed(fn, n: int) -> float:
     return e0.elapsed_time(e1) * 1000.0 / (2 * n)
 
 
-def _gd_variants(s: int, bns):
+def _gd_variants(s: int, bns, M: int = 0):
     """gdgemm.hip variants at split s: (tile width, ring depth, in-launch split-K combine, tile
     rows).  Depth 0 = shallow ring (two blocks per CU), 8 = deep ring (one block per CU);
-    128 x 128 tiles (rows 128) have their own 4-slot ring."""
+    128 x 128 tiles (rows 128) have their own 4-slot ring; 256-row tiles (8 waves, 3-slot
+    ring) only where the batch fills most of them (M > 160)."""
     for bn in bns:
         for ns in (0, 8):
             for inl in ((False, True) if s > 1 else (False,)):
@@ -87,6 +88,9 @@ def _gd_variants(s: int, bns):
         if bn == 128:
             for inl in ((False, True) if s > 1 else (False,)):
                 yield bn, 4, inl, 128
+        if M > 160:
+            for inl in ((False, True) if s > 1 else (False,)):
+                yield bn, 3, inl, 256
 
 
 def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out, ln_out,
@@ -105,9 +109,12 @@ def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out
 
 
 def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
-         margin: float = 0.03, pfs=(2, 4, 8), bns=(64, 128), kms=(16, 32)) -> Choice:
+         margin: float = 0.03, pfs=(2, 4, 8), bns=(64, 128), kms=(16, 32),
+         lm_head: bool = False) -> Choice:
     """Pick the fastest way to compute x[M, K] @ w.T for these same-shape weights.
-    hipBLASLt is kept unless the MFMA kernel is more than `margin` faster."""
+    hipBLASLt is kept unless the MFMA kernel is more than `margin` faster.  lm_head: only the
+    256-row LDS-DMA tiles among the gdgemm variants (the narrow ones re-stream the
+    activations once per 64-128 of ~150k columns)."""
     from . import gemm_counters  # noqa: F401  (ensures the native library is loaded)
 
     w0 = weights[0]
@@ -123,7 +130,7 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
         t = _timed(lambda i: torch.ops.akap.wgemm(y, x, weights[i % n]), n)
         if t < t_best:
             best, t_best = ("wgemm",), t
-    for s in splits:
+    for s in (() if lm_head else splits):
         if K // s < 256 or K % (64 * s):
             continue
         ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
@@ -139,9 +146,9 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
             t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, pf), n)
             if t < t_best:
                 best, t_best = ("dgemm", s, pf), t
-        for bn, ns, inl, bm in _gd_variants(s, bns):  # LDS-DMA staged variants (gdgemm.hip)
+        for bn, ns, inl, bm in _gd_variants(s, bns, M):  # LDS-DMA staged variants (gdgemm.hip)
             if (not dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl, bm=bm)
-                    or (s > 1 and K // s < 256)):
+                    or (s > 1 and K // s < 256) or (lm_head and bm != 256)):
                 continue
             t = _timed(_gd_call(M, N, K, s, bn, ns, inl, y, x, weights, 0, None, None, None,
                                 None, bm), n)
@@ -165,8 +172,8 @@ def _gd_name(v) -> str:
     bn, ns, inl, km, bm = variant_fields(v)[:5]
     if km:
         return f"k{km}"
-    if bm == 128:
-        return f"g{bn}x128" + ("i" if inl else "")
+    if bm in (128, 256):
+        return f"g{bn}x{bm}" + ("i" if inl else "")
     return f"g{bn}" + ("d" if ns >= 6 else "") + ("i" if inl else "")
 
 
@@ -184,10 +191,13 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
             summary[(M, name)] = tune(M, ws)
     lm = getattr(model, "lm_head", None)
     if lm is not None and lm.is_cuda:
-        # the decode LM head: hipBLASLt vs the wide-row kernel only (split-K slabs of a
-        # vocab-wide output would be GBs)
+        # the decode LM head: hipBLASLt vs the wide-row kernel (split-K slabs of a vocab-wide
+        # output would be GBs); at M > 160 also the 256-row LDS-DMA tiles without split-K
+        # (every weight byte crosses L2 -> CU once)
         for M in Ms:
-            summary[(M, "lm_head")] = tune(M, [lm], splits=(), pfs=(), bns=(), kms=())
+            big = M > 160
+            summary[(M, "lm_head")] = tune(M, [lm], splits=(1,) if big else (), pfs=(),
+                                           bns=(128,) if big else (), kms=(), lm_head=True)
     wins = {k: v for k, v in summary.items() if v[0] != "torch"}
     log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, HIP kernel chosen for "
         f"{len(wins)}: " + ", ".join(
@@ -267,7 +277,7 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
             a_o_, ln_ = (a_o if epi == 1 else None), (ln if epi == 1 else None)
             for s in splits:
                 cands = [(pf, 0, 0, False, 0, 64) for pf in pfs] + \
-                    [(1, bn, ns, inl, 0, bm) for bn, ns, inl, bm in _gd_variants(s, bns)]
+                    [(1, bn, ns, inl, 0, bm) for bn, ns, inl, bm in _gd_variants(s, bns, M)]
                 if s == 1:
                     cands += [(1, 0, 0, False, km, 64) for km in kms
                               if kgemm_supported(M, N, K, km, epi)]

@@ -5,11 +5,11 @@ The 8-GPU TP run needs a whole node; this instantiates the real per-rank shard t
 d 8192, 3584 of 28672 FFN columns, 16,032 of 128,256 vocab rows: 17.6 GB of bf16 weights)
 and times its compute. Shapes, kernels, GEMM tuner choices and hipGraph capture are
 identical. The TP collectives are replaced by local stand-ins of the same shape:
-  tp_all_reduce           identity
-  tp_all_reduce_resnorm   the local residual + next-norm epilogue (no reduction)
+  tp_all_reduce           the custom all-reduce kernel on a one-rank communicator
+  tp_all_reduce_resnorm   the same kernel with its fused residual + next-norm epilogue
   tp_all_gather_last      the shard repeated tp times
-so the result is a per-rank compute time. A TP step adds two all-reduces per layer
-(B x 8192 bf16 each) on xGMI to it.
+so the result is a per-rank compute time including the all-reduce launches; a TP step adds
+the xGMI exchange of two B x 8192 bf16 all-reduces per layer to it.
 
 python bench/tp_shard_rehearsal.py [--model llama-3-70b] [--tp 8] [--B 64,128,256] [--ctx 1024]
 """
@@ -29,13 +29,23 @@ from aws_k8s_ansible_provisioner_amd.parallel import comm, state  # noqa: E402
 
 
 def stub_collectives(tp: int) -> None:
-    def resnorm(partial, residual, ln, a_out, ss):
-        r = (partial.float() + residual.float()).to(residual.dtype)
-        residual.copy_(r)
-        a_out.copy_((r.float() * ln.float()).to(a_out.dtype))
-        ss[: r.shape[0]] += r.float().pow(2).sum(-1)
+    """Local stand-ins of the TP collectives.  The all-reduces run the REAL custom all-reduce
+    kernels (csrc/kernels/custom_allreduce.hip) on a one-rank communicator: the same launch,
+    staging, flag protocol and fused residual + next-norm epilogue, minus the peer reads over
+    xGMI -- so the per-rank step includes the all-reduce kernels' own cost, not a chain of
+    Python elementwise stand-ins (which inflated round 2's number by ~6 ms at B=256)."""
+    h = torch.ops.akap.car_create(torch.cuda.current_device(), 0, 1, 1 << 23)
+    torch.ops.akap.car_link_local(h, [h])
 
-    comm.tp_all_reduce = lambda x: x
+    def all_reduce(x):
+        if x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0:
+            torch.ops.akap.car_all_reduce(h, x, x, False)
+        return x
+
+    def resnorm(partial, residual, ln, a_out, ss):
+        torch.ops.akap.car_all_reduce_resnorm(h, partial, residual, ln, a_out, ss, False)
+
+    comm.tp_all_reduce = all_reduce
     comm.tp_all_reduce_resnorm = resnorm
     comm.tp_all_gather_last = lambda x, out=None: torch.cat([x] * tp, dim=-1)
 

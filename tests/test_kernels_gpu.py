@@ -625,7 +625,7 @@ def test_fused_decode_gemm_in_graph():
 
 
 @pytest.mark.parametrize("ring", ["shallow", "deep", "deep-inlaunch", "shallow-inlaunch",
-                                  "rows128", "rows128-inlaunch"])
+                                  "rows128", "rows128-inlaunch", "rows256", "rows256-inlaunch"])
 @pytest.mark.parametrize("bn", [64, 128])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K,splitk", [(1, 256, 1024, 1), (37, 1024, 2048, 2),
@@ -635,9 +635,10 @@ def test_fused_decode_gemm_in_graph():
 def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
     """gdgemm.hip (global_load_lds ring) with each epilogue vs fp32 references: shallow
     (2 blocks/CU) and deep (1 block/CU) rings, split-K reduced by the separate pass or
-    combined in-launch by the last-arriving slice (also for the SwiGLU epilogue)."""
+    combined in-launch by the last-arriving slice (also for the SwiGLU epilogue); 128-row
+    tiles and 256-row tiles (8 waves, 512 threads, row tails at M = 130 / 200 / 1 / 37)."""
     inl = ring.endswith("inlaunch")
-    bm = 128 if ring.startswith("rows128") else 64
+    bm = 256 if ring.startswith("rows256") else 128 if ring.startswith("rows128") else 64
     if inl and splitk == 1:
         pytest.skip("in-launch combine needs split-K")
     if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=bn, inlaunch=inl, bm=bm):

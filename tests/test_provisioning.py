@@ -552,3 +552,51 @@ def test_gitignore_covers_reference_local_state():
 def test_cleanup_removes_kubeconfigs_and_records_reset():
     play = open(os.path.join(ROOT, "provision", "cleanup-instance.yaml")).read()
     assert 'patterns: "kubeconfig-*"' in play and "Record what was reset" in play
+
+
+def _fake_sysfs_bus(root, buses):
+    """sysfs cards whose device links resolve to PCI bus-id directories (like /sys)."""
+    for i, bus in enumerate(buses):
+        real = root / "devices" / bus
+        (real / "hwmon" / "hwmon0").mkdir(parents=True)
+        (real / "vendor").write_text("0x1002\n")
+        (real / "gpu_busy_percent").write_text(f"{10 * i}\n")
+        (real / "mem_info_vram_used").write_text(str(2**30))
+        (real / "mem_info_vram_total").write_text(str(288 * 2**30))
+        card = root / "class" / "drm" / f"card{i}"
+        card.mkdir(parents=True)
+        (card / "device").symlink_to(real)
+
+
+@pytest.mark.parametrize("with_list", [True, False])
+def test_gpu_exporter_real_amdsmi_output_matched_by_bus_id(tmp_path, with_list):
+    """Real `amd-smi metric/xgmi --json` output captured on an MI355X box (ROCm 7.2, a
+    container granted ONE of the node's eight GPUs: amd-smi calls it gpu 0, sysfs shows it as
+    card 2 at 0000:5d:00.0).  Its clocks / ECC / energy / xGMI series must land on card 2 --
+    matched by PCI bus id (from `amd-smi list`, else the xgmi report), not by index."""
+    fx = os.path.join(ROOT, "tests", "fixtures")
+    metric = open(os.path.join(fx, "amdsmi_metric_mi355x_rocm72.json")).read()
+    xgmi = open(os.path.join(fx, "amdsmi_xgmi_mi355x_rocm72.json")).read()
+    _fake_sysfs_bus(tmp_path, ["0000:75:00.0", "0000:0d:00.0", "0000:5d:00.0"])
+
+    def run(args):
+        if args[:1] == ["metric"]:
+            return metric
+        if args[:1] == ["xgmi"]:
+            return xgmi
+        if args[:1] == ["list"] and with_list:
+            return '[{"gpu": 0, "bdf": "0000:5d:00.0", "uuid": "x"}]'
+        return None
+
+    txt = gpu_exporter.Exporter(str(tmp_path), node="n1", run=run).text()
+    gfx = [ln for ln in txt.splitlines() if ln.startswith("amd_gpu_clock_mhz{") and
+           'domain="gfx"' in ln]
+    assert len(gfx) == 1 and 'pci_bus_id="0000:5d:00.0"' in gfx[0] and 'gpu="2"' in gfx[0]
+    assert gfx[0].endswith(" 157.0")  # the real reading
+    en = [ln for ln in txt.splitlines() if ln.startswith("amd_gpu_energy_joules_total{")]
+    assert len(en) == 1 and 'pci_bus_id="0000:5d:00.0"' in en[0]
+    bw = [ln for ln in txt.splitlines() if ln.startswith("amd_gpu_xgmi_max_bandwidth_gbps{")]
+    assert len(bw) == 1 and 'pci_bus_id="0000:5d:00.0"' in bw[0] and bw[0].endswith(" 608.0")
+    ecc = [ln for ln in txt.splitlines() if ln.startswith("amd_gpu_ecc_errors_total{")]
+    assert ecc and all('pci_bus_id="0000:5d:00.0"' in ln for ln in ecc)
+    assert 'block="umc"' in txt
