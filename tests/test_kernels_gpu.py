@@ -349,6 +349,25 @@ def test_fused_moe(T, E, K, d, F):
     _close(out, exp, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("T", [64, 1024])
+def test_moe_block_tp_paths_match_reference(T):
+    """TP-mode MoE block: decode sizes on fused_moe, prefill sizes (T >= 512) on the
+    torch._grouped_mm path -- both against the fp32 reference of the same routing."""
+    from aws_k8s_ansible_provisioner_amd.models.config import get_config
+    from aws_k8s_ansible_provisioner_amd.models.moe import MoEBlock
+    from aws_k8s_ansible_provisioner_amd.parallel.state import ParallelState
+
+    cfg = get_config("tiny-mixtral8")
+    blk = MoEBlock(cfg, ParallelState(rank=0, world_size=1, tp_size=1), DEV, torch.bfloat16,
+                   torch.Generator().manual_seed(0), full_then_shard=False, mode="tp")
+    torch.manual_seed(T)
+    h = torch.randn(T, cfg.hidden_size, dtype=torch.bfloat16, device=DEV)
+    out = blk.forward(h)
+    w, ids = ops.moe_router_topk(h, blk.router, blk.K, renormalize=True)
+    exp = ref.fused_moe(h.cpu(), blk.w13.cpu(), blk.w2.cpu(), w.cpu(), ids.cpu())
+    _close(out, exp, atol=3e-2, rtol=3e-2)
+
+
 def test_fused_moe_graph_capture():
     torch.manual_seed(3)
     T, E, K, d, F = 48, 8, 2, 256, 256

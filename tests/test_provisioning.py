@@ -568,6 +568,14 @@ def _fake_sysfs_bus(root, buses):
         (card / "device").symlink_to(real)
 
 
+def test_gpu_exporter_parses_real_amdsmi_list():
+    """`amd-smi list --json` as printed on an MI355X box (ROCm 7.2, one GPU granted): the
+    index -> bus id map the exporter uses to place amd-smi data on sysfs cards."""
+    raw = open(os.path.join(ROOT, "tests", "fixtures", "amdsmi_list_mi355x_rocm72.json")).read()
+    assert gpu_exporter.read_amdsmi_bdf(lambda a: raw if a == ["list", "--json"] else None) == {
+        0: "0000:0d:00.0"}
+
+
 @pytest.mark.parametrize("with_list", [True, False])
 def test_gpu_exporter_real_amdsmi_output_matched_by_bus_id(tmp_path, with_list):
     """Real `amd-smi metric/xgmi --json` output captured on an MI355X box (ROCm 7.2, a
