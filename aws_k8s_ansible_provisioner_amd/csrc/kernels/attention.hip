@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256, MINW) void paged_attn_decode_kernel(AttnParams
 // Persistent variant: a fixed grid (a few workgroups per CU) strides over all work items
 // (kv head fastest, so consecutive items of a workgroup share the sequence's block table
 // and q row in cache).  Bounded loop: every workgroup exits after its last item.
-template <bool PREFETCH, bool NT>
+template <bool PREFETCH, bool NT, bool FUSED = false>
 __global__ __launch_bounds__(256) void paged_attn_decode_persistent_kernel(AttnParams p,
                                                                            int num_seqs) {
   extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void paged_attn_decode_persistent_kernel(AttnP
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
     const int part = it % p.num_parts;
     const int sk = it / p.num_parts;
-    decode_item<PREFETCH, NT>(p, sk / p.Hkv, sk % p.Hkv, part, dyn_lds);
+    decode_item<PREFETCH, NT, FUSED>(p, sk / p.Hkv, sk % p.Hkv, part, dyn_lds);
     __syncthreads();  // LDS combine buffer is reused by the next item
   }
 }
@@ -894,6 +894,10 @@ void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) 
       paged_attn_decode_kernel<true, 1, true, true, true><<<grid, 256, smem, s>>>(p);
     else
       paged_attn_decode_kernel<true, 1, true, false, true><<<grid, 256, smem, s>>>(p);
+  } else if (p.qkv != nullptr && per_cu > 0) {  // fused, persistent grid (grid-capped)
+    const int items = num_seqs * p.Hkv * p.num_parts;
+    const int grid = min(items, num_cus() * per_cu);
+    paged_attn_decode_persistent_kernel<true, true, true><<<grid, 256, smem, s>>>(p, num_seqs);
   } else if (p.qkv != nullptr) {  // fused q/k-norm + RoPE + KV write (default flags path)
     const dim3 grid(num_seqs, p.Hkv, p.num_parts);
     if (p.flags & 1)
