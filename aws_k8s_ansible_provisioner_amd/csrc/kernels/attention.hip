@@ -160,6 +160,21 @@ __device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC
   compute_chunk<MASK>(st, qb, c, t0, limit, scale_log2);
 }
 
+// V tail: lanes whose 8-token V group is the sequence's last group (first token gstart;
+// lanes past it were clamped onto it by load_chunk) take their V^T fragments from the LDS
+// group image instead of the cache.
+template <bool F8>
+__device__ __forceinline__ void patch_v(ChunkT<F8>& c, int t0, int gstart, const bf16* img) {
+  if constexpr (!F8) {
+    const int lane = threadIdx.x & 63;
+    if (t0 + 8 * (lane >> 4) >= gstart) {
+#pragma unroll
+      for (int n = 0; n < kND; ++n)
+        c.vb[n] = *reinterpret_cast<const bf16x8*>(img + (16 * n + (lane & 15)) * 8);
+    }
+  }
+}
+
 // Load this lane's Q^T operand for query row (lane & 15) (zeros if invalid).
 __device__ __forceinline__ void load_q(bf16x8 (&qb)[kNC], const bf16* qrow_ptr, bool valid) {
   const int g = (threadIdx.x & 63) >> 4;
@@ -236,9 +251,19 @@ __global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
 // row G+1 = its value head; 16 threads per row, 8 dims each.  q rows -> per-head RMSNorm
 // (bf16-rounded, like the standalone kernel) -> NeoX RoPE -> LDS; the new token's k / v
 // (only when write_kv) -> paged cache.  Rotary pairs (d, d+64) sit in threads j and j^8.
+// V tail image helper: 16 threads (j = dims [8j, 8j+8)) hold an 8-token group token-major
+// (rows[i] = token i) and store it as the cache's [D][8] group image (dim-major, 16 B per dim)
+__device__ __forceinline__ void group_units(const bf16x8 (&rows)[8], bf16x8 (&u)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u[k][i] = rows[i][k];
+}
+
 template <bool F8>
 __device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq, int kvh,
-                                                   bool write_kv, bf16* q_s) {
+                                                   bool write_kv, bf16* q_s, int tsl,
+                                                   bf16* v_img) {
   const int G = p.G;
   const int rr = threadIdx.x >> 4;
   const int j = threadIdx.x & 15;
@@ -299,6 +324,30 @@ __device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq,
           } else {
             *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
           }
+        } else if (tsl >= 0) {
+          // V tail: the group's earlier tokens come from the tail, this token from registers;
+          // the group image goes to LDS (the attention below reads the group from there), and
+          // either the tail gets this token's row (one 256-B row per token-head) or, when the
+          // token completes the group, the cache gets the whole [D][8] group (full lines)
+          const int i0 = off & 7;
+          bf16* tb = p.v_tail + ((size_t)tsl * p.Hkv + kvh) * 8 * kD + 8 * j;
+          bf16x8 rows[8], u[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (i < i0) rows[i] = *reinterpret_cast<const bf16x8*>(tb + (size_t)i * kD);
+            else rows[i] = i == i0 ? o8 : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          }
+          group_units(rows, u);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(v_img + (8 * j + k) * 8) = u[k];
+          if (i0 == 7) {
+            bf16* e = (bf16*)p.v_cache + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
+                      (off >> 3) * kD * 8 + (size_t)(8 * j) * 8;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(e + 8 * k) = u[k];
+          } else {
+            *reinterpret_cast<bf16x8*>(tb + (size_t)i0 * kD) = o8;
+          }
         } else {
           const size_t e = ((size_t)blk * p.Hkv + kvh) * kD * p.BS + (off >> 3) * kD * 8 + (off & 7);
 #pragma unroll
@@ -340,9 +389,16 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
   float* l_s = m_s + 4 * G;                   // [4][G]
 #define OS(w_, r_, d_) o_s[((w_) * G + (r_)) * (kD + 4) + (d_)]
   bf16* q_s = reinterpret_cast<bf16*>(l_s + 4 * G);  // [G][kD] (fused only)
+  bf16* v_img = q_s + (FUSED ? G * kD : 0);          // [kD][8] V tail group image
   const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
   const int limit = kv_len - 1;
   const bool writes_kv = kv_len > 0 && pstart <= kv_len - 1 && kv_len - 1 < pend;
+  // V tail: the sequence's last 8-token group (first token gstart) is read from an LDS image
+  // instead of the cache -- fused: the image the prologue builds (tail + the new token);
+  // plain: a still-partial group straight from the tail (the writer kernel put it there)
+  const int tsl = (!F8 && p.v_tail != nullptr && kv_len > 0) ? p.tail_slot[seq] : -1;
+  const int gstart = (kv_len - 1) & ~7;
+  const bool use_img = tsl >= 0 && writes_kv && (FUSED ? p.slots[seq] >= 0 : (kv_len & 7) != 0);
   // PREFETCH: this wave's first chunk is issued before anything else (in the fused kernel,
   // before the q/k prologue, so its HBM latency overlaps the prologue's)
   int t0 = pstart + 32 * w;
@@ -350,10 +406,25 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
   if (PREFETCH && t0 < pend)
     load_chunk<NT, F8>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
   if constexpr (FUSED) {
-    fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s);
+    fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s, use_img ? tsl : -1, v_img);
     // the chunk holding the token the prologue just wrote is re-read after the barrier
     if (PREFETCH && writes_kv && t0 < pend && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
       load_chunk<NT, F8>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+  } else if (use_img) {  // uniform per workgroup
+    if (threadIdx.x < 16) {
+      const int j = threadIdx.x;
+      const int cnt = kv_len - gstart;
+      const bf16* tb = p.v_tail + ((size_t)tsl * p.Hkv + kvh) * 8 * kD + 8 * j;
+      bf16x8 rows[8], u[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        rows[i] = i < cnt ? *reinterpret_cast<const bf16x8*>(tb + (size_t)i * kD)
+                          : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      group_units(rows, u);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(v_img + (8 * j + k) * 8) = u[k];
+    }
+    __syncthreads();
   }
   WaveState st;
   wave_state_init(st);
@@ -376,6 +447,7 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
           if (more)
             load_chunk<NT, F8>(nxt, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
                                t0 + 128);
+          if (use_img && t0 <= gstart && gstart < t0 + 32) patch_v(cur, t0, gstart, v_img);
           if (t0 + 31 < kv_len)
             compute_chunk<false>(st, qb, cur, t0, limit, p.scale_log2);
           else
@@ -385,12 +457,13 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
       }
     } else {
       for (; t0 < pend; t0 += 128) {
+        ChunkT<F8> c;
+        load_chunk<NT, F8>(c, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+        if (use_img && t0 <= gstart && gstart < t0 + 32) patch_v(c, t0, gstart, v_img);
         if (t0 + 31 < kv_len)
-          attn_chunk<false, NT, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
-                                    t0, limit, p.scale_log2);
+          compute_chunk<false>(st, qb, c, t0, limit, p.scale_log2);
         else
-          attn_chunk<true, NT, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
-                                   t0, limit, p.scale_log2);
+          compute_chunk<true>(st, qb, c, t0, limit, p.scale_log2);
       }
     }
   }
@@ -886,7 +959,8 @@ static int num_cus() {
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) {
   if (num_seqs == 0) return;
   const size_t smem = (size_t)(4 * p.G * (kD + 4) + 8 * p.G) * sizeof(float) +
-                      (p.qkv ? (size_t)p.G * kD * sizeof(bf16) : 0);
+                      (p.qkv ? (size_t)p.G * kD * sizeof(bf16) : 0) +
+                      (p.v_tail ? (size_t)kD * 8 * sizeof(bf16) : 0);
   const int per_cu = (p.flags >> 3) & 7;  // flags bits 3..5: persistent, WGs per CU
   if (p.kv_fp8) {  // fp8 KV cache: prefetching + non-temporal variants only
     const dim3 grid(num_seqs, p.Hkv, p.num_parts);

@@ -18,7 +18,9 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                void* v_cache, const int64_t* positions, const int64_t* slots,
                                const float* cos_sin, const void* q_w, const void* k_w, int T,
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
-                               hipStream_t s, int kv_fp8 = 0, int v_per_token = 0);
+                               hipStream_t s, int kv_fp8 = 0, int v_per_token = 0,
+                               void* v_tail = nullptr, const int* tail_slot = nullptr,
+                               int num_decode = 0);
 void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void* v_cache,
                               const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s,
                               int kv_fp8 = 0);
@@ -58,6 +60,13 @@ struct AttnParams {
   const __bf16* q_w;         // [D] or nullptr
   const __bf16* k_w;
   float eps;
+  // V tail (bf16 caches; nullptr = off): per sequence slot, its current partial 8-token V
+  // group token-major [slots, Hkv, 8, D] -- decode writes one 256-B row per token there and
+  // the whole [D][8] group into the cache only when the group completes (16 full lines per
+  // 8 tokens instead of 16 partial lines per token); decode readers take a partial group
+  // from the tail.  tail_slot: per batch row (decode) / token (writer), -1 = no tail.
+  __bf16* v_tail;
+  const int* tail_slot;
 };
 // tile_rows: 64 -> per-wave 16-row kernel, 128 -> flash-style LDS-tiled kernel
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows, hipStream_t s);

@@ -126,7 +126,8 @@ template <bool F8>
 __device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_stride,
                                        void* __restrict__ v_cache,
                                        const int64_t* __restrict__ slots, int T, int Hq, int Hkv,
-                                       int BS, int span_id) {
+                                       int BS, int span_id, bf16* __restrict__ v_tail,
+                                       const int* __restrict__ tail_slot, int num_decode) {
   constexpr int D = 128;
   __shared__ bf16 tile[V_ROWS][D];
   __shared__ int lead_n[V_SPAN];  // run length if the token leads a run, else 0
@@ -164,10 +165,29 @@ __device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_str
   for (int j = half; j < n_leads; j += 2) {
     const int i = lead_list[j];
     const int n = lead_n[i];
-    const int64_t s = slots[t0 + i];
+    const int t = t0 + i;
+    const int64_t s = slots[t];
     const int64_t blk = s / BS;
     const int off = (int)(s % BS);
+    const int i0 = off & 7;
     const size_t g = ((size_t)blk * Hkv + vh) * D * BS + (off >> 3) * D * 8 + d * 8;
+    // V tail (bf16): this sequence's partial group, token-major; element (token k, dim d)
+    const int tsl = (!F8 && v_tail != nullptr) ? tail_slot[t] : -1;
+    bf16* trow = tsl >= 0 ? v_tail + ((size_t)tsl * Hkv + vh) * 8 * D + d : nullptr;
+    if (tsl >= 0 && t < num_decode && i0 + n == 8 && n < 8) {
+      // a decode row completing its group: the group's earlier tokens live in the tail (decode
+      // steps write no partial V lines) -> the whole [D][8] group, 16 full lines
+      bf16x8 v;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = k < i0 ? trow[(size_t)k * D] : tile[i + k - i0][d];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(v_cache) + g) = v;
+      continue;
+    }
+    if (tsl >= 0 && i0 + n < 8) {
+      // the group stays partial after this step: its tokens also go to the tail, where the
+      // decode readers (and the step that completes the group) take them from
+      for (int k = 0; k < n; ++k) trow[(size_t)(i0 + k) * D] = tile[i + k][d];
+    }
     if (n == 8) {
       bf16x8 v;
 #pragma unroll
@@ -227,22 +247,26 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
     void* __restrict__ k_cache, void* __restrict__ v_cache, const int64_t* __restrict__ positions,
     const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
     const bf16* __restrict__ q_w, const bf16* __restrict__ k_w, int T, int Hq, int Hkv, int BS,
-    float eps, int apply_rope, int qk_blocks, int v_per_token) {
+    float eps, int apply_rope, int qk_blocks, int v_per_token, bf16* __restrict__ v_tail,
+    const int* __restrict__ tail_slot, int num_decode) {
   if ((int)blockIdx.x < qk_blocks)
     qk_item<F8>(qkv, qkv_stride, q_out, k_cache, positions, slots, cos_sin, q_w, k_w, T, Hq, Hkv,
                 BS, eps, apply_rope);
   else if (v_per_token)
     v_item<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks);
   else
-    v_span<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks);
+    v_span<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks, v_tail,
+               tail_slot, num_decode);
 }
 
 void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, void* k_cache,
                                void* v_cache, const int64_t* positions, const int64_t* slots,
                                const float* cos_sin, const void* q_w, const void* k_w, int T,
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
-                               hipStream_t s, int kv_fp8, int v_per_token) {
+                               hipStream_t s, int kv_fp8, int v_per_token, void* v_tail,
+                               const int* tail_slot, int num_decode) {
   if (T == 0 || D != 128) return;
+  if (v_per_token || kv_fp8) v_tail = nullptr;  // the tail is a bf16, span-role feature
   const long qk_threads = (long)T * (Hq + Hkv) * 16;
   const int qk_blocks = (int)((qk_threads + 255) / 256);
   const int v_blocks = v_per_token ? (int)(((long)T * Hkv * 16 + 255) / 256)
@@ -251,7 +275,8 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
 #define QKR(F8)                                                                                 \
   qk_norm_rope_cache_kernel<F8><<<grid, 256, 0, s>>>(                                           \
       (const bf16*)qkv, qkv_stride, (bf16*)q_out, k_cache, v_cache, positions, slots, cos_sin, \
-      (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope, qk_blocks, v_per_token)
+      (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope, qk_blocks, v_per_token, \
+      (bf16*)v_tail, tail_slot, num_decode)
   if (kv_fp8) QKR(true); else QKR(false);
 #undef QKR
 }

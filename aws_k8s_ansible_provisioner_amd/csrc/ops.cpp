@@ -59,7 +59,9 @@ void fused_add_rmsnorm(Tensor out, Tensor residual, Tensor x, Tensor w, double e
 void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache,
                         Tensor positions, Tensor slots, Tensor cos_sin,
                         std::optional<Tensor> q_w, std::optional<Tensor> k_w, int64_t Hq,
-                        int64_t Hkv, double eps, bool apply_rope, bool decode) {
+                        int64_t Hkv, double eps, bool apply_rope, bool decode,
+                        std::optional<Tensor> v_tail, std::optional<Tensor> tail_slot,
+                        int64_t num_decode) {
   CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv); CHECK_CONTIG(q_out);
   CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
   TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong,
@@ -75,12 +77,25 @@ void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache
               "v_cache must be [NB,Hkv,BS/8,D,8]");
   TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D, "qkv too narrow");
   TORCH_CHECK(positions.numel() >= T && slots.numel() >= T, "positions/slots too short");
+  if (v_tail) {
+    TORCH_CHECK(!decode, "the V tail is written by the span (prefill / mixed) role only");
+    TORCH_CHECK(!kv_fp8_of(k_cache, v_cache), "the V tail needs a bf16 KV cache");
+    TORCH_CHECK(tail_slot && tail_slot->scalar_type() == at::kInt && tail_slot->numel() >= T,
+                "tail_slot: int32, one entry per token");
+    TORCH_CHECK(v_tail->scalar_type() == at::kBFloat16 && v_tail->dim() == 4 &&
+                    v_tail->size(1) == Hkv && v_tail->size(2) == 8 && v_tail->size(3) == D &&
+                    v_tail->is_contiguous(),
+                "v_tail must be contiguous bf16 [slots, Hkv, 8, 128]");
+    TORCH_CHECK(num_decode >= 0 && num_decode <= T, "num_decode out of range");
+  }
   const c10::DeviceGuard g(qkv.device());
   akap::launch_qk_norm_rope_cache(
       qkv.data_ptr(), qkv.stride(0), q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
       positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
       q_w ? q_w->data_ptr() : nullptr, k_w ? k_w->data_ptr() : nullptr, T, Hq, Hkv, D, BS,
-      (float)eps, apply_rope ? 1 : 0, cur_stream(), kv_fp8_of(k_cache, v_cache), decode ? 1 : 0);
+      (float)eps, apply_rope ? 1 : 0, cur_stream(), kv_fp8_of(k_cache, v_cache), decode ? 1 : 0,
+      v_tail ? v_tail->data_ptr() : nullptr, v_tail ? tail_slot->data_ptr<int>() : nullptr,
+      (int)num_decode);
 }
 
 void reshape_and_cache(Tensor k, Tensor v, Tensor k_cache, Tensor v_cache, Tensor slots) {
@@ -103,6 +118,24 @@ void silu_and_mul(Tensor out, Tensor x) {
   const c10::DeviceGuard g(x.device());
   akap::launch_silu_and_mul(out.data_ptr(), x.data_ptr(), T, F,
                             x.dim() > 1 ? x.stride(-2) : 2 * F, cur_stream());
+}
+
+// V tail arguments: v_tail [slots, Hkv, 8, D] bf16 (a bf16 cache only), tail_slot int32 with
+// at least `rows` entries
+static void set_v_tail(akap::AttnParams& p, const std::optional<Tensor>& v_tail,
+                       const std::optional<Tensor>& tail_slot, int rows) {
+  p.v_tail = nullptr;
+  p.tail_slot = nullptr;
+  if (!v_tail) return;
+  TORCH_CHECK(tail_slot && tail_slot->scalar_type() == at::kInt && tail_slot->numel() >= rows,
+              "tail_slot: int32 with one entry per row");
+  TORCH_CHECK(v_tail->scalar_type() == at::kBFloat16 && v_tail->dim() == 4 &&
+                  v_tail->size(1) == p.Hkv && v_tail->size(2) == 8 && v_tail->size(3) == 128 &&
+                  v_tail->is_contiguous(),
+              "v_tail must be contiguous bf16 [slots, Hkv, 8, 128]");
+  TORCH_CHECK(!p.kv_fp8, "the V tail needs a bf16 KV cache");
+  p.v_tail = (__bf16*)v_tail->data_ptr();
+  p.tail_slot = tail_slot->data_ptr<int>();
 }
 
 int attn_flags() {
@@ -171,9 +204,11 @@ void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cach
 void paged_attention_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache,
                             Tensor block_tables, Tensor seq_lens, std::optional<Tensor> q_start,
                             Tensor part_m, Tensor part_l, Tensor part_o, int64_t num_parts,
-                            int64_t part_size, int64_t G, double scale) {
+                            int64_t part_size, int64_t G, double scale,
+                            std::optional<Tensor> v_tail, std::optional<Tensor> tail_slot) {
   auto p = attn_params(out, q, k_cache, v_cache, block_tables, seq_lens, G, scale);
   TORCH_CHECK(G <= 16, "decode kernel supports up to 16 q heads per kv head");
+  set_v_tail(p, v_tail, tail_slot, seq_lens.numel());
   TORCH_CHECK(part_size % 128 == 0 && part_size > 0, "part_size must be a multiple of 128");
   const int B = seq_lens.numel();
   p.q_start = q_start ? q_start->data_ptr<int>() : nullptr;
@@ -199,8 +234,10 @@ void paged_attention_decode_fused(Tensor out, Tensor qkv, Tensor k_cache, Tensor
                                   Tensor slots, Tensor cos_sin, std::optional<Tensor> q_w,
                                   std::optional<Tensor> k_w, Tensor part_m, Tensor part_l,
                                   Tensor part_o, int64_t num_parts, int64_t part_size, int64_t G,
-                                  double scale, double eps) {
+                                  double scale, double eps, std::optional<Tensor> v_tail,
+                                  std::optional<Tensor> tail_slot) {
   auto p = attn_params(out, out, k_cache, v_cache, block_tables, seq_lens, G, scale);
+  set_v_tail(p, v_tail, tail_slot, seq_lens.numel());
   CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv);
   TORCH_CHECK(G + 2 <= 16, "fused decode supports up to 14 q heads per kv head");
   TORCH_CHECK(part_size % 128 == 0 && part_size > 0, "part_size must be a multiple of 128");
@@ -858,7 +895,8 @@ TORCH_LIBRARY(akap, m) {
   m.def(
       "qk_norm_rope_cache(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, "
       "Tensor positions, Tensor slots, Tensor cos_sin, Tensor? q_w, Tensor? k_w, int Hq, int Hkv, "
-      "float eps, bool apply_rope, bool decode=False) -> ()");
+      "float eps, bool apply_rope, bool decode=False, Tensor(d!)? v_tail=None, "
+      "Tensor? tail_slot=None, int num_decode=0) -> ()");
   m.def("reshape_and_cache(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def(
@@ -868,12 +906,14 @@ TORCH_LIBRARY(akap, m) {
   m.def(
       "paged_attention_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_lens, Tensor? q_start, Tensor(b!) part_m, Tensor(c!) part_l, "
-      "Tensor(d!) part_o, int num_parts, int part_size, int G, float scale) -> ()");
+      "Tensor(d!) part_o, int num_parts, int part_size, int G, float scale, "
+      "Tensor? v_tail=None, Tensor? tail_slot=None) -> ()");
   m.def(
       "paged_attention_decode_fused(Tensor(a!) out, Tensor qkv, Tensor(b!) k_cache, "
       "Tensor(c!) v_cache, Tensor block_tables, Tensor seq_lens, Tensor positions, Tensor slots, "
       "Tensor cos_sin, Tensor? q_w, Tensor? k_w, Tensor(d!) part_m, Tensor(e!) part_l, "
-      "Tensor(f!) part_o, int num_parts, int part_size, int G, float scale, float eps) -> ()");
+      "Tensor(f!) part_o, int num_parts, int part_size, int G, float scale, float eps, "
+      "Tensor(g!)? v_tail=None, Tensor? tail_slot=None) -> ()");
   m.def(
       "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
       "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs, "

@@ -38,6 +38,8 @@ static BatchBuffers batch_buffers(const Scheduler& s, py::dict bufs) {
   b.top_k = ptr_of<int32_t>(bufs, "top_k", c.max_num_seqs);
   b.seeds = ptr_of<int64_t>(bufs, "seeds", c.max_num_seqs);
   b.steps = ptr_of<int32_t>(bufs, "steps", c.max_num_seqs);
+  b.tail_slot = bufs.contains("tail_slot") ? ptr_of<int32_t>(bufs, "tail_slot", b.cap_tokens)
+                                           : nullptr;
   return b;
 }
 
@@ -98,7 +100,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readwrite("mixed_batching", &SchedConfig::mixed_batching)
       .def_readwrite("mix_backlog_steps", &SchedConfig::mix_backlog_steps)
       .def_readwrite("max_decode_stall_steps", &SchedConfig::max_decode_stall_steps)
-      .def_readwrite("held_kv_ttl_s", &SchedConfig::held_kv_ttl_s);
+      .def_readwrite("held_kv_ttl_s", &SchedConfig::held_kv_ttl_s)
+      .def_readwrite("num_tail_slots", &SchedConfig::num_tail_slots);
 
   py::class_<Scheduler>(m, "Scheduler")
       .def(py::init<const SchedConfig&, int, bool>(), py::arg("config"), py::arg("num_blocks"),
@@ -172,6 +175,8 @@ PYBIND11_MODULE(_runtime, m) {
            py::arg("seed") = 0, py::arg("stream") = false)
       .def("activate", &Scheduler::activate)
       .def("set_first_token", &Scheduler::set_first_token)
+      .def("tail_slot", &Scheduler::tail_slot)
+      .def_property_readonly("num_free_tail_slots", &Scheduler::num_free_tail_slots)
       .def_property_readonly("total_preemptions", &Scheduler::total_preemptions)
       .def("request_info", [](const Scheduler& s, int64_t id) -> py::object {
         auto r = s.get(id);

@@ -10,6 +10,31 @@ Scheduler::Scheduler(const SchedConfig& cfg, int num_blocks, bool prefix_cache)
     : cfg_(cfg), bm_(num_blocks, cfg.block_size, prefix_cache) {
   if (cfg_.max_blocks_per_seq * cfg_.block_size < cfg_.max_model_len)
     throw std::invalid_argument("max_blocks_per_seq * block_size < max_model_len");
+  for (int i = cfg_.num_tail_slots - 1; i >= 0; --i) free_tails_.push_back(i);
+}
+
+int32_t Scheduler::tail_of(Request& r) {
+  if (r.tail_slot == -2) {
+    if (free_tails_.empty()) {
+      r.tail_slot = -1;  // no slot: this sequence keeps the plain V cache write path
+    } else {
+      r.tail_slot = free_tails_.back();
+      free_tails_.pop_back();
+    }
+  }
+  return r.tail_slot;
+}
+
+void Scheduler::drop_tail(Request& r) {
+  // a step still in flight may write the old slot: it runs before any step that hands the
+  // slot to another sequence (one stream), so the slot is free for reuse at once
+  if (r.tail_slot >= 0) free_tails_.push_back(r.tail_slot);
+  r.tail_slot = -2;
+}
+
+int Scheduler::tail_slot(int64_t id) {
+  auto it = reqs_.find(id);
+  return it == reqs_.end() ? -1 : tail_of(*it->second);
 }
 
 void Scheduler::add_request(int64_t id, const std::vector<int32_t>& prompt, int max_tokens,
@@ -152,6 +177,7 @@ void Scheduler::activate(int64_t id) {
   if (it == reqs_.end() || it->second->status != PENDING_KV) return;
   it->second->status = RUNNING;
   running_.push_back(it->second.get());
+  tail_of(*it->second);  // the engine fills the tail from the received KV right after
 }
 
 bool Scheduler::abort_request(int64_t id) {
@@ -179,6 +205,7 @@ void Scheduler::finish(Request& r, int reason) {
   }
   r.blocks.clear();
   r.hashes.clear();
+  drop_tail(r);
   r.status = FINISHED;
   r.finish = reason;
 }
@@ -209,6 +236,7 @@ void Scheduler::publish_full_blocks(Request& r) {
 
 void Scheduler::preempt(Request& r) {
   bm_.free_blocks(r.blocks);
+  drop_tail(r);  // recomputed from scratch: the prefill rewrites the tail of a new slot
   r.blocks.clear();
   r.hashes.clear();
   r.num_computed = 0;
@@ -366,6 +394,10 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
       buf.positions[T + j] = pos;
       buf.slots[T + j] = (int64_t)r->blocks[pos / bs] * bs + pos % bs;
     }
+    if (buf.tail_slot != nullptr) {
+      const int32_t ts = tail_of(*r);
+      for (int j = 0; j < q; ++j) buf.tail_slot[T + j] = ts;
+    }
     const int kv = start + q;
     buf.seq_lens[s] = kv;
     info.max_seq_len = std::max(info.max_seq_len, kv);
@@ -446,6 +478,7 @@ StepInfo Scheduler::schedule_lookahead(BatchBuffers& buf, int64_t* src_rows) {
     buf.positions[ns] = pos;
     buf.slots[ns] = (int64_t)r->blocks[pos / bs] * bs + pos % bs;
     buf.seq_lens[ns] = pos + 1;
+    if (buf.tail_slot != nullptr) buf.tail_slot[ns] = tail_of(*r);
     info.max_seq_len = std::max(info.max_seq_len, pos + 1);
     int32_t* row = buf.block_tables + (size_t)ns * mb;
     const int nb = (int)r->blocks.size();

@@ -53,6 +53,9 @@ struct Request {
   int64_t seed = 0;
   bool stream = false;  // report every token (else only first token + finish)
   bool hold_kv = false; // P/D prefill side: keep KV blocks after finishing (for transfer)
+  // V-tail slot (the GPU keeps this sequence's partial 8-token V group there): -2 = not yet
+  // assigned, -1 = none (pool empty / tails off); held from first schedule to finish/preempt
+  int tail_slot = -2;
   int num_generated() const { return (int)tokens.size() - num_prompt; }
 };
 
@@ -69,6 +72,7 @@ struct SchedConfig {
   int mix_backlog_steps = 1;       // mix when pending prefill <= this many steps' budget
   int max_decode_stall_steps = 8;  // ... or after this many prefill-only steps in a row
   double held_kv_ttl_s = 120.0;  // P/D: held KV never pulled by a decode engine is freed
+  int num_tail_slots = 0;        // V-tail slots (0: tails off, every row gets -1)
 };
 
 // Views into caller buffers (numpy, pinned).  Sizes are checked by the binding.
@@ -90,6 +94,7 @@ struct BatchBuffers {
   int32_t* top_k;
   int64_t* seeds;
   int32_t* steps;
+  int32_t* tail_slot;     // per token: its sequence's V-tail slot (nullptr: not staged)
   int cap_tokens, cap_tiles;
 };
 
@@ -174,6 +179,9 @@ class Scheduler {
   // P/D streamed hand-off: blocks are reserved (and filled chunk by chunk) before the prefill
   // has sampled the first token; it is set here, before activate()
   void set_first_token(int64_t id, int32_t tok);
+  // V-tail slot of a request (assigning one if it has none yet; -1 = no tail)
+  int tail_slot(int64_t id);
+  int num_free_tail_slots() const { return (int)free_tails_.size(); }
   size_t num_held() const { return held_.size(); }
   // free every held-KV entry whose deadline passed (schedule() calls it with the steady
   // clock); returns the number expired
@@ -189,6 +197,8 @@ class Scheduler {
   void publish_full_blocks(Request& r);
   void preempt(Request& r);
   void finish(Request& r, int reason);
+  int32_t tail_of(Request& r);
+  void drop_tail(Request& r);
 
   SchedConfig cfg_;
   BlockManager bm_;
@@ -209,6 +219,7 @@ class Scheduler {
   };
   std::unordered_map<int64_t, HeldKV> held_;
   std::unordered_map<int64_t, std::vector<int32_t>> in_transfer_;  // held KV being sent
+  std::vector<int32_t> free_tails_;  // V-tail slot pool (LIFO)
   int64_t preemptions_ = 0;
   int64_t held_expired_ = 0;
   int prefill_only_run_ = 0;

@@ -87,6 +87,7 @@ class LLMEngine:
         sc.mix_backlog_steps = ecfg.mix_backlog_steps
         sc.max_decode_stall_steps = ecfg.max_decode_stall_steps
         sc.held_kv_ttl_s = ecfg.held_kv_ttl_s
+        sc.num_tail_slots = self.runner.num_tail_slots
         self.sched = rt.Scheduler(sc, self.runner.num_blocks, ecfg.enable_prefix_caching)
         self.tokenizer = get_tokenizer(ecfg.weights_path, self.mcfg.vocab_size, self.mcfg.bos_id,
                                        self.mcfg.eos_id)
@@ -260,6 +261,13 @@ class LLMEngine:
     def activate(self, iid: int) -> None:
         with self._lock:
             self.sched.activate(int(iid))
+            if self.runner.v_tails is not None:
+                # the prompt's KV arrived whole: its partial last V group -> the V tail
+                info = self.sched.request_info(int(iid))
+                if info is not None:
+                    self.runner.fill_tail(self.sched.tail_slot(int(iid)),
+                                          self.sched.block_table(int(iid)),
+                                          int(info["num_computed"]))
 
     def _apply_aborts(self) -> None:
         with self._lock:

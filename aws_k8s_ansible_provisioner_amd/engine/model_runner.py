@@ -33,7 +33,7 @@ DEFAULT_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 2
 
 # per-step decode inputs (one row per sequence), staged together: see _stage_decode
 DECODE_FIELDS = ("input_ids", "positions", "slots", "seeds", "seq_lens", "temperature", "top_p",
-                 "top_k", "steps", "src_rows")
+                 "top_k", "steps", "src_rows", "tail_slot")
 
 
 class ModelRunner:
@@ -83,6 +83,15 @@ class ModelRunner:
         self.log(f"[runner] KV cache: {self.num_blocks} blocks x {self.bs} tokens "
                  f"({self.kv.numel() * self.kv.element_size() / 2**30:.1f} GiB, "
                  f"{'fp8 e4m3' if self.kv.dtype == torch.uint8 else 'bf16'})")
+        # V tail (see AttnParams.v_tail): one slot per live sequence (2x max_num_seqs, as P/D
+        # activations can briefly exceed it; a sequence without a slot uses the plain path)
+        self.v_tails: Optional[list] = None
+        self.num_tail_slots = 0
+        if self.v_tail_enabled():
+            self.num_tail_slots = 2 * self.max_seqs
+            self._tail = torch.zeros(mcfg.num_layers, self.num_tail_slots, self.model.hkv, 8,
+                                     self.model.D, dtype=torch.bfloat16, device=self.device)
+            self.v_tails = list(self._tail.unbind(0))
         # workspace sized for the finest split any bucket uses (256-token partitions)
         self.num_parts = max(1, math.ceil(ecfg.max_model_len / 128))
         self._alloc_buffers()
@@ -99,6 +108,26 @@ class ModelRunner:
         self.buckets: list[int] = []
         if self.is_gpu and not ecfg.enforce_eager and self.model.graph_safe:
             self.capture_graphs()
+
+    def v_tail_enabled(self) -> bool:
+        """Decode keeps each sequence's partial 8-token V group in a token-major tail and
+        writes the cache only in whole groups (csrc/kernels/attention.hip): GPU, bf16 KV
+        cache, fused decode attention.  AKAP_V_TAIL=0 restores the per-token cache write."""
+        from ..models import transformer as tfm
+
+        return (self.is_gpu and self.kv.dtype == torch.bfloat16 and tfm.FUSED_DECODE and
+                os.environ.get("AKAP_V_TAIL", "1") != "0" and
+                not (self.ecfg.kv_role == "decode" and self.ps.tp_size > 1))
+
+    def fill_tail(self, slot: int, block_table: list, n: int) -> None:
+        """A sequence whose KV arrived whole (P/D decode side): copy its partial last V group
+        (tokens [n & ~7, n)) from the cache into its tail before its first decode step."""
+        if self.v_tails is None or slot < 0 or n % 8 == 0:
+            return
+        g0, cnt = n & ~7, n % 8
+        blk, grp = int(block_table[g0 // self.bs]), (g0 % self.bs) // 8
+        for vt, vc in zip(self.v_tails, self.v_caches):
+            vt[slot, :, :cnt].copy_(vc[blk, :, grp, :, :cnt].transpose(-1, -2))
 
     # ------------------------------------------------------------------ sizing
     def _derive_num_blocks(self) -> int:
@@ -135,6 +164,8 @@ class ModelRunner:
             "top_k": (S, torch.int32), "seeds": (S, torch.int64), "steps": (S, torch.int32),
             # decode lookahead: in-flight row whose sampled token is this row's input
             "src_rows": (S, torch.int64),
+            # per token: its sequence's V-tail slot (-1: none)
+            "tail_slot": (T, torch.int32),
         }
         self.h = {k: self._pinned(n, dt) for k, (n, dt) in spec.items()}
         self.np = {k: v.numpy() for k, v in self.h.items()}
@@ -225,14 +256,14 @@ class ModelRunner:
 
     PREFILL_FIELDS = ("input_ids", "positions", "slots", "seq_lens", "q_start", "block_tables",
                       "tile_seq", "tile_row", "logits_idx", "temperature", "top_p", "top_k",
-                      "seeds", "steps")
+                      "seeds", "steps", "tail_slot")
 
     def _prefill_extents(self, info: dict) -> dict:
         T, B, nt, ns = info["num_tokens"], info["num_seqs"], info["num_tiles"], info["num_samples"]
         return {"input_ids": T, "positions": T, "slots": T, "seq_lens": B, "q_start": B + 1,
                 "block_tables": B * self.max_blocks, "tile_seq": nt, "tile_row": nt,
                 "logits_idx": ns, "temperature": ns, "top_p": ns, "top_k": ns, "seeds": ns,
-                "steps": ns}
+                "steps": ns, "tail_slot": T}
 
     def _stage_prefill(self, info: dict) -> dict:
         """The used prefix of every step buffer packed into ONE pinned region -> ONE H2D copy
@@ -281,7 +312,8 @@ class ModelRunner:
         nd = info.get("num_decode", 0)
         parts, ps = self.decode_partitions(nd) if nd else (1, 512)
         batch = AttnBatch(True, pos, slots, bt, sl, qs, ts, tr, parts, ps,
-                          self.workspace, tile_rows=self.tile_rows, num_decode=nd)
+                          self.workspace, tile_rows=self.tile_rows, num_decode=nd,
+                          v_tails=self.v_tails, tail_slot=v["tail_slot"])
         h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
         if ns == 0:
             # a chunk that samples nothing (a long prompt's inner chunk): the caller's
@@ -336,7 +368,8 @@ class ModelRunner:
             parts, ps = self.decode_partitions(n)
             batch = AttnBatch(False, dd["positions"][:n], dd["slots"][:n], self.dd_bt[:n],
                               dd["seq_lens"][:n], self.d["q_start"][:n + 1], None, None,
-                              parts, ps, self.workspace)
+                              parts, ps, self.workspace, v_tails=self.v_tails,
+                              tail_slot=dd["tail_slot"][:n])
             h = self.model.forward(dd["input_ids"][:n], batch, self.k_caches, self.v_caches)
         # sampler reads bf16 logits directly (no [n, V] fp32 cast pass)
         logits = self.model.compute_logits(h)
@@ -374,7 +407,8 @@ class ModelRunner:
                 parts, ps = self.decode_partitions(hi - lo)
                 batch = AttnBatch(False, dd["positions"][lo:hi], dd["slots"][lo:hi],
                                   self.dd_bt[lo:hi], dd["seq_lens"][lo:hi],
-                                  self.d["q_start"][:hi - lo + 1], None, None, parts, ps, ws)
+                                  self.d["q_start"][:hi - lo + 1], None, None, parts, ps, ws,
+                                  v_tails=self.v_tails, tail_slot=dd["tail_slot"][lo:hi])
                 out.append(self.model.forward(dd["input_ids"][lo:hi], batch, self.k_caches,
                                               self.v_caches))
         main.wait_stream(side)
@@ -406,6 +440,7 @@ class ModelRunner:
         npd["seeds"][B:n] = 0
         npd["steps"][B:n] = 0
         npd["src_rows"][B:n] = 0
+        npd["tail_slot"][B:n] = -1
 
     def execute_decode(self, info: dict) -> torch.Tensor:
         B = info["num_seqs"]

@@ -48,6 +48,10 @@ class AttnBatch:
     workspace: Optional[tuple] = None
     tile_rows: int = 64          # q rows per prefill tile of the map (128: flash-style kernel)
     num_decode: int = 0          # mixed step: leading single-token decode rows [0, num_decode)
+    # V tail (GPU, bf16 cache): per-layer [slots, Hkv, 8, D] partial-group buffers and the
+    # per-token (= per decode row) tail slot; None = the plain V cache write path
+    v_tails: Optional[list] = None
+    tail_slot: Optional[torch.Tensor] = None
 
 
 @dataclasses.dataclass
@@ -287,7 +291,7 @@ class DecoderLM:
         x = ops.embedding(ids, self.embed, vocab_start=self.vocab_start, vocab_end=self.vocab_end)
         return comm.tp_all_reduce(x)
 
-    def _attention(self, q, batch: AttnBatch, kc, vc, out):
+    def _attention(self, q, batch: AttnBatch, kc, vc, out, vt=None):
         if batch.is_prefill:
             nd = batch.num_decode
             if nd and q.is_cuda:
@@ -298,7 +302,8 @@ class DecoderLM:
                                            batch.seq_lens[:nd], self.hq // self.hkv,
                                            self.scale, workspace=batch.workspace,
                                            num_parts=batch.num_parts,
-                                           part_size=batch.part_size)
+                                           part_size=batch.part_size, v_tail=vt,
+                                           tail_slot=batch.tail_slot)
             ops.paged_attention_prefill(out, q, kc, vc, batch.block_tables, batch.seq_lens,
                                         batch.q_start, batch.tile_seq, batch.tile_row,
                                         self.hq // self.hkv, self.scale,
@@ -306,7 +311,8 @@ class DecoderLM:
         else:
             ops.paged_attention_decode(out, q, kc, vc, batch.block_tables, batch.seq_lens,
                                        self.hq // self.hkv, self.scale, workspace=batch.workspace,
-                                       num_parts=batch.num_parts, part_size=batch.part_size)
+                                       num_parts=batch.num_parts, part_size=batch.part_size,
+                                       v_tail=vt, tail_slot=batch.tail_slot)
         return out
 
     def forward(self, input_ids: torch.Tensor, batch: AttnBatch, k_caches, v_caches
@@ -335,19 +341,23 @@ class DecoderLM:
                 # the HBM-bound attention stream; the latency-bound GEMMs then hit cache
                 nxt = self.layers[li + 1].w_qkv if li + 1 < len(self.layers) else None
                 ops.l2_prefetch([lw.w_o, lw.w_gate_up, lw.w_down, nxt])
+            vt = batch.v_tails[li] if batch.v_tails is not None else None
             if not batch.is_prefill and FUSED_DECODE:
                 # q/k-norm + RoPE + KV-cache write fused into the decode attention kernel
                 ops.paged_attention_decode_fused(
                     attn, qkv, k_caches[li], v_caches[li], batch.block_tables, batch.seq_lens,
                     batch.positions, batch.slots, self.cos_sin, lw.q_norm, lw.k_norm,
                     self.hq // self.hkv, self.scale, eps, workspace=batch.workspace,
-                    num_parts=batch.num_parts, part_size=batch.part_size)
+                    num_parts=batch.num_parts, part_size=batch.part_size, v_tail=vt,
+                    tail_slot=batch.tail_slot)
             else:
                 q = torch.empty_like(attn)
                 ops.qk_norm_rope_cache(qkv, q, k_caches[li], v_caches[li], batch.positions,
                                        batch.slots, self.cos_sin, lw.q_norm, lw.k_norm, self.hq,
-                                       self.hkv, eps, True, decode=not batch.is_prefill)
-                self._attention(q, batch, k_caches[li], v_caches[li], attn)
+                                       self.hkv, eps, True, decode=not batch.is_prefill,
+                                       v_tail=vt, tail_slot=batch.tail_slot,
+                                       num_decode=batch.num_decode if batch.is_prefill else 0)
+                self._attention(q, batch, k_caches[li], v_caches[li], attn, vt)
             o = comm.tp_all_reduce(ops.linear(attn.view(T, self.hq * self.D), lw.w_o))
             h, residual = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             if lw.moe is not None:
@@ -396,7 +406,9 @@ class DecoderLM:
                 attn, qkv, k_caches[li], v_caches[li], batch.block_tables, batch.seq_lens,
                 batch.positions, batch.slots, self.cos_sin, lw.q_norm, lw.k_norm,
                 self.hq // self.hkv, self.scale, eps, workspace=batch.workspace,
-                num_parts=batch.num_parts, part_size=batch.part_size)
+                num_parts=batch.num_parts, part_size=batch.part_size,
+                v_tail=batch.v_tails[li] if batch.v_tails is not None else None,
+                tail_slot=batch.tail_slot)
             a2 = torch.empty_like(residual)
             if tp > 1:
                 part = ops.dgemm(attn.view(T, self.hq * self.D), lw.w_o, eps=eps, **c_o)

@@ -82,13 +82,18 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
 # ----------------------------------------------------------------------------- rope/cache
 def qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
                        num_q_heads: int, num_kv_heads: int, eps: float, apply_rope: bool = True,
-                       decode: bool = False):
+                       decode: bool = False, v_tail=None, tail_slot=None, num_decode: int = 0):
     """decode=True: one new token per sequence (V written per token instead of by the
-    prefill role's 64-token span scan)."""
+    prefill role's 64-token span scan).  v_tail / tail_slot (GPU, bf16 cache, span role):
+    tokens of a group still partial after this step also go to their sequence's V tail, and
+    a decode row (t < num_decode) completing a group writes the whole group from the tail
+    (csrc/kernels/rope_cache.hip); the CPU reference ignores the tail (its cache is always
+    complete)."""
     if _native(qkv):
         torch.ops.akap.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin,
                                           q_w, k_w, num_q_heads, num_kv_heads, eps, apply_rope,
-                                          decode)
+                                          decode, v_tail, tail_slot if v_tail is not None else None,
+                                          num_decode)
         return q_out
     ref.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
                            num_q_heads, num_kv_heads, eps, apply_rope)
@@ -130,7 +135,8 @@ def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_
 
 def paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens, gqa_group: int,
                            scale: float, workspace=None, num_parts: int = 1,
-                           part_size: int = 512, q_start=None):
+                           part_size: int = 512, q_start=None, v_tail=None, tail_slot=None):
+    """v_tail / tail_slot: a sequence's still-partial last V group is read from its tail."""
     if _native(q):
         if workspace is None:
             B = seq_lens.numel()
@@ -139,7 +145,8 @@ def paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens, gqa
         pm, pl, po = workspace
         torch.ops.akap.paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens,
                                               q_start, pm, pl, po, num_parts, part_size,
-                                              gqa_group, scale)
+                                              gqa_group, scale, v_tail,
+                                              tail_slot if v_tail is not None else None)
         return out
     if q_start is None:
         q_start = torch.arange(seq_lens.numel() + 1, dtype=torch.int32)
@@ -150,10 +157,11 @@ def paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens, gqa
 def paged_attention_decode_fused(out, qkv, k_cache, v_cache, block_tables, seq_lens, positions,
                                  slots, cos_sin, q_w, k_w, gqa_group: int, scale: float,
                                  eps: float, workspace=None, num_parts: int = 1,
-                                 part_size: int = 512):
+                                 part_size: int = 512, v_tail=None, tail_slot=None):
     """Decode attention that consumes the raw QKV projection: per-head q/k RMSNorm + RoPE
     and the new token's K/V cache write happen inside the attention kernel.
-    out [B, Hq, D]; qkv [B, (Hq + 2 Hkv) * D]."""
+    out [B, Hq, D]; qkv [B, (Hq + 2 Hkv) * D].  With v_tail (bf16 cache) the new token's V
+    goes to its sequence's tail row and the cache gets whole 8-token groups only."""
     if _native(qkv):
         if workspace is None:
             workspace = decode_workspace(seq_lens.numel(), k_cache.shape[1], gqa_group,
@@ -162,7 +170,8 @@ def paged_attention_decode_fused(out, qkv, k_cache, v_cache, block_tables, seq_l
         torch.ops.akap.paged_attention_decode_fused(out, qkv, k_cache, v_cache, block_tables,
                                                     seq_lens, positions, slots, cos_sin, q_w, k_w,
                                                     pm, pl, po, num_parts, part_size, gqa_group,
-                                                    scale, eps)
+                                                    scale, eps, v_tail,
+                                                    tail_slot if v_tail is not None else None)
         return out
     B, Hq = out.shape[0], out.shape[1]
     q = torch.empty_like(out)

@@ -172,8 +172,9 @@ class OpenAIServer:
                 return {"status": "ok"}
             # P/D: a broken KV channel is rebuilt by the decode side (/kv/reset); until then
             # the gateway's picker keeps this pair out of P/D routing
-            return {"status": "ok", "kv_channel": "broken" if ag.broken else "ok",
-                    "kv_generation": ag.generation}
+            broken = getattr(ag, "broken", None)
+            return {"status": "ok", "kv_channel": "broken" if broken else "ok",
+                    "kv_generation": getattr(ag, "generation", 0)}
 
         @app.get("/ready")
         async def ready():
@@ -223,7 +224,7 @@ class OpenAIServer:
             if grp is not None and self.ae.pd_group is not None and grp != self.ae.pd_group:
                 return _err(409, f"P/D group mismatch: decode {grp} vs prefill "
                                  f"{self.ae.pd_group}", "Conflict")
-            if self.ae.kv_agent.broken is not None:
+            if getattr(self.ae.kv_agent, "broken", None) is not None:
                 # the decode side rebuilds the channel (/kv/reset) and retries later requests
                 return _err(503, f"KV channel broken: {self.ae.kv_agent.broken}",
                             "KVChannelBroken")

@@ -125,7 +125,8 @@ class KVPuller:
                 AsyncEngine._release_remote(j.kvp)
                 self._resolve(j, e)
             agent = self.ae.kv_agent
-            if agent.broken is not None or "KVChannelBroken" in _http_error_text(e):
+            if (getattr(agent, "broken", None) is not None or
+                    "KVChannelBroken" in _http_error_text(e)):
                 # a timed-out transfer left stale ops in the channel (ours or the prefill
                 # side's): rebuild it on both sides so the NEXT request on this pair works
                 self.ae.rebuild_channel(url)

@@ -845,3 +845,75 @@ def test_paged_attention_prefill_deep_context():
                                 qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv, scale,
                                 tile_rows=128)
     _close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+def _v_tokens(vc, bt, s, n, bs=32):
+    """[n, Hkv, D] V rows of sequence s's first n tokens from a [NB, Hkv, BS/8, D, 8] cache."""
+    rows = []
+    for p in range(n):
+        b = int(bt[s, p // bs])
+        rows.append(vc[b, :, (p % bs) // 8, :, p % 8])
+    return torch.stack(rows)
+
+
+@pytest.mark.parametrize("num_parts,part_size", [(1, 4096), (3, 512)])
+def test_v_tail_decode_matches_the_plain_cache_path(num_parts, part_size):
+    """V tail (AttnParams.v_tail): decode steps write the new token's V to its sequence's
+    tail and whole 8-token groups to the cache; readers take the partial group from the tail.
+    Against a twin cache on the plain per-token path, over 20 steps (fused steps, plus mixed
+    steps through the writer kernel + the plain decode kernel): bit-identical attention
+    outputs, and identical V for every completed group."""
+    hq, hkv, D, BS = 16, 8, 128, 32
+    lens = [1, 5, 8, 13, 31, 200, 777]
+    steps = 20
+    seqs = [(kv + steps, 1) for kv in lens]  # blocks for the prompt + every decode token
+    _, kc, vc, bt, _, _ = _setup_attn(seqs, hq, hkv, BS, seed=7)
+    B, G = len(lens), hq // hkv
+    g = torch.Generator().manual_seed(3)
+    cs = ref.rope_cos_sin(4096, D, 1e6).to(DEV)
+    qw = torch.randn(D, generator=g).bfloat16().to(DEV)
+    kw = torch.randn(D, generator=g).bfloat16().to(DEV)
+    btg = bt.to(DEV)
+    kA, vA = kc.to(DEV), vc.to(DEV)
+    kB, vB = kA.clone(), vA.clone()
+    tail = torch.zeros(B, hkv, 8, D, dtype=torch.bfloat16, device=DEV)
+    tslot = torch.arange(B, dtype=torch.int32, device=DEV)
+    for s, n in enumerate(lens):  # the prompt's partial group -> tail (like fill_tail)
+        g0 = n & ~7
+        for p in range(g0, n):
+            b = int(bt[s, p // BS])
+            tail[s, :, p - g0] = vB[b, :, (p % BS) // 8, :, p % 8]
+    scale = 1 / math.sqrt(D)
+    cur = list(lens)
+    for step in range(steps):
+        pos = torch.tensor(cur, dtype=torch.int64)
+        slots = torch.tensor([int(bt[s, cur[s] // BS]) * BS + cur[s] % BS for s in range(B)],
+                             dtype=torch.int64).to(DEV)
+        sl = torch.tensor([c + 1 for c in cur], dtype=torch.int32, device=DEV)
+        qkv = torch.randn(B, (hq + 2 * hkv) * D, generator=g).bfloat16().to(DEV)
+        outs = []
+        for kcache, vcache, vt in ((kA, vA, None), (kB, vB, tail)):
+            out = torch.empty(B, hq, D, dtype=torch.bfloat16, device=DEV)
+            ws = ops.decode_workspace(B, hkv, G, num_parts, DEV)
+            if step % 5 == 4:  # a mixed step: writer kernel (span role) + plain decode kernel
+                q = torch.empty(B, hq, D, dtype=torch.bfloat16, device=DEV)
+                ops.qk_norm_rope_cache(qkv, q, kcache, vcache, pos.to(DEV), slots, cs, qw, kw,
+                                       hq, hkv, 1e-6, True, decode=False, v_tail=vt,
+                                       tail_slot=tslot, num_decode=B)
+                ops.paged_attention_decode(out, q, kcache, vcache, btg, sl, G, scale,
+                                           workspace=ws, num_parts=num_parts,
+                                           part_size=part_size, v_tail=vt, tail_slot=tslot)
+            else:
+                ops.paged_attention_decode_fused(out, qkv, kcache, vcache, btg, sl, pos.to(DEV),
+                                                 slots, cs, qw, kw, G, scale, 1e-6, workspace=ws,
+                                                 num_parts=num_parts, part_size=part_size,
+                                                 v_tail=vt, tail_slot=tslot)
+            outs.append(out)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), (step, (outs[0].float() - outs[1].float()).abs().max())
+        cur = [c + 1 for c in cur]
+    vA_, vB_ = vA.cpu(), vB.cpu()
+    for s, n in enumerate(cur):
+        full = n & ~7
+        assert torch.equal(_v_tokens(vA_, bt, s, full), _v_tokens(vB_, bt, s, full)), s
+    assert torch.equal(kA, kB)

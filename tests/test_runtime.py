@@ -430,3 +430,51 @@ if given is not None:
         ref_out, _, _ = _drive(False, prompts, mt, ie, num_blocks, max_seqs)
         got, _, _ = _drive(True, prompts, mt, ie, num_blocks, max_seqs)
         assert got == ref_out
+
+
+def test_v_tail_slots_follow_each_sequence_and_return_to_the_pool():
+    """V-tail slots (AttnParams.v_tail): every token row carries its sequence's slot, a slot
+    is stable while the sequence runs, and finish / abort / preemption hand it back."""
+    c = rt.SchedConfig()
+    c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = 4, 32, 32
+    c.block_size, c.gqa_group, c.tile_rows, c.eos_id = 4, 2, 64, 2
+    c.max_blocks_per_seq, c.num_tail_slots = 8, 8
+    s = rt.Scheduler(c, 6, True)
+    b = _bufs(4, 36, 8)
+    b["tail_slot"] = np.full(36, -7, np.int32)
+    s.add_request(1, list(range(3, 11)), 12)
+    s.add_request(2, list(range(13, 20)), 12)
+    s.add_request(3, list(range(23, 31)), 12)
+    i = s.schedule(b)
+    seen = {}
+    for r in range(i["num_seqs"]):
+        a, e = int(b["q_start"][r]), int(b["q_start"][r + 1])
+        ts = set(b["tail_slot"][a:e].tolist())
+        assert len(ts) == 1 and min(ts) >= 0
+        seen[int(b["req_ids"][r])] = ts.pop()
+    assert len(set(seen.values())) == len(seen)  # distinct slots
+    s.update(np.full(i["num_samples"], 4, np.int64))
+    preempted = 0
+    for _ in range(200):
+        if not s.has_work():
+            break
+        i = s.schedule(b)
+        preempted += i["num_preempted"]
+        for r in range(i["num_seqs"]):
+            rid, t = int(b["req_ids"][r]), int(b["tail_slot"][int(b["q_start"][r])])
+            assert t >= 0
+            if preempted == 0:  # stable while it runs (a recomputed sequence may move)
+                assert seen.setdefault(rid, t) == t
+        s.update(np.full(i["num_samples"], 4, np.int64))
+    assert preempted >= 1  # the 6-block pool cannot hold all three: one was recomputed
+    assert s.num_free_tail_slots == 8
+    # abort hands the slot back too; a scheduler without slots stages -1
+    s.add_request(9, [5, 6, 7], 4)
+    s.schedule(b)
+    assert s.num_free_tail_slots == 7 and s.abort_request(9)
+    assert s.num_free_tail_slots == 8
+    s0, b0 = _sched()
+    b0["tail_slot"] = np.zeros(20, np.int32)
+    s0.add_request(1, [5, 6, 7], 4)
+    s0.schedule(b0)
+    assert b0["tail_slot"][:3].tolist() == [-1, -1, -1]
