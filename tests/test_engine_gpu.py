@@ -251,3 +251,46 @@ def test_microbatched_decode_matches_single_stream(monkeypatch):
     # the numerics test)
     same = sum(a == b for a, b in zip(res["0"], res["1"]))
     assert same >= 0.6 * len(prompts), same
+
+
+def test_pd_handoff_fills_the_v_tail_and_decodes_correctly():
+    """P/D decode side on the GPU with the V tail: the prompt KV arrives as whole blocks
+    (copied engine to engine in process here, in place of the RCCL transfer), activate()
+    copies each prompt's partial last V group into the sequence's tail, and decoding from
+    there stays teacher-forced against the dense reference."""
+    pe = _engine("tiny-qwen3", kv_role="prefill")
+    de = _engine("tiny-qwen3", kv_role="decode")
+    assert de.runner.v_tails is not None
+    prompts = [list(range(5, 50)), [100, 101, 102], list(range(200, 271)), list(range(9, 41))]
+    params = SamplingParams(max_tokens=10, temperature=0, ignore_eos=True)
+    for p in prompts:
+        pe.add_request(None, None, params, prompt_ids=p,
+                       kv_transfer_params={"do_remote_decode": True})
+    done = []
+    while pe.has_unfinished():
+        done += [o for o in pe.step() if o.finished and o.kv_transfer_params]
+    assert len(done) == len(prompts)
+    bs = de.ecfg.block_size
+    for o in done:
+        tid = int(o.kv_transfer_params["transfer_id"])
+        bp = pe.take_held(tid)
+        iid, bd = de.reserve_prefilled(f"pd-{tid}", list(o.prompt_ids), int(o.output_ids[0]),
+                                       params)
+        assert len(bd) == len(bp)
+        de.runner.kv[:, :, torch.tensor(bd)] = pe.runner.kv[:, :, torch.tensor(bp)]
+        pe.finish_transfer(tid)
+        de.activate(iid)
+        n = len(o.prompt_ids)
+        slot, cnt = de.sched.tail_slot(iid), n % 8
+        assert slot >= 0
+        if cnt:  # the tail holds exactly the cache's partial group
+            blk, grp = bd[(n & ~7) // bs], ((n & ~7) % bs) // 8
+            for vt, vc in zip(de.runner.v_tails, de.runner.v_caches):
+                assert torch.equal(vt[slot, :, :cnt], vc[blk, :, grp, :, :cnt].transpose(-1, -2))
+    outs = []
+    while de.has_unfinished():
+        outs += [o for o in de.step() if o.finished]
+    assert len(outs) == len(prompts)
+    for o in outs:
+        assert len(o.output_ids) == 10
+        _check_teacher_forced(de, o.prompt_ids, o.output_ids)
