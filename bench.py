@@ -61,9 +61,12 @@ def parse():
     ap.add_argument("--mode", default="mono", choices=["mono", "pd"],
                     help="mono: every rank a monolithic replica (DP); pd: ranks [0,W/2) prefill, "
                          "[W/2,W) decode, KV handed over RCCL (Llama-3-8B disagg config)")
-    ap.add_argument("--pd-push", default="chunked", choices=["chunked", "whole"],
+    ap.add_argument("--pd-push", default="auto", choices=["auto", "chunked", "whole"],
                     help="--mode pd: stream each prompt's KV chunk by chunk while the prefill "
-                         "continues (default), or hand the whole prompt over at its end")
+                         "continues, or hand the whole prompt over at its end.  auto: chunked "
+                         "on RCCL, whole on a host-staged gloo channel, where the transfer is "
+                         "the bottleneck and per-chunk sends only add overhead "
+                         "(profiles/r3_pd_push_gpu_gloo.log)")
     ap.add_argument("--dist-backend", default=None,
                     help="override (gloo = single-GPU rehearsal of the multi-rank paths)")
     ap.add_argument("--arrival-rate", type=float, default=0.0,
@@ -188,7 +191,9 @@ def main() -> int:
         if pd:
             if is_prefill:
                 prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
-                pair.run_prefill(prompts, sp, chunked=a.pd_push == "chunked")
+                chunked = a.pd_push == "chunked" or (a.pd_push == "auto" and
+                                                     dist.get_backend() != "gloo")
+                pair.run_prefill(prompts, sp, chunked=chunked)
                 return 0, []
             r = pair.run_decode(sp, time.time())
             return r["output_tokens"], r["ttft"]
