@@ -400,8 +400,11 @@ class DecoderLM:
         a1 = ops.rms_norm(residual, self.layers[0].ln1, eps)
         ss_in = None
         for li, lw in enumerate(self.layers):
+            nxt = self.layers[li + 1].w_qkv if li + 1 < L else None
             qkv = ops.dgemm(a1, lw.w_qkv, eps=eps, ss_in=ss_in, **c_qkv)
             attn = torch.empty(T, self.hq, self.D, dtype=self.dtype, device=self.device)
+            if PREFETCH_WEIGHTS:  # A/B knob: warm the layer's remaining weights in MALL
+                ops.l2_prefetch([lw.w_o, lw.w_gate_up, lw.w_down, nxt])
             ops.paged_attention_decode_fused(
                 attn, qkv, k_caches[li], v_caches[li], batch.block_tables, batch.seq_lens,
                 batch.positions, batch.slots, self.cos_sin, lw.q_norm, lw.k_norm,
