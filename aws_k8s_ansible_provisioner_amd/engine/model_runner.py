@@ -69,6 +69,10 @@ class ModelRunner:
         # GPU kernel (AKAP_PREFILL_FA=0: the 64-row per-wave kernel)
         self.tile_rows = 128 if (dev == "cuda" and
                                  os.environ.get("AKAP_PREFILL_FA", "1") != "0") else 64
+        if dev == "cuda" and os.environ.get("AKAP_PREFILL_TILE_ROWS") in ("64", "128", "256"):
+            self.tile_rows = int(os.environ["AKAP_PREFILL_TILE_ROWS"])  # A/B knob
+            if self.tile_rows == 256 and ecfg.kv_cache_dtype.startswith("fp8"):
+                self.tile_rows = 128  # the 256-row kernel needs a bf16 KV cache
         self.cap_tiles = self.cap_tokens * self.G // 64 + self.max_seqs + 1
         self.num_blocks = ecfg.num_gpu_blocks or self._derive_num_blocks()
         if self.ps.tp_size > 1:  # every TP rank must address the same block pool
