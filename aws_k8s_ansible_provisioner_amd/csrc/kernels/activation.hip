@@ -5,15 +5,18 @@
 
 namespace akap {
 
+// IDX: int for grids below 2^31 vectors (the common case: a 64-bit division is a ~40-instruction
+// software sequence per element -- 13.8 us instead of ~5 us at Llama-3-8B decode, 256 x 14336)
+template <typename IDX>
 __global__ __launch_bounds__(256) void silu_and_mul_kernel(bf16* __restrict__ out,
-                                                            const bf16* __restrict__ in, long T,
+                                                            const bf16* __restrict__ in, IDX T,
                                                             int F, int in_stride) {
-  const int vpr = F / 8;  // vectors per row
-  const long total = T * vpr;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long t = i / vpr;
-    const int c = (int)(i % vpr) * 8;
-    const bf16* row = in + t * in_stride;
+  const IDX vpr = F / 8;  // vectors per row
+  const IDX total = T * vpr;
+  for (IDX i = (IDX)blockIdx.x * 256 + threadIdx.x; i < total; i += (IDX)gridDim.x * 256) {
+    const IDX t = i / vpr;
+    const int c = (int)(i - t * vpr) * 8;
+    const bf16* row = in + (size_t)t * in_stride;
     bf16x8 g = *reinterpret_cast<const bf16x8*>(row + c);
     bf16x8 u = *reinterpret_cast<const bf16x8*>(row + F + c);
     bf16x8 o;
@@ -24,7 +27,7 @@ __global__ __launch_bounds__(256) void silu_and_mul_kernel(bf16* __restrict__ ou
       const float sx = bf2f(f2bf(x / (1.f + __expf(-x))));
       o[j] = f2bf(sx * bf2f(u[j]));
     }
-    *reinterpret_cast<bf16x8*>(out + t * F + c) = o;
+    *reinterpret_cast<bf16x8*>(out + (size_t)t * F + c) = o;
   }
 }
 
@@ -33,7 +36,12 @@ void launch_silu_and_mul(void* out, const void* in, long T, int F, int in_stride
   const long total = T * (F / 8);
   long blocks = (total + 255) / 256;
   if (blocks > 256 * 16) blocks = 256 * 16;
-  silu_and_mul_kernel<<<(int)blocks, 256, 0, s>>>((bf16*)out, (const bf16*)in, T, F, in_stride);
+  if (total < (1L << 31) - 256L * 4096)
+    silu_and_mul_kernel<int><<<(int)blocks, 256, 0, s>>>((bf16*)out, (const bf16*)in, (int)T, F,
+                                                         in_stride);
+  else
+    silu_and_mul_kernel<long><<<(int)blocks, 256, 0, s>>>((bf16*)out, (const bf16*)in, T, F,
+                                                          in_stride);
 }
 
 }  // namespace akap

@@ -298,19 +298,21 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
 // S is a template parameter so the S slab loads of an element issue back to back: with a
 // runtime trip count hipcc waited on each load before the next (S dependent L2/HBM round
 // trips, ~4.5 us at S = 4 in profiles/r1_qwen3_bench_v6_kernel_stats.md).
-template <int SCALE, int EPI, int S>
+// IDX: 32-bit element indexing whenever M*N fits (decode sizes always do) -- the 64-bit
+// division per element otherwise costs more than the slab reads
+template <int SCALE, int EPI, int S, typename IDX = int>
 __global__ __launch_bounds__(256) void dgemm_reduce_kernel(DGemmArgs p) {
   const int M = p.M, N = p.N;
-  const long total = (long)M * N / 4;
+  const IDX total = (IDX)M * N / 4;
   const float* ws = p.ws;
   const float* ssw = ws + (size_t)S * M * N;
   bf16* Y = static_cast<bf16*>(p.Y);
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long e = i * 4;
+  for (IDX i = (IDX)blockIdx.x * 256 + threadIdx.x; i < total; i += (IDX)gridDim.x * 256) {
+    const IDX e = i * 4;
     f32x4 part[S];
 #pragma unroll
     for (int z = 0; z < S; ++z) part[z] = *reinterpret_cast<const f32x4*>(ws + (size_t)z * M * N + e);
-    const int row = (int)(e / N), col = (int)(e % N);
+    const int row = (int)(e / N), col = (int)(e - (IDX)row * N);
     float scale = 1.f;
     if constexpr (SCALE == 1) {
       float q[S];
@@ -394,14 +396,22 @@ static void dgemm_main(const DGemmArgs& p, dim3 grid, int pro, int epi, int pf, 
   }
 }
 
+template <int SCALE, int EPI, typename IDX>
+static void reduce_s_idx(const DGemmArgs& p, int splitk, int blocks, hipStream_t st) {
+  switch (splitk) {
+    case 2: dgemm_reduce_kernel<SCALE, EPI, 2, IDX><<<blocks, 256, 0, st>>>(p); break;
+    case 4: dgemm_reduce_kernel<SCALE, EPI, 4, IDX><<<blocks, 256, 0, st>>>(p); break;
+    case 8: dgemm_reduce_kernel<SCALE, EPI, 8, IDX><<<blocks, 256, 0, st>>>(p); break;
+    default: dgemm_reduce_kernel<SCALE, EPI, 16, IDX><<<blocks, 256, 0, st>>>(p); break;
+  }
+}
+
 template <int SCALE, int EPI>
 static void reduce_s(const DGemmArgs& p, int splitk, int blocks, hipStream_t st) {
-  switch (splitk) {
-    case 2: dgemm_reduce_kernel<SCALE, EPI, 2><<<blocks, 256, 0, st>>>(p); break;
-    case 4: dgemm_reduce_kernel<SCALE, EPI, 4><<<blocks, 256, 0, st>>>(p); break;
-    case 8: dgemm_reduce_kernel<SCALE, EPI, 8><<<blocks, 256, 0, st>>>(p); break;
-    default: dgemm_reduce_kernel<SCALE, EPI, 16><<<blocks, 256, 0, st>>>(p); break;
-  }
+  if ((long)p.M * p.N + 4L * blocks * 256 < (1L << 31))
+    reduce_s_idx<SCALE, EPI, int>(p, splitk, blocks, st);
+  else
+    reduce_s_idx<SCALE, EPI, long>(p, splitk, blocks, st);
 }
 
 bool dgemm_splitk_ok(int splitk) {

@@ -12,8 +12,16 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int64_t* __restric
   const int vpr = d / 8;
   const long total = (long)T * vpr;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int t = (int)(i / vpr);
-    const int c = (int)(i % vpr) * 8;
+    // 32-bit split whenever the index fits (total < 2^30 here in practice): a 64-bit
+    // division per element is a long software sequence
+    int t, c;
+    if (total < (1L << 30)) {
+      t = (int)i / vpr;
+      c = ((int)i - t * vpr) * 8;
+    } else {
+      t = (int)(i / vpr);
+      c = (int)(i % vpr) * 8;
+    }
     const int64_t id = ids[t];
     bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (id >= vs && id < ve) v = *reinterpret_cast<const bf16x8*>(table + (id - vs) * d + c);

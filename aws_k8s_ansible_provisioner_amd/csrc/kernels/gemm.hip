@@ -182,7 +182,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     const long e = i * 4;
     f32x4 s = *reinterpret_cast<const f32x4*>(ws + e);
     for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(ws + (size_t)z * M * N + e);
-    const int row = (int)(e / N), col = (int)(e % N);
+    // 32-bit row/col split when the slab fits (a 64-bit division is a long software sequence)
+    int row, col;
+    if (total < (1L << 29)) {
+      row = (int)e / N;
+      col = (int)e - row * N;
+    } else {
+      row = (int)(e / N);
+      col = (int)(e % N);
+    }
     bf16x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = f2bf(s[j]);

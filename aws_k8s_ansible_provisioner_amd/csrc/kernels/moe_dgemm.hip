@@ -186,8 +186,14 @@ __global__ __launch_bounds__(256) void moe_combine_split_kernel(const float* __r
   const int vpr = d / 8;
   const long total = (long)T * vpr;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int t = (int)(i / vpr);
-    const int c = (int)(i % vpr) * 8;
+    int t, c;  // 32-bit split when it fits (no 64-bit division per element)
+    if (total < (1L << 30)) {
+      t = (int)i / vpr;
+      c = ((int)i - t * vpr) * 8;
+    } else {
+      t = (int)(i / vpr);
+      c = (int)(i % vpr) * 8;
+    }
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int k = 0; k < topk; ++k) {
       const int pos = inv[(size_t)t * topk + k];

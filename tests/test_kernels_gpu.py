@@ -27,8 +27,8 @@ def _close(a, b, atol, rtol=0.0):
     assert bool((err <= lim).all()), f"max err {err.max().item():.4g} (atol {atol})"
 
 
-@pytest.mark.parametrize("d", [128, 1024, 4096, 8192, 1000])
-@pytest.mark.parametrize("rows", [1, 7, 300])
+@pytest.mark.parametrize("d", [128, 1024, 2048, 4096, 6144, 8192, 1000])
+@pytest.mark.parametrize("rows", [1, 7, 300, 1025])
 def test_rmsnorm(d, rows):
     torch.manual_seed(0)
     x = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16)
@@ -37,7 +37,7 @@ def test_rmsnorm(d, rows):
     _close(out, ref.rms_norm(x.cpu(), w.cpu(), 1e-6), atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("d", [1024, 4096])
+@pytest.mark.parametrize("d", [1024, 4096, 8192])
 def test_fused_add_rmsnorm(d):
     torch.manual_seed(1)
     x = torch.randn(33, d, device=DEV, dtype=torch.bfloat16)
@@ -48,7 +48,7 @@ def test_fused_add_rmsnorm(d):
     _close(out, ref.rms_norm(r_ref, torch.ones(d, dtype=torch.bfloat16), 1e-5), atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("T,F", [(1, 3072), (37, 3072), (513, 14336)])
+@pytest.mark.parametrize("T,F", [(1, 3072), (37, 3072), (256, 14336), (513, 14336)])
 def test_silu_and_mul(T, F):
     x = torch.randn(T, 2 * F, device=DEV, dtype=torch.bfloat16)
     _close(ops.silu_and_mul(x), ref.silu_and_mul(x.cpu()), atol=2e-2, rtol=1e-2)
