@@ -396,6 +396,77 @@ static void dgemm_main(const DGemmArgs& p, dim3 grid, int pro, int epi, int pf, 
   }
 }
 
+// Row-parallel RESNORM reduce for decode shapes (N = NI x 1024, M <= 1024): one workgroup per
+// output row, every slab / residual / norm-weight load of the row issued before any store, the
+// row's sum of squares reduced in LDS and added with ONE atomic per row (the element-parallel
+// form issues N/256 same-address atomics per row and waits on its loads element by element:
+// 11-14 us for Llama-3-8B's O / down at M = 256, profiles/r3_llama8b_kernel_stats_v2.md).
+template <int SCALE, int S, int NI>
+__global__ __launch_bounds__(256) void dgemm_reduce_resnorm_row_kernel(DGemmArgs p) {
+  __shared__ float scratch[16];
+  const int M = p.M, N = p.N, row = blockIdx.x;
+  const float* ws = p.ws;
+  bf16* Y = static_cast<bf16*>(p.Y);
+  const bf16* lno = static_cast<const bf16*>(p.ln_out);
+  float scale = 1.f;
+  if constexpr (SCALE == 2) scale = rsqrtf(p.ss_in[row] / (float)p.K + p.eps);
+  f32x4 acc[NI];
+  bf16x4 old[NI], g[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int c = k * 1024 + threadIdx.x * 4;
+    const size_t e = (size_t)row * N + c;
+    f32x4 part[S];
+#pragma unroll
+    for (int z = 0; z < S; ++z) part[z] = *reinterpret_cast<const f32x4*>(ws + (size_t)z * M * N + e);
+    old[k] = *reinterpret_cast<const bf16x4*>(Y + (size_t)row * p.ldy + c);
+    g[k] = *reinterpret_cast<const bf16x4*>(lno + c);
+    acc[k] = part[0];
+#pragma unroll
+    for (int z = 1; z < S; ++z) acc[k] += part[z];
+  }
+  float q2 = 0.f;
+  bf16* Ao = static_cast<bf16*>(p.Aout);
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int c = k * 1024 + threadIdx.x * 4;
+    bf16x4 o, a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = f2bf(bf2f(f2bf(acc[k][j] * scale)) + bf2f(old[k][j]));
+      const float f = bf2f(o[j]);
+      a[j] = f2bf(f * bf2f(g[k][j]));
+      q2 += f * f;
+    }
+    *reinterpret_cast<bf16x4*>(Y + (size_t)row * p.ldy + c) = o;
+    *reinterpret_cast<bf16x4*>(Ao + (size_t)row * N + c) = a;
+  }
+  q2 = block_sum(q2, scratch);
+  if (threadIdx.x == 0) atomicAdd(p.ss_out + row, q2);
+}
+
+template <int SCALE, int S>
+static bool reduce_row_ni(const DGemmArgs& p, hipStream_t st) {
+  switch (p.N / 1024) {
+    case 1: dgemm_reduce_resnorm_row_kernel<SCALE, S, 1><<<p.M, 256, 0, st>>>(p); return true;
+    case 2: dgemm_reduce_resnorm_row_kernel<SCALE, S, 2><<<p.M, 256, 0, st>>>(p); return true;
+    case 4: dgemm_reduce_resnorm_row_kernel<SCALE, S, 4><<<p.M, 256, 0, st>>>(p); return true;
+    case 8: dgemm_reduce_resnorm_row_kernel<SCALE, S, 8><<<p.M, 256, 0, st>>>(p); return true;
+    default: return false;
+  }
+}
+
+template <int SCALE>
+static bool reduce_row(const DGemmArgs& p, int splitk, hipStream_t st) {
+  if (p.N % 1024 || p.M > 1024) return false;
+  switch (splitk) {
+    case 2: return reduce_row_ni<SCALE, 2>(p, st);
+    case 4: return reduce_row_ni<SCALE, 4>(p, st);
+    case 8: return p.N <= 4096 && reduce_row_ni<SCALE, 8>(p, st);  // keep the slab registers < 256
+    default: return false;
+  }
+}
+
 template <int SCALE, int EPI, typename IDX>
 static void reduce_s_idx(const DGemmArgs& p, int splitk, int blocks, hipStream_t st) {
   switch (splitk) {
@@ -424,8 +495,11 @@ void launch_dgemm_reduce(const DGemmArgs& p, int pro, int splitk, hipStream_t st
   const int b = (int)blocks;
   const int scale = pro == PRO_ADDNORM ? 1 : (pro == PRO_PLAIN && p.ss_in ? 2 : 0);
   if (p.epi == EPI_RESNORM) {
-    if (scale == 2) reduce_s<2, EPI_RESNORM>(p, splitk, b, st);
-    else reduce_s<0, EPI_RESNORM>(p, splitk, b, st);
+    if (scale == 2) {
+      if (!reduce_row<2>(p, splitk, st)) reduce_s<2, EPI_RESNORM>(p, splitk, b, st);
+    } else {
+      if (!reduce_row<0>(p, splitk, st)) reduce_s<0, EPI_RESNORM>(p, splitk, b, st);
+    }
   } else if (scale == 1) {
     reduce_s<1, EPI_STORE>(p, splitk, b, st);
   } else if (scale == 2) {

@@ -650,7 +650,8 @@ def test_fused_decode_gemm_in_graph():
 @pytest.mark.parametrize("M,N,K,splitk", [(1, 256, 1024, 1), (37, 1024, 2048, 2),
                                           (256, 4096, 1024, 1), (130, 1024, 768, 1),
                                           (64, 1024, 2048, 4), (256, 1024, 3072, 8),
-                                          (200, 2048, 1024, 2), (96, 1024, 512, 4)])
+                                          (200, 2048, 1024, 2), (96, 1024, 512, 4),
+                                          (256, 4096, 2048, 4), (256, 4096, 2048, 8)])
 def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
     """gdgemm.hip (global_load_lds ring) with each epilogue vs fp32 references: shallow
     (2 blocks/CU) and deep (1 block/CU) rings, split-K reduced by the separate pass or
