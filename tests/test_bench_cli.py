@@ -49,6 +49,15 @@ def test_bench_mono_single_process():
     assert res["scaling"] == "weak"
 
 
+def test_bench_data_parallel_two_ranks():
+    """The driver's scaling run: N ranks, each a full replica (weak scaling); rank 0 prints the
+    whole-job aggregate over all ranks."""
+    one = _run(["--model", "tiny-qwen3"] + SMALL)
+    res = _run(["--model", "tiny-qwen3"] + SMALL, nproc=2)
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert res["scaling"] == "weak" and res["config"]["global_batch"] == 2 * one["config"]["global_batch"]
+
+
 @pytest.mark.parametrize("model,env", [("tiny-llama", {}), ("tiny-mixtral", {"AKAP_MOE_MODE": "ep"})])
 def test_bench_tensor_parallel(model, env):
     res = _run(["--tp", "2", "--model", model] + SMALL, nproc=2, env=env)
