@@ -49,13 +49,19 @@ def render(agg: dict[str, tuple[float, int]]) -> str:
 def render_windows(windows: list[str], window_s: float) -> str:
     """kernel_profiler.py's view: cumulative counters over every kept attach window plus
     the newest window's per-kernel share of GPU kernel time and its busy ratio."""
+    return render_aggregates([collect(w) for w in windows], window_s)
+
+
+def render_aggregates(windows: list[dict], window_s: float) -> str:
+    """The same view from per-window {kernel: (seconds, calls)} maps (rocprofv3 CSV windows or
+    the in-process torch.profiler windows of exporter/inprocess_profiler.py)."""
     agg: dict[str, tuple[float, int]] = {}
     for w in windows:
-        for k, (t, n) in collect(w).items():
+        for k, (t, n) in w.items():
             t0, n0 = agg.get(k, (0.0, 0))
             agg[k] = (t0 + t, n0 + n)
     lines = [render(agg).rstrip("\n")]
-    last = collect(windows[-1]) if windows else {}
+    last = windows[-1] if windows else {}
     tot = sum(t for t, _ in last.values())
 
     def esc(s):

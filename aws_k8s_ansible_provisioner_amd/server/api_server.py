@@ -187,8 +187,11 @@ class OpenAIServer:
         @app.get("/metrics")
         async def metrics():
             eng._update_gauges()
-            return PlainTextResponse(eng.metrics.render(),
-                                     media_type="text/plain; version=0.0.4; charset=utf-8")
+            body = eng.metrics.render()
+            kp = getattr(self.ae, "kernel_profiler", None)
+            if kp is not None:  # in-process kernel-stats windows (exporter/inprocess_profiler)
+                body = body.rstrip("\n") + "\n" + kp.text()
+            return PlainTextResponse(body, media_type="text/plain; version=0.0.4; charset=utf-8")
 
         @app.get("/v1/models")
         async def models():
@@ -528,6 +531,11 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--otlp-traces-endpoint", default=None,
                     help="OTLP/HTTP collector (e.g. http://otel-collector:4318); also read "
                          "from OTEL_EXPORTER_OTLP_TRACES_ENDPOINT")
+    ap.add_argument("--kernel-stats-interval", type=float, default=0.0,
+                    help="seconds between in-process GPU kernel-stats windows served as "
+                         "akap_kernel_* on /metrics (torch.profiler; 0 = off, the rocprofv3 "
+                         "sidecar then provides them)")
+    ap.add_argument("--kernel-stats-window-ms", type=int, default=1000)
     return ap
 
 
@@ -589,7 +597,12 @@ def main(argv: Optional[list] = None) -> None:
 
         backend = os.environ.get("AKAP_DIST_BACKEND") or ("gloo" if a.device == "cpu" else None)
         init_distributed(tp_size=1, backend=backend)
-    app, _ = build_app(ecfg)
+    app, ae = build_app(ecfg)
+    if a.kernel_stats_interval > 0:
+        from ..exporter.inprocess_profiler import InProcessKernelProfiler
+
+        ae.kernel_profiler = InProcessKernelProfiler(a.kernel_stats_window_ms,
+                                                     a.kernel_stats_interval).start()
     uvicorn.run(app, host=a.host, port=a.port, log_level="info", access_log=False)
 
 

@@ -294,3 +294,31 @@ def test_pd_handoff_fills_the_v_tail_and_decodes_correctly():
     for o in outs:
         assert len(o.output_ids) == 10
         _check_teacher_forced(de, o.prompt_ids, o.output_ids)
+
+
+def test_inprocess_kernel_stats_window_sees_graph_replayed_kernels():
+    """The in-process profiler (exporter/inprocess_profiler.py) taking a window from a side
+    thread while the engine serves: the decode attention replayed from hipGraphs shows up."""
+    import threading
+
+    from aws_k8s_ansible_provisioner_amd.exporter.inprocess_profiler import InProcessKernelProfiler
+
+    eng = _engine("tiny-qwen3")
+    stop = threading.Event()
+
+    def serve():
+        while not stop.is_set():
+            eng.generate(None, SamplingParams(max_tokens=32, temperature=0, ignore_eos=True),
+                         prompt_ids=[[5 + i, 6, 7] for i in range(8)])
+
+    th = threading.Thread(target=serve, daemon=True)
+    th.start()
+    try:
+        kp = InProcessKernelProfiler(window_ms=300, interval_s=3600)
+        assert kp.once(), kp.last_error
+    finally:
+        stop.set()
+        th.join(timeout=120)
+    names = " ".join(kp.windows[-1])
+    assert "paged_attn_decode" in names, names[:500]
+    assert "akap_kernel_profiler_up 1" in kp.text()

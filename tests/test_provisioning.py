@@ -608,3 +608,49 @@ def test_gpu_exporter_real_amdsmi_output_matched_by_bus_id(tmp_path, with_list):
     ecc = [ln for ln in txt.splitlines() if ln.startswith("amd_gpu_ecc_errors_total{")]
     assert ecc and all('pci_bus_id="0000:5d:00.0"' in ln for ln in ecc)
     assert 'block="umc"' in txt
+
+
+def test_kernel_stats_inprocess_mode_replaces_the_sidecar():
+    """kernelProfiling.mode=inprocess: no ptrace sidecar / shared PID namespace; the engine
+    itself takes the windows (--kernel-stats-interval) and serves akap_kernel_* on :8000,
+    which the collector's engine job already scrapes."""
+    v = installer.load_values(os.path.join(ROOT, "deploy", "values", "slim.yaml"))
+    v["kernelProfiling"] = dict(v["kernelProfiling"], mode="inprocess", intervalSeconds=60,
+                                windowMs=1500)
+    out = installer.render(v, "llm-d", "local-path", "50Gi", "Qwen/Qwen3-0.6B", hf_token="t")
+    docs = [d for text in out.values() for d in yaml.safe_load_all(text) if d]
+    eng = [d for d in docs if d["kind"] == "Deployment" and "gateway" not in d["metadata"]["name"]][0]
+    pod = eng["spec"]["template"]
+    names = [c["name"] for c in pod["spec"]["containers"]]
+    assert names == ["engine"] and "shareProcessNamespace" not in pod["spec"]
+    assert "akap.rocprof/port" not in pod["metadata"]["annotations"]
+    args = pod["spec"]["containers"][0]["args"]
+    i = args.index("--kernel-stats-interval")
+    assert args[i + 1] == "60" and args[args.index("--kernel-stats-window-ms") + 1] == "1500"
+
+
+def test_inprocess_kernel_profiler_windows_and_health():
+    from aws_k8s_ansible_provisioner_amd.exporter.inprocess_profiler import (
+        InProcessKernelProfiler, torch_window)
+
+    calls = []
+
+    def fake(window_s):
+        calls.append(window_s)
+        if len(calls) == 3:
+            raise RuntimeError("roctracer busy")
+        return {"akap::paged_attn_decode_kernel": (0.6 * window_s, 28),
+                "akap::kgemm_kernel<32, 1>": (0.2 * window_s, 56)}
+
+    kp = InProcessKernelProfiler(window_ms=500, interval_s=3600, keep=2, window_fn=fake)
+    assert kp.once() and kp.once()
+    txt = kp.text()
+    assert 'akap_kernel_calls_total{kernel="akap::paged_attn_decode_kernel"} 56' in txt
+    assert "akap_kernel_window_busy_ratio 0.8" in txt and "akap_kernel_profiler_up 1" in txt
+    assert not kp.once()  # a failing window is counted, never raised
+    txt = kp.text()
+    assert "akap_kernel_profiler_up 0" in txt
+    assert 'akap_kernel_profiler_windows_total{result="failed"} 1' in txt
+    assert calls == [0.5, 0.5, 0.5]
+    # the real window function on a CPU-only host: no GPU, an empty window
+    assert torch_window(0.01) == {}

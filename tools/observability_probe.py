@@ -128,16 +128,79 @@ def profiler_pass(out: str, model: str, window_ms: int) -> None:
         log.close()
 
 
+def inprocess_pass(out: str, model: str) -> None:
+    """The engine server (a child process) takes its own kernel-stats windows every 5 s while
+    it serves HTTP load; its /metrics must carry the akap_kernel_* series."""
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    log = open(os.path.join(out, "server_inprocess.log"), "w")
+    srv = subprocess.Popen([sys.executable, "-m", "aws_k8s_ansible_provisioner_amd.server",
+                            "--model", model, "--port", str(port), "--host", "127.0.0.1",
+                            "--max-num-seqs", "64", "--max-model-len", "2048",
+                            "--kernel-stats-interval", "5", "--kernel-stats-window-ms", "1000"],
+                           env=env, cwd=ROOT, stdout=log, stderr=subprocess.STDOUT)
+    url = f"http://127.0.0.1:{port}"
+    stop = threading.Event()
+    try:
+        t0 = time.time()
+        while True:
+            try:
+                urllib.request.urlopen(url + "/health", timeout=2)
+                break
+            except Exception:
+                if srv.poll() is not None or time.time() - t0 > 300:
+                    raise RuntimeError("engine server did not come up (see server_inprocess.log)")
+                time.sleep(1)
+        print(f"[inprocess] engine up in {time.time() - t0:.1f}s", flush=True)
+
+        def load():
+            body = json.dumps({"prompt": "profile window " * 40, "max_tokens": 128,
+                               "temperature": 0, "ignore_eos": True}).encode()
+            while not stop.is_set():
+                try:
+                    req = urllib.request.Request(url + "/v1/completions", data=body,
+                                                 headers={"Content-Type": "application/json"})
+                    urllib.request.urlopen(req, timeout=120).read()
+                except Exception:
+                    time.sleep(0.2)
+
+        for _ in range(32):
+            threading.Thread(target=load, daemon=True).start()
+        m = ""
+        for _ in range(30):  # a window every 5 s; wait for two
+            time.sleep(2)
+            m = urllib.request.urlopen(url + "/metrics").read().decode()
+            if 'akap_kernel_profiler_windows_total{result="ok"} 2' in m:
+                break
+        open(os.path.join(out, "engine_metrics_inprocess.txt"), "w").write(m)
+        ks = [ln for ln in m.splitlines() if ln.startswith("akap_kernel")]
+        print(f"[inprocess] {len(ks)} akap_kernel_* lines; head:\n" + "\n".join(ks[:14]),
+              flush=True)
+    finally:
+        stop.set()
+        srv.terminate()
+        try:
+            srv.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            srv.kill()
+        log.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "obs"))
     ap.add_argument("--model", default="qwen3-0.6b")
     ap.add_argument("--window-ms", type=int, default=1500)
     ap.add_argument("--skip-profiler", action="store_true")
+    ap.add_argument("--inprocess", action="store_true",
+                    help="start the server with --kernel-stats-interval (its own torch.profiler "
+                         "windows) and scrape its /metrics instead of attaching rocprofv3")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     exporter_pass(a.out)
-    if not a.skip_profiler:
+    if a.inprocess:
+        inprocess_pass(a.out, a.model)
+    elif not a.skip_profiler:
         profiler_pass(a.out, a.model, a.window_ms)
 
 
