@@ -1,0 +1,78 @@
+"""Tensor parallelism on the GPU: 2 TP ranks as 2 processes sharing ONE MI355X (the only
+multi-rank layout a single-GPU box allows), collectives over gloo (host-staged), eager steps.
+The HIP kernels see their real TP shapes -- head-split attention with its own KV shard, row /
+column-split MLP, vocab-parallel LM head, rank-0 step broadcast -- and every generated token
+must be the (near-)argmax of the fp32 dense reference on the same logical weights."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import json, os, sys
+import torch
+sys.path.insert(0, os.environ["ROOT"])
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
+ecfg = EngineConfig(model=os.environ["MODEL"], device="cuda", max_model_len=256, max_num_seqs=8,
+                    max_num_batched_tokens=64, block_size=32, num_gpu_blocks=96,
+                    tensor_parallel_size=int(os.environ["WORLD_SIZE"]), shard_init="full",
+                    init_std=0.15, enforce_eager=True)
+eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
+if eng is not None:
+    outs = eng.generate(None, SamplingParams(max_tokens=8, temperature=0, ignore_eos=True),
+                        prompt_ids=[list(range(5, 40)), [100, 101], [9, 9, 9]])
+    bc.shutdown()
+    print("RESULT " + json.dumps([o.output_ids for o in outs]), flush=True)
+"""
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-qwen3"])
+def test_tp2_on_one_gpu_matches_dense_reference(model):
+    from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+    from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
+    from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logits
+
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, ROOT=ROOT, MODEL=model, RANK=str(r), WORLD_SIZE="2",
+                   LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", CHILD], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    got = json.loads([ln for ln in outs[0][0].splitlines() if ln.startswith("RESULT")][0][7:])
+    ref = LLMEngine(EngineConfig(model=model, device="cuda", max_model_len=256, max_num_seqs=8,
+                                 max_num_batched_tokens=64, block_size=32, num_gpu_blocks=96,
+                                 init_std=0.15, enforce_eager=True, shard_init="full"),
+                    log=lambda *a: None)
+    prompts = [list(range(5, 40)), [100, 101], [9, 9, 9]]
+    want = [o.output_ids for o in ref.generate(
+        None, SamplingParams(max_tokens=8, temperature=0, ignore_eos=True), prompt_ids=prompts)]
+    # bf16 TP sums round differently from TP=1, so the streams may part at a near-tie of the
+    # random model (seen: 0.0007 std between the top two logits); each TP token must be the
+    # (near-)argmax of the fp32 dense reference on the same logical weights, teacher-forced
+    for p, toks in zip(prompts, got):
+        seq = list(p) + list(toks)
+        logits = dense_logits(ref.runner.model, seq).float().cpu()
+        for i, t in enumerate(toks):
+            row = logits[len(p) - 1 + i]
+            gap = float((row.max() - row[t]) / (row.std() + 1e-6))
+            assert gap <= 0.15, (p[:4], i, t, gap)
+    assert [x[0] for x in got] == [y[0] for y in want]  # prefill's first tokens agree
