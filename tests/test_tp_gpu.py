@@ -1,6 +1,6 @@
 """Tensor parallelism on the GPU: 2 TP ranks as 2 processes sharing ONE MI355X (the only
 multi-rank layout a single-GPU box allows), collectives over gloo (host-staged), eager steps.
-The HIP kernels see their real TP shapes -- head-split attention with its own KV shard, row /
+Mixtral runs its experts TP-sharded and expert-parallel (all-to-all dispatch). The HIP kernels see their real TP shapes -- head-split attention with its own KV shard, row /
 column-split MLP, vocab-parallel LM head, rank-0 step broadcast -- and every generated token
 must be the (near-)argmax of the fp32 dense reference on the same logical weights."""
 import json
@@ -41,8 +41,9 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("model", ["tiny-llama", "tiny-qwen3"])
-def test_tp2_on_one_gpu_matches_dense_reference(model):
+@pytest.mark.parametrize("model,moe_mode", [("tiny-llama", "tp"), ("tiny-qwen3", "tp"),
+                                            ("tiny-mixtral", "tp"), ("tiny-mixtral", "ep")])
+def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode):
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
     from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logits
@@ -51,6 +52,7 @@ def test_tp2_on_one_gpu_matches_dense_reference(model):
     procs = []
     for r in range(2):
         env = dict(os.environ, ROOT=ROOT, MODEL=model, RANK=str(r), WORLD_SIZE="2",
+                   AKAP_MOE_MODE=moe_mode,
                    LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, "-c", CHILD], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
