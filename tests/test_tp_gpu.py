@@ -1,6 +1,7 @@
 """Tensor parallelism on the GPU: 2 TP ranks as 2 processes sharing ONE MI355X (the only
 multi-rank layout a single-GPU box allows), collectives over gloo (host-staged), eager steps.
-Mixtral runs its experts TP-sharded and expert-parallel (all-to-all dispatch). The HIP kernels see their real TP shapes -- head-split attention with its own KV shard, row /
+Mixtral runs its experts TP-sharded and expert-parallel (all-to-all dispatch).  The HIP
+kernels see their real TP shapes -- head-split attention with its own KV shard, row /
 column-split MLP, vocab-parallel LM head, rank-0 step broadcast -- and every generated token
 must be the (near-)argmax of the fp32 dense reference on the same logical weights."""
 import json
