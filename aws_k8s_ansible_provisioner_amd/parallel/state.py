@@ -92,7 +92,11 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
             grp = dist.new_group(ranks)
             if rank in ranks:
                 st.dp_group = grp
-    if (world > 1 and tp_size > 1 and backend == "nccl"
+    # the custom all-reduce rides on RCCL ranks; AKAP_CUSTOM_AR_GLOO=1 also builds it for gloo
+    # ranks that share one GPU (single-GPU rehearsal: the IPC mappings work within a device)
+    car_gloo = (backend == "gloo" and torch.cuda.is_available()
+                and os.environ.get("AKAP_CUSTOM_AR_GLOO") == "1")
+    if (world > 1 and tp_size > 1 and (backend == "nccl" or car_gloo)
             and os.environ.get("AKAP_CUSTOM_AR", "1") != "0"):
         from .custom_allreduce import CustomAllReduce
         st.car = CustomAllReduce(group=st.tp_group, device=torch.device("cuda", local))

@@ -26,6 +26,8 @@ ecfg = EngineConfig(model=os.environ["MODEL"], device="cuda", max_model_len=256,
                     tensor_parallel_size=int(os.environ["WORLD_SIZE"]), shard_init="full",
                     init_std=0.15, enforce_eager=True)
 eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
+from aws_k8s_ansible_provisioner_amd.parallel.state import get_state
+assert (get_state().car is not None) == (os.environ["AKAP_CUSTOM_AR_GLOO"] == "1")
 if eng is not None:
     outs = eng.generate(None, SamplingParams(max_tokens=8, temperature=0, ignore_eos=True),
                         prompt_ids=[list(range(5, 40)), [100, 101], [9, 9, 9]])
@@ -42,9 +44,12 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("model,moe_mode", [("tiny-llama", "tp"), ("tiny-qwen3", "tp"),
-                                            ("tiny-mixtral", "tp"), ("tiny-mixtral", "ep")])
-def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode):
+@pytest.mark.parametrize("model,moe_mode,car", [
+    ("tiny-llama", "tp", "0"), ("tiny-qwen3", "tp", "0"), ("tiny-mixtral", "tp", "0"),
+    ("tiny-mixtral", "ep", "0"),
+    # the TP all-reduces through the custom all-reduce kernels (K13) across the two processes
+    ("tiny-llama", "tp", "1"), ("tiny-qwen3", "tp", "1")])
+def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode, car):
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
     from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logits
@@ -53,7 +58,7 @@ def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode):
     procs = []
     for r in range(2):
         env = dict(os.environ, ROOT=ROOT, MODEL=model, RANK=str(r), WORLD_SIZE="2",
-                   AKAP_MOE_MODE=moe_mode,
+                   AKAP_MOE_MODE=moe_mode, AKAP_CUSTOM_AR_GLOO=car,
                    LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, "-c", CHILD], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
