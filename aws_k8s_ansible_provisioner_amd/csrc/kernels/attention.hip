@@ -101,6 +101,36 @@ __device__ __forceinline__ void load_chunk(ChunkT<F8>& c, const void* __restrict
   for (int n = 0; n < kND; ++n) c.vb[n] = ld_raw8<F8, NT>(v_cache, vp + 16 * n * 8);
 }
 
+// Decode form: the chunk's cache block id is given (one wave-uniform value: chunks are
+// 32-token aligned and BS is a multiple of 32, so a chunk never spans two blocks).  The
+// decode loop keeps its block ids in a VGPR (lane j = the block of the wave's j-th chunk,
+// loaded once) and reads them with readlane: an SGPR, no memory instruction in the loop.
+// With a per-chunk bt[] load instead, the in-order vmcnt made every iteration wait for the
+// previous chunk's K/V AND then an L2 round trip before the next chunk's loads could issue
+// (the ISA showed `s_waitcnt vmcnt(2)` right after the three bt loads at the loop top).
+template <bool NT = false, bool F8 = false>
+__device__ __forceinline__ void load_chunk_blk(ChunkT<F8>& c, const void* __restrict__ k_cache,
+                                               const void* __restrict__ v_cache, int blk,
+                                               int kv_len, int kvh, int Hkv, int BS, int t0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int r = lane & 15;
+  const size_t kb = ((size_t)blk * Hkv + kvh) * BS * kD;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    int tok = t0 + 8 * (r >> 2) + 4 * tt + (r & 3);
+    tok = min(tok, kv_len - 1);  // clamped lanes re-read a valid row (masked later)
+    const size_t kp = kb + k_swz_offset(tok % BS) + 8 * g;
+#pragma unroll
+    for (int cc = 0; cc < kNC; ++cc) c.ka[tt][cc] = ld_raw8<F8, NT>(k_cache, kp + cc * 512);
+  }
+  int vt = t0 + 8 * g;
+  vt = min(vt, (kv_len - 1) & ~7);
+  const size_t vp = kb + ((vt % BS) >> 3) * kD * 8 + r * 8;
+#pragma unroll
+  for (int n = 0; n < kND; ++n) c.vb[n] = ld_raw8<F8, NT>(v_cache, vp + 16 * n * 8);
+}
+
 // Scores, online softmax and P.V for one staged chunk.
 // limit: last kv position this lane's query row may attend to (-1 => none).
 template <bool MASK, typename CT>
@@ -371,7 +401,7 @@ template <bool PREFETCH, bool NT = false, bool FUSED = false, bool F8 = false>
 __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
                                             float* dyn_lds) {
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int g = lane >> 4;
   const int G = p.G;
   const int kv_len = p.seq_lens[seq];
@@ -402,14 +432,24 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
   // PREFETCH: this wave's first chunk is issued before anything else (in the fused kernel,
   // before the q/k prologue, so its HBM latency overlaps the prologue's)
   int t0 = pstart + 32 * w;
+  // block ids of this wave's chunks, one per lane (lane j: chunk pstart + 32 w + 128 j)
+  int btr = 0;
+  {
+    const int tj = t0 + 128 * lane;
+    if (tj < pend) btr = bt[tj / p.BS];
+  }
+  const int tw = t0;  // the wave's first chunk (t0 itself advances in the loop below)
+  // j < 64 always: the host caps part_size at kDecodeMaxPart (64 chunks per wave)
+  auto blk_of = [=](int tc) -> int { return __builtin_amdgcn_readlane(btr, (tc - tw) >> 7); };
   ChunkT<F8> cur;
   if (PREFETCH && t0 < pend)
-    load_chunk<NT, F8>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+    load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS, t0);
   if constexpr (FUSED) {
     fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s, use_img ? tsl : -1, v_img);
     // the chunk holding the token the prologue just wrote is re-read after the barrier
     if (PREFETCH && writes_kv && t0 < pend && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
-      load_chunk<NT, F8>(cur, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+      load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS,
+                             t0);
   } else if (use_img) {  // uniform per workgroup
     if (threadIdx.x < 16) {
       const int j = threadIdx.x;
@@ -445,8 +485,8 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
           ChunkT<F8> nxt;
           const bool more = t0 + 128 < pend;
           if (more)
-            load_chunk<NT, F8>(nxt, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS,
-                               t0 + 128);
+            load_chunk_blk<NT, F8>(nxt, p.k_cache, p.v_cache, blk_of(t0 + 128), kv_len, kvh,
+                                   p.Hkv, p.BS, t0 + 128);
           if (use_img && t0 <= gstart && gstart < t0 + 32) patch_v(cur, t0, gstart, v_img);
           if (t0 + 31 < kv_len)
             compute_chunk<false>(st, qb, cur, t0, limit, p.scale_log2);
@@ -458,7 +498,7 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
     } else {
       for (; t0 < pend; t0 += 128) {
         ChunkT<F8> c;
-        load_chunk<NT, F8>(c, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0);
+        load_chunk_blk<NT, F8>(c, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS, t0);
         if (use_img && t0 <= gstart && gstart < t0 + 32) patch_v(c, t0, gstart, v_img);
         if (t0 + 31 < kv_len)
           compute_chunk<false>(st, qb, c, t0, limit, p.scale_log2);

@@ -7,6 +7,8 @@
 
 namespace akap {
 
+constexpr int kDecodeMaxPart = 8192;
+
 // ---- norm.hip ----
 void launch_rmsnorm(void* out, const void* x, const void* w, int rows, int d, int x_stride,
                     int out_stride, float eps, hipStream_t s);
@@ -43,7 +45,8 @@ struct AttnParams {
   // prefill tiling (host-built): per 64-row tile its sequence and first flattened row
   const int* tile_seq;
   const int* tile_row;
-  // decode split-KV
+  // decode split-KV (part_size <= kDecodeMaxPart: 64 wave steps of 128 tokens, one cache
+  // block id per step held in a VGPR lane)
   int num_parts, part_size;
   float* part_m;  // [B, Hkv, parts, G]
   float* part_l;

@@ -209,7 +209,8 @@ void paged_attention_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache
   auto p = attn_params(out, q, k_cache, v_cache, block_tables, seq_lens, G, scale);
   TORCH_CHECK(G <= 16, "decode kernel supports up to 16 q heads per kv head");
   set_v_tail(p, v_tail, tail_slot, seq_lens.numel());
-  TORCH_CHECK(part_size % 128 == 0 && part_size > 0, "part_size must be a multiple of 128");
+  TORCH_CHECK(part_size % 128 == 0 && part_size > 0 && part_size <= akap::kDecodeMaxPart,
+              "part_size must be a multiple of 128, at most ", akap::kDecodeMaxPart);
   const int B = seq_lens.numel();
   p.q_start = q_start ? q_start->data_ptr<int>() : nullptr;
   p.num_parts = num_parts;
@@ -240,7 +241,8 @@ void paged_attention_decode_fused(Tensor out, Tensor qkv, Tensor k_cache, Tensor
   set_v_tail(p, v_tail, tail_slot, seq_lens.numel());
   CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv);
   TORCH_CHECK(G + 2 <= 16, "fused decode supports up to 14 q heads per kv head");
-  TORCH_CHECK(part_size % 128 == 0 && part_size > 0, "part_size must be a multiple of 128");
+  TORCH_CHECK(part_size % 128 == 0 && part_size > 0 && part_size <= akap::kDecodeMaxPart,
+              "part_size must be a multiple of 128, at most ", akap::kDecodeMaxPart);
   const int B = seq_lens.numel();
   TORCH_CHECK(qkv.size(0) >= B && qkv.size(1) >= (p.Hq + 2 * p.Hkv) * 128, "qkv shape");
   TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong,

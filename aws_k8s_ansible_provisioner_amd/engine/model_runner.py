@@ -345,6 +345,9 @@ class ModelRunner:
             parts = 1
         else:
             parts = min(math.ceil(2048 / wgs), max(1, math.ceil(max_len / 256)))
+        # a partition is at most ops.DECODE_MAX_PART tokens (the kernel holds one block id
+        # per 128-token wave step in a VGPR lane: 64 steps)
+        parts = max(parts, math.ceil(max_len / ops.DECODE_MAX_PART))
         ps = math.ceil(math.ceil(max_len / parts) / 128) * 128
         parts = math.ceil(max_len / ps)
         return parts, ps

@@ -133,6 +133,10 @@ def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_
     return out
 
 
+# longest decode split-KV partition the kernel takes (csrc/kernels/kernels.h kDecodeMaxPart)
+DECODE_MAX_PART = 8192
+
+
 def paged_attention_decode(out, q, k_cache, v_cache, block_tables, seq_lens, gqa_group: int,
                            scale: float, workspace=None, num_parts: int = 1,
                            part_size: int = 512, q_start=None, v_tail=None, tail_slot=None):

@@ -799,7 +799,7 @@ def test_kgemm_in_workgroup_splitk(km, epi, M, N, K):
         assert torch.allclose(ss, res.float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("num_parts,part_size", [(1, 32768), (32, 1024), (128, 256)])
+@pytest.mark.parametrize("num_parts,part_size", [(4, 8192), (32, 1024), (128, 256)])
 def test_paged_attention_decode_long_context(num_parts, part_size):
     """Long-context decode (up to 32k cached tokens per sequence, Llama-3-70B's 64/8 heads
     per rank shape): unsplit, and split-KV with the partition combine (the engine's adaptive
@@ -818,7 +818,19 @@ def test_paged_attention_decode_long_context(num_parts, part_size):
     _close(out, exp, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("num_parts,part_size", [(1, 32768), (64, 512), (128, 256), (32, 1024)])
+def test_paged_attention_decode_rejects_oversized_partition():
+    """A partition longer than ops.DECODE_MAX_PART is refused on the host (the kernel keeps
+    one cache block id per 128-token wave step in a VGPR lane: 64 steps)."""
+    q, kc, vc, bt, sl, qs = _setup_attn([(100, 1), (7, 1)], 16, 8, 32, seed=3)
+    out = torch.empty_like(q).to(DEV)
+    ws = ops.decode_workspace(2, 8, 2, 1, DEV)
+    with pytest.raises(RuntimeError, match="part_size"):
+        ops.paged_attention_decode(out, q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV),
+                                   sl.to(DEV), 2, 0.1, workspace=ws, num_parts=1,
+                                   part_size=2 * ops.DECODE_MAX_PART)
+
+
+@pytest.mark.parametrize("num_parts,part_size", [(4, 8192), (64, 512), (128, 256), (32, 1024)])
 def test_paged_attention_decode_fused_long_context(num_parts, part_size):
     """The engine's decode kernel (fused prologue) at long context with split-KV partitions."""
     test_paged_attention_decode_fused(16, 8, True, num_parts, part_size,
