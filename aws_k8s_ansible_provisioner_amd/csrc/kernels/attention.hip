@@ -395,16 +395,53 @@ __device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq,
   __syncthreads();
 }
 
-// One (seq, kv head, partition) work item.  Ends with the LDS combine; callers that run
-// several items per workgroup must __syncthreads() before the next item's LDS writes.
-template <bool PREFETCH, bool NT = false, bool FUSED = false, bool F8 = false>
-__device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
-                                            float* dyn_lds) {
+// What a decode work item needs before its first K/V byte can be requested: the sequence's
+// length, the cache block ids of the wave's chunks (lane j: chunk pstart + 32 w + 128 j, read
+// later with readlane: an SGPR, no memory instruction in the chunk loop) and, with PREFETCH,
+// the wave's first chunk in flight.  The block-id load does not wait for the length (the
+// index is clamped into the block-table row instead of guarded by it), so the chain before
+// the first K/V load is two round trips.  The persistent pipelined kernel fetches the NEXT
+// item's head while the current item finishes (combine, output store, next prologue).
+template <bool F8>
+struct ItemHead {
+  int seq, kvh, part, kv_len, btr;
+  ChunkT<F8> cur;
+};
+
+template <bool PREFETCH, bool NT, bool F8>
+__device__ __forceinline__ void item_head(const AttnParams& p, ItemHead<F8>& h, int seq, int kvh,
+                                          int part) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  h.seq = seq;
+  h.kvh = kvh;
+  h.part = part;
+  const int pstart = part * p.part_size;
+  const int t0 = pstart + 32 * w;
+  const int bi = min((t0 + 128 * lane) / p.BS, p.bt_stride - 1);
+  h.btr = p.block_tables[(size_t)seq * p.bt_stride + bi];
+  h.kv_len = p.seq_lens[seq];
+  const int pend = min(h.kv_len, pstart + p.part_size);
+  if (PREFETCH && t0 < pend)
+    load_chunk_blk<NT, F8>(h.cur, p.k_cache, p.v_cache, __builtin_amdgcn_readlane(h.btr, 0),
+                           h.kv_len, kvh, p.Hkv, p.BS, t0);
+}
+
+// One (seq, kv head, partition) work item whose head item_head() has fetched.  after_loop()
+// runs once the chunk loop is done (h.cur / h.btr are dead then: the pipelined kernel fetches
+// the next item's head into h there), before the LDS combine.  Callers that run several
+// items per workgroup must __syncthreads() before the next item's LDS writes.
+template <bool PREFETCH, bool NT, bool FUSED, bool F8, typename AfterLoop>
+__device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>& h,
+                                              float* dyn_lds, AfterLoop after_loop) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int g = lane >> 4;
   const int G = p.G;
-  const int kv_len = p.seq_lens[seq];
+  const int seq = h.seq, kvh = h.kvh, part = h.part;
+  const int kv_len = h.kv_len;
+  const int btr = h.btr;
+  ChunkT<F8>& cur = h.cur;
   const int pstart = part * p.part_size;
   const int pend = min(kv_len, pstart + p.part_size);
   const int qr = lane & 15;
@@ -420,7 +457,6 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
 #define OS(w_, r_, d_) o_s[((w_) * G + (r_)) * (kD + 4) + (d_)]
   bf16* q_s = reinterpret_cast<bf16*>(l_s + 4 * G);  // [G][kD] (fused only)
   bf16* v_img = q_s + (FUSED ? G * kD : 0);          // [kD][8] V tail group image
-  const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
   const int limit = kv_len - 1;
   const bool writes_kv = kv_len > 0 && pstart <= kv_len - 1 && kv_len - 1 < pend;
   // V tail: the sequence's last 8-token group (first token gstart) is read from an LDS image
@@ -429,21 +465,10 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
   const int tsl = (!F8 && p.v_tail != nullptr && kv_len > 0) ? p.tail_slot[seq] : -1;
   const int gstart = (kv_len - 1) & ~7;
   const bool use_img = tsl >= 0 && writes_kv && (FUSED ? p.slots[seq] >= 0 : (kv_len & 7) != 0);
-  // PREFETCH: this wave's first chunk is issued before anything else (in the fused kernel,
-  // before the q/k prologue, so its HBM latency overlaps the prologue's)
   int t0 = pstart + 32 * w;
-  // block ids of this wave's chunks, one per lane (lane j: chunk pstart + 32 w + 128 j)
-  int btr = 0;
-  {
-    const int tj = t0 + 128 * lane;
-    if (tj < pend) btr = bt[tj / p.BS];
-  }
   const int tw = t0;  // the wave's first chunk (t0 itself advances in the loop below)
   // j < 64 always: the host caps part_size at kDecodeMaxPart (64 chunks per wave)
   auto blk_of = [=](int tc) -> int { return __builtin_amdgcn_readlane(btr, (tc - tw) >> 7); };
-  ChunkT<F8> cur;
-  if (PREFETCH && t0 < pend)
-    load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS, t0);
   if constexpr (FUSED) {
     fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s, use_img ? tsl : -1, v_img);
     // the chunk holding the token the prologue just wrote is re-read after the barrier
@@ -507,6 +532,7 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
       }
     }
   }
+  after_loop();
   float l = st.l;
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -558,6 +584,14 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
 #undef OS
 }
 
+template <bool PREFETCH, bool NT = false, bool FUSED = false, bool F8 = false>
+__device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
+                                            float* dyn_lds) {
+  ItemHead<F8> h;
+  item_head<PREFETCH, NT, F8>(p, h, seq, kvh, part);
+  decode_item_h<PREFETCH, NT, FUSED, F8>(p, h, dyn_lds, [] {});
+}
+
 // grid = (num_seqs, Hkv, num_parts): one work item per workgroup.
 template <bool PREFETCH, int MINW, bool NT = false, bool FUSED = false, bool F8 = false>
 __global__ __launch_bounds__(256, MINW) void paged_attn_decode_kernel(AttnParams p) {
@@ -569,8 +603,8 @@ __global__ __launch_bounds__(256, MINW) void paged_attn_decode_kernel(AttnParams
 // (kv head fastest, so consecutive items of a workgroup share the sequence's block table
 // and q row in cache).  Bounded loop: every workgroup exits after its last item.
 template <bool PREFETCH, bool NT, bool FUSED = false>
-__global__ __launch_bounds__(256) void paged_attn_decode_persistent_kernel(AttnParams p,
-                                                                           int num_seqs) {
+__global__ __launch_bounds__(256, 2) void paged_attn_decode_persistent_kernel(AttnParams p,
+                                                                              int num_seqs) {
   extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
   const int items = num_seqs * p.Hkv * p.num_parts;
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
@@ -578,6 +612,44 @@ __global__ __launch_bounds__(256) void paged_attn_decode_persistent_kernel(AttnP
     const int sk = it / p.num_parts;
     decode_item<PREFETCH, NT, FUSED>(p, sk / p.Hkv, sk % p.Hkv, part, dyn_lds);
     __syncthreads();  // LDS combine buffer is reused by the next item
+  }
+}
+
+// Persistent PIPELINED variant (fused, prefetching): the next item's head -- its length,
+// block ids and first K/V chunk -- is requested as soon as the current item's chunk loop is
+// done, so its round trips overlap the current item's combine, output store and the next
+// item's q/k prologue instead of opening each item with an idle CU slot.  Every workgroup
+// runs a bounded number of items (it += gridDim.x) and exits.
+template <bool NT>
+__global__ __launch_bounds__(256, 2) void paged_attn_decode_pipelined_kernel(AttnParams p,
+                                                                             int num_seqs) {
+  extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
+  const int items = num_seqs * p.Hkv * p.num_parts;
+  auto coords = [&](int it, int& seq, int& kvh, int& part) {
+    part = it % p.num_parts;
+    const int sk = it / p.num_parts;
+    seq = sk / p.Hkv;
+    kvh = sk % p.Hkv;
+  };
+  ItemHead<false> h;
+  int it = blockIdx.x;
+  if (it >= items) return;
+  {
+    int seq, kvh, part;
+    coords(it, seq, kvh, part);
+    item_head<true, NT, false>(p, h, seq, kvh, part);
+  }
+  while (it < items) {
+    const int nx = it + gridDim.x;
+    decode_item_h<true, NT, true, false>(p, h, dyn_lds, [&] {
+      if (nx < items) {
+        int seq, kvh, part;
+        coords(nx, seq, kvh, part);
+        item_head<true, NT, false>(p, h, seq, kvh, part);
+      }
+    });
+    __syncthreads();  // LDS combine buffer is reused by the next item
+    it = nx;
   }
 }
 
@@ -1011,10 +1083,15 @@ void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) 
   } else if (p.qkv != nullptr && per_cu > 0) {  // fused, persistent grid (grid-capped)
     const int items = num_seqs * p.Hkv * p.num_parts;
     const int grid = min(items, num_cus() * per_cu);
-    paged_attn_decode_persistent_kernel<true, true, true><<<grid, 256, smem, s>>>(p, num_seqs);
+    if (p.flags & 128)  // bit 7: next item's head fetched under the current item's tail
+      paged_attn_decode_pipelined_kernel<true><<<grid, 256, smem, s>>>(p, num_seqs);
+    else
+      paged_attn_decode_persistent_kernel<true, true, true><<<grid, 256, smem, s>>>(p, num_seqs);
   } else if (p.qkv != nullptr) {  // fused q/k-norm + RoPE + KV write (default flags path)
     const dim3 grid(num_seqs, p.Hkv, p.num_parts);
-    if (p.flags & 1)
+    if (p.flags & 256)  // bit 8: single-buffered chunks at 3 workgroups per CU
+      paged_attn_decode_kernel<false, 3, true, true><<<grid, 256, smem, s>>>(p);
+    else if (p.flags & 1)
       paged_attn_decode_kernel<true, 1, true, true><<<grid, 256, smem, s>>>(p);
     else
       paged_attn_decode_kernel<false, 1, true, true><<<grid, 256, smem, s>>>(p);

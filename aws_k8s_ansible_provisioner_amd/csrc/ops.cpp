@@ -138,16 +138,27 @@ static void set_v_tail(akap::AttnParams& p, const std::optional<Tensor>& v_tail,
   p.tail_slot = tail_slot->data_ptr<int>();
 }
 
-int attn_flags() {
+// bit0 (default on): register double-buffered K/V prefetch in decode (+1-2% measured)
+// bit6 (default on): non-temporal K/V loads in decode -- the cache is streamed once
+//   per step, keep it out of L2/MALL (-5.5% decode attention time measured)
+// bits3-5: persistent decode grid (WGs per CU); bit7: with bits 3-5 on the fused path, the
+//   pipelined persistent kernel (next item's head fetched under the current item's tail);
+//   bit1/2: occupancy variants (off).  AKAP_ATTN_FLAGS sets the process default;
+//   set_attn_flags() swaps it at run time (tests and in-process A/B of the variants).
+static int& attn_flags_ref() {
   static int f = [] {
-    // bit0 (default on): register double-buffered K/V prefetch in decode (+1-2% measured)
-    // bit6 (default on): non-temporal K/V loads in decode -- the cache is streamed once
-    //   per step, keep it out of L2/MALL (-5.5% decode attention time measured)
-    // bits3-5: persistent decode grid (WGs per CU); bit1/2: occupancy variants (off)
     const char* e = std::getenv("AKAP_ATTN_FLAGS");
     return e ? std::atoi(e) : 65;
   }();
   return f;
+}
+
+int attn_flags() { return attn_flags_ref(); }
+
+int64_t set_attn_flags(int64_t f) {
+  const int prev = attn_flags_ref();
+  attn_flags_ref() = (int)f;
+  return prev;
 }
 
 akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_cache,
@@ -967,6 +978,7 @@ TORCH_LIBRARY(akap, m) {
   m.def("kv_gather(Tensor cache, Tensor block_ids, Tensor(a!) out) -> ()");
   m.def("kv_scatter(Tensor buf, Tensor(a!) cache, Tensor block_ids) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start, int vocab_end) -> ()");
+  m.def("set_attn_flags(int flags) -> int");
 }
 
 TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
@@ -978,6 +990,7 @@ TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("car_error", &car_error);
   m.impl("car_link_local", &car_link_local);
   m.impl("car_destroy", &car_destroy);
+  m.impl("set_attn_flags", &set_attn_flags);
 }
 
 TORCH_LIBRARY_IMPL(akap, CUDA, m) {

@@ -133,6 +133,13 @@ def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_
     return out
 
 
+def set_attn_flags(flags: int) -> int:
+    """Swap the attention kernel-variant flags (csrc/ops.cpp attn_flags; process default
+    AKAP_ATTN_FLAGS or 65).  Returns the previous value.  For tests and in-process A/B."""
+    load_native(required=True)
+    return int(torch.ops.akap.set_attn_flags(int(flags)))
+
+
 # longest decode split-KV partition the kernel takes (csrc/kernels/kernels.h kDecodeMaxPart)
 DECODE_MAX_PART = 8192
 

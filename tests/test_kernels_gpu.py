@@ -930,3 +930,33 @@ def test_v_tail_decode_matches_the_plain_cache_path(num_parts, part_size):
         full = n & ~7
         assert torch.equal(_v_tokens(vA_, bt, s, full), _v_tokens(vB_, bt, s, full)), s
     assert torch.equal(kA, kB)
+
+
+@pytest.fixture
+def attn_flags_variant(request):
+    prev = ops.set_attn_flags(request.param)
+    yield request.param
+    ops.set_attn_flags(prev)
+
+
+# 65 = the default grid kernel; 81 = persistent grid, 2 workgroups per CU; 209 = the same with
+# the pipelined kernel (next item's head fetched under the current item's tail); 321 = the grid
+# kernel single-buffered at 3 workgroups per CU
+@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321], indirect=True)
+@pytest.mark.parametrize("num_parts,part_size,lens", [
+    (1, 4096, [1, 31, 32, 33, 200, 777, 1500] * 40),  # 280 seqs x 8 heads: > 1 item per WG
+    (3, 512, [1, 31, 32, 33, 200, 777, 1500]),
+    (4, 8192, [8001, 1, 20001, 32768, 4095])])
+def test_paged_attention_decode_fused_persistent_variants(attn_flags_variant, num_parts,
+                                                          part_size, lens):
+    """The persistent and pipelined decode kernels (a workgroup runs several work items, the
+    pipelined one prefetching each next item during the current one's tail) against the
+    reference pipeline, with more items than resident workgroups."""
+    test_paged_attention_decode_fused(16, 8, True, num_parts, part_size, lens=list(lens))
+
+
+@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321], indirect=True)
+def test_v_tail_decode_persistent_variants(attn_flags_variant):
+    """V tail path through the persistent / pipelined decode kernels: bit-identical to the
+    plain per-token cache path over 20 steps."""
+    test_v_tail_decode_matches_the_plain_cache_path(1, 4096)
