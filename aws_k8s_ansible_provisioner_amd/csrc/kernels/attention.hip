@@ -395,6 +395,312 @@ __device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq,
   __syncthreads();
 }
 
+// Fused-prologue operands loaded up front (grid decode kernel).  Every prologue load is
+// issued BEFORE the first K/V chunk's loads, so the prologue's waits (counted vmcnt: the
+// chunk's 16 loads were issued later) leave the chunk in flight; with the loads inside the
+// prologue, their first wait drained the chunk (vmcnt is in-order) and the
+// positions -> cos_sin chain added two more round trips behind it.  The V-tail rows are
+// loaded whole (8 rows, valid memory) and selected afterwards: no load under a per-row
+// runtime condition (hipcc would wait on each).
+template <bool F8>
+struct ProPre {
+  bf16x8 raw, w8;
+  f32x4 c0, c1, s0, s1;
+  bf16x8 trow[8];
+  int64_t slot;
+  int tsl;
+};
+
+template <bool F8>
+__device__ __forceinline__ void prologue_loads(const AttnParams& p, int seq, int kvh,
+                                               int64_t pos, ProPre<F8>& pp) {
+  // Branch-free: every lane loads from a valid address (lanes past the G + 2 rows re-read row
+  // G + 1's bytes; a missing norm weight / tail reads the qkv row instead), so the vmcnt
+  // counts stay exact -- an exec-masked branch here made hipcc wait vmcnt(0) at the merge.
+  const int G = p.G;
+  const int rr = min((int)(threadIdx.x >> 4), G + 1);
+  const int j = threadIdx.x & 15;
+  const int head = rr < G ? kvh * G + rr : (rr == G ? p.Hq + kvh : p.Hq + p.Hkv + kvh);
+  const bf16* row = p.qkv + (size_t)seq * p.qkv_stride;
+  pp.raw = *reinterpret_cast<const bf16x8*>(row + head * kD + 8 * j);
+  const bf16* nw = rr < G ? p.q_w : p.k_w;
+  pp.w8 = *reinterpret_cast<const bf16x8*>((nw != nullptr ? nw : row) + 8 * j);
+  const float* cs = p.cos_sin + (size_t)pos * kD;
+  const int i0 = 8 * (j & 7);
+  pp.c0 = *reinterpret_cast<const f32x4*>(cs + i0);
+  pp.c1 = *reinterpret_cast<const f32x4*>(cs + i0 + 4);
+  pp.s0 = *reinterpret_cast<const f32x4*>(cs + 64 + i0);
+  pp.s1 = *reinterpret_cast<const f32x4*>(cs + 64 + i0 + 4);
+  const bf16* tb = (!F8 && p.v_tail != nullptr)
+                       ? p.v_tail + ((size_t)max(pp.tsl, 0) * p.Hkv + kvh) * 8 * kD + 8 * j
+                       : row + 8 * j;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pp.trow[i] = *reinterpret_cast<const bf16x8*>(tb + (size_t)i * kD);
+}
+
+// fused_qkv_prologue on preloaded operands (same arithmetic, same stores)
+template <bool F8>
+__device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int kvh,
+                                                       bool write_kv, bf16* q_s, bool tail,
+                                                       bf16* v_img, const ProPre<F8>& pp) {
+  const int G = p.G;
+  const int rr = threadIdx.x >> 4;
+  const int j = threadIdx.x & 15;
+  if (rr < G + 2) {
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = bf2f(pp.raw[i]);
+    if (rr <= G) {
+      const bf16* nw = rr < G ? p.q_w : p.k_w;
+      if (nw != nullptr) {
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ss += x[i] * x[i];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+        const float inv = rsqrtf(ss / (float)kD + p.eps);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = bf2f(f2bf(x[i] * inv * bf2f(pp.w8[i])));
+      }
+      const float cv[8] = {pp.c0[0], pp.c0[1], pp.c0[2], pp.c0[3],
+                           pp.c1[0], pp.c1[1], pp.c1[2], pp.c1[3]};
+      const float sv[8] = {pp.s0[0], pp.s0[1], pp.s0[2], pp.s0[3],
+                           pp.s1[0], pp.s1[1], pp.s1[2], pp.s1[3]};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float other = __shfl_xor(x[i], 8, 16);
+        x[i] = j < 8 ? x[i] * cv[i] - other * sv[i] : x[i] * cv[i] + other * sv[i];
+      }
+    }
+    bf16x8 o8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o8[i] = f2bf(x[i]);
+    if (rr < G) {
+      *reinterpret_cast<bf16x8*>(q_s + rr * kD + 8 * j) = o8;
+    } else if (write_kv) {
+      const int64_t slot = pp.slot;
+      if (slot >= 0) {
+        const int64_t blk = slot / p.BS;
+        const int off = (int)(slot % p.BS);
+        if (rr == G) {
+          const size_t e = ((size_t)blk * p.Hkv + kvh) * p.BS * kD + k_swz_offset(off) +
+                           k_dim_offset(8 * j);
+          if constexpr (F8) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>((uint8_t*)p.k_cache + e);
+            dst[0] = f32x4_to_fp8x4((float)o8[0], (float)o8[1], (float)o8[2], (float)o8[3]);
+            dst[1] = f32x4_to_fp8x4((float)o8[4], (float)o8[5], (float)o8[6], (float)o8[7]);
+          } else {
+            *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
+          }
+        } else if (tail) {
+          const int i0 = off & 7;
+          bf16* tb = p.v_tail + ((size_t)pp.tsl * p.Hkv + kvh) * 8 * kD + 8 * j;
+          bf16x8 rows[8], u[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            rows[i] = i < i0 ? pp.trow[i] : (i == i0 ? o8 : bf16x8{0, 0, 0, 0, 0, 0, 0, 0});
+          group_units(rows, u);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(v_img + (8 * j + k) * 8) = u[k];
+          if (i0 == 7) {
+            bf16* e = (bf16*)p.v_cache + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
+                      (off >> 3) * kD * 8 + (size_t)(8 * j) * 8;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(e + 8 * k) = u[k];
+          } else {
+            *reinterpret_cast<bf16x8*>(tb + (size_t)i0 * kD) = o8;
+          }
+        } else {
+          const size_t e = ((size_t)blk * p.Hkv + kvh) * kD * p.BS + (off >> 3) * kD * 8 + (off & 7);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if constexpr (F8)
+              ((uint8_t*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = f32_to_fp8((float)o8[i]);
+            else
+              ((bf16*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = o8[i];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Barrier-free fused prologue (grid decode kernel, flags bit 9): every wave computes the q
+// fragments it feeds to the MFMAs itself, straight in the S^T = K . Q^T operand layout (lane
+// = 16 g + row: dims 32 c + 8 g .. + 7 for c = 0..3, so the RoPE partner d + 64 is the same
+// lane's c + 2 and the RMSNorm sum is a 4-lane reduce), and only the wave that owns the new
+// token's 32-token chunk writes its K/V (and builds the V-tail image that only that wave
+// reads).  With the workgroup-wide prologue (q through LDS), three of the four waves waited
+// at a barrier for wave 0's serial norm/RoPE/KV-write chain at the start of every item.
+// Measured: no faster (fused micro 113.7 vs 114.6 us, headline bench 50.7k vs 51.1k with the
+// workgroup prologue, profiles/r3_attn_rework_ab.log) -- the fused kernel's extra time over a
+// ready q is the new token's K/V line writes under the read stream, not the prologue chain --
+// so the workgroup prologue stays the default and this form is kept as an A/B variant.
+struct QPre {
+  bf16x8 raw[kNC], w[kNC];
+  f32x4 cs[2][4];  // [c = 0, 1][cos lo, cos hi, sin lo, sin hi] at dims 32 c + 8 g .. + 7
+};
+
+__device__ __forceinline__ void q_frag_loads(const AttnParams& p, int seq, int kvh, int64_t pos,
+                                             QPre& qp) {
+  const int lane = threadIdx.x & 63;
+  const int qr = lane & 15, g = lane >> 4;
+  const int head = kvh * p.G + min(qr, p.G - 1);  // rows past G re-read row G-1 (never used)
+  const bf16* src = p.qkv + (size_t)seq * p.qkv_stride + head * kD + 8 * g;
+  const bf16* wsrc = (p.q_w != nullptr ? p.q_w : src - head * kD) + 8 * g;
+  const float* cs = p.cos_sin + (size_t)pos * kD + 8 * g;
+#pragma unroll
+  for (int c = 0; c < kNC; ++c) {
+    qp.raw[c] = *reinterpret_cast<const bf16x8*>(src + 32 * c);
+    qp.w[c] = *reinterpret_cast<const bf16x8*>(wsrc + 32 * c);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    qp.cs[c][0] = *reinterpret_cast<const f32x4*>(cs + 32 * c);
+    qp.cs[c][1] = *reinterpret_cast<const f32x4*>(cs + 32 * c + 4);
+    qp.cs[c][2] = *reinterpret_cast<const f32x4*>(cs + 64 + 32 * c);
+    qp.cs[c][3] = *reinterpret_cast<const f32x4*>(cs + 64 + 32 * c + 4);
+  }
+}
+
+// q fragments of this lane (zeros for rows >= G): bf16(RMSNorm) -> NeoX RoPE in fp32 -> bf16,
+// the same arithmetic and rounding as fused_qkv_prologue
+__device__ __forceinline__ void q_frag_compute(const AttnParams& p, const QPre& qp,
+                                               bf16x8 (&qb)[kNC], bool valid) {
+  float x[kNC][8];
+#pragma unroll
+  for (int c = 0; c < kNC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[c][i] = bf2f(qp.raw[c][i]);
+  if (p.q_w != nullptr) {
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < kNC; ++c)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += x[c][i] * x[c][i];
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    const float inv = rsqrtf(ss / (float)kD + p.eps);
+#pragma unroll
+    for (int c = 0; c < kNC; ++c)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[c][i] = bf2f(f2bf(x[c][i] * inv * bf2f(qp.w[c][i])));
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float cv = i < 4 ? qp.cs[c][0][i] : qp.cs[c][1][i - 4];
+      const float sv = i < 4 ? qp.cs[c][2][i] : qp.cs[c][3][i - 4];
+      const float lo = x[c][i], hi = x[c + 2][i];
+      x[c][i] = lo * cv - hi * sv;
+      x[c + 2][i] = hi * cv + lo * sv;
+    }
+#pragma unroll
+  for (int c = 0; c < kNC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qb[c][i] = valid ? f2bf(x[c][i]) : (bf16)0.f;
+}
+
+// The new token's K (lanes 0-15) and V (lanes 16-31) of this kv head, by ONE wave: loads, K
+// norm + RoPE, cache / V-tail writes; the V-tail group image goes to this wave's LDS v_img.
+// Ends with the wave's stores drained (its later loads of those lines then see them).
+template <bool F8>
+__device__ __forceinline__ void kv_write_wave(const AttnParams& p, int seq, int kvh, int64_t slot,
+                                              int64_t pos, int tsl, bool tail, bf16* v_img) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 32 && slot >= 0) {
+    const int j = lane & 15;
+    const bool is_k = lane < 16;
+    const int head = is_k ? p.Hq + kvh : p.Hq + p.Hkv + kvh;
+    const bf16x8 raw =
+        *reinterpret_cast<const bf16x8*>(p.qkv + (size_t)seq * p.qkv_stride + head * kD + 8 * j);
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = bf2f(raw[i]);
+    const int64_t blk = slot / p.BS;
+    const int off = (int)(slot % p.BS);
+    if (is_k) {
+      if (p.k_w != nullptr) {
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ss += x[i] * x[i];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+        const float inv = rsqrtf(ss / (float)kD + p.eps);
+        const bf16x8 w8 = *reinterpret_cast<const bf16x8*>(p.k_w + 8 * j);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = bf2f(f2bf(x[i] * inv * bf2f(w8[i])));
+      }
+      const float* cs = p.cos_sin + (size_t)pos * kD;
+      const int i0 = 8 * (j & 7);
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + i0);
+      const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + i0 + 4);
+      const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + 64 + i0);
+      const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + 64 + i0 + 4);
+      const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float other = __shfl_xor(x[i], 8, 16);
+        x[i] = j < 8 ? x[i] * cv[i] - other * sv[i] : x[i] * cv[i] + other * sv[i];
+      }
+    }
+    bf16x8 o8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o8[i] = f2bf(x[i]);
+    if (is_k) {
+      const size_t e =
+          ((size_t)blk * p.Hkv + kvh) * p.BS * kD + k_swz_offset(off) + k_dim_offset(8 * j);
+      if constexpr (F8) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>((uint8_t*)p.k_cache + e);
+        dst[0] = f32x4_to_fp8x4((float)o8[0], (float)o8[1], (float)o8[2], (float)o8[3]);
+        dst[1] = f32x4_to_fp8x4((float)o8[4], (float)o8[5], (float)o8[6], (float)o8[7]);
+      } else {
+        *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
+      }
+    } else if (tail) {
+      const int i0 = off & 7;
+      bf16* tb = p.v_tail + ((size_t)tsl * p.Hkv + kvh) * 8 * kD + 8 * j;
+      bf16x8 rows[8], u[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)  // whole group loaded, then selected (no per-row branch)
+        rows[i] = *reinterpret_cast<const bf16x8*>(tb + (size_t)i * kD);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (i >= i0) rows[i] = i == i0 ? o8 : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      group_units(rows, u);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(v_img + (8 * j + k) * 8) = u[k];
+      if (i0 == 7) {
+        bf16* e = (bf16*)p.v_cache + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
+                  (off >> 3) * kD * 8 + (size_t)(8 * j) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(e + 8 * k) = u[k];
+      } else {
+        *reinterpret_cast<bf16x8*>(tb + (size_t)i0 * kD) = o8;
+      }
+    } else {
+      const size_t e = ((size_t)blk * p.Hkv + kvh) * kD * p.BS + (off >> 3) * kD * 8 + (off & 7);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (F8)
+          ((uint8_t*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = f32_to_fp8((float)o8[i]);
+        else
+          ((bf16*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = o8[i];
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+struct QHead {
+  QPre qp;
+  int64_t pos, slot;
+  int tsl;
+};
+
 // What a decode work item needs before its first K/V byte can be requested: the sequence's
 // length, the cache block ids of the wave's chunks (lane j: chunk pstart + 32 w + 128 j, read
 // later with readlane: an SGPR, no memory instruction in the chunk loop) and, with PREFETCH,
@@ -408,9 +714,12 @@ struct ItemHead {
   ChunkT<F8> cur;
 };
 
-template <bool PREFETCH, bool NT, bool F8>
+// PRE: 0 = nothing else, 1 = the workgroup prologue's operands (ProPre), 2 = the barrier-free
+// prologue's q operands + the new token's position / slot / tail slot (QHead)
+template <bool PREFETCH, bool NT, bool F8, int PRE = 0>
 __device__ __forceinline__ void item_head(const AttnParams& p, ItemHead<F8>& h, int seq, int kvh,
-                                          int part) {
+                                          int part, ProPre<F8>* pp = nullptr,
+                                          QHead* qh = nullptr) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   h.seq = seq;
@@ -421,19 +730,40 @@ __device__ __forceinline__ void item_head(const AttnParams& p, ItemHead<F8>& h, 
   const int bi = min((t0 + 128 * lane) / p.BS, p.bt_stride - 1);
   h.btr = p.block_tables[(size_t)seq * p.bt_stride + bi];
   h.kv_len = p.seq_lens[seq];
+  if constexpr (PRE == 1) {  // fused-prologue operands: issued ahead of the chunk (see ProPre)
+    const int64_t pos = p.positions[seq];
+    pp->slot = p.slots[seq];
+    pp->tsl = (!F8 && p.v_tail != nullptr) ? p.tail_slot[seq] : -1;
+    prologue_loads<F8>(p, seq, kvh, pos, *pp);
+    __builtin_amdgcn_sched_barrier(0);
+  } else if constexpr (PRE == 2) {  // q operands ahead of the chunk (see QPre)
+    qh->pos = p.positions[seq];
+    qh->slot = p.slots[seq];
+    qh->tsl = (!F8 && p.v_tail != nullptr) ? p.tail_slot[seq] : -1;
+    q_frag_loads(p, seq, kvh, qh->pos, qh->qp);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   const int pend = min(h.kv_len, pstart + p.part_size);
-  if (PREFETCH && t0 < pend)
-    load_chunk_blk<NT, F8>(h.cur, p.k_cache, p.v_cache, __builtin_amdgcn_readlane(h.btr, 0),
-                           h.kv_len, kvh, p.Hkv, p.BS, t0);
+  if constexpr (PREFETCH) {
+    // issued unconditionally (a wave with no chunk reads block 0, never used): a branch here
+    // left the two paths with different load counts, and hipcc's merged vmcnt count then
+    // waited on part of the chunk inside the prologue
+    const bool has = t0 < pend;
+    load_chunk_blk<NT, F8>(h.cur, p.k_cache, p.v_cache,
+                           has ? __builtin_amdgcn_readlane(h.btr, 0) : 0, max(h.kv_len, 1), kvh,
+                           p.Hkv, p.BS, has ? t0 : 0);
+  }
 }
 
 // One (seq, kv head, partition) work item whose head item_head() has fetched.  after_loop()
 // runs once the chunk loop is done (h.cur / h.btr are dead then: the pipelined kernel fetches
 // the next item's head into h there), before the LDS combine.  Callers that run several
 // items per workgroup must __syncthreads() before the next item's LDS writes.
-template <bool PREFETCH, bool NT, bool FUSED, bool F8, typename AfterLoop>
+template <bool PREFETCH, bool NT, bool FUSED, bool F8, int PRE = 0, typename AfterLoop>
 __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>& h,
-                                              float* dyn_lds, AfterLoop after_loop) {
+                                              float* dyn_lds, AfterLoop after_loop,
+                                              const ProPre<F8>* pp = nullptr,
+                                              const QHead* qh = nullptr) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int g = lane >> 4;
@@ -462,15 +792,39 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
   // V tail: the sequence's last 8-token group (first token gstart) is read from an LDS image
   // instead of the cache -- fused: the image the prologue builds (tail + the new token);
   // plain: a still-partial group straight from the tail (the writer kernel put it there)
-  const int tsl = (!F8 && p.v_tail != nullptr && kv_len > 0) ? p.tail_slot[seq] : -1;
+  int tsl;
+  bool use_img;
+  if constexpr (PRE == 1) {
+    tsl = kv_len > 0 ? pp->tsl : -1;
+    use_img = tsl >= 0 && writes_kv && pp->slot >= 0;
+  } else if constexpr (PRE == 2) {
+    tsl = kv_len > 0 ? qh->tsl : -1;
+    use_img = tsl >= 0 && writes_kv && qh->slot >= 0;
+  } else {
+    tsl = (!F8 && p.v_tail != nullptr && kv_len > 0) ? p.tail_slot[seq] : -1;
+    use_img = tsl >= 0 && writes_kv && (FUSED ? p.slots[seq] >= 0 : (kv_len & 7) != 0);
+  }
   const int gstart = (kv_len - 1) & ~7;
-  const bool use_img = tsl >= 0 && writes_kv && (FUSED ? p.slots[seq] >= 0 : (kv_len & 7) != 0);
   int t0 = pstart + 32 * w;
   const int tw = t0;  // the wave's first chunk (t0 itself advances in the loop below)
   // j < 64 always: the host caps part_size at kDecodeMaxPart (64 chunks per wave)
   auto blk_of = [=](int tc) -> int { return __builtin_amdgcn_readlane(btr, (tc - tw) >> 7); };
-  if constexpr (FUSED) {
-    fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s, use_img ? tsl : -1, v_img);
+  bf16x8 qpre[kNC];
+  if constexpr (FUSED && PRE == 2) {
+    q_frag_compute(p, qh->qp, qpre, valid);
+    // the wave owning the new token's chunk writes its K/V (and the V-tail image it alone
+    // reads); if that chunk is the wave's prefetched first one, it is re-read after the write
+    if (writes_kv && (((kv_len - 1 - pstart) >> 5) & 3) == w) {
+      kv_write_wave<F8>(p, seq, kvh, qh->slot, qh->pos, tsl, use_img, v_img);
+      if (PREFETCH && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
+        load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS,
+                               t0);
+    }
+  } else if constexpr (FUSED) {
+    if constexpr (PRE == 1)
+      fused_qkv_prologue_pre<F8>(p, kvh, writes_kv, q_s, use_img, v_img, *pp);
+    else
+      fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s, use_img ? tsl : -1, v_img);
     // the chunk holding the token the prologue just wrote is re-read after the barrier
     if (PREFETCH && writes_kv && t0 < pend && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
       load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS,
@@ -495,7 +849,10 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
   wave_state_init(st);
   if (pstart < pend) {
     bf16x8 qb[kNC];
-    if constexpr (FUSED) {
+    if constexpr (FUSED && PRE == 2) {
+#pragma unroll
+      for (int c = 0; c < kNC; ++c) qb[c] = qpre[c];
+    } else if constexpr (FUSED) {
 #pragma unroll
       for (int c = 0; c < kNC; ++c)
         qb[c] = valid ? *reinterpret_cast<const bf16x8*>(q_s + qr * kD + 32 * c + 8 * g)
@@ -504,21 +861,34 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
       load_q(qb, qptr, valid);
     }
     if constexpr (PREFETCH) {
-      // register double buffer: chunk i+1's loads are in flight during chunk i's MFMAs
-      if (t0 < pend) {
-        for (; t0 < pend; t0 += 128) {
-          ChunkT<F8> nxt;
-          const bool more = t0 + 128 < pend;
-          if (more)
-            load_chunk_blk<NT, F8>(nxt, p.k_cache, p.v_cache, blk_of(t0 + 128), kv_len, kvh,
-                                   p.Hkv, p.BS, t0 + 128);
-          if (use_img && t0 <= gstart && gstart < t0 + 32) patch_v(cur, t0, gstart, v_img);
-          if (t0 + 31 < kv_len)
-            compute_chunk<false>(st, qb, cur, t0, limit, p.scale_log2);
-          else
-            compute_chunk<true>(st, qb, cur, t0, limit, p.scale_log2);
-          if (more) cur = nxt;
-        }
+      // Register double buffer as two NAMED chunk sets that alternate (the loop is unrolled
+      // by two), never copied: with `cur = nxt` hipcc moved the registers at the end of each
+      // iteration behind an `s_waitcnt vmcnt(0)`, so chunk i+2 could only be requested once
+      // chunk i+1 had landed (one chunk in flight per wave).  Here chunk i+2's loads go into
+      // the set chunk i just released while chunk i+1 may still be in flight, and each
+      // compute waits only for its own set (counted vmcnt).  Loads are issued on every step:
+      // past the last chunk every lane re-reads block 0's first rows (a few cache-resident
+      // lines, never used) -- an `if (more)` around them made hipcc's merged vmcnt count
+      // assume the no-load path and wait for the other set as well.
+      ChunkT<F8> nb;
+      auto fetch = [&](ChunkT<F8>& c, int tc) {
+        const bool has = tc < pend;
+        load_chunk_blk<NT, F8>(c, p.k_cache, p.v_cache, has ? blk_of(tc) : 0, has ? kv_len : 1,
+                               kvh, p.Hkv, p.BS, has ? tc : 0);
+      };
+      auto consume = [&](ChunkT<F8>& c, int tc) {
+        if (use_img && tc <= gstart && gstart < tc + 32) patch_v(c, tc, gstart, v_img);
+        if (tc + 31 < kv_len)
+          compute_chunk<false>(st, qb, c, tc, limit, p.scale_log2);
+        else
+          compute_chunk<true>(st, qb, c, tc, limit, p.scale_log2);
+      };
+      for (; t0 < pend; t0 += 256) {
+        fetch(nb, t0 + 128);
+        consume(cur, t0);
+        if (t0 + 128 >= pend) break;
+        fetch(cur, t0 + 256);
+        consume(nb, t0 + 128);
       }
     } else {
       for (; t0 < pend; t0 += 128) {
@@ -588,8 +958,20 @@ template <bool PREFETCH, bool NT = false, bool FUSED = false, bool F8 = false>
 __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
                                             float* dyn_lds) {
   ItemHead<F8> h;
-  item_head<PREFETCH, NT, F8>(p, h, seq, kvh, part);
-  decode_item_h<PREFETCH, NT, FUSED, F8>(p, h, dyn_lds, [] {});
+  if constexpr (FUSED && PREFETCH) {
+    if (p.flags & 512) {  // bit 9: the barrier-free prologue (A/B; measured no faster)
+      QHead qh;
+      item_head<PREFETCH, NT, F8, 2>(p, h, seq, kvh, part, nullptr, &qh);
+      decode_item_h<PREFETCH, NT, FUSED, F8, 2>(p, h, dyn_lds, [] {}, nullptr, &qh);
+    } else {  // default: workgroup prologue on operands loaded ahead of the first chunk
+      ProPre<F8> pp;
+      item_head<PREFETCH, NT, F8, 1>(p, h, seq, kvh, part, &pp);
+      decode_item_h<PREFETCH, NT, FUSED, F8, 1>(p, h, dyn_lds, [] {}, &pp);
+    }
+  } else {
+    item_head<PREFETCH, NT, F8>(p, h, seq, kvh, part);
+    decode_item_h<PREFETCH, NT, FUSED, F8>(p, h, dyn_lds, [] {});
+  }
 }
 
 // grid = (num_seqs, Hkv, num_parts): one work item per workgroup.

@@ -20,6 +20,8 @@
 // the 16 lanes of each ds_read_b128 lane group (rows 0-3, 12-15 at chunk c, rows 4-11 at c+1)
 // land on 16 distinct 16-B bank positions: conflict-free (XOR with row & 7 measured 48 %
 // bank-conflict cycles, profiles/r2_pmc_decode_v2.md).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -27,7 +29,6 @@ namespace akap {
 
 constexpr int KBN = 32;    // output columns per workgroup
 constexpr int KST = 256;   // K per stage (4 waves x 64)
-constexpr int KNS = 4;     // ring slots
 
 __device__ __forceinline__ int kswz(int row, int chunk) { return row * 32 + (chunk ^ (row & 15)); }
 
@@ -42,7 +43,10 @@ __device__ __forceinline__ void kwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BM, int EPI>
+// KNS ring slots: 4 (3 stages = 96 KB in flight) or 5 (4 stages, 128 KB: at one workgroup
+// per CU the K loop streams at in-flight bytes / load latency, so a deeper ring is the lever;
+// the 5-slot ring of 32-row stages is the whole 160 KB LDS)
+template <int BM, int EPI, int KNS>
 __global__ __launch_bounds__(256, 1) void kgemm_kernel(DGemmArgs p) {
   constexpr int ROWS = BM + KBN;            // staged rows per stage (X rows, then W rows)
   constexpr int SU = ROWS * 32;             // 16-B units per slot
@@ -182,16 +186,27 @@ bool kgemm_supported(int M, int N, int K, int bm) {
   return M > 0 && (bm == 16 || bm == 32) && N % KBN == 0 && K >= KST && K % KST == 0;
 }
 
+template <int KNS>
+static void kgemm_ns(const DGemmArgs& p, int bm, int grid, hipStream_t st) {
+  if (bm == 16) {
+    if (p.epi == EPI_RESNORM) kgemm_kernel<16, EPI_RESNORM, KNS><<<grid, 256, 0, st>>>(p);
+    else kgemm_kernel<16, EPI_STORE, KNS><<<grid, 256, 0, st>>>(p);
+  } else {
+    if (p.epi == EPI_RESNORM) kgemm_kernel<32, EPI_RESNORM, KNS><<<grid, 256, 0, st>>>(p);
+    else kgemm_kernel<32, EPI_STORE, KNS><<<grid, 256, 0, st>>>(p);
+  }
+}
+
 void launch_kgemm(const DGemmArgs& p, int bm, hipStream_t st) {
   if (p.M == 0) return;
   const int grid = ((p.M + bm - 1) / bm) * (p.N / KBN);
-  if (bm == 16) {
-    if (p.epi == EPI_RESNORM) kgemm_kernel<16, EPI_RESNORM><<<grid, 256, 0, st>>>(p);
-    else kgemm_kernel<16, EPI_STORE><<<grid, 256, 0, st>>>(p);
-  } else {
-    if (p.epi == EPI_RESNORM) kgemm_kernel<32, EPI_RESNORM><<<grid, 256, 0, st>>>(p);
-    else kgemm_kernel<32, EPI_STORE><<<grid, 256, 0, st>>>(p);
-  }
+  // ring depth: AKAP_KGEMM_NS=5 selects the 5-slot ring (A/B knob, read once)
+  static const int ns = [] {
+    const char* e = std::getenv("AKAP_KGEMM_NS");
+    return e && std::atoi(e) == 5 ? 5 : 4;
+  }();
+  if (ns == 5) kgemm_ns<5>(p, bm, grid, st);
+  else kgemm_ns<4>(p, bm, grid, st);
 }
 
 }  // namespace akap

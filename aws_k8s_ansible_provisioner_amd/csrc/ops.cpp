@@ -143,7 +143,8 @@ static void set_v_tail(akap::AttnParams& p, const std::optional<Tensor>& v_tail,
 //   per step, keep it out of L2/MALL (-5.5% decode attention time measured)
 // bits3-5: persistent decode grid (WGs per CU); bit7: with bits 3-5 on the fused path, the
 //   pipelined persistent kernel (next item's head fetched under the current item's tail);
-//   bit1/2: occupancy variants (off).  AKAP_ATTN_FLAGS sets the process default;
+//   bit8: fused grid kernel single-buffered at 3 WGs/CU; bit9: barrier-free fused prologue;
+//   bit1/2: occupancy variants (off).  All measured slower than the default or equal.  AKAP_ATTN_FLAGS sets the process default;
 //   set_attn_flags() swaps it at run time (tests and in-process A/B of the variants).
 static int& attn_flags_ref() {
   static int f = [] {

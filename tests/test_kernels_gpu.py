@@ -941,8 +941,8 @@ def attn_flags_variant(request):
 
 # 65 = the default grid kernel; 81 = persistent grid, 2 workgroups per CU; 209 = the same with
 # the pipelined kernel (next item's head fetched under the current item's tail); 321 = the grid
-# kernel single-buffered at 3 workgroups per CU
-@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321], indirect=True)
+# kernel single-buffered at 3 workgroups per CU; 577 = the barrier-free fused prologue
+@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321, 577], indirect=True)
 @pytest.mark.parametrize("num_parts,part_size,lens", [
     (1, 4096, [1, 31, 32, 33, 200, 777, 1500] * 40),  # 280 seqs x 8 heads: > 1 item per WG
     (3, 512, [1, 31, 32, 33, 200, 777, 1500]),
@@ -955,7 +955,7 @@ def test_paged_attention_decode_fused_persistent_variants(attn_flags_variant, nu
     test_paged_attention_decode_fused(16, 8, True, num_parts, part_size, lens=list(lens))
 
 
-@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321], indirect=True)
+@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321, 577], indirect=True)
 def test_v_tail_decode_persistent_variants(attn_flags_variant):
     """V tail path through the persistent / pipelined decode kernels: bit-identical to the
     plain per-token cache path over 20 steps."""
