@@ -46,6 +46,16 @@ constexpr int GBK = 64;
 
 __device__ __forceinline__ int gswz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
+// LDS image of a BKT-deep k-step: rows of BKT * 2 bytes in 16-B chunks, XOR-swizzled so the 16
+// lanes of a ds_read_b128 lane group (16 consecutive rows, one chunk) hit 16 distinct 16-B bank
+// positions.  BKT = 64: 8 chunks per row, chunk ^ (row & 7).  BKT = 32: 4 chunks per row (four
+// rows per 256-B bank row), chunk ^ ((row >> 2) & 3).
+template <int BKT>
+__device__ __forceinline__ int gswz_t(int row, int chunk) {
+  if constexpr (BKT == 64) return row * 8 + (chunk ^ (row & 7));
+  else return row * 4 + (chunk ^ ((row >> 2) & 3));
+}
+
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
@@ -58,17 +68,27 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BN, int NS, int EPI, int SPL, int OCC, int S, int GBM = 64, int NW = 4>
+// BKT: k-step depth, 64 or 32.  BKT = 32 halves the slot (the 256 x 128 tile's 48 KB -> 24 KB)
+// so the 144 KB of LDS holds a 6-slot ring with five k-steps in flight instead of two (ns = 6).
+// Measured slower on every M = 256 shape (Llama-3-8B gate_up 89.4 vs 80.2 us, qkv 32.9 vs
+// 28.3: profiles/r3_gemm_m256_deep.log): the 256-row tiles are not bound by the ring's bytes
+// in flight; twice the barriers per K and half the MFMA work between them cost more.  Kept
+// selectable (ns = 6) for A/B, not a tuner candidate.
+template <int BN, int NS, int EPI, int SPL, int OCC, int S, int GBM = 64, int NW = 4,
+          int BKT = 64>
 __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   constexpr int NT = 64 * NW;             // threads
   constexpr int WMW = NW / 2;             // waves along M (2 along N)
   constexpr int WR = GBM / WMW;           // wave tile rows (wave tile WR x BN/2)
-  constexpr int SU = (GBM + BN) * 8;      // slot size in 16-B units
+  constexpr int CPR = BKT / 8;            // 16-B chunks per staged row
+  constexpr int RPI = 64 / CPR;           // rows per DMA instruction (64 lanes x 16 B)
+  constexpr int SU = (GBM + BN) * CPR;    // slot size in 16-B units
   constexpr int MI = WR / 16;             // 16-row MFMA tiles per wave
   constexpr int JN = BN / 32;             // 16-col MFMA tiles per wave
-  constexpr int GA = GBM / (8 * NW), GW = BN / (8 * NW);  // DMA instructions per wave per k-step
+  constexpr int GA = GBM / (RPI * NW), GW = BN / (RPI * NW);  // DMA instrs per wave per k-step
   constexpr int G = GA + GW;
-  static_assert(GA * 8 * NW == GBM && GW * 8 * NW == BN, "8-row DMA pieces cover the tile");
+  static_assert(BKT == 64 || BKT == 32, "k-step 64 | 32");
+  static_assert(GA * RPI * NW == GBM && GW * RPI * NW == BN, "DMA pieces cover the tile");
   // ONE __shared__ object (a second one makes hipcc drain vmcnt inside the k-loop,
   // cdna_hip_programming.md "Projection GEMM at M = 256" item 4a); the last element is the
   // split-K "this block combines" flag
@@ -82,7 +102,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   const int m0 = tm * GBM, n0 = tn * BN;
   const int kz = blockIdx.y;
   const int kbeg = kz * p.kps;
-  const int nk = p.kps / GBK;
+  const int nk = p.kps / BKT;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int fr = lane & 15, fg = lane >> 4;
@@ -90,20 +110,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   const bf16* W = static_cast<const bf16*>(p.W);
   bf16* Y = static_cast<bf16*>(p.Y);
 
-  // per-lane DMA sources: instruction covers 8 rows x 128 B; lane -> row L/8, LDS chunk L%8
-  // holding logical chunk (L%8) ^ (L/8)  (row & 7 == L/8 since every instruction starts on a
-  // multiple of 8 rows)
-  const int lr = lane >> 3, lc = (lane & 7) ^ (lane >> 3);
+  // per-lane DMA sources: an instruction covers RPI rows x BKT*2 B; lane -> row L/CPR, LDS
+  // chunk L%CPR holding the logical chunk that gswz_t maps there (the swizzle's row bits are
+  // the lane's: every instruction starts on a multiple of RPI rows)
+  const int lr = lane / CPR;
+  const int lc = BKT == 64 ? (lane & 7) ^ (lane >> 3) : (lane & 3) ^ ((lane >> 4) & 3);
   const bf16* asrc[GA];
   const bf16* wsrc[GW];
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int row = m0 + (w * GA + i) * 8 + lr;
+    const int row = m0 + (w * GA + i) * RPI + lr;
     asrc[i] = X + (size_t)(row < p.M ? row : 0) * p.ldx + lc * 8;
   }
 #pragma unroll
   for (int i = 0; i < GW; ++i) {
-    const int v = n0 + (w * GW + i) * 8 + lr;
+    const int v = n0 + (w * GW + i) * RPI + lr;
     int wrow = v < p.N ? v : 0;
     if constexpr (EPI == EPI_SILU)
       wrow = v < p.N ? ((v >> 4) & 1) * (p.N >> 1) + (v >> 5) * 16 + (v & 15) : 0;
@@ -111,11 +132,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   }
   auto issue = [&](int step) {  // DMA k-step `step` into its ring slot
     bf16x8* slot = lds + (step % NS) * SU;
-    const int k0 = kbeg + step * GBK;
+    const int k0 = kbeg + step * BKT;
 #pragma unroll
     for (int i = 0; i < GA; ++i) glds16(asrc[i] + k0, slot + (w * GA + i) * 64);
 #pragma unroll
-    for (int i = 0; i < GW; ++i) glds16(wsrc[i] + k0, slot + GBM * 8 + (w * GW + i) * 64);
+    for (int i = 0; i < GW; ++i) glds16(wsrc[i] + k0, slot + GBM * CPR + (w * GW + i) * 64);
   };
 
   // epilogue operands from the previous launch: load before the loop (hidden under it)
@@ -171,13 +192,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
     if (t + NS - 1 < nk) issue(t + NS - 1);
     const bf16x8* slot = lds + (t % NS) * SU;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BKT / 32; ++ks) {
       bf16x8 af[MI], bfr[JN];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = slot[gswz(wm * WR + i * 16 + fr, ks * 4 + fg)];
+      for (int i = 0; i < MI; ++i) af[i] = slot[gswz_t<BKT>(wm * WR + i * 16 + fr, ks * 4 + fg)];
 #pragma unroll
       for (int j = 0; j < JN; ++j)
-        bfr[j] = slot[GBM * 8 + gswz(wn * (BN / 2) + j * 16 + fr, ks * 4 + fg)];
+        bfr[j] = slot[GBM * CPR + gswz_t<BKT>(wn * (BN / 2) + j * 16 + fr, ks * 4 + fg)];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -299,32 +320,32 @@ long gdgemm_ws_floats(int M, int N, int splitk, int bn, int bm) {
   return slabs > dense ? slabs : dense;
 }
 
-template <int BN, int NS, int OCC, int SPL, int S, int BM, int NW>
+template <int BN, int NS, int OCC, int SPL, int S, int BM, int NW, int BKT>
 static void gdgemm_epi(const DGemmArgs& p, dim3 grid, hipStream_t st) {
   if (p.epi == EPI_RESNORM) {
-    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S, BM, NW><<<grid, 64 * NW, 0, st>>>(p);
+    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S, BM, NW, BKT><<<grid, 64 * NW, 0, st>>>(p);
   } else if (p.epi == EPI_SILU) {
     if constexpr (SPL != 1)
-      gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S, BM, NW><<<grid, 64 * NW, 0, st>>>(p);
+      gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S, BM, NW, BKT><<<grid, 64 * NW, 0, st>>>(p);
   } else {
-    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S, BM, NW><<<grid, 64 * NW, 0, st>>>(p);
+    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S, BM, NW, BKT><<<grid, 64 * NW, 0, st>>>(p);
   }
 }
 
-template <int BN, int NS, int OCC, int BM = 64, int NW = 4>
+template <int BN, int NS, int OCC, int BM = 64, int NW = 4, int BKT = 64>
 static void gdgemm_ring(const DGemmArgs& p, dim3 grid, int splitk, hipStream_t st) {
   if (splitk == 1) {
-    gdgemm_epi<BN, NS, OCC, 0, 1, BM, NW>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 0, 1, BM, NW, BKT>(p, grid, st);
   } else if (p.counters == nullptr) {
-    gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW, BKT>(p, grid, st);
     launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
   } else {
     switch (splitk) {
-      case 2: gdgemm_epi<BN, NS, OCC, 2, 2, BM, NW>(p, grid, st); break;
-      case 4: gdgemm_epi<BN, NS, OCC, 2, 4, BM, NW>(p, grid, st); break;
-      case 8: gdgemm_epi<BN, NS, OCC, 2, 8, BM, NW>(p, grid, st); break;
+      case 2: gdgemm_epi<BN, NS, OCC, 2, 2, BM, NW, BKT>(p, grid, st); break;
+      case 4: gdgemm_epi<BN, NS, OCC, 2, 4, BM, NW, BKT>(p, grid, st); break;
+      case 8: gdgemm_epi<BN, NS, OCC, 2, 8, BM, NW, BKT>(p, grid, st); break;
       default:  // 16 slices: slabs + the separate reduce pass
-        gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW>(p, grid, st);
+        gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW, BKT>(p, grid, st);
         launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
         break;
     }
@@ -336,8 +357,10 @@ void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st) {
   const int tiles = ((p.M + bm - 1) / bm) * ((p.N + p.bn - 1) / p.bn);
   dim3 grid(tiles, splitk);
   const bool deep = p.ns >= 6;
-  if (bm == 256) {  // 256-row tiles, 8 waves: 3 x 48 KB (BN 128) / 3 x 40 KB (BN 64) ring
-    if (p.bn == 128) gdgemm_ring<128, 3, 1, 256, 8>(p, grid, splitk, st);
+  if (bm == 256) {  // 256-row tiles, 8 waves: 3 x 48 KB (BN 128) / 3 x 40 KB (BN 64) ring;
+                    // ns >= 6 (BN 128): 6 x 24 KB ring of 32-deep k-steps, five in flight
+    if (p.bn == 128 && p.ns >= 6) gdgemm_ring<128, 6, 1, 256, 8, 32>(p, grid, splitk, st);
+    else if (p.bn == 128) gdgemm_ring<128, 3, 1, 256, 8>(p, grid, splitk, st);
     else gdgemm_ring<64, 3, 1, 256, 8>(p, grid, splitk, st);
     return;
   }

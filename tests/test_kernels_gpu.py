@@ -644,7 +644,8 @@ def test_fused_decode_gemm_in_graph():
 
 
 @pytest.mark.parametrize("ring", ["shallow", "deep", "deep-inlaunch", "shallow-inlaunch",
-                                  "rows128", "rows128-inlaunch", "rows256", "rows256-inlaunch"])
+                                  "rows128", "rows128-inlaunch", "rows256", "rows256-inlaunch",
+                                  "rows256deep", "rows256deep-inlaunch"])
 @pytest.mark.parametrize("bn", [64, 128])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K,splitk", [(1, 256, 1024, 1), (37, 1024, 2048, 2),
@@ -656,14 +657,16 @@ def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
     """gdgemm.hip (global_load_lds ring) with each epilogue vs fp32 references: shallow
     (2 blocks/CU) and deep (1 block/CU) rings, split-K reduced by the separate pass or
     combined in-launch by the last-arriving slice (also for the SwiGLU epilogue); 128-row
-    tiles and 256-row tiles (8 waves, 512 threads, row tails at M = 130 / 200 / 1 / 37)."""
+    tiles and 256-row tiles (8 waves, 512 threads, row tails at M = 130 / 200 / 1 / 37), the
+    latter also with the 6-slot ring of 32-deep k-steps (rows256deep: ns = 6)."""
     inl = ring.endswith("inlaunch")
     bm = 256 if ring.startswith("rows256") else 128 if ring.startswith("rows128") else 64
     if inl and splitk == 1:
         pytest.skip("in-launch combine needs split-K")
     if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=bn, inlaunch=inl, bm=bm):
         pytest.skip("unsupported combination")
-    kw = dict(ns=8 if ring.startswith("deep") else 0, inlaunch=inl, bm=bm)
+    kw = dict(ns=8 if ring.startswith("deep") else 6 if "deep" in ring else 0, inlaunch=inl,
+              bm=bm)
     torch.manual_seed(M + N + K + epi + bn)
     eps = 1e-6
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)

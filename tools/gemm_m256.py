@@ -59,17 +59,21 @@ def main():
                         for inl in ((False, True) if s > 1 else (False,)):
                             if not ops.dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl, bm=bm):
                                 continue
-                            ns = 3 if bm == 256 else 4
-                            fn = gt._gd_call(M, N, K, s, bn, ns, inl, y, x, ws_, 0, None, None,
-                                             None, None, bm)
-                            if bm == 256:
-                                fn(0)
-                                torch.cuda.synchronize()
-                                err = (y.float() - ref).abs().max().item()
-                                scale = ref.abs().max().item()
-                                assert err <= 2e-2 * scale + 1e-2, (name, s, bn, inl, err, scale)
-                            t = gt._timed(fn, L)
-                            res.append((f"s{s} g{bn}x{bm}" + ("i" if inl else ""), t))
+                            for ns in ((3, 6) if bm == 256 and bn == 128 else
+                                       (3,) if bm == 256 else (4,)):
+                                fn = gt._gd_call(M, N, K, s, bn, ns, inl, y, x, ws_, 0, None,
+                                                 None, None, None, bm)
+                                if bm == 256:
+                                    y.fill_(float("nan"))
+                                    fn(0)
+                                    torch.cuda.synchronize()
+                                    err = (y.float() - ref).abs().max().item()
+                                    scale = ref.abs().max().item()
+                                    assert err <= 2e-2 * scale + 1e-2, (name, s, bn, ns, inl, err,
+                                                                        scale)
+                                t = gt._timed(fn, L)
+                                res.append((f"s{s} g{bn}x{bm}" + ("d" if ns == 6 else "") +
+                                            ("i" if inl else ""), t))
             res.sort(key=lambda r: r[1])
             best = res[0]
             tot_best += best[1]
