@@ -81,7 +81,8 @@ __device__ __forceinline__ void wait_vm() {
 // a wave's LDS reads overlap its own MFMAs.  Without it a k-step is [barrier, all 16 fragment
 // reads, all 32 MFMAs]: both waves of a SIMD read LDS together, then both run MFMAs together
 // (PMC on Llama-3-8B gate_up, 256-row tile: MFMA busy 43 %, issue stalls 40 % / waitcnt-or-
-// barrier waits 36 % of wave cycles; profiles/r3_gemm_pmc.md).  With PIPE the prologue fills
+// barrier waits 36 % of wave cycles; profiles/r3_gemm_pmc.md).  Measured within 2 % of the plain
+// loop (profiles/r3_gemm_pipe_ab.log): off by default.  With PIPE the prologue fills
 // all NS slots and each mid-step barrier frees the slot just read for step t + NS.
 template <int BN, int NS, int EPI, int SPL, int OCC, int S, int GBM = 64, int NW = 4,
           int BKT = 64, int PIPE = 0>
