@@ -205,6 +205,28 @@ __device__ __forceinline__ void patch_v(ChunkT<F8>& c, int t0, int gstart, const
   }
 }
 
+// The new token's K row from the LDS image the fused prologue wrote (serving path with the V
+// tail): the lanes whose fragment row is token `tok` of the chunk at t0 take their 4 x 16 B
+// from k_img instead of the cache, so no wave has to wait for the prologue's cache store.
+template <bool F8>
+__device__ __forceinline__ void patch_k(ChunkT<F8>& c, int t0, int tok, const bf16* k_img) {
+  if constexpr (!F8) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, r = lane & 15;
+    const int pi = tok - t0;
+    const bool hit = r == 4 * (pi >> 3) + (pi & 3);
+    const bool t1 = (pi >> 2) & 1;
+    // every lane reads the image and selects (conditional stores into one of the two tile
+    // arrays made hipcc demote the chunk to scratch: 304 B/lane, 2x slower)
+#pragma unroll
+    for (int cc = 0; cc < kNC; ++cc) {
+      const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(k_img + 32 * cc + 8 * g);
+      c.ka[0][cc] = hit && !t1 ? k8 : c.ka[0][cc];
+      c.ka[1][cc] = hit && t1 ? k8 : c.ka[1][cc];
+    }
+  }
+}
+
 // Load this lane's Q^T operand for query row (lane & 15) (zeros if invalid).
 __device__ __forceinline__ void load_q(bf16x8 (&qb)[kNC], const bf16* qrow_ptr, bool valid) {
   const int g = (threadIdx.x & 63) >> 4;
@@ -439,10 +461,17 @@ __device__ __forceinline__ void prologue_loads(const AttnParams& p, int seq, int
 }
 
 // fused_qkv_prologue on preloaded operands (same arithmetic, same stores)
+// tail (the serving path: V through the V tail): the new token's K row also goes to the LDS
+// image k_img and V to v_img, the chunk loop patches both in from LDS (patch_k / patch_v), so
+// nothing in this kernel reads the new token's cache lines back -- the closing barrier then
+// waits only for the LDS writes (lgkmcnt), not for the cache stores (with __syncthreads its
+// vmcnt(0) also drained every wave's in-flight first chunk: fused 109.8 vs 105.6 us without
+// the writes, profiles/r3_attn_fused_breakdown.log).
 template <bool F8>
 __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int kvh,
                                                        bool write_kv, bf16* q_s, bool tail,
-                                                       bf16* v_img, const ProPre<F8>& pp) {
+                                                       bf16* v_img, const ProPre<F8>& pp,
+                                                       bf16* k_img) {
   const int G = p.G;
   const int rr = threadIdx.x >> 4;
   const int j = threadIdx.x & 15;
@@ -491,6 +520,7 @@ __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int 
             dst[1] = f32x4_to_fp8x4((float)o8[4], (float)o8[5], (float)o8[6], (float)o8[7]);
           } else {
             *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
+            if (tail) *reinterpret_cast<bf16x8*>(k_img + 8 * j) = o8;
           }
         } else if (tail) {
           const int i0 = off & 7;
@@ -523,7 +553,12 @@ __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int 
       }
     }
   }
-  __syncthreads();
+  if (tail) {  // uniform: LDS images only; the cache stores stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
 }
 
 // Barrier-free fused prologue (grid decode kernel, flags bit 9): every wave computes the q
@@ -787,6 +822,7 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
 #define OS(w_, r_, d_) o_s[((w_) * G + (r_)) * (kD + 4) + (d_)]
   bf16* q_s = reinterpret_cast<bf16*>(l_s + 4 * G);  // [G][kD] (fused only)
   bf16* v_img = q_s + (FUSED ? G * kD : 0);          // [kD][8] V tail group image
+  bf16* k_img = v_img + kD * 8;                      // [kD] new token's K (fused + V tail)
   const int limit = kv_len - 1;
   const bool writes_kv = kv_len > 0 && pstart <= kv_len - 1 && kv_len - 1 < pend;
   // V tail: the sequence's last 8-token group (first token gstart) is read from an LDS image
@@ -822,11 +858,13 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
     }
   } else if constexpr (FUSED) {
     if constexpr (PRE == 1)
-      fused_qkv_prologue_pre<F8>(p, kvh, writes_kv, q_s, use_img, v_img, *pp);
+      fused_qkv_prologue_pre<F8>(p, kvh, writes_kv, q_s, use_img, v_img, *pp, k_img);
     else
       fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s, use_img ? tsl : -1, v_img);
-    // the chunk holding the token the prologue just wrote is re-read after the barrier
-    if (PREFETCH && writes_kv && t0 < pend && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
+    // the chunk holding the token the prologue just wrote is re-read after the barrier (on
+    // the PRE == 1 tail path the loop patches it from the LDS images instead)
+    if (PREFETCH && writes_kv && !(PRE == 1 && use_img) && t0 < pend && t0 <= kv_len - 1 &&
+        kv_len - 1 < t0 + 32)
       load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS,
                              t0);
   } else if (use_img) {  // uniform per workgroup
@@ -877,7 +915,10 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
                                kvh, p.Hkv, p.BS, has ? tc : 0);
       };
       auto consume = [&](ChunkT<F8>& c, int tc) {
-        if (use_img && tc <= gstart && gstart < tc + 32) patch_v(c, tc, gstart, v_img);
+        if (use_img && tc <= gstart && gstart < tc + 32) {
+          patch_v(c, tc, gstart, v_img);
+          if constexpr (FUSED && PRE == 1) patch_k(c, tc, kv_len - 1, k_img);
+        }
         if (tc + 31 < kv_len)
           compute_chunk<false>(st, qb, c, tc, limit, p.scale_log2);
         else
@@ -1454,7 +1495,8 @@ void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) 
   if (num_seqs == 0) return;
   const size_t smem = (size_t)(4 * p.G * (kD + 4) + 8 * p.G) * sizeof(float) +
                       (p.qkv ? (size_t)p.G * kD * sizeof(bf16) : 0) +
-                      (p.v_tail ? (size_t)kD * 8 * sizeof(bf16) : 0);
+                      (p.v_tail ? (size_t)kD * 8 * sizeof(bf16) : 0) +
+                      (p.qkv && p.v_tail ? (size_t)kD * sizeof(bf16) : 0);
   const int per_cu = (p.flags >> 3) & 7;  // flags bits 3..5: persistent, WGs per CU
   if (p.kv_fp8) {  // fp8 KV cache: prefetching + non-temporal variants only
     const dim3 grid(num_seqs, p.Hkv, p.num_parts);

@@ -72,8 +72,27 @@ def main():
         ops.paged_attention_decode(out, qbuf, kc, vc, bt, lens_d, G, scale, workspace=ws,
                                    num_parts=1, part_size=4096)
 
-    variants = {"plain attention (q ready)": plain, "fused prologue attention": fused,
-                "qk_norm_rope_cache + plain": split}
+    slots_none = torch.full_like(slots_d, -1)
+    vtail = torch.zeros(B, Hkv, 8, D, dtype=torch.bfloat16, device=dev)
+    tslot = torch.arange(B, dtype=torch.int32, device=dev)
+
+    def fused_nowrite():  # the prologue without the new token's K/V writes (slot -1)
+        ops.paged_attention_decode_fused(out, qkv, kc, vc, bt, lens_d, pos_d, slots_none,
+                                         cos_sin, qw, kw, G, scale, 1e-6, workspace=ws,
+                                         num_parts=1, part_size=4096)
+
+    def fused_tail():  # the serving form: V written through the per-sequence V tail
+        ops.paged_attention_decode_fused(out, qkv, kc, vc, bt, lens_d, pos_d, slots_d, cos_sin,
+                                         qw, kw, G, scale, 1e-6, workspace=ws, num_parts=1,
+                                         part_size=4096, v_tail=vtail, tail_slot=tslot)
+
+    def plain_tail():  # ready q, partial last V group read from the tail (no writes)
+        ops.paged_attention_decode(out, q, kc, vc, bt, lens_d, G, scale, workspace=ws,
+                                   num_parts=1, part_size=4096, v_tail=vtail, tail_slot=tslot)
+
+    variants = {"plain attention (q ready)": plain, "plain + V tail reads": plain_tail,
+                "fused prologue attention": fused, "fused, no K/V write": fused_nowrite,
+                "fused + V tail (serving)": fused_tail, "qk_norm_rope_cache + plain": split}
     graphs = {}
     for k, f in variants.items():
         s = torch.cuda.Stream()
