@@ -183,3 +183,17 @@ def test_max_model_len_beyond_the_rotary_table_is_rejected():
     rotary table, which the kernels index by position, ends there)."""
     with pytest.raises(ValueError, match="max_position_embeddings"):
         _engine("tiny-qwen3", max_model_len=8192)
+
+
+def test_decode_partitions_capped_at_the_kernel_limit():
+    """The split-KV plan never hands the decode kernel a partition longer than
+    ops.DECODE_MAX_PART (it keeps one cache block id per 128-token wave step in a VGPR lane),
+    at any batch size, however long max_model_len is."""
+    from aws_k8s_ansible_provisioner_amd import ops
+
+    eng = _engine("tiny-qwen3", max_model_len=4096)
+    eng.ecfg.max_model_len = 40000  # the plan only reads the configured maximum
+    for n in (1, 7, 64, 256, 1024):
+        parts, ps = eng.runner.decode_partitions(n)
+        assert ps % 128 == 0 and ps <= ops.DECODE_MAX_PART, (n, parts, ps)
+        assert parts * ps >= 40000, (n, parts, ps)
