@@ -439,25 +439,31 @@ __device__ __forceinline__ void prologue_loads(const AttnParams& p, int seq, int
   // Branch-free: every lane loads from a valid address (lanes past the G + 2 rows re-read row
   // G + 1's bytes; a missing norm weight / tail reads the qkv row instead), so the vmcnt
   // counts stay exact -- an exec-masked branch here made hipcc wait vmcnt(0) at the merge.
+  // Lanes that do not need an operand load it from one shared address (the qkv row's first
+  // 16 B: one cache line per wave instruction) instead of a private one, so the branch-free
+  // form costs no extra L1/L2 traffic: only the V-row lanes read the tail rows, only the q/k
+  // lanes the cos/sin row and the norm weight.
   const int G = p.G;
-  const int rr = min((int)(threadIdx.x >> 4), G + 1);
+  const int rr0 = threadIdx.x >> 4;
+  const int rr = min(rr0, G + 1);
   const int j = threadIdx.x & 15;
+  const bool row_lane = rr0 < G + 2, qk_lane = rr0 <= G, v_lane = rr0 == G + 1;
   const int head = rr < G ? kvh * G + rr : (rr == G ? p.Hq + kvh : p.Hq + p.Hkv + kvh);
   const bf16* row = p.qkv + (size_t)seq * p.qkv_stride;
-  pp.raw = *reinterpret_cast<const bf16x8*>(row + head * kD + 8 * j);
+  pp.raw = *reinterpret_cast<const bf16x8*>(row_lane ? row + head * kD + 8 * j : row);
   const bf16* nw = rr < G ? p.q_w : p.k_w;
-  pp.w8 = *reinterpret_cast<const bf16x8*>((nw != nullptr ? nw : row) + 8 * j);
+  pp.w8 = *reinterpret_cast<const bf16x8*>(qk_lane && nw != nullptr ? nw + 8 * j : row);
   const float* cs = p.cos_sin + (size_t)pos * kD;
-  const int i0 = 8 * (j & 7);
+  const int i0 = qk_lane ? 8 * (j & 7) : 0;
   pp.c0 = *reinterpret_cast<const f32x4*>(cs + i0);
-  pp.c1 = *reinterpret_cast<const f32x4*>(cs + i0 + 4);
-  pp.s0 = *reinterpret_cast<const f32x4*>(cs + 64 + i0);
-  pp.s1 = *reinterpret_cast<const f32x4*>(cs + 64 + i0 + 4);
-  const bf16* tb = (!F8 && p.v_tail != nullptr)
-                       ? p.v_tail + ((size_t)max(pp.tsl, 0) * p.Hkv + kvh) * 8 * kD + 8 * j
-                       : row + 8 * j;
+  pp.c1 = *reinterpret_cast<const f32x4*>(cs + (qk_lane ? i0 + 4 : 0));
+  pp.s0 = *reinterpret_cast<const f32x4*>(cs + (qk_lane ? 64 + i0 : 0));
+  pp.s1 = *reinterpret_cast<const f32x4*>(cs + (qk_lane ? 64 + i0 + 4 : 0));
+  const bool tl = !F8 && p.v_tail != nullptr && v_lane;
+  const bf16* tb = tl ? p.v_tail + ((size_t)max(pp.tsl, 0) * p.Hkv + kvh) * 8 * kD + 8 * j : row;
+  const int ts = tl ? kD : 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) pp.trow[i] = *reinterpret_cast<const bf16x8*>(tb + (size_t)i * kD);
+  for (int i = 0; i < 8; ++i) pp.trow[i] = *reinterpret_cast<const bf16x8*>(tb + (size_t)i * ts);
 }
 
 // fused_qkv_prologue on preloaded operands (same arithmetic, same stores)
