@@ -16,7 +16,12 @@
 //    softmax rescale is lane-local.
 //  * K operand: K cache [blk, Hkv, BS, D]; each lane loads 16 B per MFMA k-chunk.
 //  * Decode: grid (seq, kv_head, partition); 4 waves split a partition's 32-token
-//    chunks and combine through LDS; partitions are combined by a reduce kernel.
+//    chunks and combine through LDS; partitions are combined by a reduce kernel.  A wave's
+//    cache block ids sit in one VGPR (read by readlane), its K/V chunks alternate between
+//    two named register sets with every load unconditional (exact vmcnt counts), and in the
+//    serving form the new token's K/V reach the chunk registers from LDS images, so no wave
+//    waits on the prologue's cache stores (profiles/r3_attn_rework_ab.log,
+//    r3_attn_fused_breakdown.log).
 //  * Prefill: grid (q-tile, kv_head); each wave walks the causal range of its rows.
 #include "common.h"
 #include "kernels.h"
