@@ -63,6 +63,24 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
                                    0);
 }
+// the same with the non-temporal policy: once-read decode weights (MI355X_MICROARCH.md
+// nt-weights), never for the activation rows every column tile re-reads
+__device__ __forceinline__ void glds16_nt(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
+                                   2);
+}
+
+// AKAP_WEIGHT_NT: unset -> -1 (gdgemm weights non-temporal, kgemm default policy: measured
+// Llama-3-8B +0.7 % on both A/B pairs, Qwen3-0.6B -0.65 % with kgemm nt too,
+// profiles/r3_weight_nt_ab.log); 1 -> both non-temporal; 0 -> neither
+int weight_nt_default() {
+  static const int v = [] {
+    const char* e = std::getenv("AKAP_WEIGHT_NT");
+    return e == nullptr ? -1 : (std::atoi(e) == 1 ? 1 : 0);
+  }();
+  return v;
+}
 
 template <int N_>
 __device__ __forceinline__ void wait_vm() {
@@ -145,8 +163,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
     const int k0 = kbeg + step * BKT;
 #pragma unroll
     for (int i = 0; i < GA; ++i) glds16(asrc[i] + k0, slot + (w * GA + i) * 64);
+    if (p.ntw != 0) {
 #pragma unroll
-    for (int i = 0; i < GW; ++i) glds16(wsrc[i] + k0, slot + GBM * CPR + (w * GW + i) * 64);
+      for (int i = 0; i < GW; ++i) glds16_nt(wsrc[i] + k0, slot + GBM * CPR + (w * GW + i) * 64);
+    } else {
+#pragma unroll
+      for (int i = 0; i < GW; ++i) glds16(wsrc[i] + k0, slot + GBM * CPR + (w * GW + i) * 64);
+    }
   };
 
   // epilogue operands from the previous launch: load before the loop (hidden under it)

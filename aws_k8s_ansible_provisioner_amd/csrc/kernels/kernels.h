@@ -108,7 +108,10 @@ struct DGemmArgs {
   int ns;  // gdgemm ring depth: 0 = shallow (2 blocks/CU), >= 6 = deep ring (1 block/CU)
   int* counters;  // gdgemm split-K: zeroed per-tile tickets -> in-launch last-arriver combine
   int bm;         // gdgemm tile rows: 64 (default) | 128 (with bn = 128)
+  int ntw;        // weight DMA policy: -1 default (gdgemm nt, kgemm not), 1 both nt, 0 neither
 };
+// process default for DGemmArgs::ntw (AKAP_WEIGHT_NT, read once)
+int weight_nt_default();
 bool dgemm_supported(int M, int N, int K, int splitk, int pf);
 // split-K factors with a compiled reduce (1, 2, 4, 8, 16)
 bool dgemm_splitk_ok(int splitk);

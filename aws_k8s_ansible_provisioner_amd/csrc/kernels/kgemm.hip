@@ -37,6 +37,11 @@ __device__ __forceinline__ void kglds16(const void* g, void* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
                                    0);
 }
+__device__ __forceinline__ void kglds16_nt(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
+                                   2);
+}
 
 template <int N_>
 __device__ __forceinline__ void kwait_vm() {
@@ -88,7 +93,12 @@ __global__ __launch_bounds__(256, 1) void kgemm_kernel(DGemmArgs p) {
     bf16x8* slot = lds + (st % KNS) * SU;
     const int k0 = st * KST;
 #pragma unroll
-    for (int i = 0; i < G; ++i) kglds16(src[i] + k0, slot + (w * G + i) * 64);
+    for (int i = 0; i < G; ++i) {
+      // instruction (w, i) stages rows 2 (w G + i) and + 1: X rows below BM, weight rows above
+      // (wave-uniform), the weights non-temporal only when asked for (p.ntw == 1)
+      if (p.ntw == 1 && (w * G + i) * 2 >= BM) kglds16_nt(src[i] + k0, slot + (w * G + i) * 64);
+      else kglds16(src[i] + k0, slot + (w * G + i) * 64);
+    }
   };
 
   // epilogue operands of the previous launch, loaded under the K loop
