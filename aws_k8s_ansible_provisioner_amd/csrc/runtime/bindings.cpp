@@ -56,8 +56,14 @@ static py::dict step_info(const StepInfo& i) {
   return d;
 }
 
+#ifndef AKAP_RT_HASH
+#define AKAP_RT_HASH "unknown"
+#endif
+
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "MI355X serving engine host runtime: paged KV block manager + batch scheduler";
+  // digest of the runtime sources this module was compiled from (build_ext.runtime_tree_hash)
+  m.def("build_hash", [] { return std::string(AKAP_RT_HASH); });
 
   py::class_<BlockManager>(m, "BlockManager")
       .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"),

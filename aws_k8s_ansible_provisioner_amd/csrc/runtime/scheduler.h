@@ -222,8 +222,8 @@ class Scheduler {
   std::vector<int32_t> free_tails_;  // V-tail slot pool (LIFO)
   int64_t preemptions_ = 0;
   int64_t held_expired_ = 0;
-  int prefill_only_run_ = 0;
-  int last_appended_ = 0;  // consecutive prefill-only steps while decodes were waiting
+  int prefill_only_run_ = 0;  // consecutive prefill-only steps while decodes were waiting
+  int last_appended_ = 0;     // tokens appended to live sequences by the last update()
 };
 
 }  // namespace akap_rt

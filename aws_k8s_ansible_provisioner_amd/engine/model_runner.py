@@ -525,6 +525,19 @@ class ModelRunner:
         else:
             self._decode_body(n)
 
+    def _bucket(self, B: int) -> int:
+        for b in self.buckets:
+            if b >= B:
+                return b
+        return B
+
+    def execute_decode_eager(self, info: dict) -> None:
+        """TP follower ranks, for a decode step rank 0 runs eagerly (its extras: penalties /
+        log-probs): the same padded batch through _decode_body, so this rank issues exactly
+        the collectives rank 0 does (inputs by the in-step broadcast of rank 0's staging
+        region; an expert-parallel step takes the exact-split dispatch on every rank)."""
+        self._decode_body(self._bucket(info["num_seqs"]))
+
     @staticmethod
     def wait_decode(handle) -> np.ndarray:
         ev, host = handle

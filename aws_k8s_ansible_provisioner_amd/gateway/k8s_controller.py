@@ -78,9 +78,16 @@ class GatewayController:
         return h
 
     def _ssl(self):
+        """TLS context for the API server.  Fails closed: a bearer token is never sent over a
+        connection whose certificate is not verified (no service-account ca.crt -> the system
+        trust store, never verification off)."""
         if not self.api.startswith("https"):
+            host = self.api.split("://", 1)[-1].split("/", 1)[0].rsplit(":", 1)[0]
+            if self.token and host not in ("127.0.0.1", "localhost", "[::1]"):
+                # plain HTTP only to a loopback endpoint (kubectl proxy, tests)
+                raise RuntimeError("refusing to send the service-account token over plain HTTP")
             return None
-        return ssl.create_default_context(cafile=self.ca_file) if self.ca_file else False
+        return ssl.create_default_context(cafile=self.ca_file)
 
     async def _get(self, s: aiohttp.ClientSession, path: str) -> Optional[dict]:
         async with s.get(self.api + path, headers=self._headers(), ssl=self._ssl()) as r:

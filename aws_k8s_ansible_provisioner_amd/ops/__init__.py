@@ -33,14 +33,38 @@ def load_native(required: bool = False) -> bool:
     if not os.path.exists(_LIB):
         _load_error = f"{_LIB} not built (run python -m aws_k8s_ansible_provisioner_amd.build_ext)"
     else:
-        try:
-            torch.ops.load_library(_LIB)
-            _loaded = True
-        except Exception as e:  # pragma: no cover - depends on the box
-            _load_error = repr(e)
+        stale = native_provenance()
+        if stale.get("mismatch") and os.environ.get("AKAP_ALLOW_STALE_NATIVE") != "1":
+            _load_error = (f"{_LIB} was built from other sources (library tree "
+                           f"{stale['library'][:16]}, sources here {stale['sources'][:16]}): "
+                           f"rebuild with python -m aws_k8s_ansible_provisioner_amd.build_ext")
+        else:
+            try:
+                torch.ops.load_library(_LIB)
+                _loaded = True
+            except Exception as e:  # pragma: no cover - depends on the box
+                _load_error = repr(e)
     if required and not _loaded:
         raise RuntimeError("native HIP kernels unavailable: " + str(_load_error))
     return _loaded
+
+
+def native_provenance() -> dict:
+    """The source-tree digest compiled into _C.so vs the digest of the sources beside it
+    (build_ext.kernel_tree_hash): proves which sources the loaded library was built from."""
+    import ctypes
+
+    from .. import build_ext
+
+    lib = ctypes.CDLL(_LIB, mode=getattr(os, "RTLD_LAZY", 1) | ctypes.RTLD_GLOBAL)
+    try:
+        f = lib.akap_build_hash
+    except AttributeError:
+        return {"library": "none", "sources": "?", "mismatch": True}
+    f.restype = ctypes.c_char_p
+    have = f().decode()
+    want = build_ext.kernel_tree_hash() if os.path.exists(build_ext.CSRC) else have
+    return {"library": have, "sources": want, "mismatch": have != want}
 
 
 def native_available() -> bool:

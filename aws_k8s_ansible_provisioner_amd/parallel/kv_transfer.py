@@ -271,6 +271,12 @@ class KVTransferAgent:
         jobs).  Runs on the agent thread, after any queued transfer (which fails fast while
         broken).  Returns True if this call moved the channel to `generation`."""
 
+        if dist.get_world_size() != 2:
+            # new_group() completes only when EVERY rank of the default group calls it with
+            # this generation; only the 2-rank P/D pod guarantees that (both ends reset)
+            raise RuntimeError(f"KV channel reset needs a 2-rank P/D job, world size is "
+                               f"{dist.get_world_size()}")
+
         def fn():
             if generation <= self.generation:
                 return False

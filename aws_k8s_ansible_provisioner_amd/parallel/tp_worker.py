@@ -30,9 +30,16 @@ from .state import ParallelState, init_distributed
 
 _INFO_KEYS = ["is_prefill", "num_seqs", "num_tokens", "num_tiles", "num_samples",
               "max_seq_len", "num_preempted", "num_decode"]
-# header = info + launch mode
+# header = info + eager bit + launch mode.  eager = 1: a decode step rank 0 runs eagerly (a
+# request asked for penalties / log-probs) -- every rank then runs that step eagerly too, so
+# the group issues one and the same collective sequence (an eager expert-parallel step takes
+# the exact-split dispatch, a replayed graph the fixed-capacity one: they must never mix)
 EXECUTE, LAUNCH, CHAINED = 0, 1, 2
 STOP = -1
+
+
+def _is_eager_decode(info: dict) -> int:
+    return int(not info["is_prefill"] and bool(info.get("extras")))
 
 
 class TPStepBroadcaster:
@@ -46,7 +53,8 @@ class TPStepBroadcaster:
         return getattr(self.runner, name)
 
     def _header(self, info: dict, mode: int) -> None:
-        head = torch.tensor([info[k] for k in _INFO_KEYS] + [mode], dtype=torch.int64)
+        head = torch.tensor([info[k] for k in _INFO_KEYS] + [_is_eager_decode(info), mode],
+                            dtype=torch.int64)
         dist.broadcast(head, 0, group=self.ctrl)
 
     def execute(self, info: dict) -> np.ndarray:
@@ -58,7 +66,7 @@ class TPStepBroadcaster:
         return self.runner.launch_decode(info, chained=chained)
 
     def shutdown(self) -> None:
-        head = torch.full((len(_INFO_KEYS) + 1,), STOP, dtype=torch.int64)
+        head = torch.full((len(_INFO_KEYS) + 2,), STOP, dtype=torch.int64)
         dist.broadcast(head, 0, group=self.ctrl)
         dist.barrier(group=self.ctrl)
         dist.destroy_process_group()
@@ -69,13 +77,15 @@ def worker_loop(runner: ModelRunner, ctrl_group) -> None:
     without a host wait (their tokens are rank 0's business) unless an expert-parallel
     dispatch may need the step re-run (runner.execute checks the overflow flag)."""
     while True:
-        head = torch.zeros(len(_INFO_KEYS) + 1, dtype=torch.int64)
+        head = torch.zeros(len(_INFO_KEYS) + 2, dtype=torch.int64)
         dist.broadcast(head, 0, group=ctrl_group)
         if int(head[0]) == STOP:
             return
         vals = head.tolist()
         info = {k: int(v) for k, v in zip(_INFO_KEYS, vals)}
-        if not info["is_prefill"] and not runner._ep_moe:
+        if vals[len(_INFO_KEYS)]:
+            runner.execute_decode_eager(info)
+        elif not info["is_prefill"] and not runner._ep_moe:
             runner.replay_decode(info)
         else:
             runner.execute(info)

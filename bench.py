@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import statistics
 import sys
 import time
@@ -78,6 +79,11 @@ def parse():
     return ap.parse_args()
 
 
+def physical_devices(devs: list) -> int:
+    """Distinct GPUs among the ranks' (host, device) ids (None = a CPU rank)."""
+    return len({d for d in devs if d is not None})
+
+
 def main() -> int:
     a = parse()
     import torch
@@ -105,6 +111,14 @@ def main() -> int:
         backend = a.dist_backend or ("nccl" if gpu else "gloo")
         kw = {"device_id": torch.device("cuda", local)} if (gpu and backend == "nccl") else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    # physical devices behind the ranks: (host, device index) of every rank, de-duplicated --
+    # a single-GPU rehearsal of a multi-rank layout (ranks sharing one device) is 1 GPU
+    dev_id = (socket.gethostname(), local) if gpu else None
+    devs = [dev_id]
+    if world > 1:
+        devs = [None] * world
+        dist.all_gather_object(devs, dev_id)
+    n_dev = physical_devices(devs)
     pd = a.mode == "pd"
     if pd and (world < 2 or world % 2):
         print("error: --mode pd needs an even WORLD_SIZE >= 2", file=sys.stderr)
@@ -256,7 +270,8 @@ def main() -> int:
             "metric": "output tok/s + p50 TTFT",
             "value": round(tok / el, 2),
             "unit": "output tok/s",
-            "n_gpus": world if world > 1 else a.gpus,
+            "n_gpus": n_dev,
+            "ranks": max(world, 1),
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1000, 3),

@@ -45,7 +45,8 @@ def _run(args, nproc=1, env=None):
 
 def test_bench_mono_single_process():
     res = _run(["--model", "tiny-qwen3"] + SMALL)
-    assert res["n_gpus"] == 1 and res["config"]["parallelism"] == "dp1"
+    # n_gpus counts physical devices (none on this CPU run); ranks counts processes
+    assert res["n_gpus"] == 0 and res["ranks"] == 1 and res["config"]["parallelism"] == "dp1"
     assert res["scaling"] == "weak"
 
 
@@ -54,7 +55,7 @@ def test_bench_data_parallel_two_ranks():
     whole-job aggregate over all ranks."""
     one = _run(["--model", "tiny-qwen3"] + SMALL)
     res = _run(["--model", "tiny-qwen3"] + SMALL, nproc=2)
-    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert res["ranks"] == 2 and res["n_gpus"] == 0 and res["config"]["parallelism"] == "dp2"
     assert res["scaling"] == "weak" and res["config"]["global_batch"] == 2 * one["config"]["global_batch"]
 
 
@@ -66,5 +67,17 @@ def test_bench_tensor_parallel(model, env):
 
 def test_bench_pd_disaggregated():
     res = _run(["--mode", "pd", "--model", "tiny-qwen3"] + SMALL, nproc=2)
-    assert res["config"]["parallelism"] == "pd1x1"
+    assert res["config"]["parallelism"] == "pd1x1" and res["ranks"] == 2
     assert res["p50_ttft_ms"] > 0
+
+
+def test_bench_counts_physical_devices_not_ranks():
+    """a 2-rank rehearsal on ONE GPU is n_gpus 1 (ranks 2); ranks on two
+    devices, or on the same index of two hosts, are 2."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench.physical_devices([("h", 0), ("h", 0)]) == 1
+    assert bench.physical_devices([("h", 0), ("h", 1)]) == 2
+    assert bench.physical_devices([("a", 0), ("b", 0)]) == 2
+    assert bench.physical_devices([None, None]) == 0

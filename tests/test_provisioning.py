@@ -531,6 +531,17 @@ def test_gateway_api_objects_when_crds_present():
     assert ("HTTPRoute", "llm-d-inference-gateway") in kinds
     # our own controller implements class akap: the class, its RBAC, the gateway's SA
     assert ("GatewayClass", "akap") in kinds and ("ClusterRole", "akap-gateway-controller") in kinds
+    # least privilege: cluster scope only for GatewayClass; the namespaced objects
+    # the controller reads / patches through a Role in the release namespace
+    docs = {(d["kind"], d["metadata"]["name"]): d for d in yaml.safe_load_all(on) if d}
+    cr = docs[("ClusterRole", "akap-gateway-controller")]
+    assert {r for rule in cr["rules"] for r in rule["resources"]} == {
+        "gatewayclasses", "gatewayclasses/status"}
+    role = docs[("Role", "akap-gateway-controller")]
+    assert role["metadata"]["namespace"] == "llm-d"
+    assert {"gateways/status", "httproutes/status", "services"} <= {
+        r for rule in role["rules"] for r in rule["resources"]}
+    assert docs[("RoleBinding", "akap-gateway-controller")]["roleRef"]["kind"] == "Role"
     dep = [d for d in yaml.safe_load_all(on) if d and d["kind"] == "Deployment"][0]
     assert dep["spec"]["template"]["spec"]["serviceAccountName"] == "llm-d-inference-gateway"
     assert "auto" in dep["spec"]["template"]["spec"]["containers"][0]["args"]
@@ -654,3 +665,44 @@ def test_inprocess_kernel_profiler_windows_and_health():
     assert calls == [0.5, 0.5, 0.5]
     # the real window function on a CPU-only host: no GPU, an empty window
     assert torch_window(0.01) == {}
+
+
+def test_image_pins_the_tested_torch():
+    """the deploy image must ship the stack that was tested.  The
+    Dockerfile's TORCH_VERSION is the torch this tree's _C.so compiles and links against
+    (build_ext.torch_version) -- the version every test and bench ran on."""
+    import re
+
+    from aws_k8s_ansible_provisioner_amd import build_ext
+
+    text = open(os.path.join(ROOT, "Dockerfile")).read()
+    m = re.search(r"^ARG TORCH_VERSION=(\S+)$", text, re.M)
+    assert m, "Dockerfile must pin ARG TORCH_VERSION"
+    assert m.group(1) == build_ext.torch_version(), (m.group(1), build_ext.torch_version())
+    # the image build itself re-checks the installed torch against the pin
+    assert "torch==${TORCH_VERSION}" in text and "!= pinned" in text
+
+
+def test_build_is_content_addressed(tmp_path):
+    """objects are rebuilt on a change of the DIGEST of their inputs
+    (not mtimes); the tree digest is compiled into the libraries and checked at load."""
+    from aws_k8s_ansible_provisioner_amd import build_ext
+
+    src = tmp_path / "a.hip"
+    src.write_text("x")
+    obj = str(tmp_path / "a.o")
+    d1 = build_ext._digest([str(src)], "cmd")
+    assert build_ext._stale(obj, d1) == "no object"
+    open(obj, "w").write("o")
+    open(obj + ".sha", "w").write(d1 + "\n")
+    assert build_ext._stale(obj, d1) == ""
+    # touching the source (newer mtime, same bytes) does not rebuild; new bytes do
+    os.utime(src, None)
+    assert build_ext._stale(obj, build_ext._digest([str(src)], "cmd")) == ""
+    src.write_text("y")
+    assert build_ext._stale(obj, build_ext._digest([str(src)], "cmd")) == "inputs changed"
+    # a different compile command is a different digest too
+    assert build_ext._digest([str(src)], "cmd -O2") != build_ext._digest([str(src)], "cmd")
+    # the kernel tree digest covers every .hip / .h and ops.cpp
+    names = {os.path.basename(p) for p in build_ext.kernel_sources()}
+    assert {"ops.cpp", "common.h", "attention.hip"} <= names

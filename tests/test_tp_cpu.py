@@ -166,6 +166,12 @@ def test_tp_step_is_one_host_broadcast(monkeypatch):
            "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3}
     assert bc.execute(dec) == "ran"
     assert len(sent) == 1 and sent[0].tolist()[-1] == tp_worker.EXECUTE
+    assert sent[0].tolist()[-2] == 0  # graph-replayable decode step
+    sent.clear()
+    # a decode step with extras (log-probs / penalties) runs eagerly on rank 0: the header's
+    # eager bit makes every follower run it eagerly as well
+    bc.execute(dict(dec, extras={"logprobs": True}))
+    assert len(sent) == 1 and sent[0].tolist()[-2] == 1
     sent.clear()
     pre = dict(dec, is_prefill=1, num_tokens=20, num_tiles=2, num_decode=0)
     bc.execute(pre)
@@ -173,6 +179,88 @@ def test_tp_step_is_one_host_broadcast(monkeypatch):
     sent.clear()
     assert bc.launch_decode(dec, chained=True) == ("launched", True)
     assert len(sent) == 1 and sent[0].tolist()[-1] == tp_worker.CHAINED
+
+
+def test_tp_follower_mirrors_eager_decode(monkeypatch):
+    """under TP x EP a decode step rank 0 runs eagerly must not meet a
+    follower's graph replay (eager EP = exact-split all_to_alls, graph = fixed-capacity ones:
+    the collective sequences differ).  The follower loop routes eager-bit headers to
+    ModelRunner.execute_decode_eager and everything else as before."""
+    import torch
+    import torch.distributed as dist
+
+    from aws_k8s_ansible_provisioner_amd.parallel import tp_worker
+
+    dec = {"is_prefill": 0, "num_seqs": 3, "num_tokens": 3, "num_tiles": 0,
+           "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3}
+    heads = [[dec[k] for k in tp_worker._INFO_KEYS] + [1, tp_worker.EXECUTE],
+             [dec[k] for k in tp_worker._INFO_KEYS] + [0, tp_worker.EXECUTE],
+             [tp_worker.STOP] * (len(tp_worker._INFO_KEYS) + 2)]
+
+    def fake_bcast(t, src, group=None):
+        t.copy_(torch.tensor(heads.pop(0), dtype=torch.int64))
+
+    monkeypatch.setattr(dist, "broadcast", fake_bcast)
+    calls = []
+
+    class Follower:
+        _ep_moe = True
+
+        def execute_decode_eager(self, info):
+            calls.append(("eager", info["num_seqs"]))
+
+        def execute(self, info):
+            calls.append(("execute", info["num_seqs"]))
+
+        def replay_decode(self, info):
+            calls.append(("replay", info["num_seqs"]))
+
+    tp_worker.worker_loop(Follower(), ctrl_group=None)
+    assert calls == [("eager", 3), ("execute", 3)]
+
+
+EP_EXTRAS_CHILD = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["ROOT"])
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
+ecfg = EngineConfig(model="tiny-mixtral", device="cpu", max_model_len=256, max_num_seqs=8,
+                    max_num_batched_tokens=32, block_size=32, num_gpu_blocks=96,
+                    tensor_parallel_size=2, shard_init="full", init_std=0.15)
+eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
+if eng is not None:
+    ps = [SamplingParams(max_tokens=6, temperature=0, ignore_eos=True, logprobs=1),
+          SamplingParams(max_tokens=6, temperature=0, ignore_eos=True,
+                         repetition_penalty=1.0, presence_penalty=0.5)]
+    names = [eng.add_request(None, None, p, prompt_ids=q)
+             for q, p in zip([list(range(5, 30)), [7, 8, 9]], ps)]
+    final = {}
+    while eng.has_unfinished():
+        for o in eng.step():
+            if o.finished:
+                final[o.req_id] = o.output_ids
+    bc.shutdown()
+    print("RESULT " + json.dumps([final[n] for n in names]), flush=True)
+"""
+
+
+def test_tp_ep_decode_with_logprobs_and_penalties():
+    """TP x EP (tiny-Mixtral, 2 ranks, exact-split eager dispatch) with a log-probs request and
+    a penalty request in the batch: every step carries extras, the followers mirror the eager
+    steps and the group finishes (no collective mismatch / hang)."""
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROOT=ROOT,
+                   AKAP_MOE_MODE="ep", AKAP_EP_FIXED_MAX_T="0", OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", EP_EXTRAS_CHILD], env=env, cwd=ROOT,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
+    line = [l for l in outs[0][0].splitlines() if l.startswith("RESULT ")][0]
+    res = json.loads(line[7:])
+    assert [len(r) for r in res] == [6, 6]
 
 
 LOOKAHEAD_CHILD = r"""
