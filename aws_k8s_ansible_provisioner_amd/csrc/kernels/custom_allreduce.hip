@@ -38,6 +38,17 @@
 //            peer, i.e. after every peer finished launch e (stream order), so no peer can
 //            still be reading epoch e's bytes.
 // Every spin-wait is bounded: on timeout the kernel records an error flag and exits.
+//
+// Siblings on the same buffers, flags and per-block epochs (so a TP decode hipGraph holds
+// only these kernels -- no RCCL call -- and replays across processes that share one GPU as
+// well as across the xGMI mesh):
+//   all-gather  every rank stages its [R, n] shard (sc0 sc1 stores), one flag exchange, then
+//               reads every peer's shard (sc0 sc1 loads) into out[R, W*n] (rank-major column
+//               blocks: the vocab-parallel logits);
+//   broadcast   the root stages the bytes, one flag exchange, the other ranks read them (the
+//               TP decode step's input staging region).
+// Both keep the block -> element-chunk map a pure function of the size, identical on every
+// rank, so the epoch / parity reuse argument above holds for any mix of launches.
 #include "common.h"
 #include "kernels.h"
 
@@ -262,6 +273,64 @@ __global__ __launch_bounds__(256) void car_multi_kernel(CarMulti m, long n8, int
                      n8, m.epi[r], m.warm != 0);
 }
 
+// All-gather: rank r's shard in[R, n] -> out[R, W*n] columns [r*n, (r+1)*n); n % 8 == 0.
+__device__ __forceinline__ void car_allgather(const CarArgs& a, int bid, int nblk,
+                                              const bf16* __restrict__ in,
+                                              bf16* __restrict__ out, long n8, int n) {
+  const uint32_t ep = car_epoch(a, bid);
+  const size_t par = (ep & 1) * a.half_elems;
+  const __amdgpu_buffer_rsrc_t mine = car_rsrc(a.bufs[a.rank], a);
+  const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
+  const long stride = (long)nblk * 256;
+  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride)
+    car_st(mine, par + (size_t)i * 8, src[i]);
+  car_barrier(a, bid, ep, 0);
+  const long W = a.world;
+  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride) {
+    bf16x8 v[kCarMaxRanks];
+#pragma unroll
+    for (int p = 0; p < kCarMaxRanks; ++p)  // every peer load in flight before the stores
+      if (p < a.world && p != a.rank) v[p] = car_ld(car_rsrc(a.bufs[p], a), par + (size_t)i * 8);
+    const long e = i * 8, row = e / n, col = e % n;
+    bf16* o = out + row * W * n + col;
+#pragma unroll
+    for (int p = 0; p < kCarMaxRanks; ++p) {
+      if (p >= a.world) break;
+      *reinterpret_cast<bf16x8*>(o + (long)p * n) = p == a.rank ? src[i] : v[p];
+    }
+  }
+}
+
+// Broadcast of n8 16-byte vectors of `buf` from rank `root` to every rank (in place).
+__device__ __forceinline__ void car_bcast(const CarArgs& a, int bid, int nblk, bf16* buf,
+                                          long n8, int root) {
+  const uint32_t ep = car_epoch(a, bid);
+  const size_t par = (ep & 1) * a.half_elems;
+  const long stride = (long)nblk * 256;
+  bf16x8* b8 = reinterpret_cast<bf16x8*>(buf);
+  if (a.rank == root) {
+    const __amdgpu_buffer_rsrc_t mine = car_rsrc(a.bufs[a.rank], a);
+    for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride)
+      car_st(mine, par + (size_t)i * 8, b8[i]);
+  }
+  car_barrier(a, bid, ep, 0);
+  if (a.rank != root) {
+    const __amdgpu_buffer_rsrc_t rr = car_rsrc(a.bufs[root], a);
+    for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride)
+      b8[i] = car_ld(rr, par + (size_t)i * 8);
+  }
+}
+
+__global__ __launch_bounds__(256) void car_allgather_kernel(CarArgs a, const bf16* __restrict__ in,
+                                                            bf16* __restrict__ out, long n8,
+                                                            int n) {
+  car_allgather(a, blockIdx.x, gridDim.x, in, out, n8, n);
+}
+
+__global__ __launch_bounds__(256) void car_bcast_kernel(CarArgs a, bf16* buf, long n8, int root) {
+  car_bcast(a, blockIdx.x, gridDim.x, buf, n8, root);
+}
+
 // Block count for n8 vectors: the same on every rank (a pure function of n8 and world).
 static int car_blocks(long n8, int world, bool two) {
   const long per = two ? (n8 + world - 1) / world : n8;
@@ -283,6 +352,20 @@ void launch_custom_allreduce(const CarArgs& a, const void* in, void* out, long n
     if (epi) car_oneshot_kernel<true><<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8, e);
     else car_oneshot_kernel<false><<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8, e);
   }
+}
+
+void launch_custom_allgather(const CarArgs& a, const void* in, void* out, long rows, int n,
+                             hipStream_t s) {
+  const long n8 = rows * n / 8;
+  if (n8 == 0) return;
+  car_allgather_kernel<<<car_blocks(n8, a.world, false), 256, 0, s>>>(a, (const bf16*)in,
+                                                                    (bf16*)out, n8, n);
+}
+
+void launch_custom_broadcast(const CarArgs& a, void* buf, long bytes, int root, hipStream_t s) {
+  const long n8 = bytes / 16;
+  if (n8 == 0) return;
+  car_bcast_kernel<<<car_blocks(n8, a.world, false), 256, 0, s>>>(a, (bf16*)buf, n8, root);
 }
 
 void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two_shot,

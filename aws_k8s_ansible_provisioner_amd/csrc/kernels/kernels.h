@@ -198,6 +198,21 @@ void launch_kv_gather(const void* cache, long plane_stride, int planes, int bloc
                       const int* block_ids, int nblk, void* out, hipStream_t s);
 void launch_kv_scatter(const void* in, void* cache, long plane_stride, int planes,
                        int block_elems, const int* block_ids, int nblk, hipStream_t s);
+// hipIpc pull: peer cache blocks -> own blocks, + V-tail fill of each request's partial
+// last V group (see kv_transfer.hip)
+struct KVPullArgs {
+  const __bf16* src;      // peer (IPC-mapped) or own cache base: [planes, NB_src, block_elems]
+  long src_plane_stride;  // elements
+  __bf16* dst;            // own cache base [planes, NB, block_elems]
+  long dst_plane_stride;
+  int planes, block_elems;
+  const int* pairs;       // [nblk, 2]: (src block, dst block)
+  int nblk;
+  __bf16* tail;           // [layers, tail_slots, Hkv, 8, D] or nullptr
+  const int* tail_jobs;   // [ntail, 4]: (src block, group, count 1..7, slot)
+  int ntail, layers, tail_slots, Hkv, BS, D;
+};
+void launch_kv_pull(const KVPullArgs& a, hipStream_t s);
 
 // ---- embedding.hip ----
 void launch_embedding(const int64_t* ids, const void* table, void* out, int T, int d,
@@ -226,6 +241,11 @@ struct CarEpi {
 void launch_custom_allreduce(const CarArgs& a, const void* in, void* out, long n, int two_shot,
                              hipStream_t s, const CarEpi* epi = nullptr);
 size_t custom_allreduce_signal_bytes();
+// siblings on the same buffers / flags / epochs: rank-major all-gather of [rows, n] shards
+// into [rows, world * n] (n % 8 == 0), and an in-place broadcast of `bytes` (% 16 == 0)
+void launch_custom_allgather(const CarArgs& a, const void* in, void* out, long rows, int n,
+                             hipStream_t s);
+void launch_custom_broadcast(const CarArgs& a, void* buf, long bytes, int root, hipStream_t s);
 struct CarMulti {  // test-only: every rank of a simulated group in one launch
   CarArgs args[8];
   const void* in[8];

@@ -689,6 +689,49 @@ void kv_scatter(Tensor buf, Tensor cache, Tensor block_ids) {
                           cur_stream());
 }
 
+// hipIpc KV pull (see kv_transfer.hip).  src_ptr: the peer cache base as mapped by ipc_open
+// (or this engine's own cache for a tail-only fill); dst_cache [planes, NB, block_elems].
+// Index ranges are validated by the caller (parallel/kv_transfer.py) before upload: the
+// kernel trusts pairs / tail_jobs.
+void kv_pull(int64_t src_ptr, int64_t src_plane_stride, Tensor dst_cache, Tensor pairs,
+             std::optional<Tensor> tail, std::optional<Tensor> tail_jobs, int64_t Hkv,
+             int64_t BS, int64_t D) {
+  CHECK_GPU(dst_cache); CHECK_CONTIG(dst_cache);
+  TORCH_CHECK(dst_cache.scalar_type() == at::kBFloat16, "cache viewed as bf16");
+  TORCH_CHECK(dst_cache.dim() == 3, "dst cache [planes, NB, block_elems]");
+  TORCH_CHECK(pairs.scalar_type() == at::kInt && pairs.is_cuda() && pairs.is_contiguous(),
+              "pairs int32 [n, 2] on the device");
+  TORCH_CHECK(pairs.numel() % 2 == 0, "pairs [n, 2]");
+  TORCH_CHECK(src_ptr != 0, "null source cache");
+  akap::KVPullArgs a{};
+  a.src = reinterpret_cast<const __bf16*>(src_ptr);
+  a.src_plane_stride = src_plane_stride;
+  a.dst = reinterpret_cast<__bf16*>(dst_cache.data_ptr());
+  a.dst_plane_stride = dst_cache.stride(0);
+  a.planes = dst_cache.size(0);
+  a.block_elems = dst_cache.size(2);
+  TORCH_CHECK(a.block_elems % 8 == 0 && a.block_elems == Hkv * BS * D, "block = Hkv*BS*D");
+  TORCH_CHECK(src_plane_stride % a.block_elems == 0, "source plane stride");
+  a.pairs = pairs.data_ptr<int>();
+  a.nblk = pairs.numel() / 2;
+  a.Hkv = Hkv; a.BS = BS; a.D = D;
+  a.layers = a.planes / 2;
+  if (tail && tail_jobs && tail_jobs->numel()) {
+    CHECK_CONTIG((*tail)); CHECK_BF16((*tail));
+    TORCH_CHECK(tail->dim() == 5 && tail->size(0) == a.layers && tail->size(2) == Hkv &&
+                tail->size(3) == 8 && tail->size(4) == D, "tail [L, slots, Hkv, 8, D]");
+    TORCH_CHECK(tail_jobs->scalar_type() == at::kInt && tail_jobs->is_cuda() &&
+                tail_jobs->is_contiguous() && tail_jobs->numel() % 4 == 0, "tail_jobs [m, 4]");
+    TORCH_CHECK(BS % 8 == 0, "block size % 8");
+    a.tail = reinterpret_cast<__bf16*>(tail->data_ptr());
+    a.tail_slots = tail->size(1);
+    a.tail_jobs = tail_jobs->data_ptr<int>();
+    a.ntail = tail_jobs->numel() / 4;
+  }
+  const c10::DeviceGuard g(dst_cache.device());
+  akap::launch_kv_pull(a, cur_stream());
+}
+
 void embedding(Tensor ids, Tensor table, Tensor out, int64_t vocab_start, int64_t vocab_end) {
   CHECK_GPU(ids); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CONTIG(out);
   TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
@@ -893,6 +936,91 @@ int64_t car_error(int64_t h) {
   return (int64_t)v;
 }
 
+// Rank-major all-gather of the vocab-parallel logits shard inp [R, n] -> out [R, W*n].
+void car_all_gather(int64_t h, Tensor inp, Tensor out) {
+  CarComm* c = car_get(h);
+  CHECK_GPU(inp); CHECK_BF16(inp); CHECK_CONTIG(inp); CHECK_BF16(out); CHECK_CONTIG(out);
+  const int64_t n = inp.size(-1);
+  const int64_t rows = inp.numel() / n;
+  TORCH_CHECK(n % 8 == 0, "shard width % 8");
+  TORCH_CHECK(out.numel() == inp.numel() * c->args.world, "out [R, W*n]");
+  TORCH_CHECK((size_t)inp.numel() <= c->args.half_elems, "shard larger than the buffer");
+  for (int p = 0; p < c->args.world; ++p)
+    TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
+  const c10::DeviceGuard g(inp.device());
+  akap::launch_custom_allgather(c->args, inp.data_ptr(), out.data_ptr(), rows, (int)n,
+                                cur_stream());
+}
+
+// In-place broadcast of buf (any dtype, nbytes % 16 == 0) from group rank `root`.
+void car_broadcast(int64_t h, Tensor buf, int64_t root) {
+  CarComm* c = car_get(h);
+  CHECK_GPU(buf); CHECK_CONTIG(buf);
+  const int64_t bytes = buf.numel() * buf.element_size();
+  TORCH_CHECK(bytes % 16 == 0, "broadcast bytes % 16");
+  TORCH_CHECK((size_t)bytes <= c->args.half_elems * 2, "message larger than the buffer");
+  TORCH_CHECK(root >= 0 && root < c->args.world, "root rank");
+  for (int p = 0; p < c->args.world; ++p)
+    TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
+  const c10::DeviceGuard g(buf.device());
+  akap::launch_custom_broadcast(c->args, buf.data_ptr(), bytes, (int)root, cur_stream());
+}
+
+// ---------------------------------------------------------------- hipIpc of a whole tensor
+// (the P/D KV pull): export -> [handle | offset of data_ptr in its allocation | bytes]
+namespace {
+std::vector<std::pair<int64_t, void*>>& ipc_opened() {
+  static std::vector<std::pair<int64_t, void*>> t;
+  return t;
+}
+}  // namespace
+
+Tensor ipc_export(Tensor t) {
+  CHECK_GPU(t);
+  const c10::DeviceGuard g(t.device());
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  HIP_OK(hipMemGetAddressRange(&base, &size, t.data_ptr()));
+  hipIpcMemHandle_t hd;
+  HIP_OK(hipIpcGetMemHandle(&hd, base));
+  const int64_t off = (int64_t)((char*)t.data_ptr() - (char*)base);
+  const int64_t nbytes = t.numel() * t.element_size();
+  TORCH_CHECK(off >= 0 && (size_t)(off + nbytes) <= size, "tensor outside its allocation");
+  auto out = at::empty({(int64_t)sizeof(hd) + 16}, at::kByte);
+  std::memcpy(out.data_ptr<uint8_t>(), &hd, sizeof(hd));
+  std::memcpy(out.data_ptr<uint8_t>() + sizeof(hd), &off, 8);
+  std::memcpy(out.data_ptr<uint8_t>() + sizeof(hd) + 8, &nbytes, 8);
+  return out;
+}
+
+// Map a peer's exported tensor; returns its device address (valid on `device` until
+// ipc_close).  The same GPU (two processes) or a peer GPU over xGMI.
+int64_t ipc_open(Tensor blob, int64_t device) {
+  TORCH_CHECK(blob.device().is_cpu() && blob.scalar_type() == at::kByte &&
+              blob.numel() == (int64_t)sizeof(hipIpcMemHandle_t) + 16, "ipc_export blob");
+  const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (int)device));
+  auto b = blob.contiguous();
+  hipIpcMemHandle_t hd;
+  int64_t off = 0;
+  std::memcpy(&hd, b.data_ptr<uint8_t>(), sizeof(hd));
+  std::memcpy(&off, b.data_ptr<uint8_t>() + sizeof(hd), 8);
+  void* p = nullptr;
+  HIP_OK(hipIpcOpenMemHandle(&p, hd, hipIpcMemLazyEnablePeerAccess));
+  const int64_t addr = (int64_t)((char*)p + off);
+  ipc_opened().emplace_back(addr, p);
+  return addr;
+}
+
+void ipc_close(int64_t addr) {
+  auto& t = ipc_opened();
+  for (size_t i = 0; i < t.size(); ++i)
+    if (t[i].first == addr) {
+      (void)hipIpcCloseMemHandle(t[i].second);
+      t.erase(t.begin() + i);
+      return;
+    }
+}
+
 void car_destroy(int64_t h) {
   CarComm* c = car_get(h);
   const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, c->device));
@@ -963,6 +1091,14 @@ TORCH_LIBRARY(akap, m) {
   m.def("car_all_reduce_resnorm(int h, Tensor inp, Tensor(a!) residual, Tensor ln, "
         "Tensor(b!) aout, Tensor(c!) ss, bool two_shot) -> ()");
   m.def("car_destroy(int h) -> ()");
+  m.def("car_all_gather(int h, Tensor inp, Tensor(a!) out) -> ()");
+  m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
+  m.def("ipc_export(Tensor t) -> Tensor");
+  m.def("ipc_open(Tensor blob, int device) -> int");
+  m.def("ipc_close(int addr) -> ()");
+  m.def(
+      "kv_pull(int src_ptr, int src_plane_stride, Tensor(a!) dst_cache, Tensor pairs, "
+      "Tensor(b!)? tail, Tensor? tail_jobs, int Hkv, int BS, int D) -> ()");
   m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def("moe_router_topk(Tensor h, Tensor router, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def(
@@ -993,6 +1129,8 @@ TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("car_error", &car_error);
   m.impl("car_link_local", &car_link_local);
   m.impl("car_destroy", &car_destroy);
+  m.impl("ipc_open", &ipc_open);
+  m.impl("ipc_close", &ipc_close);
   m.impl("set_attn_flags", &set_attn_flags);
 }
 
@@ -1025,5 +1163,9 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("car_all_reduce_resnorm", &car_all_reduce_resnorm);
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);
+  m.impl("kv_pull", &kv_pull);
+  m.impl("car_all_gather", &car_all_gather);
+  m.impl("car_broadcast", &car_broadcast);
+  m.impl("ipc_export", &ipc_export);
   m.impl("embedding", &embedding);
 }

@@ -258,10 +258,17 @@ class LLMEngine:
                                     int(info["num_computed"])))
         return out
 
-    def activate(self, iid: int) -> None:
+    def tail_slot(self, iid: int) -> int:
+        """The V-tail slot of a reserved request (assigned now if it has none; -1 = none)."""
+        with self._lock:
+            return int(self.sched.tail_slot(int(iid)))
+
+    def activate(self, iid: int, tail_filled: bool = False) -> None:
+        """tail_filled: the KV hand-off already wrote the request's V tail (the IPC pull
+        fills it in the same launch)."""
         with self._lock:
             self.sched.activate(int(iid))
-            if self.runner.v_tails is not None:
+            if self.runner.v_tails is not None and not tail_filled:
                 # the prompt's KV arrived whole: its partial last V group -> the V tail
                 info = self.sched.request_info(int(iid))
                 if info is not None:

@@ -130,8 +130,22 @@ class ModelRunner:
             return
         g0, cnt = n & ~7, n % 8
         blk, grp = int(block_table[g0 // self.bs]), (g0 % self.bs) // 8
+        if self.is_gpu:
+            # one launch for every layer (the tail-only form of the IPC pull kernel, reading
+            # this engine's own cache) instead of a per-layer copy loop
+            planes = self.kv_planes()
+            ops.kv_pull(planes.data_ptr(), planes.stride(0), planes.shape[1], planes, [],
+                        self.model.hkv, self.bs, self.model.D, tail=self._tail,
+                        tail_jobs=[(blk, grp, cnt, slot)])
+            return
         for vt, vc in zip(self.v_tails, self.v_caches):
             vt[slot, :, :cnt].copy_(vc[blk, :, grp, :, :cnt].transpose(-1, -2))
+
+    def kv_planes(self) -> torch.Tensor:
+        """The KV cache as [2L planes, NB, block_elems] (bf16 view: fp8 bytes move in pairs)."""
+        kv = self.kv.view(torch.bfloat16) if self.kv.dtype == torch.uint8 else self.kv
+        L, two, NB, be = kv.shape
+        return kv.view(L * two, NB, be)
 
     # ------------------------------------------------------------------ sizing
     def _derive_num_blocks(self) -> int:
@@ -361,10 +375,9 @@ class ModelRunner:
 
     def _decode_body(self, n: int, extras: Optional[dict] = None) -> None:
         if self._tp_bcast_inputs:
-            import torch.distributed as dist
+            from ..parallel import comm
 
-            dist.broadcast(self.ddec, src=self.ps.rank - self.ps.tp_rank,
-                           group=self.ps.tp_group)
+            comm.tp_broadcast(self.ddec)  # custom IPC broadcast (or RCCL), in the graph
         dd = self.dd
         if self._ep_moe:
             moe_mod.ep_overflow_reset(self.device)

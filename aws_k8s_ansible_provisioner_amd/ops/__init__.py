@@ -651,3 +651,54 @@ def kv_scatter(buf, cache_planes, block_ids):
     blk = cache_planes[0, 0].numel()
     view = cache_planes.view(planes, cache_planes.shape[1], blk)
     view[:, block_ids.long()] = buf.view(planes, block_ids.numel(), blk)
+
+
+def kv_pull(src_ptr: int, src_plane_stride: int, src_nblocks: int, dst_planes: torch.Tensor,
+            pairs, Hkv: int, BS: int, D: int, tail: Optional[torch.Tensor] = None,
+            tail_jobs=None) -> None:
+    """hipIpc KV hand-off (csrc/kernels/kv_transfer.hip): copy blocks pairs[i] = (src block,
+    dst block) of every plane from the cache at device address `src_ptr` (a peer's cache
+    mapped by ipc_open, or this engine's own) into dst_planes [planes, NB, block_elems], and
+    fill V tails: tail_jobs[j] = (src block, 8-token group, count 1..7, tail slot).  One
+    launch on the current stream.  Every index is range-checked here, on the host, before
+    anything reaches the kernel (an out-of-range block id would read or write outside the
+    caches)."""
+    nb = dst_planes.shape[1]
+    pairs = [(int(s), int(d)) for s, d in pairs]
+    for s, d in pairs:
+        if not (0 <= s < src_nblocks and 0 <= d < nb):
+            raise IndexError(f"kv_pull block pair ({s}, {d}) outside ({src_nblocks}, {nb})")
+    jobs = [tuple(int(x) for x in j) for j in (tail_jobs or [])]
+    if jobs:
+        if tail is None:
+            raise ValueError("tail jobs without a tail tensor")
+        for s, g, c, slot in jobs:
+            if not (0 <= s < src_nblocks and 0 <= g < BS // 8 and 1 <= c <= 7
+                    and 0 <= slot < tail.shape[1]):
+                raise IndexError(f"kv_pull tail job {(s, g, c, slot)} out of range")
+    if not pairs and not jobs:
+        return
+    dev = dst_planes.device
+    pt = torch.tensor(pairs, dtype=torch.int32).reshape(-1).to(dev, non_blocking=True) \
+        if pairs else torch.zeros(0, dtype=torch.int32, device=dev)
+    jt = torch.tensor(jobs, dtype=torch.int32).reshape(-1).to(dev, non_blocking=True) \
+        if jobs else None
+    torch.ops.akap.kv_pull(int(src_ptr), int(src_plane_stride), dst_planes, pt,
+                           tail if jobs else None, jt, Hkv, BS, D)
+
+
+def ipc_export(t: torch.Tensor) -> bytes:
+    """hipIpc handle of t's allocation + t's offset in it + t's byte size (ops.cpp)."""
+    load_native(required=True)
+    return torch.ops.akap.ipc_export(t).numpy().tobytes()
+
+
+def ipc_open(blob: bytes, device: int) -> int:
+    """Map a peer's ipc_export()ed tensor; returns its device address on `device`."""
+    load_native(required=True)
+    return int(torch.ops.akap.ipc_open(torch.frombuffer(bytearray(blob), dtype=torch.uint8),
+                                       device))
+
+
+def ipc_close(addr: int) -> None:
+    torch.ops.akap.ipc_close(int(addr))

@@ -5,7 +5,9 @@ switch: a ring all-reduce is bound by one link per hop.  The policy here:
   * decode-time all-reduces (a few KB-MB per layer) -> the custom one-/two-shot xGMI
     kernel (parallel/custom_allreduce.py, one launch, graph-capturable); larger ones
     (prefill) -> one RCCL all_reduce in place;
-  * vocab-parallel logits -> all_gather into a pre-allocated buffer;
+  * vocab-parallel logits -> the custom IPC all-gather (decode sizes; rank-major columns
+    straight into the pre-allocated result) or one RCCL all_gather;
+  * the TP decode step's input region -> the custom IPC broadcast (or RCCL broadcast);
   * MoE token dispatch/combine -> all_to_all_single with explicit split sizes;
   * KV hand-off (P/D) -> one packed send/recv per request (see parallel/kv_transfer.py).
 All functions are no-ops for a group of size 1, so single-GPU code paths pay nothing.
@@ -43,7 +45,9 @@ def tp_all_reduce_resnorm(partial: torch.Tensor, residual: torch.Tensor, ln: tor
         st.car.all_reduce_resnorm(partial, residual, ln, a_out, ss)
         return
     if st.tp_size > 1:
-        dist.all_reduce(partial, group=st.tp_group)
+        # no fused epilogue for this row width: the plain custom all-reduce (still one of our
+        # capturable kernels) or RCCL, then the elementwise epilogue
+        tp_all_reduce(partial)
     r = (partial.float() + residual.float()).to(residual.dtype)
     residual.copy_(r)
     a_out.copy_((r.float() * ln.float()).to(a_out.dtype))
@@ -77,12 +81,29 @@ def tp_all_gather_last(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> t
     x = x.contiguous()
     flat = x.reshape(1, -1) if x.dim() == 1 else x.reshape(-1, x.shape[-1])
     R, n = flat.shape
+    if st.car is not None and st.car.gather_ok(flat):
+        if out is None:
+            out = _gather_ws("result", R, st.tp_size * n, x.dtype, x.device)
+        st.car.all_gather(flat, out.view(R, st.tp_size * n))
+        return out.view(*x.shape[:-1], st.tp_size * n)
     buf = _gather_ws("gather", st.tp_size * R, n, x.dtype, x.device)
     dist.all_gather_into_tensor(buf, flat, group=st.tp_group)  # rank-major rows
     if out is None:
         out = _gather_ws("result", R, st.tp_size * n, x.dtype, x.device)
     out.view(R, st.tp_size, n).copy_(buf.view(st.tp_size, R, n).transpose(0, 1))
     return out.view(*x.shape[:-1], st.tp_size * n)
+
+
+def tp_broadcast(t: torch.Tensor) -> torch.Tensor:
+    """In place: every TP rank's t becomes the TP group's rank-0 copy (the custom IPC
+    broadcast when it fits -- capturable on any control backend -- else RCCL)."""
+    st = get_state()
+    if st.tp_size == 1:
+        return t
+    if st.car is not None and st.car.bcast_ok(t):
+        return st.car.broadcast(t, 0)
+    dist.broadcast(t, src=st.rank - st.tp_rank, group=st.tp_group)
+    return t
 
 
 def all_to_all(x: torch.Tensor, out_splits: list[int], in_splits: list[int], group=None

@@ -7,6 +7,11 @@ Decode-sized activations (<= ``max_bytes``) then take one kernel launch instead 
 RCCL ring; larger messages (prefill) fall back to RCCL.  The kernels keep their epochs
 on the device, so they replay correctly inside captured hipGraphs.
 
+Siblings on the same IPC buffers, flags and device-side epochs: `all_gather` (the
+vocab-parallel logits, rank-major column blocks) and `broadcast` (rank 0's decode staging
+region).  With all three, a TP decode hipGraph records no RCCL call at all: it replays
+across the xGMI mesh and across ranks that share one GPU (gloo control plane) alike.
+
 Policy (xGMI mesh, W ranks): one-shot reads (W-1) x the message over W-1 links at once
 and has one flag exchange -- best while the message is small; two-shot moves 2(W-1)/W x
 the message with two flag exchanges -- better once link bandwidth, not latency, binds.
@@ -69,6 +74,23 @@ class CustomAllReduce:
         chain's residual-add epilogue, fused into the all-reduce's store pass)."""
         two = x.numel() * 2 > self.oneshot_bytes and self.world > 2
         torch.ops.akap.car_all_reduce_resnorm(self.h, x, residual, ln, a_out, ss, two)
+
+    def gather_ok(self, x: torch.Tensor) -> bool:
+        return (self.should_use(x) and x.dim() >= 1 and x.shape[-1] % 8 == 0)
+
+    def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """x [R, n] (this rank's shard) -> out [R, world*n], rank-major column blocks."""
+        torch.ops.akap.car_all_gather(self.h, x, out)
+        return out
+
+    def bcast_ok(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * t.element_size()
+        return t.is_cuda and t.is_contiguous() and nbytes % 16 == 0 and nbytes <= self.max_bytes
+
+    def broadcast(self, t: torch.Tensor, root: int) -> torch.Tensor:
+        """In place: every rank's t becomes group rank `root`'s t."""
+        torch.ops.akap.car_broadcast(self.h, t, root)
+        return t
 
     def error(self) -> int:
         return int(torch.ops.akap.car_error(self.h))

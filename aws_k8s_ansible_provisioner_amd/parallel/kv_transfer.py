@@ -27,6 +27,15 @@ Generations are monotonic, so a repeated or crossed reset request is a no-op.  A
 Control plane: the decode side asks the prefill server (HTTP POST /kv/push) to send the
 blocks of one or more transfer ids to its rank, then posts the matching recv.  The same
 code runs on CPU with the gloo backend (tests).
+
+hipIpc PULL transport (the default between GPU engines of one node, AKAP_KV_TRANSPORT=ipc):
+the prefill engine exports its whole KV cache ONCE (`ipc_meta`: a hipIpc handle of the
+cache allocation + the cache geometry) and the decode engine maps it (`connect_ipc`).  A
+hand-off is then one `kv_pull` kernel on the decode GPU that reads the request's blocks
+straight out of the peer cache (xGMI, or the same HBM when both engines share a GPU) into
+its own block ids and fills the request's V tail in the same launch: no pack, no send /
+recv pairing, no unpack, no host staging.  The prefill keeps the blocks leased until the
+decode acknowledges the pull (HTTP POST /kv/done, or the PDPair ack channel).
 """
 from __future__ import annotations
 
@@ -104,6 +113,8 @@ class KVTransferAgent:
         # the P/D path) stage through pinned host memory
         self.gloo = dist.is_initialized() and dist.get_backend(group) == "gloo"
         self.host_staging = self.is_gpu and self.gloo
+        self.peers: dict = {}  # hipIpc: peer key -> (mapped cache address, blocks, plane stride)
+        self.pull_seconds = 0.0
 
     def nbytes(self, nblk: int) -> int:
         return self.planes.shape[0] * nblk * self.block_elems * self.kv.element_size()
@@ -293,7 +304,67 @@ class KVTransferAgent:
 
         return self._submit(fn, True)
 
+    # ---------------------------------------------------------------- hipIpc pull
+    def ipc_meta(self) -> dict:
+        """What a decode peer needs to map this engine's cache (JSON-able)."""
+        import base64
+
+        P, NB, be = self.planes.shape
+        return {"blob": base64.b64encode(ops.ipc_export(self.planes)).decode(),
+                "planes": int(P), "nblocks": int(NB), "block_elems": int(be),
+                "plane_stride": int(self.planes.stride(0))}
+
+    def connect_ipc(self, meta: dict) -> str:
+        """Map a prefill peer's cache (once per peer; the mapping lives as long as this agent).
+        Returns the peer key for pull(); a decode engine of an N:M pod maps several."""
+        import base64
+
+        P, NB, be = self.planes.shape
+        if (int(meta["planes"]), int(meta["block_elems"])) != (P, be):
+            raise ValueError(f"peer cache geometry {meta['planes']}x{meta['block_elems']} != "
+                             f"ours {P}x{be} (same model and block size required)")
+        key = meta["blob"]
+        if key not in self.peers:
+            ptr = ops.ipc_open(base64.b64decode(meta["blob"]), self.device.index)
+            self.peers[key] = (ptr, int(meta["nblocks"]), int(meta["plane_stride"]))
+        return key
+
+    @property
+    def ipc_connected(self) -> bool:
+        return bool(self.peers)
+
+    def pull(self, pairs: list, Hkv: int, BS: int, D: int, tail=None,
+             tail_jobs: Optional[list] = None, peer: Optional[str] = None) -> float:
+        """One kv_pull launch on the agent stream: pairs (peer block, own block) of every
+        plane, plus V-tail jobs (peer block, group, count, tail slot); waits for it.  Returns
+        the seconds the pull took (host-observed, launch to completion)."""
+        if not self.peers:
+            raise KVChannelBroken("no peer cache mapped (connect_ipc)")
+        if peer is None:
+            if len(self.peers) != 1:
+                raise ValueError("several peer caches mapped: name the peer")
+            peer = next(iter(self.peers))
+        ptr, nblocks, stride = self.peers[peer]
+        t0 = time.perf_counter()
+        with self._ctx():
+            ops.kv_pull(ptr, stride, nblocks, self.planes, pairs, Hkv, BS, D, tail=tail,
+                        tail_jobs=tail_jobs)
+            self.stream.synchronize()
+        dt = time.perf_counter() - t0
+        self.bytes_recv += self.nbytes(len(pairs))
+        self.pull_seconds += dt
+        self.transfers += 1
+        return dt
+
     def close(self) -> None:
+        if self.peers:
+            try:
+                torch.cuda.synchronize(self.device)
+                for ptr, _, _ in self.peers.values():
+                    ops.ipc_close(ptr)
+            except Exception:
+                pass
+            self.peers = {}
         self._q.put(None)
 
 

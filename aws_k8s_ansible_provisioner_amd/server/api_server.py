@@ -115,6 +115,7 @@ class OpenAIServer:
         self.max_model_len = max_model_len
         self.created = int(time.time())
         self._dropped_push = False  # fault injection (AKAP_FAULT_KV_PUSH=drop_once)
+        self._ipc_meta = None  # hipIpc export of this engine's KV cache (made on first lease)
         self.app = self._build()
 
     # ------------------------------------------------------------------ helpers
@@ -261,6 +262,39 @@ class OpenAIServer:
             self.ae.kv_agent.send_blocks(blocks, int(body["dst_rank"]), on_done=done)
             nb = [len(b) for b in per]
             return {"ok": True, "num_blocks": nb if "transfer_ids" in body else nb[0]}
+
+        @app.post("/kv/lease")
+        async def kv_lease(req: Request):
+            """P/D prefill side, hipIpc transport: lease the held KV of one or more transfers
+            to the decode engine, which pulls the blocks itself out of this engine's cache
+            (mapped once from `ipc`); the blocks stay owned by the lease until /kv/done."""
+            body = await req.json()
+            ag = self.ae.kv_agent
+            if ag is None or not getattr(ag, "is_gpu", False):
+                return _err(400, "not a GPU P/D prefill server")
+            tids = [int(t) for t in body["transfer_ids"]]
+            per = [eng.held_blocks(t) for t in tids]
+            missing = [t for t, b in zip(tids, per) if not b]
+            if missing:
+                return _err(404, f"no held KV for transfer(s) {missing}")
+            per = [eng.take_held(t) for t in tids]
+            if any(not b for b in per):  # expired between the check and the take
+                for t in tids:
+                    eng.finish_transfer(t)
+                return _err(404, f"held KV for transfer(s) {tids} expired")
+            if self._ipc_meta is None:
+                self._ipc_meta = ag.ipc_meta()
+            return {"ok": True, "blocks": [[int(b) for b in bl] for bl in per],
+                    "ipc": self._ipc_meta}
+
+        @app.post("/kv/done")
+        async def kv_done(req: Request):
+            """P/D prefill side: the decode engine finished pulling (or gave up on) these
+            leased transfers: free their blocks."""
+            body = await req.json()
+            for t in body["transfer_ids"]:
+                eng.finish_transfer(int(t))
+            return {"ok": True}
 
         @app.post("/kv/reset")
         async def kv_reset(req: Request):

@@ -10,6 +10,7 @@ from __future__ import annotations
 import asyncio
 import dataclasses
 import json
+import os
 import queue
 import threading
 import urllib.request
@@ -106,6 +107,9 @@ class KVPuller:
                 self._resolve(j, e)
         if not ready:
             return
+        if self.transport() == "ipc":
+            self._pull_batch_ipc(url, ready, reserved)
+            return
         try:
             body = json.dumps({"transfer_ids": [int(j.kvp["transfer_id"]) for j in ready],
                                "dst_rank": eng.rank, "group": self.ae.pd_group}).encode()
@@ -134,6 +138,73 @@ class KVPuller:
         self.batches += 1
         for j, (iid, _) in zip(ready, reserved):
             eng.activate(iid)
+            self._resolve(j, None)
+        self.ae._wake.set()
+
+
+    def transport(self) -> str:
+        """AKAP_KV_TRANSPORT: ipc (GPU default: pull the blocks out of the prefill engine's
+        hipIpc-mapped cache) or p2p (/kv/push + a packed send/recv over the process group)."""
+        env = os.environ.get("AKAP_KV_TRANSPORT", "auto")
+        if env in ("ipc", "p2p"):
+            return env
+        return "ipc" if getattr(self.ae.kv_agent, "is_gpu", False) else "p2p"
+
+    def _pull_batch_ipc(self, url: str, ready: list, reserved: list) -> None:
+        """hipIpc transport: lease the transfers' blocks (POST /kv/lease), map the prefill
+        cache on first use, ONE kv_pull launch moves every request's blocks and fills their V
+        tails, then release the lease (POST /kv/done) -- also on failure."""
+        eng = self.ae.engine
+        agent = self.ae.kv_agent
+        runner = eng.runner
+        tids = [int(j.kvp["transfer_id"]) for j in ready]
+
+        def post(path, body):
+            req = urllib.request.Request(url.rstrip("/") + path, data=json.dumps(body).encode(),
+                                         headers={"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=60) as r:
+                return json.loads(r.read())
+
+        leased = False
+        try:
+            meta = post("/kv/lease", {"transfer_ids": tids})
+            leased = True
+            src = [[int(b) for b in bl] for bl in meta["blocks"]]
+            if [len(b) for b in src] != [len(b) for _, b in reserved]:
+                raise RuntimeError(f"KV block count mismatch {[len(b) for b in src]} vs "
+                                   f"{[len(b) for _, b in reserved]}")
+            peer = agent.connect_ipc(meta["ipc"])  # one mapping per prefill engine
+            bs = eng.ecfg.block_size
+            pairs, tails = [], []
+            for j, (iid, blocks), sb in zip(ready, reserved, src):
+                pairs += list(zip(sb, blocks))
+                n = len(j.prompt_ids)
+                if runner.v_tails is not None and n % 8:
+                    slot = eng.tail_slot(iid)
+                    if slot >= 0:
+                        g0 = n & ~7
+                        tails.append((sb[g0 // bs], (g0 % bs) // 8, n % 8, slot))
+            agent.pull(pairs, runner.model.hkv, bs, runner.model.D,
+                       tail=getattr(runner, "_tail", None), tail_jobs=tails, peer=peer)
+        except Exception as e:
+            for j, (iid, _) in zip(ready, reserved):
+                eng.abort_request(j.req_id)  # frees the reserved decode blocks
+                if not leased:
+                    AsyncEngine._release_remote(j.kvp)
+                self._resolve(j, e)
+            if leased:
+                try:
+                    post("/kv/done", {"transfer_ids": tids})
+                except Exception as e2:  # the prefill side's TTL cannot free leased blocks
+                    print(f"[pd] /kv/done to {url} failed: {e2}", flush=True)
+            return
+        try:
+            post("/kv/done", {"transfer_ids": tids})
+        except Exception as e:
+            print(f"[pd] /kv/done to {url} failed: {e}", flush=True)
+        self.batches += 1
+        for j, (iid, _) in zip(ready, reserved):
+            eng.activate(iid, tail_filled=True)
             self._resolve(j, None)
         self.ae._wake.set()
 

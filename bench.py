@@ -17,9 +17,11 @@ process at R req/s (streaming, so every token is timestamped) and the line also 
 p50/p99 TTFT, TPOT (per-request mean inter-token time) and p99 inter-token latency; with
 --no-mixed-batching the prefill-first policy is measured for comparison.
 
---mode pd (even WORLD_SIZE): disaggregated prefill/decode -- ranks [0, W/2) prefill,
-[W/2, W) decode, each request's KV moved prefill->decode with one RCCL send/recv
-(parallel/pd_driver.py); TTFT is measured on the decode side (includes the hand-off).
+--mode pd: disaggregated prefill/decode -- ranks [0, N) prefill (N = --pd-prefill-ranks,
+default W/2), [N, W) decode; each request's KV moves prefill->decode by a hipIpc pull of
+the prefill engine's cache (one kv_pull launch per hand-off message; GPU default) or a
+packed send/recv (parallel/pd_driver.py); TTFT is measured on the decode side (includes
+the hand-off).
 
 Prints ONE JSON line on rank 0.
 """
@@ -60,14 +62,20 @@ def parse():
                          "engine replica (Llama-3-70B TP=8 config; Mixtral EP with "
                          "AKAP_MOE_MODE=ep)")
     ap.add_argument("--mode", default="mono", choices=["mono", "pd"],
-                    help="mono: every rank a monolithic replica (DP); pd: ranks [0,W/2) prefill, "
-                         "[W/2,W) decode, KV handed over RCCL (Llama-3-8B disagg config)")
+                    help="mono: every rank a monolithic replica (DP); pd: ranks [0,N) prefill, "
+                         "[N,W) decode, KV by hipIpc pull or send/recv (Llama-3-8B disagg config)")
     ap.add_argument("--pd-push", default="auto", choices=["auto", "chunked", "whole"],
                     help="--mode pd: stream each prompt's KV chunk by chunk while the prefill "
                          "continues, or hand the whole prompt over at its end.  auto: chunked "
                          "on RCCL, whole on a host-staged gloo channel, where the transfer is "
                          "the bottleneck and per-chunk sends only add overhead "
                          "(profiles/r3_pd_push_gpu_gloo.log)")
+    ap.add_argument("--pd-prefill-ranks", type=int, default=0,
+                    help="--mode pd: N prefill ranks (the other W-N decode; W-N a multiple of N; "
+                         "default W/2, i.e. 1:1 pairs)")
+    ap.add_argument("--kv-transport", default="auto", choices=["auto", "ipc", "p2p"],
+                    help="--mode pd: hipIpc pull of the prefill cache (GPU default) or packed "
+                         "send/recv over the process group")
     ap.add_argument("--dist-backend", default=None,
                     help="override (gloo = single-GPU rehearsal of the multi-rank paths)")
     ap.add_argument("--arrival-rate", type=float, default=0.0,
@@ -120,10 +128,16 @@ def main() -> int:
         dist.all_gather_object(devs, dev_id)
     n_dev = physical_devices(devs)
     pd = a.mode == "pd"
-    if pd and (world < 2 or world % 2):
-        print("error: --mode pd needs an even WORLD_SIZE >= 2", file=sys.stderr)
-        return 2
-    is_prefill = pd and rank < world // 2
+    n_pre = 0
+    if pd:
+        from aws_k8s_ansible_provisioner_amd.parallel.pd_driver import pd_layout
+
+        try:
+            n_pre, _ = pd_layout(world, a.pd_prefill_ranks or None)
+        except ValueError as e:
+            print(f"error: --mode pd: {e}", file=sys.stderr)
+            return 2
+    is_prefill = pd and rank < n_pre
 
     mcfg = get_config(a.model)
     ecfg = EngineConfig(model=a.model, max_model_len=a.max_model_len,
@@ -131,7 +145,7 @@ def main() -> int:
                         max_num_batched_tokens=a.max_num_batched_tokens,
                         block_size=a.block_size, enforce_eager=a.enforce_eager,
                         device="cuda" if gpu else "cpu",
-                        seed=1234 + (rank % (world // 2) if pd else rank),  # P/D pair: same weights
+                        seed=1234 if pd else 1234 + rank,  # P/D ranks: the same weights
                         num_gpu_blocks=None if gpu else 512,
                         kv_role=("prefill" if is_prefill else "decode") if pd else "both",
                         kv_cache_dtype=a.kv_cache_dtype,
@@ -162,7 +176,9 @@ def main() -> int:
         from aws_k8s_ansible_provisioner_amd.parallel.pd_driver import PDPair
 
         ctrl = dist.new_group(backend="gloo")  # small metadata messages on the host
-        pair = PDPair(eng, rank, world, ctrl_group=ctrl, data_group=None)
+        pair = PDPair(eng, rank, world, ctrl_group=ctrl, data_group=None,
+                      prefill_ranks=n_pre,
+                      transport=None if a.kv_transport == "auto" else a.kv_transport)
 
     lat = {"itl": [], "tpot": []}
 
@@ -205,8 +221,9 @@ def main() -> int:
         if pd:
             if is_prefill:
                 prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
-                chunked = a.pd_push == "chunked" or (a.pd_push == "auto" and
-                                                     dist.get_backend() != "gloo")
+                # auto: chunk by chunk, except over a host-staged gloo send/recv channel
+                chunked = a.pd_push == "chunked" or (a.pd_push == "auto" and (
+                    pair.transport == "ipc" or dist.get_backend() != "gloo"))
                 pair.run_prefill(prompts, sp, chunked=chunked)
                 return 0, []
             r = pair.run_decode(sp, time.time())
@@ -262,9 +279,19 @@ def main() -> int:
         dist.all_gather(t_all, torch.tensor([p50_local], dtype=torch.float64, device=dev))
         p50s = [x.item() for x in t_all]
         if pd:  # TTFT is observed on the decode ranks
-            p50s = p50s[world // 2:]
+            p50s = p50s[n_pre:]
         stats = torch.tensor([t_tok.item(), t_el.item(), statistics.median(p50s)])
     tok, el, p50 = float(stats[0]), float(stats[1]), float(stats[2])
+    kv_stats = None
+    if pair is not None:
+        # KV hand-off rate over the decode ranks' pulls (IPC transport)
+        kt = torch.tensor([float(pair.pulled_bytes), pair.pull_seconds], dtype=torch.float64,
+                          device=torch.device("cuda", local) if gpu else torch.device("cpu"))
+        dist.all_reduce(kt)
+        kv_stats = {"kv_transport": pair.transport,
+                    "kv_pulled_gb": round(kt[0].item() / 1e9, 3),
+                    "kv_pull_gbps": round(kt[0].item() / 1e9 / kt[1].item(), 1)
+                    if kt[1].item() > 0 else None}
     if rank == 0:
         res = {
             "metric": "output tok/s + p50 TTFT",
@@ -284,13 +311,13 @@ def main() -> int:
             "p50_ttft_ms": round(p50 * 1000, 2),
             "config": {
                 "model": mcfg.hf_id,
-                "global_batch": a.num_requests * (world // 2 if pd else
+                "global_batch": a.num_requests * (n_pre if pd else
                                                   1 if a.tp > 1 else max(world, 1)),
                 "seq_len": a.input_len + a.output_len,
                 "input_len": a.input_len,
                 "output_len": a.output_len,
-                ("requests_per_pd_pair" if pd else "requests_per_gpu"): a.num_requests,
-                "parallelism": (f"pd{world // 2}x{world // 2}" if pd else
+                ("requests_per_prefill_rank" if pd else "requests_per_gpu"): a.num_requests,
+                "parallelism": (f"pd{n_pre}x{world - n_pre}" if pd else
                                 f"tp{a.tp}" if a.tp > 1 else f"dp{max(world, 1)}"),
                 "max_num_seqs": a.max_num_seqs,
                 "sampling": "greedy" if a.temperature <= 0 else f"T={a.temperature}",
@@ -299,6 +326,8 @@ def main() -> int:
                 "mixed_batching": not a.no_mixed_batching,
             },
         }
+        if kv_stats is not None:
+            res.update(kv_stats)
         if a.arrival_rate > 0:
             res["arrival_rate_rps"] = a.arrival_rate
             res["p99_ttft_ms"] = round(pct(ttfts, 99) * 1000, 2)

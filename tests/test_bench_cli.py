@@ -81,3 +81,12 @@ def test_bench_counts_physical_devices_not_ranks():
     assert bench.physical_devices([("h", 0), ("h", 1)]) == 2
     assert bench.physical_devices([("a", 0), ("b", 0)]) == 2
     assert bench.physical_devices([None, None]) == 0
+
+
+def test_bench_pd_one_prefill_two_decode_ranks():
+    """N:M P/D in the bench: 1 prefill rank feeding 2 decode ranks (round robin), p2p KV
+    transport over gloo on CPU."""
+    res = _run(["--mode", "pd", "--pd-prefill-ranks", "1", "--kv-transport", "p2p",
+                "--model", "tiny-qwen3"] + SMALL, nproc=3)
+    assert res["config"]["parallelism"] == "pd1x2" and res["ranks"] == 3
+    assert res["config"]["global_batch"] == 6 and res["kv_transport"] == "p2p"

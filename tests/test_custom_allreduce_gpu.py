@@ -251,3 +251,150 @@ def test_custom_allreduce_resnorm_epilogue(world, two_shot, M, d):
         torch.cuda.synchronize()
         for h in hs:
             torch.ops.akap.car_destroy(h)
+
+
+def _ipc_siblings_worker(rank, world, port, q):
+    """All-reduce, all-gather and broadcast launches interleaved on one communicator (the
+    per-block epochs are shared by every kind), across `world` processes on one GPU."""
+    import torch.distributed as dist
+
+    from aws_k8s_ansible_provisioner_amd.parallel.custom_allreduce import CustomAllReduce
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        car = CustomAllReduce(group=None, device=torch.device("cuda", 0), max_bytes=1 << 20)
+        res = []
+        for it in range(4):
+            g = torch.Generator().manual_seed(100 * it + rank)
+            shard = torch.randn(37, 136, generator=g).to(torch.bfloat16).to(DEV)
+            out = torch.empty(37, 136 * world, dtype=torch.bfloat16, device=DEV)
+            car.all_gather(shard, out)
+            x = torch.randn(4096, generator=g).to(torch.bfloat16).to(DEV)
+            car.all_reduce(x)
+            # broadcast of a uint8 staging region from rank 0 (every rank starts different)
+            b = torch.full((2048 + 16 * it,), rank + 1, dtype=torch.uint8, device=DEV)
+            if rank == 0:
+                b.copy_(torch.arange(b.numel(), dtype=torch.int64).remainder(251).to(torch.uint8))
+            car.broadcast(b, 0)
+            torch.cuda.synchronize()
+            res.append((out.float().cpu().numpy(), b.cpu().numpy()))
+        err = car.error()
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+        q.put((rank, err, res))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_custom_allgather_broadcast_ipc_processes(world):
+    """The IPC all-gather (rank-major columns) and broadcast, siblings of K13, across
+    processes sharing one MI355X: exact against the host-side expectation, every rank."""
+    import numpy as np
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_siblings_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, err, res = q.get(timeout=240)
+        out[rank] = (err, res)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert out[r][0] == 0, out[r][0]
+    for it in range(4):
+        shards = [torch.randn(37, 136, generator=torch.Generator().manual_seed(100 * it + r))
+                  .to(torch.bfloat16).float().numpy() for r in range(world)]
+        want = np.concatenate(shards, axis=1)
+        bexp = (np.arange(2048 + 16 * it) % 251).astype(np.uint8)
+        for r in range(world):
+            got, b = out[r][1][it]
+            assert np.array_equal(got, want), (r, it)
+            assert np.array_equal(b, bexp), (r, it)
+
+
+def _kv_pull_worker(rank, port, q, geo):
+    """Rank 0 = prefill: a KV cache with a known pattern, exported by hipIpc.  Rank 1 =
+    decode: maps it and pulls blocks + V tails with ONE kv_pull launch."""
+    import base64
+
+    import torch.distributed as dist
+
+    from aws_k8s_ansible_provisioner_amd import ops
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=2)
+        L, Hkv, BS, D, NB0, NB1 = geo
+        be = Hkv * BS * D
+        if rank == 0:
+            g = torch.Generator().manual_seed(5)
+            kv = torch.randn(L, 2, NB0, be, generator=g).to(torch.bfloat16).to(DEV)
+            planes = kv.view(2 * L, NB0, be)
+            meta = [ops.ipc_export(planes), planes.stride(0)]
+            dist.broadcast_object_list(meta, src=0)
+            dist.barrier()  # rank 1 pulled
+            q.put((0, 0, None))
+        else:
+            meta = [None, None]
+            dist.broadcast_object_list(meta, src=0)
+            kv = torch.zeros(L, 2, NB1, be, dtype=torch.bfloat16, device=DEV)
+            planes = kv.view(2 * L, NB1, be)
+            tail = torch.zeros(L, 6, Hkv, 8, D, dtype=torch.bfloat16, device=DEV)
+            ptr = ops.ipc_open(meta[0], 0)
+            pairs = [(3, 0), (NB0 - 1, 5), (0, NB1 - 1)]
+            jobs = [(7, 1, 5, 2), (NB0 - 1, BS // 8 - 1, 3, 5)]
+            ops.kv_pull(ptr, meta[1], NB0, planes, pairs, Hkv, BS, D, tail=tail, tail_jobs=jobs)
+            torch.cuda.synchronize()
+            res = (kv.float().cpu().numpy(), tail.float().cpu().numpy())
+            ops.ipc_close(ptr)
+            dist.barrier()
+            q.put((1, 0, res))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None))
+
+
+def test_kv_pull_ipc_two_processes():
+    """P/D hipIpc transport: the decode process maps the prefill process's cache and one
+    kv_pull launch copies whole blocks (every plane) into its own block ids and writes the
+    requests' partial last V groups token-major into their tails -- exact, vs host indexing."""
+    import numpy as np
+    import torch.multiprocessing as mp
+    geo = (3, 2, 32, 128, 12, 9)  # L, Hkv, BS, D, prefill blocks, decode blocks
+    L, Hkv, BS, D, NB0, NB1 = geo
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kv_pull_worker, args=(r, port, q, geo)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        rank, err, res = q.get(timeout=240)
+        out[rank] = (err, res)
+    for p in procs:
+        p.join(timeout=60)
+    assert out[0][0] == 0 and out[1][0] == 0, (out[0][0], out[1][0])
+    kv, tail = out[1][1]
+    be = Hkv * BS * D
+    src = torch.randn(L, 2, NB0, be, generator=torch.Generator().manual_seed(5)) \
+        .to(torch.bfloat16).float().numpy()
+    want = np.zeros((L, 2, NB1, be), np.float32)
+    for s, d in [(3, 0), (NB0 - 1, 5), (0, NB1 - 1)]:
+        want[:, :, d] = src[:, :, s]
+    assert np.array_equal(kv, want)
+    tw = np.zeros((L, 6, Hkv, 8, D), np.float32)
+    for s, grp, cnt, slot in [(7, 1, 5, 2), (NB0 - 1, BS // 8 - 1, 3, 5)]:
+        v = src[:, 1, s].reshape(L, Hkv, BS // 8, D, 8)[:, :, grp]   # [L, Hkv, D, 8]
+        tw[:, slot, :, :cnt] = v[..., :cnt].transpose(0, 1, 3, 2)
+    assert np.array_equal(tail, tw)

@@ -1,8 +1,11 @@
 """Disaggregated prefill/decode on the GPU, end to end: a prefill server and a decode server
-(two processes sharing ONE MI355X, KV over a host-staged gloo channel), the gateway in front
-pairing them.  A completion through the gateway takes the P/D path (prefill engine -> held KV
--> /kv/push -> decode engine, whose activate() fills the V tail) and must produce exactly the
-monolithic engine's tokens on the same weights."""
+(two processes sharing ONE MI355X), the gateway in front pairing them.  Both KV transports:
+  ipc  the decode engine maps the prefill engine's cache (hipIpc) and pulls the request's
+       blocks + fills its V tail with one kv_pull launch (/kv/lease ... /kv/done);
+  p2p  /kv/push -> packed send over a host-staged gloo channel -> unpack, activate() fills
+       the V tail.
+A completion through the gateway takes the P/D path and must produce exactly the monolithic
+engine's tokens on the same weights."""
 import asyncio
 import os
 import socket
@@ -30,7 +33,8 @@ def _port():
     return p
 
 
-def test_pd_through_the_gateway_on_gpu_matches_monolithic():
+@pytest.mark.parametrize("transport", ["ipc", "p2p"])
+def test_pd_through_the_gateway_on_gpu_matches_monolithic(transport):
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
     from aws_k8s_ansible_provisioner_amd.gateway.picker import PickerConfig
@@ -43,7 +47,7 @@ def test_pd_through_the_gateway_on_gpu_matches_monolithic():
             port = _port()
             env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
                        MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master),
-                       AKAP_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+                       AKAP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, AKAP_KV_TRANSPORT=transport)
             procs.append(subprocess.Popen(
                 [sys.executable, "-m", "aws_k8s_ansible_provisioner_amd.server", *COMMON,
                  "--kv-role", role, "--port", str(port), "--host", "127.0.0.1"],

@@ -1,5 +1,8 @@
 """Tensor parallelism on the GPU: 2 TP ranks as 2 processes sharing ONE MI355X (the only
-multi-rank layout a single-GPU box allows), collectives over gloo (host-staged), eager steps.
+multi-rank layout a single-GPU box allows), control plane over gloo.  Eager steps (gloo
+collectives), and the production form: hipGraph-captured decode steps whose every
+collective is one of our IPC kernels (K13 all-reduce, IPC broadcast of rank 0's step inputs,
+IPC all-gather of the vocab-parallel logits) replayed by both processes.
 Mixtral runs its experts TP-sharded and expert-parallel (all-to-all dispatch).  The HIP
 kernels see their real TP shapes -- head-split attention with its own KV shard, row /
 column-split MLP, vocab-parallel LM head, rank-0 step broadcast -- and every generated token
@@ -24,11 +27,13 @@ from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
 ecfg = EngineConfig(model=os.environ["MODEL"], device="cuda", max_model_len=256, max_num_seqs=8,
                     max_num_batched_tokens=64, block_size=32, num_gpu_blocks=96,
                     tensor_parallel_size=int(os.environ["WORLD_SIZE"]), shard_init="full",
-                    init_std=0.15, enforce_eager=True)
+                    init_std=0.15, enforce_eager=os.environ["EAGER"] == "1")
 eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
 from aws_k8s_ansible_provisioner_amd.parallel.state import get_state
 assert (get_state().car is not None) == (os.environ["AKAP_CUSTOM_AR_GLOO"] == "1")
 if eng is not None:
+    if os.environ["EAGER"] == "0":
+        assert eng.runner.graphs, "decode graphs were not captured"
     outs = eng.generate(None, SamplingParams(max_tokens=8, temperature=0, ignore_eos=True),
                         prompt_ids=[list(range(5, 40)), [100, 101], [9, 9, 9]])
     bc.shutdown()
@@ -44,12 +49,15 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("model,moe_mode,car", [
-    ("tiny-llama", "tp", "0"), ("tiny-qwen3", "tp", "0"), ("tiny-mixtral", "tp", "0"),
-    ("tiny-mixtral", "ep", "0"),
+@pytest.mark.parametrize("model,moe_mode,car,eager", [
+    ("tiny-llama", "tp", "0", "1"), ("tiny-qwen3", "tp", "0", "1"),
+    ("tiny-mixtral", "tp", "0", "1"), ("tiny-mixtral", "ep", "0", "1"),
     # the TP all-reduces through the custom all-reduce kernels (K13) across the two processes
-    ("tiny-llama", "tp", "1"), ("tiny-qwen3", "tp", "1")])
-def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode, car):
+    ("tiny-llama", "tp", "1", "1"), ("tiny-qwen3", "tp", "1", "1"),
+    # captured decode graphs replayed across the two processes: only IPC kernels inside
+    ("tiny-llama", "tp", "1", "0"), ("tiny-qwen3", "tp", "1", "0"),
+    ("tiny-mixtral", "tp", "1", "0")])
+def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode, car, eager):
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
     from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logits
@@ -58,7 +66,8 @@ def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode, car):
     procs = []
     for r in range(2):
         env = dict(os.environ, ROOT=ROOT, MODEL=model, RANK=str(r), WORLD_SIZE="2",
-                   AKAP_MOE_MODE=moe_mode, AKAP_CUSTOM_AR_GLOO=car,
+                   AKAP_MOE_MODE=moe_mode, AKAP_CUSTOM_AR_GLOO=car, EAGER=eager,
+                   AKAP_GEMM_TUNE="0",
                    LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, "-c", CHILD], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
