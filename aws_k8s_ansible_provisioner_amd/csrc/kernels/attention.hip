@@ -74,38 +74,6 @@ __device__ __forceinline__ auto ld_raw8(const void* base, size_t off) {
   }
 }
 
-// Issue the loads of the 32-token chunk at absolute kv position t0.
-// K cache layout inside a (block, kv head) is MFMA-fragment ordered (see k_swz_offset in
-// common.h): for each 32-token chunk, [tile tt][k-step cc][row r][32 dims], so one load
-// instruction (fixed tt, cc) reads 16 rows x 64 B = 1 KiB contiguous (a row-major K gives
-// 16 scattered 64-B segments per instruction: -10% decode attention time measured).
-template <bool NT = false, bool F8 = false>
-__device__ __forceinline__ void load_chunk(ChunkT<F8>& c, const void* __restrict__ k_cache,
-                                           const void* __restrict__ v_cache,
-                                           const int* __restrict__ bt, int kv_len, int kvh,
-                                           int Hkv, int BS, int t0) {
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 4;
-  const int r = lane & 15;
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
-    int tok = t0 + 8 * (r >> 2) + 4 * tt + (r & 3);
-    tok = min(tok, kv_len - 1);  // clamped lanes re-read a valid row (masked later)
-    const int blk = bt[tok / BS];
-    const int off = tok % BS;
-    const size_t kp = ((size_t)blk * Hkv + kvh) * BS * kD + k_swz_offset(off) + 8 * g;
-#pragma unroll
-    for (int cc = 0; cc < kNC; ++cc) c.ka[tt][cc] = ld_raw8<F8, NT>(k_cache, kp + cc * 512);
-  }
-  int vt = t0 + 8 * g;
-  vt = min(vt, (kv_len - 1) & ~7);
-  const int vblk = bt[vt / BS];
-  const int voff = vt % BS;
-  const size_t vp = ((size_t)vblk * Hkv + kvh) * kD * BS + (voff >> 3) * kD * 8 + r * 8;
-#pragma unroll
-  for (int n = 0; n < kND; ++n) c.vb[n] = ld_raw8<F8, NT>(v_cache, vp + 16 * n * 8);
-}
-
 // Decode form: the chunk's cache block id is given (one wave-uniform value: chunks are
 // 32-token aligned and BS is a multiple of 32, so a chunk never spans two blocks).  The
 // decode loop keeps its block ids in a VGPR (lane j = the block of the wave's j-th chunk,
@@ -184,17 +152,6 @@ __device__ __forceinline__ void compute_chunk(WaveState& st, const bf16x8 (&qb)[
   }
 }
 
-template <bool MASK, bool NT = false, bool F8 = false>
-__device__ __forceinline__ void attn_chunk(WaveState& st, const bf16x8 (&qb)[kNC],
-                                           const void* __restrict__ k_cache,
-                                           const void* __restrict__ v_cache,
-                                           const int* __restrict__ bt, int kv_len, int kvh,
-                                           int Hkv, int BS, int t0, int limit, float scale_log2) {
-  ChunkT<F8> c;
-  load_chunk<NT, F8>(c, k_cache, v_cache, bt, kv_len, kvh, Hkv, BS, t0);
-  compute_chunk<MASK>(st, qb, c, t0, limit, scale_log2);
-}
-
 // V tail: lanes whose 8-token V group is the sequence's last group (first token gstart;
 // lanes past it were clamped onto it by load_chunk) take their V^T fragments from the LDS
 // group image instead of the cache.
@@ -245,62 +202,6 @@ __device__ __forceinline__ void load_q(bf16x8 (&qb)[kNC], const bf16* qrow_ptr, 
 }
 
 // ----------------------------------------------------------------------------------
-// Prefill / chunked-prefill / prefix-cached attention.
-// grid.x = q tiles (64 flattened rows each: 4 waves x 16), grid.y = kv heads.
-// ----------------------------------------------------------------------------------
-template <bool F8>
-__global__ __launch_bounds__(256) void paged_attn_prefill_kernel(AttnParams p) {
-  const int tile = blockIdx.x;
-  const int kvh = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int seq = p.tile_seq[tile];
-  const int q0 = p.q_start[seq];
-  const int q_len = p.q_start[seq + 1] - q0;
-  const int kv_len = p.seq_lens[seq];
-  const int G = p.G;
-  const int row = p.tile_row[tile] + 16 * w + (lane & 15);
-  const int pos = row / G;
-  const int hig = row % G;
-  const bool valid = pos < q_len;
-  const int limit = valid ? (kv_len - q_len + pos) : -1;
-  const bf16* qptr = p.q + ((size_t)(q0 + pos) * p.Hq + kvh * G + hig) * kD;
-  bf16x8 qb[kNC];
-  load_q(qb, qptr, valid);
-  const int wave_limit = (int)wave_max((float)limit);
-  const int wave_min = -(int)wave_max((float)(valid ? -limit : -(1 << 30)));
-  const int* bt = p.block_tables + (size_t)seq * p.bt_stride;
-  WaveState st;
-  wave_state_init(st);
-  if (wave_limit >= 0) {
-    int t0 = 0;
-    // chunks fully inside every row's causal window need no mask
-    for (; t0 + 31 <= wave_min; t0 += 32)
-      attn_chunk<false, false, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0,
-                                   limit,
-                        p.scale_log2);
-    for (; t0 <= wave_limit; t0 += 32)
-      attn_chunk<true, false, F8>(st, qb, p.k_cache, p.v_cache, bt, kv_len, kvh, p.Hkv, p.BS, t0,
-                                  limit,
-                       p.scale_log2);
-  }
-  float l = st.l;
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  if (!valid) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  bf16* op = p.out + ((size_t)(q0 + pos) * p.Hq + kvh * G + hig) * kD;
-  const int g = lane >> 4;
-#pragma unroll
-  for (int n = 0; n < kND; ++n) {
-    bf16x4 o4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o4[i] = f2bf(st.o[n][i] * inv);
-    *reinterpret_cast<bf16x4*>(op + 16 * n + 4 * g) = o4;
-  }
-}
-
-// ----------------------------------------------------------------------------------
 // Decode: one new token per sequence, rows = the G q-heads of one kv head.
 // grid = (num_seqs, Hkv, num_parts); 4 waves split the partition's chunks.
 // ----------------------------------------------------------------------------------
@@ -315,111 +216,6 @@ __device__ __forceinline__ void group_units(const bf16x8 (&rows)[8], bf16x8 (&u)
   for (int k = 0; k < 8; ++k)
 #pragma unroll
     for (int i = 0; i < 8; ++i) u[k][i] = rows[i][k];
-}
-
-template <bool F8>
-__device__ __forceinline__ void fused_qkv_prologue(const AttnParams& p, int seq, int kvh,
-                                                   bool write_kv, bf16* q_s, int tsl,
-                                                   bf16* v_img) {
-  const int G = p.G;
-  const int rr = threadIdx.x >> 4;
-  const int j = threadIdx.x & 15;
-  if (rr < G + 2) {
-    int head;
-    if (rr < G) head = kvh * G + rr;
-    else if (rr == G) head = p.Hq + kvh;
-    else head = p.Hq + p.Hkv + kvh;
-    const bf16x8 raw =
-        *reinterpret_cast<const bf16x8*>(p.qkv + (size_t)seq * p.qkv_stride + head * kD + 8 * j);
-    float x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = bf2f(raw[i]);
-    if (rr <= G) {
-      const bf16* nw = rr < G ? p.q_w : p.k_w;
-      if (nw != nullptr) {
-        float ss = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ss += x[i] * x[i];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
-        const float inv = rsqrtf(ss / (float)kD + p.eps);
-        const bf16x8 w8 = *reinterpret_cast<const bf16x8*>(nw + 8 * j);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = bf2f(f2bf(x[i] * inv * bf2f(w8[i])));
-      }
-      const float* cs = p.cos_sin + (size_t)p.positions[seq] * kD;
-      const int i0 = 8 * (j & 7);
-      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + i0);
-      const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + i0 + 4);
-      const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + 64 + i0);
-      const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + 64 + i0 + 4);
-      const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-      const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float other = __shfl_xor(x[i], 8, 16);
-        x[i] = j < 8 ? x[i] * cv[i] - other * sv[i] : x[i] * cv[i] + other * sv[i];
-      }
-    }
-    bf16x8 o8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o8[i] = f2bf(x[i]);
-    if (rr < G) {
-      *reinterpret_cast<bf16x8*>(q_s + rr * kD + 8 * j) = o8;
-    } else if (write_kv) {
-      const int64_t slot = p.slots[seq];
-      if (slot >= 0) {
-        const int64_t blk = slot / p.BS;
-        const int off = (int)(slot % p.BS);
-        if (rr == G) {
-          const size_t e = ((size_t)blk * p.Hkv + kvh) * p.BS * kD + k_swz_offset(off) +
-                           k_dim_offset(8 * j);
-          if constexpr (F8) {
-            uint32_t* dst = reinterpret_cast<uint32_t*>((uint8_t*)p.k_cache + e);
-            dst[0] = f32x4_to_fp8x4((float)o8[0], (float)o8[1], (float)o8[2], (float)o8[3]);
-            dst[1] = f32x4_to_fp8x4((float)o8[4], (float)o8[5], (float)o8[6], (float)o8[7]);
-          } else {
-            *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
-          }
-        } else if (tsl >= 0) {
-          // V tail: the group's earlier tokens come from the tail, this token from registers;
-          // the group image goes to LDS (the attention below reads the group from there), and
-          // either the tail gets this token's row (one 256-B row per token-head) or, when the
-          // token completes the group, the cache gets the whole [D][8] group (full lines)
-          const int i0 = off & 7;
-          bf16* tb = p.v_tail + ((size_t)tsl * p.Hkv + kvh) * 8 * kD + 8 * j;
-          bf16x8 rows[8], u[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (i < i0) rows[i] = *reinterpret_cast<const bf16x8*>(tb + (size_t)i * kD);
-            else rows[i] = i == i0 ? o8 : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-          }
-          group_units(rows, u);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(v_img + (8 * j + k) * 8) = u[k];
-          if (i0 == 7) {
-            bf16* e = (bf16*)p.v_cache + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
-                      (off >> 3) * kD * 8 + (size_t)(8 * j) * 8;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(e + 8 * k) = u[k];
-          } else {
-            *reinterpret_cast<bf16x8*>(tb + (size_t)i0 * kD) = o8;
-          }
-        } else {
-          const size_t e = ((size_t)blk * p.Hkv + kvh) * kD * p.BS + (off >> 3) * kD * 8 + (off & 7);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if constexpr (F8)
-              ((uint8_t*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = f32_to_fp8((float)o8[i]);
-            else
-              ((bf16*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = o8[i];
-          }
-        }
-      }
-    }
-  }
-  // q rows visible in LDS and the new K/V visible to every wave of this workgroup
-  __syncthreads();
 }
 
 // Fused-prologue operands loaded up front (grid decode kernel).  Every prologue load is
@@ -572,254 +368,52 @@ __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int 
   }
 }
 
-// Barrier-free fused prologue (grid decode kernel, flags bit 9): every wave computes the q
-// fragments it feeds to the MFMAs itself, straight in the S^T = K . Q^T operand layout (lane
-// = 16 g + row: dims 32 c + 8 g .. + 7 for c = 0..3, so the RoPE partner d + 64 is the same
-// lane's c + 2 and the RMSNorm sum is a 4-lane reduce), and only the wave that owns the new
-// token's 32-token chunk writes its K/V (and builds the V-tail image that only that wave
-// reads).  With the workgroup-wide prologue (q through LDS), three of the four waves waited
-// at a barrier for wave 0's serial norm/RoPE/KV-write chain at the start of every item.
-// Measured: no faster (fused micro 113.7 vs 114.6 us, headline bench 50.7k vs 51.1k with the
-// workgroup prologue, profiles/r3_attn_rework_ab.log) -- the fused kernel's extra time over a
-// ready q is the new token's K/V line writes under the read stream, not the prologue chain --
-// so the workgroup prologue stays the default and this form is kept as an A/B variant.
-struct QPre {
-  bf16x8 raw[kNC], w[kNC];
-  f32x4 cs[2][4];  // [c = 0, 1][cos lo, cos hi, sin lo, sin hi] at dims 32 c + 8 g .. + 7
-};
+// Decode K/V chunks stream with non-temporal loads (read once per step; keeping them out of
+// the caches leaves the L2 / MALL to the block tables, q rows and weights)
+constexpr bool kDecodeNT = true;
 
-__device__ __forceinline__ void q_frag_loads(const AttnParams& p, int seq, int kvh, int64_t pos,
-                                             QPre& qp) {
-  const int lane = threadIdx.x & 63;
-  const int qr = lane & 15, g = lane >> 4;
-  const int head = kvh * p.G + min(qr, p.G - 1);  // rows past G re-read row G-1 (never used)
-  const bf16* src = p.qkv + (size_t)seq * p.qkv_stride + head * kD + 8 * g;
-  const bf16* wsrc = (p.q_w != nullptr ? p.q_w : src - head * kD) + 8 * g;
-  const float* cs = p.cos_sin + (size_t)pos * kD + 8 * g;
-#pragma unroll
-  for (int c = 0; c < kNC; ++c) {
-    qp.raw[c] = *reinterpret_cast<const bf16x8*>(src + 32 * c);
-    qp.w[c] = *reinterpret_cast<const bf16x8*>(wsrc + 32 * c);
-  }
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    qp.cs[c][0] = *reinterpret_cast<const f32x4*>(cs + 32 * c);
-    qp.cs[c][1] = *reinterpret_cast<const f32x4*>(cs + 32 * c + 4);
-    qp.cs[c][2] = *reinterpret_cast<const f32x4*>(cs + 64 + 32 * c);
-    qp.cs[c][3] = *reinterpret_cast<const f32x4*>(cs + 64 + 32 * c + 4);
-  }
-}
-
-// q fragments of this lane (zeros for rows >= G): bf16(RMSNorm) -> NeoX RoPE in fp32 -> bf16,
-// the same arithmetic and rounding as fused_qkv_prologue
-__device__ __forceinline__ void q_frag_compute(const AttnParams& p, const QPre& qp,
-                                               bf16x8 (&qb)[kNC], bool valid) {
-  float x[kNC][8];
-#pragma unroll
-  for (int c = 0; c < kNC; ++c)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[c][i] = bf2f(qp.raw[c][i]);
-  if (p.q_w != nullptr) {
-    float ss = 0.f;
-#pragma unroll
-    for (int c = 0; c < kNC; ++c)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ss += x[c][i] * x[c][i];
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    const float inv = rsqrtf(ss / (float)kD + p.eps);
-#pragma unroll
-    for (int c = 0; c < kNC; ++c)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) x[c][i] = bf2f(f2bf(x[c][i] * inv * bf2f(qp.w[c][i])));
-  }
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float cv = i < 4 ? qp.cs[c][0][i] : qp.cs[c][1][i - 4];
-      const float sv = i < 4 ? qp.cs[c][2][i] : qp.cs[c][3][i - 4];
-      const float lo = x[c][i], hi = x[c + 2][i];
-      x[c][i] = lo * cv - hi * sv;
-      x[c + 2][i] = hi * cv + lo * sv;
-    }
-#pragma unroll
-  for (int c = 0; c < kNC; ++c)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) qb[c][i] = valid ? f2bf(x[c][i]) : (bf16)0.f;
-}
-
-// The new token's K (lanes 0-15) and V (lanes 16-31) of this kv head, by ONE wave: loads, K
-// norm + RoPE, cache / V-tail writes; the V-tail group image goes to this wave's LDS v_img.
-// Ends with the wave's stores drained (its later loads of those lines then see them).
-template <bool F8>
-__device__ __forceinline__ void kv_write_wave(const AttnParams& p, int seq, int kvh, int64_t slot,
-                                              int64_t pos, int tsl, bool tail, bf16* v_img) {
-  const int lane = threadIdx.x & 63;
-  if (lane < 32 && slot >= 0) {
-    const int j = lane & 15;
-    const bool is_k = lane < 16;
-    const int head = is_k ? p.Hq + kvh : p.Hq + p.Hkv + kvh;
-    const bf16x8 raw =
-        *reinterpret_cast<const bf16x8*>(p.qkv + (size_t)seq * p.qkv_stride + head * kD + 8 * j);
-    float x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = bf2f(raw[i]);
-    const int64_t blk = slot / p.BS;
-    const int off = (int)(slot % p.BS);
-    if (is_k) {
-      if (p.k_w != nullptr) {
-        float ss = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ss += x[i] * x[i];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
-        const float inv = rsqrtf(ss / (float)kD + p.eps);
-        const bf16x8 w8 = *reinterpret_cast<const bf16x8*>(p.k_w + 8 * j);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = bf2f(f2bf(x[i] * inv * bf2f(w8[i])));
-      }
-      const float* cs = p.cos_sin + (size_t)pos * kD;
-      const int i0 = 8 * (j & 7);
-      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + i0);
-      const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + i0 + 4);
-      const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + 64 + i0);
-      const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + 64 + i0 + 4);
-      const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-      const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float other = __shfl_xor(x[i], 8, 16);
-        x[i] = j < 8 ? x[i] * cv[i] - other * sv[i] : x[i] * cv[i] + other * sv[i];
-      }
-    }
-    bf16x8 o8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o8[i] = f2bf(x[i]);
-    if (is_k) {
-      const size_t e =
-          ((size_t)blk * p.Hkv + kvh) * p.BS * kD + k_swz_offset(off) + k_dim_offset(8 * j);
-      if constexpr (F8) {
-        uint32_t* dst = reinterpret_cast<uint32_t*>((uint8_t*)p.k_cache + e);
-        dst[0] = f32x4_to_fp8x4((float)o8[0], (float)o8[1], (float)o8[2], (float)o8[3]);
-        dst[1] = f32x4_to_fp8x4((float)o8[4], (float)o8[5], (float)o8[6], (float)o8[7]);
-      } else {
-        *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
-      }
-    } else if (tail) {
-      const int i0 = off & 7;
-      bf16* tb = p.v_tail + ((size_t)tsl * p.Hkv + kvh) * 8 * kD + 8 * j;
-      bf16x8 rows[8], u[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)  // whole group loaded, then selected (no per-row branch)
-        rows[i] = *reinterpret_cast<const bf16x8*>(tb + (size_t)i * kD);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (i >= i0) rows[i] = i == i0 ? o8 : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      group_units(rows, u);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(v_img + (8 * j + k) * 8) = u[k];
-      if (i0 == 7) {
-        bf16* e = (bf16*)p.v_cache + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
-                  (off >> 3) * kD * 8 + (size_t)(8 * j) * 8;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(e + 8 * k) = u[k];
-      } else {
-        *reinterpret_cast<bf16x8*>(tb + (size_t)i0 * kD) = o8;
-      }
-    } else {
-      const size_t e = ((size_t)blk * p.Hkv + kvh) * kD * p.BS + (off >> 3) * kD * 8 + (off & 7);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if constexpr (F8)
-          ((uint8_t*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = f32_to_fp8((float)o8[i]);
-        else
-          ((bf16*)p.v_cache)[e + (size_t)(8 * j + i) * 8] = o8[i];
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-}
-
-struct QHead {
-  QPre qp;
-  int64_t pos, slot;
-  int tsl;
-};
-
-// What a decode work item needs before its first K/V byte can be requested: the sequence's
-// length, the cache block ids of the wave's chunks (lane j: chunk pstart + 32 w + 128 j, read
-// later with readlane: an SGPR, no memory instruction in the chunk loop) and, with PREFETCH,
-// the wave's first chunk in flight.  The block-id load does not wait for the length (the
-// index is clamped into the block-table row instead of guarded by it), so the chain before
-// the first K/V load is two round trips.  The persistent pipelined kernel fetches the NEXT
-// item's head while the current item finishes (combine, output store, next prologue).
-template <bool F8>
-struct ItemHead {
-  int seq, kvh, part, kv_len, btr;
-  ChunkT<F8> cur;
-};
-
-// PRE: 0 = nothing else, 1 = the workgroup prologue's operands (ProPre), 2 = the barrier-free
-// prologue's q operands + the new token's position / slot / tail slot (QHead)
-template <bool PREFETCH, bool NT, bool F8, int PRE = 0>
-__device__ __forceinline__ void item_head(const AttnParams& p, ItemHead<F8>& h, int seq, int kvh,
-                                          int part, ProPre<F8>* pp = nullptr,
-                                          QHead* qh = nullptr) {
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  h.seq = seq;
-  h.kvh = kvh;
-  h.part = part;
-  const int pstart = part * p.part_size;
-  const int t0 = pstart + 32 * w;
-  const int bi = min((t0 + 128 * lane) / p.BS, p.bt_stride - 1);
-  h.btr = p.block_tables[(size_t)seq * p.bt_stride + bi];
-  h.kv_len = p.seq_lens[seq];
-  if constexpr (PRE == 1) {  // fused-prologue operands: issued ahead of the chunk (see ProPre)
-    const int64_t pos = p.positions[seq];
-    pp->slot = p.slots[seq];
-    pp->tsl = (!F8 && p.v_tail != nullptr) ? p.tail_slot[seq] : -1;
-    prologue_loads<F8>(p, seq, kvh, pos, *pp);
-    __builtin_amdgcn_sched_barrier(0);
-  } else if constexpr (PRE == 2) {  // q operands ahead of the chunk (see QPre)
-    qh->pos = p.positions[seq];
-    qh->slot = p.slots[seq];
-    qh->tsl = (!F8 && p.v_tail != nullptr) ? p.tail_slot[seq] : -1;
-    q_frag_loads(p, seq, kvh, qh->pos, qh->qp);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  const int pend = min(h.kv_len, pstart + p.part_size);
-  if constexpr (PREFETCH) {
-    // issued unconditionally (a wave with no chunk reads block 0, never used): a branch here
-    // left the two paths with different load counts, and hipcc's merged vmcnt count then
-    // waited on part of the chunk inside the prologue
-    const bool has = t0 < pend;
-    load_chunk_blk<NT, F8>(h.cur, p.k_cache, p.v_cache,
-                           has ? __builtin_amdgcn_readlane(h.btr, 0) : 0, max(h.kv_len, 1), kvh,
-                           p.Hkv, p.BS, has ? t0 : 0);
-  }
-}
-
-// One (seq, kv head, partition) work item whose head item_head() has fetched.  after_loop()
-// runs once the chunk loop is done (h.cur / h.btr are dead then: the pipelined kernel fetches
-// the next item's head into h there), before the LDS combine.  Callers that run several
-// items per workgroup must __syncthreads() before the next item's LDS writes.
-template <bool PREFETCH, bool NT, bool FUSED, bool F8, int PRE = 0, typename AfterLoop>
-__device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>& h,
-                                              float* dyn_lds, AfterLoop after_loop,
-                                              const ProPre<F8>* pp = nullptr,
-                                              const QHead* qh = nullptr) {
+// One (seq, kv head, partition) work item of the decode grid.
+//  head: what the item needs before its first K/V byte can be requested -- the sequence's
+//    length, the cache block ids of the wave's chunks (lane j: chunk pstart + 32 w + 128 j,
+//    read later with readlane: an SGPR, no memory instruction in the chunk loop), in the
+//    fused form the prologue's operands (ProPre, issued ahead of the chunk), then the wave's
+//    first chunk in flight.  The block-id load does not wait for the length (the index is
+//    clamped into the block-table row instead of guarded by it), so the chain before the
+//    first K/V load is two round trips.
+//  body: fused q/k-norm + RoPE + new-token K/V write (FUSED), the chunk loop over two named
+//    register sets, the 4-wave LDS combine, the output (or split-KV partial) store.
+template <bool FUSED, bool F8>
+__device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
+                                            float* dyn_lds) {
+  constexpr bool NT = kDecodeNT;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int g = lane >> 4;
   const int G = p.G;
-  const int seq = h.seq, kvh = h.kvh, part = h.part;
-  const int kv_len = h.kv_len;
-  const int btr = h.btr;
-  ChunkT<F8>& cur = h.cur;
   const int pstart = part * p.part_size;
+  int t0 = pstart + 32 * w;
+  const int tw = t0;  // the wave's first chunk (t0 itself advances in the loop below)
+  const int btr =
+      p.block_tables[(size_t)seq * p.bt_stride + min((t0 + 128 * lane) / p.BS, p.bt_stride - 1)];
+  const int kv_len = p.seq_lens[seq];
+  ProPre<F8> pp;
+  if constexpr (FUSED) {  // fused-prologue operands: issued ahead of the chunk (see ProPre)
+    const int64_t pos = p.positions[seq];
+    pp.slot = p.slots[seq];
+    pp.tsl = (!F8 && p.v_tail != nullptr) ? p.tail_slot[seq] : -1;
+    prologue_loads<F8>(p, seq, kvh, pos, pp);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   const int pend = min(kv_len, pstart + p.part_size);
+  ChunkT<F8> cur;
+  {
+    // issued unconditionally (a wave with no chunk reads block 0, never used): a branch here
+    // left the two paths with different load counts, and hipcc's merged vmcnt count then
+    // waited on part of the chunk inside the prologue
+    const bool has = t0 < pend;
+    load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, has ? __builtin_amdgcn_readlane(btr, 0) : 0,
+                           max(kv_len, 1), kvh, p.Hkv, p.BS, has ? t0 : 0);
+  }
   const int qr = lane & 15;
   const bool valid = qr < G && kv_len > 0;
   const int q_tok = p.q_start ? p.q_start[seq] : seq;
@@ -841,41 +435,21 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
   // plain: a still-partial group straight from the tail (the writer kernel put it there)
   int tsl;
   bool use_img;
-  if constexpr (PRE == 1) {
-    tsl = kv_len > 0 ? pp->tsl : -1;
-    use_img = tsl >= 0 && writes_kv && pp->slot >= 0;
-  } else if constexpr (PRE == 2) {
-    tsl = kv_len > 0 ? qh->tsl : -1;
-    use_img = tsl >= 0 && writes_kv && qh->slot >= 0;
+  if constexpr (FUSED) {
+    tsl = kv_len > 0 ? pp.tsl : -1;
+    use_img = tsl >= 0 && writes_kv && pp.slot >= 0;
   } else {
     tsl = (!F8 && p.v_tail != nullptr && kv_len > 0) ? p.tail_slot[seq] : -1;
-    use_img = tsl >= 0 && writes_kv && (FUSED ? p.slots[seq] >= 0 : (kv_len & 7) != 0);
+    use_img = tsl >= 0 && writes_kv && (kv_len & 7) != 0;
   }
   const int gstart = (kv_len - 1) & ~7;
-  int t0 = pstart + 32 * w;
-  const int tw = t0;  // the wave's first chunk (t0 itself advances in the loop below)
   // j < 64 always: the host caps part_size at kDecodeMaxPart (64 chunks per wave)
   auto blk_of = [=](int tc) -> int { return __builtin_amdgcn_readlane(btr, (tc - tw) >> 7); };
-  bf16x8 qpre[kNC];
-  if constexpr (FUSED && PRE == 2) {
-    q_frag_compute(p, qh->qp, qpre, valid);
-    // the wave owning the new token's chunk writes its K/V (and the V-tail image it alone
-    // reads); if that chunk is the wave's prefetched first one, it is re-read after the write
-    if (writes_kv && (((kv_len - 1 - pstart) >> 5) & 3) == w) {
-      kv_write_wave<F8>(p, seq, kvh, qh->slot, qh->pos, tsl, use_img, v_img);
-      if (PREFETCH && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
-        load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS,
-                               t0);
-    }
-  } else if constexpr (FUSED) {
-    if constexpr (PRE == 1)
-      fused_qkv_prologue_pre<F8>(p, kvh, writes_kv, q_s, use_img, v_img, *pp, k_img);
-    else
-      fused_qkv_prologue<F8>(p, seq, kvh, writes_kv, q_s, use_img ? tsl : -1, v_img);
+  if constexpr (FUSED) {
+    fused_qkv_prologue_pre<F8>(p, kvh, writes_kv, q_s, use_img, v_img, pp, k_img);
     // the chunk holding the token the prologue just wrote is re-read after the barrier (on
-    // the PRE == 1 tail path the loop patches it from the LDS images instead)
-    if (PREFETCH && writes_kv && !(PRE == 1 && use_img) && t0 < pend && t0 <= kv_len - 1 &&
-        kv_len - 1 < t0 + 32)
+    // the V-tail path the loop patches it from the LDS images instead)
+    if (writes_kv && !use_img && t0 < pend && t0 <= kv_len - 1 && kv_len - 1 < t0 + 32)
       load_chunk_blk<NT, F8>(cur, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS,
                              t0);
   } else if (use_img) {  // uniform per workgroup
@@ -898,10 +472,7 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
   wave_state_init(st);
   if (pstart < pend) {
     bf16x8 qb[kNC];
-    if constexpr (FUSED && PRE == 2) {
-#pragma unroll
-      for (int c = 0; c < kNC; ++c) qb[c] = qpre[c];
-    } else if constexpr (FUSED) {
+    if constexpr (FUSED) {
 #pragma unroll
       for (int c = 0; c < kNC; ++c)
         qb[c] = valid ? *reinterpret_cast<const bf16x8*>(q_s + qr * kD + 32 * c + 8 * g)
@@ -909,52 +480,39 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
     } else {
       load_q(qb, qptr, valid);
     }
-    if constexpr (PREFETCH) {
-      // Register double buffer as two NAMED chunk sets that alternate (the loop is unrolled
-      // by two), never copied: with `cur = nxt` hipcc moved the registers at the end of each
-      // iteration behind an `s_waitcnt vmcnt(0)`, so chunk i+2 could only be requested once
-      // chunk i+1 had landed (one chunk in flight per wave).  Here chunk i+2's loads go into
-      // the set chunk i just released while chunk i+1 may still be in flight, and each
-      // compute waits only for its own set (counted vmcnt).  Loads are issued on every step:
-      // past the last chunk every lane re-reads block 0's first rows (a few cache-resident
-      // lines, never used) -- an `if (more)` around them made hipcc's merged vmcnt count
-      // assume the no-load path and wait for the other set as well.
-      ChunkT<F8> nb;
-      auto fetch = [&](ChunkT<F8>& c, int tc) {
-        const bool has = tc < pend;
-        load_chunk_blk<NT, F8>(c, p.k_cache, p.v_cache, has ? blk_of(tc) : 0, has ? kv_len : 1,
-                               kvh, p.Hkv, p.BS, has ? tc : 0);
-      };
-      auto consume = [&](ChunkT<F8>& c, int tc) {
-        if (use_img && tc <= gstart && gstart < tc + 32) {
-          patch_v(c, tc, gstart, v_img);
-          if constexpr (FUSED && PRE == 1) patch_k(c, tc, kv_len - 1, k_img);
-        }
-        if (tc + 31 < kv_len)
-          compute_chunk<false>(st, qb, c, tc, limit, p.scale_log2);
-        else
-          compute_chunk<true>(st, qb, c, tc, limit, p.scale_log2);
-      };
-      for (; t0 < pend; t0 += 256) {
-        fetch(nb, t0 + 128);
-        consume(cur, t0);
-        if (t0 + 128 >= pend) break;
-        fetch(cur, t0 + 256);
-        consume(nb, t0 + 128);
+    // Register double buffer as two NAMED chunk sets that alternate (the loop is unrolled by
+    // two), never copied: with `cur = nxt` hipcc moved the registers at the end of each
+    // iteration behind an `s_waitcnt vmcnt(0)`, so chunk i+2 could only be requested once
+    // chunk i+1 had landed (one chunk in flight per wave).  Here chunk i+2's loads go into the
+    // set chunk i just released while chunk i+1 may still be in flight, and each compute waits
+    // only for its own set (counted vmcnt).  Loads are issued on every step: past the last
+    // chunk every lane re-reads block 0's first rows (a few cache-resident lines, never used)
+    // -- an `if (more)` around them made hipcc's merged vmcnt count assume the no-load path
+    // and wait for the other set as well.
+    ChunkT<F8> nb;
+    auto fetch = [&](ChunkT<F8>& c, int tc) {
+      const bool has = tc < pend;
+      load_chunk_blk<NT, F8>(c, p.k_cache, p.v_cache, has ? blk_of(tc) : 0, has ? kv_len : 1,
+                             kvh, p.Hkv, p.BS, has ? tc : 0);
+    };
+    auto consume = [&](ChunkT<F8>& c, int tc) {
+      if (use_img && tc <= gstart && gstart < tc + 32) {
+        patch_v(c, tc, gstart, v_img);
+        if constexpr (FUSED) patch_k(c, tc, kv_len - 1, k_img);
       }
-    } else {
-      for (; t0 < pend; t0 += 128) {
-        ChunkT<F8> c;
-        load_chunk_blk<NT, F8>(c, p.k_cache, p.v_cache, blk_of(t0), kv_len, kvh, p.Hkv, p.BS, t0);
-        if (use_img && t0 <= gstart && gstart < t0 + 32) patch_v(c, t0, gstart, v_img);
-        if (t0 + 31 < kv_len)
-          compute_chunk<false>(st, qb, c, t0, limit, p.scale_log2);
-        else
-          compute_chunk<true>(st, qb, c, t0, limit, p.scale_log2);
-      }
+      if (tc + 31 < kv_len)
+        compute_chunk<false>(st, qb, c, tc, limit, p.scale_log2);
+      else
+        compute_chunk<true>(st, qb, c, tc, limit, p.scale_log2);
+    };
+    for (; t0 < pend; t0 += 256) {
+      fetch(nb, t0 + 128);
+      consume(cur, t0);
+      if (t0 + 128 >= pend) break;
+      fetch(cur, t0 + 256);
+      consume(nb, t0 + 128);
     }
   }
-  after_loop();
   float l = st.l;
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -1006,85 +564,13 @@ __device__ __forceinline__ void decode_item_h(const AttnParams& p, ItemHead<F8>&
 #undef OS
 }
 
-template <bool PREFETCH, bool NT = false, bool FUSED = false, bool F8 = false>
-__device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kvh, int part,
-                                            float* dyn_lds) {
-  ItemHead<F8> h;
-  if constexpr (FUSED && PREFETCH) {
-    if (p.flags & 512) {  // bit 9: the barrier-free prologue (A/B; measured no faster)
-      QHead qh;
-      item_head<PREFETCH, NT, F8, 2>(p, h, seq, kvh, part, nullptr, &qh);
-      decode_item_h<PREFETCH, NT, FUSED, F8, 2>(p, h, dyn_lds, [] {}, nullptr, &qh);
-    } else {  // default: workgroup prologue on operands loaded ahead of the first chunk
-      ProPre<F8> pp;
-      item_head<PREFETCH, NT, F8, 1>(p, h, seq, kvh, part, &pp);
-      decode_item_h<PREFETCH, NT, FUSED, F8, 1>(p, h, dyn_lds, [] {}, &pp);
-    }
-  } else {
-    item_head<PREFETCH, NT, F8>(p, h, seq, kvh, part);
-    decode_item_h<PREFETCH, NT, FUSED, F8>(p, h, dyn_lds, [] {});
-  }
-}
-
-// grid = (num_seqs, Hkv, num_parts): one work item per workgroup.
-template <bool PREFETCH, int MINW, bool NT = false, bool FUSED = false, bool F8 = false>
-__global__ __launch_bounds__(256, MINW) void paged_attn_decode_kernel(AttnParams p) {
+// grid = (num_seqs, Hkv, num_parts): one work item per workgroup.  (Persistent, pipelined
+// persistent, single-buffered 3-WG/CU and barrier-free-prologue forms were measured equal or
+// slower and removed: profiles/r3_attn_rework_ab.log, r3_attn_variants_ab.log.)
+template <bool FUSED, bool F8>
+__global__ __launch_bounds__(256, 1) void paged_attn_decode_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
-  decode_item<PREFETCH, NT, FUSED, F8>(p, blockIdx.x, blockIdx.y, blockIdx.z, dyn_lds);
-}
-
-// Persistent variant: a fixed grid (a few workgroups per CU) strides over all work items
-// (kv head fastest, so consecutive items of a workgroup share the sequence's block table
-// and q row in cache).  Bounded loop: every workgroup exits after its last item.
-template <bool PREFETCH, bool NT, bool FUSED = false>
-__global__ __launch_bounds__(256, 2) void paged_attn_decode_persistent_kernel(AttnParams p,
-                                                                              int num_seqs) {
-  extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
-  const int items = num_seqs * p.Hkv * p.num_parts;
-  for (int it = blockIdx.x; it < items; it += gridDim.x) {
-    const int part = it % p.num_parts;
-    const int sk = it / p.num_parts;
-    decode_item<PREFETCH, NT, FUSED>(p, sk / p.Hkv, sk % p.Hkv, part, dyn_lds);
-    __syncthreads();  // LDS combine buffer is reused by the next item
-  }
-}
-
-// Persistent PIPELINED variant (fused, prefetching): the next item's head -- its length,
-// block ids and first K/V chunk -- is requested as soon as the current item's chunk loop is
-// done, so its round trips overlap the current item's combine, output store and the next
-// item's q/k prologue instead of opening each item with an idle CU slot.  Every workgroup
-// runs a bounded number of items (it += gridDim.x) and exits.
-template <bool NT>
-__global__ __launch_bounds__(256, 2) void paged_attn_decode_pipelined_kernel(AttnParams p,
-                                                                             int num_seqs) {
-  extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
-  const int items = num_seqs * p.Hkv * p.num_parts;
-  auto coords = [&](int it, int& seq, int& kvh, int& part) {
-    part = it % p.num_parts;
-    const int sk = it / p.num_parts;
-    seq = sk / p.Hkv;
-    kvh = sk % p.Hkv;
-  };
-  ItemHead<false> h;
-  int it = blockIdx.x;
-  if (it >= items) return;
-  {
-    int seq, kvh, part;
-    coords(it, seq, kvh, part);
-    item_head<true, NT, false>(p, h, seq, kvh, part);
-  }
-  while (it < items) {
-    const int nx = it + gridDim.x;
-    decode_item_h<true, NT, true, false>(p, h, dyn_lds, [&] {
-      if (nx < items) {
-        int seq, kvh, part;
-        coords(nx, seq, kvh, part);
-        item_head<true, NT, false>(p, h, seq, kvh, part);
-      }
-    });
-    __syncthreads();  // LDS combine buffer is reused by the next item
-    it = nx;
-  }
+  decode_item<FUSED, F8>(p, blockIdx.x, blockIdx.y, blockIdx.z, dyn_lds);
 }
 
 
@@ -1308,11 +794,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
         blk_next = blk_of(t + 2);
       }
     } else {
-      // timing experiments (wrong numerics): flags 256 = no K/V reloads, 512 = no compute
-      if (more && !(p.flags & 256)) stage_load(t + 1);
+      if (more) stage_load(t + 1);
     }
     const int key0 = t * kFaKeys;
-    if (wave_active && key0 <= w_limit && !(p.flags & 512)) {
+    if (wave_active && key0 <= w_limit) {
       const bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
       const bf16* vl = kl + kFaKeys * kD;
       // S^T = K . Q^T for the two 32-key sub-tiles (interleaved: independent chains)
@@ -1478,28 +963,12 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows
                                hipStream_t s) {
   if (num_tiles == 0) return;
   const dim3 grid(num_tiles, p.Hkv);
-  if (tile_rows == 2 * kFaRows && !p.kv_fp8) {
+  if (tile_rows == 2 * kFaRows && !p.kv_fp8)  // 256 rows, 8 waves (bf16 caches)
     paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(p);
-  } else if (tile_rows == kFaRows) {
-    // bf16 caches: LDS-DMA staging (flags bit 10 selects the register-staged form for A/B)
-    if (p.kv_fp8) paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
-    else if (p.flags & 1024) paged_attn_prefill_fa_kernel<false, false><<<grid, 256, 0, s>>>(p);
-    else paged_attn_prefill_fa_kernel<false, true><<<grid, 256, 0, s>>>(p);
-  } else {
-    if (p.kv_fp8) paged_attn_prefill_kernel<true><<<grid, 256, 0, s>>>(p);
-    else paged_attn_prefill_kernel<false><<<grid, 256, 0, s>>>(p);
-  }
-}
-
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    if (n <= 0) n = 256;
-  }
-  return n;
+  else if (p.kv_fp8)  // fp8 caches: register-staged (widened to bf16 on the way into LDS)
+    paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
+  else  // bf16 caches: LDS-DMA staging
+    paged_attn_prefill_fa_kernel<false, true><<<grid, 256, 0, s>>>(p);
 }
 
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) {
@@ -1508,53 +977,13 @@ void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) 
                       (p.qkv ? (size_t)p.G * kD * sizeof(bf16) : 0) +
                       (p.v_tail ? (size_t)kD * 8 * sizeof(bf16) : 0) +
                       (p.qkv && p.v_tail ? (size_t)kD * sizeof(bf16) : 0);
-  const int per_cu = (p.flags >> 3) & 7;  // flags bits 3..5: persistent, WGs per CU
-  if (p.kv_fp8) {  // fp8 KV cache: prefetching + non-temporal variants only
-    const dim3 grid(num_seqs, p.Hkv, p.num_parts);
-    if (p.qkv != nullptr)
-      paged_attn_decode_kernel<true, 1, true, true, true><<<grid, 256, smem, s>>>(p);
-    else
-      paged_attn_decode_kernel<true, 1, true, false, true><<<grid, 256, smem, s>>>(p);
-  } else if (p.qkv != nullptr && per_cu > 0) {  // fused, persistent grid (grid-capped)
-    const int items = num_seqs * p.Hkv * p.num_parts;
-    const int grid = min(items, num_cus() * per_cu);
-    if (p.flags & 128)  // bit 7: next item's head fetched under the current item's tail
-      paged_attn_decode_pipelined_kernel<true><<<grid, 256, smem, s>>>(p, num_seqs);
-    else
-      paged_attn_decode_persistent_kernel<true, true, true><<<grid, 256, smem, s>>>(p, num_seqs);
-  } else if (p.qkv != nullptr) {  // fused q/k-norm + RoPE + KV write (default flags path)
-    const dim3 grid(num_seqs, p.Hkv, p.num_parts);
-    if (p.flags & 256)  // bit 8: single-buffered chunks at 3 workgroups per CU
-      paged_attn_decode_kernel<false, 3, true, true><<<grid, 256, smem, s>>>(p);
-    else if (p.flags & 1)
-      paged_attn_decode_kernel<true, 1, true, true><<<grid, 256, smem, s>>>(p);
-    else
-      paged_attn_decode_kernel<false, 1, true, true><<<grid, 256, smem, s>>>(p);
-  } else if (per_cu > 0) {
-    const int items = num_seqs * p.Hkv * p.num_parts;
-    const int grid = min(items, num_cus() * per_cu);
-    const bool nt = p.flags & 64;
-    if (p.flags & 1) {
-      if (nt) paged_attn_decode_persistent_kernel<true, true><<<grid, 256, smem, s>>>(p, num_seqs);
-      else paged_attn_decode_persistent_kernel<true, false><<<grid, 256, smem, s>>>(p, num_seqs);
-    } else {
-      if (nt) paged_attn_decode_persistent_kernel<false, true><<<grid, 256, smem, s>>>(p, num_seqs);
-      else paged_attn_decode_persistent_kernel<false, false><<<grid, 256, smem, s>>>(p, num_seqs);
-    }
+  const dim3 grid(num_seqs, p.Hkv, p.num_parts);
+  if (p.kv_fp8) {
+    if (p.qkv != nullptr) paged_attn_decode_kernel<true, true><<<grid, 256, smem, s>>>(p);
+    else paged_attn_decode_kernel<false, true><<<grid, 256, smem, s>>>(p);
   } else {
-    const dim3 grid(num_seqs, p.Hkv, p.num_parts);
-    if ((p.flags & 64) && (p.flags & 1))
-      paged_attn_decode_kernel<true, 1, true><<<grid, 256, smem, s>>>(p);
-    else if (p.flags & 64)
-      paged_attn_decode_kernel<false, 1, true><<<grid, 256, smem, s>>>(p);
-    else if (p.flags & 1)
-      paged_attn_decode_kernel<true, 1><<<grid, 256, smem, s>>>(p);
-    else if (p.flags & 2)
-      paged_attn_decode_kernel<false, 5><<<grid, 256, smem, s>>>(p);
-    else if (p.flags & 4)
-      paged_attn_decode_kernel<false, 6><<<grid, 256, smem, s>>>(p);
-    else
-      paged_attn_decode_kernel<false, 1><<<grid, 256, smem, s>>>(p);
+    if (p.qkv != nullptr) paged_attn_decode_kernel<true, false><<<grid, 256, smem, s>>>(p);
+    else paged_attn_decode_kernel<false, false><<<grid, 256, smem, s>>>(p);
   }
   if (p.num_parts > 1) paged_attn_reduce_kernel<<<dim3(num_seqs, p.Hkv), 256, 0, s>>>(p);
 }

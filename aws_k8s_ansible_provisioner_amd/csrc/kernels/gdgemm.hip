@@ -88,22 +88,12 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-// BKT: k-step depth, 64 or 32.  BKT = 32 halves the slot (the 256 x 128 tile's 48 KB -> 24 KB)
-// so the 144 KB of LDS holds a 6-slot ring with five k-steps in flight instead of two (ns = 6).
-// Measured slower on every M = 256 shape (Llama-3-8B gate_up 89.4 vs 80.2 us, qkv 32.9 vs
-// 28.3: profiles/r3_gemm_m256_deep.log): the 256-row tiles are not bound by the ring's bytes
-// in flight; twice the barriers per K and half the MFMA work between them cost more.  Kept
-// selectable (ns = 6) for A/B, not a tuner candidate.
-// PIPE (BKT = 64): the fragment reads of the next 32-deep half-step are issued before the
-// MFMAs of the current one, and the ring barrier sits between the two halves of a k-step, so
-// a wave's LDS reads overlap its own MFMAs.  Without it a k-step is [barrier, all 16 fragment
-// reads, all 32 MFMAs]: both waves of a SIMD read LDS together, then both run MFMAs together
-// (PMC on Llama-3-8B gate_up, 256-row tile: MFMA busy 43 %, issue stalls 40 % / waitcnt-or-
-// barrier waits 36 % of wave cycles; profiles/r3_gemm_pmc.md).  Measured within 2 % of the plain
-// loop (profiles/r3_gemm_pipe_ab.log): off by default.  With PIPE the prologue fills
-// all NS slots and each mid-step barrier frees the slot just read for step t + NS.
+// BKT: k-step depth (64 in every served variant).  Measured and removed: a 6-slot ring of
+// 32-deep k-steps for the 256-row tiles (five in flight; slower on every M = 256 shape,
+// profiles/r3_gemm_m256_deep.log) and a half-step pipelined K loop (fragment reads of the next
+// half-step under the current MFMAs; within 2 %, profiles/r3_gemm_pipe_ab.log).
 template <int BN, int NS, int EPI, int SPL, int OCC, int S, int GBM = 64, int NW = 4,
-          int BKT = 64, int PIPE = 0>
+          int BKT = 64>
 __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   constexpr int NT = 64 * NW;             // threads
   constexpr int WMW = NW / 2;             // waves along M (2 along N)
@@ -213,47 +203,6 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   // prologue: up to NS-1 k-steps in flight.  At step t the wait below leaves the NS-2 later
   // steps in flight only when all of them exist (t + NS - 2 < nk), else drains to 0, so a
   // short K range (nk < NS - 1) is handled by the same counts.
-  if constexpr (PIPE && BKT == 64) {
-    auto frags = [&](const bf16x8* slot, int ks, bf16x8 (&af)[MI], bf16x8 (&bfr)[JN]) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = slot[gswz_t<64>(wm * WR + i * 16 + fr, ks * 4 + fg)];
-#pragma unroll
-      for (int j = 0; j < JN; ++j)
-        bfr[j] = slot[GBM * CPR + gswz_t<64>(wn * (BN / 2) + j * 16 + fr, ks * 4 + fg)];
-    };
-    auto mfmas = [&](const bf16x8 (&af)[MI], const bf16x8 (&bfr)[JN]) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < JN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    };
-    // all NS slots filled; step 0 landed with the NS-1 later steps left in flight
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      if (s < nk) issue(s);
-    if (NS - 1 < nk) wait_vm<G * (NS - 1)>();
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    bf16x8 a0[MI], b0[JN], a1[MI], b1[JN];
-    frags(lds, 0, a0, b0);
-    for (int t = 0; t < nk; ++t) {
-      frags(lds + (t % NS) * SU, 1, a1, b1);  // second half of step t, under the first's MFMAs
-      mfmas(a0, b0);
-      if (t + 1 < nk) {
-        // step t+1 landed (steps t+2 .. t+NS-1 stay in flight); every wave's reads of slot
-        // t % NS are done (lgkmcnt(0) before the barrier), so it takes step t + NS
-        if (t + NS - 1 < nk) wait_vm<G * (NS - 2)>();
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (t + NS < nk) issue(t + NS);
-        frags(lds + ((t + 1) % NS) * SU, 0, a0, b0);  // first half of step t+1
-      }
-      mfmas(a1, b1);
-    }
-  } else {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) issue(s);
@@ -279,7 +228,6 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
         for (int j = 0; j < JN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-  }
   }
 
   if constexpr (SPL == 2) {
@@ -395,48 +343,39 @@ long gdgemm_ws_floats(int M, int N, int splitk, int bn, int bm) {
   return slabs > dense ? slabs : dense;
 }
 
-template <int BN, int NS, int OCC, int SPL, int S, int BM, int NW, int BKT, int PIPE>
+template <int BN, int NS, int OCC, int SPL, int S, int BM, int NW>
 static void gdgemm_epi(const DGemmArgs& p, dim3 grid, hipStream_t st) {
   if (p.epi == EPI_RESNORM) {
-    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S, BM, NW, BKT, PIPE>
+    gdgemm_kernel<BN, NS, EPI_RESNORM, SPL, OCC, S, BM, NW>
         <<<grid, 64 * NW, 0, st>>>(p);
   } else if (p.epi == EPI_SILU) {
     if constexpr (SPL != 1)
-      gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S, BM, NW, BKT, PIPE>
+      gdgemm_kernel<BN, NS, EPI_SILU, SPL, OCC, S, BM, NW>
           <<<grid, 64 * NW, 0, st>>>(p);
   } else {
-    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S, BM, NW, BKT, PIPE>
+    gdgemm_kernel<BN, NS, EPI_STORE, SPL, OCC, S, BM, NW>
         <<<grid, 64 * NW, 0, st>>>(p);
   }
 }
 
-template <int BN, int NS, int OCC, int BM = 64, int NW = 4, int BKT = 64, int PIPE = 0>
+template <int BN, int NS, int OCC, int BM = 64, int NW = 4>
 static void gdgemm_ring(const DGemmArgs& p, dim3 grid, int splitk, hipStream_t st) {
   if (splitk == 1) {
-    gdgemm_epi<BN, NS, OCC, 0, 1, BM, NW, BKT, PIPE>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 0, 1, BM, NW>(p, grid, st);
   } else if (p.counters == nullptr) {
-    gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW, BKT, PIPE>(p, grid, st);
+    gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW>(p, grid, st);
     launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
   } else {
     switch (splitk) {
-      case 2: gdgemm_epi<BN, NS, OCC, 2, 2, BM, NW, BKT, PIPE>(p, grid, st); break;
-      case 4: gdgemm_epi<BN, NS, OCC, 2, 4, BM, NW, BKT, PIPE>(p, grid, st); break;
-      case 8: gdgemm_epi<BN, NS, OCC, 2, 8, BM, NW, BKT, PIPE>(p, grid, st); break;
+      case 2: gdgemm_epi<BN, NS, OCC, 2, 2, BM, NW>(p, grid, st); break;
+      case 4: gdgemm_epi<BN, NS, OCC, 2, 4, BM, NW>(p, grid, st); break;
+      case 8: gdgemm_epi<BN, NS, OCC, 2, 8, BM, NW>(p, grid, st); break;
       default:  // 16 slices: slabs + the separate reduce pass
-        gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW, BKT, PIPE>(p, grid, st);
+        gdgemm_epi<BN, NS, OCC, 1, 1, BM, NW>(p, grid, st);
         launch_dgemm_reduce(p, PRO_PLAIN, splitk, st);
         break;
     }
   }
-}
-
-// AKAP_GDGEMM_PIPE=1: 256-row tiles with the half-step pipelined K loop (A/B knob, read once)
-static bool gdgemm_pipe() {
-  static const bool on = [] {
-    const char* e = std::getenv("AKAP_GDGEMM_PIPE");
-    return e != nullptr && std::atoi(e) == 1;
-  }();
-  return on;
 }
 
 void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st) {
@@ -444,12 +383,8 @@ void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st) {
   const int tiles = ((p.M + bm - 1) / bm) * ((p.N + p.bn - 1) / p.bn);
   dim3 grid(tiles, splitk);
   const bool deep = p.ns >= 6;
-  if (bm == 256) {  // 256-row tiles, 8 waves: 3 x 48 KB (BN 128) / 3 x 40 KB (BN 64) ring;
-                    // ns >= 6 (BN 128): 6 x 24 KB ring of 32-deep k-steps, five in flight
-    if (p.bn == 128 && p.ns >= 6) gdgemm_ring<128, 6, 1, 256, 8, 32>(p, grid, splitk, st);
-    else if (p.bn == 128 && gdgemm_pipe()) gdgemm_ring<128, 3, 1, 256, 8, 64, 1>(p, grid, splitk, st);
-    else if (p.bn == 128) gdgemm_ring<128, 3, 1, 256, 8>(p, grid, splitk, st);
-    else if (gdgemm_pipe()) gdgemm_ring<64, 3, 1, 256, 8, 64, 1>(p, grid, splitk, st);
+  if (bm == 256) {  // 256-row tiles, 8 waves: 3 x 48 KB (BN 128) / 3 x 40 KB (BN 64) ring
+    if (p.bn == 128) gdgemm_ring<128, 3, 1, 256, 8>(p, grid, splitk, st);
     else gdgemm_ring<64, 3, 1, 256, 8>(p, grid, splitk, st);
     return;
   }

@@ -51,7 +51,7 @@ struct AttnParams {
   float* part_m;  // [B, Hkv, parts, G]
   float* part_l;
   float* part_o;  // [B, Hkv, parts, G, D]
-  int flags;      // bit0: register double-buffered K/V prefetch in decode
+  int flags;      // reserved (0)
   int kv_fp8;     // caches hold OCP e4m3fn bytes (scale 1) instead of bf16
   // fused decode (qkv != nullptr): the kernel itself applies per-head q/k RMSNorm + RoPE to
   // the raw QKV projection row and writes the new token's K/V into the paged cache
@@ -71,7 +71,7 @@ struct AttnParams {
   __bf16* v_tail;
   const int* tail_slot;
 };
-// tile_rows: 64 -> per-wave 16-row kernel, 128 -> flash-style LDS-tiled kernel
+// tile_rows: 128 -> flash-style LDS-tiled kernel (4 waves), 256 -> its 8-wave form (bf16 KV)
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows, hipStream_t s);
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s);
 

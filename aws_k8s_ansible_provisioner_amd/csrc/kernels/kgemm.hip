@@ -20,8 +20,6 @@
 // the 16 lanes of each ds_read_b128 lane group (rows 0-3, 12-15 at chunk c, rows 4-11 at c+1)
 // land on 16 distinct 16-B bank positions: conflict-free (XOR with row & 7 measured 48 %
 // bank-conflict cycles, profiles/r2_pmc_decode_v2.md).
-#include <cstdlib>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -48,9 +46,8 @@ __device__ __forceinline__ void kwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-// KNS ring slots: 4 (3 stages = 96 KB in flight) or 5 (4 stages, 128 KB: at one workgroup
-// per CU the K loop streams at in-flight bytes / load latency, so a deeper ring is the lever;
-// the 5-slot ring of 32-row stages is the whole 160 KB LDS)
+// KNS = 4 ring slots: 3 stages (96 KB) in flight (a 5-slot ring lost 0.5 % end to end and was
+// removed, profiles/r3_gemm_m256_deep.log)
 template <int BM, int EPI, int KNS>
 __global__ __launch_bounds__(256, 1) void kgemm_kernel(DGemmArgs p) {
   constexpr int ROWS = BM + KBN;            // staged rows per stage (X rows, then W rows)
@@ -196,8 +193,10 @@ bool kgemm_supported(int M, int N, int K, int bm) {
   return M > 0 && (bm == 16 || bm == 32) && N % KBN == 0 && K >= KST && K % KST == 0;
 }
 
-template <int KNS>
-static void kgemm_ns(const DGemmArgs& p, int bm, int grid, hipStream_t st) {
+void launch_kgemm(const DGemmArgs& p, int bm, hipStream_t st) {
+  if (p.M == 0) return;
+  constexpr int KNS = 4;
+  const int grid = ((p.M + bm - 1) / bm) * (p.N / KBN);
   if (bm == 16) {
     if (p.epi == EPI_RESNORM) kgemm_kernel<16, EPI_RESNORM, KNS><<<grid, 256, 0, st>>>(p);
     else kgemm_kernel<16, EPI_STORE, KNS><<<grid, 256, 0, st>>>(p);
@@ -205,18 +204,6 @@ static void kgemm_ns(const DGemmArgs& p, int bm, int grid, hipStream_t st) {
     if (p.epi == EPI_RESNORM) kgemm_kernel<32, EPI_RESNORM, KNS><<<grid, 256, 0, st>>>(p);
     else kgemm_kernel<32, EPI_STORE, KNS><<<grid, 256, 0, st>>>(p);
   }
-}
-
-void launch_kgemm(const DGemmArgs& p, int bm, hipStream_t st) {
-  if (p.M == 0) return;
-  const int grid = ((p.M + bm - 1) / bm) * (p.N / KBN);
-  // ring depth: AKAP_KGEMM_NS=5 selects the 5-slot ring (A/B knob, read once)
-  static const int ns = [] {
-    const char* e = std::getenv("AKAP_KGEMM_NS");
-    return e && std::atoi(e) == 5 ? 5 : 4;
-  }();
-  if (ns == 5) kgemm_ns<5>(p, bm, grid, st);
-  else kgemm_ns<4>(p, bm, grid, st);
 }
 
 }  // namespace akap

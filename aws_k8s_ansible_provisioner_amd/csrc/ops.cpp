@@ -138,30 +138,6 @@ static void set_v_tail(akap::AttnParams& p, const std::optional<Tensor>& v_tail,
   p.tail_slot = tail_slot->data_ptr<int>();
 }
 
-// bit0 (default on): register double-buffered K/V prefetch in decode (+1-2% measured)
-// bit6 (default on): non-temporal K/V loads in decode -- the cache is streamed once
-//   per step, keep it out of L2/MALL (-5.5% decode attention time measured)
-// bits3-5: persistent decode grid (WGs per CU); bit7: with bits 3-5 on the fused path, the
-//   pipelined persistent kernel (next item's head fetched under the current item's tail);
-//   bit8: fused grid kernel single-buffered at 3 WGs/CU; bit9: barrier-free fused prologue;
-//   bit1/2: occupancy variants (off).  All measured slower than the default or equal.  AKAP_ATTN_FLAGS sets the process default;
-//   set_attn_flags() swaps it at run time (tests and in-process A/B of the variants).
-static int& attn_flags_ref() {
-  static int f = [] {
-    const char* e = std::getenv("AKAP_ATTN_FLAGS");
-    return e ? std::atoi(e) : 65;
-  }();
-  return f;
-}
-
-int attn_flags() { return attn_flags_ref(); }
-
-int64_t set_attn_flags(int64_t f) {
-  const int prev = attn_flags_ref();
-  attn_flags_ref() = (int)f;
-  return prev;
-}
-
 akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_cache,
                              Tensor& block_tables, Tensor& seq_lens, int64_t G, double scale) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out); CHECK_CONTIG(k_cache);
@@ -187,7 +163,6 @@ akap::AttnParams attn_params(Tensor& out, Tensor& q, Tensor& k_cache, Tensor& v_
   TORCH_CHECK(p.Hq == p.Hkv * G, "Hq must equal Hkv * G");
   TORCH_CHECK(p.BS % 32 == 0, "block size must be a multiple of 32 (K cache chunk layout)");
   p.scale_log2 = (float)(scale * 1.4426950408889634);
-  p.flags = attn_flags();
   return p;
 }
 
@@ -196,13 +171,12 @@ void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cach
                              Tensor tile_seq, Tensor tile_row, int64_t G, double scale,
                              int64_t tile_rows) {
   auto p = attn_params(out, q, k_cache, v_cache, block_tables, seq_lens, G, scale);
-  TORCH_CHECK(tile_rows == 64 || tile_rows == 128 || tile_rows == 256,
-              "tile_rows must be 64, 128 or 256");
+  TORCH_CHECK(tile_rows == 128 || tile_rows == 256, "tile_rows must be 128 or 256");
   TORCH_CHECK(tile_rows != 256 || k_cache.scalar_type() == at::kBFloat16,
               "tile_rows=256 needs a bf16 KV cache");
   // the flash-style kernel caches a sequence's block ids in LDS: <= 32768 keys
-  TORCH_CHECK(tile_rows == 64 || block_tables.size(1) * k_cache.size(2) <= 32768,
-              "tile_rows=128/256 support contexts up to 32768 tokens");
+  TORCH_CHECK(block_tables.size(1) * k_cache.size(2) <= 32768,
+              "prefill attention supports contexts up to 32768 tokens");
   TORCH_CHECK(q_start.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
                   tile_row.scalar_type() == at::kInt,
               "q_start/tile maps must be int32");
@@ -1046,7 +1020,7 @@ TORCH_LIBRARY(akap, m) {
   m.def(
       "paged_attention_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_lens, Tensor q_start, Tensor tile_seq, Tensor tile_row, "
-      "int G, float scale, int tile_rows=64) -> ()");
+      "int G, float scale, int tile_rows=128) -> ()");
   m.def(
       "paged_attention_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_lens, Tensor? q_start, Tensor(b!) part_m, Tensor(c!) part_l, "
@@ -1117,7 +1091,6 @@ TORCH_LIBRARY(akap, m) {
   m.def("kv_gather(Tensor cache, Tensor block_ids, Tensor(a!) out) -> ()");
   m.def("kv_scatter(Tensor buf, Tensor(a!) cache, Tensor block_ids) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start, int vocab_end) -> ()");
-  m.def("set_attn_flags(int flags) -> int");
 }
 
 TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
@@ -1131,7 +1104,6 @@ TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("car_destroy", &car_destroy);
   m.impl("ipc_open", &ipc_open);
   m.impl("ipc_close", &ipc_close);
-  m.impl("set_attn_flags", &set_attn_flags);
 }
 
 TORCH_LIBRARY_IMPL(akap, CUDA, m) {

@@ -66,10 +66,9 @@ class ModelRunner:
         # a mixed step holds a full prefill token budget plus one decode row per sequence
         self.cap_tokens = ecfg.max_num_batched_tokens + self.max_seqs
         # prefill tile map granularity: 128 flattened q rows per workgroup for the flash-style
-        # GPU kernel (AKAP_PREFILL_FA=0: the 64-row per-wave kernel)
-        self.tile_rows = 128 if (dev == "cuda" and
-                                 os.environ.get("AKAP_PREFILL_FA", "1") != "0") else 64
-        if dev == "cuda" and os.environ.get("AKAP_PREFILL_TILE_ROWS") in ("64", "128", "256"):
+        # GPU kernel (the CPU reference attention ignores the tile map)
+        self.tile_rows = 128 if dev == "cuda" else 64
+        if dev == "cuda" and os.environ.get("AKAP_PREFILL_TILE_ROWS") in ("128", "256"):
             self.tile_rows = int(os.environ["AKAP_PREFILL_TILE_ROWS"])  # A/B knob
             if self.tile_rows == 256 and ecfg.kv_cache_dtype.startswith("fp8"):
                 self.tile_rows = 128  # the 256-row kernel needs a bf16 KV cache
@@ -106,8 +105,6 @@ class ModelRunner:
         self.last_top: Optional[tuple] = None
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.ep_overflow_steps = 0  # decode steps re-run after an EP dispatch overflow
-        self._side_stream = None  # second decode micro-batch (AKAP_UBATCH)
-        self.workspace_b = None
         self.graph_pool = None
         self.buckets: list[int] = []
         if self.is_gpu and not ecfg.enforce_eager and self.model.graph_safe:
@@ -381,58 +378,17 @@ class ModelRunner:
         dd = self.dd
         if self._ep_moe:
             moe_mod.ep_overflow_reset(self.device)
-        nA = self._ubatch_split(n)
-        if nA:
-            h = self._forward_ubatched(n, nA)
-        else:
-            parts, ps = self.decode_partitions(n)
-            batch = AttnBatch(False, dd["positions"][:n], dd["slots"][:n], self.dd_bt[:n],
-                              dd["seq_lens"][:n], self.d["q_start"][:n + 1], None, None,
-                              parts, ps, self.workspace, v_tails=self.v_tails,
-                              tail_slot=dd["tail_slot"][:n])
-            h = self.model.forward(dd["input_ids"][:n], batch, self.k_caches, self.v_caches)
+        parts, ps = self.decode_partitions(n)
+        batch = AttnBatch(False, dd["positions"][:n], dd["slots"][:n], self.dd_bt[:n],
+                          dd["seq_lens"][:n], self.d["q_start"][:n + 1], None, None,
+                          parts, ps, self.workspace, v_tails=self.v_tails,
+                          tail_slot=dd["tail_slot"][:n])
+        h = self.model.forward(dd["input_ids"][:n], batch, self.k_caches, self.v_caches)
         # sampler reads bf16 logits directly (no [n, V] fp32 cast pass)
         logits = self.model.compute_logits(h)
         self._sample(logits, n, extras, src=dd)
         if self._ep_moe:
             moe_mod.ep_overflow_reduce(self.device)
-
-    UBATCH_MIN = int(os.environ.get("AKAP_UBATCH_MIN", "64"))
-
-    def _ubatch_split(self, n: int) -> int:
-        """Rows of the first micro-batch when the decode step runs as two concurrent halves,
-        else 0.  Why: per layer the decode step alternates an HBM-bound attention (the KV
-        stream) with latency-bound projection GEMMs that leave most of the chip's bandwidth
-        idle; two independent halves of the batch on two streams let one half's GEMMs run
-        inside the other half's attention.  Single-GPU / DP replicas only (a TP step's
-        collectives stay on one stream), dense models, hipGraph-captured steps."""
-        if (os.environ.get("AKAP_UBATCH", "0") != "1" or not self.is_gpu or n < self.UBATCH_MIN
-                or self.ps.tp_size > 1 or any(getattr(l, "moe", None) is not None
-                                              for l in self.model.layers)):
-            return 0
-        return (n // 2 + 7) // 8 * 8
-
-    def _forward_ubatched(self, n: int, nA: int) -> torch.Tensor:
-        dd = self.dd
-        if self._side_stream is None:
-            self._side_stream = torch.cuda.Stream(device=self.device)
-            self.workspace_b = ops.decode_workspace(self.max_seqs, self.model.hkv, self.G,
-                                                    self.num_parts, self.device)
-        main, side = torch.cuda.current_stream(), self._side_stream
-        side.wait_stream(main)
-        out = []
-        for lo, hi, strm, ws in ((0, nA, main, self.workspace),
-                                 (nA, n, side, self.workspace_b)):
-            with torch.cuda.stream(strm):
-                parts, ps = self.decode_partitions(hi - lo)
-                batch = AttnBatch(False, dd["positions"][lo:hi], dd["slots"][lo:hi],
-                                  self.dd_bt[lo:hi], dd["seq_lens"][lo:hi],
-                                  self.d["q_start"][:hi - lo + 1], None, None, parts, ps, ws,
-                                  v_tails=self.v_tails, tail_slot=dd["tail_slot"][lo:hi])
-                out.append(self.model.forward(dd["input_ids"][lo:hi], batch, self.k_caches,
-                                              self.v_caches))
-        main.wait_stream(side)
-        return torch.cat(out)
 
     @property
     def _ep_moe(self) -> bool:

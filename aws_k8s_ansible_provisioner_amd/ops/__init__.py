@@ -145,9 +145,9 @@ def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
 
 # ----------------------------------------------------------------------------- attention
 def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_start, tile_seq,
-                            tile_row, gqa_group: int, scale: float, tile_rows: int = 64):
+                            tile_row, gqa_group: int, scale: float, tile_rows: int = 128):
     """tile_rows = flattened q rows per tile of the host tile map: 128 selects the flash-style
-    LDS-tiled kernel (32x32x16 MFMA), 64 the per-wave 16-row kernel."""
+    LDS-tiled kernel (32x32x16 MFMA, 4 waves), 256 its 8-wave form (bf16 KV cache)."""
     if _native(q):
         torch.ops.akap.paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens,
                                                q_start, tile_seq, tile_row, gqa_group, scale,
@@ -155,13 +155,6 @@ def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_
         return out
     out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale))
     return out
-
-
-def set_attn_flags(flags: int) -> int:
-    """Swap the attention kernel-variant flags (csrc/ops.cpp attn_flags; process default
-    AKAP_ATTN_FLAGS or 65).  Returns the previous value.  For tests and in-process A/B."""
-    load_native(required=True)
-    return int(torch.ops.akap.set_attn_flags(int(flags)))
 
 
 # longest decode split-KV partition the kernel takes (csrc/kernels/kernels.h kDecodeMaxPart)

@@ -228,31 +228,6 @@ def test_long_prompt_chunked_prefill_and_split_kv_decode():
     _check_teacher_forced(eng, prompt, out.output_ids, tol=0.25)
 
 
-def test_microbatched_decode_matches_single_stream(monkeypatch):
-    """AKAP_UBATCH=1: a decode step of >= 64 rows runs as two concurrent half-batches on two
-    streams inside the hipGraph; greedy tokens equal the single-stream step's and stay
-    (near-)argmax of the dense reference."""
-    prompts = [list(range(3 + i, 40 + i)) for i in range(72)]
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("AKAP_UBATCH", mode)
-        eng = _engine("tiny-qwen3", max_num_seqs=96, cuda_graph_max_bs=96,
-                      max_num_batched_tokens=4096, num_gpu_blocks=512)
-        out = eng.generate(None, SamplingParams(max_tokens=6, temperature=0, ignore_eos=True),
-                           prompt_ids=prompts)
-        res[mode] = [o.output_ids for o in out]
-        if mode == "1":
-            assert eng.runner._side_stream is not None, "micro-batched step never ran"
-            for p, o in list(zip(prompts, out))[::9]:
-                _check_teacher_forced(eng, p, o.output_ids)
-        del eng
-    # different M per GEMM -> different kernels / rounding: a bf16 near-tie flip diverges the
-    # rest of that sequence, so streams are compared loosely (the teacher-forced check above is
-    # the numerics test)
-    same = sum(a == b for a, b in zip(res["0"], res["1"]))
-    assert same >= 0.6 * len(prompts), same
-
-
 def test_pd_handoff_fills_the_v_tail_and_decodes_correctly():
     """P/D decode side on the GPU with the V tail: the prompt KV arrives as whole blocks
     (copied engine to engine in process here, in place of the RCCL transfer), activate()

@@ -127,7 +127,7 @@ def _tiles(seqs, G, rows=64):
 
 @pytest.mark.parametrize("bs", [32, 64])
 @pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (8, 8), (64, 8)])
-@pytest.mark.parametrize("tile_rows", [64, 128, 256])
+@pytest.mark.parametrize("tile_rows", [128, 256])
 def test_paged_attention_prefill(bs, hq, hkv, tile_rows):
     seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (520, 7), (64, 1), (700, 650)]
     q, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, bs, seed=bs + hq)
@@ -567,7 +567,7 @@ def test_paged_attention_decode_fp8(num_parts, part_size, fused):
     assert torch.equal(vg.cpu(), vr)  # the new token's V group is stored back whole
 
 
-@pytest.mark.parametrize("tile_rows", [64, 128])
+@pytest.mark.parametrize("tile_rows", [128])
 def test_paged_attention_prefill_fp8(tile_rows):
     seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (700, 650)]
     hq, hkv = 16, 8
@@ -933,33 +933,3 @@ def test_v_tail_decode_matches_the_plain_cache_path(num_parts, part_size):
         full = n & ~7
         assert torch.equal(_v_tokens(vA_, bt, s, full), _v_tokens(vB_, bt, s, full)), s
     assert torch.equal(kA, kB)
-
-
-@pytest.fixture
-def attn_flags_variant(request):
-    prev = ops.set_attn_flags(request.param)
-    yield request.param
-    ops.set_attn_flags(prev)
-
-
-# 65 = the default grid kernel; 81 = persistent grid, 2 workgroups per CU; 209 = the same with
-# the pipelined kernel (next item's head fetched under the current item's tail); 321 = the grid
-# kernel single-buffered at 3 workgroups per CU; 577 = the barrier-free fused prologue
-@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321, 577], indirect=True)
-@pytest.mark.parametrize("num_parts,part_size,lens", [
-    (1, 4096, [1, 31, 32, 33, 200, 777, 1500] * 40),  # 280 seqs x 8 heads: > 1 item per WG
-    (3, 512, [1, 31, 32, 33, 200, 777, 1500]),
-    (4, 8192, [8001, 1, 20001, 32768, 4095])])
-def test_paged_attention_decode_fused_persistent_variants(attn_flags_variant, num_parts,
-                                                          part_size, lens):
-    """The persistent and pipelined decode kernels (a workgroup runs several work items, the
-    pipelined one prefetching each next item during the current one's tail) against the
-    reference pipeline, with more items than resident workgroups."""
-    test_paged_attention_decode_fused(16, 8, True, num_parts, part_size, lens=list(lens))
-
-
-@pytest.mark.parametrize("attn_flags_variant", [81, 209, 321, 577], indirect=True)
-def test_v_tail_decode_persistent_variants(attn_flags_variant):
-    """V tail path through the persistent / pipelined decode kernels: bit-identical to the
-    plain per-token cache path over 20 steps."""
-    test_v_tail_decode_matches_the_plain_cache_path(1, 4096)
