@@ -199,10 +199,33 @@ def build_runtime(force: bool = False, out_dir: str = PKG, sanitize: bool = Fals
     return out
 
 
+def build_pmc_tool(force: bool = False, log=None) -> str:
+    """The rocprofiler-sdk counter tool (csrc/tools/pmc_tool.cpp) -> libakap_pmc.so: host code
+    only, loaded by the ROCm runtime through ROCP_TOOL_LIBRARIES (exporter/pmc_sampler.py)."""
+    log = log or BuildLog()
+    src = os.path.join(CSRC, "tools", "pmc_tool.cpp")
+    out = os.path.join(PKG, "libakap_pmc.so")
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-shared", "-fPIC", "-fvisibility=hidden",
+           "-I/opt/rocm/include", src, "-o", out, "-L/opt/rocm/lib", "-lrocprofiler-sdk",
+           "-Wl,-rpath,/opt/rocm/lib"]
+    digest = _digest([src], " ".join(cmd))
+    why = "forced" if force else _stale(out, digest)
+    if why:
+        log(f"build libakap_pmc.so ({why})")
+        _run(cmd)
+        with open(out + ".sha", "w") as f:
+            f.write(digest + "\n")
+    else:
+        log("reuse libakap_pmc.so: built from this tree")
+    return out
+
+
 def build(force: bool = False, jobs: int = 8) -> list[str]:
-    """Build both libraries; returns the log lines (what was compiled or reused, and why)."""
+    """Build every native library; returns the log lines (what was compiled or reused, and
+    why)."""
     log = BuildLog()
     build_runtime(force, log=log)
+    build_pmc_tool(force, log=log)
     build_kernels(force, jobs, log=log)
     return log.lines
 

@@ -16,6 +16,7 @@ another collective.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -118,15 +119,29 @@ def make_tp_engine(ecfg: EngineConfig, backend: Optional[str] = None, log=print)
     return eng, bc
 
 
-def serve_tp(ecfg: EngineConfig, host: str, port: int) -> None:
+def serve_tp(ecfg: EngineConfig, host: str, port: int, telemetry=None) -> None:
+    """telemetry(labels) -> text providers of this rank (kernel-stats windows, GPU counters):
+    rank 0 serves its own and merges the followers' (written under /dev/shm by a
+    rank_metrics.RankMetricsWriter on each follower) into /metrics, rank-labelled."""
     import uvicorn
 
+    from ..exporter import rank_metrics
     from ..server.api_server import build_app
 
+    rank = int(os.environ.get("RANK", "0"))
+    tag = f"tp-{os.environ.get('MASTER_PORT', '0')}"
+    providers = telemetry({"rank": str(rank)}) if telemetry else []
+    writer = None
+    if rank != 0 and providers:
+        writer = rank_metrics.RankMetricsWriter(tag, rank, providers).start()
     eng, bc = make_tp_engine(ecfg)
     if eng is None:
+        if writer is not None:
+            writer.stop()
         return
     app, ae = build_app(ecfg, engine=eng)
+    ae.telemetry = providers
+    ae.rank_metrics_tag = tag
     try:
         uvicorn.run(app, host=host, port=port, log_level="info", access_log=False)
     finally:

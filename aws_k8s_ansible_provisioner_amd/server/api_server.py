@@ -189,9 +189,18 @@ class OpenAIServer:
         async def metrics():
             eng._update_gauges()
             body = eng.metrics.render()
-            kp = getattr(self.ae, "kernel_profiler", None)
-            if kp is not None:  # in-process kernel-stats windows (exporter/inprocess_profiler)
-                body = body.rstrip("\n") + "\n" + kp.text()
+            # this process's telemetry (kernel-stats windows, GPU counters) and, on rank 0 of a
+            # multi-process TP engine, every follower rank's (exporter/rank_metrics.py)
+            extra = [t() for t in getattr(self.ae, "telemetry", [])]
+            tag = getattr(self.ae, "rank_metrics_tag", None)
+            if tag:
+                from ..exporter import rank_metrics
+
+                extra += rank_metrics.read_peers(tag)
+            if extra:
+                from ..exporter import rank_metrics
+
+                body = body.rstrip("\n") + "\n" + rank_metrics.merge(extra)
             return PlainTextResponse(body, media_type="text/plain; version=0.0.4; charset=utf-8")
 
         @app.get("/v1/models")
@@ -570,6 +579,10 @@ def make_parser() -> argparse.ArgumentParser:
                          "akap_kernel_* on /metrics (torch.profiler; 0 = off, the rocprofv3 "
                          "sidecar then provides them)")
     ap.add_argument("--kernel-stats-window-ms", type=int, default=1000)
+    ap.add_argument("--pmc-interval", type=float, default=0.0,
+                    help="seconds between GPU hardware-counter reads served as akap_gpu_pmc_* "
+                         "on /metrics (0 = off; needs ROCP_TOOL_LIBRARIES=<libakap_pmc.so> in "
+                         "the environment at process start)")
     return ap
 
 
@@ -598,6 +611,26 @@ def pd_group_id() -> str:
            f"{os.environ.get('MASTER_PORT', '')}"
 
 
+def make_telemetry(a, labels: dict) -> list:
+    """This process's in-process telemetry providers (text callables for /metrics): kernel-stats
+    windows (--kernel-stats-interval) and GPU hardware counters (--pmc-interval), labelled with
+    `labels` (the TP rank in multi-process engines)."""
+    from ..exporter import rank_metrics
+
+    out = []
+    if a.kernel_stats_interval > 0:
+        from ..exporter.inprocess_profiler import InProcessKernelProfiler
+
+        kp = InProcessKernelProfiler(a.kernel_stats_window_ms, a.kernel_stats_interval).start()
+        out.append(lambda: rank_metrics.add_labels(kp.text(), labels))
+    if a.pmc_interval > 0:
+        from ..exporter.pmc_sampler import PMCSampler
+
+        pmc = PMCSampler(a.pmc_interval, labels=labels).start()
+        out.append(pmc.text)
+    return out
+
+
 def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:
     from ..engine.llm_engine import LLMEngine
 
@@ -623,7 +656,7 @@ def main(argv: Optional[list] = None) -> None:
     if a.tensor_parallel_size > 1:
         from ..parallel.tp_worker import serve_tp
 
-        serve_tp(ecfg, a.host, a.port)
+        serve_tp(ecfg, a.host, a.port, telemetry=lambda labels: make_telemetry(a, labels))
         return
     if a.kv_role != "both":
         # P/D: this process is one rank of the prefill/decode KV-transfer group (torchrun)
@@ -632,11 +665,7 @@ def main(argv: Optional[list] = None) -> None:
         backend = os.environ.get("AKAP_DIST_BACKEND") or ("gloo" if a.device == "cpu" else None)
         init_distributed(tp_size=1, backend=backend)
     app, ae = build_app(ecfg)
-    if a.kernel_stats_interval > 0:
-        from ..exporter.inprocess_profiler import InProcessKernelProfiler
-
-        ae.kernel_profiler = InProcessKernelProfiler(a.kernel_stats_window_ms,
-                                                     a.kernel_stats_interval).start()
+    ae.telemetry = make_telemetry(a, {})
     uvicorn.run(app, host=a.host, port=a.port, log_level="info", access_log=False)
 
 
