@@ -128,6 +128,18 @@ void launch_gdgemm(const DGemmArgs& p, int splitk, hipStream_t st);
 bool kgemm_supported(int M, int N, int K, int bm);
 void launch_kgemm(const DGemmArgs& p, int bm, hipStream_t st);
 
+// ---- pgemm.hip: prefill / large-M GEMM Y = X . W^T, 256 x 256 tiles, optional expert groups
+struct PGemmArgs {
+  const void* X;    // bf16 [M, K] (row stride ldx); grouped: rows sorted by group
+  const void* W;    // bf16 [N, K] dense, or [groups, N, K]
+  void* Y;          // bf16 [M, N] (row stride ldy), or [M, N/2] with the SwiGLU epilogue
+  const int* offs;  // grouped: [groups] cumulative row ends (device)
+  int groups;       // 0 = dense
+  int M, N, K, ldx, ldy;
+};
+bool pgemm_supported(int M, int N, int K);
+void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st);
+
 // ---- wgemm.hip: wide-row weight-streaming GEMM (LM head) Y[M,N] = X[M,K] . W[N,K]^T ----
 struct WGemmArgs {
   const void* X;  // bf16 [M, K] (row stride ldx)

@@ -706,6 +706,41 @@ void kv_pull(int64_t src_ptr, int64_t src_plane_stride, Tensor dst_cache, Tensor
   akap::launch_kv_pull(a, cur_stream());
 }
 
+// Prefill / large-M GEMM (pgemm.hip): out = x . w^T (epi 0) or silu(gate) * up over the
+// [gate; up] halves of w (epi 2, out [M, N/2]).  offs (int32 [G], device) -> expert-grouped:
+// rows of x sorted by group, w [G, N, K].
+void pgemm(Tensor out, Tensor x, Tensor w, int64_t epi, std::optional<Tensor> offs) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_LAST_CONTIG(x); CHECK_CONTIG(w); CHECK_LAST_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "x, out must be 2-D");
+  TORCH_CHECK(epi == akap::EPI_STORE || epi == akap::EPI_SILU, "pgemm epilogue: store | silu");
+  akap::PGemmArgs a{};
+  a.M = x.size(0);
+  a.K = x.size(1);
+  a.N = w.size(-2);
+  TORCH_CHECK(w.size(-1) == a.K, "w [.., N, K] must match x [M, K]");
+  TORCH_CHECK(akap::pgemm_supported(a.M, a.N, a.K), "pgemm: N % 256 == 0 and K % 64 == 0 needed");
+  TORCH_CHECK(out.size(0) == a.M && out.size(1) == (epi == akap::EPI_SILU ? a.N / 2 : a.N),
+              "out shape");
+  if (offs) {
+    TORCH_CHECK(w.dim() == 3 && offs->scalar_type() == at::kInt && offs->is_cuda() &&
+                    offs->numel() == w.size(0),
+                "grouped pgemm: w [G, N, K], offs int32 [G] on the device");
+    a.offs = offs->data_ptr<int>();
+    a.groups = offs->numel();
+  } else {
+    TORCH_CHECK(w.dim() == 2, "dense pgemm: w [N, K]");
+  }
+  a.X = x.data_ptr();
+  a.W = w.data_ptr();
+  a.Y = out.data_ptr();
+  a.ldx = x.stride(0);
+  a.ldy = out.stride(0);
+  TORCH_CHECK(a.ldx % 8 == 0 && a.ldy % 4 == 0, "row strides must keep 16-B / 8-B alignment");
+  const c10::DeviceGuard g(x.device());
+  akap::launch_pgemm(a, (int)epi, cur_stream());
+}
+
 void embedding(Tensor ids, Tensor table, Tensor out, int64_t vocab_start, int64_t vocab_end) {
   CHECK_GPU(ids); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CONTIG(out);
   TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
@@ -1050,6 +1085,7 @@ TORCH_LIBRARY(akap, m) {
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
       "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None, int bm=64) -> ()");
   m.def("wgemm(Tensor(a!) out, Tensor x, Tensor w) -> ()");
+  m.def("pgemm(Tensor(a!) out, Tensor x, Tensor w, int epi=0, Tensor? offs=None) -> ()");
   m.def("kgemm(Tensor(a!) out, Tensor x, Tensor w, int bm, int epi, float eps, Tensor? ss_in, "
         "Tensor(b!)? ss_out, Tensor(c!)? aout, Tensor? ln_out) -> ()");
   m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
@@ -1121,6 +1157,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("dgemm", &dgemm);
   m.impl("wgemm", &wgemm);
+  m.impl("pgemm", &pgemm);
   m.impl("kgemm", &kgemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_router_topk", &moe_router_topk);

@@ -695,3 +695,20 @@ def ipc_open(blob: bytes, device: int) -> int:
 
 def ipc_close(addr: int) -> None:
     torch.ops.akap.ipc_close(int(addr))
+
+
+def pgemm(x: torch.Tensor, w: torch.Tensor, silu: bool = False,
+          offs: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
+    """Prefill / large-M GEMM (csrc/kernels/pgemm.hip): y = x @ w.T, 256 x 256 tiles.
+    silu=True: w is the [gate; up] weight [2F, K] and y = silu(x @ gate.T) * (x @ up.T) [M, F].
+    offs (int32 [G] cumulative row ends): expert-grouped -- x rows sorted by group, w [G, N, K].
+    The CPU path is the fp32 reference of the same op."""
+    M, K = x.shape
+    N = w.shape[-2]
+    if out is None:
+        out = torch.empty(M, N // 2 if silu else N, dtype=x.dtype, device=x.device)
+    if _native(x):
+        torch.ops.akap.pgemm(out, x, w, EPI_SILU if silu else EPI_STORE, offs)
+        return out
+    out.copy_(ref.pgemm(x, w, silu, offs))
+    return out

@@ -10,6 +10,7 @@ engine path.  Cache layouts (BS % 32 == 0, D = 128 on the GPU path):
 from __future__ import annotations
 
 import math
+from typing import Optional
 
 import torch
 
@@ -283,3 +284,20 @@ def apply_penalties(logits, rows, toks, counts, presence, frequency, repetition)
         x -= float(frequency[r]) * c + (float(presence[r]) if c > 0 else 0.0)
         out[r, t] = x
     return out
+
+
+def pgemm(x: torch.Tensor, w: torch.Tensor, silu: bool = False,
+          offs: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 reference of ops.pgemm: x @ w.T (bf16-rounded), or silu(gate) * up over the
+    [gate; up] halves of w; offs (cumulative row ends): rows of group g use w[g]."""
+    xf = x.float()
+    if offs is None:
+        y = (xf @ w.float().t()).to(x.dtype)
+    else:
+        y = torch.empty(x.shape[0], w.shape[-2], dtype=x.dtype, device=x.device)
+        lo = 0
+        for g, hi in enumerate(offs.tolist()):
+            if hi > lo:
+                y[lo:hi] = (xf[lo:hi] @ w[g].float().t()).to(x.dtype)
+            lo = hi
+    return silu_and_mul(y) if silu else y

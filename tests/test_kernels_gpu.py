@@ -933,3 +933,56 @@ def test_v_tail_decode_matches_the_plain_cache_path(num_parts, part_size):
         full = n & ~7
         assert torch.equal(_v_tokens(vA_, bt, s, full), _v_tokens(vB_, bt, s, full)), s
     assert torch.equal(kA, kB)
+
+
+# ----------------------------------------------------------------------------- prefill GEMM
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 512, 128), (256, 1024, 1024),
+                                   (1000, 768, 2048), (4096, 4096, 1024), (517, 256, 4096)])
+def test_pgemm_matches_fp32(M, N, K):
+    """pgemm (256x256 tiles, phased LDS-DMA pipeline) vs an fp32 reference, asymmetric random
+    operands, M not a multiple of the tile, K from one to 64 K tiles."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
+    y = ops.pgemm(x.to(DEV), w.to(DEV))
+    exp = x.float() @ w.float().t()
+    err = (y.float().cpu() - exp).abs().max().item()
+    assert err <= 2e-2 * exp.abs().max().item() + 1e-2, err
+
+
+def test_pgemm_identity_and_layout():
+    """A = I on the first K columns, W asymmetric: catches a transposed C write or a wrong
+    fragment map exactly (cdna_hip_programming.md section 3)."""
+    M, N, K = 256, 512, 256
+    x = torch.zeros(M, K)
+    x[:, :].fill_diagonal_(1.0)
+    w = (torch.arange(N * K, dtype=torch.float32).reshape(N, K) % 61 - 30) / 8
+    y = ops.pgemm(x.bfloat16().to(DEV), w.bfloat16().to(DEV)).float().cpu()
+    assert torch.equal(y, (x @ w.bfloat16().float().t()).bfloat16().float())
+
+
+@pytest.mark.parametrize("M,F,K", [(300, 256, 256), (2048, 1536, 1024)])
+def test_pgemm_silu_epilogue(M, F, K):
+    g = torch.Generator().manual_seed(F + K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(2 * F, K, generator=g) * 0.05).bfloat16()
+    y = ops.pgemm(x.to(DEV), w.to(DEV), silu=True).float().cpu()
+    exp = ref.pgemm(x, w, silu=True).float()
+    assert (y - exp).abs().max().item() <= 3e-2 * exp.abs().max().item() + 1e-2
+
+
+@pytest.mark.parametrize("counts", [[300, 0, 517, 1, 256, 0, 0, 40], [0, 0, 1024], [5]])
+def test_pgemm_grouped(counts):
+    """Expert-grouped form over device-side offsets: empty groups, 1-row groups and groups that
+    are not a multiple of the tile; every group's rows use its own weight."""
+    G = len(counts)
+    M = sum(counts)
+    N, K = 512, 256
+    g = torch.Generator().manual_seed(G + M)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(G, N, K, generator=g) * 0.05).bfloat16()
+    offs = torch.tensor(counts).cumsum(0).int()
+    for silu in (False, True):
+        y = ops.pgemm(x.to(DEV), w.to(DEV), silu=silu, offs=offs.to(DEV)).float().cpu()
+        exp = ref.pgemm(x, w, silu, offs).float()
+        assert (y - exp).abs().max().item() <= 3e-2 * exp.abs().max().item() + 1e-2, silu
