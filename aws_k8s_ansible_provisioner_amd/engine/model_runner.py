@@ -563,7 +563,8 @@ class ModelRunner:
             cache = os.environ.get("AKAP_GEMM_TUNE_CACHE")
             if cache and self.model.ps.world_size > 1:
                 cache = f"{cache}.rank{self.model.ps.rank}"
-            loaded = bool(cache) and gemm_tuner.load_cache(cache, self.model, tune_ms)
+            pre_m = self.ecfg.max_num_batched_tokens
+            loaded = bool(cache) and gemm_tuner.load_cache(cache, self.model, tune_ms, pre_m)
             if self.ps.tp_size > 1:
                 # tune_fused broadcasts rank 0's plan over the TP group: every rank must take
                 # the same branch, so one rank's missing / stale cache file retunes them all
@@ -580,8 +581,10 @@ class ModelRunner:
                 gemm_tuner.tune_model(self.model, tune_ms, log=self.log)
                 if os.environ.get("AKAP_FUSED_GEMM", "1") != "0":
                     gemm_tuner.tune_fused(self.model, tune_ms, log=self.log)
+                if ops.PREFILL_GEMM == "auto" and pre_m >= ops.PGEMM_MIN_M:
+                    gemm_tuner.tune_prefill(self.model, pre_m, log=self.log)
                 if cache:
-                    gemm_tuner.save_cache(cache, self.model, tune_ms)
+                    gemm_tuner.save_cache(cache, self.model, tune_ms, pre_m)
             self.log(f"[runner] GEMM tuning {time.time() - t1:.1f}s")
         self._stage_decode(self.max_seqs)
         torch.cuda.synchronize()

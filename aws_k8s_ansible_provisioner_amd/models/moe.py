@@ -204,9 +204,10 @@ class MoEBlock:
     def _expert_rows(self, x: torch.Tensor, e: torch.Tensor,
                      src: Optional[torch.Tensor] = None) -> torch.Tensor:
         """y[i] = expert e[i]'s SwiGLU FFN of x[src[i]] (src = identity when None), unweighted.
-        Rows are sorted by expert on the device and run through torch._grouped_mm (the ROCm
-        library grouped GEMM) over device-side group offsets: no host sync, no per-expert
-        loop.  Mixtral-8x7B shapes on MI355X: 1081 TFLOP/s at T=16384 and 847 at T=4096, vs
+        Rows are sorted by expert on the device and run through a grouped GEMM over device-side
+        group offsets -- the hand-written pgemm (SwiGLU fused into the first GEMM's epilogue) or
+        torch._grouped_mm (the ROCm library grouped GEMM), whichever measured faster at engine
+        start (gemm_tuner.tune_prefill): no host sync, no per-expert loop.  Mixtral-8x7B shapes on MI355X: 1081 TFLOP/s at T=16384 and 847 at T=4096, vs
         617 / 444 for fused_moe and level with the host-synced per-expert hipBLASLt loop it
         replaces (profiles/r3_moe_prefill.log).  Outputs come back in row order (a permutation
         store: deterministic, no float atomics)."""
@@ -214,8 +215,15 @@ class MoEBlock:
         order = torch.argsort(e, stable=True)
         offs = torch.cumsum(torch.bincount(e, minlength=self.e_local), 0).to(torch.int32)
         xs = x[order if src is None else src[order]]
-        a = ops.silu_and_mul(torch._grouped_mm(xs, self.w13.transpose(1, 2), offs=offs))
-        y = torch._grouped_mm(a, self.w2.transpose(1, 2), offs=offs)
+        if ops.use_pgemm(xs, self.w13.shape[1], silu=True, grouped=True):
+            # hand-written grouped GEMM with SwiGLU in its epilogue (csrc/kernels/pgemm.hip)
+            a = ops.pgemm(xs, self.w13, silu=True, offs=offs)
+        else:
+            a = ops.silu_and_mul(torch._grouped_mm(xs, self.w13.transpose(1, 2), offs=offs))
+        if ops.use_pgemm(a, self.w2.shape[1], grouped=True):
+            y = ops.pgemm(a, self.w2, offs=offs)
+        else:
+            y = torch._grouped_mm(a, self.w2.transpose(1, 2), offs=offs)
         out = torch.empty_like(y)
         out[order] = y
         return out

@@ -363,8 +363,7 @@ class DecoderLM:
             if lw.moe is not None:
                 x = lw.moe.forward(h)
             else:
-                gu = ops.linear(h, lw.w_gate_up)
-                x = comm.tp_all_reduce(ops.linear(ops.silu_and_mul(gu), lw.w_down))
+                x = comm.tp_all_reduce(ops.linear(ops.linear_silu(h, lw.w_gate_up), lw.w_down))
         h, _ = ops.fused_add_rms_norm(x, residual, self.final_norm, eps)
         return h
 

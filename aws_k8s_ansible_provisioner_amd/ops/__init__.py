@@ -222,13 +222,56 @@ def decode_workspace(max_seqs: int, num_kv_heads: int, gqa_group: int, num_parts
 # ----------------------------------------------------------------------------- GEMM
 _GEMM_MODE = os.environ.get("AKAP_GEMM", "torch")  # torch (hipBLASLt) | auto | hip
 GEMM_MAX_M = int(os.environ.get("AKAP_GEMM_MAX_M", "512"))
+# prefill-sized GEMMs: "auto" = per weight shape, whichever of hipBLASLt and the hand-written
+# 256 x 256 pgemm (csrc/kernels/pgemm.hip) measured faster at engine start
+# (gemm_tuner.tune_prefill); "pgemm" / "lib" force one.  PGEMM_MIN_M: smallest M routed to it.
+PREFILL_GEMM = os.environ.get("AKAP_PREFILL_GEMM", "auto")
+PGEMM_MIN_M = int(os.environ.get("AKAP_PGEMM_MIN_M", "1024"))
+
+
+def pgemm_supported(M: int, N: int, K: int) -> bool:
+    """Mirror of pgemm_supported (csrc/kernels/pgemm.hip)."""
+    return M > 0 and N > 0 and N % 256 == 0 and K >= 64 and K % 64 == 0
+
+
+def use_pgemm(x: torch.Tensor, N: int, silu: bool = False, grouped: bool = False) -> bool:
+    """Route x [M, K] times an [N, K] weight (or a grouped [G, N, K] one) to pgemm?"""
+    if not (x.is_cuda and x.dim() == 2 and x.stride(-1) == 1 and x.shape[0] >= PGEMM_MIN_M
+            and pgemm_supported(x.shape[0], N, x.shape[1])):
+        return False
+    if PREFILL_GEMM == "pgemm":
+        return True
+    if PREFILL_GEMM == "auto":
+        from . import gemm_tuner
+
+        return bool(gemm_tuner.prefill_choice("grouped" if grouped else "dense", N, x.shape[1],
+                                              silu))
+    return False
+
+
+def _use_pgemm(x: torch.Tensor, w: torch.Tensor, silu: bool = False) -> bool:
+    return w.dim() == 2 and use_pgemm(x, w.shape[0], silu)
+
+
+def linear_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """silu(x @ gate.T) * (x @ up.T) for the [gate; up] weight w [2F, K]: one pgemm launch
+    with the SwiGLU epilogue for prefill-sized M (no [M, 2F] intermediate round trip through
+    HBM), else linear + silu_and_mul."""
+    if _use_pgemm(x, w, silu=True):
+        load_native(required=True)
+        return pgemm(x, w, silu=True)
+    return silu_and_mul(linear(x, w))
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w.T.  Decode-sized M on the GPU -> the hand-written MFMA GEMM (small tiles +
-    split-K to fill 256 CUs); large M (prefill) -> hipBLASLt via torch."""
+    split-K to fill 256 CUs); large M (prefill) -> hipBLASLt via torch, or the hand-written
+    256 x 256 pgemm where it measured faster (AKAP_PREFILL_GEMM)."""
     M = x.shape[0]
     split = None
+    if _use_pgemm(x, w):
+        load_native(required=True)
+        return pgemm(x, w, out=out)
     if x.is_cuda and x.dim() == 2:
         from . import gemm_tuner
 

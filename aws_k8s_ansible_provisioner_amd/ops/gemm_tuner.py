@@ -43,9 +43,10 @@ def plan() -> dict:
 
 
 def reset() -> None:
-    """Forget every tuned choice (per-shape plan and fused chains)."""
+    """Forget every tuned choice (per-shape plan, fused chains, prefill GEMM choices)."""
     _PLAN.clear()
     _FUSED.clear()
+    _PREFILL.clear()
 
 
 def lookup(M: int, N: int, K: int) -> Optional[Choice]:
@@ -340,15 +341,93 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
     return chosen
 
 
+# ----------------------------------------------------------------------------- prefill GEMMs
+# Prefill-sized projections (M = the prefill chunk, thousands of rows): hipBLASLt vs the
+# hand-written 256 x 256 pgemm (csrc/kernels/pgemm.hip), per weight shape, with the SwiGLU
+# epilogue variant for gate|up (pgemm + fused epilogue vs hipBLASLt + silu_and_mul) and the
+# expert-grouped form for MoE layers (pgemm over device offsets vs torch._grouped_mm).
+# Keys: ("dense", N, K, silu) | ("grouped", N, K, silu) -> True when pgemm measured faster.
+_PREFILL: dict = {}
+
+
+def prefill_choice(kind: str, N: int, K: int, silu: bool = False) -> Optional[bool]:
+    return _PREFILL.get((kind, N, K, bool(silu)))
+
+
+def tune_prefill(model, M: int, log=print, margin: float = 0.02) -> dict:
+    """Time both paths for every prefill projection shape of `model` at M rows, on the real
+    layer weights (rotating through the layers inside one captured graph)."""
+    from . import pgemm_supported, silu_and_mul
+
+    groups: dict = {}
+    for lw in model.layers:
+        for name in ("w_qkv", "w_o", "w_gate_up", "w_down"):
+            w = getattr(lw, name, None)
+            if w is not None and w.is_cuda:
+                groups.setdefault(tuple(w.shape) + (name == "w_gate_up",), []).append(w)
+    out = {}
+    dev = None
+    for (N, K, gu), ws in groups.items():
+        if not pgemm_supported(M, N, K):
+            continue
+        dev = ws[0].device
+        x = torch.randn(M, K, device=dev, dtype=ws[0].dtype) * 0.1
+        y = torch.empty(M, N, device=dev, dtype=ws[0].dtype)
+        n = len(ws)
+        t_lib = _timed(lambda i: torch.matmul(x, ws[i % n].t(), out=y), n)
+        t_pg = _timed(lambda i: torch.ops.akap.pgemm(y, x, ws[i % n], 0, None), n)
+        _PREFILL[("dense", N, K, False)] = t_pg < t_lib * (1.0 - margin)
+        out[("dense", N, K, False)] = (t_pg, t_lib)
+        if gu:
+            a = torch.empty(M, N // 2, device=dev, dtype=ws[0].dtype)
+            t_lib_s = _timed(lambda i: silu_and_mul(torch.matmul(x, ws[i % n].t(), out=y), a), n)
+            t_pg_s = _timed(lambda i: torch.ops.akap.pgemm(a, x, ws[i % n], 2, None), n)
+            _PREFILL[("dense", N, K, True)] = t_pg_s < t_lib_s * (1.0 - margin)
+            out[("dense", N, K, True)] = (t_pg_s, t_lib_s)
+        del x, y
+    for lw in model.layers:  # MoE experts: one representative layer
+        moe = getattr(lw, "moe", None)
+        if moe is None or not moe.w13.is_cuda:
+            continue
+        E = moe.w13.shape[0]
+        rows = M * moe.K
+        g = torch.Generator(device="cpu").manual_seed(0)
+        cnt = torch.multinomial(torch.ones(E), rows, replacement=True,
+                                generator=g).bincount(minlength=E)
+        offs = cnt.cumsum(0).to(torch.int32).to(moe.w13.device)
+        for w, silu in ((moe.w13, True), (moe.w2, False)):
+            _, N, K = w.shape
+            if not pgemm_supported(rows, N, K):
+                continue
+            x = torch.randn(rows, K, device=w.device, dtype=w.dtype) * 0.1
+            o = torch.empty(rows, N // 2 if silu else N, device=w.device, dtype=w.dtype)
+            wt = w.transpose(1, 2)
+            if silu:
+                lib = lambda i: silu_and_mul(torch._grouped_mm(x, wt, offs=offs), o)  # noqa: E731
+            else:
+                lib = lambda i: torch._grouped_mm(x, wt, offs=offs)  # noqa: E731
+            t_lib = _timed(lib, 2)
+            t_pg = _timed(lambda i: torch.ops.akap.pgemm(o, x, w, 2 if silu else 0, offs), 2)
+            _PREFILL[("grouped", N, K, silu)] = t_pg < t_lib * (1.0 - margin)
+            out[("grouped", N, K, silu)] = (t_pg, t_lib)
+            del x, o
+        break
+    if out:
+        log(f"[gemm-tuner] prefill GEMMs at M={M} (us pgemm/library): " + ", ".join(
+            f"{k[0]} {k[1]}x{k[2]}{' silu' if k[3] else ''} {a:.0f}/{b:.0f}"
+            + ("*" if _PREFILL[k] else "") for k, (a, b) in out.items()))
+    return out
+
+
 # ----------------------------------------------------------------------------- tuning cache
 # The plan is a pure function of (GPU, kernel library, model shapes, TP layout, batch
 # buckets): a JSON file keyed on those lets a restarted engine skip the ~3-10 s of timing
 # (AKAP_GEMM_TUNE_CACHE=path, engine/model_runner.py), and keeps a profiled run free of the
 # tuning candidates' launches.  Any key mismatch -> retune and overwrite.
-CACHE_VERSION = 1
+CACHE_VERSION = 2
 
 
-def cache_key(model, Ms: Sequence[int]) -> dict:
+def cache_key(model, Ms: Sequence[int], prefill_m: int = 0) -> dict:
     import os
 
     from . import _LIB
@@ -370,16 +449,18 @@ def cache_key(model, Ms: Sequence[int]) -> dict:
     return {"version": CACHE_VERSION, "arch": arch, "lib": lib,
             "tp": [model.ps.tp_size, model.ps.tp_rank], "layers": len(model.layers),
             "shapes": [[n, list(sh)] for n, sh in shapes],
-            "lm_head": list(lm.shape) if lm is not None else None, "Ms": sorted(int(m) for m in Ms)}
+            "lm_head": list(lm.shape) if lm is not None else None, "Ms": sorted(int(m) for m in Ms),
+            "prefill_m": int(prefill_m)}
 
 
-def save_cache(path: str, model, Ms: Sequence[int]) -> None:
+def save_cache(path: str, model, Ms: Sequence[int], prefill_m: int = 0) -> None:
     import json
     import os
 
-    data = {"key": cache_key(model, Ms),
+    data = {"key": cache_key(model, Ms, prefill_m),
             "plan": [[list(k), list(v)] for k, v in sorted(_PLAN.items())],
-            "fused": [[m, {n: list(t) for n, t in pl.items()}] for m, pl in sorted(_FUSED.items())]}
+            "fused": [[m, {n: list(t) for n, t in pl.items()}] for m, pl in sorted(_FUSED.items())],
+            "prefill": [[list(k), v] for k, v in sorted(_PREFILL.items())]}
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     tmp = f"{path}.tmp{os.getpid()}"
     with open(tmp, "w") as f:
@@ -387,7 +468,7 @@ def save_cache(path: str, model, Ms: Sequence[int]) -> None:
     os.replace(tmp, path)  # readers never see a half-written file
 
 
-def load_cache(path: str, model, Ms: Sequence[int]) -> bool:
+def load_cache(path: str, model, Ms: Sequence[int], prefill_m: int = 0) -> bool:
     """Install the cached plan when its key matches this model/GPU/library; False otherwise."""
     import json
 
@@ -396,7 +477,7 @@ def load_cache(path: str, model, Ms: Sequence[int]) -> bool:
             data = json.load(f)
     except (OSError, ValueError):
         return False
-    if data.get("key") != cache_key(model, Ms):
+    if data.get("key") != cache_key(model, Ms, prefill_m):
         return False
     _PLAN.clear()
     _FUSED.clear()
@@ -404,6 +485,9 @@ def load_cache(path: str, model, Ms: Sequence[int]) -> bool:
         _PLAN[tuple(k)] = tuple(v)
     for m, pl in data["fused"]:
         _FUSED[int(m)] = {n: tuple(t) for n, t in pl.items()}
+    _PREFILL.clear()
+    for k, v in data.get("prefill", []):
+        _PREFILL[tuple(k)] = bool(v)
     return True
 
 

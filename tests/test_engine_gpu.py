@@ -297,3 +297,29 @@ def test_inprocess_kernel_stats_window_sees_graph_replayed_kernels():
     names = " ".join(kp.windows[-1])
     assert "paged_attn_decode" in names, names[:500]
     assert "akap_kernel_profiler_up 1" in kp.text()
+
+
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-mixtral", "qwen3-0.6b"])
+def test_prefill_on_hand_written_gemm(model, monkeypatch):
+    """AKAP_PREFILL_GEMM=pgemm: every prefill projection on csrc/kernels/pgemm.hip (SwiGLU fused
+    into the gate|up GEMM; Mixtral's experts on its grouped form) -- generations still match
+    the dense reference."""
+    from aws_k8s_ansible_provisioner_amd import ops
+    from aws_k8s_ansible_provisioner_amd.models import moe
+
+    calls = []
+    real = ops.pgemm
+    monkeypatch.setattr(ops, "pgemm", lambda *a, **k: calls.append(k) or real(*a, **k))
+    monkeypatch.setattr(ops, "PREFILL_GEMM", "pgemm")
+    monkeypatch.setattr(ops, "PGEMM_MIN_M", 16)
+    monkeypatch.setattr(moe.MoEBlock, "grouped_min_t", 16)
+    kw = dict(max_model_len=256, num_gpu_blocks=64, init_std=0.02) if model == "qwen3-0.6b" else {}
+    eng = _engine(model, **kw)
+    prompts = [list(range(5, 90)), list(range(300, 340))]
+    outs = eng.generate(None, SamplingParams(max_tokens=4, temperature=0, ignore_eos=True),
+                        prompt_ids=prompts)
+    assert any(k.get("silu") for k in calls)
+    if model == "tiny-mixtral":
+        assert any(k.get("offs") is not None for k in calls)
+    for p, o in zip(prompts, outs):
+        _check_teacher_forced(eng, p, o.output_ids, tol=0.2)
