@@ -7,7 +7,8 @@ and times its compute. Shapes, kernels, GEMM tuner choices and hipGraph capture 
 identical. The TP collectives are replaced by local stand-ins of the same shape:
   tp_all_reduce           the custom all-reduce kernel on a one-rank communicator
   tp_all_reduce_resnorm   the same kernel with its fused residual + next-norm epilogue
-  tp_all_gather_last      the shard repeated tp times
+  tp_all_gather_last      the custom IPC all-gather kernel on the same communicator, then the
+                          shard repeated tp times
 so the result is a per-rank compute time including the all-reduce launches; a TP step adds
 the xGMI exchange of two B x 8192 bf16 all-reduces per layer to it.
 
@@ -45,9 +46,17 @@ def stub_collectives(tp: int) -> None:
     def resnorm(partial, residual, ln, a_out, ss):
         torch.ops.akap.car_all_reduce_resnorm(h, partial, residual, ln, a_out, ss, False)
 
+    def all_gather_last(x, out=None):
+        # the real IPC all-gather kernel (one-rank communicator: the own shard's staging
+        # write, flag exchange and store), then the shard repeated to the full width
+        flat = x.contiguous().view(-1, x.shape[-1])
+        mine = torch.empty_like(flat)
+        torch.ops.akap.car_all_gather(h, flat, mine)
+        return torch.cat([mine.view_as(x)] * tp, dim=-1)
+
     comm.tp_all_reduce = all_reduce
     comm.tp_all_reduce_resnorm = resnorm
-    comm.tp_all_gather_last = lambda x, out=None: torch.cat([x] * tp, dim=-1)
+    comm.tp_all_gather_last = all_gather_last
 
 
 def main():

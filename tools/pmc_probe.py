@@ -45,13 +45,29 @@ def main() -> int:
     # MFMA: 8192^3 bf16 matmuls
     a = torch.randn(8192, 8192, dtype=torch.bfloat16, device="cuda")
     b = torch.randn(8192, 8192, dtype=torch.bfloat16, device="cuda")
-    s.once()
-    for _ in range(30):
-        a @ b
+    c = torch.empty_like(a)
+    for _ in range(3):
+        torch.matmul(a, b, out=c)
     torch.cuda.synchronize()
     s.once()
-    res["matmul"] = {"derived": s.derived(), "rates": s.rates}
-    print("matmul derived:", json.dumps(s.derived()), flush=True)
+    t0 = time.time()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    n = 0
+    while time.time() - t0 < 1.5:  # ~1.5 s of back-to-back MFMA-bound work
+        for _ in range(20):
+            torch.matmul(a, b, out=c)
+        n += 20
+        torch.cuda.synchronize()
+    e1.record()
+    torch.cuda.synchronize()
+    gpu_s = e0.elapsed_time(e1) / 1e3
+    s.once()
+    res["matmul"] = {"derived": s.derived(), "rates": s.rates, "gpu_seconds": gpu_s,
+                     "host_seconds": time.time() - t0,
+                     "tflops": n * 2 * 8192 ** 3 / gpu_s / 1e12}
+    print("matmul derived:", json.dumps(s.derived()), "tflops", res["matmul"]["tflops"],
+          "rates", json.dumps(s.rates), flush=True)
     # idle
     time.sleep(1.0)
     s.once()
