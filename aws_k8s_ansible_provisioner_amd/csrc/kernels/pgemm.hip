@@ -48,9 +48,7 @@ namespace akap {
 constexpr int PG_T = 256;        // tile rows / cols
 constexpr int PG_BK = 64;        // K tile
 constexpr int PG_THREADS = 512;  // 8 waves
-constexpr int PG_SLOT = 128 * 8;  // 16-B units per half-tile slot (128 rows x 64 k = 16 KB)
-constexpr int PG_SLOTS = 10;      // LDS ring: 10 x 16 KB = all 160 KB of the CU
-constexpr int PG_D = 10;          // issue distance in half-tiles (<= PG_SLOTS)
+constexpr int PG_BUF = 2 * PG_T * 8;  // 16-B units per LDS buffer (A 256 rows + W 256 rows)
 
 __device__ __forceinline__ int pg_unit(int row, int chunk) {
   return row * 8 + (chunk ^ ((row >> 1) & 7));
@@ -71,22 +69,13 @@ __device__ __forceinline__ void pg_sync() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// wait until at most 2 * `later` of this wave's DMA instructions (2 per half-tile) are
-// outstanding; later <= PG_D - 2 (the prologue's wait)
+// wait until at most 2 * `later` of this wave's DMA instructions are outstanding
 __device__ __forceinline__ void pg_wait(int later) {
-  switch (later) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-  }
+  if (later >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (later == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (later == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-static_assert(PG_D <= PG_SLOTS && PG_D - 2 <= 8, "pg_wait covers later <= 8");
 
 template <int V>
 struct HalfTile {
@@ -99,7 +88,7 @@ using H3 = HalfTile<3>;  // A rows of the bottom quadrants
 
 template <int EPI, bool GROUPED>
 __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
-  __shared__ bf16x8 lds[PG_SLOTS * PG_SLOT];
+  __shared__ bf16x8 lds[2 * PG_BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -150,40 +139,45 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   const bf16* W = static_cast<const bf16*>(p.W) + (GROUPED ? (size_t)group * p.N * p.K : 0);
 
   // ---- per-lane DMA sources: half-tile h (0 A top, 1 W left, 2 W right, 3 A bottom), the
-  // wave's two 8-row pieces q = 2w, 2w+1 of its 128 slot rows.  Slot row lr of an A half is
-  // tile row (lr >> 6) * 128 + (h == 3) * 64 + (lr & 63); of a W half, tile column
-  // (lr >> 5) * 64 + (h == 2) * 32 + (lr & 31).  Rows past the tile's valid range re-read a
+  // wave's two 8-row pieces q = 2w, 2w+1 of it.  Rows past the tile's valid range re-read a
   // valid row (results never stored).
   const bf16* src[4][2];
+  int dst[4][2];  // 16-B unit offset inside a buffer
 #pragma unroll
   for (int h = 0; h < 4; ++h)
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int lr = (2 * w + e) * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((lr >> 1) & 7);
+      const int q = 2 * w + e;
+      int r0;
+      if (h == 0) r0 = (q >> 3) * 128 + (q & 7) * 8;
+      else if (h == 3) r0 = (q >> 3) * 128 + 64 + (q & 7) * 8;
+      else if (h == 1) r0 = (q >> 2) * 64 + (q & 3) * 8;
+      else r0 = (q >> 2) * 64 + 32 + (q & 3) * 8;
+      const int row = r0 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
       if (h == 0 || h == 3) {
-        const int m = m0 + (lr >> 6) * 128 + (h == 3 ? 64 : 0) + (lr & 63);
+        const int m = m0 + row;
         src[h][e] = X + (size_t)(m < row_hi ? m : row_lo) * p.ldx + chunk * 8;
+        dst[h][e] = r0 * 8;
       } else {
-        const int v = n0 + (lr >> 5) * 64 + (h == 2 ? 32 : 0) + (lr & 31);
+        const int v = n0 + row;
         int wr = v;
         if constexpr (EPI == EPI_SILU) wr = ((v >> 4) & 1) * (p.N >> 1) + (v >> 5) * 16 + (v & 15);
         src[h][e] = W + (size_t)wr * p.K + chunk * 8;
+        dst[h][e] = PG_T * 8 + r0 * 8;
       }
     }
-  const int dst0 = 2 * w * 64;  // the wave's first 16-B unit inside a slot (8 rows x 8 units)
-  // half-tile seq s = 4 j + h lives in slot s % PG_SLOTS; every call site names h at compile
-  // time (no dynamic register indexing)
-  auto slot = [&](int s) { return lds + (s % PG_SLOTS) * PG_SLOT; };
+  // half-tile seq s = 4 j + h (tile j, h in consumption order A top, W left, W right, A bottom);
+  // every call site names h at compile time (no dynamic register indexing)
   auto issue = [&](auto hc, int j) {
     constexpr int h = decltype(hc)::value;
     if (j >= nk) return;
-    bf16x8* buf = slot(4 * j + h);
+    bf16x8* buf = lds + (j & 1) * PG_BUF;
     const int k0 = j * PG_BK;
 #pragma unroll
-    for (int e = 0; e < 2; ++e) pg_glds(src[h][e] + k0, buf + dst0 + e * 64);
+    for (int e = 0; e < 2; ++e) pg_glds(src[h][e] + k0, buf + dst[h][e]);
   };
-  auto later = [&](int s) { return min(PG_D - 3, 4 * nk - 1 - s); };
+  auto later = [&](int s) { return min(3, 4 * nk - 1 - s); };
 
   // ---- fragments -----------------------------------------------------------------------------
   bf16x8 at[4][2], ab[4][2], bl[2][2], br[2][2];
@@ -193,17 +187,19 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto rd_a = [&](bf16x8 (&a)[4][2], const bf16x8* buf) {
+  auto rd_a = [&](bf16x8 (&a)[4][2], const bf16x8* buf, int half) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) a[i][s] = buf[pg_unit(wm * 64 + i * 16 + fr, fg + 4 * s)];
+      for (int s = 0; s < 2; ++s)
+        a[i][s] = buf[pg_unit(wm * 128 + half * 64 + i * 16 + fr, fg + 4 * s)];
   };
-  auto rd_b = [&](bf16x8 (&b)[2][2], const bf16x8* buf) {
+  auto rd_b = [&](bf16x8 (&b)[2][2], const bf16x8* buf, int half) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) b[j][s] = buf[pg_unit(wn * 32 + j * 16 + fr, fg + 4 * s)];
+      for (int s = 0; s < 2; ++s)
+        b[j][s] = buf[PG_T * 8 + pg_unit(wn * 64 + half * 32 + j * 16 + fr, fg + 4 * s)];
   };
   auto mma = [&](const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int i0, int j0) {
     __builtin_amdgcn_s_setprio(1);
@@ -218,50 +214,49 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // ---- prologue: half-tiles 0..PG_D-1 in flight, tile 0's A top + W left in registers ------
+  // ---- prologue: half-tiles 0..5 in flight, tile 0's A top + W left in registers -------------
   issue(H0{}, 0);
   issue(H1{}, 0);
   issue(H2{}, 0);
   issue(H3{}, 0);
   issue(H0{}, 1);
   issue(H1{}, 1);
-  issue(H2{}, 1);
-  issue(H3{}, 1);
-  issue(H0{}, 2);
-  issue(H1{}, 2);
-  static_assert(PG_D == 10, "prologue issues seqs 0..9");
-  pg_wait(min(PG_D, 4 * nk) - 2);  // seqs 0, 1 landed
+  {
+    const int outstanding = min(6, 4 * nk) - 2;  // half-tiles after seq 1 already issued
+    if (outstanding >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // nk == 1: seqs 2, 3 after it
+  }
   pg_sync();
-  rd_a(at, slot(0));
-  rd_b(bl, slot(1));
+  rd_a(at, lds, 0);
+  rd_b(bl, lds, 0);
 
-  // phase P = 4 t + (phase - 1) issues seq P + PG_D into the slot of seq P, whose last
-  // reads (phase <= P - 1) retired before this phase's barrier
   for (int t = 0; t < nk; ++t) {
-    // phase 1: W right of t landed -> its fragments; quadrant top x left
+    const bf16x8* cur = lds + (t & 1) * PG_BUF;
+    const bf16x8* nxt = lds + ((t + 1) & 1) * PG_BUF;
+    // phase 1: W right of t landed -> its fragments; DMA W right (t+1); quadrant top x left
     pg_wait(later(4 * t + 2));
     pg_sync();
-    rd_b(br, slot(4 * t + 2));
-    issue(H2{}, t + 2);
+    rd_b(br, cur, 1);
+    issue(H2{}, t + 1);
     mma(at, bl, 0, 0);
-    // phase 2: A bottom of t -> fragments; quadrant top x right
+    // phase 2: A bottom of t -> fragments; DMA A bottom (t+1); quadrant top x right
     pg_wait(later(4 * t + 3));
     pg_sync();
-    rd_a(ab, slot(4 * t + 3));
-    issue(H3{}, t + 2);
+    rd_a(ab, cur, 1);
+    issue(H3{}, t + 1);
     mma(at, br, 0, 2);
-    // phase 3: quadrant bottom x left
+    // phase 3: buffer t&1 fully read -> DMA A top (t+2) into it; quadrant bottom x left
     pg_sync();
-    issue(H0{}, t + 3);
+    issue(H0{}, t + 2);
     mma(ab, bl, 4, 0);
-    // phase 4: A top + W left of t+1 -> fragments; quadrant bottom x right
+    // phase 4: A top + W left of t+1 -> fragments; DMA W left (t+2); quadrant bottom x right
     if (t + 1 < nk) {
       pg_wait(later(4 * (t + 1) + 1));
       pg_sync();
-      rd_a(at, slot(4 * (t + 1)));
-      rd_b(bl, slot(4 * (t + 1) + 1));
+      rd_a(at, nxt, 0);
+      rd_b(bl, nxt, 0);
     }
-    issue(H1{}, t + 3);
+    issue(H1{}, t + 2);
     mma(ab, br, 4, 2);
   }
 

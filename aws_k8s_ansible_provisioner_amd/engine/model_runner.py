@@ -152,12 +152,15 @@ class ModelRunner:
             return max(64, min(4096, (self.max_seqs * self.ecfg.max_model_len) // self.bs + 8))
         torch.cuda.synchronize()
         free, total = torch.cuda.mem_get_info(self.device)
-        used = total - free
+        # this process's own footprint (allocator + ~1 GiB of runtime / library state), not
+        # the device-wide total - free: ranks that share one GPU (P/D or TP rehearsals) each
+        # get their gpu_memory_utilization share, whichever sizes its cache first
+        used = torch.cuda.memory_reserved(self.device) + 2**30
         d = self.mcfg.hidden_size
         width = d * 4 + (self.model.hq + 2 * self.model.hkv) * self.model.D + 3 * self.model.ffn
         act = self.cap_tokens * width * 2 * 3 + self.max_seqs * self.mcfg.vocab_size * 12
         reserve = act + 3 * 2**30
-        budget = total * self.ecfg.gpu_memory_utilization - used - reserve
+        budget = min(total * self.ecfg.gpu_memory_utilization - used, free) - reserve
         n = int(budget // per_block)
         if n < self.max_blocks:
             raise RuntimeError(f"not enough HBM for the KV cache ({budget / 2**30:.1f} GiB)")

@@ -10,7 +10,12 @@ previous read, plus derived series:
   akap_gpu_pmc_up                              1 while reads succeed
   akap_gpu_pmc_rate{counter="SQ_WAVES"}        events per second, every collected counter
   akap_gpu_pmc_gpu_busy_ratio                  GRBM_GUI_ACTIVE / GRBM_COUNT
-  akap_gpu_pmc_mfma_busy_ratio                 SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES, per SIMD
+  akap_gpu_pmc_mfma_busy_ratio                 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x CUs per
+                                               XCD x 4 SIMDs): GRBM counters are summed over the
+                                               8 XCDs, MFMA busy over every SIMD.  Calibrated on
+                                               back-to-back 8192^3 bf16 matmuls at 1.37 PFLOP/s:
+                                               0.68, vs 0.64 of the clock-scaled peak
+                                               (profiles/r4_pmc_probe.log)
   akap_gpu_pmc_mem_read_bytes_per_second       TCC_EA0_RDREQ x 128 B (memory-side reads: HBM +
                                                Infinity Cache; 128-B requests, the calibration of
                                                profiles/r3_pmc_calibrated_decode.md)
@@ -33,6 +38,7 @@ from typing import Optional
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(PKG, "libakap_pmc.so")
 SIMDS_PER_CU = 4
+CUS_PER_XCD = int(os.environ.get("AKAP_PMC_CUS_PER_XCD", "32"))  # MI355X: 256 CUs / 8 XCDs
 
 
 def tool_env() -> dict:
@@ -136,9 +142,9 @@ class PMCSampler:
         out = {}
         if r.get("GRBM_COUNT"):
             out["gpu_busy_ratio"] = r.get("GRBM_GUI_ACTIVE", 0.0) / r["GRBM_COUNT"]
-        if r.get("SQ_BUSY_CYCLES"):
+        if r.get("GRBM_GUI_ACTIVE"):
             out["mfma_busy_ratio"] = min(1.0, r.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) /
-                                         (r["SQ_BUSY_CYCLES"] * SIMDS_PER_CU))
+                                         (r["GRBM_GUI_ACTIVE"] * CUS_PER_XCD * SIMDS_PER_CU))
         if "TCC_EA0_RDREQ_sum" in r:
             out["mem_read_bytes_per_second"] = r["TCC_EA0_RDREQ_sum"] * 128.0
         if "TCC_EA0_WRREQ_sum" in r:

@@ -29,7 +29,8 @@ def test_pmc_rates_cumulative_counters(monkeypatch):
     assert abs(s.rates["GRBM_COUNT"] - 1e9) < 1  # (4e9 - 2e9) / 2 s
     d = s.derived()
     assert abs(d["gpu_busy_ratio"] - 0.5) < 1e-9
-    assert abs(d["mfma_busy_ratio"] - 0.5) < 1e-9   # 1e9 / (5e8 x 4 SIMDs)
+    # MFMA busy over every SIMD vs XCD-summed GUI_ACTIVE: 1e9 / (1e9 x 32 CUs/XCD x 4 SIMDs)
+    assert abs(d["mfma_busy_ratio"] - 1.0 / 128) < 1e-9
     assert abs(d["mem_read_bytes_per_second"] - 0.5e8 * 128) < 1
     text = s.text()
     assert 'akap_gpu_pmc_up{rank="3"} 1' in text
