@@ -31,11 +31,11 @@
 // holds 4 CONSECUTIVE output columns of one row per lane, stored as one 8-byte write.
 //
 // Grid: XCD-aware (common.h xcd_remap: 32 consecutive logical tiles share an XCD and its L2)
-// and grouped rasterisation (8 M-tiles x N-tiles per group, M fastest), so the WGs of one XCD
-// stream the same K slices of 8 X panels and 4 W panels together.
-// Grouped (MoE): group g owns rows [offs[g-1], offs[g]) of X and weight W + g*N*K; the grid is
-// an upper bound (sum of ceil(rows_g / 256) <= ceil(M / 256) + G) and surplus WGs exit.
-//
+// and grouped rasterisation (8 M-tiles x N-tiles per block, M fastest), so the WGs of one XCD
+// stream the same K slices of 8 X panels and 4 W panels together (pg_tile).
+// Grouped (MoE): group g owns rows [offs[g-1], offs[g]) of X and weight W + g*N*K; the same
+// raster runs over the concatenated list of every group's M tiles; the grid is an upper bound
+// (sum of ceil(rows_g / 256) <= ceil(M / 256) + G) and surplus WGs exit.
 // SwiGLU epilogue (EPI_SILU): W rows are the [gate; up] halves of a [2F, K] weight; tile column
 // v reads weight row ((v >> 4) & 1) * F + (v >> 5) * 16 + (v & 15) (the gdgemm.hip mapping), so
 // gate and up of one output column land in the same lane of adjacent fragments and the kernel
@@ -86,6 +86,50 @@ using H1 = HalfTile<1>;  // W rows of the left quadrants
 using H2 = HalfTile<2>;  // W rows of the right quadrants
 using H3 = HalfTile<3>;  // A rows of the bottom quadrants
 
+// Workgroup -> output tile.  Dense: XCD-aware ids (common.h xcd_remap: 32 consecutive ids per
+// XCD) rasterised in blocks of GM M-tiles x all N-tiles, M fastest, so the WGs of one XCD share
+// a few X and W panels in its L2.  Grouped (MoE): the same raster over the concatenated list of
+// every group's M tiles (group g owns rows [offs[g-1], offs[g]), ceil(rows_g / 256) tiles); the
+// grid is the upper bound ceil(M / 256) + G tiles and surplus ids return false (uniform).
+template <bool GROUPED>
+__device__ __forceinline__ bool pg_tile(const PGemmArgs& p, int& tm, int& tn, int& group,
+                                        int& row_lo, int& row_hi) {
+  constexpr int GM = 8;
+  const int tiles_n = p.N / PG_T;
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tiles_m = nwg / tiles_n;  // dense: exact; grouped: the upper bound
+  const int per_block = GM * tiles_n;
+  const int first_m = (id / per_block) * GM;
+  const int gm = min(tiles_m - first_m, GM);
+  const int in = id % per_block;
+  int mt = first_m + in % gm;
+  tn = in / gm;
+  group = 0;
+  row_lo = 0;
+  row_hi = p.M;
+  if constexpr (!GROUPED) {
+    tm = mt;
+    return true;
+  } else {
+    int lo = 0;
+    for (int g = 0; g < p.groups; ++g) {
+      const int hi = p.offs[g];
+      const int nt = (hi - lo + PG_T - 1) / PG_T;
+      if (mt < nt) {
+        tm = mt;
+        group = g;
+        row_lo = lo;
+        row_hi = hi;
+        return true;
+      }
+      mt -= nt;
+      lo = hi;
+    }
+    return false;
+  }
+}
+
 template <int EPI, bool GROUPED>
 __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   __shared__ bf16x8 lds[2 * PG_BUF];
@@ -95,44 +139,8 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   const int fr = lane & 15, fg = lane >> 4;
 
   // ---- tile of this workgroup --------------------------------------------------------------
-  const int tiles_n = p.N / PG_T;
-  int row_lo = 0, row_hi = p.M, tm, tn, group = 0;
-  {
-    const int nwg = gridDim.x;
-    const int id = xcd_remap(blockIdx.x, nwg);
-    if constexpr (!GROUPED) {
-      const int tiles_m = (p.M + PG_T - 1) / PG_T;
-      constexpr int GM = 8;
-      const int per_group = GM * tiles_n;
-      const int g0 = id / per_group;
-      const int first_m = g0 * GM;
-      const int gm = min(tiles_m - first_m, GM);
-      const int in = id % per_group;
-      tm = first_m + in % gm;
-      tn = in / gm;
-    } else {
-      // tiles of group g: ceil(rows_g / 256) x tiles_n, groups in order, N fastest within a
-      // group's M tile
-      tn = id % tiles_n;
-      int mt = id / tiles_n;
-      tm = -1;
-      int lo = 0;
-      for (int g = 0; g < p.groups; ++g) {
-        const int hi = p.offs[g];
-        const int nt = (hi - lo + PG_T - 1) / PG_T;
-        if (mt < nt) {
-          tm = mt;
-          group = g;
-          row_lo = lo;
-          row_hi = hi;
-          break;
-        }
-        mt -= nt;
-        lo = hi;
-      }
-      if (tm < 0) return;  // surplus workgroup of the upper-bound grid (uniform)
-    }
-  }
+  int tm, tn, group, row_lo, row_hi;
+  if (!pg_tile<GROUPED>(p, tm, tn, group, row_lo, row_hi)) return;  // surplus WG (uniform)
   const int m0 = row_lo + tm * PG_T, n0 = tn * PG_T;
   const int nk = p.K / PG_BK;
   const bf16* X = static_cast<const bf16*>(p.X);
@@ -316,42 +324,8 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm3_kernel(PGemmArgs p) {
   const int wm = w >> 2, wn = w & 3;
   const int fr = lane & 15, fg = lane >> 4;
 
-  const int tiles_n = p.N / PG_T;
-  int row_lo = 0, row_hi = p.M, tm, tn, group = 0;
-  {
-    const int nwg = gridDim.x;
-    const int id = xcd_remap(blockIdx.x, nwg);
-    if constexpr (!GROUPED) {
-      const int tiles_m = (p.M + PG_T - 1) / PG_T;
-      constexpr int GM = 8;
-      const int per_group = GM * tiles_n;
-      const int g0 = id / per_group;
-      const int first_m = g0 * GM;
-      const int gm = min(tiles_m - first_m, GM);
-      const int in = id % per_group;
-      tm = first_m + in % gm;
-      tn = in / gm;
-    } else {
-      tn = id % tiles_n;
-      int mt = id / tiles_n;
-      tm = -1;
-      int lo = 0;
-      for (int g = 0; g < p.groups; ++g) {
-        const int hi = p.offs[g];
-        const int nt = (hi - lo + PG_T - 1) / PG_T;
-        if (mt < nt) {
-          tm = mt;
-          group = g;
-          row_lo = lo;
-          row_hi = hi;
-          break;
-        }
-        mt -= nt;
-        lo = hi;
-      }
-      if (tm < 0) return;
-    }
-  }
+  int tm, tn, group, row_lo, row_hi;
+  if (!pg_tile<GROUPED>(p, tm, tn, group, row_lo, row_hi)) return;  // surplus WG (uniform)
   const int m0 = row_lo + tm * PG_T, n0 = tn * PG_T;
   const int nk = p.K / 32;  // even (K % 64 == 0)
   const bf16* X = static_cast<const bf16*>(p.X);
