@@ -316,12 +316,14 @@ __device__ __forceinline__ int p3_unit(int row, int chunk) {
   return row * P3_ROWU + (chunk ^ ((-(row >> 2)) & 3));
 }
 
-template <int EPI, bool GROUPED, int NS>
-__global__ __launch_bounds__(PG_THREADS, 1) void pgemm3_kernel(PGemmArgs p) {
+// WM x WN waves, each owning a (256 / WM) x (256 / WN) sub-tile
+template <int EPI, bool GROUPED, int NS, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 1) void pgemm3_kernel(PGemmArgs p) {
+  constexpr int NW = WM * WN, FA = 256 / WM / 16, FB = 256 / WN / 16, DPW = 32 / NW;
   __shared__ bf16x8 lds[NS * P3_SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / WN, wn = w % WN;
   const int fr = lane & 15, fg = lane >> 4;
 
   int tm, tn, group, row_lo, row_hi;
@@ -331,12 +333,12 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm3_kernel(PGemmArgs p) {
   const bf16* X = static_cast<const bf16*>(p.X);
   const bf16* W = static_cast<const bf16*>(p.W) + (GROUPED ? (size_t)group * p.N * p.K : 0);
 
-  // DMA: 32 instructions per slot (16 rows x 64 B each), 4 per wave; waves 0-3 stage A rows,
-  // waves 4-7 W rows
-  const bf16* src[4];
+  // DMA: 32 instructions per slot (16 rows x 64 B each), DPW per wave; the first half of the
+  // instructions stage A rows, the second half W rows
+  const bf16* src[DPW];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int q = w * 4 + e;
+  for (int e = 0; e < DPW; ++e) {
+    const int q = w * DPW + e;
     const int lr = (q & 15) * 16 + (lane >> 2);  // row within the A or W half of the slot
     const int chunk = (lane & 3) ^ ((-(lr >> 2)) & 3);
     if (q < 16) {
@@ -349,47 +351,56 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm3_kernel(PGemmArgs p) {
       src[e] = W + (size_t)wr * p.K + chunk * 8;
     }
   }
-  const int dst0 = w * 4 * 64;
+  const int dst0 = w * DPW * 64;
   auto issue = [&](int j) {
     if (j >= nk) return;
     bf16x8* buf = lds + (j % NS) * P3_SLOT;
     const int k0 = j * 32;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) pg_glds(src[e] + k0, buf + dst0 + e * 64);
+    for (int e = 0; e < DPW; ++e) pg_glds(src[e] + k0, buf + dst0 + e * 64);
   };
   // wait until step j's DMAs (this wave's) landed: steps issued so far end at min(j0, nk - 1)
   auto wait_for = [&](int j, int issued_last) {
     const int later = min(issued_last, nk - 1) - j;  // steps after j still allowed in flight
-    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (DPW == 4) {
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      static_assert(DPW == 8, "4 or 8 waves");
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   };
 
-  bf16x8 a0[8], b0[4], a1[8], b1[4];
-  f32x4 acc[8][4];
+  bf16x8 a0[FA], b0[FB], a1[FA], b1[FB];
+  f32x4 acc[FA][FB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < FA; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto rd = [&](bf16x8 (&a)[8], bf16x8 (&b)[4], int j) {
+  auto rd = [&](bf16x8 (&a)[FA], bf16x8 (&b)[FB], int j) {
     const bf16x8* buf = lds + (j % NS) * P3_SLOT;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = buf[p3_unit(wm * 128 + i * 16 + fr, fg)];
+    for (int i = 0; i < FA; ++i) a[i] = buf[p3_unit(wm * (FA * 16) + i * 16 + fr, fg)];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) b[jj] = buf[PG_T * P3_ROWU + p3_unit(wn * 64 + jj * 16 + fr, fg)];
+    for (int jj = 0; jj < FB; ++jj)
+      b[jj] = buf[PG_T * P3_ROWU + p3_unit(wn * (FB * 16) + jj * 16 + fr, fg)];
   };
-  auto mma = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[4]) {
+  auto mma = [&](const bf16x8 (&a)[FA], const bf16x8 (&b)[FB]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < FA; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < FB; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
   // one K step: the next step's fragments land in (an, bn) while (ac, bc) feed the MFMAs
-  auto step = [&](int t, bf16x8 (&ac)[8], bf16x8 (&bc)[4], bf16x8 (&an)[8], bf16x8 (&bn)[4]) {
+  auto step = [&](int t, bf16x8 (&ac)[FA], bf16x8 (&bc)[FB], bf16x8 (&an)[FA],
+                  bf16x8 (&bn)[FB]) {
     if (t + 1 < nk) {
       wait_for(t + 1, t + NS - 1);
       pg_sync();  // step t+1 landed for every wave; every read of step t's slot retired
@@ -411,13 +422,13 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm3_kernel(PGemmArgs p) {
 
   bf16* Y = static_cast<bf16*>(p.Y);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = m0 + wm * 128 + i * 16 + fr;
+  for (int i = 0; i < FA; ++i) {
+    const int row = m0 + wm * (FA * 16) + i * 16 + fr;
     if (row >= row_hi) continue;
     if constexpr (EPI == EPI_SILU) {
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int col = (n0 >> 1) + wn * 32 + jj * 16 + fg * 4;
+      for (int jj = 0; jj < FB / 2; ++jj) {
+        const int col = (n0 >> 1) + wn * (FB * 8) + jj * 16 + fg * 4;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -429,8 +440,8 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm3_kernel(PGemmArgs p) {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + j * 16 + fg * 4;
+      for (int j = 0; j < FB; ++j) {
+        const int col = n0 + wn * (FB * 16) + j * 16 + fg * 4;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[i][j][r]);
@@ -444,14 +455,15 @@ bool pgemm_supported(int M, int N, int K) {
   return M > 0 && N > 0 && N % PG_T == 0 && K >= PG_BK && K % PG_BK == 0;
 }
 
-template <int NS>
+template <int NS, int WM, int WN>
 static void launch_pgemm3(const PGemmArgs& p, int epi, int grid, hipStream_t st) {
+  constexpr int T = 64 * WM * WN;
   if (p.groups > 0) {
-    if (epi == EPI_SILU) pgemm3_kernel<EPI_SILU, true, NS><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm3_kernel<EPI_STORE, true, NS><<<grid, PG_THREADS, 0, st>>>(p);
+    if (epi == EPI_SILU) pgemm3_kernel<EPI_SILU, true, NS, WM, WN><<<grid, T, 0, st>>>(p);
+    else pgemm3_kernel<EPI_STORE, true, NS, WM, WN><<<grid, T, 0, st>>>(p);
   } else {
-    if (epi == EPI_SILU) pgemm3_kernel<EPI_SILU, false, NS><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm3_kernel<EPI_STORE, false, NS><<<grid, PG_THREADS, 0, st>>>(p);
+    if (epi == EPI_SILU) pgemm3_kernel<EPI_SILU, false, NS, WM, WN><<<grid, T, 0, st>>>(p);
+    else pgemm3_kernel<EPI_STORE, false, NS, WM, WN><<<grid, T, 0, st>>>(p);
   }
 }
 
@@ -464,8 +476,10 @@ void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
   const int tiles_n = p.N / PG_T;
   const int grid = p.groups > 0 ? ((p.M + PG_T - 1) / PG_T + p.groups) * tiles_n
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
-  if (variant == 33) return launch_pgemm3<3>(p, epi, grid, st);
-  if (variant == 34) return launch_pgemm3<4>(p, epi, grid, st);
+  if (variant == 33) return launch_pgemm3<3, 2, 4>(p, epi, grid, st);
+  if (variant == 34) return launch_pgemm3<4, 2, 4>(p, epi, grid, st);
+  if (variant == 43) return launch_pgemm3<3, 2, 2>(p, epi, grid, st);
+  if (variant == 44) return launch_pgemm3<4, 2, 2>(p, epi, grid, st);
   if (p.groups > 0) {
     if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true><<<grid, PG_THREADS, 0, st>>>(p);
     else pgemm_kernel<EPI_STORE, true><<<grid, PG_THREADS, 0, st>>>(p);

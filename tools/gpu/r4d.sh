@@ -7,7 +7,11 @@ PM="python3 tools/pgemm_pmc_probe.py"
 P="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
 AKAP_PGEMM_V=33 run t33 200 $P tests/test_kernels_gpu.py -k pgemm &&
 AKAP_PGEMM_V=34 run t34 200 $P tests/test_kernels_gpu.py -k pgemm &&
+AKAP_PGEMM_V=43 run t43 200 $P tests/test_kernels_gpu.py -k pgemm &&
+AKAP_PGEMM_V=44 run t44 200 $P tests/test_kernels_gpu.py -k pgemm &&
 AKAP_PGEMM_V=33 run b33 300 python -u tools/pgemm_bench.py &&
+AKAP_PGEMM_V=43 run b43 300 python -u tools/pgemm_bench.py &&
+AKAP_PGEMM_V=44 run b44 300 python -u tools/pgemm_bench.py &&
 AKAP_PGEMM_V=34 run b34 300 python -u tools/pgemm_bench.py &&
 run b1 300 python -u tools/pgemm_bench.py &&
 C1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
