@@ -301,185 +301,15 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   }
 }
 
-// ---- v3 (A/B candidate): 32-deep K steps, ONE barrier per step ------------------------------
-// Slot = one 32-k step of A (256 rows) and W (256 rows), 64-B rows (4 chunks of 16 B), 32 KB;
-// NS slots, the step t + NS DMA'd while step t computes.  Each wave reads the NEXT step's 12
-// fragments into the other register set while its 32 MFMAs run on this step's (the loop is
-// unrolled by 2 so both sets stay in named registers).  Swizzle for 64-B rows: chunk c of row
-// r sits at c ^ g((r >> 2) & 3), g = {0, 3, 2, 1}: each ds_read_b128 lane group then covers
-// all 16 16-B bank slots once (worked through for the four lane groups in the docstring of
-// MI355X_MICROARCH.md's LDS table).
-constexpr int P3_ROWU = 4;                // 16-B units per 64-B row
-constexpr int P3_SLOT = 2 * PG_T * P3_ROWU;  // units per slot (A then W): 2048 = 32 KB
-
-__device__ __forceinline__ int p3_unit(int row, int chunk) {
-  return row * P3_ROWU + (chunk ^ ((-(row >> 2)) & 3));
-}
-
-// WM x WN waves, each owning a (256 / WM) x (256 / WN) sub-tile
-template <int EPI, bool GROUPED, int NS, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN, 1) void pgemm3_kernel(PGemmArgs p) {
-  constexpr int NW = WM * WN, FA = 256 / WM / 16, FB = 256 / WN / 16, DPW = 32 / NW;
-  __shared__ bf16x8 lds[NS * P3_SLOT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w / WN, wn = w % WN;
-  const int fr = lane & 15, fg = lane >> 4;
-
-  int tm, tn, group, row_lo, row_hi;
-  if (!pg_tile<GROUPED>(p, tm, tn, group, row_lo, row_hi)) return;  // surplus WG (uniform)
-  const int m0 = row_lo + tm * PG_T, n0 = tn * PG_T;
-  const int nk = p.K / 32;  // even (K % 64 == 0)
-  const bf16* X = static_cast<const bf16*>(p.X);
-  const bf16* W = static_cast<const bf16*>(p.W) + (GROUPED ? (size_t)group * p.N * p.K : 0);
-
-  // DMA: 32 instructions per slot (16 rows x 64 B each), DPW per wave; the first half of the
-  // instructions stage A rows, the second half W rows
-  const bf16* src[DPW];
-#pragma unroll
-  for (int e = 0; e < DPW; ++e) {
-    const int q = w * DPW + e;
-    const int lr = (q & 15) * 16 + (lane >> 2);  // row within the A or W half of the slot
-    const int chunk = (lane & 3) ^ ((-(lr >> 2)) & 3);
-    if (q < 16) {
-      const int m = m0 + lr;
-      src[e] = X + (size_t)(m < row_hi ? m : row_lo) * p.ldx + chunk * 8;
-    } else {
-      const int v = n0 + lr;
-      int wr = v;
-      if constexpr (EPI == EPI_SILU) wr = ((v >> 4) & 1) * (p.N >> 1) + (v >> 5) * 16 + (v & 15);
-      src[e] = W + (size_t)wr * p.K + chunk * 8;
-    }
-  }
-  const int dst0 = w * DPW * 64;
-  auto issue = [&](int j) {
-    if (j >= nk) return;
-    bf16x8* buf = lds + (j % NS) * P3_SLOT;
-    const int k0 = j * 32;
-#pragma unroll
-    for (int e = 0; e < DPW; ++e) pg_glds(src[e] + k0, buf + dst0 + e * 64);
-  };
-  // wait until step j's DMAs (this wave's) landed: steps issued so far end at min(j0, nk - 1)
-  auto wait_for = [&](int j, int issued_last) {
-    const int later = min(issued_last, nk - 1) - j;  // steps after j still allowed in flight
-    if constexpr (DPW == 4) {
-      if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      static_assert(DPW == 8, "4 or 8 waves");
-      if (later >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (later == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  };
-
-  bf16x8 a0[FA], b0[FB], a1[FA], b1[FB];
-  f32x4 acc[FA][FB];
-#pragma unroll
-  for (int i = 0; i < FA; ++i)
-#pragma unroll
-    for (int j = 0; j < FB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto rd = [&](bf16x8 (&a)[FA], bf16x8 (&b)[FB], int j) {
-    const bf16x8* buf = lds + (j % NS) * P3_SLOT;
-#pragma unroll
-    for (int i = 0; i < FA; ++i) a[i] = buf[p3_unit(wm * (FA * 16) + i * 16 + fr, fg)];
-#pragma unroll
-    for (int jj = 0; jj < FB; ++jj)
-      b[jj] = buf[PG_T * P3_ROWU + p3_unit(wn * (FB * 16) + jj * 16 + fr, fg)];
-  };
-  auto mma = [&](const bf16x8 (&a)[FA], const bf16x8 (&b)[FB]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FA; ++i)
-#pragma unroll
-      for (int j = 0; j < FB; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  // one K step: the next step's fragments land in (an, bn) while (ac, bc) feed the MFMAs
-  auto step = [&](int t, bf16x8 (&ac)[FA], bf16x8 (&bc)[FB], bf16x8 (&an)[FA],
-                  bf16x8 (&bn)[FB]) {
-    if (t + 1 < nk) {
-      wait_for(t + 1, t + NS - 1);
-      pg_sync();  // step t+1 landed for every wave; every read of step t's slot retired
-      issue(t + NS);
-      rd(an, bn, t + 1);
-    }
-    mma(ac, bc);
-  };
-
-#pragma unroll
-  for (int j = 0; j < NS; ++j) issue(j);
-  wait_for(0, NS - 1);
-  pg_sync();
-  rd(a0, b0, 0);
-  for (int t = 0; t < nk; t += 2) {
-    step(t, a0, b0, a1, b1);
-    step(t + 1, a1, b1, a0, b0);
-  }
-
-  bf16* Y = static_cast<bf16*>(p.Y);
-#pragma unroll
-  for (int i = 0; i < FA; ++i) {
-    const int row = m0 + wm * (FA * 16) + i * 16 + fr;
-    if (row >= row_hi) continue;
-    if constexpr (EPI == EPI_SILU) {
-#pragma unroll
-      for (int jj = 0; jj < FB / 2; ++jj) {
-        const int col = (n0 >> 1) + wn * (FB * 8) + jj * 16 + fg * 4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = bf2f(f2bf(acc[i][2 * jj][r]));
-          const float u = bf2f(f2bf(acc[i][2 * jj + 1][r]));
-          o[r] = f2bf(bf2f(f2bf(g / (1.f + __expf(-g)))) * u);
-        }
-        *reinterpret_cast<bf16x4*>(Y + (size_t)row * p.ldy + col) = o;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        const int col = n0 + wn * (FB * 16) + j * 16 + fg * 4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[i][j][r]);
-        *reinterpret_cast<bf16x4*>(Y + (size_t)row * p.ldy + col) = o;
-      }
-    }
-  }
-}
-
 bool pgemm_supported(int M, int N, int K) {
   return M > 0 && N > 0 && N % PG_T == 0 && K >= PG_BK && K % PG_BK == 0;
 }
 
-template <int NS, int WM, int WN>
-static void launch_pgemm3(const PGemmArgs& p, int epi, int grid, hipStream_t st) {
-  constexpr int T = 64 * WM * WN;
-  if (p.groups > 0) {
-    if (epi == EPI_SILU) pgemm3_kernel<EPI_SILU, true, NS, WM, WN><<<grid, T, 0, st>>>(p);
-    else pgemm3_kernel<EPI_STORE, true, NS, WM, WN><<<grid, T, 0, st>>>(p);
-  } else {
-    if (epi == EPI_SILU) pgemm3_kernel<EPI_SILU, false, NS, WM, WN><<<grid, T, 0, st>>>(p);
-    else pgemm3_kernel<EPI_STORE, false, NS, WM, WN><<<grid, T, 0, st>>>(p);
-  }
-}
-
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
   if (p.M == 0) return;
-  static const int variant = [] {
-    const char* e = getenv("AKAP_PGEMM_V");
-    return e ? atoi(e) : 1;
-  }();
   const int tiles_n = p.N / PG_T;
   const int grid = p.groups > 0 ? ((p.M + PG_T - 1) / PG_T + p.groups) * tiles_n
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
-  if (variant == 33) return launch_pgemm3<3, 2, 4>(p, epi, grid, st);
-  if (variant == 34) return launch_pgemm3<4, 2, 4>(p, epi, grid, st);
-  if (variant == 43) return launch_pgemm3<3, 2, 2>(p, epi, grid, st);
-  if (variant == 44) return launch_pgemm3<4, 2, 2>(p, epi, grid, st);
   if (p.groups > 0) {
     if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true><<<grid, PG_THREADS, 0, st>>>(p);
     else pgemm_kernel<EPI_STORE, true><<<grid, PG_THREADS, 0, st>>>(p);
