@@ -94,6 +94,11 @@ def physical_devices(devs: list) -> int:
 
 def main() -> int:
     a = parse()
+    if os.environ.get("AKAP_BENCH_STACKS"):
+        # diagnostics: every N seconds, every thread's Python stack to stderr
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["AKAP_BENCH_STACKS"]), repeat=True)
     import torch
     import torch.distributed as dist
 
