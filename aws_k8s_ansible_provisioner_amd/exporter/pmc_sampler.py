@@ -62,6 +62,7 @@ class PMCSampler:
         self._prev: Optional[list] = None
         self._t_prev = 0.0
         self.cumulative: Optional[bool] = None
+        self.settle_s = 0.1
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
@@ -101,8 +102,12 @@ class PMCSampler:
             vals = self._read()
             now = time.monotonic()
             if self.cumulative is None:
-                # two back-to-back reads tell the service's semantics apart: cumulative
-                # counters barely move in between, per-read (reset) counters restart near 0
+                # the first read starts the counting context (values ~0): let the counters run
+                # for a moment, then two back-to-back reads tell the service's semantics apart
+                # -- cumulative counters barely move in between, per-read (reset) counters
+                # restart near 0
+                time.sleep(self.settle_s)
+                vals = self._read()
                 again = self._read()
                 now = time.monotonic()
                 big = [i for i, v in enumerate(vals) if v > 1e6]

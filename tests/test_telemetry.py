@@ -20,8 +20,9 @@ def test_pmc_rates_cumulative_counters(monkeypatch):
     """Device-counting reads that accumulate: rates are deltas over the read interval; the
     first read's back-to-back probe classifies the semantics."""
     s = PMCSampler(interval_s=1.0, labels={"rank": "3"})
+    s.settle_s = 0.0
     base = [2e9, 1e9, 5e8, 1e9, 1e8]
-    _fake(s, [base, base, [b * 2 for b in base]])
+    _fake(s, [[0.0] * 5, base, base, [b * 2 for b in base]])  # start read, settle, probe
     t = iter([10.0, 10.0, 12.0])
     monkeypatch.setattr("time.monotonic", lambda: next(t))
     assert s.once() and s.cumulative is True and s.rates == {}
@@ -42,7 +43,9 @@ def test_pmc_rates_cumulative_counters(monkeypatch):
 def test_pmc_rates_per_read_counters(monkeypatch):
     """Reads that restart from zero: each read is the interval's own count."""
     s = PMCSampler(interval_s=1.0)
-    _fake(s, [[2e9, 1e9, 5e8, 1e9, 1e8], [1e3, 1e3, 1e3, 1e3, 1e3], [4e9, 1e9, 5e8, 0, 2e8]])
+    s.settle_s = 0.0
+    _fake(s, [[0.0] * 5, [2e9, 1e9, 5e8, 1e9, 1e8], [1e3, 1e3, 1e3, 1e3, 1e3],
+              [4e9, 1e9, 5e8, 0, 2e8]])
     t = iter([10.0, 10.0, 14.0])
     monkeypatch.setattr("time.monotonic", lambda: next(t))
     assert s.once() and s.cumulative is False
