@@ -130,7 +130,7 @@ __device__ __forceinline__ bool pg_tile(const PGemmArgs& p, int& tm, int& tn, in
   }
 }
 
-template <int EPI, bool GROUPED>
+template <int EPI, bool GROUPED, int NB>
 __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   __shared__ bf16x8 lds[2 * PG_BUF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -149,7 +149,15 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   // ---- per-lane DMA sources: half-tile h (0 A top, 1 W left, 2 W right, 3 A bottom), the
   // wave's two 8-row pieces q = 2w, 2w+1 of it.  Rows past the tile's valid range re-read a
   // valid row (results never stored).
-  const bf16* src[4][2];
+  // DMA through buffer resources (buffer_load_dwordx4 ... lds): SGPR descriptors for X and W,
+  // 32-bit per-lane byte offsets (8 VGPRs for the 8 sources), the K position in the scalar
+  // offset.  X rows past M fall outside the descriptor's range and read as 0 (rows of a
+  // neighbouring group inside it are harmless: those accumulator rows are never stored).
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, (short)0, (int)((size_t)p.M * p.ldx * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)W, (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
+  uint32_t voff[4][2];
   int dst[4][2];  // 16-B unit offset inside a buffer
 #pragma unroll
   for (int h = 0; h < 4; ++h)
@@ -164,14 +172,13 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
       const int row = r0 + (lane >> 3);
       const int chunk = (lane & 7) ^ ((row >> 1) & 7);
       if (h == 0 || h == 3) {
-        const int m = m0 + row;
-        src[h][e] = X + (size_t)(m < row_hi ? m : row_lo) * p.ldx + chunk * 8;
+        voff[h][e] = (uint32_t)(((m0 + row) * p.ldx + chunk * 8) * 2);
         dst[h][e] = r0 * 8;
       } else {
         const int v = n0 + row;
         int wr = v;
         if constexpr (EPI == EPI_SILU) wr = ((v >> 4) & 1) * (p.N >> 1) + (v >> 5) * 16 + (v & 15);
-        src[h][e] = W + (size_t)wr * p.K + chunk * 8;
+        voff[h][e] = (uint32_t)((wr * p.K + chunk * 8) * 2);
         dst[h][e] = PG_T * 8 + r0 * 8;
       }
     }
@@ -181,9 +188,12 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
     constexpr int h = decltype(hc)::value;
     if (j >= nk) return;
     bf16x8* buf = lds + (j & 1) * PG_BUF;
-    const int k0 = j * PG_BK;
+    const uint32_t kb = (uint32_t)(j * PG_BK * 2);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) pg_glds(src[h][e] + k0, buf + dst[h][e]);
+    for (int e = 0; e < 2; ++e)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          h == 0 || h == 3 ? rx : rw, (__attribute__((address_space(3))) void*)(buf + dst[h][e]),
+          16, voff[h][e], kb, 0, 0);
   };
   auto later = [&](int s) { return min(3, 4 * nk - 1 - s); };
 
@@ -238,28 +248,48 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   rd_a(at, lds, 0);
   rd_b(bl, lds, 0);
 
+  // outstanding half-tiles allowed while waiting for seq s when seqs <= last were issued
+  auto allow = [&](int s, int last) { return max(0, min(last, 4 * nk - 1) - s); };
   for (int t = 0; t < nk; ++t) {
     const bf16x8* cur = lds + (t & 1) * PG_BUF;
     const bf16x8* nxt = lds + ((t + 1) & 1) * PG_BUF;
-    // phase 1: W right of t landed -> its fragments; DMA W right (t+1); quadrant top x left
-    pg_wait(later(4 * t + 2));
-    pg_sync();
-    rd_b(br, cur, 1);
-    issue(H2{}, t + 1);
-    mma(at, bl, 0, 0);
-    // phase 2: A bottom of t -> fragments; DMA A bottom (t+1); quadrant top x right
-    pg_wait(later(4 * t + 3));
-    pg_sync();
-    rd_a(ab, cur, 1);
-    issue(H3{}, t + 1);
-    mma(at, br, 0, 2);
-    // phase 3: buffer t&1 fully read -> DMA A top (t+2) into it; quadrant bottom x left
-    pg_sync();
-    issue(H0{}, t + 2);
-    mma(ab, bl, 4, 0);
+    if constexpr (NB == 4) {
+      // phase 1: W right of t landed -> its fragments; DMA W right (t+1); quadrant top x left
+      pg_wait(later(4 * t + 2));
+      pg_sync();
+      rd_b(br, cur, 1);
+      issue(H2{}, t + 1);
+      mma(at, bl, 0, 0);
+      // phase 2: A bottom of t -> fragments; DMA A bottom (t+1); quadrant top x right
+      pg_wait(later(4 * t + 3));
+      pg_sync();
+      rd_a(ab, cur, 1);
+      issue(H3{}, t + 1);
+      mma(at, br, 0, 2);
+      // phase 3: buffer t&1 fully read -> DMA A top (t+2) into it; quadrant bottom x left
+      pg_sync();
+      issue(H0{}, t + 2);
+      mma(ab, bl, 4, 0);
+    } else {
+      // phase 1: W right + A bottom of t landed -> both fragment sets; DMA both for t+1
+      pg_wait(allow(4 * t + 3, 4 * t + 5));
+      pg_sync();
+      rd_b(br, cur, 1);
+      rd_a(ab, cur, 1);
+      issue(H2{}, t + 1);
+      issue(H3{}, t + 1);
+      mma(at, bl, 0, 0);
+      // phase 2 (no barrier): quadrant top x right
+      mma(at, br, 0, 2);
+      // phase 3 (no barrier): A top of t+2 into buffer t&1 -- its last reads (phase 4 of t-1)
+      // retired before phase 1's barrier; quadrant bottom x left
+      issue(H0{}, t + 2);
+      mma(ab, bl, 4, 0);
+    }
     // phase 4: A top + W left of t+1 -> fragments; DMA W left (t+2); quadrant bottom x right
     if (t + 1 < nk) {
-      pg_wait(later(4 * (t + 1) + 1));
+      if constexpr (NB == 4) pg_wait(later(4 * (t + 1) + 1));
+      else pg_wait(allow(4 * t + 5, 4 * t + 8));
       pg_sync();
       rd_a(at, nxt, 0);
       rd_b(bl, nxt, 0);
@@ -305,18 +335,28 @@ bool pgemm_supported(int M, int N, int K) {
   return M > 0 && N > 0 && N % PG_T == 0 && K >= PG_BK && K % PG_BK == 0;
 }
 
+template <int NB>
+static void launch_pgemm_nb(const PGemmArgs& p, int epi, int grid, hipStream_t st) {
+  if (p.groups > 0) {
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, NB><<<grid, PG_THREADS, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, true, NB><<<grid, PG_THREADS, 0, st>>>(p);
+  } else {
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, NB><<<grid, PG_THREADS, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, false, NB><<<grid, PG_THREADS, 0, st>>>(p);
+  }
+}
+
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
   if (p.M == 0) return;
   const int tiles_n = p.N / PG_T;
   const int grid = p.groups > 0 ? ((p.M + PG_T - 1) / PG_T + p.groups) * tiles_n
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
-  if (p.groups > 0) {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, true><<<grid, PG_THREADS, 0, st>>>(p);
-  } else {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, false><<<grid, PG_THREADS, 0, st>>>(p);
-  }
+  static const int nb = [] {
+    const char* e = getenv("AKAP_PGEMM_NB");
+    return e ? atoi(e) : 4;
+  }();
+  if (nb == 2) return launch_pgemm_nb<2>(p, epi, grid, st);
+  launch_pgemm_nb<4>(p, epi, grid, st);
 }
 
 }  // namespace akap
