@@ -4,22 +4,29 @@
 //
 // Tile: 256 x 256 outputs per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 per
 // wave = 8 x 4 MFMA 16x16x32 fragments, 128 accumulator VGPRs), K in 64-deep tiles through two
-// 64 KB LDS buffers filled by global_load_lds (LDS-DMA, 16 B per lane).  The K loop is cut into
-// four PHASES per K tile; each phase computes one 64 x 32 quadrant of the wave's outputs (16
-// MFMAs), and is bracketed by one raw s_barrier:
-//   phase | counted wait (this wave's DMAs) | ds_reads issued (for the NEXT phase) | DMA issued
-//   1     | B right half of tile t           | B right fragments (t)                 | B right (t+1)
-//   2     | A bottom half of tile t          | A bottom fragments (t)                | A bottom (t+1)
-//   3     | -- (WAR barrier only)            | --                                    | A top (t+2)
-//   4     | A top + B left halves of t+1     | A top + B left fragments (t+1)        | B left (t+2)
-// A "half-tile" is 128 rows x 64 k (16 KB: two 1-KiB DMA instructions per wave).  Half-tiles
-// are issued in the order the phases consume them, three ahead of their consumer, so every
-// wait is a counted `s_waitcnt vmcnt(6)` (never 0 in steady state: cdna_hip_programming.md
-// "Pipelining across barriers", T3+T4), each DMA has ~4 phases (~1 us) to land, and every
-// ds_read of a buffer sits one barrier after the wait that retired its bytes.  Fragment reads
-// for phase p+1 are issued in phase p before its MFMAs, so LDS latency hides under them.  One
-// __shared__ array (no second LDS object: the compiler would drain vmcnt in the loop, ibid.
-// item 4a), raw s_barrier (never __syncthreads, whose fence drains the DMAs in flight).
+// 64 KB LDS buffers filled by buffer_load_dwordx4 ... lds (LDS-DMA through SGPR buffer
+// descriptors: 32-bit per-lane offsets, X rows past M read as 0).  The K loop is cut into four
+// PHASES per K tile; each computes one 64 x 32 quadrant of the wave's outputs (16 MFMAs).  A
+// "half-tile" is 128 rows x 64 k (16 KB: two 1-KiB DMA instructions per wave), issued in the
+// order the phases consume them, so every wait is a counted `s_waitcnt vmcnt` (never 0 in
+// steady state: cdna_hip_programming.md "Pipelining across barriers", T3+T4).
+// NB = 2 (plain store; two raw s_barriers per K tile):
+//   phase | counted wait + barrier           | ds_reads issued            | DMA issued
+//   1     | W right + A bottom of tile t     | B right + A bottom (t)     | W right, A bottom (t+1)
+//   2     | --                               | --                         | --
+//   3     | --                               | --                         | A top (t+2)
+//   4     | A top + W left of t+1            | A top + B left (t+1)       | W left (t+2)
+// NB = 4 (SwiGLU epilogue: reading both fragment sets in phase 1 would spill there) adds a
+// barrier to phases 2 and 3 and reads A bottom in phase 2.  WAR safety: a half-tile region is
+// re-filled only after the barrier that follows its last reads (A top / W left of tile t+2 go
+// into buffer t&1 after phase 1 of t, whose barrier retired their phase-4-of-(t-1) reads).
+// Fragment reads for the next phases are issued before the current MFMAs, so LDS latency hides
+// under them.  One __shared__ array (no second LDS object: the compiler would drain vmcnt in the
+// loop, ibid. item 4a), raw s_barrier (never __syncthreads, whose fence drains the DMAs).
+// Measured: 0.81-0.86x of hipBLASLt on dense 8B-class shapes, 1.1-3.2x torch._grouped_mm on
+// expert-grouped ones (profiles/r4_pgemm_nb_ab.log); deeper rings, one barrier per 32-deep step
+// and 4-wave 128 x 128 sub-tiles were slower (r4_pgemm_v2_ring_rejected.log,
+// r4_pgemm_variants_pmc.log).
 //
 // LDS image: 128-B rows (64 bf16 of K), 16-B chunk c of row r stored at chunk c ^ ((r >> 1) & 7):
 // for each ds_read_b128 lane group (rows {0-3, 12-15} at chunk c and rows {4-11} at chunk c+1,
@@ -335,28 +342,20 @@ bool pgemm_supported(int M, int N, int K) {
   return M > 0 && N > 0 && N % PG_T == 0 && K >= PG_BK && K % PG_BK == 0;
 }
 
-template <int NB>
-static void launch_pgemm_nb(const PGemmArgs& p, int epi, int grid, hipStream_t st) {
-  if (p.groups > 0) {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, NB><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, true, NB><<<grid, PG_THREADS, 0, st>>>(p);
-  } else {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, NB><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, false, NB><<<grid, PG_THREADS, 0, st>>>(p);
-  }
-}
-
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
   if (p.M == 0) return;
   const int tiles_n = p.N / PG_T;
   const int grid = p.groups > 0 ? ((p.M + PG_T - 1) / PG_T + p.groups) * tiles_n
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
-  static const int nb = [] {
-    const char* e = getenv("AKAP_PGEMM_NB");
-    return e ? atoi(e) : 4;
-  }();
-  if (nb == 2) return launch_pgemm_nb<2>(p, epi, grid, st);
-  launch_pgemm_nb<4>(p, epi, grid, st);
+  // two barriers per K tile (measured 1-4 % faster than four, profiles/r4_pgemm_nb_ab.log); the
+  // SwiGLU form keeps four: with both fragment sets read in phase 1 it would spill
+  if (p.groups > 0) {
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, 4><<<grid, PG_THREADS, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, true, 2><<<grid, PG_THREADS, 0, st>>>(p);
+  } else {
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, 4><<<grid, PG_THREADS, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, false, 2><<<grid, PG_THREADS, 0, st>>>(p);
+  }
 }
 
 }  // namespace akap
