@@ -18,7 +18,7 @@ from typing import Optional
 class ModelConfig:
     name: str
     hf_id: str
-    arch: str  # "qwen3" | "llama" | "mixtral"
+    arch: str  # "qwen3" | "llama" | "mixtral" | "qwen3_moe"
     vocab_size: int
     hidden_size: int
     intermediate_size: int
@@ -34,6 +34,7 @@ class ModelConfig:
     qk_norm: bool = False
     num_experts: int = 0
     experts_per_token: int = 0
+    moe_renormalize: bool = True  # top-k router weights renormalised to sum 1 (norm_topk_prob)
     bos_id: int = 1
     eos_id: int = 2
     dtype: str = "bfloat16"
@@ -71,20 +72,23 @@ class ModelConfig:
     @staticmethod
     def from_hf_dict(name: str, d: dict) -> "ModelConfig":
         mt = d.get("model_type", "llama")
-        arch = {"qwen3": "qwen3", "mixtral": "mixtral"}.get(mt, "llama")
+        arch = {"qwen3": "qwen3", "mixtral": "mixtral", "qwen3_moe": "qwen3_moe"}.get(mt, "llama")
         heads = d["num_attention_heads"]
+        moe_ffn = d.get("moe_intermediate_size") if arch == "qwen3_moe" else None
         return ModelConfig(
             name=name, hf_id=name, arch=arch, vocab_size=d["vocab_size"],
-            hidden_size=d["hidden_size"], intermediate_size=d["intermediate_size"],
+            hidden_size=d["hidden_size"], intermediate_size=moe_ffn or d["intermediate_size"],
             num_layers=d["num_hidden_layers"], num_heads=heads,
             num_kv_heads=d.get("num_key_value_heads", heads),
             head_dim=d.get("head_dim") or d["hidden_size"] // heads,
             rms_eps=d.get("rms_norm_eps", 1e-6), rope_theta=d.get("rope_theta", 10000.0),
             rope_scaling=d.get("rope_scaling"),
             max_position=d.get("max_position_embeddings", 32768),
-            tie_embeddings=d.get("tie_word_embeddings", False), qk_norm=arch == "qwen3",
-            num_experts=d.get("num_local_experts", 0),
+            tie_embeddings=d.get("tie_word_embeddings", False),
+            qk_norm=arch in ("qwen3", "qwen3_moe"),
+            num_experts=d.get("num_local_experts", d.get("num_experts", 0)),
             experts_per_token=d.get("num_experts_per_tok", 0),
+            moe_renormalize=bool(d.get("norm_topk_prob", True)),
             bos_id=d.get("bos_token_id", 1) or 1,
             eos_id=(d.get("eos_token_id", 2) if not isinstance(d.get("eos_token_id"), list)
                     else d["eos_token_id"][0]),
@@ -125,6 +129,14 @@ MIXTRAL_8X7B = register(ModelConfig(
     num_heads=32, num_kv_heads=8, head_dim=128, rms_eps=1e-5, rope_theta=1_000_000.0,
     max_position=32768, num_experts=8, experts_per_token=2, bos_id=1, eos_id=2))
 
+# Qwen3 mixture-of-experts: 128 fine-grained experts, 8 per token (3.3B of 30.5B parameters
+# active); every layer MoE, q/k RMSNorm like the dense Qwen3
+QWEN3_30B_A3B = register(ModelConfig(
+    name="qwen3-30b-a3b", hf_id="Qwen/Qwen3-30B-A3B", arch="qwen3_moe", vocab_size=151936,
+    hidden_size=2048, intermediate_size=768, num_layers=48, num_heads=32, num_kv_heads=4,
+    head_dim=128, rms_eps=1e-6, rope_theta=1_000_000.0, max_position=40960, qk_norm=True,
+    num_experts=128, experts_per_token=8, bos_id=151643, eos_id=151645))
+
 # tiny shapes for CPU tests / smoke (same code paths, seconds to run)
 TINY_QWEN3 = register(ModelConfig(
     name="tiny-qwen3", hf_id="test/tiny-qwen3", arch="qwen3", vocab_size=512,
@@ -142,6 +154,13 @@ TINY_MIXTRAL = register(ModelConfig(
     hidden_size=256, intermediate_size=256, num_layers=2, num_heads=4, num_kv_heads=2,
     head_dim=128, rope_theta=1_000_000.0, max_position=4096, num_experts=4,
     experts_per_token=2, bos_id=1, eos_id=2))
+
+
+TINY_QWEN3_MOE = register(ModelConfig(
+    name="tiny-qwen3-moe", hf_id="test/tiny-qwen3-moe", arch="qwen3_moe", vocab_size=512,
+    hidden_size=256, intermediate_size=256, num_layers=2, num_heads=4, num_kv_heads=2,
+    head_dim=128, rope_theta=1_000_000.0, max_position=4096, qk_norm=True, num_experts=16,
+    experts_per_token=4, bos_id=1, eos_id=2))
 
 
 # the real multi-GPU layouts at world size 8: Llama-3-70B's 8 KV heads (one per TP rank, GQA

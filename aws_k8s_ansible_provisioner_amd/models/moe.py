@@ -1,4 +1,4 @@
-"""Mixture-of-experts FFN (Mixtral) with tensor-parallel or expert-parallel experts.
+"""Mixture-of-experts FFN (Mixtral, Qwen3-MoE) with tensor-parallel or expert-parallel experts.
 
 Routing is the HIP `moe_topk_softmax` kernel; token grouping is `moe_align` (expert-
 sorted, tile-padded index list).  Two placements:
@@ -105,13 +105,25 @@ class MoEBlock:
     def numel(self) -> int:
         return self.router.numel() + self.w13.numel() + self.w2.numel()
 
+    def _hf_names(self, prefix: str, e: int) -> tuple:
+        """HF checkpoint names: (router, gate, up, down) of expert e -- Mixtral's
+        block_sparse_moe.{gate, experts.e.w1/w3/w2} or Qwen3-MoE's mlp.{gate,
+        experts.e.gate_proj/up_proj/down_proj}."""
+        if self.cfg.arch == "qwen3_moe":
+            p = f"{prefix}mlp.experts.{e}."
+            return (prefix + "mlp.gate.weight", p + "gate_proj.weight", p + "up_proj.weight",
+                    p + "down_proj.weight")
+        p = f"{prefix}block_sparse_moe.experts.{e}."
+        return (prefix + "block_sparse_moe.gate.weight", p + "w1.weight", p + "w3.weight",
+                p + "w2.weight")
+
     def load_state_dict(self, sd: dict, prefix: str) -> None:
         r, tp = self.ps.tp_rank, self.ps.tp_size
-        self.router.copy_(sd[prefix + "block_sparse_moe.gate.weight"])
+        self.router.copy_(sd[self._hf_names(prefix, 0)[0]])
         for j in range(self.e_local):
             e = self.e0 + j
-            p = f"{prefix}block_sparse_moe.experts.{e}."
-            w1, w3, w2 = sd[p + "w1.weight"], sd[p + "w3.weight"], sd[p + "w2.weight"]
+            _, n1, n3, n2 = self._hf_names(prefix, e)
+            w1, w3, w2 = sd[n1], sd[n3], sd[n2]
             if self.mode != "ep":
                 fs = slice(r * self.f_local, (r + 1) * self.f_local)
                 w1, w3, w2 = w1[fs], w3[fs], w2[:, fs]
@@ -119,16 +131,16 @@ class MoEBlock:
             self.w2[j].copy_(w2)
 
     def hf_state_dict(self, prefix: str) -> dict:
-        """HF (Mixtral) names of this unsharded block's router and experts."""
+        """HF names (Mixtral or Qwen3-MoE) of this unsharded block's router and experts."""
         if self.e_local != self.E or self.f_local != self.cfg.intermediate_size:
             raise ValueError("hf_state_dict needs the unsharded MoE block")
         Fn = self.f_local
-        sd = {prefix + "block_sparse_moe.gate.weight": self.router.clone()}
+        sd = {self._hf_names(prefix, 0)[0]: self.router.clone()}
         for e in range(self.E):
-            p = f"{prefix}block_sparse_moe.experts.{e}."
-            sd[p + "w1.weight"] = self.w13[e, :Fn].clone()
-            sd[p + "w3.weight"] = self.w13[e, Fn:].clone()
-            sd[p + "w2.weight"] = self.w2[e].clone()
+            _, n1, n3, n2 = self._hf_names(prefix, e)
+            sd[n1] = self.w13[e, :Fn].clone()
+            sd[n3] = self.w13[e, Fn:].clone()
+            sd[n2] = self.w2[e].clone()
         return sd
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
@@ -174,7 +186,8 @@ class MoEBlock:
 
     def _forward_tokens(self, h: torch.Tensor) -> torch.Tensor:
         T, d = h.shape
-        w, ids = ops.moe_router_topk(h, self.router, self.K, renormalize=True)
+        w, ids = ops.moe_router_topk(h, self.router, self.K,
+                                     renormalize=self.cfg.moe_renormalize)
         capturing = h.is_cuda and torch.cuda.is_current_stream_capturing()
         if self.mode == "ep":
             if capturing:

@@ -51,7 +51,8 @@ def dense_logits(model, ids: list[int]) -> torch.Tensor:
             moe = lw.moe
             p = torch.softmax(h @ moe.router.float().t(), -1)
             w, e = torch.topk(p, moe.K, -1)
-            w = w / w.sum(-1, keepdim=True)
+            if moe.cfg.moe_renormalize:
+                w = w / w.sum(-1, keepdim=True)
             y = torch.zeros_like(h)
             for j in range(moe.K):
                 for ex in range(moe.E):

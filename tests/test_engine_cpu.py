@@ -25,7 +25,7 @@ def _near_argmax(eng, prompt, out, tol=0.1):
         assert gap <= tol, (i, tok, gap)
 
 
-@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama", "tiny-mixtral"])
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama", "tiny-mixtral", "tiny-qwen3-moe"])
 def test_engine_vs_dense_reference(model):
     eng = _engine(model)
     prompts = [list(range(5, 45)), [100, 101], [7, 8, 9] * 14, list(range(5, 45))]

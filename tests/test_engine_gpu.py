@@ -29,7 +29,7 @@ def _check_teacher_forced(eng, prompt, out, tol=0.15):
         assert gap <= tol, f"step {i}: token {tok} is {gap:.3f} std below the argmax"
 
 
-@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama"])
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama", "tiny-qwen3-moe"])
 @pytest.mark.parametrize("eager", [False, True])
 def test_engine_matches_dense_reference(model, eager):
     eng = _engine(model, eager)
@@ -299,7 +299,7 @@ def test_inprocess_kernel_stats_window_sees_graph_replayed_kernels():
     assert "akap_kernel_profiler_up 1" in kp.text()
 
 
-@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-mixtral", "qwen3-0.6b"])
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-mixtral", "tiny-qwen3-moe", "qwen3-0.6b"])
 def test_prefill_on_hand_written_gemm(model, monkeypatch):
     """AKAP_PREFILL_GEMM=pgemm: every prefill projection on csrc/kernels/pgemm.hip (SwiGLU fused
     into the gate|up GEMM; Mixtral's experts on its grouped form) -- generations still match
@@ -319,7 +319,7 @@ def test_prefill_on_hand_written_gemm(model, monkeypatch):
     outs = eng.generate(None, SamplingParams(max_tokens=4, temperature=0, ignore_eos=True),
                         prompt_ids=prompts)
     assert any(k.get("silu") for k in calls)
-    if model == "tiny-mixtral":
+    if "mixtral" in model or "moe" in model:
         assert any(k.get("offs") is not None for k in calls)
     for p, o in zip(prompts, outs):
         _check_teacher_forced(eng, p, o.output_ids, tol=0.2)

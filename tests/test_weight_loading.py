@@ -33,12 +33,15 @@ def _export(model, tmp_path):
     return src, sd, str(d)
 
 
-@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama", "tiny-mixtral"])
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-llama", "tiny-mixtral", "tiny-qwen3-moe"])
 def test_hf_names_round_trip_tp1(model, tmp_path):
     src, sd, _ = _export(model, tmp_path)
     names = set(sd)
     assert "model.layers.0.self_attn.q_proj.weight" in names
-    if get_config(model).is_moe:
+    if get_config(model).arch == "qwen3_moe":
+        assert "model.layers.0.mlp.experts.1.up_proj.weight" in names
+        assert "model.layers.0.mlp.gate.weight" in names
+    elif get_config(model).is_moe:
         assert "model.layers.0.block_sparse_moe.experts.1.w3.weight" in names
     else:
         assert "model.layers.0.mlp.gate_proj.weight" in names
@@ -78,7 +81,8 @@ def _port():
 
 
 @pytest.mark.parametrize("model,moe_mode", [("tiny-llama", "tp"), ("tiny-qwen3", "tp"),
-                                            ("tiny-mixtral", "tp"), ("tiny-mixtral", "ep")])
+                                            ("tiny-mixtral", "tp"), ("tiny-mixtral", "ep"),
+                                            ("tiny-qwen3-moe", "tp"), ("tiny-qwen3-moe", "ep")])
 def test_hf_checkpoint_sharded_load_tp2(model, moe_mode, tmp_path):
     """The same safetensors checkpoint loaded by a tp=2 engine (each rank takes its q/kv-head,
     ffn-row, vocab and expert shards) generates the tokens of the tp=1 engine that loaded it."""
@@ -109,3 +113,25 @@ def test_hf_checkpoint_sharded_load_tp2(model, moe_mode, tmp_path):
                        prompt_ids=PROMPTS)
     agree = sum(a == b for o, t in zip(one, tp_out) for a, b in zip(o.output_ids, t))
     assert agree >= 0.8 * sum(len(t) for t in tp_out)
+
+
+def test_qwen3_moe_hf_config_and_names():
+    """A Qwen3-MoE config.json maps to arch qwen3_moe (q/k norm, moe_intermediate_size as the
+    expert FFN, num_experts, norm_topk_prob) and its experts load from mlp.experts.* names."""
+    from aws_k8s_ansible_provisioner_amd.models.config import ModelConfig
+
+    d = {"model_type": "qwen3_moe", "vocab_size": 151936, "hidden_size": 2048,
+         "intermediate_size": 6144, "moe_intermediate_size": 768, "num_hidden_layers": 48,
+         "num_attention_heads": 32, "num_key_value_heads": 4, "head_dim": 128,
+         "num_experts": 128, "num_experts_per_tok": 8, "norm_topk_prob": True,
+         "rope_theta": 1000000.0, "max_position_embeddings": 40960}
+    c = ModelConfig.from_hf_dict("q", d)
+    assert (c.arch, c.qk_norm, c.intermediate_size, c.num_experts, c.experts_per_token,
+            c.moe_renormalize) == ("qwen3_moe", True, 768, 128, 8, True)
+    from aws_k8s_ansible_provisioner_amd.models.config import get_config
+
+    ref = get_config("qwen3-30b-a3b")
+    for f in ("hidden_size", "intermediate_size", "num_layers", "num_heads", "num_kv_heads",
+              "num_experts", "experts_per_token", "vocab_size"):
+        assert getattr(ref, f) == getattr(c, f), f
+    assert 30e9 < ref.num_params() < 31e9
