@@ -77,6 +77,20 @@ def _timed(fn, n: int) -> float:
     return e0.elapsed_time(e1) * 1000.0 / (2 * n)
 
 
+def _timed_eager(fn, n: int) -> float:
+    """us per call of fn(i), i < n, launched eagerly (for library calls that refuse stream
+    capture, e.g. torch._grouped_mm)."""
+    fn(0)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    e0.record()
+    for i in range(n):
+        fn(i)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / n
+
+
 def _gd_variants(s: int, bns, M: int = 0):
     """gdgemm.hip variants at split s: (tile width, ring depth, in-launch split-K combine, tile
     rows).  Depth 0 = shallow ring (two blocks per CU), 8 = deep ring (one block per CU);
@@ -406,8 +420,9 @@ def tune_prefill(model, M: int, log=print, margin: float = 0.02) -> dict:
                 lib = lambda i: silu_and_mul(torch._grouped_mm(x, wt, offs=offs), o)  # noqa: E731
             else:
                 lib = lambda i: torch._grouped_mm(x, wt, offs=offs)  # noqa: E731
-            t_lib = _timed(lib, 2)
-            t_pg = _timed(lambda i: torch.ops.akap.pgemm(o, x, w, 2 if silu else 0, offs), 2)
+            t_lib = _timed_eager(lib, 3)
+            t_pg = _timed_eager(lambda i: torch.ops.akap.pgemm(o, x, w, 2 if silu else 0, offs),
+                                3)
             _PREFILL[("grouped", N, K, silu)] = t_pg < t_lib * (1.0 - margin)
             out[("grouped", N, K, silu)] = (t_pg, t_lib)
             del x, o

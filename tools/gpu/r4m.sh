@@ -1,8 +1,7 @@
 set -u
-O=gpurun_out/r4m; mkdir -p $O
+O=gpurun_out/r4n; mkdir -p $O
 run() { n=$1; t=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.log 2>&1; rc=$?; echo "$n rc=$rc"; [ $rc -le 1 ]; }
-run tmoe 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_engine_gpu.py -k "moe" &&
 run qwen3moe 600 python -u bench.py --model qwen3-30b-a3b --steps 2 &&
-run mixtral 600 python -u bench.py --model mixtral-8x7b --num-requests 128 --max-num-seqs 128 --steps 1 &&
-run llama8b 600 python -u bench.py --model llama-3-8b --steps 2
+AKAP_PREFILL_GEMM=lib run qwen3moe_lib 600 python -u bench.py --model qwen3-30b-a3b --steps 2 &&
+run mixtral 600 python -u bench.py --model mixtral-8x7b --num-requests 128 --max-num-seqs 128 --steps 1
 echo done
