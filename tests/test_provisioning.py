@@ -127,7 +127,7 @@ def test_cli_cleanup(tmp_path):
     assert not list(tmp_path.glob("gpu-inventory-*.ini"))
 
 
-@pytest.mark.parametrize("preset", ["slim", "pd", "tp8", "moe", "kind"])
+@pytest.mark.parametrize("preset", ["slim", "pd", "tp8", "moe", "moe-qwen3", "kind"])
 def test_manifests_render(preset):
     v = installer.load_values(os.path.join(ROOT, "deploy", "values", f"{preset}.yaml"))
     out = installer.render(v, "llm-d", "local-path", "50Gi", "Qwen/Qwen3-0.6B", hf_token="t0k")
