@@ -1,6 +1,6 @@
 // Mixture-of-experts routing kernels for gfx950.
 //  * moe_topk_softmax: router logits [T, E] -> softmax -> top-k (+ optional renorm).
-//    One lane per token (E <= 256 keeps the row in registers/L1).
+//    One lane per token for E <= 32 (Mixtral), one wave per token above (Qwen3-MoE, E <= 256).
 //  * moe_align: groups the T*K (token, expert) pairs by expert, padding every
 //    expert's segment to a multiple of the grouped-GEMM row tile so each tile of
 //    the sorted list belongs to exactly one expert.  Single workgroup, LDS counts.
@@ -119,9 +119,79 @@ void launch_moe_router_topk(const void* h, int ldh, const void* W, int d, int E,
                                            topk_ids, renormalize);
 }
 
+// Many-expert routing (Qwen3-MoE: E = 128, K = 8): one WAVE per token.  Lane l holds logits
+// l, l + 64, l + 128, l + 192 (E <= 256); max and sum-of-exp are wave reductions; each of the
+// K picks is a wave argmax over the lanes' best unpicked logit (ties -> lowest expert id, as in
+// topk_softmax_row).  The one-lane-per-token kernel above spends E x K serial steps per lane:
+// 189 us per call at T = 256, E = 128, K = 8 (profiles/r4_qwen3_moe_kernel_stats.md).
+__device__ __forceinline__ void wave_argmax(float& v, int& idx) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    if (ov > v || (ov == v && oi < idx)) {
+      v = ov;
+      idx = oi;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void moe_topk_softmax_wave_kernel(
+    const bf16* __restrict__ logits, int ld, int E, int K, float* __restrict__ topk_w,
+    int32_t* __restrict__ topk_ids, int Tn, int renorm) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= Tn) return;  // wave-uniform
+  const bf16* x = logits + (size_t)t * ld;
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = lane + 64 * j;
+    v[j] = e < E ? bf2f(x[e]) : -INFINITY;
+  }
+  float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float z = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) z += lane + 64 * j < E ? __expf(v[j] - mx) : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) z += __shfl_xor(z, o, 64);
+  const float invz = 1.f / z;
+  float my_w = 0.f, wsum = 0.f;
+  int my_id = 0;
+  for (int k = 0; k < K; ++k) {
+    float best = v[0];
+    int bi = lane;
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      if (v[j] > best) {  // strict: the lower expert id of a lane wins ties
+        best = v[j];
+        bi = lane + 64 * j;
+      }
+    wave_argmax(best, bi);
+    if ((bi & 63) == lane) v[bi >> 6] = -INFINITY;  // the owning lane retires the pick
+    const float w = __expf(best - mx) * invz;
+    wsum += w;
+    if (lane == k) {
+      my_w = w;
+      my_id = bi;
+    }
+  }
+  if (lane < K) {
+    topk_w[(size_t)t * K + lane] = renorm ? my_w / wsum : my_w;
+    topk_ids[(size_t)t * K + lane] = my_id;
+  }
+}
+
 void launch_moe_topk_softmax(const void* logits, int ld, int E, int K, float* topk_w,
                              int32_t* topk_ids, int T, int renormalize, hipStream_t s) {
   if (T == 0) return;
+  if (E > 32) {
+    moe_topk_softmax_wave_kernel<<<(T + 3) / 4, 256, 0, s>>>(
+        (const bf16*)logits, ld, E, K, topk_w, topk_ids, T, renormalize);
+    return;
+  }
   moe_topk_softmax_kernel<bf16><<<(T + 255) / 256, 256, 0, s>>>(
       (const bf16*)logits, ld, E, K, topk_w, topk_ids, T, renormalize);
 }

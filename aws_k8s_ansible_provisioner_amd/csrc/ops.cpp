@@ -514,6 +514,10 @@ void argmax(Tensor logits, Tensor out) {
 void moe_topk_softmax(Tensor logits, Tensor topk_w, Tensor topk_ids, bool renorm) {
   CHECK_GPU(logits); CHECK_BF16(logits); CHECK_LAST_CONTIG(logits);
   TORCH_CHECK(logits.size(1) <= 256, "at most 256 experts");
+  TORCH_CHECK(topk_w.size(1) >= 1 && topk_w.size(1) <= 8 && topk_w.size(1) <= logits.size(1),
+              "top-k in 1..min(8, E)");
+  TORCH_CHECK(topk_ids.sizes() == topk_w.sizes() && topk_w.size(0) == logits.size(0),
+              "topk_w / topk_ids [T, K]");
   const c10::DeviceGuard g(logits.device());
   akap::launch_moe_topk_softmax(logits.data_ptr(), logits.stride(0), logits.size(1),
                                 topk_w.size(1), topk_w.data_ptr<float>(),

@@ -206,24 +206,35 @@ class MoEBlock:
             out = ops.fused_moe(h, self.w13, self.w2, w, ids)
         else:
             src = torch.arange(T * self.K, device=h.device) // self.K
-            y = self._expert_rows(h, ids.reshape(-1), src)
-            out = (y.view(T, self.K, d).float() * w.view(T, self.K, 1).float()).sum(1)
-            out = out.to(h.dtype)
+            if h.is_cuda:
+                # expert-sorted rows straight into the weighted combine (moe_combine gathers
+                # each token's K rows through inv): no permutation store of the [T*K, d] rows
+                ys, order = self._expert_rows(h, ids.reshape(-1), src, sorted_out=True)
+                inv = torch.empty_like(order, dtype=torch.int32)
+                inv[order] = torch.arange(order.numel(), dtype=torch.int32, device=h.device)
+                out = torch.empty(T, d, dtype=h.dtype, device=h.device)
+                torch.ops.akap.moe_combine(ys, w.float().contiguous(), inv, out)
+            else:
+                y = self._expert_rows(h, ids.reshape(-1), src)
+                out = (y.view(T, self.K, d).float() * w.view(T, self.K, 1).float()).sum(1)
+                out = out.to(h.dtype)
         comm.tp_all_reduce(out)
         return out
 
     grouped_min_t = int(os.environ.get("AKAP_MOE_GROUPED_MIN_T", "512"))
 
     def _expert_rows(self, x: torch.Tensor, e: torch.Tensor,
-                     src: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     src: Optional[torch.Tensor] = None, sorted_out: bool = False):
         """y[i] = expert e[i]'s SwiGLU FFN of x[src[i]] (src = identity when None), unweighted.
         Rows are sorted by expert on the device and run through a grouped GEMM over device-side
         group offsets -- the hand-written pgemm (SwiGLU fused into the first GEMM's epilogue) or
         torch._grouped_mm (the ROCm library grouped GEMM), whichever measured faster at engine
-        start (gemm_tuner.tune_prefill): no host sync, no per-expert loop.  Mixtral-8x7B shapes on MI355X: 1081 TFLOP/s at T=16384 and 847 at T=4096, vs
+        start (gemm_tuner.tune_prefill): no host sync, no per-expert loop.  Mixtral-8x7B shapes
+        on MI355X: 1081 TFLOP/s at T=16384 and 847 at T=4096, vs
         617 / 444 for fused_moe and level with the host-synced per-expert hipBLASLt loop it
         replaces (profiles/r3_moe_prefill.log).  Outputs come back in row order (a permutation
-        store: deterministic, no float atomics)."""
+        store: deterministic, no float atomics), or with sorted_out as (expert-sorted rows,
+        order) for a caller that gathers them itself."""
         e = e.reshape(-1).long()
         order = torch.argsort(e, stable=True)
         offs = torch.cumsum(torch.bincount(e, minlength=self.e_local), 0).to(torch.int32)
@@ -237,6 +248,8 @@ class MoEBlock:
             y = ops.pgemm(a, self.w2, offs=offs)
         else:
             y = torch._grouped_mm(a, self.w2.transpose(1, 2), offs=offs)
+        if sorted_out:
+            return y, order
         out = torch.empty_like(y)
         out[order] = y
         return out

@@ -296,6 +296,25 @@ def test_moe_router_topk_fused(T, E, K, d):
     assert torch.equal(ids2.cpu(), ids.cpu())
 
 
+@pytest.mark.parametrize("T,E,K", [(256, 128, 8), (37, 256, 8), (1000, 64, 4), (5, 48, 1)])
+def test_moe_topk_softmax_many_experts(T, E, K):
+    """The wave-per-token routing kernel (E > 32) vs the fp32 reference: same experts, same
+    weights; renormalised and raw."""
+    g = torch.Generator().manual_seed(T + E)
+    # distinct logits per row (no bf16 ties at the K-th boundary): a random permutation of an
+    # evenly spaced grid in [-1, 1), exactly representable in bf16
+    perm = torch.argsort(torch.rand(T, E, generator=g), dim=-1).float()
+    logits = ((perm - E / 2) * (2.0 / E)).bfloat16()
+    assert all(len(set(r.tolist())) == E for r in logits.float())
+    for renorm in (True, False):
+        w, ids = ops.moe_topk_softmax(logits.to(DEV), K, renormalize=renorm)
+        rw, rid = ref.moe_topk_softmax(logits, K, renorm)
+        oi, o = ids.cpu().long().sort(dim=-1)
+        ri, r = rid.long().sort(dim=-1)
+        assert torch.equal(oi, ri)
+        _close(w.cpu().gather(1, o), rw.gather(1, r), atol=1e-4)
+
+
 def test_moe_routing():
     torch.manual_seed(6)
     T, E, K = 300, 8, 2
