@@ -208,34 +208,45 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int32_t* __restri
                                                          int32_t* __restrict__ tile_expert,
                                                          int max_tiles) {
   extern __shared__ int sm[];
-  int* cnt = sm;          // [E]
-  int* cursor = sm + E;   // [E]
+  int* cnt = sm;             // [E]
+  int* cursor = sm + E;      // [E]
+  int* offs = sm + 2 * E;    // [E + 1], LDS copy of the padded segment starts
   for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
   // ids outside [0, E) (expert-parallel padding rows) are skipped: no slot, inv = -1
   for (int i = threadIdx.x; i < n; i += blockDim.x)
     if ((unsigned)ids[i] < (unsigned)E) atomicAdd(&cnt[ids[i]], 1);
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // E <= 256 LDS-only adds
     int acc = 0;
     for (int e = 0; e < E; ++e) {
-      offsets[e] = acc;
-      cursor[e] = acc;
+      offs[e] = acc;
       acc += (cnt[e] + block - 1) / block * block;
     }
-    offsets[E] = acc;
+    offs[E] = acc;
     *num_padded = acc;
   }
   __syncthreads();
-  const int total = offsets[E];
+  for (int e = threadIdx.x; e <= E; e += blockDim.x) {
+    offsets[e] = offs[e];
+    if (e < E) cursor[e] = offs[e];
+  }
+  const int total = offs[E];
   for (int i = threadIdx.x; i < total; i += blockDim.x) sorted_ids[i] = n;
   if (tile_expert != nullptr) {
+    // expert of tile t: the last e with offs[e] <= t * block (binary search over LDS; empty
+    // experts share their start with the next one, the search lands past them)
     for (int t = threadIdx.x; t < max_tiles; t += blockDim.x) {
       const int r0 = t * block;
       int e = -1;
       if (r0 < total) {
-        e = 0;
-        while (e + 1 < E && offsets[e + 1] <= r0) ++e;
+        int lo = 0, hi = E - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (offs[mid] <= r0) lo = mid;
+          else hi = mid - 1;
+        }
+        e = lo;
       }
       tile_expert[t] = e;
     }
@@ -408,7 +419,7 @@ void launch_moe_combine(const void* Y, const float* wts, const int32_t* inv, voi
 void launch_moe_align(const int32_t* topk_ids, int n, int E, int block, int32_t* sorted_ids,
                       int32_t* expert_offsets, int32_t* num_padded, int32_t* inv,
                       int32_t* tile_expert, int max_tiles, hipStream_t s) {
-  moe_align_kernel<<<1, 1024, 2 * E * sizeof(int), s>>>(topk_ids, n, E, block, sorted_ids,
+  moe_align_kernel<<<1, 1024, (3 * E + 1) * sizeof(int), s>>>(topk_ids, n, E, block, sorted_ids,
                                                         expert_offsets, num_padded, inv,
                                                         tile_expert, max_tiles);
 }
