@@ -2,15 +2,19 @@
 
 Rank 0 of the group owns the C++ scheduler, the HTTP server and the request state; every
 rank owns its weight shard, its KV-cache shard (its kv heads) and its hipGraphs.  Each
-engine step, rank 0 broadcasts the step header (StepInfo + a launch mode, 9 int64) over a
-gloo control group -- ONE host broadcast per step: the step inputs themselves travel as one
-RCCL broadcast of rank 0's device staging region (decode: at the head of the step, inside
-the hipGraph, ModelRunner._decode_body; prefill: ModelRunner._stage_prefill's packed region).
+engine step, rank 0 broadcasts the step header (StepInfo + an eager bit + a launch mode,
+10 int64) over a gloo control group -- ONE host broadcast per step: the step inputs
+themselves travel as one device broadcast of rank 0's staging region (decode: at the head of
+the step, inside the hipGraph, ModelRunner._decode_body -> comm.tp_broadcast, the custom IPC
+broadcast kernel when it fits, else RCCL; prefill: ModelRunner._stage_prefill's packed
+region).
 Decode lookahead works across the group: rank 0 broadcasts a lookahead step's header as it
 launches it (mode LAUNCH / CHAINED) and followers replay without waiting on the host
 (ModelRunner.replay_decode), so every rank's GPU queue holds the next step.  The
 forward's all-reduces (O-proj, down-proj) and the vocab-parallel logits all-gather run on
-RCCL over xGMI (and are captured inside the decode hipGraphs).  Every rank sees the full
+the custom IPC kernels over xGMI at decode sizes (K13 all-reduce and its all-gather
+sibling, parallel/custom_allreduce.py), RCCL above them: a captured decode graph then holds
+only our kernels, which is what lets ranks sharing one GPU (gloo control plane) replay it.  Every rank sees the full
 logits and runs the same seeded sampler, so all ranks produce identical tokens without
 another collective.
 """
