@@ -121,7 +121,7 @@ __device__ __forceinline__ bool pg_tile(const PGemmArgs& p, int& tm, int& tn, in
   } else {
     int lo = 0;
     for (int g = 0; g < p.groups; ++g) {
-      const int hi = p.offs[g];
+      const int hi = min(p.offs[g], p.M);  // offsets past M never store out of bounds
       const int nt = (hi - lo + PG_T - 1) / PG_T;
       if (mt < nt) {
         tm = mt;

@@ -741,6 +741,10 @@ void pgemm(Tensor out, Tensor x, Tensor w, int64_t epi, std::optional<Tensor> of
   a.ldx = x.stride(0);
   a.ldy = out.stride(0);
   TORCH_CHECK(a.ldx % 8 == 0 && a.ldy % 4 == 0, "row strides must keep 16-B / 8-B alignment");
+  // the DMA addresses X and one group's W through buffer descriptors with 32-bit offsets
+  TORCH_CHECK((int64_t)a.M * a.ldx * 2 < (int64_t(1) << 31) &&
+                  (int64_t)a.N * a.K * 2 < (int64_t(1) << 31),
+              "pgemm: X and each weight matrix must stay below 2 GiB");
   const c10::DeviceGuard g(x.device());
   akap::launch_pgemm(a, (int)epi, cur_stream());
 }

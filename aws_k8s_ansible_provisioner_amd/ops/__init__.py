@@ -230,8 +230,10 @@ PGEMM_MIN_M = int(os.environ.get("AKAP_PGEMM_MIN_M", "1024"))
 
 
 def pgemm_supported(M: int, N: int, K: int) -> bool:
-    """Mirror of pgemm_supported (csrc/kernels/pgemm.hip)."""
-    return M > 0 and N > 0 and N % 256 == 0 and K >= 64 and K % 64 == 0
+    """Mirror of pgemm_supported (csrc/kernels/pgemm.hip) and the 2 GiB operand limit of its
+    buffer-descriptor DMA (ops.cpp)."""
+    return (M > 0 and N > 0 and N % 256 == 0 and K >= 64 and K % 64 == 0
+            and M * K * 2 < 2 ** 31 and N * K * 2 < 2 ** 31)
 
 
 def use_pgemm(x: torch.Tensor, N: int, silu: bool = False, grouped: bool = False) -> bool:
