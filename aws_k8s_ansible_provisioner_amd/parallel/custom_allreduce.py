@@ -38,15 +38,20 @@ def oneshot_limit(world: int) -> int:
 
 class CustomAllReduce:
     def __init__(self, group=None, device: Optional[torch.device] = None,
-                 max_bytes: int = DEFAULT_MAX_BYTES):
+                 max_bytes: int = DEFAULT_MAX_BYTES, buffer_bytes: int = 0):
+        """max_bytes: all-reduce policy threshold (larger messages go to RCCL); buffer_bytes:
+        staging capacity, raised above max_bytes so the all-gather of a decode step's
+        vocab-parallel logits (rows x vocab/tp) and the step broadcast always fit -- a decode
+        hipGraph then never falls back to a process-group collective."""
         ops.load_native(required=True)
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.max_bytes = max_bytes
+        self.buffer_bytes = max(max_bytes, buffer_bytes)
         self.oneshot_bytes = oneshot_limit(self.world)
-        max_elems = (max_bytes // 2 + 7) // 8 * 8
+        max_elems = (self.buffer_bytes // 2 + 7) // 8 * 8
         self.h = torch.ops.akap.car_create(self.device.index, self.rank, self.world, max_elems)
         mine = torch.ops.akap.car_ipc_handles(self.h)
         allh: list = [None] * self.world
@@ -76,7 +81,10 @@ class CustomAllReduce:
         torch.ops.akap.car_all_reduce_resnorm(self.h, x, residual, ln, a_out, ss, two)
 
     def gather_ok(self, x: torch.Tensor) -> bool:
-        return (self.should_use(x) and x.dim() >= 1 and x.shape[-1] % 8 == 0)
+        nbytes = x.numel() * x.element_size()
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
+                and x.numel() % 8 == 0 and nbytes <= self.buffer_bytes and x.dim() >= 1
+                and x.shape[-1] % 8 == 0)
 
     def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """x [R, n] (this rank's shard) -> out [R, world*n], rank-major column blocks."""
@@ -85,7 +93,8 @@ class CustomAllReduce:
 
     def bcast_ok(self, t: torch.Tensor) -> bool:
         nbytes = t.numel() * t.element_size()
-        return t.is_cuda and t.is_contiguous() and nbytes % 16 == 0 and nbytes <= self.max_bytes
+        return (t.is_cuda and t.is_contiguous() and nbytes % 16 == 0
+                and nbytes <= self.buffer_bytes)
 
     def broadcast(self, t: torch.Tensor, root: int) -> torch.Tensor:
         """In place: every rank's t becomes group rank `root`'s t."""

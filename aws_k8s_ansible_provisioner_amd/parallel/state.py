@@ -52,7 +52,8 @@ def env_rank_info() -> tuple[int, int, int]:
 
 
 def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
-                     device: Optional[str] = None, timeout_s: int = 600) -> ParallelState:
+                     device: Optional[str] = None, timeout_s: int = 600,
+                     car_buffer_bytes: int = 0) -> ParallelState:
     """Initialise torch.distributed from torchrun env vars and build TP/DP groups.
 
     backend: "nccl" (RCCL over xGMI on MI355X) when GPUs are present, else "gloo".
@@ -99,7 +100,8 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
     if (world > 1 and tp_size > 1 and (backend == "nccl" or car_gloo)
             and os.environ.get("AKAP_CUSTOM_AR", "1") != "0"):
         from .custom_allreduce import CustomAllReduce
-        st.car = CustomAllReduce(group=st.tp_group, device=torch.device("cuda", local))
+        st.car = CustomAllReduce(group=st.tp_group, device=torch.device("cuda", local),
+                                 buffer_bytes=car_buffer_bytes)
     _STATE = st
     return st
 

@@ -98,11 +98,16 @@ def worker_loop(runner: ModelRunner, ctrl_group) -> None:
 
 def build_tp(ecfg: EngineConfig, backend: Optional[str] = None, log=print):
     """Initialise the TP group and this rank's runner.  Returns (state, runner, ctrl)."""
-    st = init_distributed(tp_size=ecfg.tensor_parallel_size, backend=backend)
+    mcfg = get_config(ecfg.model)
+    tp = ecfg.tensor_parallel_size
+    # IPC staging large enough for the decode step's vocab-parallel logits all-gather
+    # (rows x vocab/tp bf16) so every captured decode graph keeps it on the IPC kernel
+    rows = max(ecfg.max_num_seqs, ecfg.cuda_graph_max_bs or 0)
+    car_bytes = rows * (-(-mcfg.vocab_size // tp) + 64) * 2
+    st = init_distributed(tp_size=tp, backend=backend, car_buffer_bytes=car_bytes)
     if st.world_size != ecfg.tensor_parallel_size:
         raise ValueError("one engine replica per job: WORLD_SIZE must equal TP size")
     ctrl = dist.new_group(backend="gloo")
-    mcfg = get_config(ecfg.model)
     runner = ModelRunner(ecfg, mcfg, st, log=log if st.rank == 0 else (lambda *a: None))
     return st, runner, ctrl
 

@@ -168,6 +168,10 @@ def main() -> int:
 
         ecfg.tensor_parallel_size = a.tp
         ecfg.seed = 1234
+        if gpu and dist.get_backend() == "gloo":
+            # ranks sharing one GPU over a gloo control plane: the decode graphs' collectives
+            # must be the IPC kernels (a gloo collective cannot be captured)
+            os.environ.setdefault("AKAP_CUSTOM_AR_GLOO", "1")
         eng, tp_bc = make_tp_engine(ecfg, log=log)
         if eng is None:  # ranks != 0 mirrored every step until rank 0 shut the group down
             return 0
