@@ -28,8 +28,22 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
         return x
     if st.car is not None and st.car.should_use(x):
         return st.car.all_reduce(x)
+    if st.car is not None and st.backend == "gloo" and _car_pieces_ok(x, st.car):
+        # ranks sharing one GPU over a gloo control plane (single-GPU rehearsal): prefill-sized
+        # all-reduces stay on the device in max_bytes pieces of the IPC kernel instead of a
+        # host-staged gloo all-reduce
+        flat = x.view(-1)
+        step = st.car.max_bytes // x.element_size() // 8 * 8
+        for i in range(0, flat.numel(), step):
+            st.car.all_reduce(flat[i:i + step])
+        return x
     dist.all_reduce(x, group=st.tp_group)
     return x
+
+
+def _car_pieces_ok(x: torch.Tensor, car) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
+            and x.numel() % 8 == 0 and car.max_bytes >= 4096)
 
 
 def tp_all_reduce_resnorm(partial: torch.Tensor, residual: torch.Tensor, ln: torch.Tensor,
