@@ -64,7 +64,12 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
         # more ranks than devices only in single-GPU rehearsals (gloo): share the device
         local = local % max(1, torch.cuda.device_count())
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # an already initialised default group (bench.py, tests) decides: its collectives are
+        # what tp_all_reduce falls back to
+        if dist.is_initialized():
+            backend = dist.get_backend()
+        else:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
