@@ -321,6 +321,44 @@ __device__ __forceinline__ void car_bcast(const CarArgs& a, int bid, int nblk, b
   }
 }
 
+// All-to-all with equal segments: in = [W][seg8 vectors] (segment d goes to rank d), out =
+// [W][seg8] with out[p] = rank p's in[rank].  Each block stages, for every destination, the
+// same vector indices it later reads from the peers (i in its grid-stride set over seg8), so
+// the per-block flag exchange (car_barrier) covers exactly the data each block reads -- the
+// ordering argument of the one-shot all-reduce, unchanged.
+__device__ __forceinline__ void car_alltoall(const CarArgs& a, int bid, int nblk,
+                                             const bf16* __restrict__ in, bf16* __restrict__ out,
+                                             long seg8) {
+  const uint32_t ep = car_epoch(a, bid);
+  const size_t par = (ep & 1) * a.half_elems;
+  const __amdgpu_buffer_rsrc_t mine = car_rsrc(a.bufs[a.rank], a);
+  const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
+  bf16x8* dst = reinterpret_cast<bf16x8*>(out);
+  const long stride = (long)nblk * 256;
+  const int W = a.world;
+  for (long i = (long)bid * 256 + threadIdx.x; i < seg8; i += stride)
+    for (int d = 0; d < W; ++d)
+      if (d != a.rank) car_st(mine, par + (size_t)(d * seg8 + i) * 8, src[d * seg8 + i]);
+  car_barrier(a, bid, ep, 0);
+  for (long i = (long)bid * 256 + threadIdx.x; i < seg8; i += stride) {
+    bf16x8 v[kCarMaxRanks];
+#pragma unroll
+    for (int p = 0; p < kCarMaxRanks; ++p)  // every peer load in flight before the stores
+      if (p < W && p != a.rank)
+        v[p] = car_ld(car_rsrc(a.bufs[p], a), par + (size_t)(a.rank * seg8 + i) * 8);
+#pragma unroll
+    for (int p = 0; p < kCarMaxRanks; ++p) {
+      if (p >= W) break;
+      dst[p * seg8 + i] = p == a.rank ? src[a.rank * seg8 + i] : v[p];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void car_alltoall_kernel(CarArgs a, const bf16* __restrict__ in,
+                                                           bf16* __restrict__ out, long seg8) {
+  car_alltoall(a, blockIdx.x, gridDim.x, in, out, seg8);
+}
+
 __global__ __launch_bounds__(256) void car_allgather_kernel(CarArgs a, const bf16* __restrict__ in,
                                                             bf16* __restrict__ out, long n8,
                                                             int n) {
@@ -360,6 +398,14 @@ void launch_custom_allgather(const CarArgs& a, const void* in, void* out, long r
   if (n8 == 0) return;
   car_allgather_kernel<<<car_blocks(n8, a.world, false), 256, 0, s>>>(a, (const bf16*)in,
                                                                     (bf16*)out, n8, n);
+}
+
+void launch_custom_alltoall(const CarArgs& a, const void* in, void* out, long seg_elems,
+                            hipStream_t s) {
+  const long seg8 = seg_elems / 8;
+  if (seg8 == 0) return;
+  car_alltoall_kernel<<<car_blocks(seg8, a.world, false), 256, 0, s>>>(a, (const bf16*)in,
+                                                                      (bf16*)out, seg8);
 }
 
 void launch_custom_broadcast(const CarArgs& a, void* buf, long bytes, int root, hipStream_t s) {

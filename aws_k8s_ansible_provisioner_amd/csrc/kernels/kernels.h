@@ -258,6 +258,9 @@ size_t custom_allreduce_signal_bytes();
 void launch_custom_allgather(const CarArgs& a, const void* in, void* out, long rows, int n,
                              hipStream_t s);
 void launch_custom_broadcast(const CarArgs& a, void* buf, long bytes, int root, hipStream_t s);
+// equal-segment all-to-all: in/out [world][seg_elems] bf16 (seg_elems % 8 == 0)
+void launch_custom_alltoall(const CarArgs& a, const void* in, void* out, long seg_elems,
+                            hipStream_t s);
 struct CarMulti {  // test-only: every rank of a simulated group in one launch
   CarArgs args[8];
   const void* in[8];

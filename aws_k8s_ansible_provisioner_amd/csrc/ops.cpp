@@ -969,6 +969,23 @@ void car_all_gather(int64_t h, Tensor inp, Tensor out) {
                                 cur_stream());
 }
 
+// Equal-segment all-to-all: inp/out [world * seg] bf16, segment d of inp goes to rank d and
+// segment p of out comes from rank p.
+void car_all_to_all(int64_t h, Tensor inp, Tensor out) {
+  CarComm* c = car_get(h);
+  CHECK_GPU(inp); CHECK_BF16(inp); CHECK_CONTIG(inp); CHECK_BF16(out); CHECK_CONTIG(out);
+  const int64_t W = c->args.world;
+  TORCH_CHECK(inp.numel() == out.numel() && inp.numel() % (W * 8) == 0,
+              "all-to-all: inp/out [world * seg] with seg % 8 == 0");
+  TORCH_CHECK((size_t)inp.numel() <= c->args.half_elems, "message larger than the buffer");
+  TORCH_CHECK(inp.data_ptr() != out.data_ptr(), "all-to-all is out of place");
+  for (int p = 0; p < c->args.world; ++p)
+    TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
+  const c10::DeviceGuard g(inp.device());
+  akap::launch_custom_alltoall(c->args, inp.data_ptr(), out.data_ptr(), inp.numel() / W,
+                               cur_stream());
+}
+
 // In-place broadcast of buf (any dtype, nbytes % 16 == 0) from group rank `root`.
 void car_broadcast(int64_t h, Tensor buf, int64_t root) {
   CarComm* c = car_get(h);
@@ -1111,6 +1128,7 @@ TORCH_LIBRARY(akap, m) {
   m.def("car_destroy(int h) -> ()");
   m.def("car_all_gather(int h, Tensor inp, Tensor(a!) out) -> ()");
   m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
+  m.def("car_all_to_all(int h, Tensor inp, Tensor(a!) out) -> ()");
   m.def("ipc_export(Tensor t) -> Tensor");
   m.def("ipc_open(Tensor blob, int device) -> int");
   m.def("ipc_close(int addr) -> ()");
@@ -1183,6 +1201,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("kv_pull", &kv_pull);
   m.impl("car_all_gather", &car_all_gather);
   m.impl("car_broadcast", &car_broadcast);
+  m.impl("car_all_to_all", &car_all_to_all);
   m.impl("ipc_export", &ipc_export);
   m.impl("embedding", &embedding);
 }

@@ -5,7 +5,8 @@ sorted, tile-padded index list).  Two placements:
   * "tp": every rank holds all experts with the FFN dim split by tp (one all-reduce,
     like a dense layer) -- best at small batch on a single xGMI node;
   * "ep": rank e holds experts [e*E/ep, (e+1)*E/ep) whole; tokens are dispatched and
-    combined with two RCCL all_to_all_single calls over the EP (=dp x tp) group.
+    combined with two all-to-alls over the EP (=dp x tp) group (the custom IPC kernel at
+    decode sizes when the TP group spans the job, else RCCL all_to_all_single).
 Expert GEMMs: `ops.fused_moe` -- device-side sort + grouped MFMA GEMMs + gather-combine,
 no host sync, at every batch size in "tp" mode (decode steps inside the hipGraph, prefill
 chunks eagerly); the per-expert loop below serves only the CPU reference path.
@@ -49,7 +50,17 @@ def ep_overflow_reduce(device) -> torch.Tensor:
     sees the same value, so all of them re-run an overflowed step together."""
     f = MoEBlock.overflow_flag(device)
     if torch.distributed.is_initialized():
-        torch.distributed.all_reduce(f, op=torch.distributed.ReduceOp.MAX)
+        from ..parallel.state import get_state
+
+        st = get_state()
+        if st is not None and st.car is not None and st.tp_size == st.world_size:
+            # inside a captured decode step: the custom IPC all-reduce (a bf16 sum of 0/1 flags
+            # is exact for <= 8 ranks), no process-group collective in the graph
+            b = f.to(torch.bfloat16).repeat(8)
+            st.car.all_reduce(b)
+            f.copy_(torch.gt(b[:1], 0).to(torch.int32))
+        else:
+            torch.distributed.all_reduce(f, op=torch.distributed.ReduceOp.MAX)
     return f
 
 
@@ -275,22 +286,25 @@ class MoEBlock:
         flag = self.overflow_flag(h.device) if flag is None else flag
         torch.maximum(flag, (~fits).any().to(torch.int32).view(1), out=flag)
         tok = torch.arange(n, device=h.device) // K
-        send_x = h.new_zeros(ep * C + 1, d)
-        send_x.index_copy_(0, pos, h[tok])
-        send_e = torch.full((ep * C + 1,), -1, dtype=torch.int32, device=h.device)
-        send_e.index_copy_(0, pos, (flat - dest * el).to(torch.int32))
-        send_x, send_e = send_x[:ep * C], send_e[:ep * C]
-        recv_x = torch.empty_like(send_x)
-        recv_e = torch.empty_like(send_e)
-        grp = None  # the EP group is the whole job (dp x tp ranks)
-        torch.distributed.all_to_all_single(recv_x, send_x, group=grp)
-        torch.distributed.all_to_all_single(recv_e, send_e, group=grp)
+        # one message per row: the token's hidden vector plus 8 trailing bf16 slots whose
+        # first two carry the int32 local expert id (-1 = empty slot), so the dispatch is ONE
+        # all-to-all (the EP group is the whole job: dp x tp ranks)
+        send = h.new_zeros(ep * C + 1, d + 8)
+        send[:, :d].index_copy_(0, pos, h[tok])
+        ids_col = send[:, d:d + 2].view(torch.int32)  # [ep*C + 1, 1] view into the rows
+        ids_col.fill_(-1)
+        ids_col.index_copy_(0, pos, (flat - dest * el).to(torch.int32).view(-1, 1))
+        send = send[:ep * C]
+        recv = torch.empty_like(send)
+        comm.ep_all_to_all_equal(recv, send)
+        recv_x = recv[:, :d].contiguous()
+        recv_e = recv[:, d:d + 2].contiguous().view(torch.int32).reshape(-1, 1)
         # every received row is one (token, local expert) pair: K = 1, weight 1 (the router
         # weight is applied by the sender at combine); empty slots (id -1) give zero rows
         ones = torch.ones(ep * C, 1, dtype=torch.float32, device=h.device)
-        y = ops.fused_moe(recv_x, self.w13, self.w2, ones, recv_e.view(-1, 1))
+        y = ops.fused_moe(recv_x, self.w13, self.w2, ones, recv_e)
         back = h.new_zeros(ep * C + 1, d)
-        torch.distributed.all_to_all_single(back[:ep * C], y, group=grp)
+        comm.ep_all_to_all_equal(back[:ep * C], y.contiguous())
         mine = back.index_select(0, pos).view(T, K, d).float()
         return (mine * w.view(T, K, 1)).sum(1).to(h.dtype)
 

@@ -8,7 +8,8 @@ switch: a ring all-reduce is bound by one link per hop.  The policy here:
   * vocab-parallel logits -> the custom IPC all-gather (decode sizes; rank-major columns
     straight into the pre-allocated result) or one RCCL all_gather;
   * the TP decode step's input region -> the custom IPC broadcast (or RCCL broadcast);
-  * MoE token dispatch/combine -> all_to_all_single with explicit split sizes;
+  * MoE token dispatch/combine -> the custom IPC all-to-all (fixed-capacity decode steps,
+    equal splits) or all_to_all_single with explicit split sizes;
   * KV hand-off (P/D) -> one packed send/recv per request (see parallel/kv_transfer.py).
 All functions are no-ops for a group of size 1, so single-GPU code paths pay nothing.
 """
@@ -106,6 +107,18 @@ def tp_all_gather_last(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> t
         out = _gather_ws("result", R, st.tp_size * n, x.dtype, x.device)
     out.view(R, st.tp_size, n).copy_(buf.view(st.tp_size, R, n).transpose(0, 1))
     return out.view(*x.shape[:-1], st.tp_size * n)
+
+
+def ep_all_to_all_equal(recv: torch.Tensor, send: torch.Tensor) -> torch.Tensor:
+    """All-to-all over the whole job with equal splits (the fixed-capacity EP dispatch /
+    combine): the custom IPC kernel when the TP group is the whole job and the message fits
+    its staging (capturable on any control backend), else all_to_all_single."""
+    st = get_state()
+    if (st.car is not None and st.tp_size == st.world_size and st.car.a2a_ok(send)
+            and recv.is_contiguous() and recv.dtype == send.dtype):
+        return st.car.all_to_all(send.view(-1), recv.view(-1)).view_as(recv)
+    dist.all_to_all_single(recv, send)
+    return recv
 
 
 def tp_broadcast(t: torch.Tensor) -> torch.Tensor:

@@ -8,8 +8,8 @@ RCCL ring; larger messages (prefill) fall back to RCCL.  The kernels keep their 
 on the device, so they replay correctly inside captured hipGraphs.
 
 Siblings on the same IPC buffers, flags and device-side epochs: `all_gather` (the
-vocab-parallel logits, rank-major column blocks) and `broadcast` (rank 0's decode staging
-region).  With all three, a TP decode hipGraph records no RCCL call at all: it replays
+vocab-parallel logits, rank-major column blocks), `broadcast` (rank 0's decode staging
+region) and `all_to_all` (the expert-parallel fixed-capacity dispatch and combine).  With all three, a TP decode hipGraph records no RCCL call at all: it replays
 across the xGMI mesh and across ranks that share one GPU (gloo control plane) alike.
 
 Policy (xGMI mesh, W ranks): one-shot reads (W-1) x the message over W-1 links at once
@@ -89,6 +89,16 @@ class CustomAllReduce:
     def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """x [R, n] (this rank's shard) -> out [R, world*n], rank-major column blocks."""
         torch.ops.akap.car_all_gather(self.h, x, out)
+        return out
+
+    def a2a_ok(self, x: torch.Tensor) -> bool:
+        nbytes = x.numel() * x.element_size()
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
+                and x.numel() % (8 * self.world) == 0 and nbytes <= self.buffer_bytes)
+
+    def all_to_all(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Equal segments: x [world * seg] (segment d to rank d) -> out (segment p from rank p)."""
+        torch.ops.akap.car_all_to_all(self.h, x, out)
         return out
 
     def bcast_ok(self, t: torch.Tensor) -> bool:

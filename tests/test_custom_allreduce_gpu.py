@@ -277,8 +277,14 @@ def _ipc_siblings_worker(rank, world, port, q):
             if rank == 0:
                 b.copy_(torch.arange(b.numel(), dtype=torch.int64).remainder(251).to(torch.uint8))
             car.broadcast(b, 0)
+            # equal-segment all-to-all: segment d of rank r holds r * 1000 + d * 10 + j % 7
+            seg = 24 * (it + 1)
+            send = torch.cat([(torch.arange(seg) % 7 + rank * 1000 + d * 10).float()
+                              for d in range(world)]).to(torch.bfloat16).to(DEV)
+            recv = torch.empty_like(send)
+            car.all_to_all(send, recv)
             torch.cuda.synchronize()
-            res.append((out.float().cpu().numpy(), b.cpu().numpy()))
+            res.append((out.float().cpu().numpy(), b.cpu().numpy(), recv.float().cpu().numpy()))
         err = car.error()
         dist.barrier()
         car.close()
@@ -291,8 +297,8 @@ def _ipc_siblings_worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_custom_allgather_broadcast_ipc_processes(world):
-    """The IPC all-gather (rank-major columns) and broadcast, siblings of K13, across
-    processes sharing one MI355X: exact against the host-side expectation, every rank."""
+    """The IPC all-gather (rank-major columns), broadcast and all-to-all, siblings of K13,
+    across processes sharing one MI355X: exact against the host-side expectation, every rank."""
     import numpy as np
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -315,10 +321,14 @@ def test_custom_allgather_broadcast_ipc_processes(world):
                   .to(torch.bfloat16).float().numpy() for r in range(world)]
         want = np.concatenate(shards, axis=1)
         bexp = (np.arange(2048 + 16 * it) % 251).astype(np.uint8)
+        seg = 24 * (it + 1)
         for r in range(world):
-            got, b = out[r][1][it]
+            got, b, a2a = out[r][1][it]
             assert np.array_equal(got, want), (r, it)
             assert np.array_equal(b, bexp), (r, it)
+            # segment p of rank r's result is rank p's segment r
+            exp = np.concatenate([(np.arange(seg) % 7 + p * 1000 + r * 10) for p in range(world)])
+            assert np.array_equal(a2a, torch.tensor(exp).float().bfloat16().float().numpy()), (r, it)
 
 
 def _kv_pull_worker(rank, port, q, geo):

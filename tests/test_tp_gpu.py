@@ -56,7 +56,9 @@ def _port():
     ("tiny-llama", "tp", "1", "1"), ("tiny-qwen3", "tp", "1", "1"),
     # captured decode graphs replayed across the two processes: only IPC kernels inside
     ("tiny-llama", "tp", "1", "0"), ("tiny-qwen3", "tp", "1", "0"),
-    ("tiny-mixtral", "tp", "1", "0")])
+    ("tiny-mixtral", "tp", "1", "0"),
+    # expert parallel, captured: the fixed-capacity dispatch / combine on the IPC all-to-all
+    ("tiny-mixtral", "ep", "1", "0"), ("tiny-qwen3-moe", "ep", "1", "0")])
 def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode, car, eager):
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
