@@ -296,7 +296,7 @@ def _ipc_siblings_worker(rank, world, port, q):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_custom_allgather_broadcast_ipc_processes(world):
+def test_custom_allgather_broadcast_alltoall_ipc_processes(world):
     """The IPC all-gather (rank-major columns), broadcast and all-to-all, siblings of K13,
     across processes sharing one MI355X: exact against the host-side expectation, every rank."""
     import numpy as np
