@@ -165,7 +165,7 @@ class MoEBlock:
             hp = torch.cat([h, h.new_zeros(pad, h.shape[1])]) if pad else h
             mine = self._forward_tokens(hp[r * per:(r + 1) * per].contiguous())
             full = torch.empty(per * tp, h.shape[1], dtype=h.dtype, device=h.device)
-            torch.distributed.all_gather_into_tensor(full, mine, group=self.ps.tp_group)
+            comm.tp_all_gather_rows(full, mine)
             return full[:T]
         return self._forward_tokens(h)
 

@@ -109,6 +109,18 @@ def tp_all_gather_last(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> t
     return out.view(*x.shape[:-1], st.tp_size * n)
 
 
+def tp_all_gather_rows(out: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """Concatenate every TP rank's x along dim 0 into out (rank order): the IPC all-gather of
+    the flattened rows when it fits (capturable on any control backend), else RCCL."""
+    st = get_state()
+    flat = x.contiguous().view(1, -1)
+    if st.car is not None and st.car.gather_ok(flat) and out.is_contiguous():
+        st.car.all_gather(flat, out.view(1, -1))
+        return out
+    dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
+    return out
+
+
 def ep_all_to_all_equal(recv: torch.Tensor, send: torch.Tensor) -> torch.Tensor:
     """All-to-all over the whole job with equal splits (the fixed-capacity EP dispatch /
     combine): the custom IPC kernel when the TP group is the whole job and the message fits
