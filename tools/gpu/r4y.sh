@@ -1,5 +1,5 @@
 set -u
-O=gpurun_out/r4y; mkdir -p $O
+O=gpurun_out/r4z; mkdir -p $O
 run() { n=$1; t=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.log 2>&1; rc=$?; echo "$n rc=$rc"; [ $rc -le 1 ]; }
 P="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 run car 300 $P tests/test_custom_allreduce_gpu.py -k "alltoall" &&
