@@ -279,5 +279,7 @@ struct PrefetchList {
   int n;
 };
 void launch_l2_prefetch(const PrefetchList& L, uint32_t* sink, hipStream_t s);
+// host (pinned, device-mapped) -> device copy as a kernel on the stream
+void launch_h2d_stage(const void* host_src, void* dst, long bytes, hipStream_t s);
 
 }  // namespace akap

@@ -749,6 +749,18 @@ void pgemm(Tensor out, Tensor x, Tensor w, int64_t epi, std::optional<Tensor> of
   akap::launch_pgemm(a, (int)epi, cur_stream());
 }
 
+// dst (device) <- src (pinned host) by a kernel that reads the device mapping of the host
+// buffer (no hipMemcpyAsync): the caller keeps src untouched until the stream passes it
+void h2d_stage(Tensor dst, Tensor src) {
+  CHECK_GPU(dst); CHECK_CONTIG(dst); CHECK_CONTIG(src);
+  TORCH_CHECK(!src.is_cuda() && src.is_pinned(), "h2d_stage: src must be pinned host memory");
+  TORCH_CHECK(src.nbytes() == dst.nbytes(), "h2d_stage: size mismatch");
+  void* dev_src = nullptr;
+  HIP_OK(hipHostGetDevicePointer(&dev_src, src.data_ptr(), 0));
+  const c10::DeviceGuard g(dst.device());
+  akap::launch_h2d_stage(dev_src, dst.data_ptr(), (long)dst.nbytes(), cur_stream());
+}
+
 void embedding(Tensor ids, Tensor table, Tensor out, int64_t vocab_start, int64_t vocab_end) {
   CHECK_GPU(ids); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CONTIG(out);
   TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
@@ -1129,6 +1141,7 @@ TORCH_LIBRARY(akap, m) {
   m.def("car_all_gather(int h, Tensor inp, Tensor(a!) out) -> ()");
   m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
   m.def("car_all_to_all(int h, Tensor inp, Tensor(a!) out) -> ()");
+  m.def("h2d_stage(Tensor(a!) dst, Tensor src) -> ()");
   m.def("ipc_export(Tensor t) -> Tensor");
   m.def("ipc_open(Tensor blob, int device) -> int");
   m.def("ipc_close(int addr) -> ()");
@@ -1166,6 +1179,7 @@ TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("car_destroy", &car_destroy);
   m.impl("ipc_open", &ipc_open);
   m.impl("ipc_close", &ipc_close);
+  m.impl("h2d_stage", &h2d_stage);  // pinned CPU source + device destination
 }
 
 TORCH_LIBRARY_IMPL(akap, CUDA, m) {

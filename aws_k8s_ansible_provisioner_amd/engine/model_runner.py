@@ -27,6 +27,9 @@ from ..models.transformer import AttnBatch, DecoderLM
 from ..parallel.state import ParallelState, drain_pending_collectives, get_state
 from .config import EngineConfig
 
+# decode staging H2D as a kernel reading the pinned buffer (1) or hipMemcpyAsync (0, A/B)
+H2D_KERNEL = os.environ.get("AKAP_H2D_KERNEL", "1") != "0"
+
 DEFAULT_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320,
                    384, 448, 512]
 
@@ -231,7 +234,12 @@ class ModelRunner:
         nb = n * self.max_blocks
         hd_np["block_tables"][:nb] = self.np["block_tables"][:nb]
         end = self._dec_bt_off + nb * 4
-        self.ddec[:end].copy_(self.hdecs[slot][:end], non_blocking=True)
+        if self.is_gpu and H2D_KERNEL:
+            # a kernel reading the pinned buffer's device mapping: the step's next kernel
+            # follows it on the stream without the idle gap a hipMemcpyAsync H2D left
+            torch.ops.akap.h2d_stage(self.ddec[:end], self.hdecs[slot][:end])
+        else:
+            self.ddec[:end].copy_(self.hdecs[slot][:end], non_blocking=True)
         return slot
 
     def _h2d(self, key: str, n: int) -> torch.Tensor:

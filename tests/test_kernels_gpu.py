@@ -1005,3 +1005,13 @@ def test_pgemm_grouped(counts):
         y = ops.pgemm(x.to(DEV), w.to(DEV), silu=silu, offs=offs.to(DEV)).float().cpu()
         exp = ref.pgemm(x, w, silu, offs).float()
         assert (y - exp).abs().max().item() <= 3e-2 * exp.abs().max().item() + 1e-2, silu
+
+
+def test_h2d_stage_kernel_copies_pinned_host_memory():
+    """The in-stream staging copy (a kernel reading the pinned buffer's device mapping)."""
+    for n in (1, 15, 16, 4099, 65536 + 7):
+        src = torch.randint(0, 255, (n,), dtype=torch.uint8).pin_memory()
+        dst = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        torch.ops.akap.h2d_stage(dst, src)
+        torch.cuda.synchronize()
+        assert torch.equal(dst.cpu(), src)
