@@ -756,7 +756,8 @@ void h2d_stage(Tensor dst, Tensor src) {
   TORCH_CHECK(!src.is_cuda() && src.is_pinned(), "h2d_stage: src must be pinned host memory");
   TORCH_CHECK(src.nbytes() == dst.nbytes(), "h2d_stage: size mismatch");
   void* dev_src = nullptr;
-  HIP_OK(hipHostGetDevicePointer(&dev_src, src.data_ptr(), 0));
+  TORCH_CHECK(hipHostGetDevicePointer(&dev_src, src.data_ptr(), 0) == hipSuccess,
+              "h2d_stage: the pinned buffer has no device mapping");
   const c10::DeviceGuard g(dst.device());
   akap::launch_h2d_stage(dev_src, dst.data_ptr(), (long)dst.nbytes(), cur_stream());
 }
