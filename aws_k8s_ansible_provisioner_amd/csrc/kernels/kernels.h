@@ -281,6 +281,5 @@ struct PrefetchList {
 void launch_l2_prefetch(const PrefetchList& L, uint32_t* sink, hipStream_t s);
 // host (pinned, device-mapped) -> device copy as a kernel on the stream
 void launch_h2d_stage(const void* host_src, void* dst, long bytes, hipStream_t s);
-void launch_d2h_stage(const void* src, void* host_dst, long bytes, hipStream_t s);
 
 }  // namespace akap

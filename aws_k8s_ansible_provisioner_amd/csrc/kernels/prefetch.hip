@@ -42,28 +42,6 @@ __global__ __launch_bounds__(256) void h2d_stage_kernel(const uint8_t* __restric
   for (long j = (n16 << 4) + gid; j < bytes; j += stride) dst[j] = src[j];
 }
 
-// and back: the step's sampled tokens written straight into the pinned host buffer's device
-// mapping (the host reads them after the step's completion event)
-__global__ __launch_bounds__(256) void d2h_stage_kernel(const uint8_t* __restrict__ src,
-                                                        uint8_t* __restrict__ host_dst,
-                                                        long bytes) {
-  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-  const long stride = (long)gridDim.x * 256;
-  const long n16 = bytes >> 4;
-  for (long j = gid; j < n16; j += stride)
-    __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(src)[j],
-                                reinterpret_cast<u32x4*>(host_dst) + j);
-  for (long j = (n16 << 4) + gid; j < bytes; j += stride) host_dst[j] = src[j];
-}
-
-void launch_d2h_stage(const void* src, void* host_dst, long bytes, hipStream_t s) {
-  if (bytes <= 0) return;
-  long blocks = ((bytes >> 4) + 255) / 256;
-  if (blocks < 1) blocks = 1;
-  if (blocks > 64) blocks = 64;
-  d2h_stage_kernel<<<(int)blocks, 256, 0, s>>>((const uint8_t*)src, (uint8_t*)host_dst, bytes);
-}
-
 void launch_h2d_stage(const void* host_src, void* dst, long bytes, hipStream_t s) {
   if (bytes <= 0) return;
   long blocks = ((bytes >> 4) + 255) / 256;

@@ -762,18 +762,6 @@ void h2d_stage(Tensor dst, Tensor src) {
   akap::launch_h2d_stage(dev_src, dst.data_ptr(), (long)dst.nbytes(), cur_stream());
 }
 
-// dst (pinned host) <- src (device) by a kernel writing the host buffer's device mapping
-void d2h_stage(Tensor dst, Tensor src) {
-  CHECK_GPU(src); CHECK_CONTIG(dst); CHECK_CONTIG(src);
-  TORCH_CHECK(!dst.is_cuda() && dst.is_pinned(), "d2h_stage: dst must be pinned host memory");
-  TORCH_CHECK(src.nbytes() == dst.nbytes(), "d2h_stage: size mismatch");
-  void* dev_dst = nullptr;
-  TORCH_CHECK(hipHostGetDevicePointer(&dev_dst, dst.data_ptr(), 0) == hipSuccess,
-              "d2h_stage: the pinned buffer has no device mapping");
-  const c10::DeviceGuard g(src.device());
-  akap::launch_d2h_stage(src.data_ptr(), dev_dst, (long)src.nbytes(), cur_stream());
-}
-
 void embedding(Tensor ids, Tensor table, Tensor out, int64_t vocab_start, int64_t vocab_end) {
   CHECK_GPU(ids); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_CONTIG(out);
   TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
@@ -1155,7 +1143,6 @@ TORCH_LIBRARY(akap, m) {
   m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
   m.def("car_all_to_all(int h, Tensor inp, Tensor(a!) out) -> ()");
   m.def("h2d_stage(Tensor(a!) dst, Tensor src) -> ()");
-  m.def("d2h_stage(Tensor(a!) dst, Tensor src) -> ()");
   m.def("ipc_export(Tensor t) -> Tensor");
   m.def("ipc_open(Tensor blob, int device) -> int");
   m.def("ipc_close(int addr) -> ()");
@@ -1194,7 +1181,6 @@ TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("ipc_open", &ipc_open);
   m.impl("ipc_close", &ipc_close);
   m.impl("h2d_stage", &h2d_stage);  // pinned CPU source + device destination
-  m.impl("d2h_stage", &d2h_stage);  // device source + pinned CPU destination
 }
 
 TORCH_LIBRARY_IMPL(akap, CUDA, m) {

@@ -27,8 +27,7 @@ from ..models.transformer import AttnBatch, DecoderLM
 from ..parallel.state import ParallelState, drain_pending_collectives, get_state
 from .config import EngineConfig
 
-# decode staging H2D / token D2H as kernels on the pinned buffers' device mappings (1) or
-# hipMemcpyAsync (0, A/B)
+# decode staging H2D as a kernel reading the pinned buffer (1) or hipMemcpyAsync (0, A/B)
 H2D_KERNEL = os.environ.get("AKAP_H2D_KERNEL", "1") != "0"
 
 DEFAULT_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320,
@@ -485,10 +484,7 @@ class ModelRunner:
         if not self.is_gpu:
             return None, self.out_tokens[:B].clone()
         host = self.tok_host[slot][:B]
-        if H2D_KERNEL:
-            torch.ops.akap.d2h_stage(host, self.out_tokens[:B])
-        else:
-            host.copy_(self.out_tokens[:B], non_blocking=True)
+        host.copy_(self.out_tokens[:B], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ev, host

@@ -1008,16 +1008,10 @@ def test_pgemm_grouped(counts):
 
 
 def test_h2d_stage_kernel_copies_pinned_host_memory():
-    """The in-stream staging copies (kernels on the pinned buffers' device mappings)."""
+    """The in-stream staging copy (a kernel reading the pinned buffer's device mapping)."""
     for n in (1, 15, 16, 4099, 65536 + 7):
         src = torch.randint(0, 255, (n,), dtype=torch.uint8).pin_memory()
         dst = torch.zeros(n, dtype=torch.uint8, device=DEV)
         torch.ops.akap.h2d_stage(dst, src)
         torch.cuda.synchronize()
         assert torch.equal(dst.cpu(), src)
-        back = torch.zeros(n, dtype=torch.uint8).pin_memory()
-        torch.ops.akap.d2h_stage(back, dst)
-        ev = torch.cuda.Event()
-        ev.record()
-        ev.synchronize()  # the engine's protocol: the host reads after the step's event
-        assert torch.equal(back, src)
