@@ -136,7 +136,6 @@ struct PGemmArgs {
   const int* offs;  // grouped: [groups] cumulative row ends (device)
   int groups;       // 0 = dense
   int M, N, K, ldx, ldy;
-  int gm;           // M tiles per raster block (0 = default 8)
 };
 bool pgemm_supported(int M, int N, int K);
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st);

@@ -101,7 +101,7 @@ using H3 = HalfTile<3>;  // A rows of the bottom quadrants
 template <bool GROUPED>
 __device__ __forceinline__ bool pg_tile(const PGemmArgs& p, int& tm, int& tn, int& group,
                                         int& row_lo, int& row_hi) {
-  const int GM = p.gm > 0 ? p.gm : 8;
+  constexpr int GM = 8;
   const int tiles_n = p.N / PG_T;
   const int nwg = gridDim.x;
   const int id = xcd_remap(blockIdx.x, nwg);

@@ -740,11 +740,6 @@ void pgemm(Tensor out, Tensor x, Tensor w, int64_t epi, std::optional<Tensor> of
   a.Y = out.data_ptr();
   a.ldx = x.stride(0);
   a.ldy = out.stride(0);
-  static const int gm_env = [] {
-    const char* e = getenv("AKAP_PGEMM_GM");
-    return e ? atoi(e) : 0;
-  }();
-  a.gm = gm_env;
   TORCH_CHECK(a.ldx % 8 == 0 && a.ldy % 4 == 0, "row strides must keep 16-B / 8-B alignment");
   // the DMA addresses X and one group's W through buffer descriptors with 32-bit offsets
   TORCH_CHECK((int64_t)a.M * a.ldx * 2 < (int64_t(1) << 31) &&
