@@ -211,6 +211,15 @@ class ModelRunner:
                        for h in self.hdecs]
         self._dslot = 0
         self.dd = {k: view(self.ddec, o, dt, n) for k, (o, dt, n) in lay.items()}
+        # the staging kernel needs the pinned buffers' device mapping: probe it once, fall back
+        # to hipMemcpyAsync where the host allocator does not provide one
+        self._h2d_kernel = False
+        if self.is_gpu and H2D_KERNEL:
+            try:
+                torch.ops.akap.h2d_stage(self.ddec[:16], self.hdecs[0][:16])
+                self._h2d_kernel = True
+            except RuntimeError as e:
+                self.log(f"[runner] staging kernel unavailable ({e}); using hipMemcpyAsync")
         self.dd_bt = self.dd["block_tables"].view(S, mb)
         self._dec_bt_off = lay["block_tables"][0]
         self.out_tokens = torch.zeros(S, dtype=torch.int64, device=self.device)
@@ -234,7 +243,7 @@ class ModelRunner:
         nb = n * self.max_blocks
         hd_np["block_tables"][:nb] = self.np["block_tables"][:nb]
         end = self._dec_bt_off + nb * 4
-        if self.is_gpu and H2D_KERNEL:
+        if self._h2d_kernel:
             # a kernel reading the pinned buffer's device mapping: the step's next kernel
             # follows it on the stream without the idle gap a hipMemcpyAsync H2D left
             torch.ops.akap.h2d_stage(self.ddec[:end], self.hdecs[slot][:end])
