@@ -33,10 +33,17 @@
 //   epochs   per-block counters in device memory, read and written by thread 0 through the
 //            vector path (an agent-scope atomic, not s_load: the scalar cache is not kept
 //            coherent with vector stores), so a captured launch replays with fresh epochs.
-//   reuse    staging / result buffers alternate by epoch parity.  A rank writes the parity of
-//            epoch e+2 only inside launch e+2; it got there after epoch e+1's flags of every
-//            peer, i.e. after every peer finished launch e (stream order), so no peer can
-//            still be reading epoch e's bytes.
+//   reuse    staging / result buffers alternate by epoch parity.  EVERY launch runs all
+//            kCarMaxBlocks blocks, and every block advances its epoch and takes part in every
+//            flag exchange of the launch (blocks with no vectors of a small message exchange
+//            flags only), so all blocks of a rank hold the same epoch = the launch count.  A
+//            block writes the parity of epoch e+2 only inside launch e+2; it got there after
+//            its own epoch-(e+1) flags from every peer, i.e. after every peer STARTED launch
+//            e+1 and so finished ALL blocks of launch e (stream order) -- no peer block can
+//            still be reading any epoch-e bytes, whatever index -> block map launch e used.
+//            (With a size-dependent grid a block that sat out a small launch lagged its
+//            siblings' epoch, and a mixed-kind sequence could restage a region a peer's
+//            other block was still reading.)
 // Every spin-wait is bounded: on timeout the kernel records an error flag and exits.
 //
 // Siblings on the same buffers, flags and per-block epochs (so a TP decode hipGraph holds
@@ -47,8 +54,9 @@
 //               blocks: the vocab-parallel logits);
 //   broadcast   the root stages the bytes, one flag exchange, the other ranks read them (the
 //               TP decode step's input staging region).
-// Both keep the block -> element-chunk map a pure function of the size, identical on every
-// rank, so the epoch / parity reuse argument above holds for any mix of launches.
+// The reuse argument above needs only that every launch runs the full kCarMaxBlocks grid
+// (car_blocks), so it holds for any mix of sizes and kinds (tests/test_custom_allreduce_gpu.py
+// runs mixed back-to-back sequences with no host sync).
 #include "common.h"
 #include "kernels.h"
 
@@ -369,13 +377,10 @@ __global__ __launch_bounds__(256) void car_bcast_kernel(CarArgs a, bf16* buf, lo
   car_bcast(a, blockIdx.x, gridDim.x, buf, n8, root);
 }
 
-// Block count for n8 vectors: the same on every rank (a pure function of n8 and world).
-static int car_blocks(long n8, int world, bool two) {
-  const long per = two ? (n8 + world - 1) / world : n8;
-  long b = (per + 255) / 256;
-  if (b < 1) b = 1;
-  return (int)(b > kCarMaxBlocks ? kCarMaxBlocks : b);
-}
+// Block count of every launch: always the full kCarMaxBlocks, whatever the size and kind, so
+// every block's epoch counts every launch (header, "reuse").  Blocks past a small message's
+// vectors only exchange flags: ~W system-scope stores + polls each, in parallel with the rest.
+static int car_blocks(long, int, bool) { return kCarMaxBlocks; }
 
 void launch_custom_allreduce(const CarArgs& a, const void* in, void* out, long n, int two_shot,
                              hipStream_t s, const CarEpi* epi) {

@@ -139,6 +139,14 @@ struct PGemmArgs {
 };
 bool pgemm_supported(int M, int N, int K);
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st);
+// decode-sized M: the same 256 x 256 body with K split over `splits` workgroups per tile and
+// the slices combined in the launch (DGemmArgs epilogues: store | RESNORM | SILU, ss_in row
+// scale).  Needs grid = tiles * splits <= the CU count (all slices resident); ws fp32
+// pgemm_sk_ws_floats(); counters: 2 zeroed ints per tile (re-armed by the kernel), the error
+// word at counters[65535].
+bool pgemm_sk_supported(int M, int N, int K, int splits, int cus);
+long pgemm_sk_ws_floats(int M, int N, int splits);
+void launch_pgemm_sk(const DGemmArgs& p, int splits, hipStream_t st);
 
 // ---- wgemm.hip: wide-row weight-streaming GEMM (LM head) Y[M,N] = X[M,K] . W[N,K]^T ----
 struct WGemmArgs {
@@ -164,7 +172,10 @@ struct SampleParams {
   float* out_logprobs;       // [B] log-prob of the sampled token (may be null)
   int greedy_logprobs;       // also compute log-probs for greedy rows (one extra pass)
 };
-void launch_sample(const SampleParams& p, int B, hipStream_t s);
+// grid (sample_chunks(B, V) chunks, B rows); ws >= B * kMaxChunks * 32 bytes of partials,
+// tickets[B] int32 zeroed once (each row's last chunk re-arms its ticket)
+int sample_chunks(int B, int V);
+void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, hipStream_t s);
 // OpenAI/vLLM penalties on logits in place, for unique (row, token) entries:
 // repetition (prompt + output tokens, divide positive / multiply negative logits),
 // frequency * count and presence * [count > 0] (output tokens; count 0 = prompt-only)

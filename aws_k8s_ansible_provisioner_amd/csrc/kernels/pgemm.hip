@@ -47,6 +47,8 @@
 // v reads weight row ((v >> 4) & 1) * F + (v >> 5) * 16 + (v & 15) (the gdgemm.hip mapping), so
 // gate and up of one output column land in the same lane of adjacent fragments and the kernel
 // writes act[M, F] = silu(gate) * up directly.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -76,13 +78,29 @@ __device__ __forceinline__ void pg_sync() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// wait until at most 2 * `later` of this wave's DMA instructions are outstanding
+// wait until at most P * `later` of this wave's DMA instructions are outstanding (P = DMA
+// pieces per half-tile per wave: 2 with 8 waves, 4 with 4 waves)
+template <int P>
 __device__ __forceinline__ void pg_wait(int later) {
-  if (later >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (later == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (later == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  if (later >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P) : "memory");
+  else if (later == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+  else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+
+// Wave geometry of the 256 x 256 tile: WAVES = 8 -> 2 (M) x 4 (N) waves of 128 x 64 outputs;
+// WAVES = 4 -> 2 x 2 waves of 128 x 128 (one wave per SIMD: 64 accumulator fragments = 256
+// accumulator registers, a third fewer LDS fragment reads per MFMA).  Each wave's rows split
+// into a top and a bottom 64-row half, its columns into a left and a right half, so both forms
+// run the same four-quadrant phase pipeline over the same four half-tiles.
+template <int WAVES>
+struct PgGeo {
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int P = 16 / WAVES;        // DMA pieces (1 KiB) per half-tile per wave
+  static constexpr int WN = WAVES / 2;        // waves along N
+  static constexpr int WCOLS = PG_T / WN;     // output columns per wave
+  static constexpr int NJ = WCOLS / 32;       // 16-column fragments per column half
+};
 
 template <int V>
 struct HalfTile {
@@ -137,22 +155,28 @@ __device__ __forceinline__ bool pg_tile(const PGemmArgs& p, int& tm, int& tn, in
   }
 }
 
-template <int EPI, bool GROUPED, int NB>
-__global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
-  __shared__ bf16x8 lds[2 * PG_BUF];
+// The 256 x 256 main loop over K tiles [kt0, kt0 + nk): X rows from m0 (rows past the X
+// descriptor's range read as 0), W rows of tile columns n0.. (SILU_ROWS: the [gate; up] row
+// interleave of the SwiGLU epilogue, `nhalf` = F).  Leaves the tile in acc (lane: rows
+// wm*128 + i*16 + fr, 4 consecutive columns wn*64 + j*16 + fg*4 per fragment).
+// a wave's accumulator fragments: rows i (8 x 16), columns j (2 NJ x 16)
+template <int NJ2>
+struct PgAcc {
+  f32x4 v[8][NJ2];
+};
+
+template <int NB, bool SILU_ROWS, int WAVES, typename ACC>
+__device__ __forceinline__ void pg_mainloop(bf16x8* lds, const __amdgpu_buffer_rsrc_t rx,
+                                            const __amdgpu_buffer_rsrc_t rw, int ldx, int K,
+                                            int nhalf, int m0, int n0, int kt0, int nk,
+                                            ACC& accs) {
+  using G = PgGeo<WAVES>;
+  constexpr int P = G::P, NJ = G::NJ;
+  auto& acc = accs.v;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / G::WN, wn = w % G::WN;
   const int fr = lane & 15, fg = lane >> 4;
-
-  // ---- tile of this workgroup --------------------------------------------------------------
-  int tm, tn, group, row_lo, row_hi;
-  if (!pg_tile<GROUPED>(p, tm, tn, group, row_lo, row_hi)) return;  // surplus WG (uniform)
-  const int m0 = row_lo + tm * PG_T, n0 = tn * PG_T;
-  const int nk = p.K / PG_BK;
-  const bf16* X = static_cast<const bf16*>(p.X);
-  const bf16* W = static_cast<const bf16*>(p.W) + (GROUPED ? (size_t)group * p.N * p.K : 0);
-
   // ---- per-lane DMA sources: half-tile h (0 A top, 1 W left, 2 W right, 3 A bottom), the
   // wave's two 8-row pieces q = 2w, 2w+1 of it.  Rows past the tile's valid range re-read a
   // valid row (results never stored).
@@ -160,32 +184,28 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   // 32-bit per-lane byte offsets (8 VGPRs for the 8 sources), the K position in the scalar
   // offset.  X rows past M fall outside the descriptor's range and read as 0 (rows of a
   // neighbouring group inside it are harmless: those accumulator rows are never stored).
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)X, (short)0, (int)((size_t)p.M * p.ldx * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)W, (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
-  uint32_t voff[4][2];
-  int dst[4][2];  // 16-B unit offset inside a buffer
+  uint32_t voff[4][PgGeo<WAVES>::P];
+  int dst[4][PgGeo<WAVES>::P];  // 16-B unit offset inside a buffer
 #pragma unroll
   for (int h = 0; h < 4; ++h)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int q = 2 * w + e;
+    for (int e = 0; e < P; ++e) {
+      const int q = P * w + e;  // the half-tile's 16 pieces of 8 rows
       int r0;
       if (h == 0) r0 = (q >> 3) * 128 + (q & 7) * 8;
       else if (h == 3) r0 = (q >> 3) * 128 + 64 + (q & 7) * 8;
-      else if (h == 1) r0 = (q >> 2) * 64 + (q & 3) * 8;
-      else r0 = (q >> 2) * 64 + 32 + (q & 3) * 8;
+      else if constexpr (WAVES == 8) r0 = (q >> 2) * 64 + (h == 2 ? 32 : 0) + (q & 3) * 8;
+      else r0 = (q >> 3) * 128 + (h == 2 ? 64 : 0) + (q & 7) * 8;
       const int row = r0 + (lane >> 3);
       const int chunk = (lane & 7) ^ ((row >> 1) & 7);
       if (h == 0 || h == 3) {
-        voff[h][e] = (uint32_t)(((m0 + row) * p.ldx + chunk * 8) * 2);
+        voff[h][e] = (uint32_t)(((m0 + row) * ldx + chunk * 8) * 2);
         dst[h][e] = r0 * 8;
       } else {
         const int v = n0 + row;
         int wr = v;
-        if constexpr (EPI == EPI_SILU) wr = ((v >> 4) & 1) * (p.N >> 1) + (v >> 5) * 16 + (v & 15);
-        voff[h][e] = (uint32_t)((wr * p.K + chunk * 8) * 2);
+        if constexpr (SILU_ROWS) wr = ((v >> 4) & 1) * nhalf + (v >> 5) * 16 + (v & 15);
+        voff[h][e] = (uint32_t)((wr * K + chunk * 8) * 2);
         dst[h][e] = PG_T * 8 + r0 * 8;
       }
     }
@@ -195,22 +215,25 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
     constexpr int h = decltype(hc)::value;
     if (j >= nk) return;
     bf16x8* buf = lds + (j & 1) * PG_BUF;
-    const uint32_t kb = (uint32_t)(j * PG_BK * 2);
+    const uint32_t kb = (uint32_t)((kt0 + j) * PG_BK * 2);
+    // (the host pass of hipcc rejects this builtin inside the wave-count template's generic
+    // lambda during overload resolution; the device pass compiles it)
+#if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
-    for (int e = 0; e < 2; ++e)
+    for (int e = 0; e < PgGeo<WAVES>::P; ++e)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           h == 0 || h == 3 ? rx : rw, (__attribute__((address_space(3))) void*)(buf + dst[h][e]),
           16, voff[h][e], kb, 0, 0);
+#endif
   };
   auto later = [&](int s) { return min(3, 4 * nk - 1 - s); };
 
   // ---- fragments -----------------------------------------------------------------------------
-  bf16x8 at[4][2], ab[4][2], bl[2][2], br[2][2];
-  f32x4 acc[8][4];
+  bf16x8 at[4][2], ab[4][2], bl[PgGeo<WAVES>::NJ][2], br[PgGeo<WAVES>::NJ][2];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2 * NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto rd_a = [&](bf16x8 (&a)[4][2], const bf16x8* buf, int half) {
 #pragma unroll
@@ -219,21 +242,23 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
       for (int s = 0; s < 2; ++s)
         a[i][s] = buf[pg_unit(wm * 128 + half * 64 + i * 16 + fr, fg + 4 * s)];
   };
-  auto rd_b = [&](bf16x8 (&b)[2][2], const bf16x8* buf, int half) {
+  auto rd_b = [&](bf16x8 (&b)[PgGeo<WAVES>::NJ][2], const bf16x8* buf, int half) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        b[j][s] = buf[PG_T * 8 + pg_unit(wn * 64 + half * 32 + j * 16 + fr, fg + 4 * s)];
+        b[j][s] = buf[PG_T * 8 + pg_unit(wn * G::WCOLS + half * (G::WCOLS / 2) + j * 16 + fr,
+                                         fg + 4 * s)];
   };
-  auto mma = [&](const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int i0, int j0) {
+  auto mma = [&](const bf16x8 (&a)[4][2], const bf16x8 (&b)[PgGeo<WAVES>::NJ][2], int i0,
+                 int j0) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i0 + i][j0 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s], a[i][s], acc[i0 + i][j0 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
@@ -248,8 +273,8 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
   issue(H1{}, 1);
   {
     const int outstanding = min(6, 4 * nk) - 2;  // half-tiles after seq 1 already issued
-    if (outstanding >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // nk == 1: seqs 2, 3 after it
+    if (outstanding >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * P) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");  // nk == 1: seqs 2, 3
   }
   pg_sync();
   rd_a(at, lds, 0);
@@ -262,24 +287,24 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
     const bf16x8* nxt = lds + ((t + 1) & 1) * PG_BUF;
     if constexpr (NB == 4) {
       // phase 1: W right of t landed -> its fragments; DMA W right (t+1); quadrant top x left
-      pg_wait(later(4 * t + 2));
+      pg_wait<P>(later(4 * t + 2));
       pg_sync();
       rd_b(br, cur, 1);
       issue(H2{}, t + 1);
       mma(at, bl, 0, 0);
       // phase 2: A bottom of t -> fragments; DMA A bottom (t+1); quadrant top x right
-      pg_wait(later(4 * t + 3));
+      pg_wait<P>(later(4 * t + 3));
       pg_sync();
       rd_a(ab, cur, 1);
       issue(H3{}, t + 1);
-      mma(at, br, 0, 2);
+      mma(at, br, 0, NJ);
       // phase 3: buffer t&1 fully read -> DMA A top (t+2) into it; quadrant bottom x left
       pg_sync();
       issue(H0{}, t + 2);
       mma(ab, bl, 4, 0);
     } else {
       // phase 1: W right + A bottom of t landed -> both fragment sets; DMA both for t+1
-      pg_wait(allow(4 * t + 3, 4 * t + 5));
+      pg_wait<P>(allow(4 * t + 3, 4 * t + 5));
       pg_sync();
       rd_b(br, cur, 1);
       rd_a(ab, cur, 1);
@@ -287,7 +312,7 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
       issue(H3{}, t + 1);
       mma(at, bl, 0, 0);
       // phase 2 (no barrier): quadrant top x right
-      mma(at, br, 0, 2);
+      mma(at, br, 0, NJ);
       // phase 3 (no barrier): A top of t+2 into buffer t&1 -- its last reads (phase 4 of t-1)
       // retired before phase 1's barrier; quadrant bottom x left
       issue(H0{}, t + 2);
@@ -295,15 +320,41 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
     }
     // phase 4: A top + W left of t+1 -> fragments; DMA W left (t+2); quadrant bottom x right
     if (t + 1 < nk) {
-      if constexpr (NB == 4) pg_wait(later(4 * (t + 1) + 1));
-      else pg_wait(allow(4 * t + 5, 4 * t + 8));
+      if constexpr (NB == 4) pg_wait<P>(later(4 * (t + 1) + 1));
+      else pg_wait<P>(allow(4 * t + 5, 4 * t + 8));
       pg_sync();
       rd_a(at, nxt, 0);
       rd_b(bl, nxt, 0);
     }
     issue(H1{}, t + 2);
-    mma(ab, br, 4, 2);
+    mma(ab, br, 4, NJ);
   }
+}
+
+template <int EPI, bool GROUPED, int NB, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void pgemm_kernel(PGemmArgs p) {
+  using G = PgGeo<WAVES>;
+  constexpr int NJ = G::NJ;
+  __shared__ bf16x8 lds[2 * PG_BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / G::WN, wn = w % G::WN;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  // ---- tile of this workgroup --------------------------------------------------------------
+  int tm, tn, group, row_lo, row_hi;
+  if (!pg_tile<GROUPED>(p, tm, tn, group, row_lo, row_hi)) return;  // surplus WG (uniform)
+  const int m0 = row_lo + tm * PG_T, n0 = tn * PG_T;
+  const bf16* X = static_cast<const bf16*>(p.X);
+  const bf16* W = static_cast<const bf16*>(p.W) + (GROUPED ? (size_t)group * p.N * p.K : 0);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, (short)0, (int)((size_t)p.M * p.ldx * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)W, (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
+  PgAcc<2 * PgGeo<WAVES>::NJ> accs;
+  auto& acc = accs.v;
+  pg_mainloop<NB, EPI == EPI_SILU, WAVES>(lds, rx, rw, p.ldx, p.K, p.N >> 1, m0, n0, 0,
+                                          p.K / PG_BK, accs);
 
   // ---- epilogue: lane holds rows wm*128 + i*16 + fr, 4 consecutive cols per fragment ---------
   bf16* Y = static_cast<bf16*>(p.Y);
@@ -314,8 +365,8 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
     if constexpr (EPI == EPI_SILU) {
       // fragments j (gate) and j+1 (up) of one 32-column group -> 16 output columns
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int col = (n0 >> 1) + wn * 32 + jj * 16 + fg * 4;
+      for (int jj = 0; jj < NJ; ++jj) {
+        const int col = (n0 >> 1) + wn * (G::WCOLS / 2) + jj * 16 + fg * 4;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -327,8 +378,8 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + j * 16 + fg * 4;
+      for (int j = 0; j < 2 * NJ; ++j) {
+        const int col = n0 + wn * G::WCOLS + j * 16 + fg * 4;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[i][j][r]);
@@ -336,6 +387,242 @@ __global__ __launch_bounds__(PG_THREADS, 1) void pgemm_kernel(PGemmArgs p) {
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Decode-sized M (<= a few row tiles) with the K range split over workgroups and the slices
+// combined INSIDE the launch (DGemmArgs form, the decode chain's epilogues).  At M = 256 a
+// Llama-3-8B projection has only N / 256 = 16 .. 112 output tiles, so one tile per workgroup
+// leaves most of the 256 CUs idle; here tile t runs as `splits` workgroups, slice s taking K
+// tiles [s nk / splits, (s+1) nk / splits) through the same 256 x 256 main loop, and then:
+//   publish  the fp32 partial tile goes to its slab with write-through (sc1) 16-B stores, every
+//            wave drains (`s_waitcnt vmcnt(0)`), the workgroup barrier, one agent-scope ticket
+//            add on the tile's arrival counter (MI355X_MICROARCH.md "Valid forms", the first
+//            row of the sc1 table: no release fence, no acquire);
+//   combine  every slice waits (one lane, relaxed agent polls, bounded) until all `splits`
+//            slices arrived -- the grid is sized <= the CU count at one 512-thread, 128 KB-LDS
+//            workgroup per CU, so all slices are resident -- then reduces ITS 256 / splits
+//            rows of the tile over all slabs with sc1 16-B loads and applies the epilogue
+//            (row scale by ss_in, plain store / residual + next-norm / SwiGLU);
+//   re-arm   the last slice to finish its rows zeroes the tile's two counters.
+// The distributed combine keeps each workgroup's slab reads to 256 KB whatever the split
+// (a last-arriver combine would read (splits - 1) x 256 KB on one CU).
+__device__ __forceinline__ bool pg_spin_ge(const int* c, int v) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+    if (wall_clock64() - t0 > 100000000ull) return false;  // ~1 s: give up (error flag)
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+constexpr int kPgSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1-bypass loads)
+
+// Epilogue of 4 consecutive output columns (col) of one row, values y (fp32, before the row
+// scale): EPI_STORE / EPI_RESNORM; returns the row's sum-of-squares contribution (RESNORM).
+template <int EPI>
+__device__ __forceinline__ float pg_epi4(const DGemmArgs& p, int row, int col, f32x4 y,
+                                         float scale) {
+  bf16* Y = static_cast<bf16*>(p.Y);
+  bf16x4 o;
+  if constexpr (EPI == EPI_RESNORM) {
+    const bf16x4 r = *reinterpret_cast<const bf16x4*>(Y + (size_t)row * p.ldy + col);
+    const bf16x4 g = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.ln_out) + col);
+    bf16x4 a;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = f2bf(bf2f(f2bf(y[k] * scale)) + bf2f(r[k]));
+      const float f = bf2f(o[k]);
+      a[k] = f2bf(f * bf2f(g[k]));
+      q += f * f;
+    }
+    *reinterpret_cast<bf16x4*>(Y + (size_t)row * p.ldy + col) = o;
+    *reinterpret_cast<bf16x4*>(static_cast<bf16*>(p.Aout) + (size_t)row * p.N + col) = a;
+    return q;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = f2bf(y[k] * scale);
+    *reinterpret_cast<bf16x4*>(Y + (size_t)row * p.ldy + col) = o;
+    return 0.f;
+  }
+}
+
+// SwiGLU epilogue of 4 output features: gate g, up u (fp32, before the row scale)
+__device__ __forceinline__ void pg_epi_silu(const DGemmArgs& p, int row, int col, f32x4 g,
+                                            f32x4 u, float scale) {
+  bf16x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gg = bf2f(f2bf(g[k] * scale));
+    const float uu = bf2f(f2bf(u[k] * scale));
+    o[k] = f2bf(bf2f(f2bf(gg / (1.f + __expf(-gg)))) * uu);
+  }
+  *reinterpret_cast<bf16x4*>(static_cast<bf16*>(p.Y) + (size_t)row * p.ldy + col) = o;
+}
+
+__device__ __forceinline__ float pg_row_scale(const DGemmArgs& p, int row) {
+  return p.ss_in != nullptr ? rsqrtf(p.ss_in[row] / (float)p.K + p.eps) : 1.f;
+}
+
+template <int EPI, int NB, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void pgemm_sk_kernel(DGemmArgs p, int splits) {
+  using G = PgGeo<WAVES>;
+  constexpr int NJ = G::NJ, THREADS = G::THREADS;
+  __shared__ bf16x8 lds[2 * PG_BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / G::WN, wn = w % G::WN;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int tiles_n = p.N / PG_T;
+  const int tiles_m = (p.M + PG_T - 1) / PG_T;
+  const int nwg = tiles_m * tiles_n * splits;
+  const int id = xcd_remap(blockIdx.x, nwg);  // a tile's slices on consecutive ids (one XCD)
+  const int tile = id / splits, s = id % splits;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * PG_T, n0 = tn * PG_T;
+  const int nk = p.K / PG_BK;
+  const int kt0 = s * nk / splits, kt1 = (s + 1) * nk / splits;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.X), (short)0, (int)((size_t)p.M * p.ldx * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.W), (short)0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
+  PgAcc<2 * PgGeo<WAVES>::NJ> accs;
+  auto& acc = accs.v;
+  pg_mainloop<NB, EPI == EPI_SILU, WAVES>(lds, rx, rw, p.ldx, p.ldw, p.N >> 1, m0, n0, kt0,
+                                          kt1 - kt0, accs);
+
+  if (splits == 1) {  // whole K in this workgroup: the epilogue straight from the registers
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = m0 + wm * 128 + i * 16 + fr;
+      if (row >= p.M) continue;
+      const float sc = pg_row_scale(p, row);
+      if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj)
+          pg_epi_silu(p, row, (n0 >> 1) + wn * (G::WCOLS / 2) + jj * 16 + fg * 4,
+                      acc[i][2 * jj], acc[i][2 * jj + 1], sc);
+      } else {
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2 * NJ; ++j)
+          q += pg_epi4<EPI>(p, row, n0 + wn * G::WCOLS + j * 16 + fg * 4, acc[i][j], sc);
+        if constexpr (EPI == EPI_RESNORM) atomicAdd(p.ss_out + row, q);
+      }
+    }
+    return;
+  }
+  // ---- publish the partial tile (write-through), take a ticket ----
+  constexpr int SLAB = PG_T * PG_T;  // floats
+  float* slabs = p.ws + (size_t)tile * splits * SLAB;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)slabs, (short)0, (int)((size_t)splits * SLAB * 4), 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * NJ; ++j) {
+      const int r = wm * 128 + i * 16 + fr, c = wn * G::WCOLS + j * 16 + fg * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                             (int)(((size_t)s * SLAB + r * PG_T + c) * 4), 0,
+                                             kPgSc1);
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
+  __syncthreads();
+  int* arrive = p.counters + 2 * tile;
+  int* done = arrive + 1;
+  if (tid == 0) {
+    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!pg_spin_ge(arrive, splits))
+      __hip_atomic_fetch_or(p.counters + 65535, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  // ---- combine rows [r0, r1) of the tile over every slab (sc1 loads) ----
+  const int r0 = s * PG_T / splits, r1 = (s + 1) * PG_T / splits;
+  if constexpr (EPI == EPI_SILU) {
+    // a row has 32 gate chunks of 4 columns; gate chunk cg <-> tile columns 32 (cg/4) + 4 (cg%4)
+    // (gate) and + 16 (up): output features n0/2 + 16 (cg/4) + 4 (cg%4) .. + 3
+    for (int e = tid; e < (r1 - r0) * 32; e += THREADS) {
+      const int r = r0 + e / 32, cg = e % 32;
+      const int row = m0 + r;
+      if (row >= p.M) continue;
+      const int cgate = (cg >> 2) * 32 + (cg & 3) * 4;
+      f32x4 g = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < splits; ++q) {
+        const size_t base = ((size_t)q * SLAB + r * PG_T + cgate) * 4;
+        g += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)base, 0,
+                                                                              kPgSc1));
+        u += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rs, (int)(base + 64), 0, kPgSc1));
+      }
+      pg_epi_silu(p, row, (n0 >> 1) + (cg >> 2) * 16 + (cg & 3) * 4, g, u, pg_row_scale(p, row));
+    }
+  } else {
+    // 64 chunks of 4 columns per row; with RESNORM the 64 lanes of a wave own one row (its
+    // sum of squares is reduced across the wave, one atomic per row)
+    for (int e = tid; e < (r1 - r0) * 64; e += THREADS) {
+      const int r = r0 + e / 64, c = (e % 64) * 4;
+      const int row = m0 + r;
+      f32x4 y = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < splits; ++q)
+        y += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rs, (int)(((size_t)q * SLAB + r * PG_T + c) * 4), 0,
+                                           kPgSc1));
+      float qs = 0.f;
+      if (row < p.M) qs = pg_epi4<EPI>(p, row, n0 + c, y, pg_row_scale(p, row));
+      if constexpr (EPI == EPI_RESNORM) {
+        qs = wave_sum(qs);
+        if (lane == 0 && row < p.M) atomicAdd(p.ss_out + row, qs);
+      }
+    }
+  }
+  // ---- re-arm the tile's counters (the last slice to finish its rows) ----
+  __syncthreads();
+  if (tid == 0) {
+    const int d = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == splits - 1) {
+      __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+bool pgemm_sk_supported(int M, int N, int K, int splits, int cus) {
+  const int nk = K / PG_BK;
+  const long grid = (long)((M + PG_T - 1) / PG_T) * (N / PG_T) * splits;
+  return M > 0 && N % PG_T == 0 && K % PG_BK == 0 && splits >= 1 && splits <= 32 &&
+         nk >= splits && grid <= cus && (N / PG_T) * ((M + PG_T - 1) / PG_T) * 2 < 65535;
+}
+
+long pgemm_sk_ws_floats(int M, int N, int splits) {
+  if (splits <= 1) return 0;
+  return (long)((M + PG_T - 1) / PG_T) * (N / PG_T) * splits * PG_T * PG_T;
+}
+
+// Wave form of the 256 x 256 body: AKAP_PGEMM_WAVES = 8 (2 x 4 waves of 128 x 64) or 4 (2 x 2
+// waves of 128 x 128), read once per process.
+int pgemm_waves() {
+  static int w = [] {
+    const char* e = getenv("AKAP_PGEMM_WAVES");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return w;
+}
+
+template <int WAVES>
+static void launch_pgemm_sk_w(const DGemmArgs& p, int splits, hipStream_t st) {
+  const int grid = ((p.M + PG_T - 1) / PG_T) * (p.N / PG_T) * splits;
+  constexpr int T = WAVES * 64;
+  if (p.epi == EPI_SILU) pgemm_sk_kernel<EPI_SILU, 4, WAVES><<<grid, T, 0, st>>>(p, splits);
+  else if (p.epi == EPI_RESNORM)
+    pgemm_sk_kernel<EPI_RESNORM, 2, WAVES><<<grid, T, 0, st>>>(p, splits);
+  else pgemm_sk_kernel<EPI_STORE, 2, WAVES><<<grid, T, 0, st>>>(p, splits);
+}
+
+void launch_pgemm_sk(const DGemmArgs& p, int splits, hipStream_t st) {
+  if (p.M == 0) return;
+  if (pgemm_waves() == 4) launch_pgemm_sk_w<4>(p, splits, st);
+  else launch_pgemm_sk_w<8>(p, splits, st);
 }
 
 bool pgemm_supported(int M, int N, int K) {
@@ -349,12 +636,23 @@ void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
   // two barriers per K tile (measured 1-4 % faster than four, profiles/r4_pgemm_nb_ab.log); the
   // SwiGLU form keeps four: with both fragment sets read in phase 1 it would spill
+  if (pgemm_waves() == 4) {
+    constexpr int T = 4 * 64;
+    if (p.groups > 0) {
+      if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, 4, 4><<<grid, T, 0, st>>>(p);
+      else pgemm_kernel<EPI_STORE, true, 2, 4><<<grid, T, 0, st>>>(p);
+    } else {
+      if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, 4, 4><<<grid, T, 0, st>>>(p);
+      else pgemm_kernel<EPI_STORE, false, 2, 4><<<grid, T, 0, st>>>(p);
+    }
+    return;
+  }
   if (p.groups > 0) {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, 4><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, true, 2><<<grid, PG_THREADS, 0, st>>>(p);
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, 4, 8><<<grid, PG_THREADS, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, true, 2, 8><<<grid, PG_THREADS, 0, st>>>(p);
   } else {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, 4><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, false, 2><<<grid, PG_THREADS, 0, st>>>(p);
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, 4, 8><<<grid, PG_THREADS, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, false, 2, 8><<<grid, PG_THREADS, 0, st>>>(p);
   }
 }
 

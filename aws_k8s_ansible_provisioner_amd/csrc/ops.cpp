@@ -307,6 +307,19 @@ void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk,
 // rout = x + r out, ln = norm weight), 2 SiLU(gate) * up over x = [gate|up].
 // epi 0 store, 1 residual/next-norm (out = residual in/out, aout = bf16(out * ln_out),
 // ss_out += row sums of squares), 2 SwiGLU over gate/up-interleaved rows (out [M, N/2]).
+// Compute units of a device (cached): the persistent / in-launch-combine GEMM grids must fit.
+static int device_cus(int dev) {
+  static int cached[16] = {0};
+  if (dev < 0 || dev >= 16) dev = 0;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t splitk, int64_t pf,
            std::optional<Tensor> r, std::optional<Tensor> rout, std::optional<Tensor> ln,
            double eps, int64_t epi, std::optional<Tensor> ss_in, std::optional<Tensor> ss_out,
@@ -324,9 +337,15 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
               "dgemm: out shape");
   TORCH_CHECK(bn == 0 || pro == akap::PRO_PLAIN, "dgemm: the LDS-DMA variant has the plain prologue");
   TORCH_CHECK(bm == 64 || bn > 0, "dgemm: 128-row tiles are an LDS-DMA (bn > 0) variant");
-  TORCH_CHECK(bn > 0 ? akap::gdgemm_supported(M, N, K, splitk, bn, bm)
-                     : akap::dgemm_supported(M, N, K, splitk, pf),
+  // bn == 256: the 256 x 256 pgemm body with an in-launch distributed split-K combine
+  // (pgemm.hip pgemm_sk_kernel); the grid must fit the CUs (every slice resident)
+  const bool sk = bn == 256;
+  TORCH_CHECK(sk ? akap::pgemm_sk_supported(M, N, K, (int)splitk, device_cus(x.device().index()))
+                 : bn > 0 ? akap::gdgemm_supported(M, N, K, splitk, bn, bm)
+                          : akap::dgemm_supported(M, N, K, splitk, pf),
               "dgemm: unsupported M/N/K/splitk/pf/bn");
+  TORCH_CHECK(!sk || splitk == 1 || counters.has_value(),
+              "dgemm bn=256: split-K needs the counters (2 per tile)");
   const bool inlaunch = counters.has_value() && splitk > 1 && bn > 0;
   TORCH_CHECK(inlaunch ? (epi != akap::EPI_SILU || N % 32 == 0)
                        : akap::dgemm_epi_supported(N, epi, splitk),
@@ -335,8 +354,9 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
               "dgemm: 16-byte aligned rows");
   if (splitk > 1) {
-    const int64_t need = bn > 0 ? akap::gdgemm_ws_floats(M, N, (int)splitk, (int)bn, (int)bm)
-                                : splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
+    const int64_t need = sk ? akap::pgemm_sk_ws_floats(M, N, (int)splitk)
+                         : bn > 0 ? akap::gdgemm_ws_floats(M, N, (int)splitk, (int)bn, (int)bm)
+                                  : splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
     TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= need,
                 "dgemm: fp32 workspace of splitk*M*N (+ splitk*M for the norm)");
     TORCH_CHECK(out.stride(0) == N || (counters.has_value() && bn > 0),
@@ -358,8 +378,9 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   if (counters && splitk > 1 && bn > 0) {
     // in-launch split-K combine: one zeroed int32 ticket per output tile
     TORCH_CHECK(counters->scalar_type() == at::kInt && counters->is_cuda() &&
-                    counters->numel() >= (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn),
-                "dgemm: counters int32, one per output tile");
+                    counters->numel() >= (sk ? 65536 : (int64_t)((M + bm - 1) / bm) *
+                                                           ((N + bn - 1) / bn)),
+                "dgemm: counters int32, one per output tile (bn=256: the 65536-int array)");
     a.counters = counters->data_ptr<int>();
   }
   if (pro == akap::PRO_ADDNORM) {
@@ -390,6 +411,10 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
     a.ln_out = ln_out->data_ptr();
   }
   const c10::DeviceGuard g(x.device());
+  if (sk) {
+    akap::launch_pgemm_sk(a, (int)splitk, cur_stream());
+    return;
+  }
   akap::launch_dgemm(a, (int)pro, (int)splitk, (int)pf, cur_stream());
 }
 
@@ -454,7 +479,8 @@ bool dgemm_ok(int64_t M, int64_t N, int64_t K, int64_t splitk, int64_t pf) {
 }
 
 void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
-            Tensor steps, Tensor out_tokens, Tensor out_logprobs, bool greedy_logprobs) {
+            Tensor steps, Tensor out_tokens, Tensor out_logprobs, bool greedy_logprobs,
+            Tensor ws, Tensor tickets) {
   CHECK_GPU(logits);
   TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16,
               "sampler expects fp32 or bf16 logits");
@@ -477,8 +503,16 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tenso
   p.out_tokens = out_tokens.data_ptr<int64_t>();
   p.out_logprobs = out_logprobs.numel() ? out_logprobs.data_ptr<float>() : nullptr;
   p.greedy_logprobs = greedy_logprobs ? 1 : 0;
+  // workspace: per-(row, chunk) 32-byte partial records + one ticket per row (ops.sample keeps
+  // both persistent; the tickets are zeroed once and re-armed by each row's last chunk)
+  CHECK_GPU(ws); CHECK_CONTIG(ws); CHECK_GPU(tickets); CHECK_CONTIG(tickets);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && tickets.scalar_type() == at::kInt,
+              "sampler workspace fp32, tickets int32");
+  TORCH_CHECK(ws.numel() >= (int64_t)B * (64 * 8 + 4),
+              "sampler workspace too small (B x 64 chunk records + B row summaries)");
+  TORCH_CHECK(tickets.numel() >= B, "one ticket per row");
   const c10::DeviceGuard g(logits.device());
-  akap::launch_sample(p, B, cur_stream());
+  akap::launch_sample(p, B, ws.data_ptr(), tickets.data_ptr<int>(), cur_stream());
 }
 
 void apply_penalties(Tensor logits, Tensor rows, Tensor toks, Tensor counts, Tensor presence,
@@ -688,13 +722,18 @@ void kv_pull(int64_t src_ptr, int64_t src_plane_stride, Tensor dst_cache, Tensor
   a.dst_plane_stride = dst_cache.stride(0);
   a.planes = dst_cache.size(0);
   a.block_elems = dst_cache.size(2);
-  TORCH_CHECK(a.block_elems % 8 == 0 && a.block_elems == Hkv * BS * D, "block = Hkv*BS*D");
+  // bf16 cache: block = Hkv*BS*D; an fp8 (byte) cache is moved as bf16 pairs, block =
+  // Hkv*BS*D/2 -- the copy jobs are dtype-agnostic 16-byte moves; V tails exist only for bf16
+  const bool byte_cache = (int64_t)a.block_elems * 2 == Hkv * BS * D;
+  TORCH_CHECK(a.block_elems % 8 == 0 && (a.block_elems == Hkv * BS * D || byte_cache),
+              "block = Hkv*BS*D (bf16) or Hkv*BS*D/2 (fp8 bytes viewed as bf16)");
   TORCH_CHECK(src_plane_stride % a.block_elems == 0, "source plane stride");
   a.pairs = pairs.data_ptr<int>();
   a.nblk = pairs.numel() / 2;
   a.Hkv = Hkv; a.BS = BS; a.D = D;
   a.layers = a.planes / 2;
   if (tail && tail_jobs && tail_jobs->numel()) {
+    TORCH_CHECK(!byte_cache, "V-tail jobs need a bf16 cache");
     CHECK_CONTIG((*tail)); CHECK_BF16((*tail));
     TORCH_CHECK(tail->dim() == 5 && tail->size(0) == a.layers && tail->size(2) == Hkv &&
                 tail->size(3) == 8 && tail->size(4) == D, "tail [L, slots, Hkv, 8, D]");
@@ -866,11 +905,19 @@ void car_open(int64_t h, Tensor all_handles) {
   }
 }
 
+// The IPC kernels move 16-byte vectors (bf16x8 loads / stores on the user tensors).
+static void car_check_aligned(const Tensor& a, const Tensor& b) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+              "custom collective: tensors must be 16-byte aligned");
+}
+
 void car_all_reduce(int64_t h, Tensor inp, Tensor out, bool two_shot) {
   CarComm* c = car_get(h);
   CHECK_GPU(inp); CHECK_BF16(inp); CHECK_CONTIG(inp); CHECK_CONTIG(out); CHECK_BF16(out);
   TORCH_CHECK(inp.numel() == out.numel(), "size mismatch");
   TORCH_CHECK(inp.numel() % 8 == 0, "numel % 8");
+  car_check_aligned(inp, out);
   TORCH_CHECK((size_t)inp.numel() <= c->args.half_elems, "message larger than the buffer");
   for (int p = 0; p < c->args.world; ++p)
     TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
@@ -909,6 +956,8 @@ void car_all_reduce_resnorm(int64_t h, Tensor inp, Tensor residual, Tensor ln, T
   for (int p = 0; p < c->args.world; ++p)
     TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
   const akap::CarEpi e = car_epi_of(residual, ln, aout, ss, inp.numel());
+  car_check_aligned(inp, residual);
+  car_check_aligned(ln, aout);
   const c10::DeviceGuard g(inp.device());
   akap::launch_custom_allreduce(c->args, inp.data_ptr(), nullptr, inp.numel(),
                                 two_shot ? 1 : 0, cur_stream(), &e);
@@ -974,6 +1023,7 @@ void car_all_gather(int64_t h, Tensor inp, Tensor out) {
   const int64_t rows = inp.numel() / n;
   TORCH_CHECK(n % 8 == 0, "shard width % 8");
   TORCH_CHECK(out.numel() == inp.numel() * c->args.world, "out [R, W*n]");
+  car_check_aligned(inp, out);
   TORCH_CHECK((size_t)inp.numel() <= c->args.half_elems, "shard larger than the buffer");
   for (int p = 0; p < c->args.world; ++p)
     TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
@@ -992,6 +1042,7 @@ void car_all_to_all(int64_t h, Tensor inp, Tensor out) {
               "all-to-all: inp/out [world * seg] with seg % 8 == 0");
   TORCH_CHECK((size_t)inp.numel() <= c->args.half_elems, "message larger than the buffer");
   TORCH_CHECK(inp.data_ptr() != out.data_ptr(), "all-to-all is out of place");
+  car_check_aligned(inp, out);
   for (int p = 0; p < c->args.world; ++p)
     TORCH_CHECK(c->args.bufs[p] != nullptr, "peer buffers not opened (call car_open)");
   const c10::DeviceGuard g(inp.device());
@@ -1005,6 +1056,7 @@ void car_broadcast(int64_t h, Tensor buf, int64_t root) {
   CHECK_GPU(buf); CHECK_CONTIG(buf);
   const int64_t bytes = buf.numel() * buf.element_size();
   TORCH_CHECK(bytes % 16 == 0, "broadcast bytes % 16");
+  car_check_aligned(buf, buf);
   TORCH_CHECK((size_t)bytes <= c->args.half_elems * 2, "message larger than the buffer");
   TORCH_CHECK(root >= 0 && root < c->args.world, "root rank");
   for (int p = 0; p < c->args.world; ++p)
@@ -1108,7 +1160,7 @@ TORCH_LIBRARY(akap, m) {
   m.def(
       "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
       "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs, "
-      "bool greedy_logprobs=False) -> ()");
+      "bool greedy_logprobs, Tensor(c!) ws, Tensor(d!) tickets) -> ()");
   m.def(
       "apply_penalties(Tensor(a!) logits, Tensor rows, Tensor toks, Tensor counts, "
       "Tensor presence, Tensor frequency, Tensor repetition) -> ()");

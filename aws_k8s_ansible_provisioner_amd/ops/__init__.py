@@ -365,6 +365,9 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
     bm = 128 (with bn = 128): 128-row LDS-DMA tiles (weights cross L2 -> CU half as often at
     M = 256; the large-weight projections); bm = 256 (bn 64 | 128, 8 waves): the whole
     256-row batch per tile, every weight byte crosses L2 -> CU once.
+    bn = 256 (bm = 256) selects the 256 x 256 pgemm body with the K range split over
+    `splitk` workgroups per tile and the slices combined inside the launch by every slice
+    (csrc/kernels/pgemm.hip pgemm_sk_kernel; all epilogues, grid <= the CU count).
     km = 16 | 32 selects csrc/kernels/kgemm.hip instead: km x 32 output tiles with the K split
     over the workgroup's waves (plain prologue, store / residual epilogues, no split-K)."""
     M = x.shape[0]
@@ -401,7 +404,7 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
         n = (gdgemm_ws_floats(M, N, splitk, bn, bm) if bn else
              splitk * M * N + (splitk * M if pro == PRO_ADDNORM else 0))
         ws = torch.empty(n, dtype=torch.float32, device=x.device)
-        if inlaunch and bn:
+        if (inlaunch and bn) or bn == 256:  # bn 256: the combine is always in the launch
             counters = gemm_counters(x.device)
     else:
         ws = _EMPTY_F32.get(x.device)
@@ -415,6 +418,10 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
 def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI_STORE,
                     bn: int = 0, inlaunch: bool = False, bm: int = 64) -> bool:
     """Mirror of dgemm_supported / gdgemm_supported / dgemm_epi_supported (host-side)."""
+    if bn == 256:  # pgemm_sk: 256 x 256 tiles, any split, grid <= the CU count
+        if bm != 256 or N % 256 or K % 64 or not 1 <= splitk <= 32 or K // 64 < splitk:
+            return False
+        return -(-M // 256) * (N // 256) * splitk <= device_cus()
     if splitk not in (1, 2, 4, 8, 16):
         return False
     if bm != 64 and not (bm == 128 and bn == 128) and not (bm == 256 and bn in (64, 128)):
@@ -431,6 +438,23 @@ def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI
     if M <= 0 or N <= 0 or K <= 0 or N % 4 or pf not in (1, 2, 4, 8) or K % splitk:
         return False
     return (K // splitk) % (64 * pf) == 0
+
+
+_CUS: dict = {}
+
+
+def device_cus(device=None) -> int:
+    """Compute units of the (current) GPU; 256 (MI355X) without one."""
+    key = str(device)
+    if key not in _CUS:
+        n = 256
+        if torch.cuda.is_available():
+            try:
+                n = torch.cuda.get_device_properties(device or 0).multi_processor_count
+            except Exception:  # pragma: no cover - device query failure
+                pass
+        _CUS[key] = n
+    return _CUS[key]
 
 
 def kgemm_supported(M: int, N: int, K: int, km: int, epi: int = EPI_STORE, pro: int = 0) -> bool:
@@ -471,6 +495,27 @@ def gemm_splitk(M: int, N: int, K: int) -> int:
 
 
 # ----------------------------------------------------------------------------- sampling
+SAMPLE_MAX_CHUNKS = 64  # csrc/kernels/sampling.hip kMaxChunks
+_SAMPLE_WS: dict = {}
+_SAMPLE_OLD: list = []  # outgrown workspaces stay alive: captured hipGraphs address them
+
+
+def _sample_ws(device, B: int):
+    """Persistent sampler workspace per device: B x 64 chunk records of 32 B, B row summaries
+    (M, Z, key range) for the filter kernel, and B row tickets (zeroed once; each row's last
+    chunk re-arms its ticket in the kernel).  Grown, never
+    shrunk: a decode hipGraph keeps the addresses it was captured with."""
+    cur = _SAMPLE_WS.get(device)
+    if cur is None or cur[1].numel() < B:
+        if cur is not None:
+            _SAMPLE_OLD.append(cur)
+        n = max(B, 256)
+        cur = (torch.zeros(n * (SAMPLE_MAX_CHUNKS * 8 + 4), dtype=torch.float32, device=device),
+               torch.zeros(n, dtype=torch.int32, device=device))
+        _SAMPLE_WS[device] = cur
+    return cur
+
+
 def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out_logprobs=None,
            greedy_logprobs: bool = False):
     """greedy_logprobs: also return the log-prob of greedy (temperature 0) picks."""
@@ -480,8 +525,9 @@ def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out
     if out_logprobs is None:
         out_logprobs = torch.empty(B, dtype=torch.float32, device=logits.device)
     if _native(logits):
+        ws, tickets = _sample_ws(logits.device, B)
         torch.ops.akap.sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens,
-                              out_logprobs, greedy_logprobs)
+                              out_logprobs, greedy_logprobs, ws, tickets)
         return out_tokens, out_logprobs
     t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps, greedy_logprobs)
     out_tokens.copy_(t)

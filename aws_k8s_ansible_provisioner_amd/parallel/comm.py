@@ -34,9 +34,16 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
         # all-reduces stay on the device in max_bytes pieces of the IPC kernel instead of a
         # host-staged gloo all-reduce
         flat = x.view(-1)
-        step = st.car.max_bytes // x.element_size() // 8 * 8
+        cap = st.car.max_bytes // x.element_size() // 8 * 8
+        pieces = -(-flat.numel() // cap)
+        per = -(-flat.numel() // pieces)
+        step = (per + 7) // 8 * 8  # near-equal pieces, each 16-B aligned
         for i in range(0, flat.numel(), step):
             st.car.all_reduce(flat[i:i + step])
+        # a piece whose flag wait timed out only raises the kernel's error word: check it
+        # here (this eager rehearsal path can afford the sync) instead of summing on silently
+        if st.car.error():
+            raise RuntimeError("custom all-reduce timed out in a piecewise prefill all-reduce")
         return x
     dist.all_reduce(x, group=st.tp_group)
     return x

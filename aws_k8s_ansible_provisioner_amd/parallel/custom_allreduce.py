@@ -36,6 +36,11 @@ def oneshot_limit(world: int) -> int:
     return (512 << 10) if world <= 4 else (256 << 10)
 
 
+def _aligned(t: torch.Tensor) -> bool:
+    """The IPC kernels move 16-byte vectors of the user tensor (ops.cpp car_check_aligned)."""
+    return t.data_ptr() % 16 == 0
+
+
 class CustomAllReduce:
     def __init__(self, group=None, device: Optional[torch.device] = None,
                  max_bytes: int = DEFAULT_MAX_BYTES, buffer_bytes: int = 0):
@@ -64,7 +69,7 @@ class CustomAllReduce:
     def should_use(self, x: torch.Tensor) -> bool:
         nbytes = x.numel() * x.element_size()
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
-                and x.numel() % 8 == 0 and nbytes <= self.max_bytes)
+                and x.numel() % 8 == 0 and nbytes <= self.max_bytes and _aligned(x))
 
     def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         out = x if out is None else out
@@ -84,7 +89,7 @@ class CustomAllReduce:
         nbytes = x.numel() * x.element_size()
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
                 and x.numel() % 8 == 0 and nbytes <= self.buffer_bytes and x.dim() >= 1
-                and x.shape[-1] % 8 == 0)
+                and x.shape[-1] % 8 == 0 and _aligned(x))
 
     def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """x [R, n] (this rank's shard) -> out [R, world*n], rank-major column blocks."""
@@ -94,7 +99,8 @@ class CustomAllReduce:
     def a2a_ok(self, x: torch.Tensor) -> bool:
         nbytes = x.numel() * x.element_size()
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
-                and x.numel() % (8 * self.world) == 0 and nbytes <= self.buffer_bytes)
+                and x.numel() % (8 * self.world) == 0 and nbytes <= self.buffer_bytes
+                and _aligned(x))
 
     def all_to_all(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """Equal segments: x [world * seg] (segment d to rank d) -> out (segment p from rank p)."""
@@ -104,7 +110,7 @@ class CustomAllReduce:
     def bcast_ok(self, t: torch.Tensor) -> bool:
         nbytes = t.numel() * t.element_size()
         return (t.is_cuda and t.is_contiguous() and nbytes % 16 == 0
-                and nbytes <= self.buffer_bytes)
+                and nbytes <= self.buffer_bytes and _aligned(t))
 
     def broadcast(self, t: torch.Tensor, root: int) -> torch.Tensor:
         """In place: every rank's t becomes group rank `root`'s t."""

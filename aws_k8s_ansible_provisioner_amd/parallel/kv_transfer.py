@@ -62,6 +62,36 @@ class KVChannelBroken(RuntimeError):
     pass
 
 
+class KVIpcOpenTimeout(KVChannelBroken):
+    """hipIpcOpenMemHandle of a peer cache did not return in time (the caller falls back to
+    the p2p transport for that peer)."""
+
+
+IPC_OPEN_TIMEOUT_S = float(os.environ.get("AKAP_IPC_OPEN_TIMEOUT_S", "60"))
+
+
+def bounded_call(fn: Callable, timeout_s: float, what: str):
+    """Run fn() on a daemon thread and wait at most timeout_s: a driver call that never
+    returns (hipIpcOpenMemHandle of a large export on a shared device) leaves that thread
+    parked but never blocks the caller -- a server thread, a handshake -- forever."""
+    box: dict = {}
+
+    def run():
+        try:
+            box["v"] = fn()
+        except BaseException as e:  # surfaced to the caller
+            box["e"] = e
+
+    t = threading.Thread(target=run, name="kv-ipc-open", daemon=True)
+    t.start()
+    t.join(timeout_s)
+    if t.is_alive():
+        raise KVIpcOpenTimeout(f"{what} did not return within {timeout_s:.0f}s")
+    if "e" in box:
+        raise box["e"]
+    return box["v"]
+
+
 def _wait(work, timeout_s: float, what: str, gloo: bool) -> None:
     """Bounded wait on an async P2P op.  gloo: its send/recv work completes inside wait(),
     which takes the deadline itself.  RCCL: poll the op's completion event against the
@@ -85,10 +115,17 @@ def _wait(work, timeout_s: float, what: str, gloo: bool) -> None:
 
 
 class KVTransferAgent:
-    def __init__(self, kv_cache: torch.Tensor, group=None, timeout_s: float = DEFAULT_TIMEOUT_S):
+    def __init__(self, kv_cache: torch.Tensor, group=None, timeout_s: float = DEFAULT_TIMEOUT_S,
+                 pair=None):
         """kv_cache: the engine's [L, 2, NB, block_elems] cache tensor (bf16, or uint8 fp8
-        bytes -- moved as bf16 pairs: the copy kernels are dtype-agnostic 16-byte moves)."""
-        if kv_cache.dtype == torch.uint8:
+        bytes -- moved as bf16 pairs: the copy kernels are dtype-agnostic 16-byte moves).
+        pair: (ProcessGroup, backend name) of a two-rank channel between two independently
+        started servers (two-pod P/D, `connect_pair` / `PairHost`) -- used instead of a
+        group of the default torch.distributed world."""
+        # fp8: bytes moved as bf16 pairs; kv_pull takes the halved block (ops.cpp), and an fp8
+        # cache has no V tail
+        self.byte_cache = kv_cache.dtype == torch.uint8
+        if self.byte_cache:
             kv_cache = kv_cache.view(torch.bfloat16)
         self.kv = kv_cache
         L, two, NB, be = kv_cache.shape
@@ -111,9 +148,15 @@ class KVTransferAgent:
         self.resets = 0
         # gloo moves host tensors only: GPU caches on a gloo group (single-GPU rehearsal of
         # the P/D path) stage through pinned host memory
-        self.gloo = dist.is_initialized() and dist.get_backend(group) == "gloo"
+        self.pg = pair[0] if pair is not None else None
+        if pair is not None:
+            self.gloo = pair[1] == "gloo"
+        else:
+            self.gloo = dist.is_initialized() and dist.get_backend(group) == "gloo"
         self.host_staging = self.is_gpu and self.gloo
         self.peers: dict = {}  # hipIpc: peer key -> (mapped cache address, blocks, plane stride)
+        self.ipc_failed: dict = {}  # peer key -> why its mapping failed (-> p2p for that peer)
+        self.ipc_open_timeout_s = IPC_OPEN_TIMEOUT_S
         self.pull_seconds = 0.0
 
     def nbytes(self, nblk: int) -> int:
@@ -158,6 +201,16 @@ class KVTransferAgent:
             self.broken = str(e)
 
     # ---------------------------------------------------------------- ops
+    def _isend(self, buf: torch.Tensor, dst: int):
+        if self.pg is not None:
+            return self.pg.send([buf], dst, 0)
+        return dist.isend(buf, dst, group=self.group)
+
+    def _irecv(self, buf: torch.Tensor, src: int):
+        if self.pg is not None:
+            return self.pg.recv([buf], src, 0)
+        return dist.irecv(buf, src, group=self.group)
+
     def _ctx(self):
         return torch.cuda.stream(self.stream) if self.is_gpu else _Null()
 
@@ -179,7 +232,7 @@ class KVTransferAgent:
                         if self.is_gpu:
                             self.stream.synchronize()
                         buf = buf.cpu() if self.is_gpu else buf
-                    work = dist.isend(buf, dst, group=self.group)
+                    work = self._isend(buf, dst)
                     _wait(work, t_out, f"KV send of {len(block_ids)} blocks to rank {dst}",
                           self.gloo)
                     if self.is_gpu:
@@ -225,7 +278,7 @@ class KVTransferAgent:
                     if self.host_staging:
                         self.stream.synchronize()
                         b = buf.cpu()
-                    work = dist.isend(b, dst, group=self.group)
+                    work = self._isend(b, dst)
                     _wait(work, t_out, f"KV send of {buf.shape[1]} blocks to rank {dst}",
                           self.gloo)
                     if self.is_gpu:
@@ -257,11 +310,11 @@ class KVTransferAgent:
                                       dtype=self.kv.dtype, device=self.device)
                     if self.host_staging:
                         hb = torch.empty(buf.shape, dtype=buf.dtype)
-                        _wait(dist.irecv(hb, src, group=self.group), t_out,
+                        _wait(self._irecv(hb, src), t_out,
                               f"KV recv of {n} blocks from rank {src}", True)
                         buf.copy_(hb)
                     else:
-                        _wait(dist.irecv(buf, src, group=self.group), t_out,
+                        _wait(self._irecv(buf, src), t_out,
                               f"KV recv of {n} blocks from rank {src}", self.gloo)
                     ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
                     ops.kv_scatter(buf, self.planes, ids)
@@ -282,6 +335,8 @@ class KVTransferAgent:
         jobs).  Runs on the agent thread, after any queued transfer (which fails fast while
         broken).  Returns True if this call moved the channel to `generation`."""
 
+        if self.pg is not None:
+            raise RuntimeError("a pair channel is rebuilt by a new connect_pair (generation + 1)")
         if dist.get_world_size() != 2:
             # new_group() completes only when EVERY rank of the default group calls it with
             # this generation; only the 2-rank P/D pod guarantees that (both ends reset)
@@ -324,8 +379,19 @@ class KVTransferAgent:
             raise ValueError(f"peer cache geometry {meta['planes']}x{meta['block_elems']} != "
                              f"ours {P}x{be} (same model and block size required)")
         key = meta["blob"]
+        if key in self.ipc_failed:
+            raise KVIpcOpenTimeout(self.ipc_failed[key])
         if key not in self.peers:
-            ptr = ops.ipc_open(base64.b64decode(meta["blob"]), self.device.index)
+            blob = base64.b64decode(meta["blob"])
+            dev = self.device.index
+            try:
+                ptr = bounded_call(lambda: ops.ipc_open(blob, dev), self.ipc_open_timeout_s,
+                                   f"hipIpc mapping of a {meta['planes']}-plane peer cache")
+            except KVIpcOpenTimeout as e:
+                self.ipc_failed[key] = str(e)
+                print(f"[kv-transfer] {e}: this peer falls back to the p2p transport",
+                      flush=True)
+                raise
             self.peers[key] = (ptr, int(meta["nblocks"]), int(meta["plane_stride"]))
         return key
 
@@ -345,6 +411,8 @@ class KVTransferAgent:
                 raise ValueError("several peer caches mapped: name the peer")
             peer = next(iter(self.peers))
         ptr, nblocks, stride = self.peers[peer]
+        if self.byte_cache and tail_jobs:
+            raise ValueError("V-tail jobs with an fp8 KV cache (fp8 caches have no V tail)")
         t0 = time.perf_counter()
         with self._ctx():
             ops.kv_pull(ptr, stride, nblocks, self.planes, pairs, Hkv, BS, D, tail=tail,
@@ -374,3 +442,93 @@ class _Null:
 
     def __exit__(self, *a):
         return False
+
+
+# ------------------------------------------------------------------------------ two-pod P/D
+# Prefill and decode servers started independently (separate Deployments / pods, no shared
+# launcher or MASTER_ADDR) bootstrap a KV channel per (decode peer, generation) over HTTP:
+# the decode server POSTs /kv/hello {peer, generation} to the prefill server, which answers
+# with the port of its TCPStore and joins a fresh two-rank process group (prefill rank 0,
+# decode rank 1) under the prefix "<peer>/<generation>" while the decode server joins the same
+# group as a store client.  A broken channel is replaced by a hello at generation + 1.  The
+# hipIpc pull needs no channel at all (/kv/lease carries the export handle); this channel
+# carries the p2p transport (and the p2p fallback of a peer whose cache cannot be mapped).
+
+def pair_backend(kv: torch.Tensor) -> str:
+    """gloo on CPU caches (and AKAP_PD_PAIR_BACKEND=gloo: host-staged, works between pods that
+    see no common device), RCCL between GPU engines."""
+    env = os.environ.get("AKAP_PD_PAIR_BACKEND")
+    if env in ("gloo", "nccl"):
+        return env
+    return "nccl" if kv.is_cuda else "gloo"
+
+
+def _pair_group(store, prefix: str, rank: int, backend: str, timeout_s: float, device=None):
+    ps = dist.PrefixStore(prefix, store)
+    to = datetime.timedelta(seconds=timeout_s)
+    if backend == "gloo":
+        return dist.ProcessGroupGloo(ps, rank, 2, to)
+    opts = dist.ProcessGroupNCCL.Options()
+    opts._timeout = to
+    return dist.ProcessGroupNCCL(ps, rank, 2, opts)
+
+
+class PairHost:
+    """Prefill side of the two-pod bootstrap: a TCPStore server on `port` and the pair agents
+    formed so far (peer id -> KVTransferAgent)."""
+
+    def __init__(self, kv: torch.Tensor, port: int, timeout_s: float = DEFAULT_TIMEOUT_S):
+        self.kv = kv
+        self.timeout_s = timeout_s
+        self.store = dist.TCPStore("0.0.0.0", port, None, True,
+                                   datetime.timedelta(seconds=max(timeout_s, 60.0)),
+                                   wait_for_workers=False)
+        self.port = self.store.port
+        self.agents: dict = {}
+        self.errors: dict = {}
+        self.lock = threading.Lock()
+
+    def accept(self, peer: str, generation: int, backend: str) -> str:
+        """Join the pair group for (peer, generation) in the background; returns the prefix."""
+        prefix = f"akap-pair/{peer}/{int(generation)}"
+
+        def form():
+            try:
+                pg = _pair_group(self.store, prefix, 0, backend, self.timeout_s)
+                ag = KVTransferAgent(self.kv, timeout_s=self.timeout_s, pair=(pg, backend))
+                ag.generation = int(generation)
+                with self.lock:
+                    old = self.agents.get(peer)
+                    self.agents[peer] = ag
+                    self.errors.pop(peer, None)
+                if old is not None:
+                    old.close()
+            except Exception as e:  # the decode side times out and retries with a new hello
+                with self.lock:
+                    self.errors[peer] = repr(e)
+
+        threading.Thread(target=form, name=f"kv-pair-{peer}", daemon=True).start()
+        return prefix
+
+    def agent(self, peer: str, wait_s: float = 10.0) -> Optional["KVTransferAgent"]:
+        """The pair agent of `peer` (waits briefly: the decode side may return from the group
+        rendezvous a moment before this side registers it)."""
+        deadline = time.monotonic() + wait_s
+        while True:
+            with self.lock:
+                ag = self.agents.get(peer)
+            if ag is not None or time.monotonic() > deadline:
+                return ag
+            time.sleep(0.01)
+
+
+def connect_pair(kv: torch.Tensor, host: str, port: int, prefix: str, backend: str,
+                 timeout_s: float = DEFAULT_TIMEOUT_S) -> "KVTransferAgent":
+    """Decode side of the two-pod bootstrap: join the pair group the prefill server opened for
+    us (rank 1) and return an agent on it."""
+    store = dist.TCPStore(host, int(port), None, False,
+                          datetime.timedelta(seconds=max(timeout_s, 60.0)))
+    pg = _pair_group(store, prefix, 1, backend, timeout_s)
+    ag = KVTransferAgent(kv, timeout_s=timeout_s, pair=(pg, backend))
+    ag._store = store  # keep the client alive with the group
+    return ag

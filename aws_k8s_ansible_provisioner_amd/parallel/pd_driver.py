@@ -45,7 +45,7 @@ import torch
 import torch.distributed as dist
 
 from ..engine.config import SamplingParams
-from .kv_transfer import KVTransferAgent
+from .kv_transfer import KVIpcOpenTimeout, KVTransferAgent
 
 _END = -1
 _CHUNK, _FINAL = 0, 1
@@ -121,7 +121,22 @@ class PDPair:
             else:
                 meta = [None]
                 dist.recv_object_list(meta, self.peer, group=self.ctrl)
-                self.agent.connect_ipc(meta[0])
+            # a mapping that does not return in time (bounded: KVTransferAgent.connect_ipc)
+            # moves the WHOLE job to the p2p transport -- every rank must agree before the
+            # first hand-off, since the two transports pair differently
+            ok = 1
+            if not self.is_prefill:
+                try:
+                    self.agent.connect_ipc(meta[0])
+                except KVIpcOpenTimeout:
+                    ok = 0
+            flag = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.ctrl)
+            if not int(flag.item()):
+                if rank == 0:
+                    print("[pd] hipIpc mapping timed out on a decode rank: the job uses the "
+                          "p2p transport", flush=True)
+                self.transport = "p2p"
 
     # ------------------------------------------------------------------ prefill side
     def run_prefill(self, prompts: list[list[int]], params: SamplingParams,

@@ -237,22 +237,36 @@ class OpenAIServer:
             if grp is not None and self.ae.pd_group is not None and grp != self.ae.pd_group:
                 return _err(409, f"P/D group mismatch: decode {grp} vs prefill "
                                  f"{self.ae.pd_group}", "Conflict")
-            if getattr(self.ae.kv_agent, "broken", None) is not None:
-                # the decode side rebuilds the channel (/kv/reset) and retries later requests
-                return _err(503, f"KV channel broken: {self.ae.kv_agent.broken}",
-                            "KVChannelBroken")
+            agent = self.ae.kv_agent
+            if body.get("peer") is not None:  # two-pod bootstrap: this peer's pair channel
+                host = getattr(self.ae, "pair_host", None)
+                agent = host.agent(str(body["peer"])) if host is not None else None
+                if agent is None:
+                    return _err(409, f"no KV channel to peer {body['peer']} (POST /kv/hello)",
+                                "KVChannelBroken")
+            if getattr(agent, "broken", None) is not None:
+                # the decode side rebuilds the channel (/kv/reset, or a new /kv/hello) and
+                # retries later requests
+                return _err(503, f"KV channel broken: {agent.broken}", "KVChannelBroken")
             tids = [int(t) for t in (body.get("transfer_ids") or [body["transfer_id"]])]
-            per = [eng.held_blocks(t) for t in tids]
-            missing = [t for t, b in zip(tids, per) if not b]
-            if missing:
-                return _err(404, f"no held KV for transfer(s) {missing}")
-            # from here the blocks are owned by the send (not the TTL sweep, not /kv/release)
-            # until its completion frees them
-            per = [eng.take_held(t) for t in tids]
-            if any(not b for b in per):  # expired between the check and the take
-                for t in tids:
-                    eng.finish_transfer(t)
-                return _err(404, f"held KV for transfer(s) {tids} expired")
+            if body.get("leased_blocks") is not None:
+                # the decode side leased these transfers for a hipIpc pull and could not map
+                # this cache in time: the lease already owns the blocks (until finish_transfer)
+                per = [[int(b) for b in bl] for bl in body["leased_blocks"]]
+                if len(per) != len(tids):
+                    return _err(400, "leased_blocks: one block list per transfer id")
+            else:
+                per = [eng.held_blocks(t) for t in tids]
+                missing = [t for t, b in zip(tids, per) if not b]
+                if missing:
+                    return _err(404, f"no held KV for transfer(s) {missing}")
+                # from here the blocks are owned by the send (not the TTL sweep, not
+                # /kv/release) until its completion frees them
+                per = [eng.take_held(t) for t in tids]
+                if any(not b for b in per):  # expired between the check and the take
+                    for t in tids:
+                        eng.finish_transfer(t)
+                    return _err(404, f"held KV for transfer(s) {tids} expired")
             blocks = [b for bl in per for b in bl]
             fault = os.environ.get("AKAP_FAULT_KV_PUSH")
             if fault == "drop" or (fault == "drop_once" and not self._dropped_push):
@@ -268,9 +282,26 @@ class OpenAIServer:
                 for t in ts:
                     eng.finish_transfer(t)
 
-            self.ae.kv_agent.send_blocks(blocks, int(body["dst_rank"]), on_done=done)
+            agent.send_blocks(blocks, int(body["dst_rank"]), on_done=done)
             nb = [len(b) for b in per]
             return {"ok": True, "num_blocks": nb if "transfer_ids" in body else nb[0]}
+
+        @app.post("/kv/hello")
+        async def kv_hello(req: Request):
+            """Two-pod P/D (prefill side): open a two-rank KV channel for a decode server
+            started on its own -- returns the TCPStore port and the group prefix it joins as
+            rank 1 while this server joins as rank 0 (in the background)."""
+            body = await req.json()
+            host = getattr(self.ae, "pair_host", None)
+            if host is None:
+                return _err(400, "not a two-pod (--pd-bootstrap http) prefill server")
+            grp = body.get("group")
+            if grp is not None and grp != self.ae.pd_group:
+                return _err(409, f"P/D group mismatch: decode {grp} vs prefill "
+                                 f"{self.ae.pd_group}", "Conflict")
+            prefix = host.accept(str(body["peer"]), int(body.get("generation", 0)),
+                                 str(body.get("backend", "gloo")))
+            return {"ok": True, "store_port": host.port, "prefix": prefix}
 
         @app.post("/kv/lease")
         async def kv_lease(req: Request):
@@ -568,6 +599,16 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--load-format", default="random", choices=["random", "safetensors"])
     ap.add_argument("--weights-path", default=None)
     ap.add_argument("--kv-role", default="both", choices=["both", "prefill", "decode"])
+    ap.add_argument("--pd-bootstrap", default=os.environ.get("AKAP_PD_BOOTSTRAP", "launcher"),
+                    choices=["launcher", "http"],
+                    help="P/D roles: launcher = every prefill/decode rank of one torch.distributed "
+                         "job (server/pd_launch.py, one pod); http = independently started "
+                         "servers (separate prefill / decode Deployments): the decode server "
+                         "bootstraps a KV channel per prefill peer over HTTP (/kv/hello -> "
+                         "the prefill server's TCPStore), the hipIpc pull needs none")
+    ap.add_argument("--kv-store-port", type=int,
+                    default=int(os.environ.get("AKAP_KV_STORE_PORT", "29710")),
+                    help="--pd-bootstrap http, prefill role: TCPStore port of the pair channels")
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8", "fp8_e4m3"],
                     help="fp8: OCP e4m3 KV cache (half the bytes; decode attention streams "
                          "half as much)")
@@ -631,7 +672,8 @@ def make_telemetry(a, labels: dict) -> list:
     return out
 
 
-def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:
+def build_app(ecfg: EngineConfig, engine=None, pd_bootstrap: str = "launcher",
+              kv_store_port: int = 29710) -> tuple[FastAPI, AsyncEngine]:
     from ..engine.llm_engine import LLMEngine
 
     eng = engine or LLMEngine(ecfg)
@@ -640,7 +682,19 @@ def build_app(ecfg: EngineConfig, engine=None) -> tuple[FastAPI, AsyncEngine]:
         from ..parallel.kv_transfer import KVTransferAgent
 
         ae.kv_agent = KVTransferAgent(eng.runner.kv)
-        ae.pd_group = eng.pd_group = pd_group_id()
+        ae.pd_bootstrap = pd_bootstrap
+        if pd_bootstrap == "http":
+            # two-pod P/D: no shared job; every prefill/decode pair is its own two-rank channel
+            # (prefill rank 0, decode rank 1), formed on demand; servers of one deployment
+            # share AKAP_PD_GROUP (the gateway pairs only inside it)
+            ae.pd_group = eng.pd_group = os.environ.get("AKAP_PD_GROUP", "http")
+            eng.rank = 0 if ecfg.kv_role == "prefill" else 1
+            if ecfg.kv_role == "prefill":
+                from ..parallel.kv_transfer import PairHost
+
+                ae.pair_host = PairHost(eng.runner.kv, kv_store_port)
+        else:
+            ae.pd_group = eng.pd_group = pd_group_id()
         eng.kv_agent = ae.kv_agent
     srv = OpenAIServer(ae, eng.model_name, ecfg.chat_template, ecfg.max_model_len)
     return srv.app, ae
@@ -658,13 +712,13 @@ def main(argv: Optional[list] = None) -> None:
 
         serve_tp(ecfg, a.host, a.port, telemetry=lambda labels: make_telemetry(a, labels))
         return
-    if a.kv_role != "both":
+    if a.kv_role != "both" and a.pd_bootstrap == "launcher":
         # P/D: this process is one rank of the prefill/decode KV-transfer group (torchrun)
         from ..parallel.state import init_distributed
 
         backend = os.environ.get("AKAP_DIST_BACKEND") or ("gloo" if a.device == "cpu" else None)
         init_distributed(tp_size=1, backend=backend)
-    app, ae = build_app(ecfg)
+    app, ae = build_app(ecfg, pd_bootstrap=a.pd_bootstrap, kv_store_port=a.kv_store_port)
     ae.telemetry = make_telemetry(a, {})
     uvicorn.run(app, host=a.host, port=a.port, log_level="info", access_log=False)
 

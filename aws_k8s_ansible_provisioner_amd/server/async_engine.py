@@ -20,6 +20,7 @@ from typing import AsyncIterator, Optional
 
 from ..engine.config import SamplingParams
 from ..engine.llm_engine import LLMEngine, RequestOutput
+from ..parallel.kv_transfer import KVIpcOpenTimeout
 
 
 class EngineDeadError(RuntimeError):
@@ -57,6 +58,7 @@ class KVPuller:
         self.ae = ae
         self.q: "queue.Queue[PullJob]" = queue.Queue()
         self.batches = 0
+        self.ipc_fallback: set = set()  # prefill URLs whose cache could not be mapped
         self._thread = threading.Thread(target=self._run, name="kv-puller", daemon=True)
         self._thread.start()
 
@@ -107,12 +109,32 @@ class KVPuller:
                 self._resolve(j, e)
         if not ready:
             return
-        if self.transport() == "ipc":
-            self._pull_batch_ipc(url, ready, reserved)
-            return
+        leased = None
+        if self.transport() == "ipc" and url not in self.ipc_fallback:
+            leased = self._pull_batch_ipc(url, ready, reserved)
+            if leased is True:
+                return
+            # the peer cache could not be mapped in time: this and every later batch from
+            # this prefill server move over the process group instead (the leased blocks of
+            # this batch are pushed as they are)
+            self.ipc_fallback.add(url)
+        self._pull_batch_p2p(url, rank, ready, reserved, leased)
+
+    def _pull_batch_p2p(self, url: str, rank: int, ready: list, reserved: list,
+                        leased: Optional[list] = None) -> None:
+        eng = self.ae.engine
+        agent = self.ae.kv_agent
         try:
-            body = json.dumps({"transfer_ids": [int(j.kvp["transfer_id"]) for j in ready],
-                               "dst_rank": eng.rank, "group": self.ae.pd_group}).encode()
+            msg = {"transfer_ids": [int(j.kvp["transfer_id"]) for j in ready],
+                   "dst_rank": eng.rank, "group": self.ae.pd_group}
+            if self.ae.pd_bootstrap == "http":
+                # two-pod P/D: this prefill server's own pair channel (we are its rank 1)
+                agent = self.ae.pair_agent(url)
+                msg["peer"] = self.ae.peer_id()
+                msg["dst_rank"], rank = 1, 0
+            if leased is not None:
+                msg["leased_blocks"] = leased
+            body = json.dumps(msg).encode()
             req = urllib.request.Request(url.rstrip("/") + "/kv/push", data=body,
                                          headers={"Content-Type": "application/json"})
             with urllib.request.urlopen(req, timeout=60) as r:
@@ -122,13 +144,19 @@ class KVPuller:
                 raise RuntimeError(f"KV block count mismatch {counts} vs "
                                    f"{[len(b) for _, b in reserved]}")
             all_blocks = [b for _, bl in reserved for b in bl]
-            self.ae.kv_agent.recv_blocks(all_blocks, rank)
+            agent.recv_blocks(all_blocks, rank)
         except Exception as e:
             for j, (iid, _) in zip(ready, reserved):
                 eng.abort_request(j.req_id)  # frees the reserved decode blocks
                 AsyncEngine._release_remote(j.kvp)
                 self._resolve(j, e)
-            agent = self.ae.kv_agent
+            if self.ae.pd_bootstrap == "http":
+                # a pair channel is not reset in place: the next batch forms a new one
+                with self.ae._pair_lock:
+                    ag = self.ae.pair_agents.pop(url, None)
+                if ag is not None:
+                    ag.close()
+                return
             if (getattr(agent, "broken", None) is not None or
                     "KVChannelBroken" in _http_error_text(e)):
                 # a timed-out transfer left stale ops in the channel (ours or the prefill
@@ -150,10 +178,13 @@ class KVPuller:
             return env
         return "ipc" if getattr(self.ae.kv_agent, "is_gpu", False) else "p2p"
 
-    def _pull_batch_ipc(self, url: str, ready: list, reserved: list) -> None:
+    def _pull_batch_ipc(self, url: str, ready: list, reserved: list):
         """hipIpc transport: lease the transfers' blocks (POST /kv/lease), map the prefill
         cache on first use, ONE kv_pull launch moves every request's blocks and fills their V
-        tails, then release the lease (POST /kv/done) -- also on failure."""
+        tails, then release the lease (POST /kv/done) -- also on failure.  Returns True when
+        the batch is resolved; when the peer cache could not be mapped within
+        AKAP_IPC_OPEN_TIMEOUT_S it returns the leased prefill block lists (nothing resolved,
+        the decode blocks still reserved): the caller pushes them over the p2p transport."""
         eng = self.ae.engine
         agent = self.ae.kv_agent
         runner = eng.runner
@@ -186,6 +217,9 @@ class KVPuller:
                         tails.append((sb[g0 // bs], (g0 % bs) // 8, n % 8, slot))
             agent.pull(pairs, runner.model.hkv, bs, runner.model.D,
                        tail=getattr(runner, "_tail", None), tail_jobs=tails, peer=peer)
+        except KVIpcOpenTimeout as e:
+            print(f"[pd] {e}: KV from {url} moves over the p2p transport", flush=True)
+            return src
         except Exception as e:
             for j, (iid, _) in zip(ready, reserved):
                 eng.abort_request(j.req_id)  # frees the reserved decode blocks
@@ -197,7 +231,7 @@ class KVPuller:
                     post("/kv/done", {"transfer_ids": tids})
                 except Exception as e2:  # the prefill side's TTL cannot free leased blocks
                     print(f"[pd] /kv/done to {url} failed: {e2}", flush=True)
-            return
+            return True
         try:
             post("/kv/done", {"transfer_ids": tids})
         except Exception as e:
@@ -207,6 +241,7 @@ class KVPuller:
             eng.activate(iid, tail_filled=True)
             self._resolve(j, None)
         self.ae._wake.set()
+        return True
 
 
 def _http_error_text(e: BaseException) -> str:
@@ -228,6 +263,11 @@ class AsyncEngine:
         self.step_hook = step_hook
         self.kv_agent = None  # parallel.kv_transfer.KVTransferAgent for P/D roles
         self.pd_group: Optional[str] = None  # P/D: id of this engine's RCCL transfer group
+        self.pd_bootstrap = "launcher"  # "http": two-pod P/D, pair channels on demand
+        self.pair_host = None           # prefill (http): kv_transfer.PairHost
+        self.pair_agents: dict = {}     # decode (http): prefill URL -> pair KVTransferAgent
+        self._pair_gen = 0
+        self._pair_lock = threading.Lock()
         self.puller: Optional["KVPuller"] = None
         self._thread = threading.Thread(target=self._run, name="engine-loop", daemon=True)
         self.started = time.time()
@@ -341,6 +381,42 @@ class AsyncEngine:
             self.queues[req_id].put_nowait(RequestOutput(req_id, prompt_ids, [first], [first],
                                                          t, t, False, None))
         return None
+
+    def peer_id(self) -> str:
+        import socket
+
+        return f"{socket.gethostname()}-{os.getpid()}"
+
+    def pair_agent(self, url: str, timeout_s: float = 120.0):
+        """Two-pod P/D (decode side): the KV channel to the prefill server at `url`, formed on
+        first use by POST /kv/hello and a two-rank group rendezvous at the prefill server's
+        TCPStore (the URL's host); a broken one is dropped and re-formed at a new generation."""
+        from urllib.parse import urlparse
+
+        from ..parallel.kv_transfer import connect_pair, pair_backend
+
+        with self._pair_lock:
+            ag = self.pair_agents.get(url)
+            if ag is not None and ag.broken is None:
+                return ag
+            if ag is not None:
+                ag.close()
+                self.pair_agents.pop(url, None)
+            self._pair_gen += 1
+            gen = self._pair_gen
+            backend = pair_backend(self.kv_agent.kv)
+            body = json.dumps({"peer": self.peer_id(), "generation": gen, "backend": backend,
+                               "group": self.pd_group}).encode()
+            req = urllib.request.Request(url.rstrip("/") + "/kv/hello", data=body,
+                                         headers={"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=30) as r:
+                meta = json.loads(r.read())
+            ag = connect_pair(self.kv_agent.kv, urlparse(url).hostname, meta["store_port"],
+                              meta["prefix"], backend, timeout_s=timeout_s)
+            ag.generation = gen
+            self.pair_agents[url] = ag
+            print(f"[pd] KV channel to {url} formed (generation {gen}, {backend})", flush=True)
+            return ag
 
     def rebuild_channel(self, url: str, timeout_s: float = 120.0) -> bool:
         """Decode side: move both ends of the KV channel to a fresh process group (the next

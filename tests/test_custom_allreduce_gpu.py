@@ -331,7 +331,7 @@ def test_custom_allgather_broadcast_alltoall_ipc_processes(world):
             assert np.array_equal(a2a, torch.tensor(exp).float().bfloat16().float().numpy()), (r, it)
 
 
-def _kv_pull_worker(rank, port, q, geo):
+def _kv_pull_worker(rank, port, q, geo, fp8=False):
     """Rank 0 = prefill: a KV cache with a known pattern, exported by hipIpc.  Rank 1 =
     decode: maps it and pulls blocks + V tails with ONE kv_pull launch."""
     import base64
@@ -345,9 +345,15 @@ def _kv_pull_worker(rank, port, q, geo):
                                 world_size=2)
         L, Hkv, BS, D, NB0, NB1 = geo
         be = Hkv * BS * D
+        if fp8:  # e4m3 cache bytes, moved as bf16 pairs (no V tail)
+            be //= 2
         if rank == 0:
             g = torch.Generator().manual_seed(5)
-            kv = torch.randn(L, 2, NB0, be, generator=g).to(torch.bfloat16).to(DEV)
+            if fp8:
+                kv = torch.randint(0, 256, (L, 2, NB0, 2 * be), generator=g,
+                                   dtype=torch.uint8).to(DEV).view(torch.bfloat16)
+            else:
+                kv = torch.randn(L, 2, NB0, be, generator=g).to(torch.bfloat16).to(DEV)
             planes = kv.view(2 * L, NB0, be)
             meta = [ops.ipc_export(planes), planes.stride(0)]
             dist.broadcast_object_list(meta, src=0)
@@ -361,10 +367,11 @@ def _kv_pull_worker(rank, port, q, geo):
             tail = torch.zeros(L, 6, Hkv, 8, D, dtype=torch.bfloat16, device=DEV)
             ptr = ops.ipc_open(meta[0], 0)
             pairs = [(3, 0), (NB0 - 1, 5), (0, NB1 - 1)]
-            jobs = [(7, 1, 5, 2), (NB0 - 1, BS // 8 - 1, 3, 5)]
+            jobs = [] if fp8 else [(7, 1, 5, 2), (NB0 - 1, BS // 8 - 1, 3, 5)]
             ops.kv_pull(ptr, meta[1], NB0, planes, pairs, Hkv, BS, D, tail=tail, tail_jobs=jobs)
             torch.cuda.synchronize()
-            res = (kv.float().cpu().numpy(), tail.float().cpu().numpy())
+            res = ((kv.view(torch.uint8) if fp8 else kv.float()).cpu().numpy(),
+                   tail.float().cpu().numpy())
             ops.ipc_close(ptr)
             dist.barrier()
             q.put((1, 0, res))
@@ -374,10 +381,12 @@ def _kv_pull_worker(rank, port, q, geo):
         q.put((rank, repr(e) + traceback.format_exc(), None))
 
 
-def test_kv_pull_ipc_two_processes():
+@pytest.mark.parametrize("fp8", [False, True])
+def test_kv_pull_ipc_two_processes(fp8):
     """P/D hipIpc transport: the decode process maps the prefill process's cache and one
     kv_pull launch copies whole blocks (every plane) into its own block ids and writes the
-    requests' partial last V groups token-major into their tails -- exact, vs host indexing."""
+    requests' partial last V groups token-major into their tails -- exact, vs host indexing.
+    fp8: an e4m3 (byte) cache, moved as bf16 pairs, blocks only."""
     import numpy as np
     import torch.multiprocessing as mp
     geo = (3, 2, 32, 128, 12, 9)  # L, Hkv, BS, D, prefill blocks, decode blocks
@@ -385,7 +394,8 @@ def test_kv_pull_ipc_two_processes():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_kv_pull_worker, args=(r, port, q, geo)) for r in range(2)]
+    procs = [ctx.Process(target=_kv_pull_worker, args=(r, port, q, geo, fp8))
+             for r in range(2)]
     for p in procs:
         p.start()
     out = {}
@@ -397,6 +407,14 @@ def test_kv_pull_ipc_two_processes():
     assert out[0][0] == 0 and out[1][0] == 0, (out[0][0], out[1][0])
     kv, tail = out[1][1]
     be = Hkv * BS * D
+    if fp8:
+        src = torch.randint(0, 256, (L, 2, NB0, be), generator=torch.Generator().manual_seed(5),
+                            dtype=torch.uint8).numpy()
+        want = np.zeros((L, 2, NB1, be), np.uint8)
+        for s, d in [(3, 0), (NB0 - 1, 5), (0, NB1 - 1)]:
+            want[:, :, d] = src[:, :, s]
+        assert np.array_equal(kv, want)
+        return
     src = torch.randn(L, 2, NB0, be, generator=torch.Generator().manual_seed(5)) \
         .to(torch.bfloat16).float().numpy()
     want = np.zeros((L, 2, NB1, be), np.float32)
@@ -408,3 +426,95 @@ def test_kv_pull_ipc_two_processes():
         v = src[:, 1, s].reshape(L, Hkv, BS // 8, D, 8)[:, :, grp]   # [L, Hkv, D, 8]
         tw[:, slot, :, :cnt] = v[..., :cnt].transpose(0, 1, 3, 2)
     assert np.array_equal(tail, tw)
+
+
+def _mixed_stress_worker(rank, world, port, q, iters):
+    """Back-to-back all-reduces of three sizes (one-shot, two-shot), all-to-alls, broadcasts
+    and all-gathers on one communicator with NO host synchronisation between them: every
+    launch runs the full grid, so each block's epoch counts every launch and no region is
+    restaged while a peer block still reads it (a 1-block launch followed by a
+    many-block one of another kind).  Integer-valued inputs make every sum exact."""
+    import torch.distributed as dist
+
+    from aws_k8s_ansible_provisioner_amd.parallel.custom_allreduce import CustomAllReduce
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        car = CustomAllReduce(group=None, device=torch.device("cuda", 0), max_bytes=1 << 20)
+        keep = []
+        for it in range(iters):
+            g = torch.Generator().manual_seed(1000 * it + rank)
+            for n in (64, 20000, 300000):  # ~1 block, many blocks, two-shot when world > 2
+                x = torch.randint(-8, 9, (n,), generator=g).to(torch.bfloat16).to(DEV)
+                keep.append(car.all_reduce(x).clone())
+            seg = 8 * (1 + it % 5)
+            send = torch.randint(-8, 9, (world * seg,), generator=g).to(torch.bfloat16).to(DEV)
+            recv = torch.empty_like(send)
+            keep.append(car.all_to_all(send, recv).clone())
+            b = torch.randint(0, 255, (16 * (1 + it % 7),), generator=g).to(torch.uint8).to(DEV)
+            keep.append(car.broadcast(b, it % world).clone())
+            shard = torch.randint(-8, 9, (3, 40), generator=g).to(torch.bfloat16).to(DEV)
+            out = torch.empty(3, 40 * world, dtype=torch.bfloat16, device=DEV)
+            keep.append(car.all_gather(shard, out).clone())
+        torch.cuda.synchronize()
+        err = car.error()
+        res = [k.float().cpu().numpy() for k in keep]
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+        q.put((rank, err, res))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_custom_collectives_mixed_sequence_no_sync(world):
+    import numpy as np
+    import torch.multiprocessing as mp
+    iters = 12
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mixed_stress_worker, args=(r, world, port, q, iters))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, err, res = q.get(timeout=240)
+        out[rank] = (err, res)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert out[r][0] == 0, out[r][0]
+    # replay every rank's generator on the host
+    gens = [torch.Generator().manual_seed(0) for _ in range(world)]
+    k = 0
+    for it in range(iters):
+        for r in range(world):
+            gens[r].manual_seed(1000 * it + r)
+        for n in (64, 20000, 300000):
+            xs = [torch.randint(-8, 9, (n,), generator=gens[r]).float() for r in range(world)]
+            want = sum(xs).numpy()
+            for r in range(world):
+                assert np.array_equal(out[r][1][k], want), ("all_reduce", it, n, r)
+            k += 1
+        seg = 8 * (1 + it % 5)
+        sends = [torch.randint(-8, 9, (world * seg,), generator=gens[r]).float().numpy()
+                 for r in range(world)]
+        for r in range(world):
+            want = np.concatenate([sends[p][r * seg:(r + 1) * seg] for p in range(world)])
+            assert np.array_equal(out[r][1][k], want), ("all_to_all", it, r)
+        k += 1
+        bs = [torch.randint(0, 255, (16 * (1 + it % 7),), generator=gens[r]).numpy()
+              for r in range(world)]
+        for r in range(world):
+            assert np.array_equal(out[r][1][k], bs[it % world].astype(np.float32)), ("bcast", it)
+        k += 1
+        shards = [torch.randint(-8, 9, (3, 40), generator=gens[r]).float().numpy()
+                  for r in range(world)]
+        for r in range(world):
+            assert np.array_equal(out[r][1][k], np.concatenate(shards, axis=1)), ("gather", it)
+        k += 1

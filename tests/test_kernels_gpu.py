@@ -716,6 +716,49 @@ def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
         _close(out, want, atol=2e-2 * want.abs().max().item())
 
 
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K,splitk", [(256, 1024, 1024, 1), (256, 1024, 2048, 4),
+                                          (200, 2048, 1024, 3), (256, 4096, 4096, 16),
+                                          (37, 512, 14336, 16), (256, 6144, 4096, 10),
+                                          (300, 1024, 1024, 2), (1, 768, 640, 5)])
+def test_pgemm_split_k_inlaunch(epi, M, N, K, splitk):
+    """The 256 x 256 pgemm body with K split over workgroups and the slices combined in the
+    launch by every slice (dgemm bn=256, pgemm_sk_kernel): each epilogue with the ss_in row
+    scale vs fp32 references, uneven K splits (3, 5, 10), row tails, two row tiles, and a
+    second launch that reuses the re-armed tile counters."""
+    if not ops.dgemm_supported(M, N, K, splitk, 1, epi, bn=256, inlaunch=True, bm=256):
+        pytest.skip("unsupported combination")
+    kw = dict(splitk=splitk, bn=256, bm=256, inlaunch=True)
+    torch.manual_seed(M + N + K + epi + splitk)
+    eps = 1e-6
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    ssi = torch.rand(M, device=DEV) * K + 1.0
+    y = (x.float() @ w.float().t()) * torch.rsqrt(ssi / K + eps)[:, None]
+    if epi == ops.EPI_STORE:
+        out = ops.dgemm(x, w, ss_in=ssi, eps=eps, **kw)
+        _close(out, y, atol=2e-2 * y.abs().max().item())
+        out2 = ops.dgemm(x, w, ss_in=ssi, eps=eps, **kw)
+        assert torch.equal(out, out2)
+    elif epi == ops.EPI_RESNORM:
+        res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        res0 = res.clone()
+        ln = torch.rand(N, device=DEV, dtype=torch.bfloat16) + 0.5
+        ss = torch.zeros(M, device=DEV)
+        a = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.dgemm(x, w, out=res, epi=epi, ss_out=ss, a_out=a, ln_out=ln, ss_in=ssi, eps=eps,
+                  **kw)
+        want = y.to(torch.bfloat16).float() + res0.float()
+        _close(res, want, atol=2e-2 * want.abs().max().item())
+        _close(a, res.float() * ln.float(), atol=1e-2 * a.float().abs().max().item())
+        assert torch.allclose(ss, res.float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
+    else:
+        out = ops.dgemm(x, w, epi=epi, ss_in=ssi, eps=eps, **kw)
+        want = ref.silu_and_mul(y.to(torch.bfloat16)).float()
+        _close(out, want, atol=2e-2 * want.abs().max().item())
+    assert int(ops.gemm_counters(torch.device(DEV))[65535].item()) == 0  # no combine timed out
+
+
 @pytest.mark.parametrize("M", [1, 16, 37, 64, 100, 128, 200, 256, 300])
 @pytest.mark.parametrize("N,K", [(1000, 64), (4100, 1024), (2056, 2048)])
 def test_wide_row_gemm(M, N, K):

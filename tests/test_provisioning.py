@@ -160,11 +160,18 @@ def test_manifests_render(preset):
             assert args[args.index("--pmc-interval") + 1] == "5"
             env = {x["name"]: x.get("value") for x in c["env"]}
             assert env["ROCP_TOOL_LIBRARIES"].endswith("/libakap_pmc.so")
+            # the GEMM plan cache lives on the model PVC, one file per
+            # Deployment (per rank under TP / P/D: the runner appends .rankN), so a restarted
+            # pod loads its tuned plan instead of re-timing every candidate
+            cache = env["AKAP_GEMM_TUNE_CACHE"]
+            assert cache.startswith("/models/") and d["metadata"]["name"] in cache
+            assert any(m["mountPath"] == "/models" for m in c["volumeMounts"])
             assert "kernel-profiler" not in {x["name"] for x in pod["spec"]["containers"]}
             assert "akap.rocprof/port" not in pod["metadata"]["annotations"]
         else:
             assert "limits" not in c["resources"]
             assert "akap.rocprof/port" not in pod["metadata"]["annotations"]
+            assert "AKAP_GEMM_TUNE_CACHE" not in {x["name"] for x in c["env"]}
     if preset == "tp8":
         assert "--nproc-per-node=8" in engines[0]["spec"]["template"]["spec"]["containers"][0]["command"]
     if preset == "pd":
