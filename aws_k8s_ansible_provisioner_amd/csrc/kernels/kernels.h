@@ -224,10 +224,11 @@ void launch_kv_scatter(const void* in, void* cache, long plane_stride, int plane
 // hipIpc pull: peer cache blocks -> own blocks, + V-tail fill of each request's partial
 // last V group (see kv_transfer.hip)
 struct KVPullArgs {
-  const __bf16* src;      // peer (IPC-mapped) or own cache base: [planes, NB_src, block_elems]
-  long src_plane_stride;  // elements
-  __bf16* dst;            // own cache base [planes, NB, block_elems]
-  long dst_plane_stride;
+  // per-plane base addresses (device int64 tables [planes]): plane p of the source (a peer's
+  // IPC-mapped cache, or this engine's own) and of this engine's cache; a cache may be several
+  // allocations (layer-range segments), so planes are addressed through tables, not a stride
+  const int64_t* src_planes;  // -> [NB_src, block_elems] bf16 each
+  const int64_t* dst_planes;  // -> [NB, block_elems] bf16 each
   int planes, block_elems;
   const int* pairs;       // [nblk, 2]: (src block, dst block)
   int nblk;

@@ -59,8 +59,8 @@ __device__ __forceinline__ u32x4 pull_ld(__amdgpu_buffer_rsrc_t r, int byte_off)
 }
 
 // grid.x = nblk * planes copy jobs (then ntail * layers tail jobs).  Copy job j: plane
-// j % planes, block pair j / planes -> block_elems bf16 from src[plane][pairs[2b]] to
-// dst[plane][pairs[2b+1]].  Tail job: (src block, group, count, slot) x layer l: V-cache
+// j % planes, block pair j / planes -> block_elems bf16 from src_planes[plane][pairs[2b]] to
+// dst_planes[plane][pairs[2b+1]].  Tail job: (src block, group, count, slot) x layer l: V-cache
 // group [Hkv][D][8] of plane 2l+1 -> tail[l][slot][Hkv][8][D], first `count` tokens.
 __global__ __launch_bounds__(256) void kv_pull_kernel(KVPullArgs a) {
   const int job = blockIdx.x;
@@ -68,8 +68,8 @@ __global__ __launch_bounds__(256) void kv_pull_kernel(KVPullArgs a) {
   if (job < ncopy) {
     const int plane = job % a.planes, b = job / a.planes;
     const long sb = a.pairs[2 * b], db = a.pairs[2 * b + 1];
-    const bf16* src = a.src + (long)plane * a.src_plane_stride + sb * a.block_elems;
-    bf16* dst = a.dst + (long)plane * a.dst_plane_stride + db * a.block_elems;
+    const bf16* src = reinterpret_cast<const bf16*>(a.src_planes[plane]) + sb * a.block_elems;
+    bf16* dst = reinterpret_cast<bf16*>(a.dst_planes[plane]) + db * a.block_elems;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16*>(src), (short)0, a.block_elems * 2, 0x00020000);
     const int nv = a.block_elems / 8;  // 16-byte vectors
@@ -90,7 +90,8 @@ __global__ __launch_bounds__(256) void kv_pull_kernel(KVPullArgs a) {
   const int cnt = a.tail_jobs[4 * q + 2], slot = a.tail_jobs[4 * q + 3];
   const int D = a.D;
   // V plane 2l+1, block sblk: [Hkv][BS/8][D][8]; this group's [Hkv][D][8] rows
-  const bf16* vb = a.src + (long)(2 * l + 1) * a.src_plane_stride + (long)sblk * a.block_elems;
+  const bf16* vb = reinterpret_cast<const bf16*>(a.src_planes[2 * l + 1]) +
+                   (long)sblk * a.block_elems;
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16*>(vb), (short)0, a.block_elems * 2, 0x00020000);
   bf16* tl = a.tail + ((long)l * a.tail_slots + slot) * a.Hkv * 8 * D;

@@ -701,33 +701,32 @@ void kv_scatter(Tensor buf, Tensor cache, Tensor block_ids) {
                           cur_stream());
 }
 
-// hipIpc KV pull (see kv_transfer.hip).  src_ptr: the peer cache base as mapped by ipc_open
-// (or this engine's own cache for a tail-only fill); dst_cache [planes, NB, block_elems].
-// Index ranges are validated by the caller (parallel/kv_transfer.py) before upload: the
-// kernel trusts pairs / tail_jobs.
-void kv_pull(int64_t src_ptr, int64_t src_plane_stride, Tensor dst_cache, Tensor pairs,
+// hipIpc KV pull (see kv_transfer.hip).  src_planes / dst_planes: int64 device tables of
+// per-plane base addresses (a peer's planes as mapped by ipc_open -- or this engine's own for a
+// tail-only fill -- and this engine's planes); every plane is [NB, block_elems] bf16 (an fp8
+// cache moves as bf16 pairs).  Index ranges are validated by the caller
+// (ops.kv_pull) before upload: the kernel trusts pairs / tail_jobs.
+void kv_pull(Tensor src_planes, Tensor dst_planes, int64_t block_elems, Tensor pairs,
              std::optional<Tensor> tail, std::optional<Tensor> tail_jobs, int64_t Hkv,
              int64_t BS, int64_t D) {
-  CHECK_GPU(dst_cache); CHECK_CONTIG(dst_cache);
-  TORCH_CHECK(dst_cache.scalar_type() == at::kBFloat16, "cache viewed as bf16");
-  TORCH_CHECK(dst_cache.dim() == 3, "dst cache [planes, NB, block_elems]");
+  TORCH_CHECK(src_planes.scalar_type() == at::kLong && src_planes.is_cuda() &&
+                  src_planes.is_contiguous() && dst_planes.scalar_type() == at::kLong &&
+                  dst_planes.is_cuda() && dst_planes.is_contiguous() &&
+                  src_planes.numel() == dst_planes.numel() && src_planes.numel() % 2 == 0,
+              "plane tables: int64 [2L] on the device, same length");
   TORCH_CHECK(pairs.scalar_type() == at::kInt && pairs.is_cuda() && pairs.is_contiguous(),
               "pairs int32 [n, 2] on the device");
   TORCH_CHECK(pairs.numel() % 2 == 0, "pairs [n, 2]");
-  TORCH_CHECK(src_ptr != 0, "null source cache");
   akap::KVPullArgs a{};
-  a.src = reinterpret_cast<const __bf16*>(src_ptr);
-  a.src_plane_stride = src_plane_stride;
-  a.dst = reinterpret_cast<__bf16*>(dst_cache.data_ptr());
-  a.dst_plane_stride = dst_cache.stride(0);
-  a.planes = dst_cache.size(0);
-  a.block_elems = dst_cache.size(2);
+  a.src_planes = src_planes.data_ptr<int64_t>();
+  a.dst_planes = dst_planes.data_ptr<int64_t>();
+  a.planes = src_planes.numel();
+  a.block_elems = (int)block_elems;
   // bf16 cache: block = Hkv*BS*D; an fp8 (byte) cache is moved as bf16 pairs, block =
   // Hkv*BS*D/2 -- the copy jobs are dtype-agnostic 16-byte moves; V tails exist only for bf16
   const bool byte_cache = (int64_t)a.block_elems * 2 == Hkv * BS * D;
   TORCH_CHECK(a.block_elems % 8 == 0 && (a.block_elems == Hkv * BS * D || byte_cache),
               "block = Hkv*BS*D (bf16) or Hkv*BS*D/2 (fp8 bytes viewed as bf16)");
-  TORCH_CHECK(src_plane_stride % a.block_elems == 0, "source plane stride");
   a.pairs = pairs.data_ptr<int>();
   a.nblk = pairs.numel() / 2;
   a.Hkv = Hkv; a.BS = BS; a.D = D;
@@ -745,7 +744,7 @@ void kv_pull(int64_t src_ptr, int64_t src_plane_stride, Tensor dst_cache, Tensor
     a.tail_jobs = tail_jobs->data_ptr<int>();
     a.ntail = tail_jobs->numel() / 4;
   }
-  const c10::DeviceGuard g(dst_cache.device());
+  const c10::DeviceGuard g(dst_planes.device());
   akap::launch_kv_pull(a, cur_stream());
 }
 
@@ -1199,8 +1198,8 @@ TORCH_LIBRARY(akap, m) {
   m.def("ipc_open(Tensor blob, int device) -> int");
   m.def("ipc_close(int addr) -> ()");
   m.def(
-      "kv_pull(int src_ptr, int src_plane_stride, Tensor(a!) dst_cache, Tensor pairs, "
-      "Tensor(b!)? tail, Tensor? tail_jobs, int Hkv, int BS, int D) -> ()");
+      "kv_pull(Tensor src_planes, Tensor dst_planes, int block_elems, Tensor pairs, "
+      "Tensor(a!)? tail, Tensor? tail_jobs, int Hkv, int BS, int D) -> ()");
   m.def("moe_topk_softmax(Tensor logits, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def("moe_router_topk(Tensor h, Tensor router, Tensor(a!) topk_w, Tensor(b!) topk_ids, bool renorm) -> ()");
   m.def(

@@ -84,11 +84,17 @@ class ModelRunner:
                              device=self.device if self.is_gpu else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.ps.tp_group)
             self.num_blocks = int(t.item())
-        self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs, ecfg.kv_cache_dtype)
-        self.k_caches, self.v_caches = self.model.cache_views(self.kv, self.bs)
+        # layer-range segments, one allocation each (DecoderLM.allocate_kv_segments); `kv` is the
+        # single tensor when one segment holds every layer (small caches, tests)
+        self.kv_segs = self.model.allocate_kv_segments(self.num_blocks, self.bs,
+                                                       ecfg.kv_cache_dtype)
+        self.kv = self.kv_segs[0] if len(self.kv_segs) == 1 else None
+        self.kv_dtype = self.kv_segs[0].dtype
+        self.k_caches, self.v_caches = self.model.cache_views(self.kv_segs, self.bs)
+        gib = sum(t.numel() * t.element_size() for t in self.kv_segs) / 2**30
         self.log(f"[runner] KV cache: {self.num_blocks} blocks x {self.bs} tokens "
-                 f"({self.kv.numel() * self.kv.element_size() / 2**30:.1f} GiB, "
-                 f"{'fp8 e4m3' if self.kv.dtype == torch.uint8 else 'bf16'})")
+                 f"({gib:.1f} GiB in {len(self.kv_segs)} allocation(s), "
+                 f"{'fp8 e4m3' if self.kv_dtype == torch.uint8 else 'bf16'})")
         # V tail (see AttnParams.v_tail): one slot per live sequence (2x max_num_seqs, as P/D
         # activations can briefly exceed it; a sequence without a slot uses the plain path)
         self.v_tails: Optional[list] = None
@@ -107,7 +113,7 @@ class ModelRunner:
         # top-N alternatives of the last step's sampled rows: (token ids [n, N], log-probs)
         self.last_top: Optional[tuple] = None
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
-        self.ep_overflow_steps = 0  # decode steps re-run after an EP dispatch overflow
+        self.ep_overflow_steps = 0  # steps re-run after an EP dispatch overflow
         self.graph_pool = None
         self.buckets: list[int] = []
         if self.is_gpu and not ecfg.enforce_eager and self.model.graph_safe:
@@ -119,7 +125,7 @@ class ModelRunner:
         cache, fused decode attention.  AKAP_V_TAIL=0 restores the per-token cache write."""
         from ..models import transformer as tfm
 
-        return (self.is_gpu and self.kv.dtype == torch.bfloat16 and tfm.FUSED_DECODE and
+        return (self.is_gpu and self.kv_dtype == torch.bfloat16 and tfm.FUSED_DECODE and
                 os.environ.get("AKAP_V_TAIL", "1") != "0" and
                 not (self.ecfg.kv_role == "decode" and self.ps.tp_size > 1))
 
@@ -134,18 +140,21 @@ class ModelRunner:
             # one launch for every layer (the tail-only form of the IPC pull kernel, reading
             # this engine's own cache) instead of a per-layer copy loop
             planes = self.kv_planes()
-            ops.kv_pull(planes.data_ptr(), planes.stride(0), planes.shape[1], planes, [],
-                        self.model.hkv, self.bs, self.model.D, tail=self._tail,
-                        tail_jobs=[(blk, grp, cnt, slot)])
+            ops.kv_pull(ops.plane_table(planes), self.num_blocks, planes, [], self.model.hkv,
+                        self.bs, self.model.D, tail=self._tail, tail_jobs=[(blk, grp, cnt, slot)])
             return
         for vt, vc in zip(self.v_tails, self.v_caches):
             vt[slot, :, :cnt].copy_(vc[blk, :, grp, :, :cnt].transpose(-1, -2))
 
-    def kv_planes(self) -> torch.Tensor:
-        """The KV cache as [2L planes, NB, block_elems] (bf16 view: fp8 bytes move in pairs)."""
-        kv = self.kv.view(torch.bfloat16) if self.kv.dtype == torch.uint8 else self.kv
-        L, two, NB, be = kv.shape
-        return kv.view(L * two, NB, be)
+    def kv_planes(self) -> list:
+        """The KV cache as [2 Ls planes, NB, block_elems] views, one per segment (bf16 views:
+        fp8 bytes move in pairs)."""
+        out = []
+        for seg in self.kv_segs:
+            kv = seg.view(torch.bfloat16) if seg.dtype == torch.uint8 else seg
+            L, two, NB, be = kv.shape
+            out.append(kv.view(L * two, NB, be))
+        return out
 
     # ------------------------------------------------------------------ sizing
     def _derive_num_blocks(self) -> int:
@@ -349,7 +358,22 @@ class ModelRunner:
         batch = AttnBatch(True, pos, slots, bt, sl, qs, ts, tr, parts, ps,
                           self.workspace, tile_rows=self.tile_rows, num_decode=nd,
                           v_tails=self.v_tails, tail_slot=v["tail_slot"])
+        if self._ep_moe:
+            moe_mod.ep_overflow_reset(self.device)
         h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
+        if self._ep_moe:
+            # the fixed-capacity EP dispatch costs this step ONE host check, not a sync per MoE
+            # layer: on an overflow (any rank) every rank re-runs the forward on the exact path
+            # (same KV slots rewritten, same inputs)
+            moe_mod.ep_overflow_reduce(self.device)
+            if self._ep_overflowed():
+                self.ep_overflow_steps += 1
+                with moe_mod.exact_dispatch():
+                    h = self.model.forward(ids, batch, self.k_caches, self.v_caches)
+        if self.ps.world_size > 1:
+            from ..parallel import comm
+
+            comm.check_deferred()
         if ns == 0:
             # a chunk that samples nothing (a long prompt's inner chunk): the caller's
             # device->host copy of zero tokens does not wait for the GPU, but the H2D copies
@@ -453,16 +477,25 @@ class ModelRunner:
         extras = info.get("extras")
         if graph is not None and not extras:
             graph.replay()
-            if self._ep_overflowed():
-                # routing skew beyond the dispatch capacity: redo the step eagerly on the
-                # exact-split path (the same KV slots are rewritten, the tokens replaced)
-                self.ep_overflow_steps += 1
-                self._decode_body(n, extras)
         else:
             # penalties / log-probs requested: the same padded batch (n rows, so TP peers
             # replaying their graphs issue identical collectives), eagerly
             self._decode_body(n, extras)
+        self._ep_rerun_if_overflowed(n, extras)
+        if self.ps.world_size > 1:
+            from ..parallel import comm
+
+            comm.check_deferred()
         return self.out_tokens[:B]
+
+    def _ep_rerun_if_overflowed(self, n: int, extras: Optional[dict]) -> None:
+        """After a decode step (replayed or eager): routing skew beyond the fixed dispatch
+        capacity on any rank -> every rank redoes the step eagerly on the exact-split path (the
+        same KV slots are rewritten, the tokens replaced)."""
+        if self._ep_overflowed():
+            self.ep_overflow_steps += 1
+            with moe_mod.exact_dispatch():
+                self._decode_body(n, extras)
 
     def launch_decode(self, info: dict, chained: bool = False):
         """Queue a graph-replayed decode step without waiting for it.  chained: the step was
@@ -524,8 +557,10 @@ class ModelRunner:
         """TP follower ranks, for a decode step rank 0 runs eagerly (its extras: penalties /
         log-probs): the same padded batch through _decode_body, so this rank issues exactly
         the collectives rank 0 does (inputs by the in-step broadcast of rank 0's staging
-        region; an expert-parallel step takes the exact-split dispatch on every rank)."""
-        self._decode_body(self._bucket(info["num_seqs"]))
+        region; an expert-parallel overflow re-run happens on every rank alike)."""
+        n = self._bucket(info["num_seqs"])
+        self._decode_body(n)
+        self._ep_rerun_if_overflowed(n, None)
 
     @staticmethod
     def wait_decode(handle) -> np.ndarray:

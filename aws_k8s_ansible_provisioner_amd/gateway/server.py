@@ -37,7 +37,7 @@ class Gateway:
     def __init__(self, static: list[tuple], dns: list[tuple[str, int, str]],
                  cfg: Optional[PickerConfig] = None, scrape_interval: float = 1.0,
                  request_timeout: float = 600.0):
-        """static: (url, role[, P/D group]) tuples; dns: (host, port, role)."""
+        """static: (url, role[, P/D group]) tuples; dns: (host, port, role[, group])."""
         self.static = static
         self.dns = dns
         self.picker = EndpointPicker([], cfg)
@@ -79,12 +79,14 @@ class Gateway:
     async def refresh_dns(self) -> None:
         found = list(self.static)
         loop = asyncio.get_running_loop()
-        for host, port, role in self.dns:
+        for host, port, role, group in self.dns:
             try:
                 infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
                 for ip in sorted({i[4][0] for i in infos}):
-                    # pod IP = P/D group: a pod's prefill (:8000) and decode (:8001) ranks
-                    found.append((f"http://{ip}:{port}", role, ip))
+                    # P/D group: the pod IP by default (a pod's prefill :8000 and decode :8001
+                    # ranks); a named group for two-pod P/D, where prefill and decode are
+                    # separate Deployments whose servers form KV channels on demand
+                    found.append((f"http://{ip}:{port}", role, group or ip))
             except OSError:
                 pass
         self.picker.set_endpoints(found)
@@ -280,12 +282,15 @@ def _parse_targets(spec: str) -> list[tuple[str, str, str]]:
     return out
 
 
-def _parse_dns(spec: str) -> list[tuple[str, int, str]]:
+def _parse_dns(spec: str) -> list[tuple[str, int, str, str]]:
+    """host:port[@role[:group]],...  (group: P/D group of every resolved endpoint; default the
+    endpoint's own IP, i.e. P/D pairs only inside one pod)."""
     out = []
     for item in filter(None, (s.strip() for s in spec.split(","))):
-        hp, _, role = item.partition("@")
+        hp, _, rg = item.partition("@")
+        role, _, group = rg.partition(":")
         u = urlparse("//" + hp)
-        out.append((u.hostname, u.port or 8000, role or "both"))
+        out.append((u.hostname, u.port or 8000, role or "both", group))
     return out
 
 
@@ -294,7 +299,8 @@ def main(argv=None) -> None:
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=80)
     ap.add_argument("--endpoints", default="", help="url[@role],... (role: both|prefill|decode)")
-    ap.add_argument("--dns", default="", help="headless-service-host:port[@role],...")
+    ap.add_argument("--dns", default="",
+                    help="headless-service-host:port[@role[:group]],... (group: two-pod P/D)")
     ap.add_argument("--scrape-interval", type=float, default=1.0)
     ap.add_argument("--pd-threshold-chars", type=int, default=512)
     ap.add_argument("--w-prefix", type=float, default=2.0)

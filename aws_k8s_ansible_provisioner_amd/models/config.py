@@ -123,6 +123,15 @@ LLAMA3_70B = register(ModelConfig(
     num_heads=64, num_kv_heads=8, head_dim=128, rms_eps=1e-5, rope_theta=500000.0,
     max_position=8192, bos_id=128000, eos_id=128009))
 
+# Llama-3-70B's real layer widths (d 8192, 64/8 heads, ffn 28672, vocab 128256) at 4 layers:
+# the TP=4 / TP=8 decode collectives at their production message sizes (B=256 x 8192 bf16 =
+# 4 MiB per all-reduce) on one GPU, multi-process
+LLAMA3_70B_L4 = register(ModelConfig(
+    name="llama-3-70b-l4", hf_id="test/llama-3-70b-l4", arch="llama",
+    vocab_size=128256, hidden_size=8192, intermediate_size=28672, num_layers=4,
+    num_heads=64, num_kv_heads=8, head_dim=128, rms_eps=1e-5, rope_theta=500000.0,
+    max_position=8192, bos_id=128000, eos_id=128009))
+
 MIXTRAL_8X7B = register(ModelConfig(
     name="mixtral-8x7b", hf_id="mistralai/Mixtral-8x7B-Instruct-v0.1", arch="mixtral",
     vocab_size=32000, hidden_size=4096, intermediate_size=14336, num_layers=32,

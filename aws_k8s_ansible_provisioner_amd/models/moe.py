@@ -11,25 +11,27 @@ Expert GEMMs: `ops.fused_moe` -- device-side sort + grouped MFMA GEMMs + gather-
 no host sync, at every batch size in "tp" mode (decode steps inside the hipGraph, prefill
 chunks eagerly); the per-expert loop below serves only the CPU reference path.
 
-"ep" mode inside a captured decode step: a FIXED-CAPACITY dispatch -- every (token, expert)
-pair gets a slot (destination rank, rank-local index) computed on the device, the send buffer
-is [ep, C, d] with C = ep_capacity(n) = max(ceil(slack * n / ep), min(n, 8)) for the n = T*K
-pairs of this rank (slack 2 by default, AKAP_EP_SLACK): the exchanged bytes stay within
-slack x the exact n*d however many ranks there are, where a worst-case C = n would move
-ep*n*d.  Both all_to_all_single calls use equal splits and no split size goes to the host,
-so the whole EP MoE block (route, dispatch, grouped expert GEMMs on the received rows,
-combine) is sync-free and graph-capturable.  Empty slots carry expert id -1, which moe_align
-skips.  A pair whose destination already holds C pairs (a routing skew the capacity does not
-cover) is not sent; it raises the shared overflow flag instead, which the decode step
-all-reduces over the EP group at its end (ep_overflow_reduce): the runner then re-runs that
-step eagerly on the exact path (ModelRunner.execute_decode), so an overflow costs one extra
-step, never a wrong token.  Eager steps exchange exact split sizes (one small host sync per
-layer) and run the received rows through the same grouped GEMM; AKAP_EP_FIXED_MAX_T > 0 makes
-eager steps up to that many tokens take the fixed path too (with an immediate all-reduced
-overflow check: tests).
+"ep" mode: a FIXED-CAPACITY dispatch -- every (token, expert) pair gets a slot (destination
+rank, rank-local index) computed on the device, the send buffer is [ep, C, d] with
+C = ep_capacity(n) = max(ceil(slack * n / ep), min(n, 8)) for the n = T*K pairs of this rank
+(slack 2 by default, AKAP_EP_SLACK): the exchanged bytes stay within slack x the exact n*d
+however many ranks there are, where a worst-case C = n would move ep*n*d.  Both
+all_to_all_single calls use equal splits and no split size goes to the host, so the whole EP
+MoE block (route, dispatch, grouped expert GEMMs on the received rows, combine) is sync-free
+and graph-capturable.  Empty slots carry expert id -1: moe_align skips them at decode sizes,
+and at prefill sizes they sort into a dummy group past the last expert offset that the
+grouped GEMM never computes.  A pair whose destination already holds C pairs (a routing skew
+the capacity does not cover) is not sent; it raises the shared overflow flag instead, which
+the STEP all-reduces over the EP group at its end (ep_overflow_reduce) and checks once on the
+host: the runner then re-runs that step under exact_dispatch() (ModelRunner.execute_prefill /
+execute_decode), so an overflow costs one extra step, never a wrong token, and a prefill
+step no longer pays a host sync per MoE layer.  The exact path (split sizes to the host, one
+sync per layer) serves those re-runs, and eager steps above AKAP_EP_FIXED_MAX_T tokens
+(0 = always exact: tests).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Optional
 
@@ -62,6 +64,18 @@ def ep_overflow_reduce(device) -> torch.Tensor:
         else:
             torch.distributed.all_reduce(f, op=torch.distributed.ReduceOp.MAX)
     return f
+
+
+@contextlib.contextmanager
+def exact_dispatch():
+    """Re-run a step whose fixed-capacity dispatch overflowed: every EP layer inside takes the
+    exact-split path.  Counted in MoEBlock.ep_fallbacks."""
+    MoEBlock.ep_fallbacks += 1
+    MoEBlock.force_exact = True
+    try:
+        yield
+    finally:
+        MoEBlock.force_exact = False
 
 
 class MoEBlock:
@@ -169,10 +183,12 @@ class MoEBlock:
             return full[:T]
         return self._forward_tokens(h)
 
-    ep_fixed_max_tokens = int(os.environ.get("AKAP_EP_FIXED_MAX_T", "0"))
+    ep_fixed_max_tokens = int(os.environ.get("AKAP_EP_FIXED_MAX_T", str(1 << 30)))
     ep_slack = float(os.environ.get("AKAP_EP_SLACK", "2.0"))
     ep_min_cap = int(os.environ.get("AKAP_EP_MIN_CAP", "8"))
-    ep_fallbacks = 0  # eager fixed-path layers redone on the exact path after an overflow
+    ep_fallbacks = 0  # steps re-run on the exact path after a dispatch overflow
+    force_exact = False  # set by exact_dispatch() around such a re-run
+    ep_exact_layers = 0  # layer calls on the exact (host-synced) path
     _overflow: dict = {}  # device -> int32 [1]: a fixed-capacity dispatch dropped a pair
 
     def ep_capacity(self, n: int) -> int:
@@ -203,13 +219,10 @@ class MoEBlock:
         if self.mode == "ep":
             if capturing:
                 return self._ep_fixed(h, w, ids)
-            if T <= self.ep_fixed_max_tokens:
-                flag = torch.zeros(1, dtype=torch.int32, device=h.device)
-                y = self._ep_fixed(h, w, ids, flag)
-                torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
-                if int(flag.item()) == 0:
-                    return y
-                MoEBlock.ep_fallbacks += 1
+            if T <= self.ep_fixed_max_tokens and not MoEBlock.force_exact:
+                # no host sync here: an overflow only raises the shared flag, which the step
+                # checks once at its end (ModelRunner) and answers with an exact re-run
+                return self._ep_fixed(h, w, ids)
             return self._ep_exact(h, w, ids)
         # tp mode, no host sync at any size: decode sizes (and every captured step) on the
         # hand-written fused_moe, prefill sizes (and the CPU path) on the library grouped GEMM
@@ -237,7 +250,7 @@ class MoEBlock:
     def _expert_rows(self, x: torch.Tensor, e: torch.Tensor,
                      src: Optional[torch.Tensor] = None, sorted_out: bool = False):
         """y[i] = expert e[i]'s SwiGLU FFN of x[src[i]] (src = identity when None), unweighted.
-        Rows are sorted by expert on the device and run through a grouped GEMM over device-side
+        Rows are sorted by expert on the device (ids -1 = empty rows, skipped) and run through a grouped GEMM over device-side
         group offsets -- the hand-written pgemm (SwiGLU fused into the first GEMM's epilogue) or
         torch._grouped_mm (the ROCm library grouped GEMM), whichever measured faster at engine
         start (gemm_tuner.tune_prefill): no host sync, no per-expert loop.  Mixtral-8x7B shapes
@@ -247,8 +260,15 @@ class MoEBlock:
         store: deterministic, no float atomics), or with sorted_out as (expert-sorted rows,
         order) for a caller that gathers them itself."""
         e = e.reshape(-1).long()
-        order = torch.argsort(e, stable=True)
-        offs = torch.cumsum(torch.bincount(e, minlength=self.e_local), 0).to(torch.int32)
+        el = self.e_local
+        # empty fixed-dispatch slots (id -1) sort last into a dummy group past the final offset:
+        # the grouped GEMM never computes those rows (their outputs are never read)
+        key = torch.where(e < 0, torch.full_like(e, el), e)
+        ks, order = torch.sort(key, stable=True)
+        # group end offsets by binary search on the sorted ids: no bincount (its CUDA path reads
+        # the max id back to the host)
+        offs = torch.searchsorted(ks, torch.arange(el, device=ks.device, dtype=ks.dtype),
+                                  right=True).to(torch.int32)
         xs = x[order if src is None else src[order]]
         if ops.use_pgemm(xs, self.w13.shape[1], silu=True, grouped=True):
             # hand-written grouped GEMM with SwiGLU in its epilogue (csrc/kernels/pgemm.hip)
@@ -300,9 +320,13 @@ class MoEBlock:
         recv_x = recv[:, :d].contiguous()
         recv_e = recv[:, d:d + 2].contiguous().view(torch.int32).reshape(-1, 1)
         # every received row is one (token, local expert) pair: K = 1, weight 1 (the router
-        # weight is applied by the sender at combine); empty slots (id -1) give zero rows
-        ones = torch.ones(ep * C, 1, dtype=torch.float32, device=h.device)
-        y = ops.fused_moe(recv_x, self.w13, self.w2, ones, recv_e)
+        # weight is applied by the sender at combine); empty slots (id -1) are skipped
+        if (h.is_cuda and not torch.cuda.is_current_stream_capturing()
+                and ep * C >= self.grouped_min_t * K):
+            y = self._expert_rows(recv_x, recv_e)  # prefill sizes: the grouped GEMM
+        else:
+            ones = torch.ones(ep * C, 1, dtype=torch.float32, device=h.device)
+            y = ops.fused_moe(recv_x, self.w13, self.w2, ones, recv_e)
         back = h.new_zeros(ep * C + 1, d)
         comm.ep_all_to_all_equal(back[:ep * C], y.contiguous())
         mine = back.index_select(0, pos).view(T, K, d).float()
@@ -311,6 +335,7 @@ class MoEBlock:
     def _ep_exact(self, h: torch.Tensor, w: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
         """Prefill-size EP: exact split sizes (one host sync for the counts), received rows
         through the grouped expert GEMM (no per-expert host loop)."""
+        MoEBlock.ep_exact_layers += 1
         T, d = h.shape
         flat = ids.reshape(-1).long()
         order = torch.argsort(flat, stable=True)

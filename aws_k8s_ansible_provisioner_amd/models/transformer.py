@@ -272,18 +272,38 @@ class DecoderLM:
     # ------------------------------------------------------------------ kv cache
     def allocate_kv_cache(self, num_blocks: int, block_size: int,
                           kv_dtype: str = "auto") -> torch.Tensor:
-        """One allocation [L, 2, NB, Hkv*BS*D] (K block = [Hkv,BS,D], V block = [Hkv,BS/8,D,8]),
+        """The whole cache as ONE allocation [L, 2, NB, Hkv*BS*D] (micro-benchmarks, tests)."""
+        return self.allocate_kv_segments(num_blocks, block_size, kv_dtype,
+                                         max_segment_bytes=1 << 62)[0]
+
+    def allocate_kv_segments(self, num_blocks: int, block_size: int, kv_dtype: str = "auto",
+                             max_segment_bytes: Optional[int] = None) -> list:
+        """Layer-range segments [Ls, 2, NB, Hkv*BS*D] (K block = [Hkv,BS,D], V block =
+        [Hkv,BS/8,D,8]) of at most `max_segment_bytes` each (AKAP_KV_SEGMENT_GIB, default 32),
         zero-filled so never-written slots read as finite zeros.  kv_dtype "fp8": uint8
-        storage of OCP e4m3fn values (half the bytes of bf16)."""
+        storage of OCP e4m3fn values (half the bytes of bf16).  Each segment is its own
+        allocation, exported by hipIpc on its own (P/D pull): a single ~86 GiB export hung
+        hipIpcOpenMemHandle for a second importer on one device (profiles/
+        r4_pd_1p2d_one_gpu.log) while 3 x 28.7 GiB opened (profiles/r5_probes_s5b.md)."""
         per_block = self.hkv * block_size * self.D
         dt = torch.uint8 if kv_dtype.startswith("fp8") else self.dtype
-        return torch.zeros(self.cfg.num_layers, 2, num_blocks, per_block, dtype=dt,
-                           device=self.device)
+        if max_segment_bytes is None:
+            max_segment_bytes = int(float(os.environ.get("AKAP_KV_SEGMENT_GIB", "32")) * 2**30)
+        L = self.cfg.num_layers
+        per_layer = 2 * num_blocks * per_block * torch.empty(0, dtype=dt).element_size()
+        lps = max(1, min(L, max_segment_bytes // max(1, per_layer)))
+        return [torch.zeros(min(lps, L - l0), 2, num_blocks, per_block, dtype=dt,
+                            device=self.device) for l0 in range(0, L, lps)]
 
-    def cache_views(self, kv: torch.Tensor, block_size: int):
-        NB = kv.shape[2]
-        ks = [kv[l, 0].view(NB, self.hkv, block_size, self.D) for l in range(kv.shape[0])]
-        vs = [kv[l, 1].view(NB, self.hkv, block_size // 8, self.D, 8) for l in range(kv.shape[0])]
+    def cache_views(self, kv, block_size: int):
+        """Per-layer K / V views of the cache (one tensor or its list of layer segments)."""
+        segs = list(kv) if isinstance(kv, (list, tuple)) else [kv]
+        ks, vs = [], []
+        for seg in segs:
+            NB = seg.shape[2]
+            ks += [seg[l, 0].view(NB, self.hkv, block_size, self.D) for l in range(seg.shape[0])]
+            vs += [seg[l, 1].view(NB, self.hkv, block_size // 8, self.D, 8)
+                   for l in range(seg.shape[0])]
         return ks, vs
 
     # ------------------------------------------------------------------ forward

@@ -737,17 +737,32 @@ def kv_scatter(buf, cache_planes, block_ids):
     view[:, block_ids.long()] = buf.view(planes, block_ids.numel(), blk)
 
 
-def kv_pull(src_ptr: int, src_plane_stride: int, src_nblocks: int, dst_planes: torch.Tensor,
-            pairs, Hkv: int, BS: int, D: int, tail: Optional[torch.Tensor] = None,
-            tail_jobs=None) -> None:
+def plane_table(planes) -> list[int]:
+    """Device addresses of every plane of a cache given as [P, NB, be] plane views (one per
+    allocation segment) -- the kv_pull kernel addresses planes through such a table."""
+    out = []
+    for pl in (planes if isinstance(planes, (list, tuple)) else [planes]):
+        base, st = pl.data_ptr(), pl.stride(0) * pl.element_size()
+        out += [base + i * st for i in range(pl.shape[0])]
+    return out
+
+
+def kv_pull(src_planes: list, src_nblocks: int, dst_planes, pairs, Hkv: int, BS: int, D: int,
+            tail: Optional[torch.Tensor] = None, tail_jobs=None) -> None:
     """hipIpc KV hand-off (csrc/kernels/kv_transfer.hip): copy blocks pairs[i] = (src block,
-    dst block) of every plane from the cache at device address `src_ptr` (a peer's cache
-    mapped by ipc_open, or this engine's own) into dst_planes [planes, NB, block_elems], and
+    dst block) of every plane from the source planes (device addresses, one per plane: a
+    peer's cache segments mapped by ipc_open, or this engine's own -- plane_table) into
+    dst_planes ([P, NB, block_elems] views, one per segment of this engine's cache), and
     fill V tails: tail_jobs[j] = (src block, 8-token group, count 1..7, tail slot).  One
     launch on the current stream.  Every index is range-checked here, on the host, before
     anything reaches the kernel (an out-of-range block id would read or write outside the
     caches)."""
-    nb = dst_planes.shape[1]
+    dsts = list(dst_planes) if isinstance(dst_planes, (list, tuple)) else [dst_planes]
+    nb = dsts[0].shape[1]
+    be = dsts[0].shape[2]
+    dst_tab = plane_table(dsts)
+    if len(src_planes) != len(dst_tab):
+        raise ValueError(f"kv_pull: {len(src_planes)} source planes vs {len(dst_tab)} own")
     pairs = [(int(s), int(d)) for s, d in pairs]
     for s, d in pairs:
         if not (0 <= s < src_nblocks and 0 <= d < nb):
@@ -762,13 +777,13 @@ def kv_pull(src_ptr: int, src_plane_stride: int, src_nblocks: int, dst_planes: t
                 raise IndexError(f"kv_pull tail job {(s, g, c, slot)} out of range")
     if not pairs and not jobs:
         return
-    dev = dst_planes.device
+    dev = dsts[0].device
+    tabs = torch.tensor([list(src_planes), dst_tab], dtype=torch.int64).to(dev)
     pt = torch.tensor(pairs, dtype=torch.int32).reshape(-1).to(dev, non_blocking=True) \
         if pairs else torch.zeros(0, dtype=torch.int32, device=dev)
     jt = torch.tensor(jobs, dtype=torch.int32).reshape(-1).to(dev, non_blocking=True) \
         if jobs else None
-    torch.ops.akap.kv_pull(int(src_ptr), int(src_plane_stride), dst_planes, pt,
-                           tail if jobs else None, jt, Hkv, BS, D)
+    torch.ops.akap.kv_pull(tabs[0], tabs[1], int(be), pt, tail, jt, int(Hkv), int(BS), int(D))
 
 
 def ipc_export(t: torch.Tensor) -> bytes:

@@ -40,13 +40,26 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
         step = (per + 7) // 8 * 8  # near-equal pieces, each 16-B aligned
         for i in range(0, flat.numel(), step):
             st.car.all_reduce(flat[i:i + step])
-        # a piece whose flag wait timed out only raises the kernel's error word: check it
-        # here (this eager rehearsal path can afford the sync) instead of summing on silently
-        if st.car.error():
-            raise RuntimeError("custom all-reduce timed out in a piecewise prefill all-reduce")
+        # a piece whose flag wait timed out only raises the kernel's error word: the step
+        # checks it once at its end (check_deferred), not a device sync per all-reduce
+        _UNCHECKED[0] = True
         return x
     dist.all_reduce(x, group=st.tp_group)
     return x
+
+
+_UNCHECKED = [False]  # a piecewise / chunked IPC collective ran since the last check
+
+
+def check_deferred() -> None:
+    """End of an eager step: raise if one of its piecewise IPC collectives timed out (the
+    kernels only set an error word; silently summing on would corrupt the step)."""
+    if not _UNCHECKED[0]:
+        return
+    _UNCHECKED[0] = False
+    st = get_state()
+    if st is not None and st.car is not None and st.car.error():
+        raise RuntimeError("custom IPC collective timed out in a piecewise prefill step")
 
 
 def _car_pieces_ok(x: torch.Tensor, car) -> bool:
@@ -136,6 +149,23 @@ def ep_all_to_all_equal(recv: torch.Tensor, send: torch.Tensor) -> torch.Tensor:
     if (st.car is not None and st.tp_size == st.world_size and st.car.a2a_ok(send)
             and recv.is_contiguous() and recv.dtype == send.dtype):
         return st.car.all_to_all(send.view(-1), recv.view(-1)).view_as(recv)
+    if (st.car is not None and st.tp_size == st.world_size and st.backend == "gloo"
+            and _car_pieces_ok(send, st.car) and send.numel() % (8 * st.world_size) == 0
+            and recv.is_contiguous() and recv.dtype == send.dtype):
+        # ranks sharing one GPU over a gloo control plane (single-GPU rehearsal of an EP
+        # prefill): the dispatch stays on the device as column slabs of the IPC kernel
+        W = st.world_size
+        seg = send.numel() // W
+        cap = max(8, st.car.buffer_bytes // send.element_size() // W // 8 * 8)
+        src, dst = send.view(W, seg), recv.view(W, seg)
+        for c0 in range(0, seg, cap):
+            c1 = min(seg, c0 + cap)
+            piece = src[:, c0:c1].contiguous()
+            out = torch.empty_like(piece)
+            st.car.all_to_all(piece.view(-1), out.view(-1))
+            dst[:, c0:c1].copy_(out)
+        _UNCHECKED[0] = True
+        return recv
     dist.all_to_all_single(recv, send)
     return recv
 

@@ -122,18 +122,25 @@ class KVTransferAgent:
         pair: (ProcessGroup, backend name) of a two-rank channel between two independently
         started servers (two-pod P/D, `connect_pair` / `PairHost`) -- used instead of a
         group of the default torch.distributed world."""
+        # the cache is one tensor [L, 2, NB, be] or its layer-range segments (one allocation
+        # each: model_runner.kv_segs); planes are addressed per segment
+        segs = list(kv_cache) if isinstance(kv_cache, (list, tuple)) else [kv_cache]
         # fp8: bytes moved as bf16 pairs; kv_pull takes the halved block (ops.cpp), and an fp8
         # cache has no V tail
-        self.byte_cache = kv_cache.dtype == torch.uint8
+        self.byte_cache = segs[0].dtype == torch.uint8
         if self.byte_cache:
-            kv_cache = kv_cache.view(torch.bfloat16)
-        self.kv = kv_cache
-        L, two, NB, be = kv_cache.shape
-        self.planes = kv_cache.view(L * two, NB, be)
+            segs = [t.view(torch.bfloat16) for t in segs]
+        self.segs = segs
+        self.kv = segs[0]
+        self.planes_list = [t.view(t.shape[0] * t.shape[1], t.shape[2], t.shape[3]) for t in segs]
+        self.planes = self.planes_list[0]
+        self.num_planes = sum(p.shape[0] for p in self.planes_list)
+        self.nblocks = segs[0].shape[2]
+        be = segs[0].shape[3]
         self.block_elems = be
         self.group = group
         self.timeout_s = timeout_s
-        self.device = kv_cache.device
+        self.device = segs[0].device
         self.is_gpu = self.device.type == "cuda"
         self.stream = torch.cuda.Stream(device=self.device) if self.is_gpu else None
         self._q: "queue.Queue" = queue.Queue()
@@ -160,7 +167,19 @@ class KVTransferAgent:
         self.pull_seconds = 0.0
 
     def nbytes(self, nblk: int) -> int:
-        return self.planes.shape[0] * nblk * self.block_elems * self.kv.element_size()
+        return self.num_planes * nblk * self.block_elems * self.kv.element_size()
+
+    def _gather(self, ids: torch.Tensor) -> torch.Tensor:
+        """Pack blocks `ids` of every plane (all segments) into [planes, n, block_elems]."""
+        if len(self.planes_list) == 1:
+            return ops.kv_gather(self.planes, ids)
+        return torch.cat([ops.kv_gather(pl, ids) for pl in self.planes_list], 0)
+
+    def _scatter(self, buf: torch.Tensor, ids: torch.Tensor) -> None:
+        p0 = 0
+        for pl in self.planes_list:
+            ops.kv_scatter(buf[p0:p0 + pl.shape[0]], pl, ids)
+            p0 += pl.shape[0]
 
     # ---------------------------------------------------------------- worker
     def _run(self) -> None:
@@ -227,7 +246,7 @@ class KVTransferAgent:
                 self._check()
                 with self._ctx():
                     ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
-                    buf = ops.kv_gather(self.planes, ids)
+                    buf = self._gather(ids)
                     if self.host_staging or not self.is_gpu:
                         if self.is_gpu:
                             self.stream.synchronize()
@@ -255,7 +274,7 @@ class KVTransferAgent:
         which may reuse the blocks -- are ordered after the copy, so the caller may free the
         blocks as soon as this returns.  Returns (packed buffer, ready event) for send_packed."""
         ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
-        buf = ops.kv_gather(self.planes, ids)
+        buf = self._gather(ids)
         ev = None
         if self.is_gpu:
             ev = torch.cuda.Event()
@@ -306,7 +325,7 @@ class KVTransferAgent:
                 self._check()
                 with self._ctx():
                     n = len(block_ids)
-                    buf = torch.empty(self.planes.shape[0], n, self.block_elems,
+                    buf = torch.empty(self.num_planes, n, self.block_elems,
                                       dtype=self.kv.dtype, device=self.device)
                     if self.host_staging:
                         hb = torch.empty(buf.shape, dtype=buf.dtype)
@@ -317,7 +336,7 @@ class KVTransferAgent:
                         _wait(self._irecv(buf, src), t_out,
                               f"KV recv of {n} blocks from rank {src}", self.gloo)
                     ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
-                    ops.kv_scatter(buf, self.planes, ids)
+                    self._scatter(buf, ids)
                     if self.is_gpu:
                         self.stream.synchronize()
                 self.bytes_recv += buf.numel() * buf.element_size()
@@ -361,38 +380,48 @@ class KVTransferAgent:
 
     # ---------------------------------------------------------------- hipIpc pull
     def ipc_meta(self) -> dict:
-        """What a decode peer needs to map this engine's cache (JSON-able)."""
+        """What a decode peer needs to map this engine's cache (JSON-able): one hipIpc export
+        per cache segment (allocation) and the geometry."""
         import base64
 
-        P, NB, be = self.planes.shape
-        return {"blob": base64.b64encode(ops.ipc_export(self.planes)).decode(),
-                "planes": int(P), "nblocks": int(NB), "block_elems": int(be),
+        return {"segments": [{"blob": base64.b64encode(ops.ipc_export(pl)).decode(),
+                              "planes": int(pl.shape[0])} for pl in self.planes_list],
+                "planes": int(self.num_planes), "nblocks": int(self.nblocks),
+                "block_elems": int(self.block_elems),
                 "plane_stride": int(self.planes.stride(0))}
 
     def connect_ipc(self, meta: dict) -> str:
-        """Map a prefill peer's cache (once per peer; the mapping lives as long as this agent).
-        Returns the peer key for pull(); a decode engine of an N:M pod maps several."""
+        """Map a prefill peer's cache segments (once per peer; the mappings live as long as
+        this agent), each open bounded by AKAP_IPC_OPEN_TIMEOUT_S.  Returns the peer key for
+        pull(); a decode engine of an N:M pod maps several peers."""
         import base64
 
-        P, NB, be = self.planes.shape
-        if (int(meta["planes"]), int(meta["block_elems"])) != (P, be):
+        if (int(meta["planes"]), int(meta["block_elems"])) != (self.num_planes, self.block_elems):
             raise ValueError(f"peer cache geometry {meta['planes']}x{meta['block_elems']} != "
-                             f"ours {P}x{be} (same model and block size required)")
-        key = meta["blob"]
+                             f"ours {self.num_planes}x{self.block_elems} (same model and block "
+                             f"size required)")
+        segs = meta["segments"]
+        key = segs[0]["blob"]
         if key in self.ipc_failed:
             raise KVIpcOpenTimeout(self.ipc_failed[key])
         if key not in self.peers:
-            blob = base64.b64decode(meta["blob"])
             dev = self.device.index
+            stride = int(meta["plane_stride"]) * self.kv.element_size()
+            ptrs, table = [], []
             try:
-                ptr = bounded_call(lambda: ops.ipc_open(blob, dev), self.ipc_open_timeout_s,
-                                   f"hipIpc mapping of a {meta['planes']}-plane peer cache")
+                for sg in segs:
+                    blob = base64.b64decode(sg["blob"])
+                    ptr = bounded_call(lambda: ops.ipc_open(blob, dev), self.ipc_open_timeout_s,
+                                       f"hipIpc mapping of a {sg['planes']}-plane peer cache "
+                                       f"segment")
+                    ptrs.append(ptr)
+                    table += [ptr + i * stride for i in range(int(sg["planes"]))]
             except KVIpcOpenTimeout as e:
                 self.ipc_failed[key] = str(e)
                 print(f"[kv-transfer] {e}: this peer falls back to the p2p transport",
                       flush=True)
                 raise
-            self.peers[key] = (ptr, int(meta["nblocks"]), int(meta["plane_stride"]))
+            self.peers[key] = (table, int(meta["nblocks"]), ptrs)
         return key
 
     @property
@@ -410,12 +439,12 @@ class KVTransferAgent:
             if len(self.peers) != 1:
                 raise ValueError("several peer caches mapped: name the peer")
             peer = next(iter(self.peers))
-        ptr, nblocks, stride = self.peers[peer]
+        table, nblocks, _ = self.peers[peer]
         if self.byte_cache and tail_jobs:
             raise ValueError("V-tail jobs with an fp8 KV cache (fp8 caches have no V tail)")
         t0 = time.perf_counter()
         with self._ctx():
-            ops.kv_pull(ptr, stride, nblocks, self.planes, pairs, Hkv, BS, D, tail=tail,
+            ops.kv_pull(table, nblocks, self.planes_list, pairs, Hkv, BS, D, tail=tail,
                         tail_jobs=tail_jobs)
             self.stream.synchronize()
         dt = time.perf_counter() - t0
@@ -428,8 +457,9 @@ class KVTransferAgent:
         if self.peers:
             try:
                 torch.cuda.synchronize(self.device)
-                for ptr, _, _ in self.peers.values():
-                    ops.ipc_close(ptr)
+                for _, _, ptrs in self.peers.values():
+                    for ptr in ptrs:
+                        ops.ipc_close(ptr)
             except Exception:
                 pass
             self.peers = {}

@@ -105,7 +105,7 @@ class PDPair:
             self.peers = [self.peer]
         self.ctrl = ctrl_group
         self.transport = transport or default_transport(engine)
-        self.agent = KVTransferAgent(engine.runner.kv, group=data_group)
+        self.agent = KVTransferAgent(engine.runner.kv_segs, group=data_group)
         self.batches = 0
         self.pull_seconds = 0.0
         self.pulled_bytes = 0

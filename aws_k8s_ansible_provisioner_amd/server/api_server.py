@@ -681,7 +681,7 @@ def build_app(ecfg: EngineConfig, engine=None, pd_bootstrap: str = "launcher",
     if ecfg.kv_role in ("prefill", "decode"):
         from ..parallel.kv_transfer import KVTransferAgent
 
-        ae.kv_agent = KVTransferAgent(eng.runner.kv)
+        ae.kv_agent = KVTransferAgent(eng.runner.kv_segs)
         ae.pd_bootstrap = pd_bootstrap
         if pd_bootstrap == "http":
             # two-pod P/D: no shared job; every prefill/decode pair is its own two-rank channel
@@ -692,7 +692,7 @@ def build_app(ecfg: EngineConfig, engine=None, pd_bootstrap: str = "launcher",
             if ecfg.kv_role == "prefill":
                 from ..parallel.kv_transfer import PairHost
 
-                ae.pair_host = PairHost(eng.runner.kv, kv_store_port)
+                ae.pair_host = PairHost(eng.runner.kv_segs, kv_store_port)
         else:
             ae.pd_group = eng.pd_group = pd_group_id()
         eng.kv_agent = ae.kv_agent

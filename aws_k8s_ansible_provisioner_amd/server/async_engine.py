@@ -411,7 +411,7 @@ class AsyncEngine:
                                          headers={"Content-Type": "application/json"})
             with urllib.request.urlopen(req, timeout=30) as r:
                 meta = json.loads(r.read())
-            ag = connect_pair(self.kv_agent.kv, urlparse(url).hostname, meta["store_port"],
+            ag = connect_pair(self.kv_agent.segs, urlparse(url).hostname, meta["store_port"],
                               meta["prefix"], backend, timeout_s=timeout_s)
             ag.generation = gen
             self.pair_agents[url] = ag

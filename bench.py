@@ -186,11 +186,6 @@ def main() -> int:
 
         ctrl = dist.new_group(backend="gloo")  # small metadata messages on the host
         transport = None if a.kv_transport == "auto" else a.kv_transport
-        if transport is None and shared_ranks > 1 and world - n_pre > n_pre:
-            # several decode processes mapping one prefill cache on the SAME device hang in
-            # hipIpcOpenMemHandle at serving cache sizes (profiles/r4_pd_1p2d_one_gpu.log): the
-            # one-GPU rehearsal of an N:M layout stages through the process group instead
-            transport = "p2p"
         pair = PDPair(eng, rank, world, ctrl_group=ctrl, data_group=None,
                       prefill_ranks=n_pre, transport=transport)
 

@@ -368,7 +368,11 @@ def _kv_pull_worker(rank, port, q, geo, fp8=False):
             ptr = ops.ipc_open(meta[0], 0)
             pairs = [(3, 0), (NB0 - 1, 5), (0, NB1 - 1)]
             jobs = [] if fp8 else [(7, 1, 5, 2), (NB0 - 1, BS // 8 - 1, 3, 5)]
-            ops.kv_pull(ptr, meta[1], NB0, planes, pairs, Hkv, BS, D, tail=tail, tail_jobs=jobs)
+            # the peer's planes as a device-address table; our cache as two segments (layer 0,
+            # layers 1..) -- the cache of a large engine is several allocations
+            src = [ptr + i * meta[1] * 2 for i in range(2 * L)]
+            ops.kv_pull(src, NB0, [planes[:2], planes[2:]], pairs, Hkv, BS, D, tail=tail,
+                        tail_jobs=jobs)
             torch.cuda.synchronize()
             res = ((kv.view(torch.uint8) if fp8 else kv.float()).cpu().numpy(),
                    tail.float().cpu().numpy())

@@ -89,7 +89,10 @@ def test_parsers():
         ("http://a:8000", "prefill", ""), ("http://b:9", "both", ""),
         ("http://c:1", "decode", "g7")]
     assert _parse_dns("svc.ns.svc.cluster.local:8000@decode") == [
-        ("svc.ns.svc.cluster.local", 8000, "decode")]
+        ("svc.ns.svc.cluster.local", 8000, "decode", "")]
+    # two-pod P/D: both Deployments' services carry one named P/D group
+    assert _parse_dns("a-prefill:8000@prefill:akap-pd,a-decode:8000@decode:akap-pd") == [
+        ("a-prefill", 8000, "prefill", "akap-pd"), ("a-decode", 8000, "decode", "akap-pd")]
 
 
 def _free_port():

@@ -387,6 +387,30 @@ def test_moe_block_tp_paths_match_reference(T):
     _close(out, exp, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("R", [1536, 4096])
+def test_moe_expert_rows_skip_empty_slots_gpu(R):
+    """The EP fixed-dispatch receive rows at prefill sizes on the grouped GEMM (pgemm or
+    torch._grouped_mm): empty slots (id -1) fall in a dummy group past the last offset; real
+    rows match the fp32 reference."""
+    from aws_k8s_ansible_provisioner_amd.models.config import get_config
+    from aws_k8s_ansible_provisioner_amd.models.moe import MoEBlock
+    from aws_k8s_ansible_provisioner_amd.parallel.state import ParallelState
+
+    cfg = get_config("tiny-mixtral8")
+    blk = MoEBlock(cfg, ParallelState(rank=0, world_size=1, tp_size=1), DEV, torch.bfloat16,
+                   torch.Generator().manual_seed(0), full_then_shard=False, mode="tp")
+    torch.manual_seed(R)
+    x = torch.randn(R, cfg.hidden_size, dtype=torch.bfloat16)
+    e = torch.randint(0, blk.e_local, (R,))
+    e[torch.rand(R) < 0.5] = -1
+    y = blk._expert_rows(x.to(DEV), e.to(torch.int32).to(DEV)).cpu()
+    real = e >= 0
+    one = torch.ones(R, 1)
+    exp = ref.fused_moe(x[real], blk.w13.cpu(), blk.w2.cpu(), one[real],
+                        e[real].view(-1, 1).to(torch.int32))
+    _close(y[real], exp, atol=3e-2, rtol=3e-2)
+
+
 def test_fused_moe_graph_capture():
     torch.manual_seed(3)
     T, E, K, d, F = 48, 8, 2, 256, 256

@@ -35,8 +35,8 @@ def test_connect_ipc_times_out_then_fails_fast(monkeypatch):
             time.sleep(30)
 
         monkeypatch.setattr(ops, "ipc_open", stuck)
-        meta = {"blob": base64.b64encode(b"x" * 80).decode(), "planes": 4, "nblocks": 4,
-                "block_elems": 64, "plane_stride": 256}
+        meta = {"segments": [{"blob": base64.b64encode(b"x" * 80).decode(), "planes": 4}],
+                "planes": 4, "nblocks": 4, "block_elems": 64, "plane_stride": 256}
         t0 = time.monotonic()
         with pytest.raises(KVIpcOpenTimeout):
             ag.connect_ipc(meta)
@@ -48,7 +48,7 @@ def test_connect_ipc_times_out_then_fails_fast(monkeypatch):
         # an fp8 (byte) cache refuses V-tail jobs (no V tail in fp8 caches)
         ag8 = KVTransferAgent(torch.zeros(2, 2, 4, 128, dtype=torch.uint8))
         assert ag8.byte_cache and ag8.block_elems == 64
-        ag8.peers["k"] = (1, 4, 256)
+        ag8.peers["k"] = ([0] * 4, 4, [])
         with pytest.raises(ValueError):
             ag8.pull([(0, 0)], 1, 32, 4, tail_jobs=[(0, 0, 1, 0)], peer="k")
         ag8.peers = {}
@@ -59,3 +59,42 @@ def test_connect_ipc_times_out_then_fails_fast(monkeypatch):
 
 def test_default_timeout_env(monkeypatch):
     assert kv_transfer.IPC_OPEN_TIMEOUT_S > 0
+
+
+def test_segmented_kv_cache_views_and_packing():
+    """A large cache is several allocations (layer ranges, AKAP_KV_SEGMENT_GIB): the per-layer
+    views, the p2p pack/unpack over every segment's planes and the plane address table of the
+    IPC pull all see the same [2L planes] cache as one allocation would."""
+    from aws_k8s_ansible_provisioner_amd import ops
+    from aws_k8s_ansible_provisioner_amd.models.config import get_config
+    from aws_k8s_ansible_provisioner_amd.models.transformer import DecoderLM
+
+    m = DecoderLM(get_config("tiny-qwen3"), device="cpu", max_model_len=256)
+    L = m.cfg.num_layers
+    one = m.allocate_kv_cache(16, 32)
+    per_layer = one[0].numel() * one.element_size()
+    segs = m.allocate_kv_segments(16, 32, max_segment_bytes=per_layer)  # one layer each
+    assert len(segs) == L and all(t.shape[0] == 1 for t in segs)
+    torch.manual_seed(0)
+    for l in range(L):
+        segs[l].copy_(torch.randn(segs[l].shape).to(segs[l].dtype))
+        one[l].copy_(segs[l][0])
+    ks1, vs1 = m.cache_views(one, 32)
+    ks2, vs2 = m.cache_views(segs, 32)
+    assert all(torch.equal(a, b) for a, b in zip(ks1, ks2))
+    assert all(torch.equal(a, b) for a, b in zip(vs1, vs2))
+    a1, a2 = KVTransferAgent(one), KVTransferAgent(segs)
+    try:
+        ids = torch.tensor([3, 0, 7], dtype=torch.int32)
+        assert a2.num_planes == 2 * L and a2.nbytes(3) == a1.nbytes(3)
+        assert torch.equal(a1._gather(ids), a2._gather(ids))
+        buf = torch.randn(2 * L, 2, a2.block_elems).to(torch.bfloat16)
+        dst = torch.tensor([5, 9], dtype=torch.int32)
+        a1._scatter(buf, dst)
+        a2._scatter(buf, dst)
+        assert all(torch.equal(one[l], segs[l][0]) for l in range(L))
+        tab = ops.plane_table(a2.planes_list)
+        assert len(tab) == 2 * L and tab[1] - tab[0] == segs[0][0, 0].numel() * 2
+    finally:
+        a1.close()
+        a2.close()

@@ -49,6 +49,29 @@ def test_moe_align_reference_layout():
         assert sorted(real.tolist()) == (flat == e).nonzero().flatten().tolist()
 
 
+def test_moe_expert_rows_skip_empty_slots():
+    """EP fixed-dispatch receive buffers at prefill sizes: rows with local expert id -1 (empty
+    slots) sort into a dummy group past the last offset and are never computed; every real
+    row matches its expert's SwiGLU FFN."""
+    from aws_k8s_ansible_provisioner_amd.models.config import get_config
+    from aws_k8s_ansible_provisioner_amd.models.moe import MoEBlock
+    from aws_k8s_ansible_provisioner_amd.parallel.state import ParallelState
+
+    cfg = get_config("tiny-mixtral8")
+    blk = MoEBlock(cfg, ParallelState(rank=0, world_size=1, tp_size=1), "cpu", torch.bfloat16,
+                   torch.Generator().manual_seed(0), full_then_shard=False, mode="tp")
+    torch.manual_seed(5)
+    R = 96
+    x = torch.randn(R, cfg.hidden_size, dtype=torch.bfloat16)
+    e = torch.randint(0, blk.e_local, (R,))
+    e[torch.rand(R) < 0.4] = -1
+    y = blk._expert_rows(x, e.to(torch.int32))
+    real = e >= 0
+    one = torch.ones(R, 1)
+    exp = ops.fused_moe(x[real], blk.w13, blk.w2, one[real], e[real].view(-1, 1).to(torch.int32))
+    assert torch.allclose(y[real].float(), exp.float(), atol=3e-2, rtol=3e-2)
+
+
 def test_moe_capacity_covers_worst_case():
     for n, E, b in [(1, 8, 64), (512, 8, 64), (7, 64, 16)]:
         cap = ops.moe_capacity(n, E, b)

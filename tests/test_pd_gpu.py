@@ -33,8 +33,13 @@ def _port():
     return p
 
 
+@pytest.mark.parametrize("bootstrap", ["launcher", "http"])
 @pytest.mark.parametrize("transport", ["ipc", "p2p"])
-def test_pd_through_the_gateway_on_gpu_matches_monolithic(transport):
+def test_pd_through_the_gateway_on_gpu_matches_monolithic(transport, bootstrap):
+    """bootstrap "launcher": both servers are ranks of one torch.distributed job (one pod);
+    "http": two INDEPENDENTLY started server processes (the two-pod form: no RANK /
+    WORLD_SIZE / MASTER_ADDR) whose KV channel the decode server forms on first use over HTTP
+    (p2p: a gloo pair group -- RCCL places no two ranks on one GPU)."""
     from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
     from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
     from aws_k8s_ansible_provisioner_amd.gateway.picker import PickerConfig
@@ -45,12 +50,20 @@ def test_pd_through_the_gateway_on_gpu_matches_monolithic(transport):
     try:
         for rank, role in enumerate(["prefill", "decode"]):
             port = _port()
-            env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
-                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master),
-                       AKAP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, AKAP_KV_TRANSPORT=transport)
+            extra = []
+            if bootstrap == "launcher":
+                env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master),
+                           AKAP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, AKAP_KV_TRANSPORT=transport)
+            else:
+                env = {k: v for k, v in os.environ.items() if k not in
+                       ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+                env.update(PYTHONPATH=ROOT, AKAP_KV_TRANSPORT=transport, AKAP_PD_GROUP="pd2",
+                           AKAP_PD_PAIR_BACKEND="gloo")
+                extra = ["--pd-bootstrap", "http", "--kv-store-port", str(_port())]
             procs.append(subprocess.Popen(
                 [sys.executable, "-m", "aws_k8s_ansible_provisioner_amd.server", *COMMON,
-                 "--kv-role", role, "--port", str(port), "--host", "127.0.0.1"],
+                 "--kv-role", role, "--port", str(port), "--host", "127.0.0.1", *extra],
                 env=env, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
             urls.append(f"http://127.0.0.1:{port}")
         deadline = time.time() + 240
@@ -68,7 +81,8 @@ def test_pd_through_the_gateway_on_gpu_matches_monolithic(transport):
         prompt = "disaggregated prefill and decode on one MI355X " * 3
 
         async def run():
-            gw = Gateway([(urls[0], "prefill"), (urls[1], "decode")], [],
+            g = "pd2" if bootstrap == "http" else ""
+            gw = Gateway([(urls[0], "prefill", g), (urls[1], "decode", g)], [],
                          PickerConfig(pd_threshold_chars=32), scrape_interval=0.2)
             runner = web.AppRunner(gw.app())
             await runner.setup()

@@ -30,7 +30,7 @@ if eng is not None:
     bc.shutdown()
     print("RESULT " + json.dumps([o.output_ids for o in outs]), flush=True)
 from aws_k8s_ansible_provisioner_amd.models.moe import MoEBlock
-print("FALLBACKS", MoEBlock.ep_fallbacks, flush=True)
+print("FALLBACKS", MoEBlock.ep_fallbacks, MoEBlock.ep_exact_layers, flush=True)
 """
 
 
@@ -72,9 +72,13 @@ def test_tp_matches_tp1(model, moe_mode, world, ep_fixed):
     assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
     line = [l for l in outs[0][0].splitlines() if l.startswith("RESULT ")][0]
     tp_out = json.loads(line[7:])
-    if "slack" in moe_mode:  # the undersized dispatch overflowed and fell back every time
-        fb = [l for l in outs[0][0].splitlines() if l.startswith("FALLBACKS ")][0]
-        assert int(fb.split()[1]) > 0, fb
+    fb = [l for l in outs[0][0].splitlines() if l.startswith("FALLBACKS ")][0].split()
+    if "slack" in moe_mode:  # the undersized dispatch overflowed: steps re-ran exactly
+        assert int(fb[1]) > 0, fb
+    elif moe_mode == "ep" and ep_fixed:
+        # prefill and decode steps alike on the fixed dispatch: no step re-run, no layer on
+        # the host-synced exact path
+        assert int(fb[1]) == 0 and int(fb[2]) == 0, fb
     ref = LLMEngine(EngineConfig(model=model, device="cpu", max_model_len=256, max_num_seqs=8,
                                  max_num_batched_tokens=32, block_size=32, num_gpu_blocks=96,
                                  shard_init="full", init_std=0.15), log=lambda *a: None)

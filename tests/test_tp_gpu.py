@@ -27,7 +27,8 @@ from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
 ecfg = EngineConfig(model=os.environ["MODEL"], device="cuda", max_model_len=256, max_num_seqs=8,
                     max_num_batched_tokens=64, block_size=32, num_gpu_blocks=96,
                     tensor_parallel_size=int(os.environ["WORLD_SIZE"]), shard_init="full",
-                    init_std=0.15, enforce_eager=os.environ["EAGER"] == "1")
+                    init_std=float(os.environ.get("INIT_STD", "0.15")),
+                    enforce_eager=os.environ["EAGER"] == "1")
 eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
 from aws_k8s_ansible_provisioner_amd.parallel.state import get_state
 assert (get_state().car is not None) == (os.environ["AKAP_CUSTOM_AR_GLOO"] == "1")
@@ -95,3 +96,40 @@ def test_tp2_on_one_gpu_matches_dense_reference(model, moe_mode, car, eager):
             gap = float((row.max() - row[t]) / (row.std() + 1e-6))
             assert gap <= 0.15, (p[:4], i, t, gap)
     assert [x[0] for x in got] == [y[0] for y in want]  # prefill's first tokens agree
+
+
+def test_tp4_llama70b_widths_captured_on_one_gpu():
+    """Llama-3-70B layer widths (d 8192, 64/8 heads, ffn 28672, 128k vocab; 4 layers) at TP=4
+    as 4 processes on one MI355X: captured decode graphs whose K13 all-reduces (with the fused
+    residual/norm epilogue), IPC broadcast and IPC logits all-gather run at the real per-rank
+    shard shapes; every token teacher-forced against the fp32 dense reference."""
+    from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+    from aws_k8s_ansible_provisioner_amd.engine.llm_engine import LLMEngine
+    from aws_k8s_ansible_provisioner_amd.models.reference_forward import dense_logits
+
+    model, world, std = "llama-3-70b-l4", 4, "0.02"
+    port = _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, ROOT=ROOT, MODEL=model, RANK=str(r), WORLD_SIZE=str(world),
+                   AKAP_MOE_MODE="tp", AKAP_CUSTOM_AR_GLOO="1", EAGER="0", INIT_STD=std,
+                   AKAP_GEMM_TUNE="0",
+                   LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", CHILD], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=420) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    got = json.loads([ln for ln in outs[0][0].splitlines() if ln.startswith("RESULT")][0][7:])
+    ref = LLMEngine(EngineConfig(model=model, device="cuda", max_model_len=256, max_num_seqs=8,
+                                 max_num_batched_tokens=64, block_size=32, num_gpu_blocks=96,
+                                 init_std=float(std), enforce_eager=True, shard_init="full"),
+                    log=lambda *a: None)
+    prompts = [list(range(5, 40)), [100, 101], [9, 9, 9]]
+    for p, toks in zip(prompts, got):
+        seq = list(p) + list(toks)
+        logits = dense_logits(ref.runner.model, seq).float().cpu()
+        for i, t in enumerate(toks):
+            row = logits[len(p) - 1 + i]
+            gap = float((row.max() - row[t]) / (row.std() + 1e-6))
+            assert gap <= 0.15, (p[:4], i, t, gap)
