@@ -3,7 +3,6 @@
 set -u
 O=gpurun_out/s5c; mkdir -p $O
 run() { n=$1; t=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.log 2>&1; rc=$?; echo "$n rc=$rc"; [ $rc -eq 0 ]; }
-run overlap 300 python -u tools/overlap_probe.py &&
 run samp_t 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "sampl or argmax" &&
 run samp_b 300 python -u tools/sample_bench.py &&
 run kvpull 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_custom_allreduce_gpu.py -k "kv_pull" &&
