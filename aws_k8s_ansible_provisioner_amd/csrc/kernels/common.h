@@ -86,8 +86,9 @@ __device__ __forceinline__ uint32_t hash3(uint64_t seed, uint32_t a, uint32_t b)
 }
 
 __device__ __forceinline__ float uniform01(uint64_t seed, uint32_t a, uint32_t b) {
-  // (0, 1] open at 0 so -log(u) is finite.
-  return ((hash3(seed, a, b) >> 8) + 1) * (1.0f / 16777216.0f);
+  // strictly inside (0, 1): -log(u) and -log(-log(u)) stay finite (u = 1 would make a Gumbel
+  // draw +inf, i.e. a uniformly random token once in 2^24 elements)
+  return ((float)(hash3(seed, a, b) >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
 // ---- paged K cache layout (D = 128) --------------------------------------------------

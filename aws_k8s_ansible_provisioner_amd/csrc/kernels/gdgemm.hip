@@ -29,12 +29,12 @@
 // Split-K (gridDim.y = S slices):
 //   SPL 1: fp32 partial slabs [S, M, N], reduced (with the epilogue) by dgemm.hip's reduce pass;
 //   SPL 2: in-launch combine.  Every slice stores its accumulators as a fragment-native slab
-//          (16 B per lane per MFMA tile, fully coalesced), then publishes with the counter form
-//          of the agent-scope release/acquire hand-off (cdna_hip_programming.md "Projection
-//          GEMM at M = 256" item 2 / Guideline 16): every wave `s_waitcnt vmcnt(0)` ->
-//          barrier -> lane 0 release fence -> asm vmcnt(0) -> relaxed agent fetch_add on the
-//          tile's ticket.  The slice that draws S-1 re-arms the ticket, acquires (one lane,
-//          then vmcnt(0) + barrier), sums the S slabs and runs the epilogue.  No second
+//          (16 B per lane per MFMA tile, fully coalesced) with write-through (sc1) stores, every
+//          wave drains (`s_waitcnt vmcnt(0)`), the workgroup barrier, then lane 0 takes an
+//          agent-scope ticket on the tile's counter (its own L2 line, kCtrStride) -- the sc1
+//          hand-off of MI355X_MICROARCH.md "Valid forms" (no release / acquire fence: each
+//          costs ~1.7 us and more behind a dirty L2).  The slice that draws S-1 re-arms the
+//          ticket and sums the S slabs with sc1 loads, then runs the epilogue.  No second
 //          launch, so the GEMM -> reduce kernel boundary (~1.5 us) and the reduce body go away,
 //          and split-K becomes legal for the SwiGLU epilogue too.
 #include <cstdlib>
@@ -45,6 +45,7 @@
 namespace akap {
 
 constexpr int GBK = 64;
+constexpr int kGdSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1-bypass loads)
 
 __device__ __forceinline__ int gswz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
@@ -233,41 +234,46 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   if constexpr (SPL == 2) {
     // ---- in-launch split-K combine (see header) ----
     constexpr int NF = MI * JN;  // f32x4 fragments per lane
-    f32x4* slabs = reinterpret_cast<f32x4*>(p.ws);
     const size_t tile_stride = (size_t)NF * NT;
-    f32x4* mine = slabs + ((size_t)kz * ntiles + lt) * tile_stride + tid;
+    const size_t zs = (size_t)ntiles * tile_stride;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        p.ws, (short)0, (int)((size_t)S * zs * 16), 0x00020000);
+    const size_t mine = ((size_t)kz * ntiles + lt) * tile_stride + tid;  // f32x4 units
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < JN; ++j) mine[(i * JN + j) * NT] = acc[i][j];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int j = 0; j < JN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                               (int)((mine + (size_t)(i * JN + j) * NT) * 16), 0,
+                                               kGdSc1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
     __syncthreads();
     int* flag = reinterpret_cast<int*>(&lds[NS * SU]);
+    int* ticket = p.counters + (size_t)lt * kCtrStride;
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int prev = __hip_atomic_fetch_add(p.counters + lt, 1, __ATOMIC_RELAXED,
+      const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == S - 1;
-      if (last) {
-        __hip_atomic_store(p.counters + lt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last;
     }
     __syncthreads();
     if (*flag == 0) return;
     // the combining block sums all S slabs (its own included: one code path, every load
-    // issued back to back -- no per-slice runtime condition around a load)
-    const f32x4* t0 = slabs + (size_t)lt * tile_stride + tid;
-    const size_t zs = (size_t)ntiles * tile_stride;
+    // issued back to back -- no per-slice runtime condition around a load); sc1 loads miss
+    // the (per-XCD, non-coherent) caches a slice on another XCD could not have written through
+    const size_t t0 = (size_t)lt * tile_stride + tid;
 #pragma unroll
-    for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] = t0[f * NT];
+    for (int f = 0; f < NF; ++f)
+      acc[f / JN][f % JN] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((t0 + f * NT) * 16), 0, kGdSc1));
 #pragma unroll
     for (int z = 1; z < S; ++z)
 #pragma unroll
-      for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] += t0[z * zs + f * NT];
+      for (int f = 0; f < NF; ++f)
+        acc[f / JN][f % JN] += __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((t0 + z * zs + f * NT) * 16),
+                                                         0, kGdSc1));
   }
 
   // epilogue: lane holds rows wm*WR + i*16 + fg*4 + r, column fr of each 16-col sub-tile

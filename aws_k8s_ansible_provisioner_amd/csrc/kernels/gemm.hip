@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     if (tid == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int old = __hip_atomic_fetch_add(&counters[lt], 1, __ATOMIC_RELAXED,
+      const int old = __hip_atomic_fetch_add(&counters[lt * kCtrStride], 1, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
       *flag = old == S - 1;
     }
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
       if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        counters[lt] = 0;
+        counters[lt * kCtrStride] = 0;
       }
       __syncthreads();
       // 64x64 tile, 256 threads: each thread 4 rows x 4 consecutive columns

@@ -7,6 +7,15 @@
 
 namespace akap {
 
+// Ints per in-launch ticket counter: each counter on its own 128-B L2 line.  Atomics (and the
+// relaxed polls of a spinning combine) on one line serialise at one L2 channel -- 1024 row
+// tickets packed 32 to a line cost the sampler ~18 us at B = 16 (tools/sample_bench.py, s5c).
+constexpr int kCtrStride = 32;
+// the shared GEMM counter array (ops.gemm_counters): its size and the combine-timeout flag
+constexpr int kCtrInts = 1 << 18;
+constexpr int kCtrErr = kCtrInts - 1;
+
+
 constexpr int kDecodeMaxPart = 8192;
 
 // ---- norm.hip ----

@@ -529,12 +529,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_sk_kernel(DGemmArgs p, in
     }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its stores
   __syncthreads();
-  int* arrive = p.counters + 2 * tile;
-  int* done = arrive + 1;
+  int* arrive = p.counters + 2 * tile * kCtrStride;  // arrivals (polled) and finishes: each
+  int* done = arrive + kCtrStride;                     // on its own L2 line
   if (tid == 0) {
     __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!pg_spin_ge(arrive, splits))
-      __hip_atomic_fetch_or(p.counters + 65535, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(p.counters + kCtrErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   // ---- combine rows [r0, r1) of the tile over every slab (sc1 loads) ----
@@ -591,7 +591,8 @@ bool pgemm_sk_supported(int M, int N, int K, int splits, int cus) {
   const int nk = K / PG_BK;
   const long grid = (long)((M + PG_T - 1) / PG_T) * (N / PG_T) * splits;
   return M > 0 && N % PG_T == 0 && K % PG_BK == 0 && splits >= 1 && splits <= 32 &&
-         nk >= splits && grid <= cus && (N / PG_T) * ((M + PG_T - 1) / PG_T) * 2 < 65535;
+         nk >= splits && grid <= cus &&
+         (N / PG_T) * ((M + PG_T - 1) / PG_T) * 2 * kCtrStride < kCtrErr;
 }
 
 long pgemm_sk_ws_floats(int M, int N, int splits) {

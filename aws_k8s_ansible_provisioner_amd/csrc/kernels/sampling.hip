@@ -57,14 +57,17 @@ __device__ __forceinline__ ArgBest block_argmax(ArgBest b, float* sv, int* si) {
 //    with 16-byte vector loads and produces, in that single pass,
 //      greedy rows   the chunk's argmax (first index on ties);
 //      T > 0 rows    the chunk's max and partition sum of z = x / T (online: rescaled when the
-//                    max moves), the key range, and -- for rows without top-k / top-p -- the
-//                    Gumbel-max draw z - log(-log u(seed, step, i)) over the chunk.
+//                    max moves) and, for rows with top-k / top-p, the key range.
 //    The chunk publishes a 32-byte partial record with write-through (sc1) stores and takes
 //    a ticket on the row's counter (MI355X_MICROARCH.md "Valid forms", sc1 table row 1: no
 //    release / acquire fence -- each costs ~1.7 us and more behind a freshly written logits
 //    tensor); the LAST chunk of the row reads the S records with sc1 loads, combines them
-//    (max, rescaled sum, best draw), writes the token + log-prob of a row without filters and
-//    the row summary (M, Z, key range) of a row with them, and re-arms the counter.
+//    (max, rescaled sum), re-arms the counter and writes the token + log-prob of a greedy row,
+//    or the row summary (M, Z, key range) of a row with filters; a row without filters is
+//    drawn there by inverse CDF: u(seed, step) * Z picks the chunk from the prefix of the
+//    chunk masses, then the workgroup rescans that one chunk (a block scan of per-thread run
+//    masses) for the token -- exact sampling with one exp per element in the main pass and
+//    no per-element RNG.
 // 2. sample_filter_kernel, grid = B: rows with top-k / top-p (the others return at once) find
 //    their thresholds by an adaptive radix select over the order-preserving key image -- by
 //    COUNT for top-k, by probability MASS for top-p on the top-k renormalised distribution:
@@ -79,8 +82,8 @@ constexpr int kSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1
 
 struct SampPart {  // one chunk's partial record (32 B = two 16-B vectors)
   float m, s;      // max of z over the chunk, sum of exp(z - m)
-  float g;         // best Gumbel value (rows without filters)
-  int gi;
+  float unused0;
+  int unused1;
   float am;        // argmax value (greedy rows)
   int ai;
   uint32_t kmin, kmax;  // key range of the chunk
@@ -150,19 +153,18 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   // branch on the row kind) ----
   float m = -INFINITY, sum = 0.f;
   uint32_t kmin = 0xffffffffu, kmax = 0u;
-  ArgBest best{-INFINITY, 0x7fffffff}, gb{-INFINITY, 0x7fffffff};
+  ArgBest best{-INFINITY, 0x7fffffff};
   if (!need_sum) {
     visit_range(x, lo, hi, vec_ok, [&](float v, int i) {
       if (v > best.v) { best.v = v; best.i = i; }  // ascending i per thread: first max kept
     });
   } else if (!greedy && !filt) {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int i) {
+    // max and partition sum only (one exp per element): the draw is an inverse-CDF pick by
+    // the last chunk below, so no per-element RNG / logs in this pass
+    visit_range(x, lo, hi, vec_ok, [&](float v, int) {
       const float z = v * invT;
       if (z > m) { sum = sum * __expf(m - z) + 1.f; m = z; }
       else if (z > -INFINITY) sum += __expf(z - m);
-      const float u = uniform01(seed, step, (uint32_t)i);
-      const float g = z - __logf(-__logf(u));
-      if (g > gb.v) { gb.v = g; gb.i = i; }
     });
   } else {  // greedy with log-probs, or a filtered row (also its key range)
     visit_range(x, lo, hi, vec_ok, [&](float v, int i) {
@@ -182,7 +184,6 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
     M = block_max(m, sv);
     Z = block_sum(m == -INFINITY ? 0.f : sum * __expf(m - M), sv);
   }
-  if (!greedy && !filt) gb = block_argmax(gb, sv, si);
   __shared__ uint32_t s_kmin, s_kmax;
   if (filt) {  // exact integer min / max of the keys
     if (threadIdx.x == 0) { s_kmin = 0xffffffffu; s_kmax = 0u; }
@@ -199,59 +200,127 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   if (threadIdx.x == 0) {
     u32x4 a, b2;
     a[0] = __float_as_uint(M); a[1] = __float_as_uint(Z);
-    a[2] = __float_as_uint(gb.v); a[3] = (uint32_t)gb.i;
+    a[2] = 0u; a[3] = 0u;
     b2[0] = __float_as_uint(best.v); b2[1] = (uint32_t)best.i; b2[2] = kmin; b2[3] = kmax;
     __builtin_amdgcn_raw_buffer_store_b128(a, rws, c * 32, 0, kSc1);
     __builtin_amdgcn_raw_buffer_store_b128(b2, rws, c * 32 + 16, 0, kSc1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(tickets + row, 1, __ATOMIC_RELAXED,
+    const int t = __hip_atomic_fetch_add(tickets + row * kCtrStride, 1, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     s_last = t == S - 1;
   }
   __syncthreads();
   if (!s_last) return;
   // ---- last chunk of the row: combine the S partials (S <= 64: wave 0, sc1 loads) ----
-  if (threadIdx.x >= 64) return;
-  const int l = threadIdx.x;
-  float rm = -INFINITY, rs = 0.f;
-  ArgBest a{-INFINITY, 0x7fffffff}, g{-INFINITY, 0x7fffffff};
-  uint32_t rkmin = 0xffffffffu, rkmax = 0u;
-  if (l < S) {
-    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32, 0, kSc1);
-    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32 + 16, 0, kSc1);
-    rm = __uint_as_float(v0[0]); rs = __uint_as_float(v0[1]);
-    g = ArgBest{__uint_as_float(v0[2]), (int)v0[3]};
-    a = ArgBest{__uint_as_float(v1[0]), (int)v1[1]};
-    rkmin = v1[2]; rkmax = v1[3];
-  }
-  const float Mr = wave_max(rm);
-  const float Zr = wave_sum(rm == -INFINITY ? 0.f : rs * __expf(rm - Mr));
+  const bool draw = !greedy && !filt;  // uniform over the workgroup
+  __shared__ float s_m, s_z, s_res;
+  __shared__ int s_chunk, s_tok, s_fb;
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    float rm = -INFINITY, rs = 0.f;
+    ArgBest a{-INFINITY, 0x7fffffff};
+    uint32_t rkmin = 0xffffffffu, rkmax = 0u;
+    if (l < S) {
+      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32, 0, kSc1);
+      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32 + 16, 0, kSc1);
+      rm = __uint_as_float(v0[0]); rs = __uint_as_float(v0[1]);
+      a = ArgBest{__uint_as_float(v1[0]), (int)v1[1]};
+      rkmin = v1[2]; rkmax = v1[3];
+    }
+    const float Mr = wave_max(rm);
+    // chunk l's mass in units of exp(z - Mr); its inclusive prefix over the chunks
+    const float w = rm == -INFINITY ? 0.f : rs * __expf(rm - Mr);
+    float incl = w;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    ArgBest ca{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
-    a = arg_better(a, ca);
-    ArgBest cg{__shfl_xor(g.v, o, 64), __shfl_xor(g.i, o, 64)};
-    g = arg_better(g, cg);
-    rkmin = min(rkmin, (uint32_t)__shfl_xor((int)rkmin, o, 64));
-    rkmax = max(rkmax, (uint32_t)__shfl_xor((int)rkmax, o, 64));
+    for (int o = 1; o < 64; o <<= 1) {
+      const float u = __shfl_up(incl, o, 64);
+      if (l >= o) incl += u;
+    }
+    const float Zr = __shfl(incl, 63, 64);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      ArgBest ca{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+      a = arg_better(a, ca);
+      rkmin = min(rkmin, (uint32_t)__shfl_xor((int)rkmin, o, 64));
+      rkmax = max(rkmax, (uint32_t)__shfl_xor((int)rkmax, o, 64));
+    }
+    if (draw) {
+      // inverse CDF, level 1: the chunk whose prefix mass first reaches u * Z
+      const float target = uniform01(seed, step, 0xffffffffu) * Zr;
+      const uint64_t hit = __ballot(incl >= target && w > 0.f);
+      const uint64_t live = __ballot(w > 0.f);
+      const int c_sel = hit ? __builtin_ctzll(hit) : 63 - __builtin_clzll(live);
+      if (l == c_sel) {
+        s_chunk = l;
+        s_res = hit ? target - (incl - w) : w;  // rounding past the end: the chunk's last mass
+      }
+      if (l == 0) {
+        s_m = Mr;
+        s_z = Zr;
+        s_tok = 0x7fffffff;
+        s_fb = -1;
+      }
+    }
+    if (l == 0) {
+      __hip_atomic_store(tickets + row * kCtrStride, 0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      if (greedy) {
+        p.out_tokens[row] = a.i;
+        // greedy log-prob: x[tok] is the max, so log softmax = -log sum exp(x - M)
+        if (p.out_logprobs) p.out_logprobs[row] = p.greedy_logprobs ? -__logf(Zr) : 0.f;
+      } else if (filt) {  // sample_filter_kernel finishes the row
+        float* r = rowsum + (size_t)row * 4;
+        r[0] = Mr;
+        r[1] = Zr;
+        r[2] = __uint_as_float(rkmin);
+        r[3] = __uint_as_float(rkmax);
+      }
+    }
   }
-  if (l != 0) return;
-  __hip_atomic_store(tickets + row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  if (greedy) {
-    p.out_tokens[row] = a.i;
-    // greedy log-prob: x[tok] is the max, so log softmax = -log sum exp(x - M)
-    if (p.out_logprobs) p.out_logprobs[row] = p.greedy_logprobs ? -__logf(Zr) : 0.f;
-  } else if (!filt) {
-    int tok = g.i;
+  if (!draw) return;
+  __syncthreads();
+  // ---- inverse CDF, level 2: rescan the selected chunk (just read by its workgroup, so in
+  // L2), each thread a contiguous run; block exclusive scan of the run masses; the thread
+  // whose run crosses the residual mass walks it to the token ----
+  const float Mr = s_m, R = s_res;
+  const int lo2 = min(V, s_chunk * chunk), hi2 = min(V, lo2 + chunk);
+  const int per = (hi2 - lo2 + kChunkThreads - 1) / kChunkThreads;
+  const int a0 = min(hi2, lo2 + (int)threadIdx.x * per), a1 = min(hi2, a0 + per);
+  float ts = 0.f;
+  int last_pos = -1;
+  for (int i = a0; i < a1; ++i) {
+    const float e = __expf((float)x[i] * invT - Mr);
+    ts += e;
+    if (e > 0.f) last_pos = i;
+  }
+  // exclusive scan of ts over the workgroup (waves scan, then the 4 wave totals)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float inc = ts;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) sv[wid] = inc;
+  __syncthreads();
+  float before = inc - ts;
+  for (int wv = 0; wv < wid; ++wv) before += sv[wv];
+  if (last_pos >= 0) atomicMax(&s_fb, last_pos);
+  if (ts > 0.f && R >= before && R < before + ts) {
+    float acc = before;
+    int tok = last_pos;
+    for (int i = a0; i < a1; ++i) {
+      acc += __expf((float)x[i] * invT - Mr);
+      if (acc > R) { tok = i; break; }
+    }
+    atomicMin(&s_tok, tok);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tok = s_tok != 0x7fffffff ? s_tok : s_fb;  // rounding past the chunk's end: last mass
     if (tok < 0 || tok >= V) tok = 0;
     p.out_tokens[row] = tok;
-    if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - Mr - __logf(Zr);
-  } else {  // sample_filter_kernel finishes the row
-    float* r = rowsum + (size_t)row * 4;
-    r[0] = Mr;
-    r[1] = Zr;
-    r[2] = __uint_as_float(rkmin);
-    r[3] = __uint_as_float(rkmax);
+    if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - Mr - __logf(s_z);
   }
 }
 

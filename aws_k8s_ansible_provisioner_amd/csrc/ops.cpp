@@ -292,8 +292,8 @@ void gemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t splitk,
   int* cnt = nullptr;
   if (counters && splitk > 1) {
     TORCH_CHECK(counters->scalar_type() == at::kInt && counters->is_cuda(), "counters int32");
-    TORCH_CHECK(counters->numel() >= (int64_t)((M + 63) / 64) * ((N + 63) / 64),
-                "counters: one per 64x64 tile");
+    TORCH_CHECK(counters->numel() >= (int64_t)((M + 63) / 64) * ((N + 63) / 64) * akap::kCtrStride,
+                "counters: one L2 line (kCtrStride ints) per 64x64 tile");
     cnt = counters->data_ptr<int>();
   }
   const c10::DeviceGuard g(x.device());
@@ -378,9 +378,10 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   if (counters && splitk > 1 && bn > 0) {
     // in-launch split-K combine: one zeroed int32 ticket per output tile
     TORCH_CHECK(counters->scalar_type() == at::kInt && counters->is_cuda() &&
-                    counters->numel() >= (sk ? 65536 : (int64_t)((M + bm - 1) / bm) *
-                                                           ((N + bn - 1) / bn)),
-                "dgemm: counters int32, one per output tile (bn=256: the 65536-int array)");
+                    counters->numel() >= (sk ? (int64_t)akap::kCtrInts
+                                             : (int64_t)((M + bm - 1) / bm) *
+                                                   ((N + bn - 1) / bn) * akap::kCtrStride),
+                "dgemm: counters int32, one L2 line per output tile (bn=256: the kCtrInts array)");
     a.counters = counters->data_ptr<int>();
   }
   if (pro == akap::PRO_ADDNORM) {
@@ -510,7 +511,8 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tenso
               "sampler workspace fp32, tickets int32");
   TORCH_CHECK(ws.numel() >= (int64_t)B * (64 * 8 + 4),
               "sampler workspace too small (B x 64 chunk records + B row summaries)");
-  TORCH_CHECK(tickets.numel() >= B, "one ticket per row");
+  TORCH_CHECK(tickets.numel() >= (int64_t)B * akap::kCtrStride,
+              "one ticket per row, each on its own L2 line (kCtrStride ints)");
   const c10::DeviceGuard g(logits.device());
   akap::launch_sample(p, B, ws.data_ptr(), tickets.data_ptr<int>(), cur_stream());
 }

@@ -643,6 +643,13 @@ class ModelRunner:
             self.log(f"[runner] GEMM tuning {time.time() - t1:.1f}s")
         self._stage_decode(self.max_seqs)
         torch.cuda.synchronize()
+        if self.ps.world_size > 1:
+            # the warm-up steps below run the custom IPC collectives, whose flag waits are
+            # bounded (~2 s): a rank still tuning its prefill GEMMs (rank-local, tens of seconds
+            # at 70B widths) would time them out on its peers -- meet first
+            import torch.distributed as dist
+
+            dist.barrier()
         self.graph_pool = torch.cuda.graph_pool_handle()
         stream = torch.cuda.Stream()
         for b in reversed(self.buckets):

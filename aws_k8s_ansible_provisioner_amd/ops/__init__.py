@@ -470,6 +470,9 @@ def gdgemm_ws_floats(M: int, N: int, splitk: int, bn: int, bm: int = 64) -> int:
 
 
 _COUNTERS: dict = {}
+CTR_STRIDE = 32  # ints per ticket counter: one 128-B L2 line each (csrc/kernels/common.h)
+GEMM_CTR_INTS = 1 << 18  # kCtrInts
+GEMM_CTR_ERR = GEMM_CTR_INTS - 1  # kCtrErr: an in-launch combine timed out
 
 
 def gemm_counters(device) -> torch.Tensor:
@@ -477,7 +480,7 @@ def gemm_counters(device) -> torch.Tensor:
     (launches on one stream are ordered; each tile's last arriver re-arms its counter)."""
     c = _COUNTERS.get(device)
     if c is None:
-        c = _COUNTERS[device] = torch.zeros(1 << 16, dtype=torch.int32, device=device)
+        c = _COUNTERS[device] = torch.zeros(GEMM_CTR_INTS, dtype=torch.int32, device=device)
     return c
 
 
@@ -506,12 +509,12 @@ def _sample_ws(device, B: int):
     chunk re-arms its ticket in the kernel).  Grown, never
     shrunk: a decode hipGraph keeps the addresses it was captured with."""
     cur = _SAMPLE_WS.get(device)
-    if cur is None or cur[1].numel() < B:
+    if cur is None or cur[1].numel() < B * CTR_STRIDE:
         if cur is not None:
             _SAMPLE_OLD.append(cur)
         n = max(B, 256)
         cur = (torch.zeros(n * (SAMPLE_MAX_CHUNKS * 8 + 4), dtype=torch.float32, device=device),
-               torch.zeros(n, dtype=torch.int32, device=device))
+               torch.zeros(n * CTR_STRIDE, dtype=torch.int32, device=device))
         _SAMPLE_WS[device] = cur
     return cur
 

@@ -780,7 +780,8 @@ def test_pgemm_split_k_inlaunch(epi, M, N, K, splitk):
         out = ops.dgemm(x, w, epi=epi, ss_in=ssi, eps=eps, **kw)
         want = ref.silu_and_mul(y.to(torch.bfloat16)).float()
         _close(out, want, atol=2e-2 * want.abs().max().item())
-    assert int(ops.gemm_counters(torch.device(DEV))[65535].item()) == 0  # no combine timed out
+    # no combine timed out
+    assert int(ops.gemm_counters(torch.device(DEV))[ops.GEMM_CTR_ERR].item()) == 0
 
 
 @pytest.mark.parametrize("M", [1, 16, 37, 64, 100, 128, 200, 256, 300])

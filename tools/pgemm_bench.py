@@ -27,6 +27,11 @@ DENSE = [  # (name, M, N, K)
     ("llama3-8b gate_up", 8192, 28672, 4096),
     ("llama3-8b down", 8192, 4096, 14336),
     ("qkv M=2048", 2048, 6144, 4096),
+    # the headline model's prefill projections at a 16384-token chunk (Qwen3-0.6B)
+    ("qwen3-0.6b qkv", 16384, 4096, 1024),
+    ("qwen3-0.6b o", 16384, 1024, 2048),
+    ("qwen3-0.6b gate_up", 16384, 6144, 1024),
+    ("qwen3-0.6b down", 16384, 1024, 3072),
     ("gate_up M=16384", 16384, 24576, 4096),
 ]
 GROUPED = [  # (name, rows, experts, N, K)
