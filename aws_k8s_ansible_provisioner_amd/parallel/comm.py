@@ -137,6 +137,21 @@ def tp_all_gather_rows(out: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     if st.car is not None and st.car.gather_ok(flat) and out.is_contiguous():
         st.car.all_gather(flat, out.view(1, -1))
         return out
+    if (st.car is not None and st.backend == "gloo" and x.dim() == 2 and out.is_contiguous()
+            and _car_pieces_ok(x.contiguous(), st.car) and x.shape[1] % 8 == 0):
+        # ranks sharing one GPU over a gloo control plane (single-GPU rehearsal of an EP x TP
+        # prefill): row slabs through the IPC all-gather instead of a host-staged gloo gather
+        W, (per, d) = st.tp_size, x.shape
+        rows = max(1, st.car.buffer_bytes // (2 * d))  # the staged shard fits the buffer
+        xc, dst = x.contiguous(), out.view(W, per, d)
+        for r0 in range(0, per, rows):
+            r1 = min(per, r0 + rows)
+            piece = xc[r0:r1].reshape(1, -1)
+            tmp = torch.empty(1, W * piece.numel(), dtype=x.dtype, device=x.device)
+            st.car.all_gather(piece, tmp)
+            dst[:, r0:r1].copy_(tmp.view(W, r1 - r0, d))
+        _UNCHECKED[0] = True
+        return out
     dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
     return out
 
