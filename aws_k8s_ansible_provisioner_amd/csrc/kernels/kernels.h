@@ -184,7 +184,10 @@ struct SampleParams {
 // grid (sample_chunks(B, V) chunks, B rows); ws >= B * kMaxChunks * 32 bytes of partials,
 // tickets[B] int32 zeroed once (each row's last chunk re-arms its ticket)
 int sample_chunks(int B, int V);
-void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, hipStream_t s);
+long sample_ws_floats(int B);  // partial records + filter-pass states and histograms
+// filtered = 0: the caller guarantees no row has top-k / top-p (their passes are not launched)
+void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int filtered,
+                   hipStream_t s);
 // OpenAI/vLLM penalties on logits in place, for unique (row, token) entries:
 // repetition (prompt + output tokens, divide positive / multiply negative logits),
 // frequency * count and presence * [count > 0] (output tokens; count 0 = prompt-only)

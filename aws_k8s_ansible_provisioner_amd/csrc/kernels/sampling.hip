@@ -79,6 +79,10 @@ constexpr int kChunkThreads = 256;
 constexpr int kMaxChunks = 64;
 constexpr int kFilterThreads = 256;
 constexpr int kSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1-bypass loads)
+constexpr int kSelWords = 16;  // per-row state of the filter passes (32-bit words)
+// per-row histogram area of the filter passes, in float2: kMaxChunks x 256 (count, mass)
+// pairs, then pass A's 256 high-byte masses
+constexpr int kHistRow = kMaxChunks * 256 + 128;
 
 struct SampPart {  // one chunk's partial record (32 B = two 16-B vectors)
   float m, s;      // max of z over the chunk, sum of exp(z - m)
@@ -269,53 +273,61 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
         // greedy log-prob: x[tok] is the max, so log softmax = -log sum exp(x - M)
         if (p.out_logprobs) p.out_logprobs[row] = p.greedy_logprobs ? -__logf(Zr) : 0.f;
       } else if (filt) {  // sample_filter_kernel finishes the row
-        float* r = rowsum + (size_t)row * 4;
+        float* r = rowsum + (size_t)row * kSelWords;  // the passes' SelState: M, Z
         r[0] = Mr;
         r[1] = Zr;
-        r[2] = __uint_as_float(rkmin);
-        r[3] = __uint_as_float(rkmax);
       }
     }
   }
   if (!draw) return;
   __syncthreads();
   // ---- inverse CDF, level 2: rescan the selected chunk (just read by its workgroup, so in
-  // L2), each thread a contiguous run; block exclusive scan of the run masses; the thread
-  // whose run crosses the residual mass walks it to the token ----
-  const float Mr = s_m, R = s_res;
+  // L2) in coalesced tiles of 8 elements per thread; a block scan of the per-thread masses
+  // finds the thread whose 8 elements cross the residual mass, which walks them ----
+  const float Mr = s_m;
+  float R = s_res;
   const int lo2 = min(V, s_chunk * chunk), hi2 = min(V, lo2 + chunk);
-  const int per = (hi2 - lo2 + kChunkThreads - 1) / kChunkThreads;
-  const int a0 = min(hi2, lo2 + (int)threadIdx.x * per), a1 = min(hi2, a0 + per);
-  float ts = 0.f;
-  int last_pos = -1;
-  for (int i = a0; i < a1; ++i) {
-    const float e = __expf((float)x[i] * invT - Mr);
-    ts += e;
-    if (e > 0.f) last_pos = i;
-  }
-  // exclusive scan of ts over the workgroup (waves scan, then the 4 wave totals)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float inc = ts;
+  constexpr int TILE = kChunkThreads * 8;
+  for (int t0 = lo2; t0 < hi2; t0 += TILE) {
+    const int a0 = t0 + (int)threadIdx.x * 8, a1 = min(hi2, a0 + 8);
+    float e[8];
+    float ts = 0.f;
+    int last_pos = -1;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float u = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += u;
-  }
-  if (lane == 63) sv[wid] = inc;
-  __syncthreads();
-  float before = inc - ts;
-  for (int wv = 0; wv < wid; ++wv) before += sv[wv];
-  if (last_pos >= 0) atomicMax(&s_fb, last_pos);
-  if (ts > 0.f && R >= before && R < before + ts) {
-    float acc = before;
-    int tok = last_pos;
-    for (int i = a0; i < a1; ++i) {
-      acc += __expf((float)x[i] * invT - Mr);
-      if (acc > R) { tok = i; break; }
+    for (int j = 0; j < 8; ++j) {
+      e[j] = a0 + j < a1 ? __expf((float)x[a0 + j] * invT - Mr) : 0.f;
+      ts += e[j];
+      if (e[j] > 0.f) last_pos = a0 + j;
     }
-    atomicMin(&s_tok, tok);
+    float inc = ts;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) sv[wid] = inc;
+    __syncthreads();
+    float before = inc - ts, total = 0.f;
+    for (int wv = 0; wv < kChunkThreads / 64; ++wv) {
+      if (wv < wid) before += sv[wv];
+      total += sv[wv];
+    }
+    if (last_pos >= 0) atomicMax(&s_fb, last_pos);
+    if (ts > 0.f && R >= before && R < before + ts) {
+      float acc = before;
+      int tok = last_pos;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc += e[j];
+        if (acc > R) { tok = a0 + j; break; }
+      }
+      atomicMin(&s_tok, tok);
+    }
+    __syncthreads();
+    if (s_tok != 0x7fffffff) break;  // uniform: found in this tile
+    R -= total;
   }
-  __syncthreads();
   if (threadIdx.x == 0) {
     int tok = s_tok != 0x7fffffff ? s_tok : s_fb;  // rounding past the chunk's end: last mass
     if (tok < 0 || tok >= V) tok = 0;
@@ -324,154 +336,312 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   }
 }
 
-// Largest key tau in [floor_key, kmax] with sum_{key >= tau} w >= target, w = 1 (MASS=false)
-// or exp(x/T - M) (MASS=true); returns floor_key when the whole interval holds less.
-template <bool MASS, typename T>
-__device__ uint32_t adaptive_select(const T* x, int V, bool vec_ok, uint32_t floor_key,
-                                    uint32_t kmax, float target, float M, float invT,
-                                    float* hist /* [256][64] */, uint32_t* s_u, float* s_f) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  uint32_t lo = floor_key, hi = kmax;
-  float remaining = target;
-  while (hi > lo) {
-    const uint64_t range = (uint64_t)hi - lo + 1;
-    int sh = 0;
-    while ((range + ((1ull << sh) - 1)) >> sh > 256) ++sh;  // bins of width 2^sh, <= 256 bins
-    for (int i = tid; i < 256 * 64; i += blockDim.x) hist[i] = 0.f;
-    __syncthreads();
-    const uint32_t lo_ = lo, hi_ = hi;
-    visit_range(x, 0, V, vec_ok, [&](float v, int) {
-      const uint32_t k = fkey(v);
-      if (k < lo_ || k > hi_) return;
-      const int b = (int)((k - lo_) >> sh);
-      atomicAdd(&hist[b * 64 + lane], MASS ? __expf(v * invT - M) : 1.f);
-    });
-    __syncthreads();
-    // per-bin totals over the 64 copies (rotated reads: conflict-free), then one wave scans
-    float* tot = hist;  // reused in place below after a barrier
-    float bsum = 0.f;
-    {
-      const int b = tid;  // blockDim == 256 bins
-#pragma unroll 8
-      for (int j = 0; j < 64; ++j) bsum += hist[b * 64 + ((j + lane) & 63)];
-    }
-    __syncthreads();
-    tot[tid] = bsum;
-    __syncthreads();
-    if (tid < 64) {
-      float c[4], loc = 0.f;
+// ---------------------------------------------------------------------------------------
+// Rows with top-k / top-p: exact thresholds on the 16-bit order-preserving key of the logit
+// (k16 = fkey(x) >> 16: exact for bf16 logits, the top 16 bits of an fp32 logit), found by two
+// 256-bin histogram levels -- the key's high byte, then its low byte inside the selected
+// high-byte bin -- each pass spread over the row's S chunk workgroups like the chunk kernel:
+// per-wave LDS histograms, 256 (count, mass) pairs published per chunk with sc1 stores, a
+// ticket, and the row's last chunk sums the S histograms and selects (masses are
+// exp(x / T - M) with the row max M of the chunk kernel, so they add across chunks).
+//   pass A  high-byte histogram of the whole row -> top-k's high byte (by count) or, for a
+//           top-p-only row, top-p's high byte (by mass);
+//   pass B  low-byte histogram inside that bin -> the exact top-k key (and Zk, the top-k mass)
+//           or the exact top-p key; top-k + top-p: top-p over the top-k set, whose crossing is
+//           either inside top-k's bin (exact now) or in a higher high-byte bin (pass C);
+//   pass C  low-byte mass histogram of that higher bin -> the exact top-p key;
+//   pass D  Gumbel-max draw over {k16 >= tau} (RNG only for survivors), best per chunk, the
+//           last chunk picks the row's token.
+// Every pass reads the row once in parallel (from L2 / MALL after the chunk kernel); rows
+// without filters leave every pass at once, and a batch with no filtered row launches none
+// of them (ops.sample(filtered=False)).
+// state words: 0 M, 1 Z, 2 flags (1 top-k, 2 top-p), 3 sel_hi (pass B bin), 4 cnt_above,
+// 5 mass_above, 6 tau (final key threshold, or -1 pending), 7 Zk, 8 p_hi (pass C bin or -1),
+// 9 p_above (mass strictly above p_hi's bin inside the top-k set), 10 p_target
+struct SelState {
+  float M, Z;
+  int flags, sel_hi;
+  float cnt_above, mass_above;
+  int tau;
+  float Zk;
+  int p_hi;
+  float p_above, p_target;
+  int pad[5];
+};
+static_assert(sizeof(SelState) == kSelWords * 4, "SelState layout");
+
+__device__ __forceinline__ int k16_of(float v) { return (int)(fkey(v) >> 16); }
+
+// this chunk's (count, mass) histogram over 256 bins of elements `sel` maps to a bin (or -1),
+// published to hist[row][c] as 256 float2 (sc1); returns true in the row's last chunk, whose
+// threads then hold bin tid's row totals (cnt, mass)
+template <typename T, typename SEL>
+__device__ __forceinline__ bool hist_pass(const T* x, int lo, int hi, bool vec_ok, float invT,
+                                          float M, float* whist /* [4][2][256] LDS */,
+                                          float2* hist_row, int S, int c, int* ticket,
+                                          float& cnt, float& mass, SEL&& sel) {
+  const int tid = threadIdx.x, wid = tid >> 6;
+  __shared__ int s_last;
+  for (int i = tid; i < 4 * 512; i += kChunkThreads) whist[i] = 0.f;
+  __syncthreads();
+  float* wc = whist + wid * 512;
+  visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+    const int b = sel(v);
+    if (b < 0) return;
+    atomicAdd(&wc[b], 1.f);
+    atomicAdd(&wc[256 + b], __expf(v * invT - M));
+  });
+  __syncthreads();
+  float cc = 0.f, mm = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        c[j] = tot[255 - 4 * lane - j];
-        loc += c[j];
-      }
-      float incl = loc;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const float u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += u;
-      }
-      const float before = incl - loc;
-      const uint64_t ball = __ballot(before + loc >= remaining);
-      const int first = ball ? __builtin_ctzll(ball) : 64;
-      if (first == 64) {  // the interval holds less than the target: take all of it
-        if (lane == 0) { s_u[0] = 0xffffffffu; s_f[0] = remaining; }
-      } else if (lane == first) {
-        float cum = before;
-        int sel = 252 - 4 * lane;
-        for (int j = 0; j < 4; ++j) {
-          sel = 255 - 4 * lane - j;
-          if (cum + c[j] >= remaining) break;
-          cum += c[j];
-        }
-        s_u[0] = (uint32_t)sel;
-        s_f[0] = remaining - cum;
-      }
-    }
-    __syncthreads();
-    const uint32_t sel = s_u[0];
-    remaining = s_f[0];
-    __syncthreads();
-    if (sel == 0xffffffffu) return lo;
-    lo = lo + (sel << sh);
-    const uint64_t top = (uint64_t)lo + (1ull << sh) - 1;
-    hi = top < hi ? (uint32_t)top : hi;
+  for (int w = 0; w < 4; ++w) {
+    cc += whist[w * 512 + tid];
+    mm += whist[w * 512 + 256 + tid];
   }
-  return lo;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)hist_row, (short)0, (int)(S * 256 * 8), 0x00020000);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 v2;
+  v2[0] = __float_as_uint(cc);
+  v2[1] = __float_as_uint(mm);
+  __builtin_amdgcn_raw_buffer_store_b64(v2, rh, (c * 256 + tid) * 8, 0, kSc1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == S - 1;
+    if (s_last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return false;
+  cnt = 0.f;
+  mass = 0.f;
+  for (int q = 0; q < S; ++q) {
+    const u32x2 r = __builtin_amdgcn_raw_buffer_load_b64(rh, (q * 256 + tid) * 8, 0, kSc1);
+    cnt += __uint_as_float(r[0]);
+    mass += __uint_as_float(r[1]);
+  }
+  return true;
+}
+
+// v = this thread's bin value (bin = threadIdx.x, v >= 0).  Returns the highest bin b with
+// sum_{bins >= b} v >= target (bin 0 when even the whole sum stays below; target > 0), and
+// sum_{bins > b} v in *above_out.  Every thread calls it (barriers inside).
+__device__ __forceinline__ int suffix_select(float v, float target, float* scratch,
+                                             float* above_out) {
+  __shared__ float s_v[256];
+  __shared__ int s_pos;
+  __shared__ float s_above;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __syncthreads();  // a previous call's readers are done with s_pos / s_above
+  s_v[255 - tid] = v;  // position r holds bin 255 - r: a prefix over positions = a suffix
+  if (tid == 0) { s_pos = 255; s_above = 0.f; }
+  __syncthreads();
+  const float mine = s_v[tid];
+  float inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) scratch[wid] = inc;
+  __syncthreads();
+  float before = inc - mine;
+  for (int w = 0; w < wid; ++w) before += scratch[w];
+  // the unique first position whose inclusive prefix reaches the target (prefixes only grow)
+  if (before < target && before + mine >= target) { s_pos = tid; s_above = before; }
+  // none reaches it (rounding): bin 0, everything above it
+  if (tid == 255 && before + mine < target) s_above = before;
+  __syncthreads();
+  *above_out = s_above;
+  return 255 - s_pos;
 }
 
 template <typename T>
-__global__ __launch_bounds__(kFilterThreads) void sample_filter_kernel(SampleParams p,
-                                                                       const float* rowsum) {
-  __shared__ float hist[256 * 64];
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  __shared__ uint32_t s_u[1];
-  __shared__ float s_f[1];
-  const int row = blockIdx.x;
+__global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams p, int pass,
+                                                                    SelState* st, float2* hist,
+                                                                    int* tickets) {
+  __shared__ float whist[4 * 512];
+  __shared__ float scratch[16];
+  const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
   const float temp = p.temperature ? p.temperature[row] : 0.f;
-  if (!row_filtered(p, row, temp)) return;  // uniform: the whole workgroup leaves
+  if (!row_filtered(p, row, temp)) return;  // uniform
+  SelState& rs = st[row];
   const T* x = reinterpret_cast<const T*>(p.logits) + (size_t)row * p.ld;
   const int V = p.V;
   const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  constexpr int NV = Vec<T>::N;
+  const int chunk = ((V + S - 1) / S + NV - 1) / NV * NV;
+  const int lo = min(V, c * chunk), hi = min(V, lo + chunk);
   const float invT = 1.f / temp;
-  const float M = rowsum[row * 4], Z = rowsum[row * 4 + 1];
-  const uint32_t kmin = __float_as_uint(rowsum[row * 4 + 2]);
-  const uint32_t kmax = __float_as_uint(rowsum[row * 4 + 3]);
-  const int k = p.top_k ? p.top_k[row] : 0;
+  const float M = rs.M;
+  int* ticket = tickets + row * kCtrStride;
+  float2* hrow = hist + (size_t)row * kHistRow;
+  float* hmass = reinterpret_cast<float*>(hrow + kMaxChunks * 256);  // pass A's bin masses
+  const int tid = threadIdx.x;
+  const int kk = p.top_k ? p.top_k[row] : 0;
   const float tp = p.top_p ? p.top_p[row] : 1.f;
-  uint32_t thr = kmin;
-  float Zk = Z;
-  if (k > 0 && k < V) {
-    thr = adaptive_select<false>(x, V, vec_ok, kmin, kmax, (float)k, M, invT, hist, s_u, s_f);
-    if (tp < 1.f) {
-      float zk = 0.f;
-      visit_range(x, 0, V, vec_ok, [&](float v, int) {
-        if (fkey(v) >= thr) zk += __expf(v * invT - M);
-      });
-      Zk = block_sum(zk, sv);
+  const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
+  float cnt = 0.f, mass = 0.f;
+  if (pass == 0) {  // A: high byte of the whole row
+    if (!hist_pass(x, lo, hi, vec_ok, invT, M, whist, hrow, S, c, ticket, cnt, mass,
+                   [](float v) { return k16_of(v) >> 8; }))
+      return;
+    float above;
+    int b;
+    if (has_k) {
+      b = suffix_select(cnt, (float)kk, scratch, &above);
+      float mabove;
+      // the mass above the selected bin (suffix of masses over bins > b)
+      const float mm = tid > b ? mass : 0.f;
+      mabove = block_sum(mm, scratch);
+      if (tid == 0) {
+        rs.sel_hi = b;
+        rs.cnt_above = above;
+        rs.mass_above = mabove;
+      }
+    } else {
+      b = suffix_select(mass, tp * rs.Z, scratch, &above);
+      if (tid == 0) {
+        rs.sel_hi = b;
+        rs.mass_above = above;
+        rs.p_target = tp * rs.Z;
+      }
     }
+    // keep the row's high-byte masses for pass B's top-p-over-top-k step
+    hmass[tid] = mass;
+    if (tid == 0) { rs.tau = -1; rs.p_hi = -1; }
+    return;
   }
-  if (tp < 1.f && tp > 0.f)
-    thr = adaptive_select<true>(x, V, vec_ok, thr, kmax, tp * Zk, M, invT, hist, s_u, s_f);
-  // Gumbel-max draw over {key >= thr}
+  if (pass == 1) {  // B: low byte inside sel_hi
+    const int sh = rs.sel_hi;
+    if (!hist_pass(x, lo, hi, vec_ok, invT, M, whist, hrow, S, c, ticket, cnt, mass,
+                   [sh](float v) { const int k = k16_of(v); return (k >> 8) == sh ? (k & 255) : -1; }))
+      return;
+    float above;
+    if (has_k) {
+      const int b = suffix_select(cnt, (float)kk - rs.cnt_above, scratch, &above);
+      const int tau_k = (sh << 8) | b;
+      const float mm = tid >= b ? mass : 0.f;
+      const float Zk = rs.mass_above + block_sum(mm, scratch);
+      if (!has_p) {
+        if (tid == 0) { rs.tau = tau_k; rs.Zk = Zk; }
+        return;
+      }
+      // top-p over the top-k set: masses of the high-byte bins above sh (pass A), then the low
+      // bins >= b of sh
+      const float target = tp * Zk;
+      const float hm = tid > sh ? hmass[tid] : 0.f;
+      float habove;
+      const int hb = suffix_select(hm, target, scratch, &habove);
+      const float hsum = block_sum(hm, scratch);
+      if (hsum >= target && hb > sh) {  // crossing in a higher bin: pass C resolves it
+        if (tid == 0) { rs.p_hi = hb; rs.p_above = habove; rs.p_target = target; rs.tau = tau_k; }
+        return;
+      }
+      float lab;
+      const int lb = suffix_select(tid >= b ? mass : 0.f, target - hsum, scratch, &lab);
+      if (tid == 0) { rs.tau = max(tau_k, (sh << 8) | lb); rs.Zk = Zk; }
+      return;
+    }
+    // top-p only
+    const int b = suffix_select(mass, rs.p_target - rs.mass_above, scratch, &above);
+    if (tid == 0) rs.tau = (sh << 8) | b;
+    return;
+  }
+  if (pass == 2) {  // C: low-byte masses inside p_hi (top-k + top-p rows crossing above sh)
+    const int ph = rs.p_hi;
+    if (ph < 0) return;  // uniform per row
+    if (!hist_pass(x, lo, hi, vec_ok, invT, M, whist, hrow, S, c, ticket, cnt, mass,
+                   [ph](float v) { const int k = k16_of(v); return (k >> 8) == ph ? (k & 255) : -1; }))
+      return;
+    float above;
+    const int b = suffix_select(mass, rs.p_target - rs.p_above, scratch, &above);
+    if (tid == 0) { rs.tau = (ph << 8) | b; rs.p_hi = -1; }
+    return;
+  }
+  // D: Gumbel-max draw over the survivors
+  const int tau = rs.tau;
   const uint64_t seed = p.seeds ? (uint64_t)p.seeds[row] : 0x1234ull + row;
   const uint32_t step = p.steps ? (uint32_t)p.steps[row] : 0u;
   ArgBest b{-INFINITY, 0x7fffffff};
-  visit_range(x, 0, V, vec_ok, [&](float v, int i) {
-    if (fkey(v) < thr) return;
+  visit_range(x, lo, hi, vec_ok, [&](float v, int i) {
+    if (k16_of(v) < tau) return;
     const float u = uniform01(seed, step, (uint32_t)i);
     const float g = v * invT - __logf(-__logf(u));
     if (g > b.v) { b.v = g; b.i = i; }
   });
+  __shared__ float sv[16];
+  __shared__ int si[16];
   b = block_argmax(b, sv, si);
-  if (threadIdx.x == 0) {
-    int tok = b.i;
+  __shared__ int s_last;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)hrow, (short)0, (int)(S * 8), 0x00020000);
+  if (tid == 0) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 v2;
+    v2[0] = __float_as_uint(b.v);
+    v2[1] = (uint32_t)b.i;
+    __builtin_amdgcn_raw_buffer_store_b64(v2, rh, c * 8, 0, kSc1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == S - 1;
+    if (s_last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last || tid >= 64) return;
+  ArgBest a{-INFINITY, 0x7fffffff};
+  if (tid < S) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 r = __builtin_amdgcn_raw_buffer_load_b64(rh, tid * 8, 0, kSc1);
+    a = ArgBest{__uint_as_float(r[0]), (int)r[1]};
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgBest ca{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+    a = arg_better(a, ca);
+  }
+  if (tid == 0) {
+    int tok = a.i;
     if (tok < 0 || tok >= V) tok = 0;
     p.out_tokens[row] = tok;
-    if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - M - __logf(Z);
+    if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - M - __logf(rs.Z);
   }
 }
 
 int sample_chunks(int B, int V) {
-  // ~2k workgroups over the batch, chunks of >= 2k elements, at most kMaxChunks per row
+  // >= ~2k workgroups over the batch, chunks of >= 2k elements, and chunks of <= 4k elements
+  // (the inverse-CDF draw rescans one chunk per row), at most kMaxChunks per row
   int S = (2048 + B - 1) / max(B, 1);
   S = min(S, max(1, V / 2048));
+  S = max(S, (V + 4095) / 4096);
   return max(1, min(S, kMaxChunks));
 }
 
-void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, hipStream_t s) {
+long sample_ws_floats(int B) {
+  // partial records, selection states, per-row histograms (kMaxChunks x 256 float2; the
+  // last 256 floats keep pass A's high-byte masses)
+  return (long)B * (kMaxChunks * 8 + kSelWords + 2 * kHistRow);
+}
+
+void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int filtered,
+                   hipStream_t s) {
   if (B == 0) return;
   const dim3 grid(sample_chunks(B, p.V), B);
-  // workspace: [B][kMaxChunks] partial records, then [B][4] row summaries
   SampPart* parts = (SampPart*)ws;
-  float* rowsum = reinterpret_cast<float*>(parts + (size_t)B * kMaxChunks);
+  SelState* st = reinterpret_cast<SelState*>(parts + (size_t)B * kMaxChunks);
+  float2* hist = reinterpret_cast<float2*>(st + B);
+  float* rowsum = reinterpret_cast<float*>(st);
   if (p.is_bf16) {
     sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum);
-    sample_filter_kernel<bf16><<<B, kFilterThreads, 0, s>>>(p, rowsum);
+    if (filtered)
+      for (int ps = 0; ps < 4; ++ps)
+        sample_pass_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
   } else {
     sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum);
-    sample_filter_kernel<float><<<B, kFilterThreads, 0, s>>>(p, rowsum);
+    if (filtered)
+      for (int ps = 0; ps < 4; ++ps)
+        sample_pass_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
   }
 }
 

@@ -481,7 +481,7 @@ bool dgemm_ok(int64_t M, int64_t N, int64_t K, int64_t splitk, int64_t pf) {
 
 void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
             Tensor steps, Tensor out_tokens, Tensor out_logprobs, bool greedy_logprobs,
-            Tensor ws, Tensor tickets) {
+            Tensor ws, Tensor tickets, bool filtered) {
   CHECK_GPU(logits);
   TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16,
               "sampler expects fp32 or bf16 logits");
@@ -509,12 +509,13 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tenso
   CHECK_GPU(ws); CHECK_CONTIG(ws); CHECK_GPU(tickets); CHECK_CONTIG(tickets);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && tickets.scalar_type() == at::kInt,
               "sampler workspace fp32, tickets int32");
-  TORCH_CHECK(ws.numel() >= (int64_t)B * (64 * 8 + 4),
-              "sampler workspace too small (B x 64 chunk records + B row summaries)");
+  TORCH_CHECK(ws.numel() >= (int64_t)akap::sample_ws_floats(B),
+              "sampler workspace too small (chunk records + filter-pass states / histograms)");
   TORCH_CHECK(tickets.numel() >= (int64_t)B * akap::kCtrStride,
               "one ticket per row, each on its own L2 line (kCtrStride ints)");
   const c10::DeviceGuard g(logits.device());
-  akap::launch_sample(p, B, ws.data_ptr(), tickets.data_ptr<int>(), cur_stream());
+  akap::launch_sample(p, B, ws.data_ptr(), tickets.data_ptr<int>(), filtered ? 1 : 0,
+                      cur_stream());
 }
 
 void apply_penalties(Tensor logits, Tensor rows, Tensor toks, Tensor counts, Tensor presence,
@@ -1161,7 +1162,7 @@ TORCH_LIBRARY(akap, m) {
   m.def(
       "sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
       "Tensor steps, Tensor(a!) out_tokens, Tensor(b!) out_logprobs, "
-      "bool greedy_logprobs, Tensor(c!) ws, Tensor(d!) tickets) -> ()");
+      "bool greedy_logprobs, Tensor(c!) ws, Tensor(d!) tickets, bool filtered=True) -> ()");
   m.def(
       "apply_penalties(Tensor(a!) logits, Tensor rows, Tensor toks, Tensor counts, "
       "Tensor presence, Tensor frequency, Tensor repetition) -> ()");

@@ -113,6 +113,11 @@ class ModelRunner:
         # top-N alternatives of the last step's sampled rows: (token ids [n, N], log-probs)
         self.last_top: Optional[tuple] = None
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        # decode graphs whose sampler also runs the top-k / top-p threshold passes: captured on
+        # first use by a batch that needs them (single-rank engines; multi-rank engines capture
+        # their only graphs with the passes, since a lazy capture would issue collectives alone)
+        self.graphs_f: dict[int, torch.cuda.CUDAGraph] = {}
+        self._capture_filtered: Optional[bool] = None
         self.ep_overflow_steps = 0  # steps re-run after an EP dispatch overflow
         self.graph_pool = None
         self.buckets: list[int] = []
@@ -296,7 +301,41 @@ class ModelRunner:
         return ops.sample(logits, d["temperature"][:n], d["top_k"][:n],
                           d["top_p"][:n], d["seeds"][:n], d["steps"][:n],
                           out_tokens=self.out_tokens[:n], out_logprobs=self.out_logprobs[:n],
-                          greedy_logprobs=lp)
+                          greedy_logprobs=lp, filtered=self._host_filtered(n))
+
+    def _host_filtered(self, n: int) -> bool:
+        """Does any of the step's n sampled rows use top-k / top-p?  (From the host staging
+        arrays; inside a capture, the variant being captured.)"""
+        if self._capture_filtered is not None:
+            return self._capture_filtered
+        if not self.is_gpu:
+            return True
+        npd, V = self.np, self.mcfg.vocab_size
+        t, k, p = npd["temperature"][:n], npd["top_k"][:n], npd["top_p"][:n]
+        return bool(((t > 0) & (((k > 0) & (k < V)) | ((p > 0) & (p < 1)))).any())
+
+    def _graph_for(self, n: int, B: int):
+        """The decode graph of bucket n for a batch of B rows: the plain one, or -- when some
+        row uses top-k / top-p -- the one with the sampler's threshold passes."""
+        g = self.graphs.get(n)
+        if g is None or self.ps.world_size > 1 or not self._host_filtered(B):
+            return g
+        if n not in self.graphs_f:
+            stream = torch.cuda.Stream()
+            stream.wait_stream(torch.cuda.current_stream())
+            self._capture_filtered = True
+            try:
+                with torch.cuda.stream(stream):
+                    self._decode_body(n)  # warm-up: the same step the replay then redoes
+                stream.synchronize()
+                gf = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf, pool=self.graph_pool, stream=stream):
+                    self._decode_body(n)
+            finally:
+                self._capture_filtered = None
+            torch.cuda.current_stream().wait_stream(stream)
+            self.graphs_f[n] = gf
+        return self.graphs_f[n]
 
     PREFILL_FIELDS = ("input_ids", "positions", "slots", "seq_lens", "q_start", "block_tables",
                       "tile_seq", "tile_row", "logits_idx", "temperature", "top_p", "top_k",
@@ -476,6 +515,8 @@ class ModelRunner:
             self._stage_decode(n)  # (other TP ranks receive it by the in-graph broadcast)
         extras = info.get("extras")
         if graph is not None and not extras:
+            if not (self._tp_bcast_inputs and self.ps.tp_rank != 0):
+                graph = self._graph_for(n, B)
             graph.replay()
         else:
             # penalties / log-probs requested: the same padded batch (n rows, so TP peers
@@ -520,7 +561,7 @@ class ModelRunner:
                 torch.index_select(self.out_tokens[:self.max_seqs], 0, self.dd["src_rows"][:n],
                                    out=self.dd["input_ids"][:n])
             if graph is not None:
-                graph.replay()
+                self._graph_for(n, B).replay()
             else:
                 self._decode_body(n)
         if not self.is_gpu:
@@ -652,6 +693,7 @@ class ModelRunner:
             dist.barrier()
         self.graph_pool = torch.cuda.graph_pool_handle()
         stream = torch.cuda.Stream()
+        self._capture_filtered = self.ps.world_size > 1
         for b in reversed(self.buckets):
             with torch.cuda.stream(stream):
                 self._decode_body(b)  # warm-up (hipBLASLt heuristics, allocator)
@@ -662,6 +704,7 @@ class ModelRunner:
             with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
                 self._decode_body(b)
             self.graphs[b] = g
+        self._capture_filtered = None
         torch.cuda.synchronize()
         if tunable:
             torch.cuda.tunable.tuning_enable(False)

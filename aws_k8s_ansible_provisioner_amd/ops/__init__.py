@@ -499,6 +499,9 @@ def gemm_splitk(M: int, N: int, K: int) -> int:
 
 # ----------------------------------------------------------------------------- sampling
 SAMPLE_MAX_CHUNKS = 64  # csrc/kernels/sampling.hip kMaxChunks
+# floats per row (sample_ws_floats): 64 chunk records of 8, a 16-word filter state, and
+# 2 x kHistRow floats of filter-pass histograms
+SAMPLE_WS_PER_ROW = SAMPLE_MAX_CHUNKS * 8 + 16 + 2 * (SAMPLE_MAX_CHUNKS * 256 + 128)
 _SAMPLE_WS: dict = {}
 _SAMPLE_OLD: list = []  # outgrown workspaces stay alive: captured hipGraphs address them
 
@@ -513,15 +516,17 @@ def _sample_ws(device, B: int):
         if cur is not None:
             _SAMPLE_OLD.append(cur)
         n = max(B, 256)
-        cur = (torch.zeros(n * (SAMPLE_MAX_CHUNKS * 8 + 4), dtype=torch.float32, device=device),
+        cur = (torch.zeros(n * SAMPLE_WS_PER_ROW, dtype=torch.float32, device=device),
                torch.zeros(n * CTR_STRIDE, dtype=torch.int32, device=device))
         _SAMPLE_WS[device] = cur
     return cur
 
 
 def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out_logprobs=None,
-           greedy_logprobs: bool = False):
-    """greedy_logprobs: also return the log-prob of greedy (temperature 0) picks."""
+           greedy_logprobs: bool = False, filtered: bool = True):
+    """greedy_logprobs: also return the log-prob of greedy (temperature 0) picks.  filtered=False:
+    the caller guarantees no row uses top-k / top-p, so their threshold passes are skipped (the
+    decode step's graph for such batches)."""
     B = logits.shape[0]
     if out_tokens is None:
         out_tokens = torch.empty(B, dtype=torch.int64, device=logits.device)
@@ -530,7 +535,7 @@ def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out
     if _native(logits):
         ws, tickets = _sample_ws(logits.device, B)
         torch.ops.akap.sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens,
-                              out_logprobs, greedy_logprobs, ws, tickets)
+                              out_logprobs, greedy_logprobs, ws, tickets, filtered)
         return out_tokens, out_logprobs
     t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps, greedy_logprobs)
     out_tokens.copy_(t)

@@ -226,6 +226,47 @@ def test_argmax_and_greedy_sample():
     assert torch.equal(tok, exp)
 
 
+@pytest.mark.parametrize("k,tp", [(50, 1.0), (0, 0.9), (40, 0.8), (2000, 0.5), (1, 1.0)])
+def test_sampling_filters_exact_sets_full_vocab(k, tp):
+    """Top-k / top-p on full-vocabulary bf16 rows (the distributed two-level threshold passes):
+    every sampled token lies in the exact allowed set computed in fp32 from the same bf16
+    values (ties at the threshold included), over many (seed, step) draws."""
+    torch.manual_seed(k + int(tp * 10))
+    B, V, T = 16, 151936, 0.9
+    base = (torch.randn(B, V) * 2.5).bfloat16()
+    base[:, :7] = 9.0  # a tie group at the top
+    logits = base.to(DEV)
+    temp = torch.full((B,), T, device=DEV)
+    tk = torch.full((B,), k, dtype=torch.int32, device=DEV)
+    tpp = torch.full((B,), tp, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 7919
+    allowed = []
+    for r in range(B):
+        z = base[r].float() / T
+        keep = torch.ones(V, dtype=torch.bool)
+        if 0 < k < V:
+            kth = torch.topk(base[r].float(), k).values[-1]
+            keep &= base[r].float() >= kth
+        if 0 < tp < 1:
+            p = torch.softmax(torch.where(keep, z, torch.tensor(-float("inf"))), -1)
+            vals = base[r].float()
+            order = torch.argsort(vals, descending=True)
+            cum = torch.cumsum(p[order], 0)
+            n = int((cum < tp - 1e-6).sum()) + 1
+            thr = vals[order[n - 1]]
+            keep &= vals >= thr
+        allowed.append(keep)
+    for step in range(24):
+        steps = torch.full((B,), step, dtype=torch.int32, device=DEV)
+        tok, lp = ops.sample(logits, temp, tk, tpp, seeds, steps)
+        tok = tok.cpu()
+        for r in range(B):
+            assert bool(allowed[r][tok[r]]), (r, step, int(tok[r]))
+    # one-token sets are deterministic
+    if k == 1:
+        assert all(int(allowed[r].sum()) >= 1 for r in range(B))
+
+
 def test_sampling_distribution_topk_topp():
     torch.manual_seed(4)
     V, N = 64, 4000
