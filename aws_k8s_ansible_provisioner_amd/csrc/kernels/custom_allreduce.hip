@@ -377,16 +377,21 @@ __global__ __launch_bounds__(256) void car_bcast_kernel(CarArgs a, bf16* buf, lo
   car_bcast(a, blockIdx.x, gridDim.x, buf, n8, root);
 }
 
-// Block count of every launch: always the full kCarMaxBlocks, whatever the size and kind, so
-// every block's epoch counts every launch (header, "reuse").  Blocks past a small message's
-// vectors only exchange flags: ~W system-scope stores + polls each, in parallel with the rest.
-static int car_blocks(long, int, bool) { return kCarMaxBlocks; }
+// Block count of every launch: the communicator's fixed grid (kCarMaxBlocks by default),
+// whatever the size and kind, so every block's epoch counts every launch (header, "reuse").
+// Blocks past a small message's vectors only exchange flags.  Ranks that SHARE one GPU (the
+// single-GPU rehearsal) use a smaller grid: their spinning blocks otherwise hold a wave slot
+// on every SIMD, and a peer's 512-VGPR GEMM workgroup then fits on no CU -- the peer never
+// reaches the collective and every wait times out.
+static int car_blocks(const CarArgs& a) {
+  return a.blocks > 0 && a.blocks <= kCarMaxBlocks ? a.blocks : kCarMaxBlocks;
+}
 
 void launch_custom_allreduce(const CarArgs& a, const void* in, void* out, long n, int two_shot,
                              hipStream_t s, const CarEpi* epi) {
   const long n8 = n / 8;
   if (n8 == 0) return;
-  const int blocks = car_blocks(n8, a.world, two_shot != 0);
+  const int blocks = car_blocks(a);
   const CarEpi e = epi ? *epi : CarEpi{};
   if (two_shot) {
     if (epi) car_twoshot_kernel<true><<<blocks, 256, 0, s>>>(a, (const bf16*)in, (bf16*)out, n8, e);
@@ -401,7 +406,7 @@ void launch_custom_allgather(const CarArgs& a, const void* in, void* out, long r
                              hipStream_t s) {
   const long n8 = rows * n / 8;
   if (n8 == 0) return;
-  car_allgather_kernel<<<car_blocks(n8, a.world, false), 256, 0, s>>>(a, (const bf16*)in,
+  car_allgather_kernel<<<car_blocks(a), 256, 0, s>>>(a, (const bf16*)in,
                                                                     (bf16*)out, n8, n);
 }
 
@@ -409,21 +414,21 @@ void launch_custom_alltoall(const CarArgs& a, const void* in, void* out, long se
                             hipStream_t s) {
   const long seg8 = seg_elems / 8;
   if (seg8 == 0) return;
-  car_alltoall_kernel<<<car_blocks(seg8, a.world, false), 256, 0, s>>>(a, (const bf16*)in,
+  car_alltoall_kernel<<<car_blocks(a), 256, 0, s>>>(a, (const bf16*)in,
                                                                       (bf16*)out, seg8);
 }
 
 void launch_custom_broadcast(const CarArgs& a, void* buf, long bytes, int root, hipStream_t s) {
   const long n8 = bytes / 16;
   if (n8 == 0) return;
-  car_bcast_kernel<<<car_blocks(n8, a.world, false), 256, 0, s>>>(a, (bf16*)buf, n8, root);
+  car_bcast_kernel<<<car_blocks(a), 256, 0, s>>>(a, (bf16*)buf, n8, root);
 }
 
 void launch_custom_allreduce_multi(const CarMulti& m, int world, long n, int two_shot,
                                    hipStream_t s) {
   const long n8 = n / 8;
   if (n8 == 0) return;
-  dim3 grid(car_blocks(n8, world, two_shot != 0), world);
+  dim3 grid(car_blocks(m.args[0]), world);
   if (m.use_epi) car_multi_kernel<true><<<grid, 256, 0, s>>>(m, n8, two_shot);
   else car_multi_kernel<false><<<grid, 256, 0, s>>>(m, n8, two_shot);
 }

@@ -267,13 +267,18 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
     for (int f = 0; f < NF; ++f)
       acc[f / JN][f % JN] = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((t0 + f * NT) * 16), 0, kGdSc1));
-#pragma unroll
-    for (int z = 1; z < S; ++z)
+    // every slice's fragments (NF per slab) requested before any is summed: one round trip
+    // past the per-XCD L2 per slab, overlapped
+    for (int z = 1; z < S; ++z) {
+      f32x4 v[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f)
-        acc[f / JN][f % JN] += __builtin_bit_cast(
+        v[f] = __builtin_bit_cast(
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((t0 + z * zs + f * NT) * 16),
                                                          0, kGdSc1));
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f / JN][f % JN] += v[f];
+    }
   }
 
   // epilogue: lane holds rows wm*WR + i*16 + fg*4 + r, column fr of each 16-col sub-tile

@@ -262,6 +262,7 @@ struct CarArgs {
   uint32_t* err;         // local error flag (spin-wait timeout)
   int rank, world;
   size_t half_elems;     // capacity in elements of one staging half
+  int blocks;            // grid of EVERY launch on this communicator (<= 128; see the header)
 };
 // Optional fused epilogue of the TP decode chain (the row-parallel O / down projection's
 // partial sums are all-reduced, then): s = bf16(bf16(sum) + residual); residual = s;

@@ -418,6 +418,26 @@ __device__ __forceinline__ bool pg_spin_ge(const int* c, int v) {
 
 constexpr int kPgSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1-bypass loads)
 
+// sum over the `splits` slabs of the f32x4 at byte offset off (slab stride bytes): the sc1
+// loads are issued 8 at a time (each is a round trip past the per-XCD L2, ~1 us; a plain loop
+// over the slices would wait for every one in turn)
+__device__ __forceinline__ f32x4 pg_sum_slabs(__amdgpu_buffer_rsrc_t rs, size_t off,
+                                              size_t stride, int splits) {
+  f32x4 y = {0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < splits; q0 += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rs, (int)(off + min(q0 + j, splits - 1) * stride), 0,
+                                           kPgSc1));
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (q0 + j < splits) y += v[j];
+  }
+  return y;
+}
+
 // Epilogue of 4 consecutive output columns (col) of one row, values y (fp32, before the row
 // scale): EPI_STORE / EPI_RESNORM; returns the row's sum-of-squares contribution (RESNORM).
 template <int EPI>
@@ -547,14 +567,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_sk_kernel(DGemmArgs p, in
       const int row = m0 + r;
       if (row >= p.M) continue;
       const int cgate = (cg >> 2) * 32 + (cg & 3) * 4;
-      f32x4 g = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < splits; ++q) {
-        const size_t base = ((size_t)q * SLAB + r * PG_T + cgate) * 4;
-        g += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)base, 0,
-                                                                              kPgSc1));
-        u += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rs, (int)(base + 64), 0, kPgSc1));
-      }
+      const size_t base = ((size_t)r * PG_T + cgate) * 4;
+      const f32x4 g = pg_sum_slabs(rs, base, (size_t)SLAB * 4, splits);
+      const f32x4 u = pg_sum_slabs(rs, base + 64, (size_t)SLAB * 4, splits);
       pg_epi_silu(p, row, (n0 >> 1) + (cg >> 2) * 16 + (cg & 3) * 4, g, u, pg_row_scale(p, row));
     }
   } else {
@@ -563,11 +578,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_sk_kernel(DGemmArgs p, in
     for (int e = tid; e < (r1 - r0) * 64; e += THREADS) {
       const int r = r0 + e / 64, c = (e % 64) * 4;
       const int row = m0 + r;
-      f32x4 y = {0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < splits; ++q)
-        y += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rs, (int)(((size_t)q * SLAB + r * PG_T + c) * 4), 0,
-                                           kPgSc1));
+      const f32x4 y = pg_sum_slabs(rs, ((size_t)r * PG_T + c) * 4, (size_t)SLAB * 4, splits);
       float qs = 0.f;
       if (row < p.M) qs = pg_epi4<EPI>(p, row, n0 + c, y, pg_row_scale(p, row));
       if constexpr (EPI == EPI_RESNORM) {

@@ -414,12 +414,22 @@ __device__ __forceinline__ bool hist_pass(const T* x, int lo, int hi, bool vec_o
   }
   __syncthreads();
   if (!s_last) return false;
+  // S sc1 loads per thread, issued 16 at a time: each is a round trip past the per-XCD L2
+  // (~1 us); a plain loop waits for every one in turn (64 us at S = 64)
   cnt = 0.f;
   mass = 0.f;
-  for (int q = 0; q < S; ++q) {
-    const u32x2 r = __builtin_amdgcn_raw_buffer_load_b64(rh, (q * 256 + tid) * 8, 0, kSc1);
-    cnt += __uint_as_float(r[0]);
-    mass += __uint_as_float(r[1]);
+  for (int q0 = 0; q0 < S; q0 += 16) {
+    u32x2 r[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      r[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (min(q0 + j, S - 1) * 256 + tid) * 8, 0,
+                                                  kSc1);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (q0 + j < S) {
+        cnt += __uint_as_float(r[j][0]);
+        mass += __uint_as_float(r[j][1]);
+      }
   }
   return true;
 }

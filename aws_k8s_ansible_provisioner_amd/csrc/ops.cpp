@@ -844,8 +844,10 @@ CarComm* car_get(int64_t h) {
   } while (0)
 }  // namespace
 
-int64_t car_create(int64_t device, int64_t rank, int64_t world, int64_t max_elems) {
+int64_t car_create(int64_t device, int64_t rank, int64_t world, int64_t max_elems,
+                   int64_t blocks) {
   TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "world must be 1..8");
+  TORCH_CHECK(blocks >= 1 && blocks <= 128, "car blocks must be 1..128");
   TORCH_CHECK(max_elems % 8 == 0, "max_elems % 8");
   const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (int)device));
   auto* c = new CarComm();
@@ -864,6 +866,7 @@ int64_t car_create(int64_t device, int64_t rank, int64_t world, int64_t max_elem
   c->args.rank = (int)rank;
   c->args.world = (int)world;
   c->args.half_elems = (size_t)max_elems;
+  c->args.blocks = (int)blocks;
   for (int p = 0; p < 8; ++p) { c->args.bufs[p] = nullptr; c->args.sigs[p] = nullptr; }
   c->args.bufs[rank] = reinterpret_cast<__bf16*>(c->buf);
   c->args.sigs[rank] = reinterpret_cast<uint32_t*>(c->sig);
@@ -1182,7 +1185,7 @@ TORCH_LIBRARY(akap, m) {
         "Tensor(b!)? ss_out, Tensor(c!)? aout, Tensor? ln_out) -> ()");
   m.def("dgemm_ok(int M, int N, int K, int splitk, int pf) -> bool");
   m.def("l2_prefetch(Tensor[] ts, Tensor(a!) sink) -> ()");
-  m.def("car_create(int device, int rank, int world, int max_elems) -> int");
+  m.def("car_create(int device, int rank, int world, int max_elems, int blocks=128) -> int");
   m.def("car_ipc_handles(int h) -> Tensor");
   m.def("car_open(int h, Tensor handles) -> ()");
   m.def("car_all_reduce(int h, Tensor inp, Tensor(a!) out, bool two_shot) -> ()");

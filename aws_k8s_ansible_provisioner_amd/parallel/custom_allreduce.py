@@ -41,6 +41,17 @@ def _aligned(t: torch.Tensor) -> bool:
     return t.data_ptr() % 16 == 0
 
 
+def car_grid(world: int) -> int:
+    """Fixed grid of every launch on a communicator: 128 blocks with one rank per GPU; ranks
+    sharing one GPU (world > visible devices: the single-GPU rehearsal) split 128 between them,
+    so their spinning blocks leave CUs free for a late peer's GEMMs (AKAP_CAR_BLOCKS)."""
+    env = os.environ.get("AKAP_CAR_BLOCKS")
+    if env:
+        return max(1, min(128, int(env)))
+    shared = world > max(1, torch.cuda.device_count())
+    return max(8, 128 // world) if shared else 128
+
+
 class CustomAllReduce:
     def __init__(self, group=None, device: Optional[torch.device] = None,
                  max_bytes: int = DEFAULT_MAX_BYTES, buffer_bytes: int = 0):
@@ -57,7 +68,9 @@ class CustomAllReduce:
         self.buffer_bytes = max(max_bytes, buffer_bytes)
         self.oneshot_bytes = oneshot_limit(self.world)
         max_elems = (self.buffer_bytes // 2 + 7) // 8 * 8
-        self.h = torch.ops.akap.car_create(self.device.index, self.rank, self.world, max_elems)
+        self.blocks = car_grid(self.world)
+        self.h = torch.ops.akap.car_create(self.device.index, self.rank, self.world, max_elems,
+                                           self.blocks)
         mine = torch.ops.akap.car_ipc_handles(self.h)
         allh: list = [None] * self.world
         dist.all_gather_object(allh, mine.numpy().tobytes(), group=group)

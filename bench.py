@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
     ap.add_argument("--block-size", type=int, default=32)
     ap.add_argument("--max-model-len", type=int, default=2048)
+    ap.add_argument("--num-gpu-blocks", type=int, default=0,
+                    help="KV cache blocks per engine (0: sized from free memory)")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--enforce-eager", action="store_true")
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
@@ -151,7 +153,7 @@ def main() -> int:
                         block_size=a.block_size, enforce_eager=a.enforce_eager,
                         device="cuda" if gpu else "cpu",
                         seed=1234 if pd else 1234 + rank,  # P/D ranks: the same weights
-                        num_gpu_blocks=None if gpu else 512,
+                        num_gpu_blocks=(a.num_gpu_blocks or None) if gpu else 512,
                         kv_role=("prefill" if is_prefill else "decode") if pd else "both",
                         kv_cache_dtype=a.kv_cache_dtype,
                         mixed_batching=not a.no_mixed_batching,
