@@ -84,6 +84,9 @@ def parse():
                     help="Poisson arrivals at this many requests/s (0 = all at t=0)")
     ap.add_argument("--no-mixed-batching", action="store_true",
                     help="prefill-first scheduling (decodes stall while a prefill runs)")
+    ap.add_argument("--torch-profile", action="store_true",
+                    help="after timing, one more wave under torch.profiler; rank 0 prints the "
+                         "kernel table")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra untimed waves run after timing (for rocprofv3 captures)")
     return ap.parse_args()
@@ -273,6 +276,20 @@ def main() -> int:
     log("[bench] execute s / steps by kind: " + ", ".join(
         f"{k} {v[0]:.3f}/{v[1]}" for k, v in getattr(eng, "step_kinds", {}).items()))
     for _ in range(a.profile_steps):
+        wave()
+    if a.torch_profile and rank == 0:
+        # in-process kernel table of one more (untimed) wave on rank 0: works under torchrun,
+        # where rocprofv3 cannot wrap the launcher
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CUDA] if gpu else [ProfilerActivity.CPU]
+        with profile(activities=acts) as prof:
+            wave()
+            if gpu:
+                torch.cuda.synchronize()
+        key = "self_device_time_total" if gpu else "self_cpu_time_total"
+        print(prof.key_averages().table(sort_by=key, row_limit=30), flush=True)
+    elif a.torch_profile:
         wave()
 
     p50_local = statistics.median(ttfts) if ttfts else 0.0
