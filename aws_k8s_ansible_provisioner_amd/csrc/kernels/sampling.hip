@@ -80,9 +80,9 @@ constexpr int kMaxChunks = 64;
 constexpr int kFilterThreads = 256;
 constexpr int kSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1-bypass loads)
 constexpr int kSelWords = 16;  // per-row state of the filter passes (32-bit words)
-// per-row histogram area of the filter passes, in float2: kMaxChunks x 256 (count, mass)
-// pairs, then pass A's 256 high-byte masses
-constexpr int kHistRow = kMaxChunks * 256 + 128;
+// per-row histogram area of the filter passes, in float2: kMaxChunks x 512 pairs (pass B
+// publishes two 256-bin sets per chunk)
+constexpr int kHistRow = kMaxChunks * 512;
 
 struct SampPart {  // one chunk's partial record (32 B = two 16-B vectors)
   float m, s;      // max of z over the chunk, sum of exp(z - m)
@@ -372,39 +372,25 @@ static_assert(sizeof(SelState) == kSelWords * 4, "SelState layout");
 
 __device__ __forceinline__ int k16_of(float v) { return (int)(fkey(v) >> 16); }
 
-// this chunk's (count, mass) histogram over 256 bins of elements `sel` maps to a bin (or -1),
-// published to hist[row][c] as 256 float2 (sc1); returns true in the row's last chunk, whose
-// threads then hold bin tid's row totals (cnt, mass)
-template <typename T, typename SEL>
-__device__ __forceinline__ bool hist_pass(const T* x, int lo, int hi, bool vec_ok, float invT,
-                                          float M, float* whist /* [4][2][256] LDS */,
-                                          float2* hist_row, int S, int c, int* ticket,
-                                          float& cnt, float& mass, SEL&& sel) {
-  const int tid = threadIdx.x, wid = tid >> 6;
-  __shared__ int s_last;
-  for (int i = tid; i < 4 * 512; i += kChunkThreads) whist[i] = 0.f;
-  __syncthreads();
-  float* wc = whist + wid * 512;
-  visit_range(x, lo, hi, vec_ok, [&](float v, int) {
-    const int b = sel(v);
-    if (b < 0) return;
-    atomicAdd(&wc[b], 1.f);
-    atomicAdd(&wc[256 + b], __expf(v * invT - M));
-  });
-  __syncthreads();
-  float cc = 0.f, mm = 0.f;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    cc += whist[w * 512 + tid];
-    mm += whist[w * 512 + 256 + tid];
-  }
-  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)hist_row, (short)0, (int)(S * 256 * 8), 0x00020000);
+// Publish this chunk's NB x 256 (x, y) bins (thread tid holds bins j * 256 + tid) to the row's
+// histogram area with sc1 stores, take the row's ticket; in the row's last chunk every thread
+// then holds the row totals of its bins in `tot` (the S chunks' loads issued 16 at a time:
+// each is a round trip past the per-XCD L2) and true is returned.
+template <int NB>
+__device__ __forceinline__ bool publish_combine(const float2 (&mine)[NB], float2* hrow, int S,
+                                                int c, int* ticket, float2 (&tot)[NB]) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  u32x2 v2;
-  v2[0] = __float_as_uint(cc);
-  v2[1] = __float_as_uint(mm);
-  __builtin_amdgcn_raw_buffer_store_b64(v2, rh, (c * 256 + tid) * 8, 0, kSc1);
+  const int tid = threadIdx.x;
+  __shared__ int s_last;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)hrow, (short)0, (int)(S * NB * 256 * 8), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    u32x2 v2;
+    v2[0] = __float_as_uint(mine[j].x);
+    v2[1] = __float_as_uint(mine[j].y);
+    __builtin_amdgcn_raw_buffer_store_b64(v2, rh, ((c * NB + j) * 256 + tid) * 8, 0, kSc1);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
   if (tid == 0) {
@@ -414,22 +400,23 @@ __device__ __forceinline__ bool hist_pass(const T* x, int lo, int hi, bool vec_o
   }
   __syncthreads();
   if (!s_last) return false;
-  // S sc1 loads per thread, issued 16 at a time: each is a round trip past the per-XCD L2
-  // (~1 us); a plain loop waits for every one in turn (64 us at S = 64)
-  cnt = 0.f;
-  mass = 0.f;
-  for (int q0 = 0; q0 < S; q0 += 16) {
-    u32x2 r[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      r[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (min(q0 + j, S - 1) * 256 + tid) * 8, 0,
-                                                  kSc1);
+  for (int j = 0; j < NB; ++j) {
+    float tx = 0.f, ty = 0.f;
+    for (int q0 = 0; q0 < S; q0 += 16) {
+      u32x2 r[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (q0 + j < S) {
-        cnt += __uint_as_float(r[j][0]);
-        mass += __uint_as_float(r[j][1]);
-      }
+      for (int k = 0; k < 16; ++k)
+        r[k] = __builtin_amdgcn_raw_buffer_load_b64(
+            rh, ((min(q0 + k, S - 1) * NB + j) * 256 + tid) * 8, 0, kSc1);
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (q0 + k < S) {
+          tx += __uint_as_float(r[k][0]);
+          ty += __uint_as_float(r[k][1]);
+        }
+    }
+    tot[j] = make_float2(tx, ty);
   }
   return true;
 }
@@ -471,7 +458,11 @@ template <typename T>
 __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams p, int pass,
                                                                     SelState* st, float2* hist,
                                                                     int* tickets) {
-  __shared__ float whist[4 * 512];
+  // pass A: a per-LANE copy of the high-byte histogram ([bin][lane], 64 KB): a wave's 64
+  // lanes never add to the same word (logits crowd into a few exponent bins, and same-word
+  // LDS atomics inside one instruction serialise); passes B / C: per-wave histograms of the
+  // few elements inside one high-byte bin (and, for top-k + top-p, above it)
+  __shared__ float lds[256 * 64];
   __shared__ float scratch[16];
   const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
   const float temp = p.temperature ? p.temperature[row] : 0.f;
@@ -487,65 +478,82 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   const float M = rs.M;
   int* ticket = tickets + row * kCtrStride;
   float2* hrow = hist + (size_t)row * kHistRow;
-  float* hmass = reinterpret_cast<float*>(hrow + kMaxChunks * 256);  // pass A's bin masses
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kk = p.top_k ? p.top_k[row] : 0;
   const float tp = p.top_p ? p.top_p[row] : 1.f;
   const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
-  float cnt = 0.f, mass = 0.f;
-  if (pass == 0) {  // A: high byte of the whole row
-    if (!hist_pass(x, lo, hi, vec_ok, invT, M, whist, hrow, S, c, ticket, cnt, mass,
-                   [](float v) { return k16_of(v) >> 8; }))
-      return;
-    float above;
-    int b;
+  if (pass == 0) {  // A: high byte of the whole row; count (top-k) or mass (top-p only)
+    for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
+    __syncthreads();
     if (has_k) {
-      b = suffix_select(cnt, (float)kk, scratch, &above);
-      float mabove;
-      // the mass above the selected bin (suffix of masses over bins > b)
-      const float mm = tid > b ? mass : 0.f;
-      mabove = block_sum(mm, scratch);
-      if (tid == 0) {
-        rs.sel_hi = b;
-        rs.cnt_above = above;
-        rs.mass_above = mabove;
-      }
+      visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], 1.f);
+      });
     } else {
-      b = suffix_select(mass, tp * rs.Z, scratch, &above);
-      if (tid == 0) {
-        rs.sel_hi = b;
-        rs.mass_above = above;
-        rs.p_target = tp * rs.Z;
-      }
+      visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], __expf(v * invT - M));
+      });
     }
-    // keep the row's high-byte masses for pass B's top-p-over-top-k step
-    hmass[tid] = mass;
-    if (tid == 0) { rs.tau = -1; rs.p_hi = -1; }
+    __syncthreads();
+    float v = 0.f;  // bin tid over the 64 lane copies (rotated: conflict-free)
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) v += lds[tid * 64 + ((j + lane) & 63)];
+    float2 mine[1] = {make_float2(v, 0.f)}, tot[1];
+    if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
+    float above;
+    const int b = suffix_select(tot[0].x, has_k ? (float)kk : tp * rs.Z, scratch, &above);
+    if (tid == 0) {
+      rs.sel_hi = b;
+      if (has_k) rs.cnt_above = above;
+      else { rs.mass_above = above; rs.p_target = tp * rs.Z; }
+      rs.tau = -1;
+      rs.p_hi = -1;
+    }
     return;
   }
-  if (pass == 1) {  // B: low byte inside sel_hi
+  if (pass == 1) {  // B: low byte inside sel_hi (count + mass); top-k + top-p: masses above
     const int sh = rs.sel_hi;
-    if (!hist_pass(x, lo, hi, vec_ok, invT, M, whist, hrow, S, c, ticket, cnt, mass,
-                   [sh](float v) { const int k = k16_of(v); return (k >> 8) == sh ? (k & 255) : -1; }))
-      return;
+    float* lc = lds;             // [4][256] low-byte counts
+    float* lm = lds + 4 * 256;   // [4][256] low-byte masses
+    float* hm = lds + 8 * 256;   // [4][256] high-byte masses of bins above sh
+    for (int i = tid; i < 12 * 256; i += kChunkThreads) lds[i] = 0.f;
+    __syncthreads();
+    const bool above_too = has_k && has_p;
+    visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+      const int k = k16_of(v), h = k >> 8;
+      if (h == sh) {
+        atomicAdd(&lc[wid * 256 + (k & 255)], 1.f);
+        atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
+      } else if (above_too && h > sh) {
+        atomicAdd(&hm[wid * 256 + h], __expf(v * invT - M));
+      }
+    });
+    __syncthreads();
+    float cc = 0.f, mm = 0.f, hh = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      cc += lc[w * 256 + tid];
+      mm += lm[w * 256 + tid];
+      hh += hm[w * 256 + tid];
+    }
+    float2 mine[2] = {make_float2(cc, mm), make_float2(hh, 0.f)}, tot[2];
+    if (!publish_combine<2>(mine, hrow, S, c, ticket, tot)) return;
+    const float cnt = tot[0].x, mass = tot[0].y, hmass = tot[1].x;
     float above;
     if (has_k) {
       const int b = suffix_select(cnt, (float)kk - rs.cnt_above, scratch, &above);
       const int tau_k = (sh << 8) | b;
-      const float mm = tid >= b ? mass : 0.f;
-      const float Zk = rs.mass_above + block_sum(mm, scratch);
       if (!has_p) {
-        if (tid == 0) { rs.tau = tau_k; rs.Zk = Zk; }
+        if (tid == 0) rs.tau = tau_k;
         return;
       }
-      // top-p over the top-k set: masses of the high-byte bins above sh (pass A), then the low
-      // bins >= b of sh
+      // top-p over the top-k set: Zk = masses of the high-byte bins above sh + low bins >= b
+      const float hsum = block_sum(hmass, scratch);
+      const float Zk = hsum + block_sum(tid >= b ? mass : 0.f, scratch);
       const float target = tp * Zk;
-      const float hm = tid > sh ? hmass[tid] : 0.f;
-      float habove;
-      const int hb = suffix_select(hm, target, scratch, &habove);
-      const float hsum = block_sum(hm, scratch);
-      if (hsum >= target && hb > sh) {  // crossing in a higher bin: pass C resolves it
+      if (hsum >= target) {  // crossing in a higher high-byte bin: pass C resolves it
+        float habove;
+        const int hb = suffix_select(hmass, target, scratch, &habove);
         if (tid == 0) { rs.p_hi = hb; rs.p_above = habove; rs.p_target = target; rs.tau = tau_k; }
         return;
       }
@@ -554,7 +562,6 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
       if (tid == 0) { rs.tau = max(tau_k, (sh << 8) | lb); rs.Zk = Zk; }
       return;
     }
-    // top-p only
     const int b = suffix_select(mass, rs.p_target - rs.mass_above, scratch, &above);
     if (tid == 0) rs.tau = (sh << 8) | b;
     return;
@@ -562,11 +569,21 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   if (pass == 2) {  // C: low-byte masses inside p_hi (top-k + top-p rows crossing above sh)
     const int ph = rs.p_hi;
     if (ph < 0) return;  // uniform per row
-    if (!hist_pass(x, lo, hi, vec_ok, invT, M, whist, hrow, S, c, ticket, cnt, mass,
-                   [ph](float v) { const int k = k16_of(v); return (k >> 8) == ph ? (k & 255) : -1; }))
-      return;
+    float* lm = lds;
+    for (int i = tid; i < 4 * 256; i += kChunkThreads) lds[i] = 0.f;
+    __syncthreads();
+    visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+      const int k = k16_of(v);
+      if ((k >> 8) == ph) atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
+    });
+    __syncthreads();
+    float mm = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mm += lm[w * 256 + tid];
+    float2 mine[1] = {make_float2(mm, 0.f)}, tot[1];
+    if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
     float above;
-    const int b = suffix_select(mass, rs.p_target - rs.p_above, scratch, &above);
+    const int b = suffix_select(tot[0].x, rs.p_target - rs.p_above, scratch, &above);
     if (tid == 0) { rs.tau = (ph << 8) | b; rs.p_hi = -1; }
     return;
   }
@@ -587,8 +604,8 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   __shared__ int s_last;
   const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
       (void*)hrow, (short)0, (int)(S * 8), 0x00020000);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   if (tid == 0) {
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     u32x2 v2;
     v2[0] = __float_as_uint(b.v);
     v2[1] = (uint32_t)b.i;
@@ -602,7 +619,6 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   if (!s_last || tid >= 64) return;
   ArgBest a{-INFINITY, 0x7fffffff};
   if (tid < S) {
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     const u32x2 r = __builtin_amdgcn_raw_buffer_load_b64(rh, tid * 8, 0, kSc1);
     a = ArgBest{__uint_as_float(r[0]), (int)r[1]};
   }

@@ -116,8 +116,9 @@ class ModelRunner:
         # decode graphs whose sampler also runs the top-k / top-p threshold passes: captured on
         # first use by a batch that needs them (single-rank engines; multi-rank engines capture
         # their only graphs with the passes, since a lazy capture would issue collectives alone)
-        self.graphs_f: dict[int, torch.cuda.CUDAGraph] = {}
-        self._capture_filtered: Optional[bool] = None
+        # decode graph variants by sampler mode (see _sample_mode), captured on first use
+        self.graphs_v: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._capture_mode: Optional[str] = None
         self.ep_overflow_steps = 0  # steps re-run after an EP dispatch overflow
         self.graph_pool = None
         self.buckets: list[int] = []
@@ -298,44 +299,55 @@ class ModelRunner:
             vals, idx = torch.topk(x, min(ntop, x.shape[-1]), dim=-1)
             vals = vals - torch.logsumexp(x, dim=-1, keepdim=True)
             self.last_top = (idx.cpu().numpy(), vals.cpu().numpy())
+        mode = self._sample_mode(n)
         return ops.sample(logits, d["temperature"][:n], d["top_k"][:n],
                           d["top_p"][:n], d["seeds"][:n], d["steps"][:n],
                           out_tokens=self.out_tokens[:n], out_logprobs=self.out_logprobs[:n],
-                          greedy_logprobs=lp, filtered=self._host_filtered(n))
+                          greedy_logprobs=lp, filtered=mode == "filtered",
+                          greedy_only=mode == "greedy" and not lp)
 
-    def _host_filtered(self, n: int) -> bool:
-        """Does any of the step's n sampled rows use top-k / top-p?  (From the host staging
-        arrays; inside a capture, the variant being captured.)"""
-        if self._capture_filtered is not None:
-            return self._capture_filtered
-        if not self.is_gpu:
-            return True
+    def _sample_mode(self, n: int) -> str:
+        """Sampler variant for the step's n sampled rows, from the host staging arrays:
+        "greedy" (every row at temperature 0: the argmax kernel), "filtered" (some row uses
+        top-k / top-p: the threshold passes), else "plain".  Inside a capture, the variant
+        being captured; multi-rank engines always run "filtered" (correct for every batch)."""
+        if self._capture_mode is not None:
+            return self._capture_mode
+        if not self.is_gpu or self.ps.world_size > 1:
+            return "filtered"
         npd, V = self.np, self.mcfg.vocab_size
         t, k, p = npd["temperature"][:n], npd["top_k"][:n], npd["top_p"][:n]
-        return bool(((t > 0) & (((k > 0) & (k < V)) | ((p > 0) & (p < 1)))).any())
+        if not (t > 0).any():
+            return "greedy"
+        if ((t > 0) & (((k > 0) & (k < V)) | ((p > 0) & (p < 1)))).any():
+            return "filtered"
+        return "plain"
 
     def _graph_for(self, n: int, B: int):
-        """The decode graph of bucket n for a batch of B rows: the plain one, or -- when some
-        row uses top-k / top-p -- the one with the sampler's threshold passes."""
+        """The decode graph of bucket n for a batch of B rows in its sampler mode: the one
+        captured at start (mode "plain"; "filtered" on multi-rank engines) or a variant
+        captured on the first batch that needs it."""
         g = self.graphs.get(n)
-        if g is None or self.ps.world_size > 1 or not self._host_filtered(B):
+        mode = self._sample_mode(B)
+        if g is None or self.ps.world_size > 1 or mode == "plain":
             return g
-        if n not in self.graphs_f:
+        key = (mode, n)
+        if key not in self.graphs_v:
             stream = torch.cuda.Stream()
             stream.wait_stream(torch.cuda.current_stream())
-            self._capture_filtered = True
+            self._capture_mode = mode
             try:
                 with torch.cuda.stream(stream):
                     self._decode_body(n)  # warm-up: the same step the replay then redoes
                 stream.synchronize()
-                gf = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gf, pool=self.graph_pool, stream=stream):
+                gv = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gv, pool=self.graph_pool, stream=stream):
                     self._decode_body(n)
             finally:
-                self._capture_filtered = None
+                self._capture_mode = None
             torch.cuda.current_stream().wait_stream(stream)
-            self.graphs_f[n] = gf
-        return self.graphs_f[n]
+            self.graphs_v[key] = gv
+        return self.graphs_v[key]
 
     PREFILL_FIELDS = ("input_ids", "positions", "slots", "seq_lens", "q_start", "block_tables",
                       "tile_seq", "tile_row", "logits_idx", "temperature", "top_p", "top_k",
@@ -693,7 +705,7 @@ class ModelRunner:
             dist.barrier()
         self.graph_pool = torch.cuda.graph_pool_handle()
         stream = torch.cuda.Stream()
-        self._capture_filtered = self.ps.world_size > 1
+        self._capture_mode = "filtered" if self.ps.world_size > 1 else "plain"
         for b in reversed(self.buckets):
             with torch.cuda.stream(stream):
                 self._decode_body(b)  # warm-up (hipBLASLt heuristics, allocator)
@@ -704,7 +716,7 @@ class ModelRunner:
             with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
                 self._decode_body(b)
             self.graphs[b] = g
-        self._capture_filtered = None
+        self._capture_mode = None
         torch.cuda.synchronize()
         if tunable:
             torch.cuda.tunable.tuning_enable(False)

@@ -500,8 +500,8 @@ def gemm_splitk(M: int, N: int, K: int) -> int:
 # ----------------------------------------------------------------------------- sampling
 SAMPLE_MAX_CHUNKS = 64  # csrc/kernels/sampling.hip kMaxChunks
 # floats per row (sample_ws_floats): 64 chunk records of 8, a 16-word filter state, and
-# 2 x kHistRow floats of filter-pass histograms
-SAMPLE_WS_PER_ROW = SAMPLE_MAX_CHUNKS * 8 + 16 + 2 * (SAMPLE_MAX_CHUNKS * 256 + 128)
+# 2 x kHistRow floats of filter-pass histograms (kHistRow = 64 x 512 float2)
+SAMPLE_WS_PER_ROW = SAMPLE_MAX_CHUNKS * 8 + 16 + 2 * SAMPLE_MAX_CHUNKS * 512
 _SAMPLE_WS: dict = {}
 _SAMPLE_OLD: list = []  # outgrown workspaces stay alive: captured hipGraphs address them
 
@@ -523,15 +523,19 @@ def _sample_ws(device, B: int):
 
 
 def sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens=None, out_logprobs=None,
-           greedy_logprobs: bool = False, filtered: bool = True):
+           greedy_logprobs: bool = False, filtered: bool = True, greedy_only: bool = False):
     """greedy_logprobs: also return the log-prob of greedy (temperature 0) picks.  filtered=False:
     the caller guarantees no row uses top-k / top-p, so their threshold passes are skipped (the
-    decode step's graph for such batches)."""
+    decode step's graph for such batches).  greedy_only: the caller guarantees every row is at
+    temperature 0 and needs no log-prob -- the argmax kernel alone (out_logprobs untouched)."""
     B = logits.shape[0]
     if out_tokens is None:
         out_tokens = torch.empty(B, dtype=torch.int64, device=logits.device)
     if out_logprobs is None:
         out_logprobs = torch.empty(B, dtype=torch.float32, device=logits.device)
+    if _native(logits) and greedy_only:
+        torch.ops.akap.argmax(logits, out_tokens)
+        return out_tokens, out_logprobs
     if _native(logits):
         ws, tickets = _sample_ws(logits.device, B)
         torch.ops.akap.sample(logits, temperature, top_k, top_p, seeds, steps, out_tokens,
