@@ -185,6 +185,10 @@ class MoEBlock:
 
     ep_fixed_max_tokens = int(os.environ.get("AKAP_EP_FIXED_MAX_T", str(1 << 30)))
     ep_slack = float(os.environ.get("AKAP_EP_SLACK", "2.0"))
+    # prefill-sized dispatches (>= 4096 pairs): the per-destination count concentrates near
+    # the mean (sd ~ sqrt(n)), so a smaller slack halves the exchanged bytes at ep = 2; an
+    # unusually skewed step overflows into the exact re-run
+    ep_slack_prefill = float(os.environ.get("AKAP_EP_SLACK_PREFILL", "1.25"))
     ep_min_cap = int(os.environ.get("AKAP_EP_MIN_CAP", "8"))
     ep_fallbacks = 0  # steps re-run on the exact path after a dispatch overflow
     force_exact = False  # set by exact_dispatch() around such a re-run
@@ -196,7 +200,8 @@ class MoEBlock:
         slack x the mean share, at least min(n, ep_min_cap = 8) (tiny decode batches), at most n."""
         import math
 
-        return min(n, max(math.ceil(self.ep_slack * n / self.ep), min(n, self.ep_min_cap)))
+        slack = self.ep_slack if n < 4096 else min(self.ep_slack, self.ep_slack_prefill)
+        return min(n, max(math.ceil(slack * n / self.ep), min(n, self.ep_min_cap)))
 
     @classmethod
     def overflow_flag(cls, device) -> torch.Tensor:
@@ -296,27 +301,38 @@ class MoEBlock:
         K, ep, el = self.K, self.ep, self.e_local
         n = T * K
         C = self.ep_capacity(n)
+        # rows per destination per exchange chunk (C unless the message must be split: the
+        # single-GPU gloo rehearsal's IPC staging); C rounded up to whole chunks
+        R = comm.ep_chunk_rows(C, d + 8, h)
+        C = -(-C // R) * R
+        nck = C // R
         flat = ids.reshape(-1).long()                       # [n] global expert ids
         dest = flat // el                                   # owning rank
         onehot = F.one_hot(dest, ep).to(torch.int32)        # [n, ep]
-        slot = ((torch.cumsum(onehot, 0) - onehot) * onehot).sum(1).long()  # rank-local index
+        # rank-local index of each pair: an inclusive scan along n of the [ep, n] transpose
+        # (an inner-dim scan; PyTorch's outer-dim scan of [n, ep] ran ~5 ms per prefill layer)
+        incl = torch.cumsum(onehot.t().contiguous(), dim=1, dtype=torch.int32)
+        slot = incl.gather(0, dest.view(1, -1)).view(-1).long() - 1
         fits = slot < C
+        # chunk-major rows [nck, ep, R]: chunk k of the exchange is one contiguous block whose
+        # segment p goes to rank p (nck = 1: the plain [ep, C] layout all_to_all_single takes);
         # overflowing pairs go to a dump row past the send buffer (never sent)
-        pos = torch.where(fits, dest * C + slot, torch.full_like(slot, ep * C))
+        pos = torch.where(fits, (slot // R * ep + dest) * R + slot % R,
+                          torch.full_like(slot, ep * C))
         flag = self.overflow_flag(h.device) if flag is None else flag
         torch.maximum(flag, (~fits).any().to(torch.int32).view(1), out=flag)
         tok = torch.arange(n, device=h.device) // K
         # one message per row: the token's hidden vector plus 8 trailing bf16 slots whose
-        # first two carry the int32 local expert id (-1 = empty slot), so the dispatch is ONE
-        # all-to-all (the EP group is the whole job: dp x tp ranks)
-        send = h.new_zeros(ep * C + 1, d + 8)
-        send[:, :d].index_copy_(0, pos, h[tok])
+        # first two carry the int32 local expert id (-1 = empty slot, whose vector is never
+        # read), so the dispatch is ONE all-to-all (the EP group is the whole job: dp x tp)
+        send = h.new_empty(ep * C + 1, d + 8)
         ids_col = send[:, d:d + 2].view(torch.int32)  # [ep*C + 1, 1] view into the rows
         ids_col.fill_(-1)
+        send[:, :d].index_copy_(0, pos, h[tok])
         ids_col.index_copy_(0, pos, (flat - dest * el).to(torch.int32).view(-1, 1))
         send = send[:ep * C]
         recv = torch.empty_like(send)
-        comm.ep_all_to_all_equal(recv, send)
+        comm.ep_all_to_all_equal(recv, send, chunks=nck)
         recv_x = recv[:, :d].contiguous()
         recv_e = recv[:, d:d + 2].contiguous().view(torch.int32).reshape(-1, 1)
         # every received row is one (token, local expert) pair: K = 1, weight 1 (the router
@@ -327,8 +343,9 @@ class MoEBlock:
         else:
             ones = torch.ones(ep * C, 1, dtype=torch.float32, device=h.device)
             y = ops.fused_moe(recv_x, self.w13, self.w2, ones, recv_e)
-        back = h.new_zeros(ep * C + 1, d)
-        comm.ep_all_to_all_equal(back[:ep * C], y.contiguous())
+        back = h.new_empty(ep * C + 1, d)
+        back[ep * C].zero_()  # the dump row overflowing pairs read (weighted, so finite)
+        comm.ep_all_to_all_equal(back[:ep * C], y.contiguous(), chunks=nck)
         mine = back.index_select(0, pos).view(T, K, d).float()
         return (mine * w.view(T, K, 1)).sum(1).to(h.dtype)
 

@@ -156,31 +156,38 @@ def tp_all_gather_rows(out: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def ep_all_to_all_equal(recv: torch.Tensor, send: torch.Tensor) -> torch.Tensor:
+def ep_chunk_rows(C: int, D: int, x: torch.Tensor) -> int:
+    """Rows per destination per chunk of a fixed-capacity EP exchange of [W, C, D] rows: C
+    (one exchange) unless the message outgrows the IPC staging on a single-GPU gloo
+    rehearsal, where it runs as chunks of [W, R, D] contiguous blocks (MoEBlock._ep_fixed lays
+    the rows out chunk-major, so no slab copies are needed)."""
+    st = get_state()
+    if (st is None or st.car is None or st.tp_size != st.world_size or not x.is_cuda
+            or x.dtype != torch.bfloat16 or D % 8):
+        return C
+    W = st.world_size
+    if W * C * D * 2 <= st.car.buffer_bytes or st.backend != "gloo":
+        return C  # one IPC launch, or RCCL all_to_all_single on a node
+    R = max(8, st.car.buffer_bytes // (2 * D * W) // 8 * 8)
+    return min(C, R)
+
+
+def ep_all_to_all_equal(recv: torch.Tensor, send: torch.Tensor, chunks: int = 1
+                        ) -> torch.Tensor:
     """All-to-all over the whole job with equal splits (the fixed-capacity EP dispatch /
     combine): the custom IPC kernel when the TP group is the whole job and the message fits
-    its staging (capturable on any control backend), else all_to_all_single."""
+    its staging (capturable on any control backend), else all_to_all_single.  chunks > 1: the
+    rows are chunk-major ([chunks, W, R, D], ep_chunk_rows) and every chunk is one IPC launch."""
     st = get_state()
+    if chunks > 1:
+        s2, r2 = send.view(chunks, -1), recv.view(chunks, -1)
+        for k in range(chunks):
+            st.car.all_to_all(s2[k], r2[k])
+        _UNCHECKED[0] = True
+        return recv
     if (st.car is not None and st.tp_size == st.world_size and st.car.a2a_ok(send)
             and recv.is_contiguous() and recv.dtype == send.dtype):
         return st.car.all_to_all(send.view(-1), recv.view(-1)).view_as(recv)
-    if (st.car is not None and st.tp_size == st.world_size and st.backend == "gloo"
-            and _car_pieces_ok(send, st.car) and send.numel() % (8 * st.world_size) == 0
-            and recv.is_contiguous() and recv.dtype == send.dtype):
-        # ranks sharing one GPU over a gloo control plane (single-GPU rehearsal of an EP
-        # prefill): the dispatch stays on the device as column slabs of the IPC kernel
-        W = st.world_size
-        seg = send.numel() // W
-        cap = max(8, st.car.buffer_bytes // send.element_size() // W // 8 * 8)
-        src, dst = send.view(W, seg), recv.view(W, seg)
-        for c0 in range(0, seg, cap):
-            c1 = min(seg, c0 + cap)
-            piece = src[:, c0:c1].contiguous()
-            out = torch.empty_like(piece)
-            st.car.all_to_all(piece.view(-1), out.view(-1))
-            dst[:, c0:c1].copy_(out)
-        _UNCHECKED[0] = True
-        return recv
     dist.all_to_all_single(recv, send)
     return recv
 
