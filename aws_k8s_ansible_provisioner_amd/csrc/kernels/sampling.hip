@@ -454,7 +454,7 @@ __device__ __forceinline__ int suffix_select(float v, float target, float* scrat
   return 255 - s_pos;
 }
 
-template <typename T>
+template <typename T, bool PASS_A>
 __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams p, int pass,
                                                                     SelState* st, float2* hist,
                                                                     int* tickets) {
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   // lanes never add to the same word (logits crowd into a few exponent bins, and same-word
   // LDS atomics inside one instruction serialise); passes B / C: per-wave histograms of the
   // few elements inside one high-byte bin (and, for top-k + top-p, above it)
-  __shared__ float lds[256 * 64];
+  __shared__ float lds[PASS_A ? 256 * 64 : 12 * 256];  // 64 KB only for pass A's lane copies
   __shared__ float scratch[16];
   const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
   const float temp = p.temperature ? p.temperature[row] : 0.f;
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   const int kk = p.top_k ? p.top_k[row] : 0;
   const float tp = p.top_p ? p.top_p[row] : 1.f;
   const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
-  if (pass == 0) {  // A: high byte of the whole row; count (top-k) or mass (top-p only)
+  if constexpr (PASS_A) {  // A: high byte of the whole row; count (top-k) or mass (top-p only)
     for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
     __syncthreads();
     if (has_k) {
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
       rs.p_hi = -1;
     }
     return;
-  }
+  } else {
   if (pass == 1) {  // B: low byte inside sel_hi (count + mass); top-k + top-p: masses above
     const int sh = rs.sel_hi;
     float* lc = lds;             // [4][256] low-byte counts
@@ -633,6 +633,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     p.out_tokens[row] = tok;
     if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - M - __logf(rs.Z);
   }
+  }  // passes B, C, D
 }
 
 int sample_chunks(int B, int V) {
@@ -650,24 +651,36 @@ long sample_ws_floats(int B) {
   return (long)B * (kMaxChunks * 8 + kSelWords + 2 * kHistRow);
 }
 
+// Chunks per row of the filter passes: each pass has a fixed cost per workgroup (publish,
+// ticket, two round trips), so they take fewer, larger chunks -- ~512 workgroups per pass
+// over the batch (one round on 256 CUs), at most sample_chunks
+static int filter_chunks(int B, int V) {
+  return max(1, min(sample_chunks(B, V), 512 / max(B, 1)));
+}
+
 void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int filtered,
                    hipStream_t s) {
   if (B == 0) return;
   const dim3 grid(sample_chunks(B, p.V), B);
+  const dim3 gridf(filter_chunks(B, p.V), B);
   SampPart* parts = (SampPart*)ws;
   SelState* st = reinterpret_cast<SelState*>(parts + (size_t)B * kMaxChunks);
   float2* hist = reinterpret_cast<float2*>(st + B);
   float* rowsum = reinterpret_cast<float*>(st);
   if (p.is_bf16) {
     sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum);
-    if (filtered)
-      for (int ps = 0; ps < 4; ++ps)
-        sample_pass_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
+    if (filtered) {
+      sample_pass_kernel<bf16, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
+      for (int ps = 1; ps < 4; ++ps)
+        sample_pass_kernel<bf16, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
+    }
   } else {
     sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum);
-    if (filtered)
-      for (int ps = 0; ps < 4; ++ps)
-        sample_pass_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
+    if (filtered) {
+      sample_pass_kernel<float, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
+      for (int ps = 1; ps < 4; ++ps)
+        sample_pass_kernel<float, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
+    }
   }
 }
 
