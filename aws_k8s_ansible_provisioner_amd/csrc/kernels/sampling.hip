@@ -113,22 +113,7 @@ __device__ __forceinline__ void visit_range(const T* x, int lo, int hi, bool vec
   if (vec_ok) {
     const int vlo = (lo + NV - 1) / NV, vhi = hi / NV;
     for (int i = lo + threadIdx.x; i < min(hi, vlo * NV); i += blockDim.x) f((float)x[i], i);
-    // U vectors per thread requested before any is used: a plain loop waits for every load in
-    // turn (one 16-B load in flight per wave: a 19k-element chunk took ~56 us, s5o)
-    constexpr int U = 8;
-    const int stride = blockDim.x;
-    int v = vlo + threadIdx.x;
-    for (; v + (U - 1) * stride < vhi; v += U * stride) {
-      typename Vec<T>::type q[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        q[u] = *reinterpret_cast<const typename Vec<T>::type*>(x + (size_t)(v + u * stride) * NV);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int j = 0; j < NV; ++j) f((float)q[u][j], (v + u * stride) * NV + j);
-    }
-    for (; v < vhi; v += stride) {
+    for (int v = vlo + threadIdx.x; v < vhi; v += blockDim.x) {
       const typename Vec<T>::type q =
           *reinterpret_cast<const typename Vec<T>::type*>(x + (size_t)v * NV);
 #pragma unroll
