@@ -454,33 +454,15 @@ __device__ __forceinline__ int suffix_select(float v, float target, float* scrat
   return 255 - s_pos;
 }
 
-// Wave-aggregated histogram add: the wave's lanes that hit the same bin (logits crowd into a
-// few key bins) are combined first -- one ballot round per distinct bin, a popcount (COUNT)
-// or a wave sum (mass) -- and only the round's leader adds to LDS.  Per-element LDS float
-// atomics bound the first build of these passes (47 % of wave cycles waiting on LDS, s5q).
-// bin < 0: the lane adds nothing.  Call with the whole wave (or the loop's active lanes).
-template <bool COUNT>
-__device__ __forceinline__ void wave_agg_add(float* h, int bin, float w) {
-  const int lane = threadIdx.x & 63;
-  uint64_t todo = __ballot(bin >= 0);
-  while (todo) {
-    const int leader = __builtin_ctzll(todo);
-    const int bl = __shfl(bin, leader, 64);
-    const uint64_t m = __ballot(bin == bl) & todo;
-    float sum;
-    if constexpr (COUNT) sum = (float)__popcll(m);
-    else sum = wave_sum(((m >> lane) & 1ull) ? w : 0.f);
-    if (lane == leader) atomicAdd(&h[bl], sum);
-    todo &= ~m;
-  }
-}
-
 template <typename T, bool PASS_A>
 __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams p, int pass,
                                                                     SelState* st, float2* hist,
                                                                     int* tickets) {
-  // per-wave histograms filled by wave-aggregated adds (wave_agg_add)
-  __shared__ float lds[12 * 256];
+  // pass A: a per-LANE copy of the high-byte histogram ([bin][lane], 64 KB): a wave's 64
+  // lanes never add to the same word (logits crowd into a few exponent bins, and same-word
+  // LDS atomics inside one instruction serialise); passes B / C: per-wave histograms of the
+  // few elements inside one high-byte bin (and, for top-k + top-p, above it)
+  __shared__ float lds[PASS_A ? 256 * 64 : 12 * 256];  // 64 KB only for pass A's lane copies
   __shared__ float scratch[16];
   const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
   const float temp = p.temperature ? p.temperature[row] : 0.f;
@@ -501,22 +483,21 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   const float tp = p.top_p ? p.top_p[row] : 1.f;
   const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
   if constexpr (PASS_A) {  // A: high byte of the whole row; count (top-k) or mass (top-p only)
-    for (int i = tid; i < 4 * 256; i += kChunkThreads) lds[i] = 0.f;
+    for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
     __syncthreads();
-    float* wh = lds + wid * 256;  // this wave's histogram
     if (has_k) {
       visit_range(x, lo, hi, vec_ok, [&](float v, int) {
-        wave_agg_add<true>(wh, k16_of(v) >> 8, 1.f);
+        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], 1.f);
       });
     } else {
       visit_range(x, lo, hi, vec_ok, [&](float v, int) {
-        wave_agg_add<false>(wh, k16_of(v) >> 8, __expf(v * invT - M));
+        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], __expf(v * invT - M));
       });
     }
     __syncthreads();
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) v += lds[w * 256 + tid];
+    float v = 0.f;  // bin tid over the 64 lane copies (rotated: conflict-free)
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) v += lds[tid * 64 + ((j + lane) & 63)];
     float2 mine[1] = {make_float2(v, 0.f)}, tot[1];
     if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
     float above;
@@ -540,10 +521,12 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     const bool above_too = has_k && has_p;
     visit_range(x, lo, hi, vec_ok, [&](float v, int) {
       const int k = k16_of(v), h = k >> 8;
-      const float e = __expf(v * invT - M);
-      wave_agg_add<true>(lc + wid * 256, h == sh ? (k & 255) : -1, 1.f);
-      wave_agg_add<false>(lm + wid * 256, h == sh ? (k & 255) : -1, e);
-      if (above_too) wave_agg_add<false>(hm + wid * 256, h > sh ? h : -1, e);
+      if (h == sh) {
+        atomicAdd(&lc[wid * 256 + (k & 255)], 1.f);
+        atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
+      } else if (above_too && h > sh) {
+        atomicAdd(&hm[wid * 256 + h], __expf(v * invT - M));
+      }
     });
     __syncthreads();
     float cc = 0.f, mm = 0.f, hh = 0.f;
@@ -591,8 +574,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     __syncthreads();
     visit_range(x, lo, hi, vec_ok, [&](float v, int) {
       const int k = k16_of(v);
-      wave_agg_add<false>(lm + wid * 256, (k >> 8) == ph ? (k & 255) : -1,
-                          __expf(v * invT - M));
+      if ((k >> 8) == ph) atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
     });
     __syncthreads();
     float mm = 0.f;

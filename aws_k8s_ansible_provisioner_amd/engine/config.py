@@ -16,6 +16,7 @@ class EngineConfig:
     block_size: int = 32
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: Optional[int] = None      # override the memory-derived block count
+    kv_cache_max_gib: Optional[float] = None  # cap on the memory-derived KV cache size
     enable_prefix_caching: bool = True
     enforce_eager: bool = False               # disable hipGraph decode
     cuda_graph_max_bs: Optional[int] = None   # largest captured decode batch

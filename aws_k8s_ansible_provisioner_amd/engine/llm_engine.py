@@ -441,7 +441,7 @@ class LLMEngine:
             elif not st.stream:
                 continue  # first-token event of a non-streaming request: metrics only
             kvp = None
-            if st.hold_kv and st.finished:
+            if st.hold_kv and st.finished and st.output_ids:  # (an aborted prompt hands off nothing)
                 kvp = {"transfer_id": iid, "num_prompt": len(st.prompt_ids),
                        "prompt_token_ids": st.prompt_ids, "first_token": st.output_ids[0],
                        "remote_rank": self.rank, "num_blocks": len(self.sched.held_blocks(iid)),

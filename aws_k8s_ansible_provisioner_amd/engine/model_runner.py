@@ -180,6 +180,8 @@ class ModelRunner:
         reserve = act + 3 * 2**30
         budget = min(total * self.ecfg.gpu_memory_utilization - used, free) - reserve
         n = int(budget // per_block)
+        if self.ecfg.kv_cache_max_gib:
+            n = min(n, int(self.ecfg.kv_cache_max_gib * 2**30 // per_block))
         if n < self.max_blocks:
             raise RuntimeError(f"not enough HBM for the KV cache ({budget / 2**30:.1f} GiB)")
         return n
