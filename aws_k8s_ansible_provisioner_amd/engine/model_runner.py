@@ -116,7 +116,7 @@ class ModelRunner:
         # decode graphs whose sampler also runs the top-k / top-p threshold passes: captured on
         # first use by a batch that needs them (single-rank engines; multi-rank engines capture
         # their only graphs with the passes, since a lazy capture would issue collectives alone)
-        # decode graph variants by sampler mode (see _sample_mode), captured on first use
+        # decode graph variants by sampler mode (see _sample_mode), captured with the buckets
         self.graphs_v: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._capture_mode: Optional[str] = None
         self.ep_overflow_steps = 0  # steps re-run after an EP dispatch overflow
@@ -326,30 +326,13 @@ class ModelRunner:
         return "plain"
 
     def _graph_for(self, n: int, B: int):
-        """The decode graph of bucket n for a batch of B rows in its sampler mode: the one
-        captured at start (mode "plain"; "filtered" on multi-rank engines) or a variant
-        captured on the first batch that needs it."""
+        """The decode graph of bucket n for a batch of B rows in its sampler mode (all modes
+        were captured with the buckets; see capture_graphs)."""
         g = self.graphs.get(n)
-        mode = self._sample_mode(B)
-        if g is None or self.ps.world_size > 1 or mode == "plain":
+        if g is None or self.ps.world_size > 1:
             return g
-        key = (mode, n)
-        if key not in self.graphs_v:
-            stream = torch.cuda.Stream()
-            stream.wait_stream(torch.cuda.current_stream())
-            self._capture_mode = mode
-            try:
-                with torch.cuda.stream(stream):
-                    self._decode_body(n)  # warm-up: the same step the replay then redoes
-                stream.synchronize()
-                gv = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gv, pool=self.graph_pool, stream=stream):
-                    self._decode_body(n)
-            finally:
-                self._capture_mode = None
-            torch.cuda.current_stream().wait_stream(stream)
-            self.graphs_v[key] = gv
-        return self.graphs_v[key]
+        mode = self._sample_mode(B)
+        return g if mode == "plain" else self.graphs_v[(mode, n)]
 
     PREFILL_FIELDS = ("input_ids", "positions", "slots", "seq_lens", "q_start", "block_tables",
                       "tile_seq", "tile_row", "logits_idx", "temperature", "top_p", "top_k",
@@ -707,17 +690,25 @@ class ModelRunner:
             dist.barrier()
         self.graph_pool = torch.cuda.graph_pool_handle()
         stream = torch.cuda.Stream()
-        self._capture_mode = "filtered" if self.ps.world_size > 1 else "plain"
-        for b in reversed(self.buckets):
-            with torch.cuda.stream(stream):
-                self._decode_body(b)  # warm-up (hipBLASLt heuristics, allocator)
-            stream.synchronize()
-            if self._graph_has_collectives():
-                drain_pending_collectives(self.ps)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
-                self._decode_body(b)
-            self.graphs[b] = g
+        # one graph per bucket and sampler mode (single-rank engines: "plain", "greedy" and
+        # "filtered", all captured here -- a capture while serving would race the P/D KV
+        # receiver's work; multi-rank engines: "filtered" only, correct for every batch)
+        modes = ["filtered"] if self.ps.world_size > 1 else ["plain", "greedy", "filtered"]
+        for mode in modes:
+            self._capture_mode = mode
+            for b in reversed(self.buckets):
+                with torch.cuda.stream(stream):
+                    self._decode_body(b)  # warm-up (hipBLASLt heuristics, allocator)
+                stream.synchronize()
+                if self._graph_has_collectives():
+                    drain_pending_collectives(self.ps)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
+                    self._decode_body(b)
+                if mode == modes[0]:
+                    self.graphs[b] = g
+                else:
+                    self.graphs_v[(mode, b)] = g
         self._capture_mode = None
         torch.cuda.synchronize()
         if tunable:
