@@ -82,7 +82,10 @@ __device__ __forceinline__ void pg_sync() {
 // pieces per half-tile per wave: 2 with 8 waves, 4 with 4 waves)
 template <int P>
 __device__ __forceinline__ void pg_wait(int later) {
-  if (later >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P) : "memory");
+  if (later >= 6) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * P) : "memory");
+  else if (later == 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * P) : "memory");
+  else if (later == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * P) : "memory");
+  else if (later == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P) : "memory");
   else if (later == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
   else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -165,7 +168,7 @@ struct PgAcc {
   f32x4 v[8][NJ2];
 };
 
-template <int NB, bool SILU_ROWS, int WAVES, typename ACC>
+template <int NB, bool SILU_ROWS, int WAVES, typename ACC, int SCHED = 1>
 __device__ __forceinline__ void pg_mainloop(bf16x8* lds, const __amdgpu_buffer_rsrc_t rx,
                                             const __amdgpu_buffer_rsrc_t rw, int ldx, int K,
                                             int nhalf, int m0, int n0, int kt0, int nk,
@@ -264,6 +267,66 @@ __device__ __forceinline__ void pg_mainloop(bf16x8* lds, const __amdgpu_buffer_r
     __builtin_amdgcn_s_setprio(0);
   };
 
+  if constexpr (SCHED == 2) {
+    // ---- early-issue schedule: every half-tile goes out as soon as its slot's previous
+    // reads retired -- A top / W left of tile t+2 right after phase 1's barrier of tile t
+    // (their slot's last reads were phase 4 of t-1), W right / A bottom of t+2 right after
+    // phase 4's barrier of t (last reads: phase 1 of t).  Issue order stays the consumption
+    // order (seq 4 j + h), so every wait is still a counted in-order vmcnt, and each
+    // half-tile is requested 1.25-1.75 tiles ahead (1.0-1.25 in the schedule below).
+    issue(H0{}, 0);
+    issue(H1{}, 0);
+    issue(H2{}, 0);
+    issue(H3{}, 0);
+    issue(H0{}, 1);
+    issue(H1{}, 1);
+    issue(H2{}, 1);
+    issue(H3{}, 1);
+    auto out = [&](int need, int last) { return max(0, min(last, 4 * nk - 1) - need); };
+    pg_wait<P>(out(1, 7));
+    pg_sync();
+    rd_a(at, lds, 0);
+    rd_b(bl, lds, 0);
+    for (int t = 0; t < nk; ++t) {
+      const bf16x8* cur = lds + (t & 1) * PG_BUF;
+      const bf16x8* nxt = lds + ((t + 1) & 1) * PG_BUF;
+      // phase 1: W right + A bottom of t landed (seq 4t+3; issued through 4t+7)
+      pg_wait<P>(out(4 * t + 3, 4 * t + 7));
+      pg_sync();
+      rd_b(br, cur, 1);
+      if constexpr (NB == 4) {
+        issue(H0{}, t + 2);
+        issue(H1{}, t + 2);
+        mma(at, bl, 0, 0);
+        pg_sync();  // (SwiGLU form: A bottom read after a barrier, as below)
+        rd_a(ab, cur, 1);
+        mma(at, br, 0, NJ);
+        pg_sync();
+        mma(ab, bl, 4, 0);
+      } else {
+        rd_a(ab, cur, 1);
+        issue(H0{}, t + 2);
+        issue(H1{}, t + 2);
+        mma(at, bl, 0, 0);
+        mma(at, br, 0, NJ);
+        mma(ab, bl, 4, 0);
+      }
+      // phase 4: A top + W left of t+1 (seq 4t+5; issued through 4t+9)
+      if (t + 1 < nk) {
+        pg_wait<P>(out(4 * t + 5, 4 * t + 9));
+        pg_sync();
+        rd_a(at, nxt, 0);
+        rd_b(bl, nxt, 0);
+      } else {
+        pg_sync();
+      }
+      issue(H2{}, t + 2);
+      issue(H3{}, t + 2);
+      mma(ab, br, 4, NJ);
+    }
+    return;
+  }
+
   // ---- prologue: half-tiles 0..5 in flight, tile 0's A top + W left in registers -------------
   issue(H0{}, 0);
   issue(H1{}, 0);
@@ -331,7 +394,7 @@ __device__ __forceinline__ void pg_mainloop(bf16x8* lds, const __amdgpu_buffer_r
   }
 }
 
-template <int EPI, bool GROUPED, int NB, int WAVES>
+template <int EPI, bool GROUPED, int NB, int WAVES, int SCHED = 1>
 __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_kernel(PGemmArgs p) {
   using G = PgGeo<WAVES>;
   constexpr int NJ = G::NJ;
@@ -353,8 +416,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_kernel(PGemmArgs p) {
       (void*)W, (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
   PgAcc<2 * PgGeo<WAVES>::NJ> accs;
   auto& acc = accs.v;
-  pg_mainloop<NB, EPI == EPI_SILU, WAVES>(lds, rx, rw, p.ldx, p.K, p.N >> 1, m0, n0, 0,
-                                          p.K / PG_BK, accs);
+  pg_mainloop<NB, EPI == EPI_SILU, WAVES, decltype(accs), SCHED>(lds, rx, rw, p.ldx, p.K,
+                                                                 p.N >> 1, m0, n0, 0,
+                                                                 p.K / PG_BK, accs);
 
   // ---- epilogue: lane holds rows wm*128 + i*16 + fr, 4 consecutive cols per fragment ---------
   bf16* Y = static_cast<bf16*>(p.Y);
@@ -485,7 +549,7 @@ __device__ __forceinline__ float pg_row_scale(const DGemmArgs& p, int row) {
   return p.ss_in != nullptr ? rsqrtf(p.ss_in[row] / (float)p.K + p.eps) : 1.f;
 }
 
-template <int EPI, int NB, int WAVES>
+template <int EPI, int NB, int WAVES, int SCHED = 1>
 __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_sk_kernel(DGemmArgs p, int splits) {
   using G = PgGeo<WAVES>;
   constexpr int NJ = G::NJ, THREADS = G::THREADS;
@@ -509,8 +573,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_sk_kernel(DGemmArgs p, in
       const_cast<void*>(p.W), (short)0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
   PgAcc<2 * PgGeo<WAVES>::NJ> accs;
   auto& acc = accs.v;
-  pg_mainloop<NB, EPI == EPI_SILU, WAVES>(lds, rx, rw, p.ldx, p.ldw, p.N >> 1, m0, n0, kt0,
-                                          kt1 - kt0, accs);
+  pg_mainloop<NB, EPI == EPI_SILU, WAVES, decltype(accs), SCHED>(lds, rx, rw, p.ldx, p.ldw,
+                                                                 p.N >> 1, m0, n0, kt0,
+                                                                 kt1 - kt0, accs);
 
   if (splits == 1) {  // whole K in this workgroup: the epilogue straight from the registers
 #pragma unroll
@@ -613,6 +678,16 @@ long pgemm_sk_ws_floats(int M, int N, int splits) {
 
 // Wave form of the 256 x 256 body: AKAP_PGEMM_WAVES = 8 (2 x 4 waves of 128 x 64) or 4 (2 x 2
 // waves of 128 x 128), read once per process.
+// K-loop issue schedule: AKAP_PGEMM_SCHED = 1 (half-tiles requested 1.0-1.25 tiles ahead) or
+// 2 (early issue, 1.25-1.75 tiles ahead; pg_mainloop), read once per process
+int pgemm_sched() {
+  static int v = [] {
+    const char* e = getenv("AKAP_PGEMM_SCHED");
+    return (e && atoi(e) == 2) ? 2 : 1;
+  }();
+  return v;
+}
+
 int pgemm_waves() {
   static int w = [] {
     const char* e = getenv("AKAP_PGEMM_WAVES");
@@ -621,24 +696,42 @@ int pgemm_waves() {
   return w;
 }
 
-template <int WAVES>
+template <int WAVES, int SCHED>
 static void launch_pgemm_sk_w(const DGemmArgs& p, int splits, hipStream_t st) {
   const int grid = ((p.M + PG_T - 1) / PG_T) * (p.N / PG_T) * splits;
   constexpr int T = WAVES * 64;
-  if (p.epi == EPI_SILU) pgemm_sk_kernel<EPI_SILU, 4, WAVES><<<grid, T, 0, st>>>(p, splits);
+  if (p.epi == EPI_SILU)
+    pgemm_sk_kernel<EPI_SILU, 4, WAVES, SCHED><<<grid, T, 0, st>>>(p, splits);
   else if (p.epi == EPI_RESNORM)
-    pgemm_sk_kernel<EPI_RESNORM, 2, WAVES><<<grid, T, 0, st>>>(p, splits);
-  else pgemm_sk_kernel<EPI_STORE, 2, WAVES><<<grid, T, 0, st>>>(p, splits);
+    pgemm_sk_kernel<EPI_RESNORM, 2, WAVES, SCHED><<<grid, T, 0, st>>>(p, splits);
+  else pgemm_sk_kernel<EPI_STORE, 2, WAVES, SCHED><<<grid, T, 0, st>>>(p, splits);
 }
 
 void launch_pgemm_sk(const DGemmArgs& p, int splits, hipStream_t st) {
   if (p.M == 0) return;
-  if (pgemm_waves() == 4) launch_pgemm_sk_w<4>(p, splits, st);
-  else launch_pgemm_sk_w<8>(p, splits, st);
+  if (pgemm_waves() == 4) {
+    if (pgemm_sched() == 2) launch_pgemm_sk_w<4, 2>(p, splits, st);
+    else launch_pgemm_sk_w<4, 1>(p, splits, st);
+  } else {
+    if (pgemm_sched() == 2) launch_pgemm_sk_w<8, 2>(p, splits, st);
+    else launch_pgemm_sk_w<8, 1>(p, splits, st);
+  }
 }
 
 bool pgemm_supported(int M, int N, int K) {
   return M > 0 && N > 0 && N % PG_T == 0 && K >= PG_BK && K % PG_BK == 0;
+}
+
+template <int WAVES, int SCHED>
+static void launch_pgemm_w(const PGemmArgs& p, int epi, int grid, hipStream_t st) {
+  constexpr int T = WAVES * 64;
+  if (p.groups > 0) {
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, 4, WAVES, SCHED><<<grid, T, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, true, 2, WAVES, SCHED><<<grid, T, 0, st>>>(p);
+  } else {
+    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, 4, WAVES, SCHED><<<grid, T, 0, st>>>(p);
+    else pgemm_kernel<EPI_STORE, false, 2, WAVES, SCHED><<<grid, T, 0, st>>>(p);
+  }
 }
 
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
@@ -648,23 +741,13 @@ void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
   // two barriers per K tile (measured 1-4 % faster than four, profiles/r4_pgemm_nb_ab.log); the
   // SwiGLU form keeps four: with both fragment sets read in phase 1 it would spill
+  const bool s2 = pgemm_sched() == 2;
   if (pgemm_waves() == 4) {
-    constexpr int T = 4 * 64;
-    if (p.groups > 0) {
-      if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, 4, 4><<<grid, T, 0, st>>>(p);
-      else pgemm_kernel<EPI_STORE, true, 2, 4><<<grid, T, 0, st>>>(p);
-    } else {
-      if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, 4, 4><<<grid, T, 0, st>>>(p);
-      else pgemm_kernel<EPI_STORE, false, 2, 4><<<grid, T, 0, st>>>(p);
-    }
-    return;
-  }
-  if (p.groups > 0) {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, true, 4, 8><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, true, 2, 8><<<grid, PG_THREADS, 0, st>>>(p);
+    if (s2) launch_pgemm_w<4, 2>(p, epi, grid, st);
+    else launch_pgemm_w<4, 1>(p, epi, grid, st);
   } else {
-    if (epi == EPI_SILU) pgemm_kernel<EPI_SILU, false, 4, 8><<<grid, PG_THREADS, 0, st>>>(p);
-    else pgemm_kernel<EPI_STORE, false, 2, 8><<<grid, PG_THREADS, 0, st>>>(p);
+    if (s2) launch_pgemm_w<8, 2>(p, epi, grid, st);
+    else launch_pgemm_w<8, 1>(p, epi, grid, st);
   }
 }
 
