@@ -282,6 +282,11 @@ __global__ __launch_bounds__(256) void car_multi_kernel(CarMulti m, long n8, int
 }
 
 // All-gather: rank r's shard in[R, n] -> out[R, W*n] columns [r*n, (r+1)*n); n % 8 == 0.
+// Each thread moves kCarU vectors per trip (all loads in flight before the stores: one
+// vector per thread left a 64-block grid latency-bound at ~1.6 TB/s); staging and reading use
+// the same index -> block map, so the per-block flag exchange still covers what it reads.
+constexpr int kCarU = 4;
+
 __device__ __forceinline__ void car_allgather(const CarArgs& a, int bid, int nblk,
                                               const bf16* __restrict__ in,
                                               bf16* __restrict__ out, long n8, int n) {
@@ -289,22 +294,40 @@ __device__ __forceinline__ void car_allgather(const CarArgs& a, int bid, int nbl
   const size_t par = (ep & 1) * a.half_elems;
   const __amdgpu_buffer_rsrc_t mine = car_rsrc(a.bufs[a.rank], a);
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
-  const long stride = (long)nblk * 256;
-  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride)
-    car_st(mine, par + (size_t)i * 8, src[i]);
+  const long step = (long)nblk * 256 * kCarU;
+  const long first = (long)bid * 256 * kCarU + threadIdx.x;
+  for (long i0 = first; i0 < n8; i0 += step) {
+    bf16x8 v[kCarU];
+#pragma unroll
+    for (int k = 0; k < kCarU; ++k)
+      if (i0 + k * 256 < n8) v[k] = src[i0 + k * 256];
+#pragma unroll
+    for (int k = 0; k < kCarU; ++k)
+      if (i0 + k * 256 < n8) car_st(mine, par + (size_t)(i0 + k * 256) * 8, v[k]);
+  }
   car_barrier(a, bid, ep, 0);
   const long W = a.world;
-  for (long i = (long)bid * 256 + threadIdx.x; i < n8; i += stride) {
-    bf16x8 v[kCarMaxRanks];
+  for (long i0 = first; i0 < n8; i0 += step) {
+    bf16x8 v[kCarMaxRanks][kCarU];
 #pragma unroll
-    for (int p = 0; p < kCarMaxRanks; ++p)  // every peer load in flight before the stores
-      if (p < a.world && p != a.rank) v[p] = car_ld(car_rsrc(a.bufs[p], a), par + (size_t)i * 8);
-    const long e = i * 8, row = e / n, col = e % n;
-    bf16* o = out + row * W * n + col;
+    for (int p = 0; p < kCarMaxRanks; ++p)  // every load in flight before the stores
 #pragma unroll
-    for (int p = 0; p < kCarMaxRanks; ++p) {
-      if (p >= a.world) break;
-      *reinterpret_cast<bf16x8*>(o + (long)p * n) = p == a.rank ? src[i] : v[p];
+      for (int k = 0; k < kCarU; ++k) {
+        const long i = i0 + k * 256;
+        if (p < a.world && i < n8)
+          v[p][k] = p == a.rank ? src[i] : car_ld(car_rsrc(a.bufs[p], a), par + (size_t)i * 8);
+      }
+#pragma unroll
+    for (int k = 0; k < kCarU; ++k) {
+      const long i = i0 + k * 256;
+      if (i >= n8) break;
+      const long e = i * 8, row = e / n, col = e % n;
+      bf16* o = out + row * W * n + col;
+#pragma unroll
+      for (int p = 0; p < kCarMaxRanks; ++p) {
+        if (p >= a.world) break;
+        *reinterpret_cast<bf16x8*>(o + (long)p * n) = v[p][k];
+      }
     }
   }
 }
@@ -342,22 +365,39 @@ __device__ __forceinline__ void car_alltoall(const CarArgs& a, int bid, int nblk
   const __amdgpu_buffer_rsrc_t mine = car_rsrc(a.bufs[a.rank], a);
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
   bf16x8* dst = reinterpret_cast<bf16x8*>(out);
-  const long stride = (long)nblk * 256;
+  const long step = (long)nblk * 256 * kCarU;
+  const long first = (long)bid * 256 * kCarU + threadIdx.x;
   const int W = a.world;
-  for (long i = (long)bid * 256 + threadIdx.x; i < seg8; i += stride)
-    for (int d = 0; d < W; ++d)
-      if (d != a.rank) car_st(mine, par + (size_t)(d * seg8 + i) * 8, src[d * seg8 + i]);
-  car_barrier(a, bid, ep, 0);
-  for (long i = (long)bid * 256 + threadIdx.x; i < seg8; i += stride) {
-    bf16x8 v[kCarMaxRanks];
+  for (long i0 = first; i0 < seg8; i0 += step)
+    for (int d = 0; d < W; ++d) {
+      if (d == a.rank) continue;
+      bf16x8 v[kCarU];
 #pragma unroll
-    for (int p = 0; p < kCarMaxRanks; ++p)  // every peer load in flight before the stores
-      if (p < W && p != a.rank)
-        v[p] = car_ld(car_rsrc(a.bufs[p], a), par + (size_t)(a.rank * seg8 + i) * 8);
+      for (int k = 0; k < kCarU; ++k)
+        if (i0 + k * 256 < seg8) v[k] = src[d * seg8 + i0 + k * 256];
+#pragma unroll
+      for (int k = 0; k < kCarU; ++k)
+        if (i0 + k * 256 < seg8) car_st(mine, par + (size_t)(d * seg8 + i0 + k * 256) * 8, v[k]);
+    }
+  car_barrier(a, bid, ep, 0);
+  for (long i0 = first; i0 < seg8; i0 += step) {
+    bf16x8 v[kCarMaxRanks][kCarU];
+#pragma unroll
+    for (int p = 0; p < kCarMaxRanks; ++p)  // every load in flight before the stores
+#pragma unroll
+      for (int k = 0; k < kCarU; ++k) {
+        const long i = i0 + k * 256;
+        if (p < W && i < seg8)
+          v[p][k] = p == a.rank ? src[a.rank * seg8 + i]
+                                : car_ld(car_rsrc(a.bufs[p], a),
+                                         par + (size_t)(a.rank * seg8 + i) * 8);
+      }
 #pragma unroll
     for (int p = 0; p < kCarMaxRanks; ++p) {
       if (p >= W) break;
-      dst[p * seg8 + i] = p == a.rank ? src[a.rank * seg8 + i] : v[p];
+#pragma unroll
+      for (int k = 0; k < kCarU; ++k)
+        if (i0 + k * 256 < seg8) dst[p * seg8 + i0 + k * 256] = v[p][k];
     }
   }
 }

@@ -267,8 +267,9 @@ def _ipc_siblings_worker(rank, world, port, q):
         res = []
         for it in range(4):
             g = torch.Generator().manual_seed(100 * it + rank)
-            shard = torch.randn(37, 136, generator=g).to(torch.bfloat16).to(DEV)
-            out = torch.empty(37, 136 * world, dtype=torch.bfloat16, device=DEV)
+            cols = 136 * (40 if it == 3 else 1)
+            shard = torch.randn(37, cols, generator=g).to(torch.bfloat16).to(DEV)
+            out = torch.empty(37, cols * world, dtype=torch.bfloat16, device=DEV)
             car.all_gather(shard, out)
             x = torch.randn(4096, generator=g).to(torch.bfloat16).to(DEV)
             car.all_reduce(x)
@@ -278,7 +279,8 @@ def _ipc_siblings_worker(rank, world, port, q):
                 b.copy_(torch.arange(b.numel(), dtype=torch.int64).remainder(251).to(torch.uint8))
             car.broadcast(b, 0)
             # equal-segment all-to-all: segment d of rank r holds r * 1000 + d * 10 + j % 7
-            seg = 24 * (it + 1)
+            # (it 3: several unrolled trips per block plus a ragged tail)
+            seg = 24 * (it + 1) + (40000 if it == 3 else 0)
             send = torch.cat([(torch.arange(seg) % 7 + rank * 1000 + d * 10).float()
                               for d in range(world)]).to(torch.bfloat16).to(DEV)
             recv = torch.empty_like(send)
@@ -317,11 +319,12 @@ def test_custom_allgather_broadcast_alltoall_ipc_processes(world):
     for r in range(world):
         assert out[r][0] == 0, out[r][0]
     for it in range(4):
-        shards = [torch.randn(37, 136, generator=torch.Generator().manual_seed(100 * it + r))
+        cols = 136 * (40 if it == 3 else 1)
+        shards = [torch.randn(37, cols, generator=torch.Generator().manual_seed(100 * it + r))
                   .to(torch.bfloat16).float().numpy() for r in range(world)]
         want = np.concatenate(shards, axis=1)
         bexp = (np.arange(2048 + 16 * it) % 251).astype(np.uint8)
-        seg = 24 * (it + 1)
+        seg = 24 * (it + 1) + (40000 if it == 3 else 0)
         for r in range(world):
             got, b, a2a = out[r][1][it]
             assert np.array_equal(got, want), (r, it)
