@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void car_multi_kernel(CarMulti m, long n8, int
 // Each thread moves kCarU vectors per trip (all loads in flight before the stores: one
 // vector per thread left a 64-block grid latency-bound at ~1.6 TB/s); staging and reading use
 // the same index -> block map, so the per-block flag exchange still covers what it reads.
-constexpr int kCarU = 4;
+constexpr int kCarU = 8;
 
 __device__ __forceinline__ void car_allgather(const CarArgs& a, int bid, int nblk,
                                               const bf16* __restrict__ in,
