@@ -57,13 +57,13 @@ __device__ __forceinline__ ArgBest block_argmax(ArgBest b, float* sv, int* si) {
 //    with 16-byte vector loads and produces, in that single pass,
 //      greedy rows   the chunk's argmax (first index on ties);
 //      T > 0 rows    the chunk's max and partition sum of z = x / T (online: rescaled when the
-//                    max moves) and, for rows with top-k / top-p, the key range.
+//                    max moves).
 //    The chunk publishes a 32-byte partial record with write-through (sc1) stores and takes
 //    a ticket on the row's counter (MI355X_MICROARCH.md "Valid forms", sc1 table row 1: no
 //    release / acquire fence -- each costs ~1.7 us and more behind a freshly written logits
 //    tensor); the LAST chunk of the row reads the S records with sc1 loads, combines them
 //    (max, rescaled sum), re-arms the counter and writes the token + log-prob of a greedy row,
-//    or the row summary (M, Z, key range) of a row with filters; a row without filters is
+//    or the row summary (M, Z) of a row with filters; a row without filters is
 //    drawn there by inverse CDF: u(seed, step) * Z picks the chunk from the prefix of the
 //    chunk masses, then the workgroup rescans that one chunk (a block scan of per-thread run
 //    masses) for the token -- exact sampling with one exp per element in the main pass and
@@ -90,7 +90,7 @@ struct SampPart {  // one chunk's partial record (32 B = two 16-B vectors)
   int unused1;
   float am;        // argmax value (greedy rows)
   int ai;
-  uint32_t kmin, kmax;  // key range of the chunk
+  uint32_t unused2, unused3;
 };
 
 template <typename T>
@@ -106,22 +106,43 @@ struct Vec<float> {
   using type = f32x4;
 };
 
-// Visit x[lo, hi) as (value, index) with 16-byte loads where the row is aligned.
+// Visit x[lo, hi) as f(value, index, ok) with 16-byte loads where the row is aligned.  The
+// vector loop issues 4 loads per thread before consuming the oldest: with one load per trip
+// every trip paid a full L2 / HBM round trip (load, s_waitcnt vmcnt(0), use), and a chunk
+// workgroup's few trips per thread were latency-bound, not bandwidth-bound.  Lanes past the
+// range still run f, with ok = false and the value -inf (so a visitor's work and the load
+// feeding it stay outside any branch: a load the compiler sinks into a conditional block
+// leaves the wait counter unknown, and every later wait becomes vmcnt(0)); visitors that
+// count or test keys must honour ok.
 template <typename T, typename F>
 __device__ __forceinline__ void visit_range(const T* x, int lo, int hi, bool vec_ok, F&& f) {
   constexpr int NV = Vec<T>::N;
+  using VT = typename Vec<T>::type;
   if (vec_ok) {
     const int vlo = (lo + NV - 1) / NV, vhi = hi / NV;
-    for (int i = lo + threadIdx.x; i < min(hi, vlo * NV); i += blockDim.x) f((float)x[i], i);
-    for (int v = vlo + threadIdx.x; v < vhi; v += blockDim.x) {
-      const typename Vec<T>::type q =
-          *reinterpret_cast<const typename Vec<T>::type*>(x + (size_t)v * NV);
+    for (int i = lo + threadIdx.x; i < min(hi, vlo * NV); i += blockDim.x) f((float)x[i], i, true);
+    const VT* xv = reinterpret_cast<const VT*>(x);
+    const int bd = blockDim.x;
+    auto use = [&](const VT& q, int v, bool ok) {
 #pragma unroll
-      for (int j = 0; j < NV; ++j) f((float)q[j], v * NV + j);
+      for (int j = 0; j < NV; ++j) f(ok ? (float)q[j] : -INFINITY, v * NV + j, ok);
+    };
+    // batches of 4 unconditional loads (index clamped to the last vector), consumed
+    // oldest-first behind counted waits
+    if (vlo < vhi) {
+      const int last = vhi - 1;
+      for (int v = vlo + threadIdx.x; v < vhi; v += 4 * bd) {
+        VT q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = xv[min(v + u * bd, last)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) use(q[u], v + u * bd, v + u * bd < vhi);
+      }
     }
-    for (int i = max(vhi * NV, vlo * NV) + threadIdx.x; i < hi; i += blockDim.x) f((float)x[i], i);
+    for (int i = max(vhi * NV, vlo * NV) + threadIdx.x; i < hi; i += blockDim.x)
+      f((float)x[i], i, true);
   } else {
-    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) f((float)x[i], i);
+    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) f((float)x[i], i, true);
   }
 }
 
@@ -156,29 +177,25 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   // ---- one pass over the chunk (the three row kinds as separate loops: no per-element
   // branch on the row kind) ----
   float m = -INFINITY, sum = 0.f;
-  uint32_t kmin = 0xffffffffu, kmax = 0u;
   ArgBest best{-INFINITY, 0x7fffffff};
   if (!need_sum) {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int i) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
       if (v > best.v) { best.v = v; best.i = i; }  // ascending i per thread: first max kept
     });
   } else if (!greedy && !filt) {
     // max and partition sum only (one exp per element): the draw is an inverse-CDF pick by
     // the last chunk below, so no per-element RNG / logs in this pass
-    visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool) {
       const float z = v * invT;
       if (z > m) { sum = sum * __expf(m - z) + 1.f; m = z; }
       else if (z > -INFINITY) sum += __expf(z - m);
     });
-  } else {  // greedy with log-probs, or a filtered row (also its key range)
-    visit_range(x, lo, hi, vec_ok, [&](float v, int i) {
+  } else {  // greedy with log-probs, or a filtered row
+    visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
       if (v > best.v) { best.v = v; best.i = i; }
       const float z = v * invT;
       if (z > m) { sum = sum * __expf(m - z) + 1.f; m = z; }
       else if (z > -INFINITY) sum += __expf(z - m);
-      const uint32_t k = fkey(v);
-      kmin = min(kmin, k);
-      kmax = max(kmax, k);
     });
   }
   // workgroup reductions
@@ -188,16 +205,6 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
     M = block_max(m, sv);
     Z = block_sum(m == -INFINITY ? 0.f : sum * __expf(m - M), sv);
   }
-  __shared__ uint32_t s_kmin, s_kmax;
-  if (filt) {  // exact integer min / max of the keys
-    if (threadIdx.x == 0) { s_kmin = 0xffffffffu; s_kmax = 0u; }
-    __syncthreads();
-    atomicMin(&s_kmin, kmin);
-    atomicMax(&s_kmax, kmax);
-    __syncthreads();
-    kmin = s_kmin;
-    kmax = s_kmax;
-  }
   // ---- publish the partial (sc1 stores), take a ticket ----
   const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(ws + (size_t)row * S), (short)0, (int)(S * sizeof(SampPart)), 0x00020000);
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
     u32x4 a, b2;
     a[0] = __float_as_uint(M); a[1] = __float_as_uint(Z);
     a[2] = 0u; a[3] = 0u;
-    b2[0] = __float_as_uint(best.v); b2[1] = (uint32_t)best.i; b2[2] = kmin; b2[3] = kmax;
+    b2[0] = __float_as_uint(best.v); b2[1] = (uint32_t)best.i; b2[2] = 0u; b2[3] = 0u;
     __builtin_amdgcn_raw_buffer_store_b128(a, rws, c * 32, 0, kSc1);
     __builtin_amdgcn_raw_buffer_store_b128(b2, rws, c * 32 + 16, 0, kSc1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -223,13 +230,11 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
     const int l = threadIdx.x;
     float rm = -INFINITY, rs = 0.f;
     ArgBest a{-INFINITY, 0x7fffffff};
-    uint32_t rkmin = 0xffffffffu, rkmax = 0u;
     if (l < S) {
       const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32, 0, kSc1);
       const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32 + 16, 0, kSc1);
       rm = __uint_as_float(v0[0]); rs = __uint_as_float(v0[1]);
       a = ArgBest{__uint_as_float(v1[0]), (int)v1[1]};
-      rkmin = v1[2]; rkmax = v1[3];
     }
     const float Mr = wave_max(rm);
     // chunk l's mass in units of exp(z - Mr); its inclusive prefix over the chunks
@@ -245,8 +250,6 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
     for (int o = 32; o > 0; o >>= 1) {
       ArgBest ca{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
       a = arg_better(a, ca);
-      rkmin = min(rkmin, (uint32_t)__shfl_xor((int)rkmin, o, 64));
-      rkmax = max(rkmax, (uint32_t)__shfl_xor((int)rkmax, o, 64));
     }
     if (draw) {
       // inverse CDF, level 1: the chunk whose prefix mass first reaches u * Z
@@ -486,11 +489,11 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
     __syncthreads();
     if (has_k) {
-      visit_range(x, lo, hi, vec_ok, [&](float v, int) {
-        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], 1.f);
+      visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], ok ? 1.f : 0.f);
       });
     } else {
-      visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+      visit_range(x, lo, hi, vec_ok, [&](float v, int, bool) {  // -inf: mass 0
         atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], __expf(v * invT - M));
       });
     }
@@ -519,8 +522,9 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     for (int i = tid; i < 12 * 256; i += kChunkThreads) lds[i] = 0.f;
     __syncthreads();
     const bool above_too = has_k && has_p;
-    visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
       const int k = k16_of(v), h = k >> 8;
+      if (!ok) return;
       if (h == sh) {
         atomicAdd(&lc[wid * 256 + (k & 255)], 1.f);
         atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
@@ -572,9 +576,9 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     float* lm = lds;
     for (int i = tid; i < 4 * 256; i += kChunkThreads) lds[i] = 0.f;
     __syncthreads();
-    visit_range(x, lo, hi, vec_ok, [&](float v, int) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
       const int k = k16_of(v);
-      if ((k >> 8) == ph) atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
+      if (ok && (k >> 8) == ph) atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
     });
     __syncthreads();
     float mm = 0.f;
@@ -592,8 +596,8 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   const uint64_t seed = p.seeds ? (uint64_t)p.seeds[row] : 0x1234ull + row;
   const uint32_t step = p.steps ? (uint32_t)p.steps[row] : 0u;
   ArgBest b{-INFINITY, 0x7fffffff};
-  visit_range(x, lo, hi, vec_ok, [&](float v, int i) {
-    if (k16_of(v) < tau) return;
+  visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool ok) {
+    if (!ok || k16_of(v) < tau) return;
     const float u = uniform01(seed, step, (uint32_t)i);
     const float g = v * invT - __logf(-__logf(u));
     if (g > b.v) { b.v = g; b.i = i; }
