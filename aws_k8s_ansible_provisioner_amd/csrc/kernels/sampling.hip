@@ -5,6 +5,8 @@
 // draw is a Gumbel-max over the surviving set with a counter-based RNG keyed by (request
 // seed, request step, token id), so a request's stream is reproducible regardless of batch
 // composition.  The row is split over several workgroups (sample_chunk_kernel below).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -641,6 +643,11 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
 }
 
 int sample_chunks(int B, int V) {
+  static const int forced = [] {
+    const char* e = std::getenv("AKAP_SAMPLE_CHUNKS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced > 0) return min(forced, kMaxChunks);
   // >= ~2k workgroups over the batch, chunks of >= 2k elements, and chunks of <= 4k elements
   // (the inverse-CDF draw rescans one chunk per row), at most kMaxChunks per row
   int S = (2048 + B - 1) / max(B, 1);
