@@ -67,9 +67,9 @@ __device__ __forceinline__ ArgBest block_argmax(ArgBest b, float* sv, int* si) {
 //    (max, rescaled sum), re-arms the counter and writes the token + log-prob of a greedy row,
 //    or the row summary (M, Z) of a row with filters; a row without filters is
 //    drawn there by inverse CDF: u(seed, step) * Z picks the chunk from the prefix of the
-//    chunk masses, then the workgroup rescans that one chunk (a block scan of per-thread run
-//    masses) for the token -- exact sampling with one exp per element in the main pass and
-//    no per-element RNG.
+//    chunk masses, then the tile from the chunk's published tile masses, then the workgroup
+//    rescans that one 2048-element tile (a block scan of per-thread masses) for the token --
+//    exact sampling with one exp per element in the main pass and no per-element RNG.
 // 2. sample_filter_kernel, grid = B: rows with top-k / top-p (the others return at once) find
 //    their thresholds by an adaptive radix select over the order-preserving key image -- by
 //    COUNT for top-k, by probability MASS for top-p on the top-k renormalised distribution:
@@ -85,6 +85,11 @@ constexpr int kSelWords = 16;  // per-row state of the filter passes (32-bit wor
 // per-row histogram area of the filter passes, in float2: kMaxChunks x 512 pairs (pass B
 // publishes two 256-bin sets per chunk)
 constexpr int kHistRow = kMaxChunks * 512;
+// draw rows (T > 0, no filter): a chunk is cut into tiles of 2048 consecutive elements (one
+// 16-byte vector per thread); the chunk kernel publishes every tile's mass, so the row's last
+// chunk rescans ONE tile for the token whatever the chunk size
+constexpr int kTile = kChunkThreads * 8;
+constexpr int kMaxTiles = 64;  // chunk <= 131072 elements
 
 struct SampPart {  // one chunk's partial record (32 B = two 16-B vectors)
   float m, s;      // max of z over the chunk, sum of exp(z - m)
@@ -148,6 +153,107 @@ __device__ __forceinline__ void visit_range(const T* x, int lo, int hi, bool vec
   }
 }
 
+// Draw rows' main pass over x[lo, hi): z = x / T in tiles of kTile consecutive elements (8 per
+// thread), 4 tiles' loads issued before the first is used (unconditional, index clamped: a
+// load under a branch would make every later wait a full drain); per tile a wave-level
+// (max, sum exp) pair, then wave 0 folds the pairs into the tile masses (units of exp(z - the
+// chunk max)), publishes them to tout with sc1 stores (drained by the caller's ticket wait in
+// the same wave) and returns the chunk's (max, sum) to every thread.
+template <typename T>
+__device__ __forceinline__ float2 draw_tiles(const T* x, int lo, int hi, bool vec_ok, float invT,
+                                             float* tout) {
+  __shared__ float2 s_t[kMaxTiles][kChunkThreads / 64];
+  __shared__ float2 s_mz;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n = hi - lo;
+  const int ntile = min(kMaxTiles, (n + kTile - 1) / kTile);  // host: chunk <= kMaxTiles tiles
+  const int nvf = vec_ok ? n / 8 : 0;  // 8-element groups read as 16-byte vectors
+  const T* xc = x + lo;
+  float tailz[8];  // the partial last group (vector rows), owned by thread nvf % 256
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tailz[j] = -INFINITY;
+  if (vec_ok && nvf * 8 < n && tid == (nvf & (kChunkThreads - 1)))
+    for (int j = 0; j < n - nvf * 8; ++j) tailz[j] = (float)xc[nvf * 8 + j] * invT;
+  for (int t0 = 0; t0 < ntile; t0 += 4) {
+    float z[4][8];
+    if (nvf > 0) {  // uniform
+      typename Vec<T>::type q[4][8 / Vec<T>::N];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int g = min((t0 + u) * kChunkThreads + tid, nvf - 1);
+#pragma unroll
+        for (int h = 0; h < 8 / Vec<T>::N; ++h)
+          q[u][h] = *reinterpret_cast<const typename Vec<T>::type*>(xc + g * 8 + h * Vec<T>::N);
+      }
+      // pin all four loads here (the compiler otherwise sinks a load into the lanes that use
+      // it, behind a branch, and every wait after that becomes a full drain)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int h = 0; h < 8 / Vec<T>::N; ++h) {
+          u32x4 r = __builtin_bit_cast(u32x4, q[u][h]);
+          asm volatile("" : "+v"(r));
+          q[u][h] = __builtin_bit_cast(typename Vec<T>::type, r);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int g = (t0 + u) * kChunkThreads + tid;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = (float)q[u][j / Vec<T>::N][j % Vec<T>::N] * invT;
+          z[u][j] = g < nvf ? v : (g == nvf ? tailz[j] : -INFINITY);
+        }
+      }
+    } else {  // unaligned row (or < 8 elements): scalar loads, index clamped
+      float q[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          q[u][j] = (float)xc[min(((t0 + u) * kChunkThreads + tid) * 8 + j, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          z[u][j] = ((t0 + u) * kChunkThreads + tid) * 8 + j < n ? q[u][j] * invT : -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // tiles past ntile (<= 63: t0 <= 60) come out empty
+      float mt = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mt = fmaxf(mt, z[u][j]);
+      float st = 0.f;
+      if (mt > -INFINITY) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st += __expf(z[u][j] - mt);
+      }
+      const float mw = wave_max(mt);
+      const float sw = wave_sum(mt == -INFINITY ? 0.f : st * __expf(mt - mw));
+      if (lane == 0) s_t[t0 + u][wid] = make_float2(mw, sw);
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    float mt = -INFINITY, stt = 0.f;
+    if (lane < ntile) {
+#pragma unroll
+      for (int w = 0; w < kChunkThreads / 64; ++w) mt = fmaxf(mt, s_t[lane][w].x);
+#pragma unroll
+      for (int w = 0; w < kChunkThreads / 64; ++w)
+        if (s_t[lane][w].x > -INFINITY) stt += s_t[lane][w].y * __expf(s_t[lane][w].x - mt);
+    }
+    const float Mc = wave_max(mt);
+    const float wl = mt == -INFINITY ? 0.f : stt * __expf(mt - Mc);
+    const float Zc = wave_sum(wl);
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc((void*)tout, (short)0, kMaxTiles * 4, 0x00020000);
+    if (lane < ntile) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wl), rt, lane * 4, 0, kSc1);
+    if (lane == 0) s_mz = make_float2(Mc, Zc);
+  }
+  __syncthreads();
+  return s_mz;
+}
+
 __device__ __forceinline__ bool row_filtered(const SampleParams& p, int row, float temp) {
   if (!(temp > 0.f)) return false;
   const int k = p.top_k ? p.top_k[row] : 0;
@@ -157,7 +263,8 @@ __device__ __forceinline__ bool row_filtered(const SampleParams& p, int row, flo
 
 template <typename T>
 __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParams p, SampPart* ws,
-                                                                     int* tickets, float* rowsum) {
+                                                                     int* tickets, float* rowsum,
+                                                                     float* tiles) {
   __shared__ float sv[16];
   __shared__ int si[16];
   __shared__ int s_last;
@@ -179,19 +286,15 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   // ---- one pass over the chunk (the three row kinds as separate loops: no per-element
   // branch on the row kind) ----
   float m = -INFINITY, sum = 0.f;
+  float2 dmz = make_float2(-INFINITY, 0.f);
   ArgBest best{-INFINITY, 0x7fffffff};
   if (!need_sum) {
     visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
       if (v > best.v) { best.v = v; best.i = i; }  // ascending i per thread: first max kept
     });
   } else if (!greedy && !filt) {
-    // max and partition sum only (one exp per element): the draw is an inverse-CDF pick by
-    // the last chunk below, so no per-element RNG / logs in this pass
-    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool) {
-      const float z = v * invT;
-      if (z > m) { sum = sum * __expf(m - z) + 1.f; m = z; }
-      else if (z > -INFINITY) sum += __expf(z - m);
-    });
+    dmz = draw_tiles(x, lo, hi, vec_ok, invT,
+                     tiles + ((size_t)row * kMaxChunks + c) * kMaxTiles);
   } else {  // greedy with log-probs, or a filtered row
     visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
       if (v > best.v) { best.v = v; best.i = i; }
@@ -201,9 +304,13 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
     });
   }
   // workgroup reductions
+  const bool draw = !greedy && !filt;  // uniform over the workgroup
   if (!need_sum || greedy) best = block_argmax(best, sv, si);
   float M = -INFINITY, Z = 0.f;
-  if (need_sum) {
+  if (draw) {
+    M = dmz.x;
+    Z = dmz.y;
+  } else if (need_sum) {
     M = block_max(m, sv);
     Z = block_sum(m == -INFINITY ? 0.f : sum * __expf(m - M), sv);
   }
@@ -225,9 +332,8 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   __syncthreads();
   if (!s_last) return;
   // ---- last chunk of the row: combine the S partials (S <= 64: wave 0, sc1 loads) ----
-  const bool draw = !greedy && !filt;  // uniform over the workgroup
   __shared__ float s_m, s_z, s_res;
-  __shared__ int s_chunk, s_tok, s_fb;
+  __shared__ int s_chunk, s_tile, s_tok, s_fb;
   if (threadIdx.x < 64) {
     const int l = threadIdx.x;
     float rm = -INFINITY, rs = 0.f;
@@ -259,11 +365,32 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
       const uint64_t hit = __ballot(incl >= target && w > 0.f);
       const uint64_t live = __ballot(w > 0.f);
       const int c_sel = hit ? __builtin_ctzll(hit) : 63 - __builtin_clzll(live);
-      if (l == c_sel) {
-        s_chunk = l;
-        s_res = hit ? target - (incl - w) : w;  // rounding past the end: the chunk's last mass
+      // level 1.5: the tile inside that chunk, from its published tile masses (each in
+      // units of exp(z - the chunk's max))
+      const float r1 = __shfl(hit ? target - (incl - w) : w, c_sel, 64);  // rounding: last mass
+      const float scale = __expf(__shfl(rm, c_sel, 64) - Mr);
+      const int chunk_len = min(V, (c_sel + 1) * chunk) - min(V, c_sel * chunk);
+      const int ntile = (chunk_len + kTile - 1) / kTile;
+      const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(tiles + ((size_t)row * kMaxChunks + c_sel) * kMaxTiles), (short)0,
+          kMaxTiles * 4, 0x00020000);
+      const float tw = l < ntile ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                       rt, l * 4, 0, kSc1)) * scale
+                                 : 0.f;
+      float tinc = tw;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_up(tinc, o, 64);
+        if (l >= o) tinc += u;
       }
+      const uint64_t thit = __ballot(tinc >= r1 && tw > 0.f);
+      const uint64_t tlive = __ballot(tw > 0.f);
+      const int t_sel = thit ? __builtin_ctzll(thit) : (tlive ? 63 - __builtin_clzll(tlive) : 0);
+      if (l == t_sel) s_res = thit ? r1 - (tinc - tw) : tw;
       if (l == 0) {
+        s_chunk = c_sel;
+        s_tile = t_sel;
+        if (!tlive) s_res = 0.f;
         s_m = Mr;
         s_z = Zr;
         s_tok = 0x7fffffff;
@@ -286,22 +413,39 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   }
   if (!draw) return;
   __syncthreads();
-  // ---- inverse CDF, level 2: rescan the selected chunk (just read by its workgroup, so in
-  // L2) in coalesced tiles of 8 elements per thread; a block scan of the per-thread masses
-  // finds the thread whose 8 elements cross the residual mass, which walks them ----
+  // ---- inverse CDF, level 2: rescan the selected tile (read by this row's chunk kernel,
+  // so in L2), 8 elements per thread; a block scan of the per-thread masses finds the thread
+  // whose 8 elements cross the residual mass, which walks them ----
   const float Mr = s_m;
   float R = s_res;
-  const int lo2 = min(V, s_chunk * chunk), hi2 = min(V, lo2 + chunk);
+  const int clo = min(V, s_chunk * chunk), chi = min(V, clo + chunk);
+  const int lo2 = min(chi, clo + s_tile * kTile), hi2 = min(chi, lo2 + kTile);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  constexpr int TILE = kChunkThreads * 8;
+  constexpr int TILE = kTile;
   for (int t0 = lo2; t0 < hi2; t0 += TILE) {
     const int a0 = t0 + (int)threadIdx.x * 8, a1 = min(hi2, a0 + 8);
     float e[8];
     float ts = 0.f;
     int last_pos = -1;
+    float xv8[8];
+    if (vec_ok && a0 + 8 <= a1) {
+      const typename Vec<T>::type q0 = *reinterpret_cast<const typename Vec<T>::type*>(x + a0);
+      if constexpr (NV == 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv8[j] = (float)q0[j];
+      } else {
+        const typename Vec<T>::type q1 =
+            *reinterpret_cast<const typename Vec<T>::type*>(x + a0 + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { xv8[j] = (float)q0[j]; xv8[4 + j] = (float)q1[j]; }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv8[j] = a0 + j < a1 ? (float)x[a0 + j] : -INFINITY;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      e[j] = a0 + j < a1 ? __expf((float)x[a0 + j] * invT - Mr) : 0.f;
+      e[j] = a0 + j < a1 ? __expf(xv8[j] * invT - Mr) : 0.f;
       ts += e[j];
       if (e[j] > 0.f) last_pos = a0 + j;
     }
@@ -647,19 +791,21 @@ int sample_chunks(int B, int V) {
     const char* e = std::getenv("AKAP_SAMPLE_CHUNKS");
     return e ? std::atoi(e) : 0;
   }();
-  if (forced > 0) return min(forced, kMaxChunks);
-  // >= ~2k workgroups over the batch, chunks of >= 2k elements, and chunks of <= 4k elements
-  // (the inverse-CDF draw rescans one chunk per row), at most kMaxChunks per row
-  int S = (2048 + B - 1) / max(B, 1);
+  const int need = (V + kMaxTiles * kTile - 1) / (kMaxTiles * kTile);  // <= kMaxTiles tiles
+  if (forced > 0) return max(need, min(forced, kMaxChunks));
+  // ~512 workgroups over the batch (each chunk streams its share with 4 loads in flight per
+  // thread; more, smaller chunks pay the per-workgroup publish / ticket / combine latency more
+  // often: profiles/r5_sampler_rework.md), chunks of >= 2k elements, at most kMaxChunks
+  int S = (512 + B - 1) / max(B, 1);
   S = min(S, max(1, V / 2048));
-  S = max(S, (V + 4095) / 4096);
+  S = max(S, need);
   return max(1, min(S, kMaxChunks));
 }
 
 long sample_ws_floats(int B) {
-  // partial records, selection states, per-row histograms (kMaxChunks x 256 float2; the
-  // last 256 floats keep pass A's high-byte masses)
-  return (long)B * (kMaxChunks * 8 + kSelWords + 2 * kHistRow);
+  // partial records, selection states, per-row histograms (kMaxChunks x 512 float2), the
+  // draw rows' tile masses (kMaxChunks x kMaxTiles)
+  return (long)B * (kMaxChunks * 8 + kSelWords + 2 * kHistRow + kMaxChunks * kMaxTiles);
 }
 
 // Chunks per row of the filter passes: each pass has a fixed cost per workgroup (publish,
@@ -678,15 +824,16 @@ void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int fil
   SelState* st = reinterpret_cast<SelState*>(parts + (size_t)B * kMaxChunks);
   float2* hist = reinterpret_cast<float2*>(st + B);
   float* rowsum = reinterpret_cast<float*>(st);
+  float* tiles = reinterpret_cast<float*>(hist + (size_t)B * kHistRow);
   if (p.is_bf16) {
-    sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum);
+    sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles);
     if (filtered) {
       sample_pass_kernel<bf16, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
       for (int ps = 1; ps < 4; ++ps)
         sample_pass_kernel<bf16, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
     }
   } else {
-    sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum);
+    sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles);
     if (filtered) {
       sample_pass_kernel<float, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
       for (int ps = 1; ps < 4; ++ps)

@@ -499,9 +499,10 @@ def gemm_splitk(M: int, N: int, K: int) -> int:
 
 # ----------------------------------------------------------------------------- sampling
 SAMPLE_MAX_CHUNKS = 64  # csrc/kernels/sampling.hip kMaxChunks
-# floats per row (sample_ws_floats): 64 chunk records of 8, a 16-word filter state, and
-# 2 x kHistRow floats of filter-pass histograms (kHistRow = 64 x 512 float2)
-SAMPLE_WS_PER_ROW = SAMPLE_MAX_CHUNKS * 8 + 16 + 2 * SAMPLE_MAX_CHUNKS * 512
+# floats per row (sample_ws_floats): 64 chunk records of 8, a 16-word filter state,
+# 2 x kHistRow floats of filter-pass histograms (kHistRow = 64 x 512 float2), and the draw
+# rows' tile masses (64 chunks x kMaxTiles = 64)
+SAMPLE_WS_PER_ROW = SAMPLE_MAX_CHUNKS * 8 + 16 + 2 * SAMPLE_MAX_CHUNKS * 512 + SAMPLE_MAX_CHUNKS * 64
 _SAMPLE_WS: dict = {}
 _SAMPLE_OLD: list = []  # outgrown workspaces stay alive: captured hipGraphs address them
 

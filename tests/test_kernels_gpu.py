@@ -303,6 +303,55 @@ def test_sampling_distribution_topk_topp():
     assert torch.equal(tok, tok2)
 
 
+@pytest.mark.parametrize("B,dtype,aligned", [(256, torch.bfloat16, True),
+                                             (8, torch.bfloat16, True),
+                                             (64, torch.float32, True),
+                                             (64, torch.bfloat16, False)])
+def test_sampling_distribution_full_vocab_tiles(B, dtype, aligned):
+    """Plain temperature draws on full-vocabulary rows: the row's chunk, then the tile inside
+    it (published tile masses), then one 2048-element rescan.  Hot tokens sit on tile and chunk
+    boundaries; their frequencies over 4096 draws match the fp32 softmax, and the log-probs
+    match.  Unaligned rows (a view one element in) take the scalar path."""
+    torch.manual_seed(B)
+    V = 151936
+    base = torch.randn(V) * 0.5
+    hot = {5: 12.0, 2047: 13.0, 2048: 11.5, 40000: 12.5, 75967: 13.0, 75968: 12.0,
+           151935: 11.0, 151930: 10.5}
+    for i, v in hot.items():
+        base[i] = v
+    vals = base.to(dtype).float()
+    T = 1.0
+    p = torch.softmax(vals / T, -1)
+    rows = vals.to(dtype).expand(B, V)
+    if aligned:
+        logits = rows.contiguous().to(DEV)
+    else:
+        big = torch.zeros(B, V + 1, dtype=dtype)
+        big[:, 1:] = rows
+        logits = big.to(DEV)[:, 1:]
+    temp = torch.full((B,), T, device=DEV)
+    tk = torch.zeros(B, dtype=torch.int32, device=DEV)
+    tp = torch.ones(B, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 104729
+    toks, lps = [], []
+    for step in range(4096 // B):
+        steps = torch.full((B,), step, dtype=torch.int32, device=DEV)
+        tok, lp = ops.sample(logits, temp, tk, tp, seeds, steps, filtered=False)
+        toks.append(tok.cpu())
+        lps.append(lp.cpu())
+    tok = torch.cat(toks)
+    lp = torch.cat(lps)
+    n = tok.numel()
+    assert int(tok.min()) >= 0 and int(tok.max()) < V
+    for i in hot:
+        f = float((tok == i).sum()) / n
+        assert abs(f - float(p[i])) < 0.03, (i, f, float(p[i]))
+    rest = 1.0 - sum(float(p[i]) for i in hot)
+    f_rest = float((~torch.isin(tok, torch.tensor(list(hot)))).sum()) / n
+    assert abs(f_rest - rest) < 0.03, (f_rest, rest)
+    _close(lp, torch.log(p[tok]), atol=2e-3)
+
+
 def test_embedding_vocab_parallel():
     table = torch.randn(1000, 1024, dtype=torch.bfloat16)
     ids = torch.tensor([0, 5, 999, 1500, 250], dtype=torch.int64)
