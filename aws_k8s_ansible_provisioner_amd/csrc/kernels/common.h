@@ -40,6 +40,32 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Wave-uniform reductions on DPP (VALU lane swaps, no LDS round trip): xor 1 and 2 as quad
+// permutes, 4 and 8 as the half-row / row mirrors (each leaves the 4- then 8- then 16-lane
+// groups uniform), then the four 16-lane rows through v_readlane.  For per-tile reductions in
+// streaming loops, where __shfl_xor's ds_bpermute chain (6 dependent LDS round trips) stalls.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp_mov<0x141>(v));  // row_half_mirror
+  v = fmaxf(v, dpp_mov<0x140>(v));  // row_mirror
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+
 // Block-wide sum for blockDim.x a multiple of 64, <= 1024. `scratch` needs 16 floats.
 __device__ __forceinline__ float block_sum(float v, float* scratch) {
   const int lane = threadIdx.x & 63;

@@ -227,8 +227,8 @@ __device__ __forceinline__ float2 draw_tiles(const T* x, int lo, int hi, bool ve
 #pragma unroll
         for (int j = 0; j < 8; ++j) st += __expf(z[u][j] - mt);
       }
-      const float mw = wave_max(mt);
-      const float sw = wave_sum(mt == -INFINITY ? 0.f : st * __expf(mt - mw));
+      const float mw = wave_max_dpp(mt);
+      const float sw = wave_sum_dpp(mt == -INFINITY ? 0.f : st * __expf(mt - mw));
       if (lane == 0) s_t[t0 + u][wid] = make_float2(mw, sw);
     }
   }
