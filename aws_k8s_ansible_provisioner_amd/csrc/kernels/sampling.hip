@@ -404,10 +404,11 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
         p.out_tokens[row] = a.i;
         // greedy log-prob: x[tok] is the max, so log softmax = -log sum exp(x - M)
         if (p.out_logprobs) p.out_logprobs[row] = p.greedy_logprobs ? -__logf(Zr) : 0.f;
-      } else if (filt) {  // sample_filter_kernel finishes the row
-        float* r = rowsum + (size_t)row * kSelWords;  // the passes' SelState: M, Z
+      } else if (filt) {  // the filter passes finish the row
+        float* r = rowsum + (size_t)row * kSelWords;  // the passes' SelState: M, Z, kmax16
         r[0] = Mr;
         r[1] = Zr;
+        r[11] = __int_as_float((int)(fkey(a.v) >> 16));
       }
     }
   }
@@ -493,6 +494,10 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
 // per-wave LDS histograms, 256 (count, mass) pairs published per chunk with sc1 stores, a
 // ticket, and the row's last chunk sums the S histograms and selects (masses are
 // exp(x / T - M) with the row max M of the chunk kernel, so they add across chunks).
+//   pass W  (count, mass) histogram of the 256 keys just below the row max: when the top-k /
+//           top-p threshold falls inside that window (any peaked distribution, and top-k
+//           for small k) the exact threshold comes out here -- only in-window elements touch
+//           the LDS -- and passes A-C return at once for the row;
 //   pass A  high-byte histogram of the whole row -> top-k's high byte (by count) or, for a
 //           top-p-only row, top-p's high byte (by mass);
 //   pass B  low-byte histogram inside that bin -> the exact top-k key (and Zk, the top-k mass)
@@ -515,7 +520,9 @@ struct SelState {
   float Zk;
   int p_hi;
   float p_above, p_target;
-  int pad[5];
+  int kmax16;    // 16-bit key of the row max (chunk kernel)
+  int resolved;  // pass W found the threshold inside the window below the max (A-C skip)
+  int pad[3];
 };
 static_assert(sizeof(SelState) == kSelWords * 4, "SelState layout");
 
@@ -632,6 +639,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   const float tp = p.top_p ? p.top_p[row] : 1.f;
   const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
   if constexpr (PASS_A) {  // A: high byte of the whole row; count (top-k) or mass (top-p only)
+    if (rs.resolved) return;  // uniform per row: pass W found the threshold
     for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
     __syncthreads();
     if (has_k) {
@@ -660,6 +668,58 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     }
     return;
   } else {
+  if (pass == 4) {  // W: the 256 keys [kmax16 - 255, kmax16]; bin b holds key kmax16 - 255 + b
+    const int km = rs.kmax16, base = km - 255;
+    float* lc = lds;            // [4][256] counts
+    float* lm = lds + 4 * 256;  // [4][256] masses
+    for (int i = tid; i < 8 * 256; i += kChunkThreads) lds[i] = 0.f;
+    __syncthreads();
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int b = k16_of(v) - base;
+      if (ok && b >= 0) {  // b <= 255: km is the row max
+        atomicAdd(&lc[wid * 256 + b], 1.f);
+        atomicAdd(&lm[wid * 256 + b], __expf(v * invT - M));
+      }
+    });
+    __syncthreads();
+    float cc = 0.f, mm = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      cc += lc[w * 256 + tid];
+      mm += lm[w * 256 + tid];
+    }
+    float2 mine[1] = {make_float2(cc, mm)}, tot[1];
+    if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
+    const float cnt = tot[0].x, mass = tot[0].y;
+    int tau = -1;
+    float above;
+    if (has_k) {
+      if (block_sum(cnt, scratch) >= (float)kk) {  // integer counts: exact
+        const int bk = suffix_select(cnt, (float)kk, scratch, &above);
+        if (!has_p) {
+          tau = base + bk;
+        } else {  // top-p over the top-k set, which lies inside the window
+          const float mk = tid >= bk ? mass : 0.f;
+          const float Zk = block_sum(mk, scratch);
+          const int bp = suffix_select(mk, tp * Zk, scratch, &above);
+          tau = base + max(bk, bp);
+          if (tid == 0) rs.Zk = Zk;
+        }
+      }
+    } else {
+      const float target = tp * rs.Z;
+      // a margin over the rounding of two summation orders: a borderline window falls back
+      // to the full passes
+      if (block_sum(mass, scratch) >= target * 1.0001f) tau = base + suffix_select(mass, target, scratch, &above);
+    }
+    if (tid == 0) {
+      rs.tau = tau;
+      rs.p_hi = -1;
+      rs.resolved = tau >= 0 ? 1 : 0;
+    }
+    return;
+  }
+  if (rs.resolved && pass < 3) return;  // passes B, C (not D): uniform per row
   if (pass == 1) {  // B: low byte inside sel_hi (count + mass); top-k + top-p: masses above
     const int sh = rs.sel_hi;
     float* lc = lds;             // [4][256] low-byte counts
@@ -828,6 +888,7 @@ void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int fil
   if (p.is_bf16) {
     sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles);
     if (filtered) {
+      sample_pass_kernel<bf16, false><<<gridf, kChunkThreads, 0, s>>>(p, 4, st, hist, tickets);
       sample_pass_kernel<bf16, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
       for (int ps = 1; ps < 4; ++ps)
         sample_pass_kernel<bf16, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
@@ -835,6 +896,7 @@ void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int fil
   } else {
     sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles);
     if (filtered) {
+      sample_pass_kernel<float, false><<<gridf, kChunkThreads, 0, s>>>(p, 4, st, hist, tickets);
       sample_pass_kernel<float, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
       for (int ps = 1; ps < 4; ++ps)
         sample_pass_kernel<float, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);

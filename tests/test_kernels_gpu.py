@@ -226,14 +226,19 @@ def test_argmax_and_greedy_sample():
     assert torch.equal(tok, exp)
 
 
-@pytest.mark.parametrize("k,tp", [(50, 1.0), (0, 0.9), (40, 0.8), (2000, 0.5), (1, 1.0)])
-def test_sampling_filters_exact_sets_full_vocab(k, tp):
-    """Top-k / top-p on full-vocabulary bf16 rows (the distributed two-level threshold passes):
-    every sampled token lies in the exact allowed set computed in fp32 from the same bf16
-    values (ties at the threshold included), over many (seed, step) draws."""
+@pytest.mark.parametrize("k,tp,scale", [(50, 1.0, 2.5), (0, 0.9, 2.5), (40, 0.8, 2.5),
+                                        (2000, 0.5, 2.5), (1, 1.0, 2.5),
+                                        # thresholds below the 256-key window under the max:
+                                        # pass W cannot resolve them, passes A-C do
+                                        (30000, 1.0, 0.3), (0, 0.9, 1.0), (40000, 0.9, 1.0)])
+def test_sampling_filters_exact_sets_full_vocab(k, tp, scale):
+    """Top-k / top-p on full-vocabulary bf16 rows (the window pass, or the distributed
+    two-level threshold passes): every sampled token lies in the exact allowed set computed in
+    fp32 from the same bf16 values (ties at the threshold included), over many (seed, step)
+    draws."""
     torch.manual_seed(k + int(tp * 10))
     B, V, T = 16, 151936, 0.9
-    base = (torch.randn(B, V) * 2.5).bfloat16()
+    base = (torch.randn(B, V) * scale).bfloat16()
     base[:, :7] = 9.0  # a tie group at the top
     logits = base.to(DEV)
     temp = torch.full((B,), T, device=DEV)
