@@ -305,7 +305,8 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   }
   // workgroup reductions
   const bool draw = !greedy && !filt;  // uniform over the workgroup
-  if (!need_sum || greedy) best = block_argmax(best, sv, si);
+  // (filtered rows: the row max feeds pass W's window)
+  if (!need_sum || greedy || filt) best = block_argmax(best, sv, si);
   float M = -INFINITY, Z = 0.f;
   if (draw) {
     M = dmz.x;
@@ -676,7 +677,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     __syncthreads();
     visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
       const int b = k16_of(v) - base;
-      if (ok && b >= 0) {  // b <= 255: km is the row max
+      if (ok && b >= 0 && b < 256) {  // (b < 256 always: km is the row max)
         atomicAdd(&lc[wid * 256 + b], 1.f);
         atomicAdd(&lm[wid * 256 + b], __expf(v * invT - M));
       }
