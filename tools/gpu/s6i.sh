@@ -1,0 +1,12 @@
+# per-launch sampler durations after pass W (kernel trace), B = 64 and 256
+set -u
+O=gpurun_out/s6i; mkdir -p $O
+export TMPDIR=/tmp
+run() { n=$1; t=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.log 2>&1; rc=$?; echo "$n rc=$rc"; [ $rc -eq 0 ]; }
+run t64 200 rocprofv3 --kernel-trace --output-format csv -d /tmp/st64 -o run -- python3 tools/sample_pass_probe.py --B 64 &&
+python3 tools/sample_pass_probe.py --summarize /tmp/st64/run_kernel_trace.csv > $O/b64.txt &&
+run t256 200 rocprofv3 --kernel-trace --output-format csv -d /tmp/st256 -o run -- python3 tools/sample_pass_probe.py --B 256 &&
+python3 tools/sample_pass_probe.py --summarize /tmp/st256/run_kernel_trace.csv > $O/b256.txt &&
+run t64k 200 rocprofv3 --kernel-trace --output-format csv -d /tmp/st64k -o run -- python3 tools/sample_pass_probe.py --B 64 --p 1.0 &&
+python3 tools/sample_pass_probe.py --summarize /tmp/st64k/run_kernel_trace.csv > $O/b64k.txt &&
+echo done
