@@ -261,255 +261,6 @@ __device__ __forceinline__ bool row_filtered(const SampleParams& p, int row, flo
   return (k > 0 && k < p.V) || (tp < 1.f && tp > 0.f);
 }
 
-template <typename T>
-__global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParams p, SampPart* ws,
-                                                                     int* tickets, float* rowsum,
-                                                                     float* tiles) {
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  __shared__ int s_last;
-  const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
-  const T* x = reinterpret_cast<const T*>(p.logits) + (size_t)row * p.ld;
-  const int V = p.V;
-  const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  constexpr int NV = Vec<T>::N;
-  const int chunk = ((V + S - 1) / S + NV - 1) / NV * NV;
-  const int lo = min(V, c * chunk), hi = min(V, lo + chunk);
-  const float temp = p.temperature ? p.temperature[row] : 0.f;
-  const bool greedy = !(temp > 0.f);
-  const bool filt = row_filtered(p, row, temp);
-  const float invT = greedy ? 1.f : 1.f / temp;
-  const bool need_sum = !greedy || (p.greedy_logprobs && p.out_logprobs);
-  const uint64_t seed = p.seeds ? (uint64_t)p.seeds[row] : 0x1234ull + row;
-  const uint32_t step = p.steps ? (uint32_t)p.steps[row] : 0u;
-
-  // ---- one pass over the chunk (the three row kinds as separate loops: no per-element
-  // branch on the row kind) ----
-  float m = -INFINITY, sum = 0.f;
-  float2 dmz = make_float2(-INFINITY, 0.f);
-  ArgBest best{-INFINITY, 0x7fffffff};
-  if (!need_sum) {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
-      if (v > best.v) { best.v = v; best.i = i; }  // ascending i per thread: first max kept
-    });
-  } else if (!greedy && !filt) {
-    dmz = draw_tiles(x, lo, hi, vec_ok, invT,
-                     tiles + ((size_t)row * kMaxChunks + c) * kMaxTiles);
-  } else {  // greedy with log-probs, or a filtered row
-    visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
-      if (v > best.v) { best.v = v; best.i = i; }
-      const float z = v * invT;
-      if (z > m) { sum = sum * __expf(m - z) + 1.f; m = z; }
-      else if (z > -INFINITY) sum += __expf(z - m);
-    });
-  }
-  // workgroup reductions
-  const bool draw = !greedy && !filt;  // uniform over the workgroup
-  // (filtered rows: the row max feeds pass W's window)
-  if (!need_sum || greedy || filt) best = block_argmax(best, sv, si);
-  float M = -INFINITY, Z = 0.f;
-  if (draw) {
-    M = dmz.x;
-    Z = dmz.y;
-  } else if (need_sum) {
-    M = block_max(m, sv);
-    Z = block_sum(m == -INFINITY ? 0.f : sum * __expf(m - M), sv);
-  }
-  // ---- publish the partial (sc1 stores), take a ticket ----
-  const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(ws + (size_t)row * S), (short)0, (int)(S * sizeof(SampPart)), 0x00020000);
-  if (threadIdx.x == 0) {
-    u32x4 a, b2;
-    a[0] = __float_as_uint(M); a[1] = __float_as_uint(Z);
-    a[2] = 0u; a[3] = 0u;
-    b2[0] = __float_as_uint(best.v); b2[1] = (uint32_t)best.i; b2[2] = 0u; b2[3] = 0u;
-    __builtin_amdgcn_raw_buffer_store_b128(a, rws, c * 32, 0, kSc1);
-    __builtin_amdgcn_raw_buffer_store_b128(b2, rws, c * 32 + 16, 0, kSc1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(tickets + row * kCtrStride, 1, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    s_last = t == S - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // ---- last chunk of the row: combine the S partials (S <= 64: wave 0, sc1 loads) ----
-  __shared__ float s_m, s_z, s_res;
-  __shared__ int s_chunk, s_tile, s_tok, s_fb;
-  if (threadIdx.x < 64) {
-    const int l = threadIdx.x;
-    float rm = -INFINITY, rs = 0.f;
-    ArgBest a{-INFINITY, 0x7fffffff};
-    if (l < S) {
-      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32, 0, kSc1);
-      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32 + 16, 0, kSc1);
-      rm = __uint_as_float(v0[0]); rs = __uint_as_float(v0[1]);
-      a = ArgBest{__uint_as_float(v1[0]), (int)v1[1]};
-    }
-    const float Mr = wave_max(rm);
-    // chunk l's mass in units of exp(z - Mr); its inclusive prefix over the chunks
-    const float w = rm == -INFINITY ? 0.f : rs * __expf(rm - Mr);
-    float incl = w;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float u = __shfl_up(incl, o, 64);
-      if (l >= o) incl += u;
-    }
-    const float Zr = __shfl(incl, 63, 64);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      ArgBest ca{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
-      a = arg_better(a, ca);
-    }
-    if (draw) {
-      // inverse CDF, level 1: the chunk whose prefix mass first reaches u * Z
-      const float target = uniform01(seed, step, 0xffffffffu) * Zr;
-      const uint64_t hit = __ballot(incl >= target && w > 0.f);
-      const uint64_t live = __ballot(w > 0.f);
-      const int c_sel = hit ? __builtin_ctzll(hit) : 63 - __builtin_clzll(live);
-      // level 1.5: the tile inside that chunk, from its published tile masses (each in
-      // units of exp(z - the chunk's max))
-      const float r1 = __shfl(hit ? target - (incl - w) : w, c_sel, 64);  // rounding: last mass
-      const float scale = __expf(__shfl(rm, c_sel, 64) - Mr);
-      const int chunk_len = min(V, (c_sel + 1) * chunk) - min(V, c_sel * chunk);
-      const int ntile = (chunk_len + kTile - 1) / kTile;
-      const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(tiles + ((size_t)row * kMaxChunks + c_sel) * kMaxTiles), (short)0,
-          kMaxTiles * 4, 0x00020000);
-      const float tw = l < ntile ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                       rt, l * 4, 0, kSc1)) * scale
-                                 : 0.f;
-      float tinc = tw;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const float u = __shfl_up(tinc, o, 64);
-        if (l >= o) tinc += u;
-      }
-      const uint64_t thit = __ballot(tinc >= r1 && tw > 0.f);
-      const uint64_t tlive = __ballot(tw > 0.f);
-      const int t_sel = thit ? __builtin_ctzll(thit) : (tlive ? 63 - __builtin_clzll(tlive) : 0);
-      if (l == t_sel) s_res = thit ? r1 - (tinc - tw) : tw;
-      if (l == 0) {
-        s_chunk = c_sel;
-        s_tile = t_sel;
-        if (!tlive) s_res = 0.f;
-        s_m = Mr;
-        s_z = Zr;
-        s_tok = 0x7fffffff;
-        s_fb = -1;
-      }
-    }
-    if (l == 0) {
-      __hip_atomic_store(tickets + row * kCtrStride, 0, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-      if (greedy) {
-        p.out_tokens[row] = a.i;
-        // greedy log-prob: x[tok] is the max, so log softmax = -log sum exp(x - M)
-        if (p.out_logprobs) p.out_logprobs[row] = p.greedy_logprobs ? -__logf(Zr) : 0.f;
-      } else if (filt) {  // the filter passes finish the row
-        float* r = rowsum + (size_t)row * kSelWords;  // the passes' SelState: M, Z, kmax16
-        r[0] = Mr;
-        r[1] = Zr;
-        r[11] = __int_as_float((int)(fkey(a.v) >> 16));
-      }
-    }
-  }
-  if (!draw) return;
-  __syncthreads();
-  // ---- inverse CDF, level 2: rescan the selected tile (read by this row's chunk kernel,
-  // so in L2), 8 elements per thread; a block scan of the per-thread masses finds the thread
-  // whose 8 elements cross the residual mass, which walks them ----
-  const float Mr = s_m;
-  float R = s_res;
-  const int clo = min(V, s_chunk * chunk), chi = min(V, clo + chunk);
-  const int lo2 = min(chi, clo + s_tile * kTile), hi2 = min(chi, lo2 + kTile);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  constexpr int TILE = kTile;
-  for (int t0 = lo2; t0 < hi2; t0 += TILE) {
-    const int a0 = t0 + (int)threadIdx.x * 8, a1 = min(hi2, a0 + 8);
-    float e[8];
-    float ts = 0.f;
-    int last_pos = -1;
-    float xv8[8];
-    if (vec_ok && a0 + 8 <= a1) {
-      const typename Vec<T>::type q0 = *reinterpret_cast<const typename Vec<T>::type*>(x + a0);
-      if constexpr (NV == 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv8[j] = (float)q0[j];
-      } else {
-        const typename Vec<T>::type q1 =
-            *reinterpret_cast<const typename Vec<T>::type*>(x + a0 + 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { xv8[j] = (float)q0[j]; xv8[4 + j] = (float)q1[j]; }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xv8[j] = a0 + j < a1 ? (float)x[a0 + j] : -INFINITY;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      e[j] = a0 + j < a1 ? __expf(xv8[j] * invT - Mr) : 0.f;
-      ts += e[j];
-      if (e[j] > 0.f) last_pos = a0 + j;
-    }
-    float inc = ts;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
-    }
-    if (lane == 63) sv[wid] = inc;
-    __syncthreads();
-    float before = inc - ts, total = 0.f;
-    for (int wv = 0; wv < kChunkThreads / 64; ++wv) {
-      if (wv < wid) before += sv[wv];
-      total += sv[wv];
-    }
-    if (last_pos >= 0) atomicMax(&s_fb, last_pos);
-    if (ts > 0.f && R >= before && R < before + ts) {
-      float acc = before;
-      int tok = last_pos;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        acc += e[j];
-        if (acc > R) { tok = a0 + j; break; }
-      }
-      atomicMin(&s_tok, tok);
-    }
-    __syncthreads();
-    if (s_tok != 0x7fffffff) break;  // uniform: found in this tile
-    R -= total;
-  }
-  if (threadIdx.x == 0) {
-    int tok = s_tok != 0x7fffffff ? s_tok : s_fb;  // rounding past the chunk's end: last mass
-    if (tok < 0 || tok >= V) tok = 0;
-    p.out_tokens[row] = tok;
-    if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - Mr - __logf(s_z);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Rows with top-k / top-p: exact thresholds on the 16-bit order-preserving key of the logit
-// (k16 = fkey(x) >> 16: exact for bf16 logits, the top 16 bits of an fp32 logit), found by two
-// 256-bin histogram levels -- the key's high byte, then its low byte inside the selected
-// high-byte bin -- each pass spread over the row's S chunk workgroups like the chunk kernel:
-// per-wave LDS histograms, 256 (count, mass) pairs published per chunk with sc1 stores, a
-// ticket, and the row's last chunk sums the S histograms and selects (masses are
-// exp(x / T - M) with the row max M of the chunk kernel, so they add across chunks).
-//   pass W  (count, mass) histogram of the 256 keys just below the row max: when the top-k /
-//           top-p threshold falls inside that window (any peaked distribution, and top-k
-//           for small k) the exact threshold comes out here -- only in-window elements touch
-//           the LDS -- and passes A-C return at once for the row;
-//   pass A  high-byte histogram of the whole row -> top-k's high byte (by count) or, for a
-//           top-p-only row, top-p's high byte (by mass);
-//   pass B  low-byte histogram inside that bin -> the exact top-k key (and Zk, the top-k mass)
-//           or the exact top-p key; top-k + top-p: top-p over the top-k set, whose crossing is
-//           either inside top-k's bin (exact now) or in a higher high-byte bin (pass C);
-//   pass C  low-byte mass histogram of that higher bin -> the exact top-p key;
-//   pass D  Gumbel-max draw over {k16 >= tau} (RNG only for survivors), best per chunk, the
-//           last chunk picks the row's token.
-// Every pass reads the row once in parallel (from L2 / MALL after the chunk kernel); rows
-// without filters leave every pass at once, and a batch with no filtered row launches none
-// of them (ops.sample(filtered=False)).
 // state words: 0 M, 1 Z, 2 flags (1 top-k, 2 top-p), 3 sel_hi (pass B bin), 4 cnt_above,
 // 5 mass_above, 6 tau (final key threshold, or -1 pending), 7 Zk, 8 p_hi (pass C bin or -1),
 // 9 p_above (mass strictly above p_hi's bin inside the top-k set), 10 p_target
@@ -611,6 +362,379 @@ __device__ __forceinline__ int suffix_select(float v, float target, float* scrat
   return 255 - s_pos;
 }
 
+// Filtered rows, inside the chunk kernel (pass W): the (count, mass) histogram of the 256
+// 16-bit keys just below the CHUNK's max key kmc (bin b = key kmc - 255 + b; masses in units
+// of exp(z - the chunk's max Mc)), published with sc1 stores to the row's histogram area at
+// chunk c.  The row window [km - 255, km] (km = the row max key) is covered: a key of this
+// chunk inside it is <= kmc and >= km - 255 >= kmc - 255.  Only in-window elements touch the
+// LDS; the chunk was just read, so this second visit comes from L2.
+template <typename T>
+__device__ __forceinline__ void window_publish(const T* x, int lo, int hi, bool vec_ok,
+                                               float invT, float Mc, int kmc, float2* hrow,
+                                               int S, int c) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __shared__ float wl[8 * 256];  // [4 waves][256] counts, then [4 waves][256] masses
+  const int tid = threadIdx.x, wid = tid >> 6;
+  for (int i = tid; i < 8 * 256; i += kChunkThreads) wl[i] = 0.f;
+  __syncthreads();
+  const int base = kmc - 255;
+  visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+    const int b = k16_of(v) - base;
+    if (ok && b >= 0 && b < 256) {
+      atomicAdd(&wl[wid * 256 + b], 1.f);
+      atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
+    }
+  });
+  __syncthreads();
+  float cc = 0.f, mm = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    cc += wl[w * 256 + tid];
+    mm += wl[1024 + w * 256 + tid];
+  }
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)hrow, (short)0, (int)(S * 256 * 8), 0x00020000);
+  u32x2 v2;
+  v2[0] = __float_as_uint(cc);
+  v2[1] = __float_as_uint(mm);
+  __builtin_amdgcn_raw_buffer_store_b64(v2, rh, (c * 256 + tid) * 8, 0, kSc1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (ticket next)
+  __syncthreads();
+}
+
+// The row's last chunk: sum the S chunk windows shifted onto the row window (bin b = key
+// km - 255 + b; masses rescaled to exp(z - Mr)), then select.  Resolved when the threshold
+// lies inside the window: top-k by count (the window holds >= k elements), top-p by mass
+// (the window holds >= the target mass, with a margin over the rounding of two summation
+// orders), top-k + top-p as top-p over the top-k set (inside the window with it).  Every
+// thread calls it (tid = bin); thread 0 writes the row's SelState.
+__device__ __forceinline__ void window_select(const SampleParams& p, int row, SelState& rs,
+                                              const float2* hrow, int S, int km, float Mr,
+                                              float Zr, const int* ckm, const float* crm) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __shared__ float scratch[16];
+  const int tid = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)hrow, (short)0, (int)(S * 256 * 8), 0x00020000);
+  float cnt = 0.f, mass = 0.f;
+  for (int q0 = 0; q0 < S; q0 += 16) {
+    u32x2 r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = min(q0 + k, S - 1);
+      const int off = min(255, tid + (km - ckm[q]));
+      r[k] = __builtin_amdgcn_raw_buffer_load_b64(rh, (q * 256 + off) * 8, 0, kSc1);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = q0 + k;
+      if (q < S && tid + (km - ckm[q]) <= 255 && crm[q] > -INFINITY) {
+        cnt += __uint_as_float(r[k][0]);
+        mass += __uint_as_float(r[k][1]) * __expf(crm[q] - Mr);
+      }
+    }
+  }
+  const int kk = p.top_k ? p.top_k[row] : 0;
+  const float tp = p.top_p ? p.top_p[row] : 1.f;
+  const bool has_k = kk > 0 && kk < p.V, has_p = tp < 1.f && tp > 0.f;
+  const int base = km - 255;
+  int tau = -1;
+  float above, Zk = 0.f;
+  if (has_k) {
+    if (block_sum(cnt, scratch) >= (float)kk) {  // integer counts: exact
+      const int bk = suffix_select(cnt, (float)kk, scratch, &above);
+      if (!has_p) {
+        tau = base + bk;
+      } else {  // top-p over the top-k set, which lies inside the window
+        const float mk = tid >= bk ? mass : 0.f;
+        Zk = block_sum(mk, scratch);
+        const int bp = suffix_select(mk, tp * Zk, scratch, &above);
+        tau = base + max(bk, bp);
+      }
+    }
+  } else {
+    const float target = tp * Zr;
+    if (block_sum(mass, scratch) >= target * 1.0001f)
+      tau = base + suffix_select(mass, target, scratch, &above);
+  }
+  if (tid == 0) {
+    rs.M = Mr;
+    rs.Z = Zr;
+    rs.kmax16 = km;
+    rs.tau = tau;
+    rs.Zk = Zk;
+    rs.p_hi = -1;
+    rs.resolved = tau >= 0 ? 1 : 0;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParams p, SampPart* ws,
+                                                                     int* tickets, float* rowsum,
+                                                                     float* tiles, float2* hist) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  __shared__ int s_last;
+  const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
+  const T* x = reinterpret_cast<const T*>(p.logits) + (size_t)row * p.ld;
+  const int V = p.V;
+  const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  constexpr int NV = Vec<T>::N;
+  const int chunk = ((V + S - 1) / S + NV - 1) / NV * NV;
+  const int lo = min(V, c * chunk), hi = min(V, lo + chunk);
+  const float temp = p.temperature ? p.temperature[row] : 0.f;
+  const bool greedy = !(temp > 0.f);
+  const bool filt = row_filtered(p, row, temp);
+  const float invT = greedy ? 1.f : 1.f / temp;
+  const bool need_sum = !greedy || (p.greedy_logprobs && p.out_logprobs);
+  const uint64_t seed = p.seeds ? (uint64_t)p.seeds[row] : 0x1234ull + row;
+  const uint32_t step = p.steps ? (uint32_t)p.steps[row] : 0u;
+
+  // ---- one pass over the chunk (the three row kinds as separate loops: no per-element
+  // branch on the row kind) ----
+  float m = -INFINITY, sum = 0.f;
+  float2 dmz = make_float2(-INFINITY, 0.f);
+  ArgBest best{-INFINITY, 0x7fffffff};
+  if (!need_sum) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
+      if (v > best.v) { best.v = v; best.i = i; }  // ascending i per thread: first max kept
+    });
+  } else if (!greedy && !filt) {
+    dmz = draw_tiles(x, lo, hi, vec_ok, invT,
+                     tiles + ((size_t)row * kMaxChunks + c) * kMaxTiles);
+  } else {  // greedy with log-probs, or a filtered row
+    visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
+      if (v > best.v) { best.v = v; best.i = i; }
+      const float z = v * invT;
+      if (z > m) { sum = sum * __expf(m - z) + 1.f; m = z; }
+      else if (z > -INFINITY) sum += __expf(z - m);
+    });
+  }
+  // workgroup reductions
+  const bool draw = !greedy && !filt;  // uniform over the workgroup
+  // (filtered rows: the row max feeds pass W's window)
+  if (!need_sum || greedy || filt) best = block_argmax(best, sv, si);
+  float M = -INFINITY, Z = 0.f;
+  if (draw) {
+    M = dmz.x;
+    Z = dmz.y;
+  } else if (need_sum) {
+    M = block_max(m, sv);
+    Z = block_sum(m == -INFINITY ? 0.f : sum * __expf(m - M), sv);
+  }
+  // filtered rows: the window histogram below this chunk's max (pass W, first half)
+  float2* hrow = hist + (size_t)row * kHistRow;
+  int kmc = 0;
+  if (filt) {
+    kmc = k16_of(best.v);
+    window_publish(x, lo, hi, vec_ok, invT, M, kmc, hrow, S, c);
+  }
+  // ---- publish the partial (sc1 stores), take a ticket ----
+  const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(ws + (size_t)row * S), (short)0, (int)(S * sizeof(SampPart)), 0x00020000);
+  if (threadIdx.x == 0) {
+    u32x4 a, b2;
+    a[0] = __float_as_uint(M); a[1] = __float_as_uint(Z);
+    a[2] = 0u; a[3] = 0u;
+    b2[0] = __float_as_uint(best.v); b2[1] = (uint32_t)best.i; b2[2] = (uint32_t)kmc; b2[3] = 0u;
+    __builtin_amdgcn_raw_buffer_store_b128(a, rws, c * 32, 0, kSc1);
+    __builtin_amdgcn_raw_buffer_store_b128(b2, rws, c * 32 + 16, 0, kSc1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(tickets + row * kCtrStride, 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == S - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // ---- last chunk of the row: combine the S partials (S <= 64: wave 0, sc1 loads) ----
+  __shared__ float s_m, s_z, s_res;
+  __shared__ int s_chunk, s_tile, s_tok, s_fb, s_km;
+  __shared__ int s_ckm[kMaxChunks];
+  __shared__ float s_crm[kMaxChunks];
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    float rm = -INFINITY, rs = 0.f;
+    ArgBest a{-INFINITY, 0x7fffffff};
+    if (l < S) {
+      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32, 0, kSc1);
+      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rws, l * 32 + 16, 0, kSc1);
+      rm = __uint_as_float(v0[0]); rs = __uint_as_float(v0[1]);
+      a = ArgBest{__uint_as_float(v1[0]), (int)v1[1]};
+      s_ckm[l] = (int)v1[2];
+      s_crm[l] = rm;
+    }
+    const float Mr = wave_max(rm);
+    // chunk l's mass in units of exp(z - Mr); its inclusive prefix over the chunks
+    const float w = rm == -INFINITY ? 0.f : rs * __expf(rm - Mr);
+    float incl = w;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float u = __shfl_up(incl, o, 64);
+      if (l >= o) incl += u;
+    }
+    const float Zr = __shfl(incl, 63, 64);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      ArgBest ca{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+      a = arg_better(a, ca);
+    }
+    if (draw) {
+      // inverse CDF, level 1: the chunk whose prefix mass first reaches u * Z
+      const float target = uniform01(seed, step, 0xffffffffu) * Zr;
+      const uint64_t hit = __ballot(incl >= target && w > 0.f);
+      const uint64_t live = __ballot(w > 0.f);
+      const int c_sel = hit ? __builtin_ctzll(hit) : 63 - __builtin_clzll(live);
+      // level 1.5: the tile inside that chunk, from its published tile masses (each in
+      // units of exp(z - the chunk's max))
+      const float r1 = __shfl(hit ? target - (incl - w) : w, c_sel, 64);  // rounding: last mass
+      const float scale = __expf(__shfl(rm, c_sel, 64) - Mr);
+      const int chunk_len = min(V, (c_sel + 1) * chunk) - min(V, c_sel * chunk);
+      const int ntile = (chunk_len + kTile - 1) / kTile;
+      const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(tiles + ((size_t)row * kMaxChunks + c_sel) * kMaxTiles), (short)0,
+          kMaxTiles * 4, 0x00020000);
+      const float tw = l < ntile ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                       rt, l * 4, 0, kSc1)) * scale
+                                 : 0.f;
+      float tinc = tw;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_up(tinc, o, 64);
+        if (l >= o) tinc += u;
+      }
+      const uint64_t thit = __ballot(tinc >= r1 && tw > 0.f);
+      const uint64_t tlive = __ballot(tw > 0.f);
+      const int t_sel = thit ? __builtin_ctzll(thit) : (tlive ? 63 - __builtin_clzll(tlive) : 0);
+      if (l == t_sel) s_res = thit ? r1 - (tinc - tw) : tw;
+      if (l == 0) {
+        s_chunk = c_sel;
+        s_tile = t_sel;
+        if (!tlive) s_res = 0.f;
+        s_m = Mr;
+        s_z = Zr;
+        s_tok = 0x7fffffff;
+        s_fb = -1;
+      }
+    }
+    if (l == 0) {
+      __hip_atomic_store(tickets + row * kCtrStride, 0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      if (greedy) {
+        p.out_tokens[row] = a.i;
+        // greedy log-prob: x[tok] is the max, so log softmax = -log sum exp(x - M)
+        if (p.out_logprobs) p.out_logprobs[row] = p.greedy_logprobs ? -__logf(Zr) : 0.f;
+      } else if (filt) {  // window_select below, then the filter passes, finish the row
+        s_m = Mr;
+        s_z = Zr;
+        s_km = k16_of(a.v);
+      }
+      // rows without filters: passes A-C return at once (their first read)
+      if (!filt) reinterpret_cast<SelState*>(rowsum)[row].resolved = 1;
+    }
+  }
+  if (filt) {
+    __syncthreads();
+    window_select(p, row, reinterpret_cast<SelState*>(rowsum)[row], hrow, S, s_km, s_m, s_z,
+                  s_ckm, s_crm);
+    return;
+  }
+  if (!draw) return;
+  __syncthreads();
+  // ---- inverse CDF, level 2: rescan the selected tile (read by this row's chunk kernel,
+  // so in L2), 8 elements per thread; a block scan of the per-thread masses finds the thread
+  // whose 8 elements cross the residual mass, which walks them ----
+  const float Mr = s_m;
+  float R = s_res;
+  const int clo = min(V, s_chunk * chunk), chi = min(V, clo + chunk);
+  const int lo2 = min(chi, clo + s_tile * kTile), hi2 = min(chi, lo2 + kTile);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int TILE = kTile;
+  for (int t0 = lo2; t0 < hi2; t0 += TILE) {
+    const int a0 = t0 + (int)threadIdx.x * 8, a1 = min(hi2, a0 + 8);
+    float e[8];
+    float ts = 0.f;
+    int last_pos = -1;
+    float xv8[8];
+    if (vec_ok && a0 + 8 <= a1) {
+      const typename Vec<T>::type q0 = *reinterpret_cast<const typename Vec<T>::type*>(x + a0);
+      if constexpr (NV == 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv8[j] = (float)q0[j];
+      } else {
+        const typename Vec<T>::type q1 =
+            *reinterpret_cast<const typename Vec<T>::type*>(x + a0 + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { xv8[j] = (float)q0[j]; xv8[4 + j] = (float)q1[j]; }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv8[j] = a0 + j < a1 ? (float)x[a0 + j] : -INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      e[j] = a0 + j < a1 ? __expf(xv8[j] * invT - Mr) : 0.f;
+      ts += e[j];
+      if (e[j] > 0.f) last_pos = a0 + j;
+    }
+    float inc = ts;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) sv[wid] = inc;
+    __syncthreads();
+    float before = inc - ts, total = 0.f;
+    for (int wv = 0; wv < kChunkThreads / 64; ++wv) {
+      if (wv < wid) before += sv[wv];
+      total += sv[wv];
+    }
+    if (last_pos >= 0) atomicMax(&s_fb, last_pos);
+    if (ts > 0.f && R >= before && R < before + ts) {
+      float acc = before;
+      int tok = last_pos;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc += e[j];
+        if (acc > R) { tok = a0 + j; break; }
+      }
+      atomicMin(&s_tok, tok);
+    }
+    __syncthreads();
+    if (s_tok != 0x7fffffff) break;  // uniform: found in this tile
+    R -= total;
+  }
+  if (threadIdx.x == 0) {
+    int tok = s_tok != 0x7fffffff ? s_tok : s_fb;  // rounding past the chunk's end: last mass
+    if (tok < 0 || tok >= V) tok = 0;
+    p.out_tokens[row] = tok;
+    if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - Mr - __logf(s_z);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Rows with top-k / top-p: exact thresholds on the 16-bit order-preserving key of the logit
+// (k16 = fkey(x) >> 16: exact for bf16 logits, the top 16 bits of an fp32 logit), found by two
+// 256-bin histogram levels -- the key's high byte, then its low byte inside the selected
+// high-byte bin -- each pass spread over the row's S chunk workgroups like the chunk kernel:
+// per-wave LDS histograms, 256 (count, mass) pairs published per chunk with sc1 stores, a
+// ticket, and the row's last chunk sums the S histograms and selects (masses are
+// exp(x / T - M) with the row max M of the chunk kernel, so they add across chunks).
+//   pass W  (count, mass) histogram of the 256 keys just below the row max: when the top-k /
+//           top-p threshold falls inside that window (any peaked distribution, and top-k
+//           for small k) the exact threshold comes out here -- only in-window elements touch
+//           the LDS -- and passes A-C return at once for the row;
+//   pass A  high-byte histogram of the whole row -> top-k's high byte (by count) or, for a
+//           top-p-only row, top-p's high byte (by mass);
+//   pass B  low-byte histogram inside that bin -> the exact top-k key (and Zk, the top-k mass)
+//           or the exact top-p key; top-k + top-p: top-p over the top-k set, whose crossing is
+//           either inside top-k's bin (exact now) or in a higher high-byte bin (pass C);
+//   pass C  low-byte mass histogram of that higher bin -> the exact top-p key;
+//   pass D  Gumbel-max draw over {k16 >= tau} (RNG only for survivors), best per chunk, the
+//           last chunk picks the row's token.
+// Every pass reads the row once in parallel (from L2 / MALL after the chunk kernel); rows
+// without filters leave every pass at once, and a batch with no filtered row launches none
+// of them (ops.sample(filtered=False)).
 template <typename T, bool PASS_A>
 __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams p, int pass,
                                                                     SelState* st, float2* hist,
@@ -622,9 +746,11 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   __shared__ float lds[PASS_A ? 256 * 64 : 12 * 256];  // 64 KB only for pass A's lane copies
   __shared__ float scratch[16];
   const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
+  SelState& rs = st[row];
+  // A-C: rows without filters, and filtered rows the window pass resolved (one read)
+  if (pass < 3 && rs.resolved) return;
   const float temp = p.temperature ? p.temperature[row] : 0.f;
   if (!row_filtered(p, row, temp)) return;  // uniform
-  SelState& rs = st[row];
   const T* x = reinterpret_cast<const T*>(p.logits) + (size_t)row * p.ld;
   const int V = p.V;
   const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
@@ -640,7 +766,6 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
   const float tp = p.top_p ? p.top_p[row] : 1.f;
   const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
   if constexpr (PASS_A) {  // A: high byte of the whole row; count (top-k) or mass (top-p only)
-    if (rs.resolved) return;  // uniform per row: pass W found the threshold
     for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
     __syncthreads();
     if (has_k) {
@@ -669,58 +794,6 @@ __global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams
     }
     return;
   } else {
-  if (pass == 4) {  // W: the 256 keys [kmax16 - 255, kmax16]; bin b holds key kmax16 - 255 + b
-    const int km = rs.kmax16, base = km - 255;
-    float* lc = lds;            // [4][256] counts
-    float* lm = lds + 4 * 256;  // [4][256] masses
-    for (int i = tid; i < 8 * 256; i += kChunkThreads) lds[i] = 0.f;
-    __syncthreads();
-    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
-      const int b = k16_of(v) - base;
-      if (ok && b >= 0 && b < 256) {  // (b < 256 always: km is the row max)
-        atomicAdd(&lc[wid * 256 + b], 1.f);
-        atomicAdd(&lm[wid * 256 + b], __expf(v * invT - M));
-      }
-    });
-    __syncthreads();
-    float cc = 0.f, mm = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      cc += lc[w * 256 + tid];
-      mm += lm[w * 256 + tid];
-    }
-    float2 mine[1] = {make_float2(cc, mm)}, tot[1];
-    if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
-    const float cnt = tot[0].x, mass = tot[0].y;
-    int tau = -1;
-    float above;
-    if (has_k) {
-      if (block_sum(cnt, scratch) >= (float)kk) {  // integer counts: exact
-        const int bk = suffix_select(cnt, (float)kk, scratch, &above);
-        if (!has_p) {
-          tau = base + bk;
-        } else {  // top-p over the top-k set, which lies inside the window
-          const float mk = tid >= bk ? mass : 0.f;
-          const float Zk = block_sum(mk, scratch);
-          const int bp = suffix_select(mk, tp * Zk, scratch, &above);
-          tau = base + max(bk, bp);
-          if (tid == 0) rs.Zk = Zk;
-        }
-      }
-    } else {
-      const float target = tp * rs.Z;
-      // a margin over the rounding of two summation orders: a borderline window falls back
-      // to the full passes
-      if (block_sum(mass, scratch) >= target * 1.0001f) tau = base + suffix_select(mass, target, scratch, &above);
-    }
-    if (tid == 0) {
-      rs.tau = tau;
-      rs.p_hi = -1;
-      rs.resolved = tau >= 0 ? 1 : 0;
-    }
-    return;
-  }
-  if (rs.resolved && pass < 3) return;  // passes B, C (not D): uniform per row
   if (pass == 1) {  // B: low byte inside sel_hi (count + mass); top-k + top-p: masses above
     const int sh = rs.sel_hi;
     float* lc = lds;             // [4][256] low-byte counts
@@ -887,17 +960,17 @@ void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int fil
   float* rowsum = reinterpret_cast<float*>(st);
   float* tiles = reinterpret_cast<float*>(hist + (size_t)B * kHistRow);
   if (p.is_bf16) {
-    sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles);
+    sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles,
+                                                             hist);
     if (filtered) {
-      sample_pass_kernel<bf16, false><<<gridf, kChunkThreads, 0, s>>>(p, 4, st, hist, tickets);
       sample_pass_kernel<bf16, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
       for (int ps = 1; ps < 4; ++ps)
         sample_pass_kernel<bf16, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
     }
   } else {
-    sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles);
+    sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles,
+                                                             hist);
     if (filtered) {
-      sample_pass_kernel<float, false><<<gridf, kChunkThreads, 0, s>>>(p, 4, st, hist, tickets);
       sample_pass_kernel<float, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
       for (int ps = 1; ps < 4; ++ps)
         sample_pass_kernel<float, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
