@@ -158,22 +158,25 @@ __device__ __forceinline__ void visit_range(const T* x, int lo, int hi, bool vec
 // load under a branch would make every later wait a full drain); per tile a wave-level
 // (max, sum exp) pair, then wave 0 folds the pairs into the tile masses (units of exp(z - the
 // chunk max)), publishes them to tout with sc1 stores (drained by the caller's ticket wait in
-// the same wave) and returns the chunk's (max, sum) to every thread.
-template <typename T>
+// the same wave) and returns the chunk's (max, sum) to every thread.  XMAX (filtered rows):
+// also the chunk's largest logit itself (exact, for the key window) in *xmax.
+template <typename T, bool XMAX = false>
 __device__ __forceinline__ float2 draw_tiles(const T* x, int lo, int hi, bool vec_ok, float invT,
-                                             float* tout) {
+                                             float* tout, float* xmax = nullptr) {
   __shared__ float2 s_t[kMaxTiles][kChunkThreads / 64];
   __shared__ float2 s_mz;
+  __shared__ float s_xm[kChunkThreads / 64];
+  float xm = -INFINITY;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n = hi - lo;
   const int ntile = min(kMaxTiles, (n + kTile - 1) / kTile);  // host: chunk <= kMaxTiles tiles
   const int nvf = vec_ok ? n / 8 : 0;  // 8-element groups read as 16-byte vectors
   const T* xc = x + lo;
-  float tailz[8];  // the partial last group (vector rows), owned by thread nvf % 256
+  float tailx[8];  // the partial last group (vector rows), owned by thread nvf % 256
 #pragma unroll
-  for (int j = 0; j < 8; ++j) tailz[j] = -INFINITY;
+  for (int j = 0; j < 8; ++j) tailx[j] = -INFINITY;
   if (vec_ok && nvf * 8 < n && tid == (nvf & (kChunkThreads - 1)))
-    for (int j = 0; j < n - nvf * 8; ++j) tailz[j] = (float)xc[nvf * 8 + j] * invT;
+    for (int j = 0; j < n - nvf * 8; ++j) tailx[j] = (float)xc[nvf * 8 + j];
   for (int t0 = 0; t0 < ntile; t0 += 4) {
     float z[4][8];
     if (nvf > 0) {  // uniform
@@ -200,8 +203,10 @@ __device__ __forceinline__ float2 draw_tiles(const T* x, int lo, int hi, bool ve
         const int g = (t0 + u) * kChunkThreads + tid;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = (float)q[u][j / Vec<T>::N][j % Vec<T>::N] * invT;
-          z[u][j] = g < nvf ? v : (g == nvf ? tailz[j] : -INFINITY);
+          const float v = (float)q[u][j / Vec<T>::N][j % Vec<T>::N];
+          const float xv = g < nvf ? v : (g == nvf ? tailx[j] : -INFINITY);
+          if constexpr (XMAX) xm = fmaxf(xm, xv);
+          z[u][j] = xv * invT;  // -inf stays -inf (invT > 0)
         }
       }
     } else {  // unaligned row (or < 8 elements): scalar loads, index clamped
@@ -214,8 +219,11 @@ __device__ __forceinline__ float2 draw_tiles(const T* x, int lo, int hi, bool ve
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          z[u][j] = ((t0 + u) * kChunkThreads + tid) * 8 + j < n ? q[u][j] * invT : -INFINITY;
+        for (int j = 0; j < 8; ++j) {
+          const float xv = ((t0 + u) * kChunkThreads + tid) * 8 + j < n ? q[u][j] : -INFINITY;
+          if constexpr (XMAX) xm = fmaxf(xm, xv);
+          z[u][j] = xv * invT;
+        }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // tiles past ntile (<= 63: t0 <= 60) come out empty
@@ -232,7 +240,17 @@ __device__ __forceinline__ float2 draw_tiles(const T* x, int lo, int hi, bool ve
       if (lane == 0) s_t[t0 + u][wid] = make_float2(mw, sw);
     }
   }
+  if constexpr (XMAX) {
+    xm = wave_max_dpp(xm);
+    if (lane == 0) s_xm[wid] = xm;
+  }
   __syncthreads();
+  if constexpr (XMAX) {
+    float r = s_xm[0];
+#pragma unroll
+    for (int w = 1; w < kChunkThreads / 64; ++w) r = fmaxf(r, s_xm[w]);
+    *xmax = r;
+  }
   if (wid == 0) {
     float mt = -INFINITY, stt = 0.f;
     if (lane < ntile) {
@@ -502,7 +520,10 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   } else if (!greedy && !filt) {
     dmz = draw_tiles(x, lo, hi, vec_ok, invT,
                      tiles + ((size_t)row * kMaxChunks + c) * kMaxTiles);
-  } else {  // greedy with log-probs, or a filtered row
+  } else if (filt) {  // (M, Z) as a draw row (its tile masses go unused) + the largest logit
+    dmz = draw_tiles<T, true>(x, lo, hi, vec_ok, invT,
+                              tiles + ((size_t)row * kMaxChunks + c) * kMaxTiles, &best.v);
+  } else {  // greedy with log-probs
     visit_range(x, lo, hi, vec_ok, [&](float v, int i, bool) {
       if (v > best.v) { best.v = v; best.i = i; }
       const float z = v * invT;
@@ -512,10 +533,9 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   }
   // workgroup reductions
   const bool draw = !greedy && !filt;  // uniform over the workgroup
-  // (filtered rows: the row max feeds pass W's window)
-  if (!need_sum || greedy || filt) best = block_argmax(best, sv, si);
+  if (!need_sum || greedy) best = block_argmax(best, sv, si);
   float M = -INFINITY, Z = 0.f;
-  if (draw) {
+  if (draw || filt) {
     M = dmz.x;
     Z = dmz.y;
   } else if (need_sum) {
@@ -929,17 +949,17 @@ __global__ __launch_bounds__(kChunkThreads) void sample_draw_kernel(SampleParams
   }
 }
 
-int sample_chunks(int B, int V) {
+int sample_chunks(int B, int V, int wgs) {
   static const int forced = [] {
     const char* e = std::getenv("AKAP_SAMPLE_CHUNKS");
     return e ? std::atoi(e) : 0;
   }();
   const int need = (V + kMaxTiles * kTile - 1) / (kMaxTiles * kTile);  // <= kMaxTiles tiles
   if (forced > 0) return max(need, min(forced, kMaxChunks));
-  // ~512 workgroups over the batch (each chunk streams its share with 4 loads in flight per
+  // ~wgs workgroups over the batch (each chunk streams its share with 4 loads in flight per
   // thread; more, smaller chunks pay the per-workgroup publish / ticket / combine latency more
-  // often: profiles/r5_sampler_rework.md), chunks of >= 2k elements, at most kMaxChunks
-  int S = (512 + B - 1) / max(B, 1);
+  // often: profiles/r5_sampler_rework_2.md), chunks of >= 2k elements, at most kMaxChunks
+  int S = (wgs + B - 1) / max(B, 1);
   S = min(S, max(1, V / 2048));
   S = max(S, need);
   return max(1, min(S, kMaxChunks));
@@ -955,13 +975,15 @@ long sample_ws_floats(int B) {
 // ticket, two round trips), so they take fewer, larger chunks -- ~512 workgroups per pass
 // over the batch (one round on 256 CUs), at most sample_chunks
 static int filter_chunks(int B, int V) {
-  return max(1, min(sample_chunks(B, V), 512 / max(B, 1)));
+  return max(1, min(sample_chunks(B, V, 512), 512 / max(B, 1)));
 }
 
 void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int filtered,
                    hipStream_t s) {
   if (B == 0) return;
-  const dim3 grid(sample_chunks(B, p.V), B);
+  // filtered batches: twice the chunks (the chunk kernel visits each chunk twice, and more
+  // waves per SIMD hide its per-element work)
+  const dim3 grid(sample_chunks(B, p.V, filtered ? 1024 : 512), B);
   const dim3 gridf(filter_chunks(B, p.V), B);
   SampPart* parts = (SampPart*)ws;
   SelState* st = reinterpret_cast<SelState*>(parts + (size_t)B * kMaxChunks);
