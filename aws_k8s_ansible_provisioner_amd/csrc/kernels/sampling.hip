@@ -416,8 +416,7 @@ __device__ __forceinline__ void window_publish(const T* x, int lo, int hi, bool 
   v2[0] = __float_as_uint(cc);
   v2[1] = __float_as_uint(mm);
   __builtin_amdgcn_raw_buffer_store_b64(v2, rh, (c * 256 + tid) * 8, 0, kSc1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (ticket next)
-  __syncthreads();
+  // (drained together with the chunk record, before the row ticket)
 }
 
 // The row's last chunk: sum the S chunk windows shifted onto the row window (bin b = key
@@ -559,6 +558,13 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
     b2[0] = __float_as_uint(best.v); b2[1] = (uint32_t)best.i; b2[2] = (uint32_t)kmc; b2[3] = 0u;
     __builtin_amdgcn_raw_buffer_store_b128(a, rws, c * 32, 0, kSc1);
     __builtin_amdgcn_raw_buffer_store_b128(b2, rws, c * 32 + 16, 0, kSc1);
+  }
+  if (filt) {  // every wave's window stores drain before the ticket (one round trip with the
+               // record's)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = __hip_atomic_fetch_add(tickets + row * kCtrStride, 1, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
