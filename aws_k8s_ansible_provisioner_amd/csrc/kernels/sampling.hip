@@ -389,20 +389,35 @@ __device__ __forceinline__ int suffix_select(float v, float target, float* scrat
 template <typename T>
 __device__ __forceinline__ void window_publish(const T* x, int lo, int hi, bool vec_ok,
                                                float invT, float Mc, int kmc, float2* hrow,
-                                               int S, int c) {
+                                               int S, int c, bool need_cnt, bool need_mass) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   __shared__ float wl[8 * 256];  // [4 waves][256] counts, then [4 waves][256] masses
   const int tid = threadIdx.x, wid = tid >> 6;
   for (int i = tid; i < 8 * 256; i += kChunkThreads) wl[i] = 0.f;
   __syncthreads();
   const int base = kmc - 255;
-  visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
-    const int b = k16_of(v) - base;
-    if (ok && b >= 0 && b < 256) {
-      atomicAdd(&wl[wid * 256 + b], 1.f);
-      atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
-    }
-  });
+  // only the histogram(s) the row's filters read: LDS atomics are this visit's cost (almost
+  // every wave has a lane in the window at every element slot); top-k alone counts, top-p
+  // alone weighs, top-k + top-p does both
+  if (need_cnt && need_mass) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int b = k16_of(v) - base;
+      if (ok && b >= 0 && b < 256) {
+        atomicAdd(&wl[wid * 256 + b], 1.f);
+        atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
+      }
+    });
+  } else if (need_cnt) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int b = k16_of(v) - base;
+      if (ok && b >= 0 && b < 256) atomicAdd(&wl[wid * 256 + b], 1.f);
+    });
+  } else {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int b = k16_of(v) - base;
+      if (ok && b >= 0 && b < 256) atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
+    });
+  }
   __syncthreads();
   float cc = 0.f, mm = 0.f;
 #pragma unroll
@@ -546,7 +561,9 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
   int kmc = 0;
   if (filt) {
     kmc = k16_of(best.v);
-    window_publish(x, lo, hi, vec_ok, invT, M, kmc, hrow, S, c);
+    const int kk = p.top_k ? p.top_k[row] : 0;
+    window_publish(x, lo, hi, vec_ok, invT, M, kmc, hrow, S, c, kk > 0 && kk < V,
+                   p.top_p && p.top_p[row] < 1.f && p.top_p[row] > 0.f);
   }
   // ---- publish the partial (sc1 stores), take a ticket ----
   const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
