@@ -396,27 +396,76 @@ __device__ __forceinline__ void window_publish(const T* x, int lo, int hi, bool 
   for (int i = tid; i < 8 * 256; i += kChunkThreads) wl[i] = 0.f;
   __syncthreads();
   const int base = kmc - 255;
-  // only the histogram(s) the row's filters read: LDS atomics are this visit's cost (almost
-  // every wave has a lane in the window at every element slot); top-k alone counts, top-p
-  // alone weighs, top-k + top-p does both
-  if (need_cnt && need_mass) {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
-      const int b = k16_of(v) - base;
-      if (ok && b >= 0 && b < 256) {
-        atomicAdd(&wl[wid * 256 + b], 1.f);
-        atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
+  // only the histogram(s) the row's filters read (top-k alone counts, top-p alone weighs),
+  // and the atomics compacted: LDS atomics are this visit's cost, and with ~10 % of the
+  // elements in the window almost every wave has a lane inside it at every element slot, so
+  // per-slot atomics issue 8 per vector anyway.  Each lane instead keeps its vector's hits as
+  // a bit mask (bins packed 8 bits apart) and the wave loops until every lane has flushed its
+  // hits -- as many atomic instructions as the busiest lane's hits, ~3 instead of 8.
+  const int n = hi - lo;
+  const int nvf = vec_ok ? n / 8 : 0;
+  const T* xc = x + lo;
+  auto flush = [&](const float (&v)[8], bool (&ok)[8]) {
+    uint32_t mask = 0u, blo = 0u, bhi = 0u;
+    float e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int bj = k16_of(v[j]) - base;
+      const bool hit = ok[j] && bj >= 0 && bj < 256;
+      mask |= hit ? (1u << j) : 0u;
+      if (j < 4) blo |= (uint32_t)(bj & 255) << (8 * j);
+      else bhi |= (uint32_t)(bj & 255) << (8 * (j - 4));
+      e[j] = need_mass ? __expf(v[j] * invT - Mc) : 0.f;
+    }
+    while (__ballot(mask != 0u)) {
+      if (mask) {
+        const int j = __builtin_ctz(mask);
+        const int bin = (int)(((j < 4 ? blo : bhi) >> (8 * (j & 3))) & 255u);
+        float ej = e[0];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) ej = j == q ? e[q] : ej;
+        if (need_cnt) atomicAdd(&wl[wid * 256 + bin], 1.f);
+        if (need_mass) atomicAdd(&wl[1024 + wid * 256 + bin], ej);
+        mask &= mask - 1u;
       }
-    });
-  } else if (need_cnt) {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
-      const int b = k16_of(v) - base;
-      if (ok && b >= 0 && b < 256) atomicAdd(&wl[wid * 256 + b], 1.f);
-    });
-  } else {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
-      const int b = k16_of(v) - base;
-      if (ok && b >= 0 && b < 256) atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
-    });
+    }
+  };
+  if (nvf > 0) {  // uniform: 16-byte vectors, 4 per thread in flight (index clamped)
+    using VT = typename Vec<T>::type;
+    constexpr int H = 8 / Vec<T>::N;
+    for (int g0 = tid; g0 < nvf; g0 += 4 * kChunkThreads) {
+      VT q[4][H];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int g = min(g0 + u * kChunkThreads, nvf - 1);
+#pragma unroll
+        for (int h = 0; h < H; ++h)
+          q[u][h] = *reinterpret_cast<const VT*>(xc + g * 8 + h * Vec<T>::N);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v[8];
+        bool ok[8];
+        const bool in = g0 + u * kChunkThreads < nvf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[j] = (float)q[u][j / Vec<T>::N][j % Vec<T>::N];
+          ok[j] = in;
+        }
+        flush(v, ok);
+      }
+    }
+  }
+  // the tail past the last whole vector (and unaligned rows): 8 elements per thread per trip
+  for (int e0 = nvf * 8 + tid * 8; e0 < n; e0 += kChunkThreads * 8) {
+    float v[8];
+    bool ok[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ok[j] = e0 + j < n;
+      v[j] = ok[j] ? (float)xc[e0 + j] : -INFINITY;
+    }
+    flush(v, ok);
   }
   __syncthreads();
   float cc = 0.f, mm = 0.f;
