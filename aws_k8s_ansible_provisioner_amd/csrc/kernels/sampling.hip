@@ -396,76 +396,27 @@ __device__ __forceinline__ void window_publish(const T* x, int lo, int hi, bool 
   for (int i = tid; i < 8 * 256; i += kChunkThreads) wl[i] = 0.f;
   __syncthreads();
   const int base = kmc - 255;
-  // only the histogram(s) the row's filters read (top-k alone counts, top-p alone weighs),
-  // and the atomics compacted: LDS atomics are this visit's cost, and with ~10 % of the
-  // elements in the window almost every wave has a lane inside it at every element slot, so
-  // per-slot atomics issue 8 per vector anyway.  Each lane instead keeps its vector's hits as
-  // a bit mask (bins packed 8 bits apart) and the wave loops until every lane has flushed its
-  // hits -- as many atomic instructions as the busiest lane's hits, ~3 instead of 8.
-  const int n = hi - lo;
-  const int nvf = vec_ok ? n / 8 : 0;
-  const T* xc = x + lo;
-  auto flush = [&](const float (&v)[8], bool (&ok)[8]) {
-    uint32_t mask = 0u, blo = 0u, bhi = 0u;
-    float e[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int bj = k16_of(v[j]) - base;
-      const bool hit = ok[j] && bj >= 0 && bj < 256;
-      mask |= hit ? (1u << j) : 0u;
-      if (j < 4) blo |= (uint32_t)(bj & 255) << (8 * j);
-      else bhi |= (uint32_t)(bj & 255) << (8 * (j - 4));
-      e[j] = need_mass ? __expf(v[j] * invT - Mc) : 0.f;
-    }
-    while (__ballot(mask != 0u)) {
-      if (mask) {
-        const int j = __builtin_ctz(mask);
-        const int bin = (int)(((j < 4 ? blo : bhi) >> (8 * (j & 3))) & 255u);
-        float ej = e[0];
-#pragma unroll
-        for (int q = 1; q < 8; ++q) ej = j == q ? e[q] : ej;
-        if (need_cnt) atomicAdd(&wl[wid * 256 + bin], 1.f);
-        if (need_mass) atomicAdd(&wl[1024 + wid * 256 + bin], ej);
-        mask &= mask - 1u;
+  // only the histogram(s) the row's filters read: LDS atomics are this visit's cost (almost
+  // every wave has a lane in the window at every element slot); top-k alone counts, top-p
+  // alone weighs, top-k + top-p does both
+  if (need_cnt && need_mass) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int b = k16_of(v) - base;
+      if (ok && b >= 0 && b < 256) {
+        atomicAdd(&wl[wid * 256 + b], 1.f);
+        atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
       }
-    }
-  };
-  if (nvf > 0) {  // uniform: 16-byte vectors, 4 per thread in flight (index clamped)
-    using VT = typename Vec<T>::type;
-    constexpr int H = 8 / Vec<T>::N;
-    for (int g0 = tid; g0 < nvf; g0 += 4 * kChunkThreads) {
-      VT q[4][H];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int g = min(g0 + u * kChunkThreads, nvf - 1);
-#pragma unroll
-        for (int h = 0; h < H; ++h)
-          q[u][h] = *reinterpret_cast<const VT*>(xc + g * 8 + h * Vec<T>::N);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float v[8];
-        bool ok[8];
-        const bool in = g0 + u * kChunkThreads < nvf;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          v[j] = (float)q[u][j / Vec<T>::N][j % Vec<T>::N];
-          ok[j] = in;
-        }
-        flush(v, ok);
-      }
-    }
-  }
-  // the tail past the last whole vector (and unaligned rows): 8 elements per thread per trip
-  for (int e0 = nvf * 8 + tid * 8; e0 < n; e0 += kChunkThreads * 8) {
-    float v[8];
-    bool ok[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ok[j] = e0 + j < n;
-      v[j] = ok[j] ? (float)xc[e0 + j] : -INFINITY;
-    }
-    flush(v, ok);
+    });
+  } else if (need_cnt) {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int b = k16_of(v) - base;
+      if (ok && b >= 0 && b < 256) atomicAdd(&wl[wid * 256 + b], 1.f);
+    });
+  } else {
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int b = k16_of(v) - base;
+      if (ok && b >= 0 && b < 256) atomicAdd(&wl[1024 + wid * 256 + b], __expf(v * invT - Mc));
+    });
   }
   __syncthreads();
   float cc = 0.f, mm = 0.f;
@@ -806,163 +757,45 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
 
 // ---------------------------------------------------------------------------------------
 // Rows with top-k / top-p: exact thresholds on the 16-bit order-preserving key of the logit
-// (k16 = fkey(x) >> 16: exact for bf16 logits, the top 16 bits of an fp32 logit).  Masses are
-// exp(x / T - M) with the row max M of the chunk kernel, so they add across chunks.
+// (k16 = fkey(x) >> 16: exact for bf16 logits, the top 16 bits of an fp32 logit), found by two
+// 256-bin histogram levels -- the key's high byte, then its low byte inside the selected
+// high-byte bin -- each pass spread over the row's S chunk workgroups like the chunk kernel:
+// per-wave LDS histograms, 256 (count, mass) pairs published per chunk with sc1 stores, a
+// ticket, and the row's last chunk sums the S histograms and selects (masses are
+// exp(x / T - M) with the row max M of the chunk kernel, so they add across chunks).
 //   pass W  (in the chunk kernel) (count, mass) histogram of the 256 keys just below the max:
 //           when the top-k / top-p threshold falls inside that window (any peaked
 //           distribution, and top-k for small k) the exact threshold comes out there -- only
-//           in-window elements touch the LDS -- and the row is marked resolved;
-//   pass A  high-byte histogram of the whole row, spread over the row's S chunk workgroups
-//           (per-lane LDS copies, 256 bins published per chunk with sc1 stores, a ticket, the
-//           row's last chunk sums the S histograms) -> top-k's high byte (by count) or, for a
+//           in-window elements touch the LDS -- and passes A-C return at once for the row
+//           (one read each; folding B and C into A's last chunk saved ~4 us per call but made
+//           unresolved rows 2-3x slower: profiles/r5_sampler_rework_2.md);
+//   pass A  high-byte histogram of the whole row -> top-k's high byte (by count) or, for a
 //           top-p-only row, top-p's high byte (by mass);
-//   pass B  (A's last chunk, whole row) low-byte histogram inside that bin -> the exact top-k
-//           key (and Zk, the top-k mass) or the exact top-p key; top-k + top-p: top-p over the
-//           top-k set, whose crossing is either inside top-k's bin (exact now) or in a higher
-//           high-byte bin (pass C);
-//   pass C  (same workgroup) low-byte mass histogram of that higher bin -> the exact top-p key;
+//   pass B  low-byte histogram inside that bin -> the exact top-k key (and Zk, the top-k mass)
+//           or the exact top-p key; top-k + top-p: top-p over the top-k set, whose crossing is
+//           either inside top-k's bin (exact now) or in a higher high-byte bin (pass C);
+//   pass C  low-byte mass histogram of that higher bin -> the exact top-p key;
 //   pass D  Gumbel-max draw over {k16 >= tau} (RNG only for survivors), best per chunk, the
 //           last chunk picks the row's token.
-// Rows without filters, and resolved rows, leave A at once; a batch with no filtered row
-// launches neither A nor D (ops.sample(filtered=False)).
-// Pass A (distributed over the row's chunk workgroups) then, in the row's last chunk, passes B
-// and C over the whole row by that one workgroup: they touch only the elements of one or two
-// high-byte bins, and run only for rows the window pass left unresolved, so folding them into
-// A's launch saves two launches per sampler call (each ~4.5 us even when every row returns at
-// once).  Pass D (the draw) is its own launch.
-template <typename T>
-__global__ __launch_bounds__(kChunkThreads) void sample_thresh_kernel(SampleParams p,
-                                                                      SelState* st,
-                                                                      float2* hist,
-                                                                      int* tickets) {
+// Every pass reads the row once in parallel (from L2 / MALL after the chunk kernel); rows
+// without filters leave every pass at once, and a batch with no filtered row launches none
+// of them (ops.sample(filtered=False)).
+template <typename T, bool PASS_A>
+__global__ __launch_bounds__(kChunkThreads) void sample_pass_kernel(SampleParams p, int pass,
+                                                                    SelState* st, float2* hist,
+                                                                    int* tickets) {
   // pass A: a per-LANE copy of the high-byte histogram ([bin][lane], 64 KB): a wave's 64
   // lanes never add to the same word (logits crowd into a few exponent bins, and same-word
-  // LDS atomics inside one instruction serialise); passes B / C reuse it as per-wave
-  // histograms of the few elements inside one high-byte bin (and, for top-k + top-p, above it)
-  __shared__ float lds[256 * 64];
+  // LDS atomics inside one instruction serialise); passes B / C: per-wave histograms of the
+  // few elements inside one high-byte bin (and, for top-k + top-p, above it)
+  __shared__ float lds[PASS_A ? 256 * 64 : 12 * 256];  // 64 KB only for pass A's lane copies
   __shared__ float scratch[16];
   const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
   SelState& rs = st[row];
-  if (rs.resolved) return;  // rows without filters, and rows the window pass resolved
+  // A-C: rows without filters, and filtered rows the window pass resolved (one read)
+  if (pass < 3 && rs.resolved) return;
   const float temp = p.temperature ? p.temperature[row] : 0.f;
   if (!row_filtered(p, row, temp)) return;  // uniform
-  const T* x = reinterpret_cast<const T*>(p.logits) + (size_t)row * p.ld;
-  const int V = p.V;
-  const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  constexpr int NV = Vec<T>::N;
-  const int chunk = ((V + S - 1) / S + NV - 1) / NV * NV;
-  const int lo = min(V, c * chunk), hi = min(V, lo + chunk);
-  const float invT = 1.f / temp;
-  const float M = rs.M, Z = rs.Z;
-  int* ticket = tickets + row * kCtrStride;
-  float2* hrow = hist + (size_t)row * kHistRow;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int kk = p.top_k ? p.top_k[row] : 0;
-  const float tp = p.top_p ? p.top_p[row] : 1.f;
-  const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
-  // ---- A: high byte of the whole row; count (top-k) or mass (top-p only) ----
-  for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
-  __syncthreads();
-  if (has_k) {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
-      atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], ok ? 1.f : 0.f);
-    });
-  } else {
-    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool) {  // -inf: mass 0
-      atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], __expf(v * invT - M));
-    });
-  }
-  __syncthreads();
-  float hv = 0.f;  // bin tid over the 64 lane copies (rotated: conflict-free)
-#pragma unroll 8
-  for (int j = 0; j < 64; ++j) hv += lds[tid * 64 + ((j + lane) & 63)];
-  float2 mine[1] = {make_float2(hv, 0.f)}, tot[1];
-  if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
-  float a_above;
-  const int sh = suffix_select(tot[0].x, has_k ? (float)kk : tp * Z, scratch, &a_above);
-  // ---- B (this workgroup, whole row): low byte inside sh (count + mass); top-k + top-p:
-  // the masses of the high-byte bins above sh ----
-  float* lc = lds;             // [4][256] low-byte counts
-  float* lm = lds + 4 * 256;   // [4][256] low-byte masses
-  float* hm = lds + 8 * 256;   // [4][256] high-byte masses of bins above sh
-  __syncthreads();
-  for (int i = tid; i < 12 * 256; i += kChunkThreads) lds[i] = 0.f;
-  __syncthreads();
-  const bool above_too = has_k && has_p;
-  visit_range(x, 0, V, vec_ok, [&](float v, int, bool ok) {
-    const int k = k16_of(v), h = k >> 8;
-    if (!ok) return;
-    if (h == sh) {
-      atomicAdd(&lc[wid * 256 + (k & 255)], 1.f);
-      atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
-    } else if (above_too && h > sh) {
-      atomicAdd(&hm[wid * 256 + h], __expf(v * invT - M));
-    }
-  });
-  __syncthreads();
-  float cnt = 0.f, mass = 0.f, hmass = 0.f;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    cnt += lc[w * 256 + tid];
-    mass += lm[w * 256 + tid];
-    hmass += hm[w * 256 + tid];
-  }
-  float above;
-  int tau = -1, p_hi = -1;
-  float p_above = 0.f, p_target = 0.f, Zk = 0.f;
-  if (has_k) {
-    const int b = suffix_select(cnt, (float)kk - a_above, scratch, &above);
-    const int tau_k = (sh << 8) | b;
-    if (!has_p) {
-      tau = tau_k;
-    } else {
-      // top-p over the top-k set: Zk = masses of the high-byte bins above sh + low bins >= b
-      const float hsum = block_sum(hmass, scratch);
-      Zk = hsum + block_sum(tid >= b ? mass : 0.f, scratch);
-      p_target = tp * Zk;
-      if (hsum >= p_target) {  // crossing in a higher high-byte bin: C resolves it
-        p_hi = suffix_select(hmass, p_target, scratch, &p_above);
-        tau = tau_k;
-      } else {
-        float lab;
-        const int lb = suffix_select(tid >= b ? mass : 0.f, p_target - hsum, scratch, &lab);
-        tau = max(tau_k, (sh << 8) | lb);
-      }
-    }
-  } else {
-    tau = (sh << 8) | suffix_select(mass, tp * Z - a_above, scratch, &above);
-  }
-  // ---- C (rare): low-byte masses inside p_hi (top-k + top-p crossing above sh) ----
-  if (p_hi >= 0) {  // uniform
-    __syncthreads();
-    for (int i = tid; i < 4 * 256; i += kChunkThreads) lds[i] = 0.f;
-    __syncthreads();
-    visit_range(x, 0, V, vec_ok, [&](float v, int, bool ok) {
-      const int k = k16_of(v);
-      if (ok && (k >> 8) == p_hi) atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
-    });
-    __syncthreads();
-    float mm = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) mm += lm[w * 256 + tid];
-    tau = (p_hi << 8) | suffix_select(mm, p_target - p_above, scratch, &above);
-  }
-  if (tid == 0) {
-    rs.tau = tau;
-    rs.Zk = Zk;
-    rs.p_hi = -1;
-  }
-}
-
-// Pass D: Gumbel-max draw over the survivors {k16 >= tau}, best per chunk, the row's last
-// chunk picks the token.
-template <typename T>
-__global__ __launch_bounds__(kChunkThreads) void sample_draw_kernel(SampleParams p, SelState* st,
-                                                                    float2* hist, int* tickets) {
-  const int row = blockIdx.y, c = blockIdx.x, S = gridDim.x;
-  const float temp = p.temperature ? p.temperature[row] : 0.f;
-  if (!row_filtered(p, row, temp)) return;  // uniform
-  SelState& rs = st[row];
   const T* x = reinterpret_cast<const T*>(p.logits) + (size_t)row * p.ld;
   const int V = p.V;
   const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
@@ -973,7 +806,117 @@ __global__ __launch_bounds__(kChunkThreads) void sample_draw_kernel(SampleParams
   const float M = rs.M;
   int* ticket = tickets + row * kCtrStride;
   float2* hrow = hist + (size_t)row * kHistRow;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kk = p.top_k ? p.top_k[row] : 0;
+  const float tp = p.top_p ? p.top_p[row] : 1.f;
+  const bool has_k = kk > 0 && kk < V, has_p = tp < 1.f && tp > 0.f;
+  if constexpr (PASS_A) {  // A: high byte of the whole row; count (top-k) or mass (top-p only)
+    for (int i = tid; i < 256 * 64; i += kChunkThreads) lds[i] = 0.f;
+    __syncthreads();
+    if (has_k) {
+      visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], ok ? 1.f : 0.f);
+      });
+    } else {
+      visit_range(x, lo, hi, vec_ok, [&](float v, int, bool) {  // -inf: mass 0
+        atomicAdd(&lds[(k16_of(v) >> 8) * 64 + lane], __expf(v * invT - M));
+      });
+    }
+    __syncthreads();
+    float v = 0.f;  // bin tid over the 64 lane copies (rotated: conflict-free)
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) v += lds[tid * 64 + ((j + lane) & 63)];
+    float2 mine[1] = {make_float2(v, 0.f)}, tot[1];
+    if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
+    float above;
+    const int b = suffix_select(tot[0].x, has_k ? (float)kk : tp * rs.Z, scratch, &above);
+    if (tid == 0) {
+      rs.sel_hi = b;
+      if (has_k) rs.cnt_above = above;
+      else { rs.mass_above = above; rs.p_target = tp * rs.Z; }
+      rs.tau = -1;
+      rs.p_hi = -1;
+    }
+    return;
+  } else {
+  if (pass == 1) {  // B: low byte inside sel_hi (count + mass); top-k + top-p: masses above
+    const int sh = rs.sel_hi;
+    float* lc = lds;             // [4][256] low-byte counts
+    float* lm = lds + 4 * 256;   // [4][256] low-byte masses
+    float* hm = lds + 8 * 256;   // [4][256] high-byte masses of bins above sh
+    for (int i = tid; i < 12 * 256; i += kChunkThreads) lds[i] = 0.f;
+    __syncthreads();
+    const bool above_too = has_k && has_p;
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int k = k16_of(v), h = k >> 8;
+      if (!ok) return;
+      if (h == sh) {
+        atomicAdd(&lc[wid * 256 + (k & 255)], 1.f);
+        atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
+      } else if (above_too && h > sh) {
+        atomicAdd(&hm[wid * 256 + h], __expf(v * invT - M));
+      }
+    });
+    __syncthreads();
+    float cc = 0.f, mm = 0.f, hh = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      cc += lc[w * 256 + tid];
+      mm += lm[w * 256 + tid];
+      hh += hm[w * 256 + tid];
+    }
+    float2 mine[2] = {make_float2(cc, mm), make_float2(hh, 0.f)}, tot[2];
+    if (!publish_combine<2>(mine, hrow, S, c, ticket, tot)) return;
+    const float cnt = tot[0].x, mass = tot[0].y, hmass = tot[1].x;
+    float above;
+    if (has_k) {
+      const int b = suffix_select(cnt, (float)kk - rs.cnt_above, scratch, &above);
+      const int tau_k = (sh << 8) | b;
+      if (!has_p) {
+        if (tid == 0) rs.tau = tau_k;
+        return;
+      }
+      // top-p over the top-k set: Zk = masses of the high-byte bins above sh + low bins >= b
+      const float hsum = block_sum(hmass, scratch);
+      const float Zk = hsum + block_sum(tid >= b ? mass : 0.f, scratch);
+      const float target = tp * Zk;
+      if (hsum >= target) {  // crossing in a higher high-byte bin: pass C resolves it
+        float habove;
+        const int hb = suffix_select(hmass, target, scratch, &habove);
+        if (tid == 0) { rs.p_hi = hb; rs.p_above = habove; rs.p_target = target; rs.tau = tau_k; }
+        return;
+      }
+      float lab;
+      const int lb = suffix_select(tid >= b ? mass : 0.f, target - hsum, scratch, &lab);
+      if (tid == 0) { rs.tau = max(tau_k, (sh << 8) | lb); rs.Zk = Zk; }
+      return;
+    }
+    const int b = suffix_select(mass, rs.p_target - rs.mass_above, scratch, &above);
+    if (tid == 0) rs.tau = (sh << 8) | b;
+    return;
+  }
+  if (pass == 2) {  // C: low-byte masses inside p_hi (top-k + top-p rows crossing above sh)
+    const int ph = rs.p_hi;
+    if (ph < 0) return;  // uniform per row
+    float* lm = lds;
+    for (int i = tid; i < 4 * 256; i += kChunkThreads) lds[i] = 0.f;
+    __syncthreads();
+    visit_range(x, lo, hi, vec_ok, [&](float v, int, bool ok) {
+      const int k = k16_of(v);
+      if (ok && (k >> 8) == ph) atomicAdd(&lm[wid * 256 + (k & 255)], __expf(v * invT - M));
+    });
+    __syncthreads();
+    float mm = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mm += lm[w * 256 + tid];
+    float2 mine[1] = {make_float2(mm, 0.f)}, tot[1];
+    if (!publish_combine<1>(mine, hrow, S, c, ticket, tot)) return;
+    float above;
+    const int b = suffix_select(tot[0].x, rs.p_target - rs.p_above, scratch, &above);
+    if (tid == 0) { rs.tau = (ph << 8) | b; rs.p_hi = -1; }
+    return;
+  }
+  // D: Gumbel-max draw over the survivors
   const int tau = rs.tau;
   const uint64_t seed = p.seeds ? (uint64_t)p.seeds[row] : 0x1234ull + row;
   const uint32_t step = p.steps ? (uint32_t)p.steps[row] : 0u;
@@ -1019,6 +962,7 @@ __global__ __launch_bounds__(kChunkThreads) void sample_draw_kernel(SampleParams
     p.out_tokens[row] = tok;
     if (p.out_logprobs) p.out_logprobs[row] = (float)x[tok] * invT - M - __logf(rs.Z);
   }
+  }  // passes B, C, D
 }
 
 int sample_chunks(int B, int V, int wgs) {
@@ -1066,15 +1010,17 @@ void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int fil
     sample_chunk_kernel<bf16><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles,
                                                              hist);
     if (filtered) {
-      sample_thresh_kernel<bf16><<<gridf, kChunkThreads, 0, s>>>(p, st, hist, tickets);
-      sample_draw_kernel<bf16><<<gridf, kChunkThreads, 0, s>>>(p, st, hist, tickets);
+      sample_pass_kernel<bf16, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
+      for (int ps = 1; ps < 4; ++ps)
+        sample_pass_kernel<bf16, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
     }
   } else {
     sample_chunk_kernel<float><<<grid, kChunkThreads, 0, s>>>(p, parts, tickets, rowsum, tiles,
                                                              hist);
     if (filtered) {
-      sample_thresh_kernel<float><<<gridf, kChunkThreads, 0, s>>>(p, st, hist, tickets);
-      sample_draw_kernel<float><<<gridf, kChunkThreads, 0, s>>>(p, st, hist, tickets);
+      sample_pass_kernel<float, true><<<gridf, kChunkThreads, 0, s>>>(p, 0, st, hist, tickets);
+      for (int ps = 1; ps < 4; ++ps)
+        sample_pass_kernel<float, false><<<gridf, kChunkThreads, 0, s>>>(p, ps, st, hist, tickets);
     }
   }
 }

@@ -23,6 +23,9 @@ def main():
     V = 151936
     for B in (1, 16, 64, 256):
         x = (torch.randn(B, V, device=dev) * 3).to(torch.bfloat16)
+        # unit-scale logits: top-p 0.9's threshold lies far below the 256-key window under the
+        # max, so these rows take the distributed histogram passes (the fallback)
+        xf = torch.randn(B, V, device=dev).to(torch.bfloat16)
         seeds = torch.arange(B, device=dev, dtype=torch.int64)
         steps = torch.zeros(B, device=dev, dtype=torch.int32)
         tok = torch.empty(B, dtype=torch.int64, device=dev)
@@ -33,6 +36,7 @@ def main():
             "top-k 50": (1.0, 50, 1.0),
             "top-p 0.9": (1.0, 0, 0.9),
             "k50+p0.9": (1.0, 50, 0.9),
+            "top-p 0.9 flat": (1.0, 0, 0.9),
         }
         row = []
         for name, (t, k, p) in cases.items():
@@ -40,7 +44,8 @@ def main():
             tk = torch.full((B,), k, device=dev, dtype=torch.int32)
             tp = torch.full((B,), p, device=dev)
             filt = k > 0 or p < 1.0  # the engine skips the threshold passes otherwise
-            us = gt._timed(lambda i: ops.sample(x, temp, tk, tp, seeds, steps, tok, lp,
+            xx = xf if name.endswith("flat") else x
+            us = gt._timed(lambda i: ops.sample(xx, temp, tk, tp, seeds, steps, tok, lp,
                                                 filtered=filt), 20)
             row.append(f"{name} {us:7.1f}")
         floor = B * V * 2 / 6.0e6
