@@ -19,8 +19,8 @@
 
 namespace akap {
 
-// q/k role: 16 lanes own one (token, head); lane i holds the 8 contiguous dims [8i, 8i+8)
-// (one 16-byte load / store), its rotate-half partner dims live in lane i ^ 8 and are
+// q/k role: 16 lanes own one token; lane i holds the 8 contiguous dims [8i, 8i+8) of a head
+// row (one 16-byte load / store), its rotate-half partner dims live in lane i ^ 8 and are
 // fetched with one DPP row-rotate per packed pair.  The K row goes to the cache as 16-byte
 // stores (8 dims never straddle a 32-dim fragment group).
 __device__ __forceinline__ uint32_t dpp_xor8(uint32_t v) {
@@ -28,87 +28,112 @@ __device__ __forceinline__ uint32_t dpp_xor8(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);
 }
 
+// Sum over a 16-lane DPP row (the lanes of one token), on VALU lane swaps: xor 1 and 2 as
+// quad permutes, then the half-row and row mirrors (each leaves 4-, 8-, 16-lane groups
+// uniform) -- no ds_bpermute round trips.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xf, 0xf, false));
+  return v;
+}
+
+// q/k role, token-major: 16 lanes own one token and walk its Hq + Hkv heads, 8 head rows'
+// loads in flight at a time (index clamped, so every load is unconditional); the token's
+// position, slot, rotary row and the two norm weights are read once per token instead of
+// once per (token, head) -- with one item per (token, head) the dependent position -> rotary
+// loads and the short-lived workgroups left the kernel latency-bound (~3.8 TB/s at 16k tokens).
 template <bool F8>
-__device__ __forceinline__ void qk_item(const bf16* __restrict__ qkv, int qkv_stride,
-                                        bf16* __restrict__ q_out, void* __restrict__ k_cache,
-                                        const int64_t* __restrict__ positions,
-                                        const int64_t* __restrict__ slots,
-                                        const float* __restrict__ cos_sin,
-                                        const bf16* __restrict__ q_w, const bf16* __restrict__ k_w,
-                                        int T, int Hq, int Hkv, int BS, float eps, int apply_rope) {
-  constexpr int D = 128, HALF = 64;
-  const int item = (blockIdx.x * 256 + threadIdx.x) >> 4;
+__device__ __forceinline__ void qk_tok(const bf16* __restrict__ qkv, int qkv_stride,
+                                       bf16* __restrict__ q_out, void* __restrict__ k_cache,
+                                       const int64_t* __restrict__ positions,
+                                       const int64_t* __restrict__ slots,
+                                       const float* __restrict__ cos_sin,
+                                       const bf16* __restrict__ q_w, const bf16* __restrict__ k_w,
+                                       int T, int Hq, int Hkv, int BS, float eps, int apply_rope) {
+  constexpr int D = 128, HALF = 64, HB = 8;
+  const int t = blockIdx.x * 16 + (threadIdx.x >> 4);
   const int li = threadIdx.x & 15;
-  // every lane of a 16-lane row shares the item, so rows exit together (DPP stays valid)
-  if (item >= T * (Hq + Hkv)) return;
-  const int t = item / (Hq + Hkv);
-  const int h = item % (Hq + Hkv);
-  const bool is_q = h < Hq;
-  const bf16x8 raw = *reinterpret_cast<const bf16x8*>(qkv + (size_t)t * qkv_stride + h * D +
-                                                      8 * li);
-  float x[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = bf2f(raw[j]);
-  const bf16* nw = is_q ? q_w : k_w;
-  if (nw != nullptr) {
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
-    const float inv = rsqrtf(ss / (float)D + eps);
-    const bf16x8 w = *reinterpret_cast<const bf16x8*>(nw + 8 * li);
-    // round-trip through bf16 like the reference module (norm output is bf16)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = bf2f(f2bf(x[j] * inv * bf2f(w[j])));
-  }
+  // every lane of a 16-lane row shares the token, so rows exit together (DPP stays valid)
+  if (t >= T) return;
+  const int H = Hq + Hkv;
+  f32x4 c0 = {1.f, 1.f, 1.f, 1.f}, c1 = c0, s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
   if (apply_rope) {
-    // partner values are exactly representable in bf16 here (raw input or bf16-rounded
-    // norm output), so they travel packed: 4 DPP moves for 8 values
-    uint32_t pk[4], pp[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bf16x2 v2 = {f2bf(x[2 * j]), f2bf(x[2 * j + 1])};
-      pk[j] = __builtin_bit_cast(uint32_t, v2);
-      pp[j] = dpp_xor8(pk[j]);
-    }
     const float* cs = cos_sin + (size_t)positions[t] * D + 8 * (li & 7);
-    const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs);
-    const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + 4);
-    const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + HALF);
-    const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + HALF + 4);
-    const float sg = li < 8 ? -1.f : 1.f;  // first half: x1 c - x2 s; second: x2 c + x1 s
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bf16x2 p2 = __builtin_bit_cast(bf16x2, pp[j >> 1]);
-      const float p = bf2f(p2[j & 1]);
-      const float c = j < 4 ? c0[j] : c1[j - 4];
-      const float s = j < 4 ? s0[j] : s1[j - 4];
-      x[j] = x[j] * c + sg * p * s;
-    }
-  }
-  bf16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = f2bf(x[j]);
-  if (is_q) {
-    *reinterpret_cast<bf16x8*>(q_out + ((size_t)t * Hq + h) * D + 8 * li) = o;
-    return;
+    c0 = *reinterpret_cast<const f32x4*>(cs);
+    c1 = *reinterpret_cast<const f32x4*>(cs + 4);
+    s0 = *reinterpret_cast<const f32x4*>(cs + HALF);
+    s1 = *reinterpret_cast<const f32x4*>(cs + HALF + 4);
   }
   const int64_t slot = slots[t];
-  if (slot < 0) return;
-  const int64_t blk = slot / BS;
-  const int off = (int)(slot % BS);
-  const size_t e = ((size_t)blk * Hkv + (h - Hq)) * BS * D + k_swz_offset(off) +
-                   k_dim_offset(8 * li);
-  if constexpr (F8) {
-    // from the bf16-rounded values (same rounding chain as the bf16 cache + reference)
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    u32x2 w;
-    w[0] = f32x4_to_fp8x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]);
-    w[1] = f32x4_to_fp8x4((float)o[4], (float)o[5], (float)o[6], (float)o[7]);
-    *reinterpret_cast<u32x2*>(reinterpret_cast<uint8_t*>(k_cache) + e) = w;
-  } else {
-    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(k_cache) + e) = o;
+  const bf16x8 zero8 = {};
+  const bf16x8 qw8 = q_w ? *reinterpret_cast<const bf16x8*>(q_w + 8 * li) : zero8;
+  const bf16x8 kw8 = k_w ? *reinterpret_cast<const bf16x8*>(k_w + 8 * li) : zero8;
+  const float sg = li < 8 ? -1.f : 1.f;  // first half: x1 c - x2 s; second: x2 c + x1 s
+  const bf16* row = qkv + (size_t)t * qkv_stride + 8 * li;
+  for (int h0 = 0; h0 < H; h0 += HB) {
+    bf16x8 raw[HB];
+#pragma unroll
+    for (int j = 0; j < HB; ++j) raw[j] = *reinterpret_cast<const bf16x8*>(row + min(h0 + j, H - 1) * D);
+#pragma unroll
+    for (int j = 0; j < HB; ++j) {
+      const int h = h0 + j;
+      if (h >= H) break;  // uniform
+      const bool is_q = h < Hq;
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = bf2f(raw[j][e]);
+      if (is_q ? q_w != nullptr : k_w != nullptr) {
+        float ss = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += x[e] * x[e];
+        const float inv = rsqrtf(row16_sum(ss) / (float)D + eps);
+        const bf16x8 w = is_q ? qw8 : kw8;
+        // round-trip through bf16 like the reference module (norm output is bf16)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = bf2f(f2bf(x[e] * inv * bf2f(w[e])));
+      }
+      if (apply_rope) {
+        // partner values are exactly representable in bf16 here (raw input or bf16-rounded
+        // norm output), so they travel packed: 4 DPP moves for 8 values
+        uint32_t pp[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bf16x2 v2 = {f2bf(x[2 * e]), f2bf(x[2 * e + 1])};
+          pp[e] = dpp_xor8(__builtin_bit_cast(uint32_t, v2));
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bf16x2 p2 = __builtin_bit_cast(bf16x2, pp[e >> 1]);
+          const float pv = bf2f(p2[e & 1]);
+          const float c = e < 4 ? c0[e] : c1[e - 4];
+          const float sn = e < 4 ? s0[e] : s1[e - 4];
+          x[e] = x[e] * c + sg * pv * sn;
+        }
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(x[e]);
+      if (is_q) {
+        *reinterpret_cast<bf16x8*>(q_out + ((size_t)t * Hq + h) * D + 8 * li) = o;
+      } else if (slot >= 0) {
+        const int64_t blk = slot / BS;
+        const int off = (int)(slot % BS);
+        const size_t e = ((size_t)blk * Hkv + (h - Hq)) * BS * D + k_swz_offset(off) +
+                         k_dim_offset(8 * li);
+        if constexpr (F8) {
+          // from the bf16-rounded values (same rounding chain as the bf16 cache + reference)
+          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+          u32x2 wv;
+          wv[0] = f32x4_to_fp8x4((float)o[0], (float)o[1], (float)o[2], (float)o[3]);
+          wv[1] = f32x4_to_fp8x4((float)o[4], (float)o[5], (float)o[6], (float)o[7]);
+          *reinterpret_cast<u32x2*>(reinterpret_cast<uint8_t*>(k_cache) + e) = wv;
+        } else {
+          *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(k_cache) + e) = o;
+        }
+      }
+    }
   }
 }
 
@@ -250,8 +275,8 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
     float eps, int apply_rope, int qk_blocks, int v_per_token, bf16* __restrict__ v_tail,
     const int* __restrict__ tail_slot, int num_decode) {
   if ((int)blockIdx.x < qk_blocks)
-    qk_item<F8>(qkv, qkv_stride, q_out, k_cache, positions, slots, cos_sin, q_w, k_w, T, Hq, Hkv,
-                BS, eps, apply_rope);
+    qk_tok<F8>(qkv, qkv_stride, q_out, k_cache, positions, slots, cos_sin, q_w, k_w, T, Hq, Hkv,
+               BS, eps, apply_rope);
   else if (v_per_token)
     v_item<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks);
   else
@@ -267,8 +292,7 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                const int* tail_slot, int num_decode) {
   if (T == 0 || D != 128) return;
   if (v_per_token || kv_fp8) v_tail = nullptr;  // the tail is a bf16, span-role feature
-  const long qk_threads = (long)T * (Hq + Hkv) * 16;
-  const int qk_blocks = (int)((qk_threads + 255) / 256);
+  const int qk_blocks = (T + 15) / 16;  // 16 tokens per workgroup (qk_tok)
   const int v_blocks = v_per_token ? (int)(((long)T * Hkv * 16 + 255) / 256)
                                    : ((T + V_SPAN - 1) / V_SPAN) * Hkv;
   const dim3 grid(qk_blocks + v_blocks);
