@@ -53,6 +53,7 @@ static py::dict step_info(const StepInfo& i) {
   d["max_seq_len"] = i.max_seq_len;
   d["num_preempted"] = i.num_preempted;
   d["num_decode"] = i.num_decode;
+  d["tile_rows"] = i.tile_rows;
   return d;
 }
 
@@ -101,6 +102,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readwrite("block_size", &SchedConfig::block_size)
       .def_readwrite("gqa_group", &SchedConfig::gqa_group)
       .def_readwrite("tile_rows", &SchedConfig::tile_rows)
+      .def_readwrite("tile_rows_short", &SchedConfig::tile_rows_short)
+      .def_readwrite("short_rows", &SchedConfig::short_rows)
       .def_readwrite("eos_id", &SchedConfig::eos_id)
       .def_readwrite("max_blocks_per_seq", &SchedConfig::max_blocks_per_seq)
       .def_readwrite("mixed_batching", &SchedConfig::mixed_batching)

@@ -381,6 +381,14 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
                           ? prefill_only_run_ + 1 : 0;
 
   // ---------------- flatten ----------------
+  int step_rows = cfg_.tile_rows;
+  if (cfg_.tile_rows_short > 0 && info.is_prefill) {
+    int longest = 0;
+    for (size_t s = (size_t)info.num_decode; s < sched.size(); ++s)
+      longest = std::max(longest, sched[s].second * cfg_.gqa_group);
+    if (longest <= cfg_.short_rows) step_rows = cfg_.tile_rows_short;
+  }
+  info.tile_rows = step_rows;
   int T = 0, tiles = 0, ns = 0;
   for (size_t s = 0; s < sched.size(); ++s) {
     Request* r = sched[s].first;
@@ -407,7 +415,7 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     buf.req_ids[s] = r->id;
     if (info.is_prefill && (int)s >= info.num_decode) {  // decode rows: decode kernel
       const int rows = q * cfg_.gqa_group;
-      for (int t0 = 0; t0 < rows; t0 += cfg_.tile_rows) {
+      for (int t0 = 0; t0 < rows; t0 += step_rows) {
         if (tiles >= buf.cap_tiles) throw std::runtime_error("tile buffer too small");
         buf.tile_seq[tiles] = (int)s;
         buf.tile_row[tiles] = t0;

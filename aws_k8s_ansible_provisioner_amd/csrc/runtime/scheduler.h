@@ -66,6 +66,12 @@ struct SchedConfig {
   int block_size = 32;
   int gqa_group = 1;      // q heads per kv head (prefill tile map)
   int tile_rows = 64;     // flattened query rows per prefill attention workgroup
+  // steps whose every prefill chunk has <= short_rows flattened q rows (chunk tokens x
+  // gqa_group) use tile_rows_short instead (0: off): the 8-wave 256-row prefill kernel
+  // wins on short prompts with small GQA groups and loses on long ones
+  // (profiles/r5_prefill_tile_rows.md)
+  int tile_rows_short = 0;
+  int short_rows = 1024;
   int eos_id = -1;
   int max_blocks_per_seq = 128;
   bool mixed_batching = true;
@@ -107,6 +113,7 @@ struct StepInfo {
   int max_seq_len = 0;
   int num_preempted = 0;
   int num_decode = 0;  // leading single-token decode rows (all rows of a pure decode step)
+  int tile_rows = 0;   // prefill tile map granularity of this step
 };
 
 class Scheduler {

@@ -81,6 +81,7 @@ class LLMEngine:
         sc.block_size = ecfg.block_size
         sc.gqa_group = self.runner.G
         sc.tile_rows = self.runner.tile_rows
+        sc.tile_rows_short = self.runner.tile_rows_short
         sc.eos_id = self.mcfg.eos_id
         sc.max_blocks_per_seq = self.runner.max_blocks
         sc.mixed_batching = ecfg.mixed_batching

@@ -71,8 +71,15 @@ class ModelRunner:
         # prefill tile map granularity: 128 flattened q rows per workgroup for the flash-style
         # GPU kernel (the CPU reference attention ignores the tile map)
         self.tile_rows = 128 if dev == "cuda" else 64
+        # steps whose prefill chunks all have <= 1024 flattened q rows (e.g. 512-token prompts
+        # at GQA 2) take the 8-wave 256-row kernel (bf16 caches): 86.8 vs 100.2 us at 32 x 512
+        # on Qwen3-0.6B heads, while it loses on long prompts and at GQA 4 x 512
+        # (profiles/r5_prefill_tile_rows.md)
+        self.tile_rows_short = 256 if dev == "cuda" and not ecfg.kv_cache_dtype.startswith(
+            "fp8") else 0
         if dev == "cuda" and os.environ.get("AKAP_PREFILL_TILE_ROWS") in ("128", "256"):
             self.tile_rows = int(os.environ["AKAP_PREFILL_TILE_ROWS"])  # A/B knob
+            self.tile_rows_short = 0
             if self.tile_rows == 256 and ecfg.kv_cache_dtype.startswith("fp8"):
                 self.tile_rows = 128  # the 256-row kernel needs a bf16 KV cache
         self.cap_tiles = self.cap_tokens * self.G // 64 + self.max_seqs + 1
@@ -392,7 +399,8 @@ class ModelRunner:
         nd = info.get("num_decode", 0)
         parts, ps = self.decode_partitions(nd) if nd else (1, 512)
         batch = AttnBatch(True, pos, slots, bt, sl, qs, ts, tr, parts, ps,
-                          self.workspace, tile_rows=self.tile_rows, num_decode=nd,
+                          self.workspace, tile_rows=info.get("tile_rows") or self.tile_rows,
+                          num_decode=nd,
                           v_tails=self.v_tails, tail_slot=v["tail_slot"])
         if self._ep_moe:
             moe_mod.ep_overflow_reset(self.device)

@@ -34,7 +34,7 @@ from ..models.config import get_config
 from .state import ParallelState, init_distributed
 
 _INFO_KEYS = ["is_prefill", "num_seqs", "num_tokens", "num_tiles", "num_samples",
-              "max_seq_len", "num_preempted", "num_decode"]
+              "max_seq_len", "num_preempted", "num_decode", "tile_rows"]
 # header = info + eager bit + launch mode.  eager = 1: a decode step rank 0 runs eagerly (a
 # request asked for penalties / log-probs) -- every rank then runs that step eagerly too, so
 # the group issues one and the same collective sequence (an eager expert-parallel step takes

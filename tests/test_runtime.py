@@ -48,10 +48,12 @@ def _bufs(max_seqs, cap_tokens, mb, tiles=256):
     }
 
 
-def _sched(num_blocks=64, bs=4, max_seqs=4, budget=16, max_len=64, prefix=True, G=2):
+def _sched(num_blocks=64, bs=4, max_seqs=4, budget=16, max_len=64, prefix=True, G=2,
+           tile_rows_short=0, short_rows=1024):
     c = rt.SchedConfig()
     c.max_num_seqs, c.max_num_batched_tokens, c.max_model_len = max_seqs, budget, max_len
     c.block_size, c.gqa_group, c.tile_rows, c.eos_id = bs, G, 64, 2
+    c.tile_rows_short, c.short_rows = tile_rows_short, short_rows
     c.max_blocks_per_seq = max_len // bs
     return rt.Scheduler(c, num_blocks, prefix), _bufs(max_seqs, budget + max_seqs, max_len // bs)
 
@@ -92,6 +94,22 @@ def test_prefill_tile_map_counts_gqa_rows():
     assert i["num_tiles"] == 4
     assert list(b["tile_seq"][:4]) == [0, 0, 0, 1] and list(b["tile_row"][:4]) == [0, 64, 128, 0]
     assert list(b["q_start"][:3]) == [0, 37, 39]
+
+
+def test_prefill_tile_rows_short_steps():
+    """tile_rows_short: a step whose every prefill chunk has <= short_rows flattened q rows maps
+    its tiles at the short granularity and reports it; a step with a longer chunk keeps
+    tile_rows."""
+    s2, b2 = _sched(budget=64, max_len=128, G=4, tile_rows_short=256, short_rows=160)
+    s2.add_request(1, list(range(3, 40)), 2)  # 37 * 4 = 148 rows <= 160 -> one 256-row tile
+    s2.add_request(2, [5, 6], 2)
+    i = s2.schedule(b2)
+    assert i["tile_rows"] == 256 and i["num_tiles"] == 2
+    assert list(b2["tile_seq"][:2]) == [0, 1] and list(b2["tile_row"][:2]) == [0, 0]
+    s3, b3 = _sched(budget=64, max_len=128, G=4, tile_rows_short=256, short_rows=100)
+    s3.add_request(1, list(range(3, 40)), 2)  # 148 rows > 100 -> tile_rows (64)
+    i = s3.schedule(b3)
+    assert i["tile_rows"] == 64 and i["num_tiles"] == 3
 
 
 def test_eos_stop_ids_and_min_tokens():
