@@ -251,6 +251,9 @@ struct KVPullArgs {
 void launch_kv_pull(const KVPullArgs& a, hipStream_t s);
 
 // ---- embedding.hip ----
+void launch_embedding_prep(const int64_t* ids, const void* table, const void* ln, void* residual,
+                           void* a_out, float* ss_out, float* zbuf, long zn, int T, int d,
+                           int vocab_start, int vocab_end, hipStream_t s);
 void launch_embedding(const int64_t* ids, const void* table, void* out, int T, int d,
                       int vocab_start, int vocab_end, hipStream_t s);
 

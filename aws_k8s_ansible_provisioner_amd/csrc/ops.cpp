@@ -813,6 +813,26 @@ void embedding(Tensor ids, Tensor table, Tensor out, int64_t vocab_start, int64_
                          d, vocab_start, vocab_end, cur_stream());
 }
 
+void embedding_prep(Tensor ids, Tensor table, Tensor ln, Tensor residual, Tensor a_out,
+                    Tensor ss_out, Tensor zbuf, int64_t vocab_start, int64_t vocab_end) {
+  CHECK_GPU(ids); CHECK_BF16(table); CHECK_CONTIG(table); CHECK_BF16(ln); CHECK_CONTIG(ln);
+  CHECK_BF16(residual); CHECK_CONTIG(residual); CHECK_BF16(a_out); CHECK_CONTIG(a_out);
+  CHECK_CONTIG(ss_out); CHECK_CONTIG(zbuf);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
+  TORCH_CHECK(ss_out.scalar_type() == at::kFloat && zbuf.scalar_type() == at::kFloat,
+              "ss_out / zbuf fp32");
+  const int T = ids.numel(), d = table.size(1);
+  TORCH_CHECK(d % 8 == 0 && ln.numel() == d, "embedding dim multiple of 8, ln of length d");
+  TORCH_CHECK(residual.numel() == (int64_t)T * d && a_out.numel() == (int64_t)T * d &&
+                  ss_out.numel() >= T,
+              "residual / a_out [T, d], ss_out >= T");
+  const c10::DeviceGuard g(ids.device());
+  akap::launch_embedding_prep(ids.data_ptr<int64_t>(), table.data_ptr(), ln.data_ptr(),
+                              residual.data_ptr(), a_out.data_ptr(), ss_out.data_ptr<float>(),
+                              zbuf.data_ptr<float>(), zbuf.numel(), T, d, vocab_start, vocab_end,
+                              cur_stream());
+}
+
 }  // namespace
 
 
@@ -1224,6 +1244,9 @@ TORCH_LIBRARY(akap, m) {
   m.def("kv_gather(Tensor cache, Tensor block_ids, Tensor(a!) out) -> ()");
   m.def("kv_scatter(Tensor buf, Tensor(a!) cache, Tensor block_ids) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start, int vocab_end) -> ()");
+  m.def("embedding_prep(Tensor ids, Tensor table, Tensor ln, Tensor(a!) residual, "
+        "Tensor(b!) a_out, Tensor(c!) ss_out, Tensor(d!) zbuf, int vocab_start, "
+        "int vocab_end) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
@@ -1276,4 +1299,5 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("car_all_to_all", &car_all_to_all);
   m.impl("ipc_export", &ipc_export);
   m.impl("embedding", &embedding);
+  m.impl("embedding_prep", &embedding_prep);
 }

@@ -414,10 +414,21 @@ class DecoderLM:
 
         c_qkv, c_o, c_gu, c_d = (cfg_(n) for n in ("w_qkv", "w_o", "w_gate_up", "w_down"))
         tp = self.ps.tp_size
-        residual = self.embed_tokens(input_ids)
-        ss = torch.zeros(2 * L, T, dtype=torch.float32, device=self.device)
-        a1 = ops.rms_norm(residual, self.layers[0].ln1, eps)
-        ss_in = None
+        if tp == 1:
+            # one launch (ops.embedding_prep): the embedding rows, the first layer's
+            # un-normalised input and its row sums of squares (the first projection applies
+            # the rsqrt, like every later one), and the zeroed per-layer accumulators
+            ssb = torch.empty(2 * L + 1, T, dtype=torch.float32, device=self.device)
+            ss, ss_in = ssb[:2 * L], ssb[2 * L]
+            residual = torch.empty(T, self.cfg.hidden_size, dtype=self.dtype, device=self.device)
+            a1 = torch.empty_like(residual)
+            ops.embedding_prep(input_ids, self.embed, self.layers[0].ln1, residual, a1, ss_in,
+                               ss, self.vocab_start, self.vocab_end)
+        else:
+            residual = self.embed_tokens(input_ids)
+            ss = torch.zeros(2 * L, T, dtype=torch.float32, device=self.device)
+            a1 = ops.rms_norm(residual, self.layers[0].ln1, eps)
+            ss_in = None
         for li, lw in enumerate(self.layers):
             nxt = self.layers[li + 1].w_qkv if li + 1 < L else None
             qkv = ops.dgemm(a1, lw.w_qkv, eps=eps, ss_in=ss_in, **c_qkv)

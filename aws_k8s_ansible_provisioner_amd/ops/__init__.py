@@ -585,6 +585,25 @@ def embedding(ids, table, out=None, vocab_start: int = 0, vocab_end: Optional[in
     return out
 
 
+def embedding_prep(ids, table, ln, residual, a_out, ss_out, zbuf, vocab_start: int = 0,
+                   vocab_end: Optional[int] = None):
+    """Decode prologue (csrc/kernels/embedding.hip embedding_prep_kernel): residual = the
+    embedding rows, a_out = residual * ln (un-normalised), ss_out[t] = sum of squares of row t,
+    zbuf zeroed -- one launch instead of embedding + RMSNorm + fill."""
+    if vocab_end is None:
+        vocab_end = vocab_start + table.shape[0]
+    if _native(ids):
+        torch.ops.akap.embedding_prep(ids, table, ln, residual, a_out, ss_out, zbuf,
+                                      vocab_start, vocab_end)
+        return residual, a_out, ss_out
+    x = ref.embedding(ids, table, vocab_start, vocab_end)
+    residual.copy_(x)
+    a_out.copy_((x.float() * ln.float()).to(a_out.dtype))
+    ss_out[:ids.numel()].copy_(x.float().pow(2).sum(-1))
+    zbuf.zero_()
+    return residual, a_out, ss_out
+
+
 def moe_topk_softmax(router_logits, top_k: int, renormalize: bool = True):
     T = router_logits.shape[0]
     w = torch.empty(T, top_k, dtype=torch.float32, device=router_logits.device)

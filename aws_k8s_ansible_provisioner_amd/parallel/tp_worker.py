@@ -58,7 +58,8 @@ class TPStepBroadcaster:
         return getattr(self.runner, name)
 
     def _header(self, info: dict, mode: int) -> None:
-        head = torch.tensor([info[k] for k in _INFO_KEYS] + [_is_eager_decode(info), mode],
+        vals = [int(info.get(k, 0)) for k in _INFO_KEYS]  # (hand-built infos may omit keys)
+        head = torch.tensor(vals + [_is_eager_decode(info), mode],
                             dtype=torch.int64)
         dist.broadcast(head, 0, group=self.ctrl)
 

@@ -357,6 +357,26 @@ def test_sampling_distribution_full_vocab_tiles(B, dtype, aligned):
     _close(lp, torch.log(p[tok]), atol=2e-3)
 
 
+@pytest.mark.parametrize("T,d", [(1, 1024), (37, 1024), (256, 4096), (5, 8)])
+def test_embedding_prep_matches_reference(T, d):
+    """Decode prologue in one launch: embedding rows, rows * ln, row sums of squares, and the
+    accumulator buffer zeroed -- against the fp32 reference of the three separate ops."""
+    g = torch.Generator().manual_seed(T + d)
+    table = (torch.randn(300, d, generator=g) * 0.5).bfloat16()
+    ln = torch.randn(d, generator=g).bfloat16()
+    ids = torch.randint(0, 400, (T,), generator=g)  # ids >= 300 fall outside this shard
+    x = ref.embedding(ids, table, 0, 300)
+    res = torch.empty(T, d, dtype=torch.bfloat16, device=DEV)
+    a = torch.empty_like(res)
+    ss = torch.full((T,), 7.0, device=DEV)
+    z = torch.full((3, T), 5.0, device=DEV)
+    ops.embedding_prep(ids.to(DEV), table.to(DEV), ln.to(DEV), res, a, ss, z, 0, 300)
+    _close(res, x, atol=0)
+    _close(a, (x.float() * ln.float()).bfloat16(), atol=1e-2, rtol=1e-2)
+    _close(ss, x.float().pow(2).sum(-1), atol=1e-3, rtol=1e-4)
+    assert float(z.abs().max()) == 0.0
+
+
 def test_embedding_vocab_parallel():
     table = torch.randn(1000, 1024, dtype=torch.bfloat16)
     ids = torch.tensor([0, 5, 999, 1500, 250], dtype=torch.int64)

@@ -167,7 +167,8 @@ def test_tp_step_is_one_host_broadcast(monkeypatch):
 
     bc = tp_worker.TPStepBroadcaster(FakeRunner(), ctrl_group=None)
     dec = {"is_prefill": 0, "num_seqs": 3, "num_tokens": 3, "num_tiles": 0,
-           "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3}
+           "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3,
+           "tile_rows": 0}
     assert bc.execute(dec) == "ran"
     assert len(sent) == 1 and sent[0].tolist()[-1] == tp_worker.EXECUTE
     assert sent[0].tolist()[-2] == 0  # graph-replayable decode step
@@ -196,7 +197,8 @@ def test_tp_follower_mirrors_eager_decode(monkeypatch):
     from aws_k8s_ansible_provisioner_amd.parallel import tp_worker
 
     dec = {"is_prefill": 0, "num_seqs": 3, "num_tokens": 3, "num_tiles": 0,
-           "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3}
+           "num_samples": 3, "max_seq_len": 9, "num_preempted": 0, "num_decode": 3,
+           "tile_rows": 0}
     heads = [[dec[k] for k in tp_worker._INFO_KEYS] + [1, tp_worker.EXECUTE],
              [dec[k] for k in tp_worker._INFO_KEYS] + [0, tp_worker.EXECUTE],
              [tp_worker.STOP] * (len(tp_worker._INFO_KEYS) + 2)]
