@@ -626,7 +626,8 @@ __global__ __launch_bounds__(kChunkThreads) void sample_chunk_kernel(SampleParam
       const float target = uniform01(seed, step, 0xffffffffu) * Zr;
       const uint64_t hit = __ballot(incl >= target && w > 0.f);
       const uint64_t live = __ballot(w > 0.f);
-      const int c_sel = hit ? __builtin_ctzll(hit) : 63 - __builtin_clzll(live);
+      // (no live chunk: every logit -inf -- chunk 0, whose tiles are empty too)
+      const int c_sel = hit ? __builtin_ctzll(hit) : (live ? 63 - __builtin_clzll(live) : 0);
       // level 1.5: the tile inside that chunk, from its published tile masses (each in
       // units of exp(z - the chunk's max))
       const float r1 = __shfl(hit ? target - (incl - w) : w, c_sel, 64);  // rounding: last mass

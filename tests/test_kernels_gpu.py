@@ -357,6 +357,29 @@ def test_sampling_distribution_full_vocab_tiles(B, dtype, aligned):
     _close(lp, torch.log(p[tok]), atol=2e-3)
 
 
+@pytest.mark.parametrize("k,tp", [(0, 1.0), (50, 1.0), (0, 0.9)])
+def test_sampling_fully_masked_row_stays_in_range(k, tp):
+    """A row whose every logit is -inf (a fully masked vocabulary) must not send the draw to a
+    chunk / tile index of -1: every token comes back inside [0, V), and the other rows of the
+    batch are unaffected (their greedy-equivalent hot token wins)."""
+    B, V = 4, 151936
+    logits = torch.full((B, V), -30.0)
+    for r in range(B):
+        logits[r, 1000 * (r + 1)] = 30.0
+    logits[2] = -float("inf")
+    x = logits.to(torch.bfloat16).to(DEV)
+    temp = torch.ones(B, device=DEV)
+    tk = torch.full((B,), k, dtype=torch.int32, device=DEV)
+    tpp = torch.full((B,), tp, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV)
+    steps = torch.zeros(B, dtype=torch.int32, device=DEV)
+    tok, _ = ops.sample(x, temp, tk, tpp, seeds, steps, filtered=k > 0 or tp < 1.0)
+    tok = tok.cpu()
+    assert int(tok.min()) >= 0 and int(tok.max()) < V
+    for r in (0, 1, 3):
+        assert int(tok[r]) == 1000 * (r + 1)
+
+
 @pytest.mark.parametrize("T,d", [(1, 1024), (37, 1024), (256, 4096), (5, 8)])
 def test_embedding_prep_matches_reference(T, d):
     """Decode prologue in one launch: embedding rows, rows * ln, row sums of squares, and the
