@@ -36,6 +36,13 @@ def main():
             res["g128x256"] = gt._timed(
                 gt._gd_call(M, V, K, 1, 128, 3, False, y, x, wv, 0, None, None, None, None, 256), 3)
         res["pgemm(VP)"] = gt._timed(lambda i: torch.ops.akap.pgemm(yp, x, ws[i % 3], 0, None), 3)
+        tok = torch.empty(M, dtype=torch.int64, device=dev)
+
+        def _wa(i):
+            torch.ops.akap.wgemm(y, x, wv[i % 3])
+            ops.argmax(y, tok)
+        res["wgemm+argmax"] = gt._timed(_wa, 3)
+        res["fused argmax"] = gt._timed(lambda i: ops.lm_head_argmax(x, wv[i % 3], tok), 3)
         ref = torch.nn.functional.linear(x, wv[0]).float()
         torch.ops.akap.pgemm(yp, x, ws[0], 0, None)
         err = (yp[:, :V].float() - ref).abs().max().item()
