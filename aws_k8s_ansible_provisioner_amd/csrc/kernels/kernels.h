@@ -163,15 +163,9 @@ struct WGemmArgs {
   const void* W;  // bf16 [N, K] (row stride ldw)
   void* Y;        // bf16 [M, N] (row stride ldy)
   int M, N, K, ldx, ldw, ldy;
-  // argmax form (greedy decode): no Y; each column tile writes its per-row (max, first index)
-  // of the bf16-rounded products to amax_ws[row * ntiles + tile], then a row kernel picks
-  float2* amax_ws = nullptr;
-  int64_t* amax_out = nullptr;
 };
 bool wgemm_supported(int M, int N, int K, int ldx, int ldw, int ldy);
 void launch_wgemm(const WGemmArgs& p, hipStream_t st);
-int wgemm_col_tiles(int M, int N);  // column tiles of the launch (argmax workspace rows)
-void launch_wgemm_argmax(const WGemmArgs& p, hipStream_t st);
 
 // ---- sampling.hip ----
 struct SampleParams {

@@ -58,24 +58,9 @@ __device__ __forceinline__ void wwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-// (value, column) pair better for an argmax: larger value, or equal value at a lower column
-// (the first maximum, like argmax_kernel on the bf16 logits)
-__device__ __forceinline__ void amax_better(float& v, int& c, float v2, int c2) {
-  if (v2 > v || (v2 == v && c2 < c)) { v = v2; c = c2; }
-}
-template <int CTRL>
-__device__ __forceinline__ void amax_dpp(float& v, int& c) {
-  const float v2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-  const int c2 = __builtin_amdgcn_update_dpp(0, c, CTRL, 0xf, 0xf, false);
-  amax_better(v, c, v2, c2);
-}
-
 // NTW: the weight stream's DMAs carry the non-temporal policy (aux = 2): every weight byte is
-// read by exactly one workgroup, once.  ARGMAX: greedy decode's LM head -- the logits are never
-// stored; the epilogue reduces each row of the tile to (max of the bf16-rounded values, first
-// column) and writes one pair per (row, column tile), 2.4 MB at M = 256 instead of 78 MB of
-// logits plus the argmax pass that re-reads them.
-template <int WM, bool NTW = false, bool ARGMAX = false>
+// read by exactly one workgroup, once
+template <int WM, bool NTW = false>
 __global__ __launch_bounds__(512, 2) void wgemm_kernel(WGemmArgs p) {
   using C = WCfg<WM>;
   // ONE __shared__ object (cdna_hip_programming.md "Projection GEMM at M = 256" item 4a)
@@ -148,47 +133,6 @@ __global__ __launch_bounds__(512, 2) void wgemm_kernel(WGemmArgs p) {
     }
   }
 
-  if constexpr (ARGMAX) {
-    // lane (fr, fg) holds rows i*16 + fg*4 + r, columns j*16 + fr of the wave tile: per row
-    // the best of its JN columns, then over the 16 lanes of its DPP row (fr), then over the
-    // WN waves of the row block through LDS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading the ring
-    float* bv = reinterpret_cast<float*>(lds);   // [BM rows][WN] values
-    int* bc = reinterpret_cast<int*>(bv + C::BM * C::WN);  // [BM rows][WN] columns
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = -INFINITY;
-        int c = 0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < C::JN; ++j) {
-          const int col = n0 + wn * C::WC + j * 16 + fr;
-          if (col < p.N) amax_better(v, c, bf2f(f2bf(acc[i][j][r])), col);
-        }
-        amax_dpp<0xB1>(v, c);   // quad_perm [1,0,3,2]
-        amax_dpp<0x4E>(v, c);   // quad_perm [2,3,0,1]
-        amax_dpp<0x141>(v, c);  // row_half_mirror
-        amax_dpp<0x140>(v, c);  // row_mirror: every lane of the DPP row holds the row's best
-        if (fr == 0) {
-          const int rr = wm * 64 + i * 16 + fg * 4 + r;
-          bv[rr * C::WN + wn] = v;
-          bc[rr * C::WN + wn] = c;
-        }
-      }
-    __syncthreads();
-    for (int rr = tid; rr < C::BM; rr += 512) {
-      const int row = m0 + rr;
-      if (row >= p.M) continue;
-      float v = bv[rr * C::WN];
-      int c = bc[rr * C::WN];
-#pragma unroll
-      for (int q = 1; q < C::WN; ++q) amax_better(v, c, bv[rr * C::WN + q], bc[rr * C::WN + q]);
-      p.amax_ws[(size_t)row * gridDim.x + tn] = make_float2(v, __int_as_float(c));
-    }
-    return;
-  }
   // ---- epilogue: accumulators -> bf16 wave tile in LDS -> 16-byte row-segment stores ----
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // every wave is done reading the ring
@@ -223,35 +167,6 @@ __global__ __launch_bounds__(512, 2) void wgemm_kernel(WGemmArgs p) {
 
 int wgemm_rows(int M) { return M <= 64 ? 1 : (M <= 128 ? 2 : 4); }
 
-int wgemm_col_tiles(int M, int N) {
-  const int bn = wgemm_rows(M) == 4 ? 128 : 256;
-  return (N + bn - 1) / bn;
-}
-
-// Per row: the best of its column tiles' pairs -> the token (one workgroup per row).
-__global__ __launch_bounds__(256) void wgemm_argmax_reduce_kernel(const float2* __restrict__ ws,
-                                                                  int ntiles,
-                                                                  int64_t* __restrict__ out) {
-  __shared__ float sv[4];
-  __shared__ int sc[4];
-  const int row = blockIdx.x, tid = threadIdx.x;
-  float v = -INFINITY;
-  int c = 0x7fffffff;
-  for (int t = tid; t < ntiles; t += 256) {
-    const float2 e = ws[(size_t)row * ntiles + t];
-    amax_better(v, c, e.x, __float_as_int(e.y));
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-    amax_better(v, c, __shfl_xor(v, o, 64), __shfl_xor(c, o, 64));
-  if ((tid & 63) == 0) { sv[tid >> 6] = v; sc[tid >> 6] = c; }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < 4; ++w) amax_better(v, c, sv[w], sc[w]);
-    out[row] = c == 0x7fffffff ? 0 : c;
-  }
-}
-
 bool wgemm_supported(int M, int N, int K, int ldx, int ldw, int ldy) {
   return M > 0 && N > 0 && K >= WBK && K % WBK == 0 && ldx % 8 == 0 && ldw % 8 == 0 &&
          ldy % 8 == 0;
@@ -274,20 +189,6 @@ void launch_wgemm(const WGemmArgs& p, hipStream_t st) {
     case 2: if (nt) wgemm_kernel<2, true><<<grid, 512, 0, st>>>(p); else wgemm_kernel<2><<<grid, 512, 0, st>>>(p); break;
     default: if (nt) wgemm_kernel<4, true><<<grid, 512, 0, st>>>(p); else wgemm_kernel<4><<<grid, 512, 0, st>>>(p); break;
   }
-}
-
-void launch_wgemm_argmax(const WGemmArgs& p, hipStream_t st) {
-  if (p.M == 0 || p.N == 0) return;
-  const int wmr = wgemm_rows(p.M);
-  const int bm = 64 * wmr;
-  const int ntiles = wgemm_col_tiles(p.M, p.N);
-  dim3 grid(ntiles, (p.M + bm - 1) / bm);
-  switch (wmr) {
-    case 1: wgemm_kernel<1, true, true><<<grid, 512, 0, st>>>(p); break;
-    case 2: wgemm_kernel<2, true, true><<<grid, 512, 0, st>>>(p); break;
-    default: wgemm_kernel<4, true, true><<<grid, 512, 0, st>>>(p); break;
-  }
-  wgemm_argmax_reduce_kernel<<<p.M, 256, 0, st>>>(p.amax_ws, ntiles, p.amax_out);
 }
 
 }  // namespace akap

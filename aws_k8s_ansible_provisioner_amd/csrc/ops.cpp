@@ -435,28 +435,6 @@ void wgemm(Tensor out, Tensor x, Tensor w) {
   akap::launch_wgemm(a, cur_stream());
 }
 
-// Greedy decode's LM head + argmax in two launches (wgemm.hip): the logits are never stored;
-// ws holds one (max, first column) pair per (row, column tile).
-void wgemm_argmax(Tensor x, Tensor w, Tensor ws, Tensor out_tokens, int64_t n_valid) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w);
-  CHECK_CONTIG(ws); CHECK_CONTIG(out_tokens);
-  TORCH_CHECK(ws.scalar_type() == at::kFloat && out_tokens.scalar_type() == at::kLong,
-              "wgemm_argmax: fp32 workspace, int64 tokens");
-  const int M = x.size(0), K = w.size(1);
-  const int N = n_valid > 0 ? (int)std::min<int64_t>(n_valid, w.size(0)) : (int)w.size(0);
-  TORCH_CHECK(x.size(1) == K && out_tokens.numel() >= M, "wgemm_argmax: shapes");
-  TORCH_CHECK(akap::wgemm_supported(M, N, K, x.stride(0), w.stride(0), 8),
-              "wgemm_argmax: K % 64 == 0 and 16-byte aligned rows");
-  TORCH_CHECK(ws.numel() >= (int64_t)M * akap::wgemm_col_tiles(M, N) * 2,
-              "wgemm_argmax: workspace of M x column tiles float2");
-  akap::WGemmArgs a{x.data_ptr(), w.data_ptr(), nullptr, M, N, K, (int)x.stride(0),
-                    (int)w.stride(0), 8};
-  a.amax_ws = reinterpret_cast<float2*>(ws.data_ptr<float>());
-  a.amax_out = out_tokens.data_ptr<int64_t>();
-  const c10::DeviceGuard g(x.device());
-  akap::launch_wgemm_argmax(a, cur_stream());
-}
-
 // Narrow-output decode GEMM with the K split inside the workgroup (csrc/kernels/kgemm.hip):
 // out = x @ w^T (rows scaled by rsqrt(ss_in / K + eps) when ss_in is given), epi 0 store,
 // 1 residual/next-norm (out = residual in/out, aout = bf16(out * ln_out), ss_out += row sums).
@@ -1222,7 +1200,6 @@ TORCH_LIBRARY(akap, m) {
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
       "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None, int bm=64) -> ()");
   m.def("wgemm(Tensor(a!) out, Tensor x, Tensor w) -> ()");
-  m.def("wgemm_argmax(Tensor x, Tensor w, Tensor(a!) ws, Tensor(b!) out_tokens, int n_valid) -> ()");
   m.def("pgemm(Tensor(a!) out, Tensor x, Tensor w, int epi=0, Tensor? offs=None) -> ()");
   m.def("kgemm(Tensor(a!) out, Tensor x, Tensor w, int bm, int epi, float eps, Tensor? ss_in, "
         "Tensor(b!)? ss_out, Tensor(c!)? aout, Tensor? ln_out) -> ()");
@@ -1300,7 +1277,6 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("gemm", &gemm);
   m.impl("dgemm", &dgemm);
-  m.impl("wgemm_argmax", &wgemm_argmax);
   m.impl("wgemm", &wgemm);
   m.impl("pgemm", &pgemm);
   m.impl("kgemm", &kgemm);

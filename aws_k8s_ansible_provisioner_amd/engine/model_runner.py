@@ -75,10 +75,6 @@ class ModelRunner:
         # at GQA 2) take the 8-wave 256-row kernel (bf16 caches): 86.8 vs 100.2 us at 32 x 512
         # on Qwen3-0.6B heads, while it loses on long prompts and at GQA 4 x 512
         # (profiles/r5_prefill_tile_rows.md)
-        # greedy decode steps fuse the LM head with the argmax (single rank: the vocabulary is
-        # not sharded; AKAP_LM_ARGMAX=0 keeps LM head + argmax kernel)
-        self._lm_argmax = (dev == "cuda" and self.ps.tp_size == 1
-                           and os.environ.get("AKAP_LM_ARGMAX", "1") != "0")
         self.tile_rows_short = 256 if dev == "cuda" and not ecfg.kv_cache_dtype.startswith(
             "fp8") else 0
         if dev == "cuda" and os.environ.get("AKAP_PREFILL_TILE_ROWS") in ("128", "256"):
@@ -476,15 +472,9 @@ class ModelRunner:
                           parts, ps, self.workspace, v_tails=self.v_tails,
                           tail_slot=dd["tail_slot"][:n])
         h = self.model.forward(dd["input_ids"][:n], batch, self.k_caches, self.v_caches)
-        if extras is None and self._lm_argmax and self._sample_mode(n) == "greedy":
-            # greedy steps: the LM head and the argmax in one pass, no [n, V] logits
-            # (ops.lm_head_argmax; profiles/r5_lm_head_argmax.md)
-            ops.lm_head_argmax(h, self.model.lm_head, self.out_tokens[:n],
-                               self.model.cfg.vocab_size)
-        else:
-            # sampler reads bf16 logits directly (no [n, V] fp32 cast pass)
-            logits = self.model.compute_logits(h)
-            self._sample(logits, n, extras, src=dd)
+        # sampler reads bf16 logits directly (no [n, V] fp32 cast pass)
+        logits = self.model.compute_logits(h)
+        self._sample(logits, n, extras, src=dd)
         if self._ep_moe:
             moe_mod.ep_overflow_reduce(self.device)
 

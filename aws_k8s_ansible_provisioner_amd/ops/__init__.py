@@ -313,32 +313,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     return out
 
 
-_AMAX_WS: dict = {}
-
-
-def lm_head_argmax(x: torch.Tensor, w: torch.Tensor, out_tokens: torch.Tensor,
-                   n_valid: int = 0) -> torch.Tensor:
-    """Greedy decode's LM head fused with the argmax (csrc/kernels/wgemm.hip, ARGMAX
-    epilogue): out_tokens[:M] = argmax over the first n_valid columns of bf16(x @ w.T), first
-    index on ties -- the logits are never written.  CPU: the reference of the same op."""
-    M = x.shape[0]
-    N = min(n_valid, w.shape[0]) if n_valid > 0 else w.shape[0]
-    if _native(x):
-        key = x.device
-        need = M * (-(-N // 128)) * 2
-        ws = _AMAX_WS.get(key)
-        if ws is None or ws.numel() < need:
-            # sized for 1024 rows up front: captured graphs keep the pointer, so the buffer
-            # must not be reallocated by a later, larger batch
-            ws = _AMAX_WS[key] = torch.empty(max(need, 1024 * (-(-N // 128)) * 2),
-                                             dtype=torch.float32, device=x.device)
-        torch.ops.akap.wgemm_argmax(x, w, ws, out_tokens, N)
-        return out_tokens
-    logits = (x.float() @ w[:N].float().t()).to(x.dtype).float()
-    out_tokens[:M].copy_(logits.argmax(-1))
-    return out_tokens
-
-
 def wgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w.T by the wide-row weight-streaming kernel (csrc/kernels/wgemm.hip): one
     workgroup owns all (<= 256) rows of a column tile, so each weight byte crosses HBM -> CU

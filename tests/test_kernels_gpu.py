@@ -357,28 +357,6 @@ def test_sampling_distribution_full_vocab_tiles(B, dtype, aligned):
     _close(lp, torch.log(p[tok]), atol=2e-3)
 
 
-@pytest.mark.parametrize("M", [1, 37, 64, 100, 129, 256])
-@pytest.mark.parametrize("N,n_valid", [(151936, 0), (4096 + 80, 4096 + 50)])
-def test_lm_head_argmax_matches_logits_argmax(M, N, n_valid):
-    """Greedy decode's fused LM head + argmax: the token equals argmax over the first n_valid
-    columns of the bf16 logits the plain wgemm writes (first index on ties; a planted tie
-    across column tiles picks the lower column)."""
-    g = torch.Generator().manual_seed(M + N)
-    K = 1024
-    x = (torch.randn(M, K, generator=g) * 0.5).bfloat16().to(DEV)
-    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16().to(DEV)
-    # rows 0 and 1 of w identical at two far-apart columns: an exact tie for every row's
-    # product there, made the maximum by scaling
-    w[7] = w[3000 if N > 3000 else N - 1] = (w[7].float() * 40).bfloat16()
-    logits = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    ops.wgemm(x, w, out=logits)
-    nv = n_valid or N
-    exp = logits[:, :nv].float().cpu().argmax(-1)
-    tok = torch.full((M,), -1, dtype=torch.int64, device=DEV)
-    ops.lm_head_argmax(x, w, tok, n_valid)
-    assert torch.equal(tok.cpu(), exp.cpu())
-
-
 @pytest.mark.parametrize("k,tp", [(0, 1.0), (50, 1.0), (0, 0.9)])
 def test_sampling_fully_masked_row_stays_in_range(k, tp):
     """A row whose every logit is -inf (a fully masked vocabulary) must not send the draw to a
