@@ -52,34 +52,33 @@ __device__ __forceinline__ ArgBest block_argmax(ArgBest b, float* sv, int* si) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Two launches.  A row of V ~ 152k logits is ~300 KB: one workgroup per row leaves most of
-// the 256 CUs idle at decode batch sizes (B = 64 -> 64 CUs) and re-streams the row per pass.
+// A row of V ~ 152k logits is ~300 KB: one workgroup per row leaves most of the 256 CUs idle
+// at decode batch sizes (B = 64 -> 64 CUs) and re-streams the row per pass.
 //
-// 1. sample_chunk_kernel, grid = (S chunks, B rows): every workgroup reads its chunk ONCE
-//    with 16-byte vector loads and produces, in that single pass,
+// 1. sample_chunk_kernel, grid = (S chunks, B rows; ~512 workgroups, ~1024 with filters): every
+//    workgroup streams its chunk with 16-byte loads, 4 in flight per thread, and produces
 //      greedy rows   the chunk's argmax (first index on ties);
-//      T > 0 rows    the chunk's max and partition sum of z = x / T (online: rescaled when the
-//                    max moves).
+//      T > 0 rows    per 2048-element tile the (max, sum) of z = x / T, folded into the
+//                    chunk's (max, sum) and published tile masses;
+//      filtered rows the same plus the chunk's largest logit, then a second visit (from L2)
+//                    histograms the 256 bf16 keys below it (pass W, below).
 //    The chunk publishes a 32-byte partial record with write-through (sc1) stores and takes
 //    a ticket on the row's counter (MI355X_MICROARCH.md "Valid forms", sc1 table row 1: no
 //    release / acquire fence -- each costs ~1.7 us and more behind a freshly written logits
 //    tensor); the LAST chunk of the row reads the S records with sc1 loads, combines them
-//    (max, rescaled sum), re-arms the counter and writes the token + log-prob of a greedy row,
-//    or the row summary (M, Z) of a row with filters; a row without filters is
-//    drawn there by inverse CDF: u(seed, step) * Z picks the chunk from the prefix of the
-//    chunk masses, then the tile from the chunk's published tile masses, then the workgroup
-//    rescans that one 2048-element tile (a block scan of per-thread masses) for the token --
-//    exact sampling with one exp per element in the main pass and no per-element RNG.
-// 2. sample_filter_kernel, grid = B: rows with top-k / top-p (the others return at once) find
-//    their thresholds by an adaptive radix select over the order-preserving key image -- by
-//    COUNT for top-k, by probability MASS for top-p on the top-k renormalised distribution:
-//    256 bins over the row's live key interval, the bin width a power of two, so bf16 logits
-//    (16-bit keys) take exactly 2 passes; per-lane copies of the histogram (bin-major, so a
-//    wave's 64 lanes always hit 64 different banks and never the same word) -- then the
-//    Gumbel draw over the survivors.
+//    (max, rescaled sum), re-arms the counter and writes the token + log-prob of a greedy row;
+//    a row without filters is drawn there by inverse CDF: u(seed, step) * Z picks the chunk
+//    from the prefix of the chunk masses, then the tile from the chunk's published tile
+//    masses, then the workgroup rescans that one 2048-element tile (a block scan of
+//    per-thread masses) for the token -- exact sampling with one exp per element in the main
+//    pass and no per-element RNG; a filtered row's threshold comes from the combined windows
+//    when it lies inside them (window_select).
+// 2. sample_pass_kernel (passes A-D, grid = (S, B)): thresholds the window could not resolve,
+//    by a distributed two-level radix select over the order-preserving 16-bit key -- by COUNT
+//    for top-k, by probability MASS for top-p on the top-k renormalised distribution -- then
+//    the Gumbel draw over the survivors (details above sample_pass_kernel).
 constexpr int kChunkThreads = 256;
 constexpr int kMaxChunks = 64;
-constexpr int kFilterThreads = 256;
 constexpr int kSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1-bypass loads)
 constexpr int kSelWords = 16;  // per-row state of the filter passes (32-bit words)
 // per-row histogram area of the filter passes, in float2: kMaxChunks x 512 pairs (pass B
