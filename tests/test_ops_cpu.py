@@ -191,8 +191,29 @@ def test_native_library_registers_all_ops():
     assert ops.load_native(), ops._load_error
     for name in ("rmsnorm", "fused_add_rmsnorm", "qk_norm_rope_cache", "paged_attention_prefill",
                  "paged_attention_decode", "paged_attention_decode_fused", "sample", "gemm",
-                 "moe_gemm", "moe_combine", "car_all_reduce", "kv_gather", "embedding"):
+                 "moe_gemm", "moe_combine", "car_all_reduce", "kv_gather", "embedding",
+                 "embedding_prep", "wgemm", "argmax", "car_all_to_all", "car_all_gather"):
         assert hasattr(torch.ops.akap, name), name
+
+
+def test_embedding_prep_reference_semantics():
+    """CPU path of ops.embedding_prep (the decode prologue): residual = embedding rows (zeros
+    outside the vocab shard), a_out = residual * ln, ss = row sums of squares, zbuf zeroed."""
+    g = torch.Generator().manual_seed(5)
+    V, d, T = 50, 64, 7
+    table = (torch.randn(V, d, generator=g) * 0.5).bfloat16()
+    ln = (torch.rand(d, generator=g) + 0.5).bfloat16()
+    ids = torch.tensor([0, 3, 49, 60, 7, 7, 20])
+    res = torch.empty(T, d, dtype=torch.bfloat16)
+    a = torch.empty_like(res)
+    ss = torch.empty(T)
+    z = torch.full((4, T), 3.0)
+    ops.embedding_prep(ids, table, ln, res, a, ss, z, 0, 40)  # shard [0, 40)
+    x = ref.embedding(ids, table[:40], 0, 40)
+    assert torch.equal(res, x) and float(res[2].abs().sum()) == 0.0  # id 49: other shard
+    assert torch.allclose(a.float(), (x.float() * ln.float()).bfloat16().float())
+    assert torch.allclose(ss, x.float().pow(2).sum(-1), rtol=1e-5)
+    assert float(z.abs().max()) == 0.0
 
 
 def test_fp8_cache_roundtrip_reference():
