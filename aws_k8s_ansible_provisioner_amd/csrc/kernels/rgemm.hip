@@ -27,14 +27,16 @@
 namespace akap {
 
 constexpr int RG_KS = 32;   // K per ring slot
-constexpr int RG_NS = 6;    // ring slots
-constexpr int RG_LAG = 2;   // steps a loader keeps in flight before publishing
 constexpr int RG_ROWS = 256;
+// ring slots and the steps a loader keeps in flight before publishing (NS > LAG + 1): as deep
+// as 160 KiB of LDS allows (BN 64: 20 KB slots, BN 128: 24 KB)
+template <int BN> struct RgRing { static constexpr int NS = BN == 64 ? 7 : 6, LAG = BN == 64 ? 4 : 3; };
 
 __device__ __forceinline__ int rg_g(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }  // {0,2,3,1}
 
 template <int BN>
 __global__ __launch_bounds__(512, 1) void rgemm_kernel(RGemmArgs p) {
+  constexpr int RG_NS = RgRing<BN>::NS, RG_LAG = RgRing<BN>::LAG;
   constexpr int SROWS = RG_ROWS + BN;          // rows per slot (X rows, then W rows)
   constexpr int SU = SROWS * 4;                // 16-B units per slot
   constexpr int PIECES = SROWS / 16;           // 1-KiB DMA pieces per slot
