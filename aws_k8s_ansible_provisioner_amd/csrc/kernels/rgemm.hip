@@ -32,6 +32,21 @@ constexpr int RG_ROWS = 256;
 // as 160 KiB of LDS allows (BN 64: 20 KB slots, BN 128: 24 KB)
 template <int BN> struct RgRing { static constexpr int NS = BN == 64 ? 7 : 6, LAG = BN == 64 ? 4 : 3; };
 
+// Ring counters are touched through inline asm: a compiler-visible LDS access in a wave with
+// LDS-DMA in flight makes hipcc drain vmcnt(0) first (it cannot tell the DMA targets apart from
+// the counter), which would serialise the ring to one step in flight.
+__device__ __forceinline__ unsigned rg_lds(const int* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) int*)p;
+}
+__device__ __forceinline__ int rg_poll(const int* p) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(rg_lds(p)) : "memory");
+  return v;
+}
+__device__ __forceinline__ void rg_add(int* p) {
+  asm volatile("ds_add_u32 %0, %1" ::"v"(rg_lds(p)), "v"(1) : "memory");
+}
+
 __device__ __forceinline__ int rg_g(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }  // {0,2,3,1}
 
 template <int BN>
@@ -80,8 +95,7 @@ __global__ __launch_bounds__(512, 1) void rgemm_kernel(RGemmArgs p) {
         const int s = t % RG_NS, use = t / RG_NS;
         if (use > 0) {
           int spins = 0;
-          while (__hip_atomic_load(freec + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                 use * 4) {
+          while (rg_poll(freec + s) < use * 4) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1 << 22)) { ok = false; break; }
           }
@@ -97,9 +111,7 @@ __global__ __launch_bounds__(512, 1) void rgemm_kernel(RGemmArgs p) {
       if (pub >= 0) {
         if (t < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * RG_LAG) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_fetch_add(full + pub % RG_NS, 1, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) rg_add(full + pub % RG_NS);
       }
     }
     if (!ok && lane == 0) __hip_atomic_fetch_or(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -118,8 +130,7 @@ __global__ __launch_bounds__(512, 1) void rgemm_kernel(RGemmArgs p) {
   for (int t = 0; t < nk; ++t) {
     const int s = t % RG_NS, use = t / RG_NS;
     int spins = 0;
-    while (__hip_atomic_load(full + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-           (use + 1) * 4) {
+    while (rg_poll(full + s) < (use + 1) * 4) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1 << 22)) { ok = false; break; }
     }
@@ -136,8 +147,7 @@ __global__ __launch_bounds__(512, 1) void rgemm_kernel(RGemmArgs p) {
       wf[j] = slot[row * 4 + (fg ^ rg_g(row))];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0)
-      __hip_atomic_fetch_add(freec + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) rg_add(freec + s);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
