@@ -167,17 +167,6 @@ struct WGemmArgs {
 bool wgemm_supported(int M, int N, int K, int ldx, int ldw, int ldy);
 void launch_wgemm(const WGemmArgs& p, hipStream_t st);
 
-// ---- rgemm.hip: loader / consumer ring GEMM for M <= 256 (experiment, see the file) ----
-struct RGemmArgs {
-  const void* X;  // bf16 [M, K] (row stride ldx)
-  const void* W;  // bf16 [N, K] (row stride ldw)
-  void* Y;        // bf16 [M, N] (row stride ldy)
-  int M, N, K, ldx, ldw, ldy;
-  int* err;       // set when a ring wait gave up (the result is then wrong)
-};
-bool rgemm_supported(int M, int N, int K, int bn);
-void launch_rgemm(const RGemmArgs& p, int bn, hipStream_t st);
-
 // ---- sampling.hip ----
 struct SampleParams {
   const void* logits;  // [B, V] (row stride ld), fp32 or bf16

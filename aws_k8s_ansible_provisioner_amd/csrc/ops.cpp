@@ -435,22 +435,6 @@ void wgemm(Tensor out, Tensor x, Tensor w) {
   akap::launch_wgemm(a, cur_stream());
 }
 
-// Loader / consumer ring GEMM (csrc/kernels/rgemm.hip), M <= 256: out = x @ w^T.
-void rgemm(Tensor out, Tensor x, Tensor w, int64_t bn, Tensor err) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
-  CHECK_LAST_CONTIG(x); CHECK_LAST_CONTIG(w); CHECK_LAST_CONTIG(out); CHECK_CONTIG(err);
-  TORCH_CHECK(err.scalar_type() == at::kInt, "rgemm: int32 error flag");
-  const int M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == N, "rgemm: shapes");
-  TORCH_CHECK(akap::rgemm_supported(M, N, K, (int)bn), "rgemm: M <= 256, N % bn, K % 32");
-  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
-              "rgemm: 16-byte aligned rows");
-  akap::RGemmArgs a{x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, (int)x.stride(0),
-                    (int)w.stride(0), (int)out.stride(0), err.data_ptr<int>()};
-  const c10::DeviceGuard g(x.device());
-  akap::launch_rgemm(a, (int)bn, cur_stream());
-}
-
 // Narrow-output decode GEMM with the K split inside the workgroup (csrc/kernels/kgemm.hip):
 // out = x @ w^T (rows scaled by rsqrt(ss_in / K + eps) when ss_in is given), epi 0 store,
 // 1 residual/next-norm (out = residual in/out, aout = bf16(out * ln_out), ss_out += row sums).
@@ -1216,7 +1200,6 @@ TORCH_LIBRARY(akap, m) {
       "Tensor? ss_in=None, Tensor(d!)? ss_out=None, Tensor(e!)? aout=None, "
       "Tensor? ln_out=None, int bn=0, int ns=0, Tensor(f!)? counters=None, int bm=64) -> ()");
   m.def("wgemm(Tensor(a!) out, Tensor x, Tensor w) -> ()");
-  m.def("rgemm(Tensor(a!) out, Tensor x, Tensor w, int bn, Tensor(b!) err) -> ()");
   m.def("pgemm(Tensor(a!) out, Tensor x, Tensor w, int epi=0, Tensor? offs=None) -> ()");
   m.def("kgemm(Tensor(a!) out, Tensor x, Tensor w, int bm, int epi, float eps, Tensor? ss_in, "
         "Tensor(b!)? ss_out, Tensor(c!)? aout, Tensor? ln_out) -> ()");
@@ -1294,7 +1277,6 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("gemm", &gemm);
   m.impl("dgemm", &dgemm);
-  m.impl("rgemm", &rgemm);
   m.impl("wgemm", &wgemm);
   m.impl("pgemm", &pgemm);
   m.impl("kgemm", &kgemm);

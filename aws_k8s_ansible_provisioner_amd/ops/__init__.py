@@ -313,31 +313,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     return out
 
 
-_RG_ERR: dict = {}
-
-
-def rgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
-          bn: int = 128) -> torch.Tensor:
-    """y = x @ w.T by the loader / consumer ring GEMM (csrc/kernels/rgemm.hip; M <= 256, an
-    experiment against the decode tiles).  CPU: plain matmul."""
-    M, N = x.shape[0], w.shape[0]
-    if out is None:
-        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-    if not _native(x):
-        out.copy_(torch.nn.functional.linear(x.float(), w.float()).to(out.dtype))
-        return out
-    err = _RG_ERR.get(x.device)
-    if err is None:
-        err = _RG_ERR[x.device] = torch.zeros(1, dtype=torch.int32, device=x.device)
-    torch.ops.akap.rgemm(out, x, w, bn, err)
-    return out
-
-
-def rgemm_error(device) -> int:
-    e = _RG_ERR.get(torch.device(device))
-    return int(e.item()) if e is not None else 0
-
-
 def wgemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w.T by the wide-row weight-streaming kernel (csrc/kernels/wgemm.hip): one
     workgroup owns all (<= 256) rows of a column tile, so each weight byte crosses HBM -> CU
