@@ -625,21 +625,17 @@ __device__ __forceinline__ void fa_glds16(const void* g, void* lds_wave_base) {
 // __syncthreads, whose fence would drain the DMA early).  The K image's XOR swizzle moves to
 // the per-lane DMA source address (the LDS destination of a DMA is lane-linear).
 // NW = waves per workgroup (4: 128 q rows, two workgroups per CU; 8: 256 q rows, one
-// workgroup per CU -- every staged K/V tile feeds twice the rows).  The 8-wave form has the CU
-// to itself, so nothing hides its DMA latency but its own ring: it keeps three K/V buffers,
-// two tiles in flight behind the one being computed (counted vmcnt), where the 4-wave form
-// (two workgroups per CU, 2 x 68 KiB) stays double-buffered.
+// workgroup per CU -- every staged K/V tile feeds twice the rows).
 template <bool F8, bool GL, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(AttnParams p) {
   constexpr int ROWS = 32 * NW;
   constexpr int NT = 64 * NW;    // threads
   constexpr int PW = 16 / NW;    // 1-KiB K (and V) DMA pieces per wave per tile
   static_assert(NW == 4 || (NW == 8 && GL), "the register-staged path assumes 256 threads");
-  constexpr int NBUF = NW == 8 ? 3 : 2;
-  // [buf][K | V][64 keys * 128 dims] bf16 = 32 KiB per buffer + the block ids of the first
+  // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
   // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
-  __shared__ __attribute__((aligned(16))) bf16 lds[NBUF * 2 * kFaKeys * kD + 2 * kFaBtCache];
-  int* bt_s = reinterpret_cast<int*>(lds + NBUF * 2 * kFaKeys * kD);
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 2 * kFaKeys * kD + 2 * kFaBtCache];
+  int* bt_s = reinterpret_cast<int*>(lds + 2 * 2 * kFaKeys * kD);
   // causal work grows with a tile's position: dispatch the map back to front so the
   // longest tiles start first and the grid's tail is made of short ones
   const int tile = gridDim.x - 1 - blockIdx.x;
@@ -775,10 +771,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
   int blk_next = 0;
   if constexpr (GL) {
     stage_glds(0, 0, blk_of(0));
-    if constexpr (NBUF == 3) {
-      if (ntiles > 1) stage_glds(1, 1, blk_of(1));
-    }
-    blk_next = blk_of(NBUF - 1);
+    blk_next = blk_of(1);
   } else {
     // register-staged form: per-piece block ids come from an LDS copy of the table
     for (int c = tid; c <= last_chunk; c += NT) bt_s[c] = bt[c * 32 / BS];
@@ -788,19 +781,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     __syncthreads();
   }
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = NBUF == 2 ? (t & 1) : t % NBUF;
+    const int buf = t & 1;
     const bool more = t + 1 < ntiles;
     if constexpr (GL) {
-      // tile t (issued NBUF - 1 iterations ago) landed for this wave -- with three buffers
-      // tile t + 1's 2 x PW DMAs may stay in flight; every wave's LDS reads of buffer
-      // (t - 1) % NBUF are done -> after the barrier it may be refilled with tile t + NBUF - 1
-      if (NBUF == 3 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // tile t (issued one iteration ago) landed for this wave; every wave's LDS reads of
+      // buffer buf^1 (tile t-1) are done -> after the barrier it may be refilled
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (t + NBUF - 1 < ntiles) {
-        stage_glds(t + NBUF - 1, (t + NBUF - 1) % NBUF, blk_next);
-        blk_next = blk_of(t + NBUF);
+      if (more) {
+        stage_glds(t + 1, buf ^ 1, blk_next);
+        blk_next = blk_of(t + 2);
       }
     } else {
       if (more) stage_load(t + 1);
@@ -902,7 +893,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
         }
     }
     if constexpr (!GL) {
-      if (more) stage_store(buf ^ 1);  // NBUF == 2 here
+      if (more) stage_store(buf ^ 1);
       __syncthreads();
     }
   }
