@@ -380,6 +380,53 @@ def test_sampling_fully_masked_row_stays_in_range(k, tp):
         assert int(tok[r]) == 1000 * (r + 1)
 
 
+@pytest.mark.parametrize("B,V", [(12, 128256), (300, 128256), (40, 32000)])
+def test_sampling_mixed_rows_one_batch(B, V):
+    """One launch whose rows mix every mode the server sends: greedy (T = 0), plain temperature,
+    top-k, top-p, top-k + top-p and k = 1, at Llama-3's and Llama-2's vocabularies (a partial last
+    tile) and past 256 rows.  Per-row state (resolved flags, thresholds) must not leak between
+    rows: greedy rows return the argmax, filtered rows stay inside their exact allowed set,
+    every token is in [0, V)."""
+    torch.manual_seed(B + V)
+    base = (torch.randn(B, V) * 2.0).bfloat16()
+    modes = [(0.0, 0, 1.0), (1.0, 0, 1.0), (0.8, 40, 1.0), (1.0, 0, 0.9), (0.7, 200, 0.8),
+             (1.0, 1, 1.0)]
+    temp, tk, tpp = [], [], []
+    for r in range(B):
+        t, k, p = modes[r % len(modes)]
+        temp.append(t)
+        tk.append(k)
+        tpp.append(p)
+    allowed = []
+    for r in range(B):
+        vals = base[r].float()
+        keep = torch.ones(V, dtype=torch.bool)
+        if temp[r] == 0.0:
+            keep = torch.zeros(V, dtype=torch.bool)
+            keep[vals.argmax()] = True
+        else:
+            if 0 < tk[r] < V:
+                keep &= vals >= torch.topk(vals, tk[r]).values[-1]
+            if tpp[r] < 1.0:
+                z = torch.where(keep, vals / temp[r], torch.tensor(-float("inf")))
+                pr = torch.softmax(z, -1)
+                order = torch.argsort(vals, descending=True)
+                cum = torch.cumsum(pr[order], 0)
+                n = int((cum < tpp[r] - 1e-6).sum()) + 1
+                keep &= vals >= vals[order[n - 1]]
+        allowed.append(keep)
+    logits = base.to(DEV)
+    args = (torch.tensor(temp, device=DEV), torch.tensor(tk, dtype=torch.int32, device=DEV),
+            torch.tensor(tpp, device=DEV), torch.arange(B, dtype=torch.int64, device=DEV) * 31)
+    for step in range(6):
+        steps = torch.full((B,), step, dtype=torch.int32, device=DEV)
+        tok, _ = ops.sample(logits, args[0], args[1], args[2], args[3], steps)
+        tok = tok.cpu()
+        assert int(tok.min()) >= 0 and int(tok.max()) < V
+        for r in range(B):
+            assert bool(allowed[r][tok[r]]), (r, step, temp[r], tk[r], tpp[r], int(tok[r]))
+
+
 @pytest.mark.parametrize("T,d", [(1, 1024), (37, 1024), (256, 4096), (5, 8)])
 def test_embedding_prep_matches_reference(T, d):
     """Decode prologue in one launch: embedding rows, rows * ln, row sums of squares, and the
