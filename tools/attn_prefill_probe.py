@@ -2,7 +2,7 @@
 chunks: us per call (captured graph), causal TFLOP/s, for the 128-row (4 waves) and 256-row
 (8 waves) tiles.
 
-    python tools/attn_prefill_probe.py
+    python tools/attn_prefill_probe.py [--only qwen3-0.6b:32x512] [--rows 256]
 """
 from __future__ import annotations
 
@@ -19,11 +19,18 @@ from aws_k8s_ansible_provisioner_amd.ops import gemm_tuner as gt  # noqa: E402
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None, help="one shape, e.g. qwen3-0.6b:32x512")
+    ap.add_argument("--rows", type=int, default=None, help="one tile size (128 or 256)")
+    a = ap.parse_args()
     ops.load_native(required=True)
     dev = "cuda"
     D, BS = 128, 32
     for name, hq, hkv, nseq, L in (("qwen3-0.6b", 16, 8, 32, 512), ("qwen3-0.6b", 16, 8, 4, 4096),
                                    ("llama-3-8b", 32, 8, 32, 512), ("llama-3-8b", 32, 8, 4, 4096)):
+        if a.only and a.only != f"{name}:{nseq}x{L}":
+            continue
         G = hq // hkv
         per = (L + BS - 1) // BS
         NB = nseq * per + 4
@@ -37,7 +44,7 @@ def main():
         out = torch.empty_like(q)
         flop = nseq * hq * (L * (L + 1) / 2) * D * 2 * 2
         res = []
-        for rows in (128, 256):
+        for rows in ((a.rows,) if a.rows else (128, 256)):
             ts, tr = [], []
             for s in range(nseq):
                 for r in range(0, L * G, rows):
