@@ -605,15 +605,6 @@ __device__ __forceinline__ float xor32_sum(float x) {
 // gives lane half h the rows 8 i + 4 h + (0..3); with this order its P^T fragment for k-slice
 // s2 (accumulator registers 8 s2 .. 8 s2 + 7) is keys 16 s2 + 8 h + 0..7 -- one whole 8-token V
 // group, so every V^T fragment is a single 16-B LDS read of the cache's group image.
-// LDS hand-off: this wave's ds_reads retired, the workgroup barrier, and no LDS read hoisted
-// above it
-__device__ __forceinline__ void pg_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 __device__ __forceinline__ int fa_row_key(int r) {
   return 16 * (r >> 4) + 8 * ((r >> 2) & 1) + 4 * ((r >> 3) & 1) + (r & 3);
 }
@@ -635,24 +626,16 @@ __device__ __forceinline__ void fa_glds16(const void* g, void* lds_wave_base) {
 // the per-lane DMA source address (the LDS destination of a DMA is lane-linear).
 // NW = waves per workgroup (4: 128 q rows, two workgroups per CU; 8: 256 q rows, one
 // workgroup per CU -- every staged K/V tile feeds twice the rows).
-// PIPE (8-wave bf16 form): software-pipelined tile loop -- step t issues the S^T MFMAs of tile
-// t+1 and then runs tile t's softmax and P.V, so the softmax VALU of one tile has the next
-// tile's independent MFMAs beside it in the same wave (without it both waves of a SIMD reach
-// the softmax together and the matrix pipe idles: 18 % MFMA-busy, 36 % issue stall,
-// profiles/r5_prefill_attn_pmc.md).  Step t reads K of tile t+1 and V of tile t, so three K/V
-// buffers rotate (tile t+2 is staged into the one step t-1 finished with).
-template <bool F8, bool GL, int NW = 4, bool PIPE = false>
+template <bool F8, bool GL, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(AttnParams p) {
   constexpr int ROWS = 32 * NW;
   constexpr int NT = 64 * NW;    // threads
   constexpr int PW = 16 / NW;    // 1-KiB K (and V) DMA pieces per wave per tile
   static_assert(NW == 4 || (NW == 8 && GL), "the register-staged path assumes 256 threads");
-  static_assert(!PIPE || (NW == 8 && GL), "the pipelined loop is the 8-wave LDS-DMA form");
-  constexpr int NBUF = PIPE ? 3 : 2;
-  // [buf][K | V][64 keys * 128 dims] bf16 = 32 KiB per buffer + the block ids of the first
+  // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
   // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
-  __shared__ __attribute__((aligned(16))) bf16 lds[NBUF * 2 * kFaKeys * kD + 2 * kFaBtCache];
-  int* bt_s = reinterpret_cast<int*>(lds + NBUF * 2 * kFaKeys * kD);
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 2 * kFaKeys * kD + 2 * kFaBtCache];
+  int* bt_s = reinterpret_cast<int*>(lds + 2 * 2 * kFaKeys * kD);
   // causal work grows with a tile's position: dispatch the map back to front so the
   // longest tiles start first and the grid's tail is made of short ones
   const int tile = gridDim.x - 1 - blockIdx.x;
@@ -786,122 +769,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
   float m_run = -1e30f, l_run = 0.f;
 
   int blk_next = 0;
-  if constexpr (PIPE) {
-    constexpr int BUFE = 2 * kFaKeys * kD;  // elements per K/V buffer
-    // S^T of one tile into s (two 32-key sub-tiles; K fragments loaded per sub-tile)
-    auto qk_tile = [&](f32x16 (&sv)[2], const bf16* kl) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        bf16x8 kf[8];
-        const int key = 32 * k + fa_row_key(r);
-#pragma unroll
-        for (int s8 = 0; s8 < 8; ++s8)
-          kf[s8] = *reinterpret_cast<const bf16x8*>(kl + key * kD + (((2 * s8 + h) ^ (key & 15)) * 8));
-        f32x16 a;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) a[j] = 0.f;
-#pragma unroll
-        for (int s8 = 0; s8 < 8; ++s8) a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s8], qf[s8], a, 0, 0, 0);
-        sv[k] = a;
-      }
-    };
-    // online softmax of one tile's S^T, head: causal mask where the tile crosses the diagonal,
-    // the running max, the O^T rescale (branches: kept ahead of the straight-line tail, so the
-    // next tile's S^T MFMAs and this tile's exponentials share one basic block)
-    auto softmax_head = [&](f32x16 (&sv)[2], int key0, float& alpha) {
-      const bool need_mask = key0 + kFaKeys - 1 > w_min_limit;
-      float mx = -INFINITY;
-      if (need_mask) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int kk = key0 + 32 * k + 16 * (j >> 3) + 8 * h + (j & 7);
-            if (kk > limit) sv[k][j] = -INFINITY;
-            mx = fmaxf(mx, sv[k][j]);
-          }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sv[k][j]);
-      }
-      mx = xor32_max(mx);
-      const float m_new = fmaxf(m_run, mx * p.scale_log2);
-      alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      if (__any(m_new != m_run)) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
-      }
-      m_run = m_new;
-    };
-    // tail: exponentials, row sums, O^T += V^T . P^T (V fragments per sub-tile)
-    auto softmax_tail_pv = [&](f32x16 (&sv)[2], const bf16* vl, float alpha) {
-      float rsp[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(sv[k][j], p.scale_log2, -m_run));
-          sv[k][j] = e;
-          rsp[j & 3] += e;
-        }
-      const float rs = xor32_sum((rsp[0] + rsp[1]) + (rsp[2] + rsp[3]));
-      l_run = l_run * alpha + rs;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        bf16x8 vf[2][4];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt)
-            vf[s2][dt] = *reinterpret_cast<const bf16x8*>(
-                vl + ((4 * k + 2 * s2 + h) * kD + 32 * dt + r) * 8);
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 pb;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pb[j] = f2bf(sv[k][8 * s2 + j]);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt)
-            oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s2][dt], pb, oacc[dt], 0, 0, 0);
-        }
-      }
-    };
-    stage_glds(0, 0, blk_of(0));
-    if (ntiles > 1) stage_glds(1, 1, blk_of(1));
-    blk_next = blk_of(2);
-    if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pg_lds_sync();
-    f32x16 sa[2], sb[2];
-    if (wave_active) qk_tile(sa, lds);  // tile 0 (key 0 <= w_limit for every active wave)
-    auto step = [&](f32x16 (&sc)[2], f32x16 (&sn)[2], int t) {
-      // tile t+1 landed (the only DMA of this wave still in flight) and every wave finished
-      // step t-1, the last reader of buffer (t-1) % 3 -> stage tile t+2 into it
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      pg_lds_sync();
-      if (t + 2 < ntiles) {
-        stage_glds(t + 2, (t + 2) % 3, blk_next);
-        blk_next = blk_of(t + 3);
-      }
-      const int key0 = t * kFaKeys;
-      if (wave_active && key0 <= w_limit) {
-        float alpha;
-        softmax_head(sc, key0, alpha);
-        // unconditional (past the last tile it reads a stale buffer and the result is unused):
-        // no branch between these MFMAs and the exponentials below
-        qk_tile(sn, lds + ((t + 1) % 3) * BUFE);
-        softmax_tail_pv(sc, lds + (t % 3) * BUFE + kFaKeys * kD, alpha);
-      }
-    };
-    for (int t = 0; t < ntiles; t += 2) {
-      step(sa, sb, t);
-      if (t + 1 < ntiles) step(sb, sa, t + 1);
-    }
-  } else if constexpr (GL) {
+  if constexpr (GL) {
     stage_glds(0, 0, blk_of(0));
     blk_next = blk_of(1);
   } else {
@@ -912,7 +780,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     stage_store(0);
     __syncthreads();
   }
-  for (int t = 0; t < (PIPE ? 0 : ntiles); ++t) {
+  for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     const bool more = t + 1 < ntiles;
     if constexpr (GL) {
@@ -1095,14 +963,8 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows
                                hipStream_t s) {
   if (num_tiles == 0) return;
   const dim3 grid(num_tiles, p.Hkv);
-  static const bool pipe = [] {
-    const char* e = getenv("AKAP_ATTN_PIPE");
-    return e && atoi(e) == 1;
-  }();
-  if (tile_rows == 2 * kFaRows && !p.kv_fp8) {  // 256 rows, 8 waves (bf16 caches)
-    if (pipe) paged_attn_prefill_fa_kernel<false, true, 8, true><<<grid, 512, 0, s>>>(p);
-    else paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(p);
-  }
+  if (tile_rows == 2 * kFaRows && !p.kv_fp8)  // 256 rows, 8 waves (bf16 caches)
+    paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(p);
   else if (p.kv_fp8)  // fp8 caches: register-staged (widened to bf16 on the way into LDS)
     paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
   else  // bf16 caches: LDS-DMA staging
