@@ -660,11 +660,63 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
 
   // Q^T fragments (B operand): lane (r, h) holds Q[row][16 s + 8 h + j]
   bf16x8 qf[8];
-  const bf16* qrow = p.q + ((size_t)(q0 + (valid ? pos : 0)) * p.Hq + kvh * G + hig) * kD;
+  if (p.qkv != nullptr) {
+    // fused q prep (the standalone qk_norm_rope_cache pass then skips these tokens' q heads):
+    // the raw q row straight from the QKV projection, per-head RMSNorm over the lane pair
+    // (r, r + 32) that holds its 128 dims (one v_permlane32_swap), bf16-rounded like the
+    // standalone kernel, then NeoX rotary -- dims d < 64 (s8 < 4) pair with d + 64 (s8 + 4)
+    // in the same lane, so the rotation is lane-local.  Same arithmetic as rope_cache.hip
+    // qk_tok.
+    const int tok = q0 + (valid ? pos : 0);
+    const bf16* src = p.qkv + (size_t)tok * p.qkv_stride + (size_t)(kvh * G + hig) * kD + 8 * h;
+    bf16x8 raw[8];
 #pragma unroll
-  for (int s8 = 0; s8 < 8; ++s8)
-    qf[s8] = valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * s8 + 8 * h)
-                   : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s8 = 0; s8 < 8; ++s8) raw[s8] = *reinterpret_cast<const bf16x8*>(src + 16 * s8);
+    const float* cs = p.cos_sin + (size_t)p.positions[tok] * kD + 8 * h;
+    float x[8][8];
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[s8][j] = bf2f(raw[s8][j]);
+    if (p.q_w != nullptr) {
+      float ss = 0.f;
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += x[s8][j] * x[s8][j];
+      const float inv = rsqrtf(xor32_sum(ss) / (float)kD + p.eps);
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8) {
+        const bf16x8 w8 = *reinterpret_cast<const bf16x8*>(p.q_w + 16 * s8 + 8 * h);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[s8][j] = bf2f(f2bf(x[s8][j] * inv * bf2f(w8[j])));
+      }
+    }
+#pragma unroll
+    for (int s8 = 0; s8 < 4; ++s8) {
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + 16 * s8);
+      const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + 16 * s8 + 4);
+      const f32x4 n0 = *reinterpret_cast<const f32x4*>(cs + 64 + 16 * s8);
+      const f32x4 n1 = *reinterpret_cast<const f32x4*>(cs + 64 + 16 * s8 + 4);
+      bf16x8 lo, hi;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = j < 4 ? c0[j] : c1[j - 4], sn = j < 4 ? n0[j] : n1[j - 4];
+        const float x1 = x[s8][j], x2 = x[s8 + 4][j];
+        lo[j] = f2bf(x1 * c + -1.f * x2 * sn);
+        hi[j] = f2bf(x2 * c + 1.f * x1 * sn);
+      }
+      const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qf[s8] = valid ? lo : z;
+      qf[s8 + 4] = valid ? hi : z;
+    }
+  } else {
+    const bf16* qrow = p.q + ((size_t)(q0 + (valid ? pos : 0)) * p.Hq + kvh * G + hig) * kD;
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8)
+      qf[s8] = valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * s8 + 8 * h)
+                     : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
 
   const int wg_last_pos = min(q_len - 1, (row0 + ROWS - 1) / G);
   const int wg_limit = ctx0 + wg_last_pos;

@@ -31,7 +31,7 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
                                hipStream_t s, int kv_fp8 = 0, int v_per_token = 0,
                                void* v_tail = nullptr, const int* tail_slot = nullptr,
-                               int num_decode = 0);
+                               int num_decode = 0, int q_rows = -1);
 void launch_reshape_and_cache(const void* k, const void* v, void* k_cache, void* v_cache,
                               const int64_t* slots, int T, int Hkv, int D, int BS, hipStream_t s,
                               int kv_fp8 = 0);

@@ -51,7 +51,8 @@ __device__ __forceinline__ void qk_tok(const bf16* __restrict__ qkv, int qkv_str
                                        const int64_t* __restrict__ slots,
                                        const float* __restrict__ cos_sin,
                                        const bf16* __restrict__ q_w, const bf16* __restrict__ k_w,
-                                       int T, int Hq, int Hkv, int BS, float eps, int apply_rope) {
+                                       int T, int Hq, int Hkv, int BS, float eps, int apply_rope,
+                                       int q_rows) {
   constexpr int D = 128, HALF = 64, HB = 8;
   const int t = blockIdx.x * 16 + (threadIdx.x >> 4);
   const int li = threadIdx.x & 15;
@@ -72,7 +73,10 @@ __device__ __forceinline__ void qk_tok(const bf16* __restrict__ qkv, int qkv_str
   const bf16x8 kw8 = k_w ? *reinterpret_cast<const bf16x8*>(k_w + 8 * li) : zero8;
   const float sg = li < 8 ? -1.f : 1.f;  // first half: x1 c - x2 s; second: x2 c + x1 s
   const bf16* row = qkv + (size_t)t * qkv_stride + 8 * li;
-  for (int h0 = 0; h0 < H; h0 += HB) {
+  // tokens at or past q_rows (>= 0) take only their k heads: their q rows are normed and
+  // rotated by the prefill attention kernel itself, straight from the QKV rows
+  const int hstart = (q_rows < 0 || t < q_rows) ? 0 : Hq;
+  for (int h0 = hstart; h0 < H; h0 += HB) {
     bf16x8 raw[HB];
 #pragma unroll
     for (int j = 0; j < HB; ++j) raw[j] = *reinterpret_cast<const bf16x8*>(row + min(h0 + j, H - 1) * D);
@@ -273,10 +277,10 @@ __global__ __launch_bounds__(256) void qk_norm_rope_cache_kernel(
     const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
     const bf16* __restrict__ q_w, const bf16* __restrict__ k_w, int T, int Hq, int Hkv, int BS,
     float eps, int apply_rope, int qk_blocks, int v_per_token, bf16* __restrict__ v_tail,
-    const int* __restrict__ tail_slot, int num_decode) {
+    const int* __restrict__ tail_slot, int num_decode, int q_rows) {
   if ((int)blockIdx.x < qk_blocks)
     qk_tok<F8>(qkv, qkv_stride, q_out, k_cache, positions, slots, cos_sin, q_w, k_w, T, Hq, Hkv,
-               BS, eps, apply_rope);
+               BS, eps, apply_rope, q_rows);
   else if (v_per_token)
     v_item<F8>(qkv, qkv_stride, v_cache, slots, T, Hq, Hkv, BS, blockIdx.x - qk_blocks);
   else
@@ -289,7 +293,7 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
                                const float* cos_sin, const void* q_w, const void* k_w, int T,
                                int Hq, int Hkv, int D, int BS, float eps, int apply_rope,
                                hipStream_t s, int kv_fp8, int v_per_token, void* v_tail,
-                               const int* tail_slot, int num_decode) {
+                               const int* tail_slot, int num_decode, int q_rows) {
   if (T == 0 || D != 128) return;
   if (v_per_token || kv_fp8) v_tail = nullptr;  // the tail is a bf16, span-role feature
   const int qk_blocks = (T + 15) / 16;  // 16 tokens per workgroup (qk_tok)
@@ -300,7 +304,7 @@ void launch_qk_norm_rope_cache(const void* qkv, int qkv_stride, void* q_out, voi
   qk_norm_rope_cache_kernel<F8><<<grid, 256, 0, s>>>(                                           \
       (const bf16*)qkv, qkv_stride, (bf16*)q_out, k_cache, v_cache, positions, slots, cos_sin, \
       (const bf16*)q_w, (const bf16*)k_w, T, Hq, Hkv, BS, eps, apply_rope, qk_blocks, v_per_token, \
-      (bf16*)v_tail, tail_slot, num_decode)
+      (bf16*)v_tail, tail_slot, num_decode, q_rows)
   if (kv_fp8) QKR(true); else QKR(false);
 #undef QKR
 }

@@ -61,8 +61,9 @@ void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache
                         std::optional<Tensor> q_w, std::optional<Tensor> k_w, int64_t Hq,
                         int64_t Hkv, double eps, bool apply_rope, bool decode,
                         std::optional<Tensor> v_tail, std::optional<Tensor> tail_slot,
-                        int64_t num_decode) {
+                        int64_t num_decode, int64_t q_rows) {
   CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv); CHECK_CONTIG(q_out);
+  TORCH_CHECK(q_rows >= -1 && q_rows <= qkv.size(0), "q_rows out of range");
   CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
   TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong,
               "positions/slots must be int64");
@@ -95,7 +96,7 @@ void qk_norm_rope_cache(Tensor qkv, Tensor q_out, Tensor k_cache, Tensor v_cache
       q_w ? q_w->data_ptr() : nullptr, k_w ? k_w->data_ptr() : nullptr, T, Hq, Hkv, D, BS,
       (float)eps, apply_rope ? 1 : 0, cur_stream(), kv_fp8_of(k_cache, v_cache), decode ? 1 : 0,
       v_tail ? v_tail->data_ptr() : nullptr, v_tail ? tail_slot->data_ptr<int>() : nullptr,
-      (int)num_decode);
+      (int)num_decode, (int)q_rows);
 }
 
 void reshape_and_cache(Tensor k, Tensor v, Tensor k_cache, Tensor v_cache, Tensor slots) {
@@ -184,6 +185,53 @@ void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cach
   p.tile_seq = tile_seq.data_ptr<int>();
   p.tile_row = tile_row.data_ptr<int>();
   const c10::DeviceGuard g(q.device());
+  akap::launch_paged_attn_prefill(p, tile_seq.numel(), (int)tile_rows, cur_stream());
+}
+
+// Prefill attention that reads its q rows raw from the QKV projection and applies the per-head
+// q RMSNorm (q_w, optional) and NeoX RoPE itself (attention.hip, prefill kernel prologue): the
+// standalone qk_norm_rope_cache pass then writes q only for the decode rows of a mixed step
+// (q_rows = num_decode), saving the q write and re-read of every prefill token.
+void paged_attention_prefill_qprep(Tensor out, Tensor qkv, Tensor k_cache, Tensor v_cache,
+                                   Tensor block_tables, Tensor seq_lens, Tensor q_start,
+                                   Tensor tile_seq, Tensor tile_row, Tensor positions,
+                                   Tensor cos_sin, std::optional<Tensor> q_w, int64_t G,
+                                   double scale, double eps, int64_t tile_rows) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_LAST_CONTIG(qkv);
+  TORCH_CHECK(positions.scalar_type() == at::kLong && positions.numel() >= qkv.size(0),
+              "positions: int64, one per token");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+                  cos_sin.size(-1) == 128,
+              "cos_sin: contiguous fp32 [max_pos, 128]");
+  TORCH_CHECK(qkv.size(0) == out.size(0), "qkv / out token counts differ");
+  TORCH_CHECK(qkv.size(1) >= (out.size(1) + 2 * k_cache.size(1)) * 128, "qkv too narrow");
+  TORCH_CHECK(qkv.stride(0) % 8 == 0 && (uintptr_t)qkv.data_ptr() % 16 == 0,
+              "qkv rows must be 16-byte aligned");
+  if (q_w) {
+    CHECK_BF16(*q_w);
+    TORCH_CHECK(q_w->is_contiguous() && q_w->numel() == 128, "q_w: contiguous bf16 [128]");
+  }
+  // `out` doubles as the q-shaped tensor for the shared parameter checks (same [T, Hq, D])
+  auto p = attn_params(out, out, k_cache, v_cache, block_tables, seq_lens, G, scale);
+  TORCH_CHECK(tile_rows == 128 || tile_rows == 256, "tile_rows must be 128 or 256");
+  TORCH_CHECK(tile_rows != 256 || k_cache.scalar_type() == at::kBFloat16,
+              "tile_rows=256 needs a bf16 KV cache");
+  TORCH_CHECK(block_tables.size(1) * k_cache.size(2) <= 32768,
+              "prefill attention supports contexts up to 32768 tokens");
+  TORCH_CHECK(q_start.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
+                  tile_row.scalar_type() == at::kInt,
+              "q_start/tile maps must be int32");
+  p.q = nullptr;
+  p.qkv = (const __bf16*)qkv.data_ptr();
+  p.qkv_stride = qkv.stride(0);
+  p.positions = positions.data_ptr<int64_t>();
+  p.cos_sin = cos_sin.data_ptr<float>();
+  p.q_w = q_w ? (const __bf16*)q_w->data_ptr() : nullptr;
+  p.eps = (float)eps;
+  p.q_start = q_start.data_ptr<int>();
+  p.tile_seq = tile_seq.data_ptr<int>();
+  p.tile_row = tile_row.data_ptr<int>();
+  const c10::DeviceGuard g(qkv.device());
   akap::launch_paged_attn_prefill(p, tile_seq.numel(), (int)tile_rows, cur_stream());
 }
 
@@ -1164,13 +1212,18 @@ TORCH_LIBRARY(akap, m) {
       "qk_norm_rope_cache(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, "
       "Tensor positions, Tensor slots, Tensor cos_sin, Tensor? q_w, Tensor? k_w, int Hq, int Hkv, "
       "float eps, bool apply_rope, bool decode=False, Tensor(d!)? v_tail=None, "
-      "Tensor? tail_slot=None, int num_decode=0) -> ()");
+      "Tensor? tail_slot=None, int num_decode=0, int q_rows=-1) -> ()");
   m.def("reshape_and_cache(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def(
       "paged_attention_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_lens, Tensor q_start, Tensor tile_seq, Tensor tile_row, "
       "int G, float scale, int tile_rows=128) -> ()");
+  m.def(
+      "paged_attention_prefill_qprep(Tensor(a!) out, Tensor qkv, Tensor k_cache, Tensor v_cache, "
+      "Tensor block_tables, Tensor seq_lens, Tensor q_start, Tensor tile_seq, Tensor tile_row, "
+      "Tensor positions, Tensor cos_sin, Tensor? q_w, int G, float scale, float eps, "
+      "int tile_rows=128) -> ()");
   m.def(
       "paged_attention_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_lens, Tensor? q_start, Tensor(b!) part_m, Tensor(c!) part_l, "
@@ -1270,6 +1323,7 @@ TORCH_LIBRARY_IMPL(akap, CUDA, m) {
   m.impl("reshape_and_cache", &reshape_and_cache);
   m.impl("silu_and_mul", &silu_and_mul);
   m.impl("paged_attention_prefill", &paged_attention_prefill);
+  m.impl("paged_attention_prefill_qprep", &paged_attention_prefill_qprep);
   m.impl("paged_attention_decode", &paged_attention_decode);
   m.impl("paged_attention_decode_fused", &paged_attention_decode_fused);
   m.impl("sample", &sample);

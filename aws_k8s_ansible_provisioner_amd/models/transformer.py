@@ -30,6 +30,9 @@ from .moe import MoEBlock
 FUSED_DECODE = os.environ.get("AKAP_FUSED_DECODE", "1") != "0"
 PREFETCH_WEIGHTS = os.environ.get("AKAP_PREFETCH_WEIGHTS", "0") == "1"
 FUSED_GEMM = os.environ.get("AKAP_FUSED_GEMM", "1") != "0"
+# prefill attention applies the q norm + RoPE itself from the QKV rows (AKAP_PREFILL_QPREP=0:
+# the standalone pass writes every q row, the kernel reads q)
+PREFILL_QPREP = os.environ.get("AKAP_PREFILL_QPREP", "1") != "0"
 
 
 @dataclasses.dataclass
@@ -311,7 +314,7 @@ class DecoderLM:
         x = ops.embedding(ids, self.embed, vocab_start=self.vocab_start, vocab_end=self.vocab_end)
         return comm.tp_all_reduce(x)
 
-    def _attention(self, q, batch: AttnBatch, kc, vc, out, vt=None):
+    def _attention(self, q, batch: AttnBatch, kc, vc, out, vt=None, qprep=None):
         if batch.is_prefill:
             nd = batch.num_decode
             if nd and q.is_cuda:
@@ -327,7 +330,7 @@ class DecoderLM:
             ops.paged_attention_prefill(out, q, kc, vc, batch.block_tables, batch.seq_lens,
                                         batch.q_start, batch.tile_seq, batch.tile_row,
                                         self.hq // self.hkv, self.scale,
-                                        tile_rows=batch.tile_rows)
+                                        tile_rows=batch.tile_rows, qprep=qprep)
         else:
             ops.paged_attention_decode(out, q, kc, vc, batch.block_tables, batch.seq_lens,
                                        self.hq // self.hkv, self.scale, workspace=batch.workspace,
@@ -372,12 +375,18 @@ class DecoderLM:
                     tail_slot=batch.tail_slot)
             else:
                 q = torch.empty_like(attn)
+                # prefill on the GPU: the attention kernel norms + rotates its own q rows from
+                # the QKV projection, so the standalone pass writes q only for the decode rows
+                qp = batch.is_prefill and PREFILL_QPREP and qkv.is_cuda
                 ops.qk_norm_rope_cache(qkv, q, k_caches[li], v_caches[li], batch.positions,
                                        batch.slots, self.cos_sin, lw.q_norm, lw.k_norm, self.hq,
                                        self.hkv, eps, True, decode=not batch.is_prefill,
                                        v_tail=vt, tail_slot=batch.tail_slot,
-                                       num_decode=batch.num_decode if batch.is_prefill else 0)
-                self._attention(q, batch, k_caches[li], v_caches[li], attn, vt)
+                                       num_decode=batch.num_decode if batch.is_prefill else 0,
+                                       q_rows=batch.num_decode if qp else -1)
+                self._attention(q, batch, k_caches[li], v_caches[li], attn, vt,
+                                qprep=(qkv, batch.positions, self.cos_sin, lw.q_norm, eps)
+                                if qp else None)
             o = comm.tp_all_reduce(ops.linear(attn.view(T, self.hq * self.D), lw.w_o))
             h, residual = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             if lw.moe is not None:

@@ -106,18 +106,21 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
 # ----------------------------------------------------------------------------- rope/cache
 def qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
                        num_q_heads: int, num_kv_heads: int, eps: float, apply_rope: bool = True,
-                       decode: bool = False, v_tail=None, tail_slot=None, num_decode: int = 0):
+                       decode: bool = False, v_tail=None, tail_slot=None, num_decode: int = 0,
+                       q_rows: int = -1):
     """decode=True: one new token per sequence (V written per token instead of by the
     prefill role's 64-token span scan).  v_tail / tail_slot (GPU, bf16 cache, span role):
     tokens of a group still partial after this step also go to their sequence's V tail, and
     a decode row (t < num_decode) completing a group writes the whole group from the tail
     (csrc/kernels/rope_cache.hip); the CPU reference ignores the tail (its cache is always
-    complete)."""
+    complete).  q_rows >= 0 (GPU): q is written only for tokens < q_rows -- the prefill
+    attention applies the q norm + RoPE of the others itself (paged_attention_prefill qprep);
+    the CPU reference always writes every q row."""
     if _native(qkv):
         torch.ops.akap.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin,
                                           q_w, k_w, num_q_heads, num_kv_heads, eps, apply_rope,
                                           decode, v_tail, tail_slot if v_tail is not None else None,
-                                          num_decode)
+                                          num_decode, q_rows)
         return q_out
     ref.qk_norm_rope_cache(qkv, q_out, k_cache, v_cache, positions, slots, cos_sin, q_w, k_w,
                            num_q_heads, num_kv_heads, eps, apply_rope)
@@ -145,9 +148,20 @@ def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
 
 # ----------------------------------------------------------------------------- attention
 def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_start, tile_seq,
-                            tile_row, gqa_group: int, scale: float, tile_rows: int = 128):
+                            tile_row, gqa_group: int, scale: float, tile_rows: int = 128,
+                            qprep=None):
     """tile_rows = flattened q rows per tile of the host tile map: 128 selects the flash-style
-    LDS-tiled kernel (32x32x16 MFMA, 4 waves), 256 its 8-wave form (bf16 KV cache)."""
+    LDS-tiled kernel (32x32x16 MFMA, 4 waves), 256 its 8-wave form (bf16 KV cache).
+    qprep = (qkv, positions, cos_sin, q_w, eps) (GPU): the kernel reads the raw q rows from
+    the QKV projection and applies the q RMSNorm + RoPE itself (q is then only read by the
+    CPU reference, whose q is always fully written)."""
+    if _native(q) and qprep is not None:
+        qkv, positions, cos_sin, q_w, eps = qprep
+        torch.ops.akap.paged_attention_prefill_qprep(out, qkv, k_cache, v_cache, block_tables,
+                                                     seq_lens, q_start, tile_seq, tile_row,
+                                                     positions, cos_sin, q_w, gqa_group, scale,
+                                                     eps, tile_rows)
+        return out
     if _native(q):
         torch.ops.akap.paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens,
                                                q_start, tile_seq, tile_row, gqa_group, scale,

@@ -141,6 +141,45 @@ def test_paged_attention_prefill(bs, hq, hkv, tile_rows):
     _close(out, exp, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8)])
+@pytest.mark.parametrize("qk_norm", [True, False])
+@pytest.mark.parametrize("tile_rows", [128, 256])
+def test_paged_attention_prefill_qprep(hq, hkv, qk_norm, tile_rows):
+    """Prefill attention that norms + rotates its own q rows from the raw QKV projection
+    (the serving prefill path) against the two-pass path: qk_norm_rope_cache writing every q
+    row, then the kernel reading q.  Also: q_rows limits the standalone pass's q writes to the
+    leading (decode) rows and leaves the others untouched."""
+    seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (520, 7), (700, 650)]
+    _, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=hq + tile_rows)
+    G, D = hq // hkv, 128
+    T = int(qs[-1])
+    g = torch.Generator().manual_seed(7 + hq)
+    qkv = (torch.randn(T, (hq + 2 * hkv) * D, generator=g) * 2.0).bfloat16().to(DEV)
+    pos = torch.cat([torch.arange(kv - ql, kv) for kv, ql in seqs]).to(torch.int64).to(DEV)
+    slots = torch.full((T,), -1, dtype=torch.int64, device=DEV)  # caches stay as built
+    cs = ref.rope_cos_sin(1024, D, 1e6, device=DEV)
+    qw = (torch.randn(D, generator=g) * 0.3 + 1.0).bfloat16().to(DEV) if qk_norm else None
+    kw = (torch.randn(D, generator=g) * 0.3 + 1.0).bfloat16().to(DEV) if qk_norm else None
+    kcd, vcd = kc.to(DEV), vc.to(DEV)
+    q = torch.empty(T, hq, D, dtype=torch.bfloat16, device=DEV)
+    ops.qk_norm_rope_cache(qkv, q, kcd, vcd, pos, slots, cs, qw, kw, hq, hkv, 1e-6, True)
+    ts, tr = _tiles(seqs, G, tile_rows)
+    args = (kcd, vcd, bt.to(DEV), sl.to(DEV), qs.to(DEV), ts.to(DEV), tr.to(DEV), G,
+            1 / math.sqrt(D))
+    exp = torch.empty_like(q)
+    ops.paged_attention_prefill(exp, q, *args, tile_rows=tile_rows)
+    out = torch.empty_like(q)
+    ops.paged_attention_prefill(out, torch.empty_like(q), *args, tile_rows=tile_rows,
+                                qprep=(qkv, pos, cs, qw, 1e-6))
+    _close(out, exp, atol=1e-2, rtol=1e-2)
+    # q_rows: only the first 5 tokens' q rows are written
+    q2 = torch.full_like(q, 3.0)
+    ops.qk_norm_rope_cache(qkv, q2, kcd, vcd, pos, slots, cs, qw, kw, hq, hkv, 1e-6, True,
+                           q_rows=5)
+    assert torch.equal(q2[:5], q[:5])
+    assert bool((q2[5:] == 3.0).all())
+
+
 @pytest.mark.parametrize("num_parts,part_size", [(1, 4096), (8, 256), (3, 512)])
 @pytest.mark.parametrize("hq,hkv", [(16, 8), (64, 8), (32, 8)])
 def test_paged_attention_decode(num_parts, part_size, hq, hkv):
