@@ -850,6 +850,34 @@ def test_paged_attention_prefill_fp8(tile_rows):
     _close(out, exp, atol=2e-2, rtol=2e-2)
 
 
+def test_paged_attention_prefill_qprep_fp8():
+    """The register-staged fp8-cache prefill kernel with its own q norm + RoPE against the same
+    kernel reading the q rows the standalone pass wrote."""
+    seqs = [(1, 1), (37, 37), (300, 300), (129, 64), (700, 650)]
+    hq, hkv, D = 16, 8, 128
+    _, kc, vc, bt, sl, qs = _setup_attn(seqs, hq, hkv, 32, seed=44)
+    kc8, vc8 = _to_fp8_cache(kc, vc)
+    kcd, vcd = kc8.to(DEV), vc8.to(DEV)
+    T = int(qs[-1])
+    g = torch.Generator().manual_seed(45)
+    qkv = (torch.randn(T, (hq + 2 * hkv) * D, generator=g) * 2.0).bfloat16().to(DEV)
+    pos = torch.cat([torch.arange(kv - ql, kv) for kv, ql in seqs]).to(torch.int64).to(DEV)
+    slots = torch.full((T,), -1, dtype=torch.int64, device=DEV)
+    cs = ref.rope_cos_sin(1024, D, 1e6, device=DEV)
+    qw = (torch.randn(D, generator=g) * 0.3 + 1.0).bfloat16().to(DEV)
+    q = torch.empty(T, hq, D, dtype=torch.bfloat16, device=DEV)
+    ops.qk_norm_rope_cache(qkv, q, kcd, vcd, pos, slots, cs, qw, qw, hq, hkv, 1e-6, True)
+    ts, tr = _tiles(seqs, hq // hkv, 128)
+    args = (kcd, vcd, bt.to(DEV), sl.to(DEV), qs.to(DEV), ts.to(DEV), tr.to(DEV), hq // hkv,
+            1 / math.sqrt(D))
+    exp = torch.empty_like(q)
+    ops.paged_attention_prefill(exp, q, *args, tile_rows=128)
+    out = torch.empty_like(q)
+    ops.paged_attention_prefill(out, torch.empty_like(q), *args, tile_rows=128,
+                                qprep=(qkv, pos, cs, qw, 1e-6))
+    _close(out, exp, atol=1e-2, rtol=1e-2)
+
+
 def _dgemm_ref(pro, x, w, r, ln, eps):
     """fp32 reference of the fused decode GEMM's prologue + GEMM (+ residual out)."""
     x, w = x.float().cpu(), w.float().cpu()

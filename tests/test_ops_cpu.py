@@ -192,8 +192,40 @@ def test_native_library_registers_all_ops():
     for name in ("rmsnorm", "fused_add_rmsnorm", "qk_norm_rope_cache", "paged_attention_prefill",
                  "paged_attention_decode", "paged_attention_decode_fused", "sample", "gemm",
                  "moe_gemm", "moe_combine", "car_all_reduce", "kv_gather", "embedding",
-                 "embedding_prep", "wgemm", "argmax", "car_all_to_all", "car_all_gather"):
+                 "embedding_prep", "wgemm", "argmax", "car_all_to_all", "car_all_gather",
+                 "paged_attention_prefill_qprep"):
         assert hasattr(torch.ops.akap, name), name
+
+
+def test_prefill_qprep_cpu_path_uses_the_written_q():
+    """On the CPU the qprep argument is ignored: qk_norm_rope_cache (reference) writes every q
+    row whatever q_rows says, and the reference attention reads q -- the same result as the
+    two-pass call."""
+    import math
+    torch.manual_seed(0)
+    hq, hkv, D, BS = 4, 2, 128, 32
+    T = 20
+    qkv = torch.randn(T, (hq + 2 * hkv) * D).bfloat16()
+    kc = torch.zeros(2, hkv, BS, D, dtype=torch.bfloat16)
+    vc = torch.zeros(2, hkv, BS // 8, D, 8, dtype=torch.bfloat16)
+    pos = torch.arange(T, dtype=torch.int64)
+    slots = torch.arange(T, dtype=torch.int64)
+    cs = ops.reference.rope_cos_sin(64, D, 1e6)
+    q = torch.empty(T, hq, D, dtype=torch.bfloat16)
+    ops.qk_norm_rope_cache(qkv, q, kc, vc, pos, slots, cs, None, None, hq, hkv, 1e-6, True,
+                           q_rows=3)
+    bt = torch.tensor([[0, 1]], dtype=torch.int32)
+    sl = torch.tensor([T], dtype=torch.int32)
+    qs = torch.tensor([0, T], dtype=torch.int32)
+    ts = torch.zeros(1, dtype=torch.int32)
+    tr = torch.zeros(1, dtype=torch.int32)
+    a = torch.empty_like(q)
+    b = torch.empty_like(q)
+    ops.paged_attention_prefill(a, q, kc, vc, bt, sl, qs, ts, tr, 2, 1 / math.sqrt(D))
+    ops.paged_attention_prefill(b, q, kc, vc, bt, sl, qs, ts, tr, 2, 1 / math.sqrt(D),
+                                qprep=(qkv, pos, cs, None, 1e-6))
+    assert torch.equal(a, b)
+    assert torch.isfinite(a.float()).all()
 
 
 def test_embedding_prep_reference_semantics():
