@@ -184,6 +184,8 @@ struct SampleParams {
 // grid (sample_chunks(B, V) chunks, B rows); ws >= B * kMaxChunks * 32 bytes of partials,
 // tickets[B] int32 zeroed once (each row's last chunk re-arms its ticket)
 int sample_chunks(int B, int V, int wgs = 512);
+// longest row the sampler covers: kMaxChunks chunks x kMaxTiles tiles x kTile elements
+constexpr long kSampleMaxVocab = 64L * 64 * 2048;
 long sample_ws_floats(int B);  // partial records + filter-pass states and histograms
 // filtered = 0: the caller guarantees no row has top-k / top-p (their passes are not launched)
 void launch_sample(const SampleParams& p, int B, void* ws, int* tickets, int filtered,

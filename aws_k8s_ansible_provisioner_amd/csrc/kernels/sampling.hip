@@ -89,6 +89,7 @@ constexpr int kHistRow = kMaxChunks * 512;
 // chunk rescans ONE tile for the token whatever the chunk size
 constexpr int kTile = kChunkThreads * 8;
 constexpr int kMaxTiles = 64;  // chunk <= 131072 elements
+static_assert((long)kMaxChunks * kMaxTiles * kTile == kSampleMaxVocab, "kernels.h bound");
 
 struct SampPart {  // one chunk's partial record (32 B = two 16-B vectors)
   float m, s;      // max of z over the chunk, sum of exp(z - m)

@@ -539,6 +539,12 @@ void sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tenso
   TORCH_CHECK(top_k.scalar_type() == at::kInt && steps.scalar_type() == at::kInt, "int32");
   TORCH_CHECK(seeds.scalar_type() == at::kLong && out_tokens.scalar_type() == at::kLong, "int64");
   const int B = logits.size(0);
+  TORCH_CHECK(logits.size(1) >= 1 && logits.size(1) <= akap::kSampleMaxVocab,
+              "sampler rows: 1 .. ", akap::kSampleMaxVocab, " logits");
+  TORCH_CHECK(temperature.numel() >= B && top_k.numel() >= B && top_p.numel() >= B &&
+                  seeds.numel() >= B && steps.numel() >= B && out_tokens.numel() >= B &&
+                  (out_logprobs.numel() == 0 || out_logprobs.numel() >= B),
+              "sampler: one parameter / output entry per row");
   akap::SampleParams p{};
   p.logits = logits.data_ptr();
   p.is_bf16 = logits.scalar_type() == at::kBFloat16;
