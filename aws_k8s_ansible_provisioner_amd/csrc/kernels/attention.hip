@@ -658,8 +658,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
   const int ctx0 = kv_len - q_len;  // keys before this chunk's first query token
   const int limit = valid ? ctx0 + pos : -1;
 
-  // Q^T fragments (B operand): lane (r, h) holds Q[row][16 s + 8 h + j]
+  // Q^T fragments (B operand): lane (r, h) holds Q[row][16 s + 8 h + j].  Loaded after the
+  // first K/V tile's DMA is issued, so the q round trips (and the fused q prep) overlap it.
   bf16x8 qf[8];
+  auto load_q = [&]() {
   if (p.qkv != nullptr) {
     // fused q prep (the standalone qk_norm_rope_cache pass then skips these tokens' q heads):
     // the raw q row straight from the QKV projection, per-head RMSNorm over the lane pair
@@ -672,7 +674,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     bf16x8 raw[8];
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) raw[s8] = *reinterpret_cast<const bf16x8*>(src + 16 * s8);
-    const float* cs = p.cos_sin + (size_t)p.positions[tok] * kD + 8 * h;
+    // rotary position = the token's key index ctx0 + pos -- the invariant the causal limit
+    // above already relies on (positions[tok] holds the same value): no dependent load
+    const float* cs = p.cos_sin + (size_t)(valid ? ctx0 + pos : 0) * kD + 8 * h;
     float x[8][8];
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8)
@@ -717,6 +721,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
       qf[s8] = valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * s8 + 8 * h)
                      : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
+  };
 
   const int wg_last_pos = min(q_len - 1, (row0 + ROWS - 1) / G);
   const int wg_limit = ctx0 + wg_last_pos;
@@ -824,7 +829,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
   if constexpr (GL) {
     stage_glds(0, 0, blk_of(0));
     blk_next = blk_of(1);
+    load_q();
   } else {
+    load_q();
     // register-staged form: per-piece block ids come from an LDS copy of the table
     for (int c = tid; c <= last_chunk; c += NT) bt_s[c] = bt[c * 32 / BS];
     __syncthreads();

@@ -16,6 +16,7 @@ import torch  # noqa: E402
 
 from aws_k8s_ansible_provisioner_amd import ops  # noqa: E402
 from aws_k8s_ansible_provisioner_amd.ops import gemm_tuner as gt  # noqa: E402
+from aws_k8s_ansible_provisioner_amd.ops import reference as ref  # noqa: E402
 
 
 def main():
@@ -23,6 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None, help="one shape, e.g. qwen3-0.6b:32x512")
     ap.add_argument("--rows", type=int, default=None, help="one tile size (128 or 256)")
+    ap.add_argument("--qprep", action="store_true",
+                    help="also time the kernel that norms + rotates its own q rows from QKV")
     a = ap.parse_args()
     ops.load_native(required=True)
     dev = "cuda"
@@ -42,6 +45,10 @@ def main():
         T = nseq * L
         q = (torch.randn(T, hq, D, device=dev) * 0.5).to(torch.bfloat16)
         out = torch.empty_like(q)
+        qkv = (torch.randn(T, (hq + 2 * hkv) * D, device=dev) * 0.5).to(torch.bfloat16)
+        pos = torch.cat([torch.arange(L) for _ in range(nseq)]).to(torch.int64).to(dev)
+        cs = ref.rope_cos_sin(L + 16, D, 1e6, device=dev)
+        qw = torch.ones(D, device=dev, dtype=torch.bfloat16)
         flop = nseq * hq * (L * (L + 1) / 2) * D * 2 * 2
         res = []
         for rows in ((a.rows,) if a.rows else (128, 256)):
@@ -55,6 +62,11 @@ def main():
             us = gt._timed(lambda i: ops.paged_attention_prefill(
                 out, q, kc, vc, bt, sl, qs, ts, tr, G, 1 / math.sqrt(D), tile_rows=rows), 4)
             res.append(f"{rows} rows {us:7.1f} us ({flop / us / 1e6:5.0f} TF)")
+            if a.qprep:
+                us = gt._timed(lambda i: ops.paged_attention_prefill(
+                    out, q, kc, vc, bt, sl, qs, ts, tr, G, 1 / math.sqrt(D), tile_rows=rows,
+                    qprep=(qkv, pos, cs, qw, 1e-6)), 4)
+                res.append(f"qprep {us:7.1f} us")
         print(f"{name} {nseq} x {L}: " + " | ".join(res), flush=True)
 
 
