@@ -671,42 +671,44 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     // qk_tok.
     const int tok = q0 + (valid ? pos : 0);
     const bf16* src = p.qkv + (size_t)tok * p.qkv_stride + (size_t)(kvh * G + hig) * kD + 8 * h;
-    bf16x8 raw[8];
-#pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8) raw[s8] = *reinterpret_cast<const bf16x8*>(src + 16 * s8);
     // rotary position = the token's key index ctx0 + pos -- the invariant the causal limit
     // above already relies on (positions[tok] holds the same value): no dependent load
     const float* cs = p.cos_sin + (size_t)(valid ? ctx0 + pos : 0) * kD + 8 * h;
-    float x[8][8];
+    // every operand load issued up front, unconditionally (one round trip; without a q norm
+    // the weight loads read valid rotary-table bytes and are ignored)
+    const bool qn = p.q_w != nullptr;
+    const bf16* wsrc = qn ? p.q_w : reinterpret_cast<const bf16*>(p.cos_sin);
+    bf16x8 raw[8], w8[8];
+    f32x4 cv[4][2], sv[4][2];
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) raw[s8] = *reinterpret_cast<const bf16x8*>(src + 16 * s8);
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) w8[s8] = *reinterpret_cast<const bf16x8*>(wsrc + 16 * s8 + 8 * h);
+#pragma unroll
+    for (int s8 = 0; s8 < 4; ++s8)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        cv[s8][k] = *reinterpret_cast<const f32x4*>(cs + 16 * s8 + 4 * k);
+        sv[s8][k] = *reinterpret_cast<const f32x4*>(cs + 64 + 16 * s8 + 4 * k);
+      }
+    float ss = 0.f;
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[s8][j] = bf2f(raw[s8][j]);
-    if (p.q_w != nullptr) {
-      float ss = 0.f;
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ss += x[s8][j] * x[s8][j];
-      const float inv = rsqrtf(xor32_sum(ss) / (float)kD + p.eps);
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8) {
-        const bf16x8 w8 = *reinterpret_cast<const bf16x8*>(p.q_w + 16 * s8 + 8 * h);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[s8][j] = bf2f(f2bf(x[s8][j] * inv * bf2f(w8[j])));
-      }
-    }
+      for (int j = 0; j < 8; ++j) ss += bf2f(raw[s8][j]) * bf2f(raw[s8][j]);
+    const float inv = rsqrtf(xor32_sum(ss) / (float)kD + p.eps);
+    // normed value of dim (s8, j), bf16-rounded like the standalone kernel (raw without a norm)
+    auto xn = [&](int s8, int j) {
+      const float v = bf2f(raw[s8][j]);
+      return qn ? bf2f(f2bf(v * inv * bf2f(w8[s8][j]))) : v;
+    };
 #pragma unroll
     for (int s8 = 0; s8 < 4; ++s8) {
-      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + 16 * s8);
-      const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + 16 * s8 + 4);
-      const f32x4 n0 = *reinterpret_cast<const f32x4*>(cs + 64 + 16 * s8);
-      const f32x4 n1 = *reinterpret_cast<const f32x4*>(cs + 64 + 16 * s8 + 4);
       bf16x8 lo, hi;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float c = j < 4 ? c0[j] : c1[j - 4], sn = j < 4 ? n0[j] : n1[j - 4];
-        const float x1 = x[s8][j], x2 = x[s8 + 4][j];
+        const float c = cv[s8][j >> 2][j & 3], sn = sv[s8][j >> 2][j & 3];
+        const float x1 = xn(s8, j), x2 = xn(s8 + 4, j);
         lo[j] = f2bf(x1 * c + -1.f * x2 * sn);
         hi[j] = f2bf(x2 * c + 1.f * x1 * sn);
       }
@@ -818,13 +820,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     for (int i = 0; i < PW; ++i) fa_glds16(vb + voff[i], vl + (w * PW + i) * 512);
   };
 
-  f32x16 oacc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
-  float m_run = -1e30f, l_run = 0.f;
-
   int blk_next = 0;
   if constexpr (GL) {
     stage_glds(0, 0, blk_of(0));
@@ -839,6 +834,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
     stage_store(0);
     __syncthreads();
   }
+  // accumulators zeroed after the prologue (not live across the q loads / q prep)
+  f32x16 oacc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     const bool more = t + 1 < ntiles;
