@@ -59,21 +59,9 @@ __device__ __forceinline__ void qk_tok(const bf16* __restrict__ qkv, int qkv_str
   // every lane of a 16-lane row shares the token, so rows exit together (DPP stays valid)
   if (t >= T) return;
   const int H = Hq + Hkv;
-  // the position first (positions always holds T entries, host-checked): its wait then leaves
-  // the head-row loads below in flight (in-order vmcnt)
-  const int64_t pos_t = positions[t];
-  const bf16* row = qkv + (size_t)t * qkv_stride + 8 * li;
-  // tokens at or past q_rows (>= 0) take only their k heads: their q rows are normed and
-  // rotated by the prefill attention kernel itself, straight from the QKV rows
-  const int hstart = (q_rows < 0 || t < q_rows) ? 0 : Hq;
-  // the first batch of head rows is requested before the position -> rotary-row chain, so the
-  // two round trips overlap (a prefill token past q_rows has only this one batch: its k heads)
-  bf16x8 raw[HB];
-#pragma unroll
-  for (int j = 0; j < HB; ++j) raw[j] = *reinterpret_cast<const bf16x8*>(row + min(hstart + j, H - 1) * D);
   f32x4 c0 = {1.f, 1.f, 1.f, 1.f}, c1 = c0, s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
   if (apply_rope) {
-    const float* cs = cos_sin + (size_t)pos_t * D + 8 * (li & 7);
+    const float* cs = cos_sin + (size_t)positions[t] * D + 8 * (li & 7);
     c0 = *reinterpret_cast<const f32x4*>(cs);
     c1 = *reinterpret_cast<const f32x4*>(cs + 4);
     s0 = *reinterpret_cast<const f32x4*>(cs + HALF);
@@ -84,11 +72,14 @@ __device__ __forceinline__ void qk_tok(const bf16* __restrict__ qkv, int qkv_str
   const bf16x8 qw8 = q_w ? *reinterpret_cast<const bf16x8*>(q_w + 8 * li) : zero8;
   const bf16x8 kw8 = k_w ? *reinterpret_cast<const bf16x8*>(k_w + 8 * li) : zero8;
   const float sg = li < 8 ? -1.f : 1.f;  // first half: x1 c - x2 s; second: x2 c + x1 s
+  const bf16* row = qkv + (size_t)t * qkv_stride + 8 * li;
+  // tokens at or past q_rows (>= 0) take only their k heads: their q rows are normed and
+  // rotated by the prefill attention kernel itself, straight from the QKV rows
+  const int hstart = (q_rows < 0 || t < q_rows) ? 0 : Hq;
   for (int h0 = hstart; h0 < H; h0 += HB) {
-    if (h0 != hstart) {
+    bf16x8 raw[HB];
 #pragma unroll
-      for (int j = 0; j < HB; ++j) raw[j] = *reinterpret_cast<const bf16x8*>(row + min(h0 + j, H - 1) * D);
-    }
+    for (int j = 0; j < HB; ++j) raw[j] = *reinterpret_cast<const bf16x8*>(row + min(h0 + j, H - 1) * D);
 #pragma unroll
     for (int j = 0; j < HB; ++j) {
       const int h = h0 + j;
