@@ -192,6 +192,9 @@ void paged_attention_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cach
 // q RMSNorm (q_w, optional) and NeoX RoPE itself (attention.hip, prefill kernel prologue): the
 // standalone qk_norm_rope_cache pass then writes q only for the decode rows of a mixed step
 // (q_rows = num_decode), saving the q write and re-read of every prefill token.
+// The rotary row of a q token is its key index kv_len - q_len + i: the same invariant the
+// kernel's causal mask relies on, and what the engine's positions hold for every prefill
+// token.  `positions` is shape-checked and passed through but not read by the kernel.
 void paged_attention_prefill_qprep(Tensor out, Tensor qkv, Tensor k_cache, Tensor v_cache,
                                    Tensor block_tables, Tensor seq_lens, Tensor q_start,
                                    Tensor tile_seq, Tensor tile_row, Tensor positions,

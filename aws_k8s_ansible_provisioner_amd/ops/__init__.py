@@ -154,7 +154,9 @@ def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_
     LDS-tiled kernel (32x32x16 MFMA, 4 waves), 256 its 8-wave form (bf16 KV cache).
     qprep = (qkv, positions, cos_sin, q_w, eps) (GPU): the kernel reads the raw q rows from
     the QKV projection and applies the q RMSNorm + RoPE itself (q is then only read by the
-    CPU reference, whose q is always fully written)."""
+    CPU reference, whose q is always fully written).  The kernel rotates token i of a chunk
+    by its key index seq_len - q_len + i -- the invariant its causal mask already assumes and
+    what `positions` holds for prefill tokens."""
     if _native(q) and qprep is not None:
         qkv, positions, cos_sin, q_w, eps = qprep
         torch.ops.akap.paged_attention_prefill_qprep(out, qkv, k_cache, v_cache, block_tables,
