@@ -232,9 +232,11 @@ void launch_moe_combine(const void* Y, const float* wts, const int32_t* inv, voi
 // ---- kv_transfer.hip ----
 // The paged cache is `planes` planes (layer x {K,V}) of [NB, block_elems] bf16.
 void launch_kv_gather(const void* cache, long plane_stride, int planes, int block_elems,
-                      const int* block_ids, int nblk, void* out, hipStream_t s);
+                      int cache_blocks, const int* block_ids, int nblk, void* out,
+                      hipStream_t s);
 void launch_kv_scatter(const void* in, void* cache, long plane_stride, int planes,
-                       int block_elems, const int* block_ids, int nblk, hipStream_t s);
+                       int block_elems, int cache_blocks, const int* block_ids, int nblk,
+                       hipStream_t s);
 // hipIpc pull: peer cache blocks -> own blocks, + V-tail fill of each request's partial
 // last V group (see kv_transfer.hip)
 struct KVPullArgs {

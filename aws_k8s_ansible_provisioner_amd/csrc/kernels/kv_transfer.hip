@@ -23,10 +23,14 @@ template <bool GATHER>
 __global__ __launch_bounds__(256) void kv_copy_kernel(bf16* __restrict__ cache, long plane_stride,
                                                       int block_elems,
                                                       const int* __restrict__ block_ids,
-                                                      int nblk, bf16* __restrict__ buf) {
+                                                      int nblk, int cache_blocks,
+                                                      bf16* __restrict__ buf) {
   const int plane = blockIdx.y;
   const int b = blockIdx.x;
   const long src_blk = block_ids[b];
+  // the ids are range-checked on the host (KVTransferAgent._ids); this guard keeps a bad id
+  // from touching memory past the cache even if a caller skips that check
+  if (src_blk < 0 || src_blk >= cache_blocks) return;
   bf16* c = cache + plane * plane_stride + src_blk * block_elems;
   bf16* f = buf + ((long)plane * nblk + b) * block_elems;
   for (int i = threadIdx.x * 8; i < block_elems; i += 256 * 8) {
@@ -38,18 +42,21 @@ __global__ __launch_bounds__(256) void kv_copy_kernel(bf16* __restrict__ cache, 
 }
 
 void launch_kv_gather(const void* cache, long plane_stride, int planes, int block_elems,
-                      const int* block_ids, int nblk, void* out, hipStream_t s) {
+                      int cache_blocks, const int* block_ids, int nblk, void* out,
+                      hipStream_t s) {
   if (nblk == 0) return;
   kv_copy_kernel<true><<<dim3(nblk, planes), 256, 0, s>>>((bf16*)cache, plane_stride, block_elems,
-                                                         block_ids, nblk, (bf16*)out);
+                                                         block_ids, nblk, cache_blocks,
+                                                         (bf16*)out);
 }
 
 void launch_kv_scatter(const void* in, void* cache, long plane_stride, int planes,
-                       int block_elems, const int* block_ids, int nblk, hipStream_t s) {
+                       int block_elems, int cache_blocks, const int* block_ids, int nblk,
+                       hipStream_t s) {
   if (nblk == 0) return;
   kv_copy_kernel<false><<<dim3(nblk, planes), 256, 0, s>>>((bf16*)cache, plane_stride,
                                                           block_elems, block_ids, nblk,
-                                                          (bf16*)in);
+                                                          cache_blocks, (bf16*)in);
 }
 
 constexpr int kPullCoh = 17;  // buffer op cache bits: sc0 | sc1 (system-coherent)

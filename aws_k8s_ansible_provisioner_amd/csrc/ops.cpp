@@ -747,7 +747,8 @@ void kv_gather(Tensor cache, Tensor block_ids, Tensor out) {
   TORCH_CHECK(block_elems % 2048 == 0 || block_elems % 8 == 0, "block must be 16B multiple");
   TORCH_CHECK(out.numel() >= (int64_t)planes * block_ids.numel() * block_elems, "out too small");
   const c10::DeviceGuard g(cache.device());
-  akap::launch_kv_gather(cache.data_ptr(), plane_stride, planes, block_elems,
+  TORCH_CHECK(block_ids.is_cuda() && block_ids.scalar_type() == at::kInt, "int32 GPU block ids");
+  akap::launch_kv_gather(cache.data_ptr(), plane_stride, planes, block_elems, cache.size(1),
                          block_ids.data_ptr<int>(), block_ids.numel(), out.data_ptr(),
                          cur_stream());
 }
@@ -756,9 +757,12 @@ void kv_scatter(Tensor buf, Tensor cache, Tensor block_ids) {
   CHECK_GPU(cache); CHECK_CONTIG(cache); CHECK_CONTIG(buf);
   const int planes = cache.size(0);
   const c10::DeviceGuard g(cache.device());
+  TORCH_CHECK(block_ids.is_cuda() && block_ids.scalar_type() == at::kInt, "int32 GPU block ids");
+  TORCH_CHECK(buf.numel() >= (int64_t)planes * block_ids.numel() * cache.stride(1),
+              "buf too small");
   akap::launch_kv_scatter(buf.data_ptr(), cache.data_ptr(), cache.stride(0), planes,
-                          cache.stride(1), block_ids.data_ptr<int>(), block_ids.numel(),
-                          cur_stream());
+                          cache.stride(1), cache.size(1), block_ids.data_ptr<int>(),
+                          block_ids.numel(), cur_stream());
 }
 
 // hipIpc KV pull (see kv_transfer.hip).  src_planes / dst_planes: int64 device tables of
@@ -1097,6 +1101,16 @@ int64_t car_error(int64_t h) {
   return (int64_t)v;
 }
 
+// The communicator's device error word as a 1-element int32 tensor (no copy): a replayed
+// decode graph enqueues an async copy of it to pinned host memory after its last collective,
+// and the host checks it before the step's tokens are emitted (ModelRunner._err_probe).
+Tensor car_error_word(int64_t h) {
+  CarComm* c = car_get(h);
+  return at::from_blob(c->args.err, {1},
+                       at::TensorOptions().dtype(at::kInt).device(
+                           c10::Device(c10::DeviceType::CUDA, c->device)));
+}
+
 // Rank-major all-gather of the vocab-parallel logits shard inp [R, n] -> out [R, W*n].
 void car_all_gather(int64_t h, Tensor inp, Tensor out) {
   CarComm* c = car_get(h);
@@ -1272,6 +1286,7 @@ TORCH_LIBRARY(akap, m) {
   m.def("car_open(int h, Tensor handles) -> ()");
   m.def("car_all_reduce(int h, Tensor inp, Tensor(a!) out, bool two_shot) -> ()");
   m.def("car_error(int h) -> int");
+  m.def("car_error_word(int h) -> Tensor");
   m.def("car_link_local(int h, int[] peers) -> ()");
   m.def("car_all_reduce_multi(int[] hs, Tensor[] ins, Tensor(a!)[] outs, bool two_shot, "
         "Tensor(b!)[]? epi=None, bool warm=False) -> ()");
@@ -1318,6 +1333,7 @@ TORCH_LIBRARY_IMPL(akap, CompositeExplicitAutograd, m) {
   m.impl("car_ipc_handles", &car_ipc_handles);
   m.impl("car_open", &car_open);
   m.impl("car_error", &car_error);
+  m.impl("car_error_word", &car_error_word);
   m.impl("car_link_local", &car_link_local);
   m.impl("car_destroy", &car_destroy);
   m.impl("ipc_open", &ipc_open);

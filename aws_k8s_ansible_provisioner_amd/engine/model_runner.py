@@ -249,6 +249,12 @@ class ModelRunner:
         self.out_tokens = torch.zeros(S, dtype=torch.int64, device=self.device)
         # sampled tokens of launched decode steps land here (one region per staging slot)
         self.tok_host = [self._pinned(S, torch.int64) for _ in range(2)]
+        # error-word probes: slots 0/1 follow tok_host (lookahead), 2 the synchronous path,
+        # 3..6 a TP follower's un-waited replays (_err_probe)
+        self._err_host = [self._pinned(1, torch.int32) for _ in range(7)]
+        self._pending_err = None
+        self._follower_err: list = []
+        self._follower_slot = 0
         self.out_logprobs = torch.zeros(S, dtype=torch.float32, device=self.device)
         self.workspace = ops.decode_workspace(S, self.model.hkv, self.G, self.num_parts,
                                               self.device)
@@ -322,7 +328,7 @@ class ModelRunner:
         being captured; multi-rank engines always run "filtered" (correct for every batch)."""
         if self._capture_mode is not None:
             return self._capture_mode
-        if not self.is_gpu or self.ps.world_size > 1:
+        if not self.is_gpu or self._peer_step:
             return "filtered"
         npd, V = self.np, self.mcfg.vocab_size
         t, k, p = npd["temperature"][:n], npd["top_k"][:n], npd["top_p"][:n]
@@ -336,7 +342,7 @@ class ModelRunner:
         """The decode graph of bucket n for a batch of B rows in its sampler mode (all modes
         were captured with the buckets; see capture_graphs)."""
         g = self.graphs.get(n)
-        if g is None or self.ps.world_size > 1:
+        if g is None or self._peer_step:
             return g
         mode = self._sample_mode(B)
         return g if mode == "plain" else self.graphs_v[(mode, n)]
@@ -479,6 +485,43 @@ class ModelRunner:
             moe_mod.ep_overflow_reduce(self.device)
 
     @property
+    def _peer_step(self) -> bool:
+        """Every step issues collectives with peer ranks (TP, or expert-parallel MoE over the
+        job): all ranks must replay the same graph variant.  DP replicas and P/D roles share a
+        torch.distributed world but run their steps alone (world_size > 1, tp_size == 1)."""
+        return self.ps.tp_size > 1 or self._ep_moe
+
+    def _err_probe(self, slot: int):
+        """Enqueue an async copy of the custom IPC collectives' error word to pinned host
+        memory behind this step's kernels (None when the step runs no IPC collective).  A
+        replayed graph cannot raise: a peer that never arrived only sets that word, and the
+        step's sums are then stale -- the host checks it before the tokens are used."""
+        car = self.ps.car
+        if car is None or not self.is_gpu or not self._peer_step:
+            return None
+        h = self._err_host[slot]
+        h.copy_(car.err_word, non_blocking=True)
+        return h
+
+    @staticmethod
+    def _check_err(h) -> None:
+        if h is not None and int(h[0]) != 0:
+            from ..parallel.comm import CollectiveTimeout
+
+            raise CollectiveTimeout(
+                "custom IPC collective timed out in a decode step (a peer rank stalled): the "
+                "step's tokens are discarded and the engine is marked unhealthy")
+
+    def _check_follower_err(self) -> None:
+        """TP followers do not wait for their steps: check the newest probe whose copy has
+        completed (a lag of a step or two), so a follower that summed stale staging stops
+        before its corrupted KV writes feed later steps."""
+        pend = self._follower_err
+        while pend and pend[0][0].query():
+            ev, h = pend.pop(0)
+            self._check_err(h)
+
+    @property
     def _ep_moe(self) -> bool:
         """Expert-parallel MoE layers over more than one rank (fixed-capacity dispatch)."""
         return self.ps.world_size > 1 and any(
@@ -532,6 +575,7 @@ class ModelRunner:
             from ..parallel import comm
 
             comm.check_deferred()
+        self._pending_err = self._err_probe(2)
         return self.out_tokens[:B]
 
     def _ep_rerun_if_overflowed(self, n: int, extras: Optional[dict]) -> None:
@@ -570,12 +614,13 @@ class ModelRunner:
             else:
                 self._decode_body(n)
         if not self.is_gpu:
-            return None, self.out_tokens[:B].clone()
+            return None, self.out_tokens[:B].clone(), self._err_probe(slot)
         host = self.tok_host[slot][:B]
         host.copy_(self.out_tokens[:B], non_blocking=True)
+        err = self._err_probe(slot)
         ev = torch.cuda.Event()
         ev.record()
-        return ev, host
+        return ev, host, err
 
     def replay_decode(self, info: dict) -> None:
         """TP follower ranks: the decode step's graph replay alone -- inputs arrive by the
@@ -592,6 +637,14 @@ class ModelRunner:
             graph.replay()
         else:
             self._decode_body(n)
+        if self.is_gpu and self.ps.car is not None:
+            self._check_follower_err()
+            slot = self._follower_slot = (self._follower_slot + 1) % 4
+            h = self._err_probe(3 + slot)
+            if h is not None:
+                ev = torch.cuda.Event()
+                ev.record()
+                self._follower_err.append((ev, h))
 
     def _bucket(self, B: int) -> int:
         for b in self.buckets:
@@ -608,11 +661,12 @@ class ModelRunner:
         self._decode_body(n)
         self._ep_rerun_if_overflowed(n, None)
 
-    @staticmethod
-    def wait_decode(handle) -> np.ndarray:
-        ev, host = handle
+    @classmethod
+    def wait_decode(cls, handle) -> np.ndarray:
+        ev, host, err = handle
         if ev is not None:
             ev.synchronize()
+        cls._check_err(err)  # never hand out tokens of a step whose collectives timed out
         return host.numpy()
 
     def execute(self, info: dict) -> np.ndarray:
@@ -622,10 +676,15 @@ class ModelRunner:
         else:
             with profiling.phase("akap.decode"):
                 toks = self.execute_decode(info)
+        if info["is_prefill"]:
+            self._pending_err = self._err_probe(2)
         extras = info.get("extras")
         if extras and extras.get("logprobs"):
             self.last_logprobs = self.out_logprobs[:toks.shape[0]].to("cpu").numpy()
-        return toks.to("cpu").numpy()
+        out = toks.to("cpu").numpy()  # blocking: the probe copy queued before it is done
+        err, self._pending_err = self._pending_err, None
+        self._check_err(err)
+        return out
 
     # ------------------------------------------------------------------ graphs
     def _graph_has_collectives(self) -> bool:
@@ -689,19 +748,21 @@ class ModelRunner:
             self.log(f"[runner] GEMM tuning {time.time() - t1:.1f}s")
         self._stage_decode(self.max_seqs)
         torch.cuda.synchronize()
-        if self.ps.world_size > 1:
+        if self._peer_step:
             # the warm-up steps below run the custom IPC collectives, whose flag waits are
             # bounded (~2 s): a rank still tuning its prefill GEMMs (rank-local, tens of seconds
-            # at 70B widths) would time them out on its peers -- meet first
+            # at 70B widths) would time them out on its peers -- meet first.  Only the ranks
+            # that share the step's collectives meet (the TP group; the whole job for
+            # expert-parallel MoE): DP replicas and P/D roles capture on their own
             import torch.distributed as dist
 
-            dist.barrier()
+            dist.barrier(group=None if self._ep_moe else self.ps.tp_group)
         self.graph_pool = torch.cuda.graph_pool_handle()
         stream = torch.cuda.Stream()
         # one graph per bucket and sampler mode (single-rank engines: "plain", "greedy" and
         # "filtered", all captured here -- a capture while serving would race the P/D KV
         # receiver's work; multi-rank engines: "filtered" only, correct for every batch)
-        modes = ["filtered"] if self.ps.world_size > 1 else ["plain", "greedy", "filtered"]
+        modes = ["filtered"] if self._peer_step else ["plain", "greedy", "filtered"]
         for mode in modes:
             self._capture_mode = mode
             for b in reversed(self.buckets):

@@ -51,6 +51,13 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
 _UNCHECKED = [False]  # a piecewise / chunked IPC collective ran since the last check
 
 
+class CollectiveTimeout(RuntimeError):
+    """A custom IPC collective gave up waiting for a peer (its bounded flag wait expired):
+    the step summed stale staging, so its outputs must not be used.  The kernels' error word
+    is sticky, so every later step fails too: the engine reports unhealthy and is restarted
+    (device-side epochs cannot be realigned across ranks without one)."""
+
+
 def check_deferred() -> None:
     """End of an eager step: raise if one of its piecewise IPC collectives timed out (the
     kernels only set an error word; silently summing on would corrupt the step)."""
@@ -59,7 +66,7 @@ def check_deferred() -> None:
     _UNCHECKED[0] = False
     st = get_state()
     if st is not None and st.car is not None and st.car.error():
-        raise RuntimeError("custom IPC collective timed out in a piecewise prefill step")
+        raise CollectiveTimeout("custom IPC collective timed out in a piecewise prefill step")
 
 
 def _car_pieces_ok(x: torch.Tensor, car) -> bool:

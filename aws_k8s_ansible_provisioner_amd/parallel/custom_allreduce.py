@@ -77,6 +77,9 @@ class CustomAllReduce:
         handles = torch.stack([torch.frombuffer(bytearray(b), dtype=torch.uint8).view(2, -1)
                                for b in allh])
         torch.ops.akap.car_open(self.h, handles)
+        # the kernels' sticky timeout word (device int32): replayed decode steps copy it to
+        # pinned host memory and the runner checks it before emitting tokens
+        self.err_word = torch.ops.akap.car_error_word(self.h)
         dist.barrier(group=group)
 
     def should_use(self, x: torch.Tensor) -> bool:

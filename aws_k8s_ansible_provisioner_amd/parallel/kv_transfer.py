@@ -166,6 +166,16 @@ class KVTransferAgent:
         self.ipc_open_timeout_s = IPC_OPEN_TIMEOUT_S
         self.pull_seconds = 0.0
 
+    def _ids(self, block_ids) -> torch.Tensor:
+        """Block ids as a device tensor, range-checked on the host first: the gather / scatter
+        kernels index the cache with them unchecked, so an id outside [0, nblocks) (e.g. from
+        a malformed control message) would read or write past the cache."""
+        ids = [int(b) for b in block_ids]
+        bad = [b for b in ids if not 0 <= b < self.nblocks]
+        if bad:
+            raise IndexError(f"KV block ids {bad[:8]} outside the cache's {self.nblocks} blocks")
+        return torch.tensor(ids, dtype=torch.int32, device=self.device)
+
     def nbytes(self, nblk: int) -> int:
         return self.num_planes * nblk * self.block_elems * self.kv.element_size()
 
@@ -245,7 +255,7 @@ class KVTransferAgent:
             try:
                 self._check()
                 with self._ctx():
-                    ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
+                    ids = self._ids(block_ids)
                     buf = self._gather(ids)
                     if self.host_staging or not self.is_gpu:
                         if self.is_gpu:
@@ -273,7 +283,7 @@ class KVTransferAgent:
         """Pack blocks NOW on the caller's (compute) stream: later kernels of that stream --
         which may reuse the blocks -- are ordered after the copy, so the caller may free the
         blocks as soon as this returns.  Returns (packed buffer, ready event) for send_packed."""
-        ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
+        ids = self._ids(block_ids)
         buf = self._gather(ids)
         ev = None
         if self.is_gpu:
@@ -335,7 +345,7 @@ class KVTransferAgent:
                     else:
                         _wait(self._irecv(buf, src), t_out,
                               f"KV recv of {n} blocks from rank {src}", self.gloo)
-                    ids = torch.tensor(block_ids, dtype=torch.int32, device=self.device)
+                    ids = self._ids(block_ids)
                     self._scatter(buf, ids)
                     if self.is_gpu:
                         self.stream.synchronize()

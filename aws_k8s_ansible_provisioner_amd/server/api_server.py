@@ -116,6 +116,9 @@ class OpenAIServer:
         self.created = int(time.time())
         self._dropped_push = False  # fault injection (AKAP_FAULT_KV_PUSH=drop_once)
         self._ipc_meta = None  # hipIpc export of this engine's KV cache (made on first lease)
+        # transfer id -> blocks handed out by /kv/lease (owned by the lease until /kv/done or
+        # a /kv/push fallback): the server's own record, never the client's block list
+        self._leases: dict[int, list[int]] = {}
         self.app = self._build()
 
     # ------------------------------------------------------------------ helpers
@@ -251,10 +254,26 @@ class OpenAIServer:
             tids = [int(t) for t in (body.get("transfer_ids") or [body["transfer_id"]])]
             if body.get("leased_blocks") is not None:
                 # the decode side leased these transfers for a hipIpc pull and could not map
-                # this cache in time: the lease already owns the blocks (until finish_transfer)
-                per = [[int(b) for b in bl] for bl in body["leased_blocks"]]
-                if len(per) != len(tids):
+                # this cache in time: the lease already owns the blocks (until finish_transfer).
+                # The blocks come from this server's lease record; the client's list must
+                # match it exactly (a stale or forged list would ship other requests' KV or
+                # index past the cache)
+                claimed = body["leased_blocks"]
+                if not isinstance(claimed, list) or len(claimed) != len(tids):
                     return _err(400, "leased_blocks: one block list per transfer id")
+                unknown = [t for t in tids if t not in self._leases]
+                if unknown:
+                    return _err(404, f"no lease for transfer(s) {unknown}")
+                try:
+                    claimed = [[int(b) for b in bl] for bl in claimed]
+                except (TypeError, ValueError):
+                    return _err(400, "leased_blocks: integer block ids")
+                per = [self._leases[t] for t in tids]
+                if claimed != per:
+                    return _err(409, "leased_blocks do not match this server's leases",
+                                "Conflict")
+                for t in tids:
+                    self._leases.pop(t, None)
             else:
                 per = [eng.held_blocks(t) for t in tids]
                 missing = [t for t, b in zip(tids, per) if not b]
@@ -324,6 +343,8 @@ class OpenAIServer:
                 return _err(404, f"held KV for transfer(s) {tids} expired")
             if self._ipc_meta is None:
                 self._ipc_meta = ag.ipc_meta()
+            for t, bl in zip(tids, per):
+                self._leases[t] = [int(b) for b in bl]
             return {"ok": True, "blocks": [[int(b) for b in bl] for bl in per],
                     "ipc": self._ipc_meta}
 
@@ -333,6 +354,7 @@ class OpenAIServer:
             leased transfers: free their blocks."""
             body = await req.json()
             for t in body["transfer_ids"]:
+                self._leases.pop(int(t), None)
                 eng.finish_transfer(int(t))
             return {"ok": True}
 
@@ -360,6 +382,7 @@ class OpenAIServer:
             body = await req.json()
             tids = [int(t) for t in (body.get("transfer_ids") or [body["transfer_id"]])]
             for t in tids:
+                self._leases.pop(t, None)
                 eng.free_held(t)
             return {"ok": True, "released": len(tids)}
 

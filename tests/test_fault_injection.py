@@ -136,3 +136,102 @@ def test_gateway_survives_replica_loss_mid_run():
     finally:
         for t in servers:
             t.server.should_exit = True
+
+
+class _FakeIpcAgent:
+    """P/D prefill-side agent stand-in: records what /kv/push would send."""
+    is_gpu = True
+    broken = None
+
+    def __init__(self):
+        self.sent = []
+
+    def ipc_meta(self):
+        return {"handles": []}
+
+    def send_blocks(self, blocks, dst, on_done=None):
+        self.sent.append((list(blocks), dst))
+        if on_done:
+            on_done()
+
+
+def test_kv_push_uses_server_lease_record_not_client_blocks():
+    """a /kv/push fallback after /kv/lease ships the blocks this server
+    leased, never a client-supplied list (forged ids would read past the cache or ship
+    other requests' KV)."""
+    app, ae = build_app(_cfg())
+    eng = ae.engine
+    held = {5: [1, 2], 6: [3]}
+    finished = []
+    eng.held_blocks = lambda t: list(held.get(t, []))
+    eng.take_held = lambda t: held.pop(t, [])
+    eng.finish_transfer = lambda t: finished.append(t)
+    ag = _FakeIpcAgent()
+    ae.kv_agent = ag
+    with TestClient(app) as c:
+        r = c.post("/kv/lease", json={"transfer_ids": [5]})
+        assert r.status_code == 200 and r.json()["blocks"] == [[1, 2]]
+        # forged list for a leased transfer: refused, nothing sent
+        r = c.post("/kv/push", json={"transfer_ids": [5], "leased_blocks": [[10 ** 9]],
+                                     "dst_rank": 1})
+        assert r.status_code == 409 and not ag.sent
+        # a transfer that was never leased: refused
+        r = c.post("/kv/push", json={"transfer_ids": [6], "leased_blocks": [[3]],
+                                     "dst_rank": 1})
+        assert r.status_code == 404 and not ag.sent
+        # the genuine fallback ships the recorded blocks once
+        r = c.post("/kv/push", json={"transfer_ids": [5], "leased_blocks": [[1, 2]],
+                                     "dst_rank": 1})
+        assert r.status_code == 200 and ag.sent == [([1, 2], 1)] and finished == [5]
+        r = c.post("/kv/push", json={"transfer_ids": [5], "leased_blocks": [[1, 2]],
+                                     "dst_rank": 1})
+        assert r.status_code == 404  # the lease was consumed
+
+
+def test_kv_agent_rejects_out_of_range_block_ids():
+    import torch
+
+    from aws_k8s_ansible_provisioner_amd.parallel.kv_transfer import KVTransferAgent
+
+    kv = torch.zeros(2, 2, 8, 64, dtype=torch.bfloat16)
+    ag = KVTransferAgent(kv)
+    assert ag._ids([0, 7]).tolist() == [0, 7]
+    for bad in ([8], [-1], [0, 100]):
+        with pytest.raises(IndexError):
+            ag._ids(bad)
+    with pytest.raises(IndexError):
+        ag.gather([9])
+
+
+def test_collective_timeout_word_fails_step_not_tokens():
+    """a custom IPC collective that timed out inside a replayed decode
+    step only sets the kernels' error word.  The runner copies it to the host behind the
+    step and checks it before any token is used: the request errors, /health goes 503, and
+    no token of that step reaches the client.  (CPU engine; the word is injected.)"""
+    import torch
+
+    from aws_k8s_ansible_provisioner_amd.engine.model_runner import ModelRunner
+    from aws_k8s_ansible_provisioner_amd.parallel.comm import CollectiveTimeout
+
+    with pytest.raises(CollectiveTimeout):
+        ModelRunner._check_err(torch.tensor([1], dtype=torch.int32))
+    ModelRunner._check_err(torch.tensor([0], dtype=torch.int32))
+    ModelRunner._check_err(None)
+    with pytest.raises(CollectiveTimeout):
+        ModelRunner.wait_decode((None, torch.tensor([5, 6]), torch.tensor([1], dtype=torch.int32)))
+
+    app, ae = build_app(_cfg())
+    runner = ae.engine.runner
+    steps = {"n": 0}
+
+    def probe(slot):
+        steps["n"] += 1
+        # the third step's collectives "time out" (sticky from then on, like the kernel word)
+        return torch.tensor([1 if steps["n"] >= 3 else 0], dtype=torch.int32)
+
+    runner._err_probe = probe
+    with TestClient(app) as c:
+        r = c.post("/v1/completions", json={"prompt": "hello", "max_tokens": 16,
+                                            "ignore_eos": True})
+        assert r.status_code == 500 and "timed out" in r.text
+        assert c.get("/health").status_code == 503
