@@ -1,10 +1,24 @@
-// Token sampling for gfx950: greedy, temperature, top-k, top-p in one launch.
+// Token sampling for gfx950: greedy, temperature, top-k, top-p over bf16 (or fp32) logits.
 //
-// No sort: top-k / top-p thresholds are found by a radix select on the order-preserving
-// uint32 image of the logits -- by COUNT for top-k and by probability MASS for top-p.  The
-// draw is a Gumbel-max over the surviving set with a counter-based RNG keyed by (request
-// seed, request step, token id), so a request's stream is reproducible regardless of batch
-// composition.  The row is split over several workgroups (sample_chunk_kernel below).
+// Launch structure (launch_sample): ONE sample_chunk_kernel launch, then -- only for batches
+// where some row uses top-k / top-p (filtered != 0) -- FOUR sample_pass_kernel launches
+// (passes 0..3: histogram passes, a third only when top-p crosses above top-k's bin, and the
+// draw); a pass launch whose rows were all resolved earlier returns at once.  Greedy-only batches run argmax_kernel
+// instead (one launch).
+//   * sample_chunk_kernel: every row is split over chunk workgroups; each publishes an sc1
+//     partial record (max, sum of exp, greedy winner, tile masses) and bumps the row's ticket
+//     (its own L2 line); the last chunk of a row combines them.  Temperature rows (no filter)
+//     are drawn here by INVERSE CDF in three levels -- chunk, then a 2048-element tile from the
+//     published tile masses, then one rescan of that tile -- with one exp per element and no
+//     per-element RNG.  The chunk kernel also histograms the 256 bf16 keys below each chunk's
+//     max: when a row's top-k / top-p threshold falls inside that window it is set exactly here
+//     and the row is marked resolved.
+//   * sample_pass_kernel: distributed 256-bin histogram passes over the order-preserving
+//     16-bit key of the remaining rows find the threshold (by COUNT for top-k, by probability
+//     MASS for top-p); the last pass draws a Gumbel-max over the surviving set with a
+//     counter-based RNG keyed by (request seed, request step, token id), so a request's stream
+//     is reproducible regardless of batch composition.
+// No sort anywhere.
 #include <cstdlib>
 
 #include "common.h"

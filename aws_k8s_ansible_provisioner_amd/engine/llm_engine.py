@@ -530,6 +530,13 @@ class LLMEngine:
             m.kv_resets.set_total(agent.resets, model_name=name)
             m.kv_xfer_bytes.set_total(agent.bytes_sent, model_name=name, direction="send")
             m.kv_xfer_bytes.set_total(agent.bytes_recv, model_name=name, direction="recv")
+            from ..parallel.kv_transfer import CHANNEL_PROBES
+
+            for peer, pr in list(CHANNEL_PROBES.items()):
+                m.kv_probe_gbps.set(round(pr["gbps"], 3), model_name=name, peer=peer,
+                                    transport=pr["transport"], role=pr["role"])
+            probe = getattr(self, "kv_ipc_state", None)  # set by the serving layer (decode)
+            m.kv_ipc.set(1.0 if probe is not None and probe() else 0.0, model_name=name)
 
     # ------------------------------------------------------------------ offline API
     def generate(self, prompts: Iterable, params: Optional[SamplingParams] = None,

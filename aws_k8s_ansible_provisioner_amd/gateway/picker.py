@@ -11,7 +11,8 @@ hashes (same chained-hash scheme as the engine's prefix cache, computed on the p
 text in fixed-size character blocks), so routing is cache-aware without asking pods.
 
 Disaggregated prefill/decode: with both roles present and a prompt of at least
-`pd_threshold` characters, `pick_pd` returns a (prefill, decode) pair.  A prefill and a decode
+`pd_threshold` characters, `pick_pd` returns a (prefill, decode) pair; pairs whose decode
+endpoint pulls KV by hipIpc (akap:kv_transport_ipc) get `w_ipc` on top of their score.  A prefill and a decode
 endpoint can only be paired inside one P/D transfer group (the torch.distributed / RCCL group
 their processes share -- in the `pd` preset, the two processes of one pod), so every endpoint
 carries a `group` and the pair is the best-scoring (prefill + decode) within a group.
@@ -41,6 +42,7 @@ class Endpoint:
     failures: int = 0
     served: int = 0
     kv_broken: bool = False  # P/D: its KV-transfer channel awaits a rebuild
+    kv_ipc: bool = False     # P/D decode: pulls KV by hipIpc (no peer fell back to p2p)
 
     def load_score(self) -> float:
         return 1.0 / (1.0 + self.waiting + 0.25 * self.running + self.inflight)
@@ -91,6 +93,7 @@ class PickerConfig:
     w_queue: float = 1.0
     w_kv: float = 1.0
     w_prefix: float = 2.0
+    w_ipc: float = 1.0  # P/D pairs whose decode side pulls KV by hipIpc (xGMI / same GPU)
     stale_after_s: float = 15.0
     pd_threshold_chars: int = 512
     block_chars: int = 64
@@ -123,12 +126,13 @@ class EndpointPicker:
         return list(self.eps.values())
 
     def update_metrics(self, url: str, running: float, waiting: float, kv: float,
-                       kv_broken: bool = False) -> None:
+                       kv_broken: bool = False, kv_ipc: bool = False) -> None:
         e = self.eps.get(url)
         if e is None:
             return
         e.running, e.waiting, e.kv_usage = running, waiting, kv
         e.kv_broken = kv_broken
+        e.kv_ipc = kv_ipc
         e.last_scrape = time.time()
         e.healthy = True
         e.failures = 0
@@ -192,6 +196,8 @@ class EndpointPicker:
                         if p.group != d.group or p.kv_broken or d.kv_broken:
                             continue  # other transfer group, or a channel being rebuilt
                         s = self.score(p, match, len(hs)) + self.score(d, {}, 0)
+                        if d.kv_ipc:  # the hipIpc pull beats any send/recv path
+                            s += self.cfg.w_ipc
                         if s > best_s + 1e-9 or (abs(s - best_s) <= 1e-9 and
                                                  self.rng.random() < 0.5):
                             best, best_s = (p, d), s

@@ -107,7 +107,8 @@ class Gateway:
                 self.picker.update_metrics(e.url, m.get("vllm:num_requests_running", 0.0),
                                            m.get("vllm:num_requests_waiting", 0.0),
                                            m.get("vllm:gpu_cache_usage_perc", 0.0),
-                                           kv_broken=m.get("akap:kv_channel_broken", 0.0) > 0)
+                                           kv_broken=m.get("akap:kv_channel_broken", 0.0) > 0,
+                                           kv_ipc=m.get("akap:kv_transport_ipc", 0.0) > 0)
             except (aiohttp.ClientError, asyncio.TimeoutError, OSError):
                 self.picker.mark_failure(e.url)
             self.m_up.set(1.0 if e.healthy else 0.0, endpoint=e.url, role=e.role)

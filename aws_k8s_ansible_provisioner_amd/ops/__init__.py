@@ -159,6 +159,8 @@ def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_
     what `positions` holds for prefill tokens."""
     if _native(q) and qprep is not None:
         qkv, positions, cos_sin, q_w, eps = qprep
+        if DEBUG_CHECKS:
+            check_qprep_positions(positions, seq_lens, q_start, cos_sin.shape[0])
         torch.ops.akap.paged_attention_prefill_qprep(out, qkv, k_cache, v_cache, block_tables,
                                                      seq_lens, q_start, tile_seq, tile_row,
                                                      positions, cos_sin, q_w, gqa_group, scale,
@@ -171,6 +173,32 @@ def paged_attention_prefill(out, q, k_cache, v_cache, block_tables, seq_lens, q_
         return out
     out.copy_(ref.paged_attention(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale))
     return out
+
+
+# AKAP_DEBUG_CHECKS=1: host-side invariant checks that cost a device sync (off in serving)
+DEBUG_CHECKS = os.environ.get("AKAP_DEBUG_CHECKS", "0") == "1"
+
+
+def check_qprep_positions(positions, seq_lens, q_start, table_rows: int) -> None:
+    """The q-prep prefill kernel rotates token i of a sequence's chunk by its KEY index
+    seq_len - q_len + i (it never reads `positions`): raise if any prefill token's position
+    differs from that index (e.g. a future M-RoPE or shifted-position model), or if the
+    rotary table has fewer rows than the largest key index."""
+    qs = q_start.to("cpu", torch.int64)
+    sl = seq_lens.to("cpu", torch.int64)
+    pos = positions.to("cpu", torch.int64)
+    for b in range(sl.numel()):
+        n = int(qs[b + 1] - qs[b])
+        if n <= 0:
+            continue
+        want = torch.arange(int(sl[b]) - n, int(sl[b]), dtype=torch.int64)
+        got = pos[int(qs[b]):int(qs[b + 1])]
+        if not torch.equal(got, want):
+            raise ValueError(f"prefill q-prep: sequence {b} positions {got[:4].tolist()}... "
+                             f"are not its key indices {want[:4].tolist()}...")
+        if int(sl[b]) > table_rows:
+            raise ValueError(f"prefill q-prep: key index {int(sl[b]) - 1} past the rotary "
+                             f"table's {table_rows} rows")
 
 
 # longest decode split-KV partition the kernel takes (csrc/kernels/kernels.h kDecodeMaxPart)
@@ -383,7 +411,11 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
     256-row batch per tile, every weight byte crosses L2 -> CU once.
     bn = 256 (bm = 256) selects the 256 x 256 pgemm body with the K range split over
     `splitk` workgroups per tile and the slices combined inside the launch by every slice
-    (csrc/kernels/pgemm.hip pgemm_sk_kernel; all epilogues, grid <= the CU count).
+    (csrc/kernels/pgemm.hip pgemm_sk_kernel; all epilogues, grid <= the CU count).  That
+    variant is PROBE-ONLY: when its all-slices spin times out (slices not co-resident) it only
+    sets counters[GEMM_CTR_ERR] -- read by gemm_ctr_error() in tests and probes, never by a
+    serving step -- so the tuner never emits it and gemm_tuner.load_cache refuses plans
+    naming it.
     km = 16 | 32 selects csrc/kernels/kgemm.hip instead: km x 32 output tiles with the K split
     over the workgroup's waves (plain prologue, store / residual epilogues, no split-K)."""
     M = x.shape[0]
@@ -498,6 +530,15 @@ def gemm_counters(device) -> torch.Tensor:
     if c is None:
         c = _COUNTERS[device] = torch.zeros(GEMM_CTR_INTS, dtype=torch.int32, device=device)
     return c
+
+
+def gemm_ctr_error(device, clear: bool = True) -> int:
+    """The in-launch combines' timeout flag (probe-only bn = 256 variant); host sync."""
+    c = gemm_counters(device)
+    v = int(c[GEMM_CTR_ERR].item())
+    if clear and v:
+        c[GEMM_CTR_ERR].zero_()
+    return v
 
 
 _EMPTY_F32: dict = {}

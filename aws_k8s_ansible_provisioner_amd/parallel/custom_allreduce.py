@@ -41,15 +41,33 @@ def _aligned(t: torch.Tensor) -> bool:
     return t.data_ptr() % 16 == 0
 
 
-def car_grid(world: int) -> int:
-    """Fixed grid of every launch on a communicator: 128 blocks with one rank per GPU; ranks
-    sharing one GPU (world > visible devices: the single-GPU rehearsal) split 128 between them,
-    so their spinning blocks leave CUs free for a late peer's GEMMs (AKAP_CAR_BLOCKS)."""
+def car_grid(world: int, sharing: int = 1) -> int:
+    """Fixed grid of every launch on a communicator: 128 blocks with one rank per GPU; when
+    `sharing` ranks run on one physical GPU (the single-GPU rehearsal) they split 128 between
+    them, so their spinning blocks leave CUs free for a late peer's GEMMs (AKAP_CAR_BLOCKS)."""
     env = os.environ.get("AKAP_CAR_BLOCKS")
     if env:
         return max(1, min(128, int(env)))
-    shared = world > max(1, torch.cuda.device_count())
-    return max(8, 128 // world) if shared else 128
+    return max(8, 128 // sharing) if sharing > 1 else 128
+
+
+def _device_key(device: torch.device) -> str:
+    """Physical identity of a GPU: host + PCI domain/bus/device (not the visible index, which
+    is 0 in every rank when each rank sees only its own GPU)."""
+    import socket
+
+    p = torch.cuda.get_device_properties(device)
+    return (f"{socket.gethostname()}:{getattr(p, 'pci_domain_id', 0)}:"
+            f"{getattr(p, 'pci_bus_id', 0)}:{getattr(p, 'pci_device_id', 0)}")
+
+
+def agree_grid(keys: list, grids: list) -> int:
+    """Every rank must launch the same fixed grid (the epoch argument in the kernel header):
+    the minimum of the ranks' own choices, each made from how many ranks share its physical
+    GPU (from the gathered device keys)."""
+    share = max(sum(1 for k in keys if k == key) for key in keys)
+    auto = max(8, 128 // share) if share > 1 else 128
+    return max(1, min(auto, min(grids)))
 
 
 class CustomAllReduce:
@@ -68,7 +86,15 @@ class CustomAllReduce:
         self.buffer_bytes = max(max_bytes, buffer_bytes)
         self.oneshot_bytes = oneshot_limit(self.world)
         max_elems = (self.buffer_bytes // 2 + 7) // 8 * 8
-        self.blocks = car_grid(self.world)
+        # one grid for the whole communicator: gathered device identities decide sharing, and
+        # the ranks take the minimum (a rank with a different env or visibility cannot leave
+        # the others waiting on flags its smaller grid never sets)
+        info: list = [None] * self.world
+        env = os.environ.get("AKAP_CAR_BLOCKS")
+        dist.all_gather_object(info, (_device_key(self.device),
+                                      max(1, min(128, int(env))) if env else 128),
+                               group=group)
+        self.blocks = agree_grid([k for k, _ in info], [g for _, g in info])
         self.h = torch.ops.akap.car_create(self.device.index, self.rank, self.world, max_elems,
                                            self.blocks)
         mine = torch.ops.akap.car_ipc_handles(self.h)

@@ -176,6 +176,36 @@ class KVTransferAgent:
             raise IndexError(f"KV block ids {bad[:8]} outside the cache's {self.nblocks} blocks")
         return torch.tensor(ids, dtype=torch.int32, device=self.device)
 
+    def probe_channel(self, rank: int, peer: str, nbytes: int, log=print) -> Optional[dict]:
+        """Time one `nbytes` transfer over this pair channel (rank 0 sends, rank 1 receives),
+        right after the channel formed and before any KV moves on it: the achieved GB/s and
+        RCCL's chosen transport go to CHANNEL_PROBES[peer] (and /metrics), so a deployment
+        sees what its prefill -> decode path really is (xGMI peer-to-peer vs host-staged)."""
+        if nbytes <= 0 or self.pg is None:
+            return None
+        on_dev = self.is_gpu and not self.gloo
+        dev = self.device if on_dev else torch.device("cpu")
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        op = self._isend if rank == 0 else self._irecv
+        other = 1 - rank
+        what = f"KV channel probe with {peer}"
+        with self._ctx():
+            _wait(op(buf[: 1 << 20], other), self.timeout_s, what, self.gloo)  # connect + sync
+            if on_dev:
+                self.stream.synchronize()
+            t0 = time.perf_counter()
+            _wait(op(buf, other), self.timeout_s, what, self.gloo)
+            if on_dev:
+                self.stream.synchronize()
+            dt = time.perf_counter() - t0
+        backend = "gloo" if self.gloo else "nccl"
+        res = {"gbps": nbytes / dt / 1e9, "bytes": nbytes, "seconds": dt,
+               "transport": channel_transport(backend), "role": "send" if rank == 0 else "recv"}
+        CHANNEL_PROBES[peer] = res
+        log(f"[pd] KV channel probe {peer}: {nbytes / 2**20:.0f} MiB in {dt * 1e3:.1f} ms = "
+            f"{res['gbps']:.2f} GB/s over {res['transport']} ({backend})")
+        return res
+
     def nbytes(self, nblk: int) -> int:
         return self.num_planes * nblk * self.block_elems * self.kv.element_size()
 
@@ -494,6 +524,65 @@ class _Null:
 # hipIpc pull needs no channel at all (/kv/lease carries the export handle); this channel
 # carries the p2p transport (and the p2p fallback of a peer whose cache cannot be mapped).
 
+# peer -> the channel probe's result ({"gbps", "bytes", "seconds", "transport", "role"}): what
+# a freshly formed pair channel actually moves, exported as akap:kv_channel_probe_gbps
+CHANNEL_PROBES: dict = {}
+
+
+def probe_bytes(gpu: bool) -> int:
+    """Size of the channel probe (AKAP_PD_PROBE_MIB; 0 disables): 256 MiB between GPU
+    engines -- large enough that link bandwidth, not latency, sets the rate -- 8 MiB on CPU."""
+    env = os.environ.get("AKAP_PD_PROBE_MIB")
+    mib = float(env) if env else (256.0 if gpu else 8.0)
+    return int(mib * 2**20)
+
+
+def transport_from_rccl_log(text: str) -> str:
+    """RCCL's transport for a connection, from its INFO log (NCCL_DEBUG=INFO with the P2P /
+    SHM / NET subsystems): "P2P" (peer mapping: xGMI / PCIe peer-to-peer), "SHM" (host shared
+    memory), "NET" (sockets / IB: what two pods that see neither each other's GPU nor a common
+    /dev/shm end up on), else "unknown"."""
+    seen = set()
+    for line in text.splitlines():
+        if " via " not in line:
+            continue
+        via = line.split(" via ", 1)[1].strip()
+        for kind in ("P2P", "SHM", "NET"):
+            if via.startswith(kind):
+                seen.add(kind)
+    for kind in ("NET", "SHM", "P2P"):  # the slowest path any channel took
+        if kind in seen:
+            return kind
+    return "unknown"
+
+
+def channel_transport(backend: str) -> str:
+    if backend == "gloo":
+        return "gloo-tcp"
+    path = os.environ.get("NCCL_DEBUG_FILE")
+    if not path:
+        return "unknown"
+    import socket
+
+    path = path.replace("%h", socket.gethostname()).replace("%p", str(os.getpid()))
+    try:
+        with open(path, errors="replace") as f:
+            return transport_from_rccl_log(f.read())
+    except OSError:
+        return "unknown"
+
+
+def enable_rccl_transport_log() -> None:
+    """Before the first RCCL communicator of this process: have RCCL log its connection
+    transports to a per-process file (unless the operator configured NCCL_DEBUG already), so
+    the channel probe can report which one the pair channel got."""
+    if "NCCL_DEBUG" in os.environ:
+        return
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,P2P,SHM,NET")
+    os.environ.setdefault("NCCL_DEBUG_FILE", "/tmp/akap-rccl.%h.%p.log")
+
+
 def pair_backend(kv: torch.Tensor) -> str:
     """gloo on CPU caches (and AKAP_PD_PAIR_BACKEND=gloo: host-staged, works between pods that
     see no common device), RCCL between GPU engines."""
@@ -537,6 +626,9 @@ class PairHost:
                 pg = _pair_group(self.store, prefix, 0, backend, self.timeout_s)
                 ag = KVTransferAgent(self.kv, timeout_s=self.timeout_s, pair=(pg, backend))
                 ag.generation = int(generation)
+                # the decode side receives this right after joining; registered only after
+                # it, so no KV send can interleave with the probe on the channel
+                ag.probe_channel(0, peer, probe_bytes(ag.is_gpu))
                 with self.lock:
                     old = self.agents.get(peer)
                     self.agents[peer] = ag
@@ -571,4 +663,5 @@ def connect_pair(kv: torch.Tensor, host: str, port: int, prefix: str, backend: s
     pg = _pair_group(store, prefix, 1, backend, timeout_s)
     ag = KVTransferAgent(kv, timeout_s=timeout_s, pair=(pg, backend))
     ag._store = store  # keep the client alive with the group
+    ag.probe_channel(1, f"{host}:{port}", probe_bytes(ag.is_gpu))
     return ag

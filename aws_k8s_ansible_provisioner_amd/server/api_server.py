@@ -719,6 +719,13 @@ def build_app(ecfg: EngineConfig, engine=None, pd_bootstrap: str = "launcher",
         else:
             ae.pd_group = eng.pd_group = pd_group_id()
         eng.kv_agent = ae.kv_agent
+        if ecfg.kv_role == "decode":
+            from .async_engine import decode_transport
+
+            # /metrics akap:kv_transport_ipc: 1 while this decode server pulls KV by hipIpc
+            # (no prefill peer fell back to p2p) -- the gateway prefers such pairs
+            eng.kv_ipc_state = lambda: (decode_transport(ae.kv_agent) == "ipc" and not (
+                ae.puller is not None and ae.puller.ipc_fallback))
     srv = OpenAIServer(ae, eng.model_name, ecfg.chat_template, ecfg.max_model_len)
     return srv.app, ae
 
@@ -735,6 +742,12 @@ def main(argv: Optional[list] = None) -> None:
 
         serve_tp(ecfg, a.host, a.port, telemetry=lambda labels: make_telemetry(a, labels))
         return
+    if a.kv_role != "both" and a.pd_bootstrap == "http" and a.device != "cpu":
+        # two-pod P/D: log RCCL's connection transports so the channel probe can report which
+        # one the pair channel got (P2P over xGMI vs SHM vs NET sockets)
+        from ..parallel.kv_transfer import enable_rccl_transport_log
+
+        enable_rccl_transport_log()
     if a.kv_role != "both" and a.pd_bootstrap == "launcher":
         # P/D: this process is one rank of the prefill/decode KV-transfer group (torchrun)
         from ..parallel.state import init_distributed

@@ -45,6 +45,15 @@ class PullJob:
     loop: "asyncio.AbstractEventLoop"
 
 
+def decode_transport(kv_agent) -> str:
+    """AKAP_KV_TRANSPORT: ipc (GPU default: pull the blocks out of the prefill engine's
+    hipIpc-mapped cache) or p2p (/kv/push + a packed send/recv over the process group)."""
+    env = os.environ.get("AKAP_KV_TRANSPORT", "auto")
+    if env in ("ipc", "p2p"):
+        return env
+    return "ipc" if getattr(kv_agent, "is_gpu", False) else "p2p"
+
+
 class KVPuller:
     """Decode-side P/D data path.  Pulls queued at the same moment from the same prefill
     server are coalesced: blocks are reserved for each request, ONE POST /kv/push names all
@@ -171,12 +180,7 @@ class KVPuller:
 
 
     def transport(self) -> str:
-        """AKAP_KV_TRANSPORT: ipc (GPU default: pull the blocks out of the prefill engine's
-        hipIpc-mapped cache) or p2p (/kv/push + a packed send/recv over the process group)."""
-        env = os.environ.get("AKAP_KV_TRANSPORT", "auto")
-        if env in ("ipc", "p2p"):
-            return env
-        return "ipc" if getattr(self.ae.kv_agent, "is_gpu", False) else "p2p"
+        return decode_transport(self.ae.kv_agent)
 
     def _pull_batch_ipc(self, url: str, ready: list, reserved: list):
         """hipIpc transport: lease the transfers' blocks (POST /kv/lease), map the prefill

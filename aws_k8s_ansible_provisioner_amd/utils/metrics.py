@@ -186,6 +186,13 @@ class EngineMetrics:
         self.kv_xfer_bytes = r.add(Counter("akap:kv_transfer_bytes_total",
                                            "KV bytes moved over the transfer group",
                                            ("model_name", "direction")))
+        self.kv_probe_gbps = r.add(Gauge(
+            "akap:kv_channel_probe_gbps",
+            "Two-pod P/D: GB/s of the probe transfer over a freshly formed KV channel",
+            ("model_name", "peer", "transport", "role")))
+        self.kv_ipc = r.add(Gauge(
+            "akap:kv_transport_ipc",
+            "1 when this engine moves KV by the hipIpc pull (no failed peer mapping)", L))
         # aliases queried by the reference's OTel verification play
         self.req_total = r.add(Counter("vllm_request_total", "Requests received (alias)", L))
         self.active = r.add(Gauge("vllm_active_requests", "Requests in flight (alias)", L))

@@ -81,6 +81,34 @@ def test_picker_pd_pairs_only_within_a_transfer_group():
     assert pre is None and dec.url == "http://10.0.0.1:8001"
 
 
+def test_picker_pd_prefers_ipc_decode():
+    """among valid P/D pairs the gateway prefers one whose decode endpoint
+    pulls KV by hipIpc (akap:kv_transport_ipc) over a slightly less loaded send/recv pair."""
+    p = EndpointPicker([], PickerConfig(pd_threshold_chars=10), seed=1)
+    p.set_endpoints([("http://a:8000", "prefill", "g"), ("http://b:8001", "decode", "g"),
+                     ("http://c:8001", "decode", "g")])
+    p.update_metrics("http://a:8000", 0, 0, 0.0)
+    p.update_metrics("http://b:8001", running=2, waiting=0, kv=0.2, kv_ipc=True)
+    p.update_metrics("http://c:8001", 0, 0, 0.0, kv_ipc=False)
+    for _ in range(10):
+        pre, dec = p.pick_pd("x" * 40)
+        assert dec.url == "http://b:8001"
+    p.update_metrics("http://b:8001", running=2, waiting=0, kv=0.2, kv_ipc=False)
+    pre, dec = p.pick_pd("x" * 40)
+    assert dec.url == "http://c:8001"
+
+
+def test_rccl_transport_parse():
+    from aws_k8s_ansible_provisioner_amd.parallel.kv_transfer import transport_from_rccl_log
+
+    log = ("host:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC\n"
+           "host:1:2 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC\n")
+    assert transport_from_rccl_log(log) == "P2P"
+    assert transport_from_rccl_log(log + "x NCCL INFO Channel 02/0 : 0 -> 1 via SHM/direct/direct") == "SHM"
+    assert transport_from_rccl_log("NCCL INFO Channel 00/0 : 0[0] -> 1[0] [send] via NET/Socket/0") == "NET"
+    assert transport_from_rccl_log("nothing") == "unknown"
+
+
 def test_parsers():
     m = parse_prometheus('# HELP x\nvllm:num_requests_running{model_name="m"} 3.0\n'
                          'vllm:num_requests_running{model_name="n"} 2\nbad line\n')

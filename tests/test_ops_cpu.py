@@ -298,3 +298,21 @@ def test_fused_decode_gemm_support_rules():
     assert not ops.dgemm_supported(256, 1024, 2048, 4, 3)    # prefetch depth 1|2|4
     assert not ops.dgemm_supported(256, 1022, 1024, 1, 1)    # N % 4
     assert not ops.dgemm_supported(256, 1024, 1024, 8, 4)    # K/split not a multiple of 64*pf
+
+
+def test_qprep_position_invariant_check():
+    """the q-prep prefill kernel rotates by key index, not by `positions`; the
+    debug check (AKAP_DEBUG_CHECKS=1) refuses batches where the two differ or where the
+    rotary table is too short."""
+    import pytest
+
+    from aws_k8s_ansible_provisioner_amd import ops
+
+    q_start = torch.tensor([0, 3, 5], dtype=torch.int32)
+    seq_lens = torch.tensor([10, 2], dtype=torch.int32)
+    pos = torch.tensor([7, 8, 9, 0, 1])
+    ops.check_qprep_positions(pos, seq_lens, q_start, 16)
+    with pytest.raises(ValueError, match="key indices"):
+        ops.check_qprep_positions(torch.tensor([7, 8, 10, 0, 1]), seq_lens, q_start, 16)
+    with pytest.raises(ValueError, match="rotary"):
+        ops.check_qprep_positions(pos, seq_lens, q_start, 8)

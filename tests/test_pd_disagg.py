@@ -457,6 +457,16 @@ def test_two_pod_pd_independent_servers_through_gateway():
         chunks = [_j.loads(l[6:]) for l in sse.splitlines() if l.startswith("data: {")]
         assert "".join(c["choices"][0]["text"] for c in chunks if c.get("choices")) == \
             "".join(ref.tokenizer.decode_token(t) for t in expect.output_ids)
+        # the fresh channel was probed once on each side; both export the
+        # achieved rate and the transport (gloo here: host TCP), the decode side its pull path
+        for u, role in ((urls[0], "send"), (urls[1], "recv")):
+            text = urllib.request.urlopen(u + "/metrics").read().decode()
+            probe = [ln for ln in text.splitlines()
+                     if ln.startswith("akap:kv_channel_probe_gbps{")]
+            assert len(probe) == 1 and f'role="{role}"' in probe[0], text[-2000:]
+            assert 'transport="gloo-tcp"' in probe[0] and float(probe[0].rsplit(" ", 1)[1]) > 0
+        dtext = urllib.request.urlopen(urls[1] + "/metrics").read().decode()
+        assert 'akap:kv_transport_ipc{model_name=' in dtext  # p2p on CPU: 0
     finally:
         for p in procs:
             p.kill()

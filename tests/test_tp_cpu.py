@@ -369,3 +369,16 @@ def test_ep_dispatch_bytes_bounded():
             assert blk.a2a_rows(T) <= 2 * exact, (ep, T, blk.a2a_rows(T), exact)
         # one-token steps: capacity covers every pair (no overflow possible)
         assert blk.ep_capacity(cfg.experts_per_token) == cfg.experts_per_token
+
+
+def test_car_grid_agreed_from_physical_devices():
+    """the K13 grid is one value for the whole communicator -- the minimum of the
+    ranks' overrides and of the sharing rule, where sharing is counted from gathered physical
+    device keys (one visible GPU per rank is NOT sharing)."""
+    from aws_k8s_ansible_provisioner_amd.parallel.custom_allreduce import agree_grid
+
+    own = ["h:0:1:0", "h:0:2:0", "h:0:3:0", "h:0:4:0"]
+    assert agree_grid(own, [128] * 4) == 128            # 4 GPUs, index 0 visible in each rank
+    assert agree_grid(["h:0:1:0"] * 4, [128] * 4) == 32  # 4 ranks on one GPU
+    assert agree_grid(["h:0:1:0"] * 2 + ["h:0:2:0"] * 2, [128] * 4) == 64
+    assert agree_grid(own, [128, 128, 16, 128]) == 16   # one rank's override binds everyone

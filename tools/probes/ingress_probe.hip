@@ -1,0 +1,267 @@
+// Decode-GEMM ingress ceiling on one MI355X: how fast can the decode projections' operand tiles
+// (X rows of the batch + W rows of the output columns, the bytes a GEMM workgroup must bring
+// into its CU) be streamed into LDS with NO math, per shape, tile and ring depth, from cold
+// (HBM) and warm (MALL-resident) weights?  If the streaming alone takes about as long as the
+// GEMM kernel, the kernel sits at the ingress ceiling and only fewer bytes per CU (tiling) or
+// overlap across launches can help; if it is much faster, the GEMM's pipeline is the loss.
+//
+// Each workgroup (WAVES x 64 threads) owns a BM x BN output tile, i.e. streams BM x K of X and
+// BN x K of W in KST-deep stages through an NS-slot LDS ring by LDS-DMA (global_load_lds 16 B
+// per lane), counted vmcnt + barrier per stage (the kgemm / pgemm discipline), and reads one
+// 16-B LDS word per lane per stage so the data is consumed.  Grid: one workgroup per tile,
+// a column tile's row tiles on one XCD (xcd_remap, as the GEMMs).
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/probes/ingress_probe tools/probes/ingress_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short bf16raw;
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = orig % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / 8;
+}
+
+struct Args {
+  const bf16raw* X;
+  const bf16raw* W;
+  int M, N, K, BM, BN, KST, NS;
+  unsigned* out;
+};
+
+// LDS ring: NS slots of (BM + BN) rows x KST bf16.  DMA piece = 64 lanes x 16 B = 1 KiB.
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_ingress(Args a) {
+  extern __shared__ u32x4 ring[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_m = a.M / a.BM, tiles_n = a.N / a.BN;
+  const int lt = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = lt / tiles_m, tm = lt % tiles_m;
+  const int m0 = tm * a.BM, n0 = tn * a.BN;
+  const int rows = a.BM + a.BN;
+  const int cpr = a.KST / 8;                 // 16-B chunks per staged row
+  const int units = rows * cpr;              // 16-B units per slot
+  const int pieces = units / 64;             // 1 KiB DMA pieces per slot
+  const int per_wave = (pieces + WAVES - 1) / WAVES;
+  const int nst = a.K / a.KST;
+  auto issue = [&](int st) {
+    u32x4* slot = ring + (st % a.NS) * units;
+    for (int i = 0; i < per_wave; ++i) {
+      const int pc = w * per_wave + i;
+      if (pc >= pieces) break;
+      const int u = pc * 64 + lane;
+      const int row = u / cpr, ch = u % cpr;
+      const bf16raw* src = row < a.BM ? a.X + (size_t)(m0 + row) * a.K
+                                      : a.W + (size_t)(n0 + row - a.BM) * a.K;
+      src += (size_t)st * a.KST + ch * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(slot + pc * 64),
+                                       16, 0, 0);
+    }
+  };
+  unsigned acc = 0;
+  for (int s = 0; s < a.NS - 1 && s < nst; ++s) issue(s);
+  for (int t = 0; t < nst; ++t) {
+    // stages t+1 .. t+NS-2 may stay in flight: per_wave pieces per stage (uniform upper bound)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + a.NS - 1 < nst) issue(t + a.NS - 1);
+    const u32x4* slot = ring + (t % a.NS) * units;
+    acc ^= slot[(tid * 7) % units].x;
+  }
+  if (acc == 0x9e3779b9u) a.out[0] = acc;
+}
+
+// Variant with exact counted waits: compile-time pieces per wave (P) and depth (NS) so the
+// vmcnt immediate is exact -- stages t+1..t+NS-2 stay in flight across the barrier.
+template <int WAVES, int P, int NS>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_c(Args a) {
+  extern __shared__ u32x4 ring[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_m = a.M / a.BM, tiles_n = a.N / a.BN;
+  const int lt = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = lt / tiles_m, tm = lt % tiles_m;
+  const int m0 = tm * a.BM, n0 = tn * a.BN;
+  const int cpr = a.KST / 8;
+  const int units = (a.BM + a.BN) * cpr;
+  const int nst = a.K / a.KST;
+  const bf16raw* src[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int u = (w * P + i) * 64 + lane;
+    const int row = u / cpr, ch = u % cpr;
+    src[i] = (row < a.BM ? a.X + (size_t)(m0 + row) * a.K
+                         : a.W + (size_t)(n0 + row - a.BM) * a.K) + ch * 8;
+  }
+  auto issue = [&](int st) {
+    u32x4* slot = ring + (st % NS) * units;
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src[i] + (size_t)st * a.KST),
+          (__attribute__((address_space(3))) void*)(slot + (w * P + i) * 64), 16, 0, 0);
+  };
+  unsigned acc = 0;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nst) issue(s);
+  for (int t = 0; t < nst; ++t) {
+    if (t + NS - 2 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * (NS - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + NS - 1 < nst) issue(t + NS - 1);
+    const u32x4* slot = ring + (t % NS) * units;
+    acc ^= slot[(tid * 7) % units].x;
+  }
+  if (acc == 0x9e3779b9u) a.out[0] = acc;
+}
+
+// Register path: each thread loads its share of every stage straight into VGPRs
+// (global_load_dwordx4), D stages in flight, no LDS.
+template <int WAVES, int P, int D>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_reg(Args a) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_m = a.M / a.BM, tiles_n = a.N / a.BN;
+  const int lt = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = lt / tiles_m, tm = lt % tiles_m;
+  const int m0 = tm * a.BM, n0 = tn * a.BN;
+  const int cpr = a.KST / 8;
+  const int nst = a.K / a.KST;
+  const u32x4* src[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int u = (w * P + i) * 64 + lane;
+    const int row = u / cpr, ch = u % cpr;
+    src[i] = reinterpret_cast<const u32x4*>(
+        (row < a.BM ? a.X + (size_t)(m0 + row) * a.K : a.W + (size_t)(n0 + row - a.BM) * a.K) +
+        ch * 8);
+  }
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 buf[D][P];
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+#pragma unroll
+    for (int i = 0; i < P; ++i) buf[s][i] = s < nst ? src[i][(size_t)s * a.KST / 8] : acc;
+  for (int t = 0; t < nst; t += D) {
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) acc ^= buf[s][i];
+      if (t + s + D < nst) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) buf[s][i] = src[i][(size_t)(t + s + D) * a.KST / 8];
+      }
+    }
+  }
+  if ((acc.x ^ acc.y) == 0x9e3779b9u) a.out[0] = acc.x;
+}
+
+struct Shape {
+  const char* name;
+  int N, K;
+};
+
+int main(int argc, char** argv) {
+  const int M = 256;
+  const int reps = 50;
+  Shape shapes[] = {{"qkv", 4096, 1024}, {"o", 1024, 2048}, {"gate_up", 6144, 1024},
+                    {"down", 1024, 3072}};
+  // per-shape weights laid out back to back (28 layers' worth would not fit MALL; here 4 x
+  // layer-sized tensors, flushed by a 512 MiB write for the cold arm)
+  size_t wmax = 0;
+  for (auto& s : shapes) wmax = std::max(wmax, (size_t)s.N * s.K);
+  bf16raw *X, *W;
+  unsigned* out;
+  void* flush;
+  const size_t flush_bytes = 512ull << 20;
+  CK(hipMalloc(&X, (size_t)M * 4096 * 2));
+  CK(hipMalloc(&W, wmax * 2));
+  CK(hipMalloc(&out, 64));
+  CK(hipMalloc(&flush, flush_bytes));
+  CK(hipMemset(X, 1, (size_t)M * 4096 * 2));
+  CK(hipMemset(W, 1, wmax * 2));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  printf("shape,tile,kst,ns,waves,path,weights,us,bytes_per_cu_KB,GBps_per_cu,wgs\n");
+  auto run = [&](const char* nm, const Shape& s, int BM, int BN, int KST, int NS, int waves,
+                 const char* path, auto launch) {
+    const int wgs = (M / BM) * (s.N / BN);
+    const double per_cu = (double)(BM + BN) * s.K * 2;
+    for (int cold = 0; cold < 2; ++cold) {
+      float tot = 0.f;
+      for (int r = 0; r < reps + 3; ++r) {
+        if (cold) CK(hipMemsetAsync(flush, r & 0xff, flush_bytes, 0));
+        CK(hipEventRecord(e0, 0));
+        launch(wgs);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 3) tot += ms;
+      }
+      const double us = tot / reps * 1000.0;
+      printf("%s,%dx%d,%d,%d,%d,%s,%s,%.2f,%.0f,%.1f,%d\n", nm, BM, BN, KST, NS, waves, path,
+             cold ? "cold" : "warm", us, per_cu / 1024, per_cu / (us * 1e-6) / 1e9, wgs);
+      fflush(stdout);
+    }
+  };
+  for (auto& s : shapes) {
+    struct T {
+      int BM, BN, KST;
+    };
+    std::vector<T> tiles;
+    if (s.N == 1024) tiles = {{32, 32, 256}, {64, 16, 256}, {16, 64, 256}, {64, 64, 128}};
+    else if (s.N == 4096) tiles = {{64, 64, 256}, {64, 64, 128}, {128, 32, 256}, {32, 128, 256}};
+    else tiles = {{64, 96, 256}, {64, 128, 128}, {64, 128, 256}, {128, 48, 256}};
+    for (auto& t : tiles) {
+      if (M % t.BM || s.N % t.BN || s.K % t.KST) continue;
+      const int units = (t.BM + t.BN) * t.KST / 8;
+      const int pieces = units / 64;
+      for (int NS : {3, 4, 6}) {
+        const size_t lds = (size_t)NS * units * 16;
+        if (lds > 160 * 1024) continue;
+        Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, NS, out};
+        run(s.name, s, t.BM, t.BN, t.KST, NS, 4, "lds_drain", [&](int wgs) {
+          k_ingress<4><<<wgs, 256, lds, 0>>>(a);
+        });
+        // exact counted waits for the common piece counts
+        if (pieces % 4 == 0) {
+          const int P = pieces / 4;
+#define CASE(PP, NN)                                                                 \
+  if (P == PP && NS == NN)                                                           \
+    run(s.name, s, t.BM, t.BN, t.KST, NS, 4, "lds_counted",                          \
+        [&](int wgs) { k_ingress_c<4, PP, NN><<<wgs, 256, lds, 0>>>(a); });
+          CASE(4, 3) CASE(4, 4) CASE(4, 6) CASE(8, 3) CASE(8, 4) CASE(6, 3) CASE(6, 4)
+          CASE(10, 3) CASE(10, 4) CASE(5, 3) CASE(5, 4) CASE(5, 6) CASE(12, 3)
+#undef CASE
+        }
+      }
+      if (pieces % 4 == 0) {
+        const int P = pieces / 4;
+        Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, 0, out};
+#define RCASE(PP, DD)                                                                  \
+  if (P == PP)                                                                         \
+    run(s.name, s, t.BM, t.BN, t.KST, DD, 4, "reg",                                    \
+        [&](int wgs) { k_ingress_reg<4, PP, DD><<<wgs, 256, 0, 0>>>(a); });
+        RCASE(4, 4) RCASE(4, 2) RCASE(8, 2) RCASE(6, 2) RCASE(5, 2) RCASE(5, 4) RCASE(10, 2)
+#undef RCASE
+      }
+    }
+  }
+  return 0;
+}
