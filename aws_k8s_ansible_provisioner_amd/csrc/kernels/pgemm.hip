@@ -394,6 +394,147 @@ __device__ __forceinline__ void pg_mainloop(bf16x8* lds, const __amdgpu_buffer_r
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// SCHED 3: the unit-pipelined 4-wave body (built from the ISA of the library kernel that wins
+// the prefill shapes, hipBLASLt's MT256x256x64_MI16x16x1 "SK3" kernel: 4 waves of 128 x 128,
+// one wave per SIMD, 256 accumulators, every LDS fragment read and every LDS-DMA piece issued
+// BETWEEN MFMAs, 3 vmcnt waits and ~2 barriers per 64-deep K tile; profiles/
+// r6_pgemm_isa_diff.md).  Against the phase pipeline above (same tile, same waves) it drops:
+//   * runtime-selected waits (pg_wait's if-chain: s_cbranch + SALU per wait),
+//   * bursts of 16-24 fragment reads before the MFMAs that consume them one by one,
+//   * the four-quadrant split of the accumulators (a quadrant's 16 MFMAs per phase).
+// Unit u = 32 K columns of the 256 x 256 tile (A 256 rows x 64 B + W 256 rows x 64 B = 32 KiB,
+// 8 1-KiB LDS-DMA pieces per wave) in LDS slot u % 4 (128 KiB).  Iteration u:
+//   wait unit u+1 landed (vmcnt(16): units u+2, u+3 stay in flight) + lgkmcnt(0) (this wave's
+//   fragments of u are in registers), barrier (every wave's are -> slot u % 4 is free);
+//   64 MFMAs of unit u on register set u & 1, with the 8 DMA pieces of unit u + 4 (into slot
+//   u % 4) and the 16 fragment reads of unit u + 1 (set (u + 1) & 1) interleaved between them
+//   (sched_group_barrier: per 8 MFMAs 2 reads and 1 DMA piece).
+// One barrier per 32-deep unit; every unit is requested 3 units (1.5 K tiles) ahead.
+// LDS rows are 64 B (4 chunks); chunk c of row r is stored at c ^ g((r >> 2) & 3), g = {0, 2,
+// 3, 1}: for every ds_read_b128 lane group the 16 (row, chunk) pairs of a 16 x 32 fragment
+// read land on 16 distinct 16-B bank slots (conflict-free; derivation in the r6 profile).
+constexpr int PU_SLOT = 2 * PG_T * 4;  // 16-B units per slot: A 256 rows + W 256 rows x 4
+
+__device__ __forceinline__ int pu_swz(int row, int c) {
+  return c ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3);
+}
+
+template <bool SILU_ROWS, typename ACC>
+__device__ __forceinline__ void pg_mainloop_u(bf16x8* lds, const __amdgpu_buffer_rsrc_t rx,
+                                              const __amdgpu_buffer_rsrc_t rw, int ldx, int K,
+                                              int nhalf, int m0, int n0, int ku0, int nu,
+                                              ACC& accs) {
+  auto& acc = accs.v;  // [8][8]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  // ---- DMA sources: piece e (0..7) of this wave: e < 4 -> A rows (4w+e)*16.., else W rows
+  uint32_t voff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int r16 = (e & 3) + 4 * w;  // which 16-row block of A (e < 4) or W (e >= 4)
+    const int row = r16 * 16 + (lane >> 2);
+    const int c = pu_swz(row, lane & 3);  // logical chunk held by this lane's LDS slot
+    if (e < 4) {
+      voff[e] = (uint32_t)(((m0 + row) * ldx + c * 8) * 2);
+    } else {
+      const int v = n0 + row;
+      int wr = v;
+      if constexpr (SILU_ROWS) wr = ((v >> 4) & 1) * nhalf + (v >> 5) * 16 + (v & 15);
+      voff[e] = (uint32_t)((wr * K + c * 8) * 2);
+    }
+  }
+  auto dma = [&](int u, int e) {  // piece e of unit u into slot u % 4
+    bf16x8* slot = lds + (u & 3) * PU_SLOT;
+    const int r16 = (e & 3) + 4 * w;
+    bf16x8* dst = slot + (e < 4 ? 0 : PG_T * 4) + r16 * 64;
+    // units past the end are issued too (no branch in the pipelined body) with a scalar
+    // offset past every descriptor's range: the buffer unit drops them without a memory
+    // access (the slot they land in is never read again)
+    const uint32_t kb = u < nu ? (uint32_t)((ku0 + u) * 32 * 2) : 0x7fff0000u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(e < 4 ? rx : rw,
+                                             (__attribute__((address_space(3))) void*)dst, 16,
+                                             voff[e], kb, 0, 0);
+#endif
+  };
+  // ---- fragment reads: set f (0/1) of unit u: A rows wm*128 + 16 i + fr, W rows wn*128 + ...
+  bf16x8 fa[2][8], fb[2][8];
+  const int ra = wm * 128 + fr, rb = wn * 128 + fr;
+  auto rd = [&](auto fc, int u) {
+    constexpr int f = decltype(fc)::value;
+    const bf16x8* slot = lds + (u & 3) * PU_SLOT;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = ra + 16 * i;
+      fa[f][i] = slot[r * 4 + pu_swz(r, fg)];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = rb + 16 * j;
+      fb[f][j] = slot[PG_T * 4 + r * 4 + pu_swz(r, fg)];
+    }
+  };
+  auto mma = [&](auto fc) {
+    constexpr int f = decltype(fc)::value;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[f][j], fa[f][i], acc[i][j], 0, 0, 0);
+  };
+  using F0 = HalfTile<0>;
+  using F1 = HalfTile<1>;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: units 0..3 requested, unit 0's fragments in set 0 ----
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dma(u, e);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  rd(F0{}, 0);
+
+  // one unit: wait for unit u + 1, barrier, MFMAs of u (set F) + DMA of u + 4 + reads of
+  // u + 1.  ONE loop over all units, two per iteration (the register sets alternate); the
+  // waits near the end are picked by uniform branches (a peeled tail made the register
+  // allocator rotate the 256 accumulators through copies every iteration)
+  auto step = [&](auto fc, auto gc, int u) {
+    // units u + 2, u + 3 are younger than u + 1 (16 pieces).  Near the end those are dropped
+    // pieces, and the waits are taken by uniform branches anyway: with one branch-free body
+    // the register allocator rotated the 256 accumulators through AGPR copies every unit
+    const int younger = min(nu - 2 - u, 2);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dma(u + 4, e);
+    // the fragment reads of unit u + 1 (past the last unit: a harmless re-read of a landed
+    // slot) and the 64 MFMAs of unit u in one scheduling region: the machine scheduler spreads
+    // the DMA pieces and reads between the MFMAs itself (explicit interleaving -- per-group
+    // sched_barrier fences or sched_group_barrier -- also made the allocator rotate them)
+    rd(gc, u + 1);
+    mma(fc);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int u = 0; u < nu; u += 2) {  // nu even
+    step(F0{}, F1{}, u);
+    step(F1{}, F0{}, u + 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the main loop
+}
+
 template <int EPI, bool GROUPED, int NB, int WAVES, int SCHED = 1>
 __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_kernel(PGemmArgs p) {
   using G = PgGeo<WAVES>;
@@ -416,9 +557,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_kernel(PGemmArgs p) {
       (void*)W, (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
   PgAcc<2 * PgGeo<WAVES>::NJ> accs;
   auto& acc = accs.v;
-  pg_mainloop<NB, EPI == EPI_SILU, WAVES, decltype(accs), SCHED>(lds, rx, rw, p.ldx, p.K,
-                                                                 p.N >> 1, m0, n0, 0,
-                                                                 p.K / PG_BK, accs);
+  if constexpr (SCHED == 3) {
+    static_assert(WAVES == 4, "the unit-pipelined body is the 4-wave 128 x 128 form");
+    pg_mainloop_u<EPI == EPI_SILU>(lds, rx, rw, p.ldx, p.K, p.N >> 1, m0, n0, 0, p.K / 32,
+                                   accs);
+  } else {
+    pg_mainloop<NB, EPI == EPI_SILU, WAVES, decltype(accs), SCHED>(lds, rx, rw, p.ldx, p.K,
+                                                                   p.N >> 1, m0, n0, 0,
+                                                                   p.K / PG_BK, accs);
+  }
 
   // ---- epilogue: lane holds rows wm*128 + i*16 + fr, 4 consecutive cols per fragment ---------
   bf16* Y = static_cast<bf16*>(p.Y);
@@ -683,7 +830,8 @@ long pgemm_sk_ws_floats(int M, int N, int splits) {
 int pgemm_sched() {
   static int v = [] {
     const char* e = getenv("AKAP_PGEMM_SCHED");
-    return (e && atoi(e) == 2) ? 2 : 1;
+    const int x = e ? atoi(e) : 1;
+    return (x == 2 || x == 3) ? x : 1;
   }();
   return v;
 }
@@ -739,6 +887,10 @@ void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
   const int tiles_n = p.N / PG_T;
   const int grid = p.groups > 0 ? ((p.M + PG_T - 1) / PG_T + p.groups) * tiles_n
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
+  if (pgemm_sched() == 3 && p.K % 128 == 0) {  // unit-pipelined 4-wave body (K >= 128)
+    launch_pgemm_w<4, 3>(p, epi, grid, st);
+    return;
+  }
   // two barriers per K tile (measured 1-4 % faster than four, profiles/r4_pgemm_nb_ab.log); the
   // SwiGLU form keeps four: with both fragment sets read in phase 1 it would spill
   const bool s2 = pgemm_sched() == 2;

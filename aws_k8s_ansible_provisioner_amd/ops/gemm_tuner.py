@@ -129,13 +129,55 @@ def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out
                                           bm)
 
 
+# choice rankings of the anchor batch sizes (shape class pruning, see tune_model)
+_RANK: dict = {}
+
+
+def _plain_candidates(M, weights, x, y, splits, pfs, bns, kms, lm_head):
+    """(choice, fn) for every hand-written way to compute x[M, K] @ w.T (hipBLASLt apart)."""
+    from . import dgemm_supported, kgemm_supported
+
+    w0 = weights[0]
+    N, K = w0.shape
+    dev = w0.device
+    n = len(weights)
+    if K % 64 == 0:  # wide-row weight-streaming kernel (csrc/kernels/wgemm.hip)
+        yield ("wgemm",), (lambda i: torch.ops.akap.wgemm(y, x, weights[i % n]))
+    for s in (() if lm_head else splits):
+        if K // s < 256 or K % (64 * s):
+            continue
+        ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
+        yield ("hip", s), (lambda i, ws=ws, s=s: torch.ops.akap.gemm(y, x, weights[i % n], ws, s))
+    for s in splits:
+        for pf in pfs:
+            if not dgemm_supported(M, N, K, s, pf) or (s > 1 and K // s < 256):
+                continue
+            ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
+            yield ("dgemm", s, pf), (lambda i, ws=ws, s=s, pf=pf: torch.ops.akap.dgemm(
+                y, x, weights[i % n], ws, 0, s, pf))
+        for bn, ns, inl, bm in _gd_variants(s, bns, M):  # LDS-DMA staged variants (gdgemm.hip)
+            if (not dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl, bm=bm)
+                    or (s > 1 and K // s < 256) or (lm_head and bm != 256)):
+                continue
+            yield (("dgemm", s, 1, bn, ns, inl, 0, bm),
+                   _gd_call(M, N, K, s, bn, ns, inl, y, x, weights, 0, None, None, None, None,
+                            bm))
+    for km in kms:  # K split inside the workgroup (csrc/kernels/kgemm.hip)
+        if not kgemm_supported(M, N, K, km):
+            continue
+        yield (("dgemm", 1, 1, 0, 0, False, km),
+               lambda i, km=km: torch.ops.akap.kgemm(y, x, weights[i % n], km, 0, 1e-6, None,
+                                                     None, None, None))
+
+
 def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
          margin: float = 0.03, pfs=(2, 4, 8), bns=(64, 128), kms=(16, 32),
-         lm_head: bool = False) -> Choice:
+         lm_head: bool = False, allowed: Optional[set] = None) -> Choice:
     """Pick the fastest way to compute x[M, K] @ w.T for these same-shape weights.
     hipBLASLt is kept unless the MFMA kernel is more than `margin` faster.  lm_head: only the
     256-row LDS-DMA tiles among the gdgemm variants (the narrow ones re-stream the
-    activations once per 64-128 of ~150k columns)."""
+    activations once per 64-128 of ~150k columns).  allowed: time only these choices (the
+    shape-class pruning of tune_model); the ranking lands in _RANK[(M, N, K)]."""
     from . import gemm_counters  # noqa: F401  (ensures the native library is loaded)
 
     w0 = weights[0]
@@ -144,49 +186,52 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
     x = torch.randn(M, K, device=dev, dtype=w0.dtype) * 0.1
     y = torch.empty(M, N, device=dev, dtype=w0.dtype)
     n = len(weights)
-    best: Choice = ("torch",)
-    t_best = _timed(lambda i: torch.nn.functional.linear(x, weights[i % n]), n)
-    t_torch = t_best
-    if K % 64 == 0:  # wide-row weight-streaming kernel (csrc/kernels/wgemm.hip)
-        t = _timed(lambda i: torch.ops.akap.wgemm(y, x, weights[i % n]), n)
-        if t < t_best:
-            best, t_best = ("wgemm",), t
-    for s in (() if lm_head else splits):
-        if K // s < 256 or K % (64 * s):
+    t_torch = _timed(lambda i: torch.nn.functional.linear(x, weights[i % n]), n)
+    timed = [(t_torch, ("torch",))]
+    for choice, fn in _plain_candidates(M, weights, x, y, splits, pfs, bns, kms, lm_head):
+        if allowed is not None and choice not in allowed:
             continue
-        ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
-        t = _timed(lambda i: torch.ops.akap.gemm(y, x, weights[i % n], ws, s), n)
-        if t < t_best:
-            best, t_best = ("hip", s), t
-    from . import dgemm_supported
-    for s in splits:
-        for pf in pfs:
-            if not dgemm_supported(M, N, K, s, pf) or (s > 1 and K // s < 256):
-                continue
-            ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
-            t = _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, s, pf), n)
-            if t < t_best:
-                best, t_best = ("dgemm", s, pf), t
-        for bn, ns, inl, bm in _gd_variants(s, bns, M):  # LDS-DMA staged variants (gdgemm.hip)
-            if (not dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl, bm=bm)
-                    or (s > 1 and K // s < 256) or (lm_head and bm != 256)):
-                continue
-            t = _timed(_gd_call(M, N, K, s, bn, ns, inl, y, x, weights, 0, None, None, None,
-                                None, bm), n)
-            if t < t_best:
-                best, t_best = ("dgemm", s, 1, bn, ns, inl, 0, bm), t
-    from . import kgemm_supported
-    for km in kms:  # K split inside the workgroup (csrc/kernels/kgemm.hip)
-        if not kgemm_supported(M, N, K, km):
-            continue
-        t = _timed(lambda i, km=km: torch.ops.akap.kgemm(y, x, weights[i % n], km, 0, 1e-6,
-                                                         None, None, None, None), n)
-        if t < t_best:
-            best, t_best = ("dgemm", 1, 1, 0, 0, False, km), t
+        timed.append((_timed(fn, n), choice))
+    timed.sort(key=lambda tc: tc[0])
+    _RANK[(M, N, K)] = [c for _, c in timed]
+    t_best, best = timed[0]
     if best[0] != "torch" and t_best > t_torch * (1.0 - margin):
         best = ("torch",)
     _PLAN[(M, N, K)] = best
     return best
+
+
+def anchor_ms(Ms: Sequence[int]) -> list:
+    """Batch sizes tuned over every candidate (AKAP_GEMM_TUNE_FULL=1: all of them): the
+    smallest, 64, 128 and the largest bucket.  The others time only the top
+    AKAP_GEMM_TUNE_TOP (3) choices of their two neighbouring anchors: the decode GEMMs fall
+    into shape classes whose winning variant changes only at a few batch sizes (round-5
+    plans: kgemm below 128 rows, register ring / 128-wide LDS-DMA tiles above), so the
+    per-bucket search is mostly re-confirming a neighbour's pick (Llama-3-8B cold start
+    128.8 s, profiles/r5 pd_llama8b)."""
+    import os
+
+    ms = sorted(set(int(m) for m in Ms))
+    if os.environ.get("AKAP_GEMM_TUNE_FULL", "0") == "1" or len(ms) <= 4:
+        return ms
+    want = {ms[0], ms[-1]} | {m for m in (64, 128) if m in ms}
+    return sorted(want)
+
+
+def _neighbour_allowed(M: int, anchors: list, rank_of) -> Optional[set]:
+    """Union of the top choices of the anchors just below and above M (None: M is an
+    anchor)."""
+    import os
+
+    if M in anchors:
+        return None
+    top = int(os.environ.get("AKAP_GEMM_TUNE_TOP", "3"))
+    lo = [a for a in anchors if a < M]
+    hi = [a for a in anchors if a > M]
+    allowed: set = set()
+    for a in ([lo[-1]] if lo else []) + ([hi[0]] if hi else []):
+        allowed.update(rank_of(a)[:top])
+    return allowed
 
 
 def _gd_name(v) -> str:
@@ -207,9 +252,14 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
             if w is not None:
                 groups.setdefault((name, tuple(w.shape)), []).append(w)
     summary = {}
-    for M in Ms:
+    anchors = anchor_ms(Ms)
+    order = anchors + [m for m in sorted(set(Ms)) if m not in anchors]
+    for M in order:
         for (name, shape), ws in groups.items():
-            summary[(M, name)] = tune(M, ws)
+            N, K = shape
+            allowed = _neighbour_allowed(M, anchors,
+                                         lambda a, N=N, K=K: _RANK.get((a, N, K), []))
+            summary[(M, name)] = tune(M, ws, allowed=allowed)
     lm = getattr(model, "lm_head", None)
     if lm is not None and lm.is_cuda:
         # the decode LM head: hipBLASLt vs the wide-row kernel (split-K slabs of a vocab-wide
@@ -277,11 +327,17 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
     # all-reduce, comm.tp_all_reduce_resnorm), so they are timed with the plain store
     roles = _FUSED_ROLES if model.ps.tp_size == 1 else tuple(
         (n, 0 if n in ("w_o", "w_down") else e) for n, e in _FUSED_ROLES)
-    for M in Ms:
+    anchors = anchor_ms(Ms)
+    franks: dict = {}  # (M, name) -> candidate tuples by time (anchors only)
+    order = anchors + [m for m in sorted(set(Ms)) if m not in anchors]
+    for M in order:
         t_unfused = _time_unfused(M, model)
         plan_m, t_fused = {}, 0.0
         detail = []
         for name, epi in roles:
+            allowed = _neighbour_allowed(M, anchors,
+                                         lambda a, name=name: franks.get((a, name), []))
+            timed_c: list = []
             ws_ = [getattr(l, name) for l in model.layers]
             N, K = ws_[0].shape
             t_plain = _time_best_plain(M, name, ws_)
@@ -303,10 +359,13 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
                     cands += [(1, 0, 0, False, km, 64) for km in kms
                               if kgemm_supported(M, N, K, km, epi)]
                 for pf, bn, ns, inl, km, bm in cands:
+                    if allowed is not None and (s, pf, bn, ns, inl, km, bm) not in allowed:
+                        continue
                     if km:
                         fn = (lambda i, km=km: torch.ops.akap.kgemm(
                             out, x, ws_[i % L], km, epi, 1e-6, ss_in_, ss_out_, a_o_, ln_))
                         t = _timed(fn, L)
+                        timed_c.append((t, (s, pf, bn, ns, inl, km, bm)))
                         if best is None or t < best[0]:
                             best = (t, s, pf, bn, ns, inl, km, bm)
                         continue
@@ -322,8 +381,10 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
                             out, x, ws_[i % L], wsp, 0, s, pf, None, None, None, 1e-6, epi,
                             ss_in_, ss_out_, a_o_, ln_, 0))
                     t = _timed(fn, L)
+                    timed_c.append((t, (s, pf, bn, ns, inl, 0, bm)))
                     if best is None or t < best[0]:
                         best = (t, s, pf, bn, ns, inl, 0, bm)
+            franks[(M, name)] = [c for _, c in sorted(timed_c, key=lambda tc: tc[0])]
             if best is None:
                 plan_m = None
                 break
@@ -356,7 +417,8 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
     used = [m for m in Ms if m in _FUSED]
     log("[gemm-tuner] fused decode layer chain (us/layer fused vs unfused): " + ", ".join(
         f"M={m} {c[0]:.1f}/{c[1]:.1f}" + ("*" if m in _FUSED else "")
-        for m, c in chosen.items()) + f"  -> fused for {len(used)} of {len(Ms)} batch sizes")
+        for m, c in sorted(chosen.items())) + f"  -> fused for {len(used)} of {len(Ms)} "
+        f"batch sizes (full search at M={anchors})")
     return chosen
 
 

@@ -316,3 +316,20 @@ def test_qprep_position_invariant_check():
         ops.check_qprep_positions(torch.tensor([7, 8, 10, 0, 1]), seq_lens, q_start, 16)
     with pytest.raises(ValueError, match="rotary"):
         ops.check_qprep_positions(pos, seq_lens, q_start, 8)
+
+
+def test_tuner_shape_class_pruning():
+    """only the anchor batch sizes search every GEMM variant; the others
+    time the top choices of their two neighbouring anchors."""
+    from aws_k8s_ansible_provisioner_amd.ops import gemm_tuner as gt
+
+    ms = [16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256]
+    a = gt.anchor_ms(ms)
+    assert a == [16, 64, 128, 256]
+    ranks = {16: [("x",), ("y",), ("z",), ("w",)], 64: [("y",), ("q",), ("torch",)],
+             128: [("k",)], 256: [("g",)]}
+    assert gt._neighbour_allowed(64, a, ranks.get) is None
+    assert gt._neighbour_allowed(48, a, ranks.get) == {("x",), ("y",), ("z",), ("q",),
+                                                       ("torch",)}
+    assert gt._neighbour_allowed(200, a, ranks.get) == {("k",), ("g",)}
+    assert gt.anchor_ms([16, 32, 64]) == [16, 32, 64]

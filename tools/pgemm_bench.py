@@ -34,6 +34,21 @@ DENSE = [  # (name, M, N, K)
     ("qwen3-0.6b down", 16384, 1024, 3072),
     ("gate_up M=16384", 16384, 24576, 4096),
 ]
+# every dense prefill projection of the two benchmark models at a
+# 16384-token chunk (silu: the gate|up GEMM with the SwiGLU epilogue vs hipBLASLt +
+# silu_and_mul), and Mixtral's grouped w13 (SwiGLU) / w2
+VERDICT = [  # (name, M, N, K, silu)
+    ("qwen3-0.6b qkv", 16384, 4096, 1024, False),
+    ("qwen3-0.6b o", 16384, 1024, 2048, False),
+    ("qwen3-0.6b gate_up", 16384, 6144, 1024, False),
+    ("qwen3-0.6b gate_up silu", 16384, 6144, 1024, True),
+    ("qwen3-0.6b down", 16384, 1024, 3072, False),
+    ("llama3-8b qkv", 16384, 6144, 4096, False),
+    ("llama3-8b o", 16384, 4096, 4096, False),
+    ("llama3-8b gate_up", 16384, 28672, 4096, False),
+    ("llama3-8b gate_up silu", 16384, 28672, 4096, True),
+    ("llama3-8b down", 16384, 4096, 14336, False),
+]
 GROUPED = [  # (name, rows, experts, N, K)
     ("mixtral w13", 16384 * 2, 8, 28672, 4096),
     ("mixtral w2", 16384 * 2, 8, 4096, 14336),
@@ -58,9 +73,34 @@ def timeit(fn, iters=20):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default="")
+    ap.add_argument("--set", default="all", choices=["all", "verdict"])
     a = ap.parse_args()
     dev = "cuda"
     rows = []
+    if a.set == "verdict":
+        for name, M, N, K, silu in VERDICT:
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            fl = 2.0 * M * N * K
+            if silu:
+                act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
+                t_lib = timeit(lambda: ops.silu_and_mul(torch.matmul(x, w.t(), out=y), act))
+                t_pg = timeit(lambda: ops.pgemm(x, w, silu=True, out=act))
+                ref = ops.silu_and_mul(torch.matmul(x, w.t()))
+                err = (ops.pgemm(x, w, silu=True).float() - ref.float()).abs().max().item()
+            else:
+                t_lib = timeit(lambda: torch.matmul(x, w.t(), out=y))
+                t_pg = timeit(lambda: ops.pgemm(x, w, out=y))
+                err = (ops.pgemm(x, w).float() - torch.matmul(x, w.t()).float()).abs().max().item()
+            r = {"shape": name, "M": M, "N": N, "K": K, "lib_us": round(t_lib * 1e6, 1),
+                 "pgemm_us": round(t_pg * 1e6, 1), "hipblaslt_tflops": fl / t_lib / 1e12,
+                 "pgemm_tflops": fl / t_pg / 1e12, "speedup": t_lib / t_pg, "max_err": err}
+            rows.append(r)
+            print(json.dumps(r), flush=True)
+            del x, w, y
+        DENSE.clear()
+        del GROUPED[2:]
     for name, M, N, K in DENSE:
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02

@@ -15,6 +15,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                   \
@@ -41,7 +42,20 @@ struct Args {
   const bf16raw* W;
   int M, N, K, BM, BN, KST, NS;
   unsigned* out;
+  int map;  // 0: xcd_remap (a column tile's row tiles on one XCD), 1: identity
+  int op;   // 0: X and W rows, 1: X rows only (both halves from X), 2: W rows only
 };
+
+__device__ __forceinline__ int tile_id(const Args& a, int nwg) {
+  return a.map == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
+}
+__device__ __forceinline__ const bf16raw* src_row(const Args& a, int row, int m0, int n0) {
+  // op 1: the "W" rows re-read X rows (every operand byte from the shared 512 KB matrix);
+  // op 2: the "X" rows read W rows of a disjoint range (nothing shared between row tiles)
+  if (row < a.BM)
+    return a.op == 2 ? a.W + (size_t)((n0 + row + a.BN) % a.N) * a.K : a.X + (size_t)(m0 + row) * a.K;
+  return a.op == 1 ? a.X + (size_t)((m0 + row) % a.M) * a.K : a.W + (size_t)(n0 + row - a.BM) * a.K;
+}
 
 // LDS ring: NS slots of (BM + BN) rows x KST bf16.  DMA piece = 64 lanes x 16 B = 1 KiB.
 template <int WAVES>
@@ -49,7 +63,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress(Args a) {
   extern __shared__ u32x4 ring[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tiles_m = a.M / a.BM, tiles_n = a.N / a.BN;
-  const int lt = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int lt = tile_id(a, tiles_m * tiles_n);
   const int tn = lt / tiles_m, tm = lt % tiles_m;
   const int m0 = tm * a.BM, n0 = tn * a.BN;
   const int rows = a.BM + a.BN;
@@ -65,9 +79,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress(Args a) {
       if (pc >= pieces) break;
       const int u = pc * 64 + lane;
       const int row = u / cpr, ch = u % cpr;
-      const bf16raw* src = row < a.BM ? a.X + (size_t)(m0 + row) * a.K
-                                      : a.W + (size_t)(n0 + row - a.BM) * a.K;
-      src += (size_t)st * a.KST + ch * 8;
+      const bf16raw* src = src_row(a, row, m0, n0) + (size_t)st * a.KST + ch * 8;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(slot + pc * 64),
                                        16, 0, 0);
@@ -93,7 +105,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_c(Args a) {
   extern __shared__ u32x4 ring[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tiles_m = a.M / a.BM, tiles_n = a.N / a.BN;
-  const int lt = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int lt = tile_id(a, tiles_m * tiles_n);
   const int tn = lt / tiles_m, tm = lt % tiles_m;
   const int m0 = tm * a.BM, n0 = tn * a.BN;
   const int cpr = a.KST / 8;
@@ -104,8 +116,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_c(Args a) {
   for (int i = 0; i < P; ++i) {
     const int u = (w * P + i) * 64 + lane;
     const int row = u / cpr, ch = u % cpr;
-    src[i] = (row < a.BM ? a.X + (size_t)(m0 + row) * a.K
-                         : a.W + (size_t)(n0 + row - a.BM) * a.K) + ch * 8;
+    src[i] = src_row(a, row, m0, n0) + ch * 8;
   }
   auto issue = [&](int st) {
     u32x4* slot = ring + (st % NS) * units;
@@ -136,7 +147,7 @@ template <int WAVES, int P, int D>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_reg(Args a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tiles_m = a.M / a.BM, tiles_n = a.N / a.BN;
-  const int lt = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int lt = tile_id(a, tiles_m * tiles_n);
   const int tn = lt / tiles_m, tm = lt % tiles_m;
   const int m0 = tm * a.BM, n0 = tn * a.BN;
   const int cpr = a.KST / 8;
@@ -146,9 +157,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_reg(Args a) {
   for (int i = 0; i < P; ++i) {
     const int u = (w * P + i) * 64 + lane;
     const int row = u / cpr, ch = u % cpr;
-    src[i] = reinterpret_cast<const u32x4*>(
-        (row < a.BM ? a.X + (size_t)(m0 + row) * a.K : a.W + (size_t)(n0 + row - a.BM) * a.K) +
-        ch * 8);
+    src[i] = reinterpret_cast<const u32x4*>(src_row(a, row, m0, n0) + ch * 8);
   }
   u32x4 acc = {0, 0, 0, 0};
   u32x4 buf[D][P];
@@ -176,12 +185,13 @@ struct Shape {
 };
 
 int main(int argc, char** argv) {
+  // optional filter: only configs whose CSV prefix "shape,tile,kst,ns,waves,path,map,op"
+  // starts with argv[1] (one config per process for rocprofv3 --pmc passes)
+  const char* filt = argc > 1 ? argv[1] : nullptr;
+  const int reps = argc > 2 ? atoi(argv[2]) : 50;
   const int M = 256;
-  const int reps = 50;
   Shape shapes[] = {{"qkv", 4096, 1024}, {"o", 1024, 2048}, {"gate_up", 6144, 1024},
                     {"down", 1024, 3072}};
-  // per-shape weights laid out back to back (28 layers' worth would not fit MALL; here 4 x
-  // layer-sized tensors, flushed by a 512 MiB write for the cold arm)
   size_t wmax = 0;
   for (auto& s : shapes) wmax = std::max(wmax, (size_t)s.N * s.K);
   bf16raw *X, *W;
@@ -197,9 +207,13 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  printf("shape,tile,kst,ns,waves,path,weights,us,bytes_per_cu_KB,GBps_per_cu,wgs\n");
+  printf("shape,tile,kst,ns,waves,path,map,op,weights,us,bytes_per_cu_KB,GBps_per_cu,wgs\n");
   auto run = [&](const char* nm, const Shape& s, int BM, int BN, int KST, int NS, int waves,
-                 const char* path, auto launch) {
+                 const char* path, int map, int op, auto launch) {
+    char key[128];
+    snprintf(key, sizeof key, "%s,%dx%d,%d,%d,%d,%s,%d,%d", nm, BM, BN, KST, NS, waves, path,
+             map, op);
+    if (filt && strncmp(key, filt, strlen(filt)) != 0) return;
     const int wgs = (M / BM) * (s.N / BN);
     const double per_cu = (double)(BM + BN) * s.K * 2;
     for (int cold = 0; cold < 2; ++cold) {
@@ -215,8 +229,8 @@ int main(int argc, char** argv) {
         if (r >= 3) tot += ms;
       }
       const double us = tot / reps * 1000.0;
-      printf("%s,%dx%d,%d,%d,%d,%s,%s,%.2f,%.0f,%.1f,%d\n", nm, BM, BN, KST, NS, waves, path,
-             cold ? "cold" : "warm", us, per_cu / 1024, per_cu / (us * 1e-6) / 1e9, wgs);
+      printf("%s,%s,%.2f,%.0f,%.1f,%d\n", key, cold ? "cold" : "warm", us, per_cu / 1024,
+             per_cu / (us * 1e-6) / 1e9, wgs);
       fflush(stdout);
     }
   };
@@ -225,42 +239,40 @@ int main(int argc, char** argv) {
       int BM, BN, KST;
     };
     std::vector<T> tiles;
-    if (s.N == 1024) tiles = {{32, 32, 256}, {64, 16, 256}, {16, 64, 256}, {64, 64, 128}};
-    else if (s.N == 4096) tiles = {{64, 64, 256}, {64, 64, 128}, {128, 32, 256}, {32, 128, 256}};
-    else tiles = {{64, 96, 256}, {64, 128, 128}, {64, 128, 256}, {128, 48, 256}};
+    if (s.N == 1024) tiles = {{32, 32, 256}, {64, 64, 128}};
+    else if (s.N == 4096) tiles = {{64, 64, 128}, {128, 32, 256}};
+    else tiles = {{64, 128, 128}, {64, 96, 128}};
     for (auto& t : tiles) {
       if (M % t.BM || s.N % t.BN || s.K % t.KST) continue;
       const int units = (t.BM + t.BN) * t.KST / 8;
       const int pieces = units / 64;
-      for (int NS : {3, 4, 6}) {
-        const size_t lds = (size_t)NS * units * 16;
-        if (lds > 160 * 1024) continue;
-        Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, NS, out};
-        run(s.name, s, t.BM, t.BN, t.KST, NS, 4, "lds_drain", [&](int wgs) {
-          k_ingress<4><<<wgs, 256, lds, 0>>>(a);
-        });
-        // exact counted waits for the common piece counts
-        if (pieces % 4 == 0) {
-          const int P = pieces / 4;
-#define CASE(PP, NN)                                                                 \
-  if (P == PP && NS == NN)                                                           \
-    run(s.name, s, t.BM, t.BN, t.KST, NS, 4, "lds_counted",                          \
+      for (int map = 0; map < 2; ++map)
+        for (int op = 0; op < 3; ++op) {
+          for (int NS : {4}) {
+            const size_t lds = (size_t)NS * units * 16;
+            if (lds > 160 * 1024) continue;
+            Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, NS, out, map, op};
+            if (pieces % 4 == 0) {
+              const int P = pieces / 4;
+#define CASE(PP, NN)                                                                   \
+  if (P == PP && NS == NN)                                                             \
+    run(s.name, s, t.BM, t.BN, t.KST, NS, 4, "lds_counted", map, op,                   \
         [&](int wgs) { k_ingress_c<4, PP, NN><<<wgs, 256, lds, 0>>>(a); });
-          CASE(4, 3) CASE(4, 4) CASE(4, 6) CASE(8, 3) CASE(8, 4) CASE(6, 3) CASE(6, 4)
-          CASE(10, 3) CASE(10, 4) CASE(5, 3) CASE(5, 4) CASE(5, 6) CASE(12, 3)
+              CASE(4, 4) CASE(8, 4) CASE(6, 4) CASE(5, 4) CASE(10, 4) CASE(12, 4)
 #undef CASE
-        }
-      }
-      if (pieces % 4 == 0) {
-        const int P = pieces / 4;
-        Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, 0, out};
-#define RCASE(PP, DD)                                                                  \
-  if (P == PP)                                                                         \
-    run(s.name, s, t.BM, t.BN, t.KST, DD, 4, "reg",                                    \
+            }
+          }
+          if (pieces % 4 == 0) {
+            const int P = pieces / 4;
+            Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, 0, out, map, op};
+#define RCASE(PP, DD)                                                                    \
+  if (P == PP)                                                                           \
+    run(s.name, s, t.BM, t.BN, t.KST, DD, 4, "reg", map, op,                             \
         [&](int wgs) { k_ingress_reg<4, PP, DD><<<wgs, 256, 0, 0>>>(a); });
-        RCASE(4, 4) RCASE(4, 2) RCASE(8, 2) RCASE(6, 2) RCASE(5, 2) RCASE(5, 4) RCASE(10, 2)
+            RCASE(4, 2) RCASE(8, 2) RCASE(6, 2) RCASE(5, 2) RCASE(10, 2) RCASE(12, 2)
 #undef RCASE
-      }
+          }
+        }
     }
   }
   return 0;
