@@ -59,6 +59,12 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
   const int kz = blockIdx.y;
   const int kbeg = kz * p.kps;
   const int nk = p.kps / DBK;  // host: K % kps == 0, kps % (DBK * PF) == 0
+  const int st0 = gemm_stagger0(p.stag, tm, tn, nk);
+  auto kpos = [&](int i) {  // K offset of this workgroup's i-th k-tile (staggered walk)
+    int ks = i + st0;
+    if (ks >= nk) ks -= nk;
+    return kbeg + ks * DBK;
+  };
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
@@ -195,15 +201,15 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
 
   // prologue: PF k-tiles in flight
 #pragma unroll
-  for (int q = 0; q < PF; ++q) gload(q, kbeg + q * DBK);
+  for (int q = 0; q < PF; ++q) gload(q, kpos(q));
   int t = 0;
   for (; t + PF < nk; t += PF) {  // steady state: consume slot q, refill it PF tiles ahead
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int buf = (t + q) & 1;
-      sstore(q, buf, kbeg + (t + q) * DBK);
+      sstore(q, buf, kpos(t + q));
       __syncthreads();
-      gload(q, kbeg + (t + q + PF) * DBK);
+      gload(q, kpos(t + q + PF));
       // pin the refill here: left alone, the scheduler sinks it below the NEXT slot's
       // ds_write (whose vmcnt wait then drains every load: a 1-deep pipeline)
       __builtin_amdgcn_sched_barrier(0);
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
 #pragma unroll
   for (int q = 0; q < PF; ++q) {  // drain: the last PF tiles, no more loads
     const int buf = (t + q) & 1;
-    sstore(q, buf, kbeg + (t + q) * DBK);
+    sstore(q, buf, kpos(t + q));
     __syncthreads();
     mfma(buf);
   }

@@ -75,6 +75,14 @@ __device__ __forceinline__ void glds16_nt(const void* g, void* lds_wave_base) {
 // AKAP_WEIGHT_NT: unset -> -1 (gdgemm weights non-temporal, kgemm default policy: measured
 // Llama-3-8B +0.7 % on both A/B pairs, Qwen3-0.6B -0.65 % with kgemm nt too,
 // profiles/r3_weight_nt_ab.log); 1 -> both non-temporal; 0 -> neither
+int gemm_stagger_default() {
+  static const int v = [] {
+    const char* e = std::getenv("AKAP_GEMM_STAGGER");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  return v;
+}
+
 int weight_nt_default() {
   static const int v = [] {
     const char* e = std::getenv("AKAP_WEIGHT_NT");
@@ -122,6 +130,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   const int kz = blockIdx.y;
   const int kbeg = kz * p.kps;
   const int nk = p.kps / BKT;
+  const int st0 = gemm_stagger0(p.stag, tm, tn, nk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int fr = lane & 15, fg = lane >> 4;
@@ -151,7 +160,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void gdgemm_kernel(DGemmArgs p) {
   }
   auto issue = [&](int step) {  // DMA k-step `step` into its ring slot
     bf16x8* slot = lds + (step % NS) * SU;
-    const int k0 = kbeg + step * BKT;
+    int ks = step + st0;
+    if (ks >= nk) ks -= nk;
+    const int k0 = kbeg + ks * BKT;
 #pragma unroll
     for (int i = 0; i < GA; ++i) glds16(asrc[i] + k0, slot + (w * GA + i) * 64);
     if (p.ntw != 0) {

@@ -118,9 +118,18 @@ struct DGemmArgs {
   int* counters;  // gdgemm split-K: zeroed per-tile tickets -> in-launch last-arriver combine
   int bm;         // gdgemm tile rows: 64 (default) | 128 (with bn = 128)
   int ntw;        // weight DMA policy: -1 default (gdgemm nt, kgemm not), 1 both nt, 0 neither
+  int stag;       // 1: each workgroup walks its K range from a tile-dependent offset (wrapping)
 };
 // process default for DGemmArgs::ntw (AKAP_WEIGHT_NT, read once)
 int weight_nt_default();
+// process default for DGemmArgs::stag (AKAP_GEMM_STAGGER, read once)
+int gemm_stagger_default();
+// K-step at which tile (tm, tn) starts its walk of nk steps: workgroups that share an X panel
+// (same tm) or a W panel (same tn) start at different steps, so the ones resident together do
+// not request the same L2 lines at the same moment (hipBLASLt's "StaggerU")
+__device__ __forceinline__ int gemm_stagger0(int stag, int tm, int tn, int nk) {
+  return stag ? (tn + 3 * tm) % nk : 0;
+}
 bool dgemm_supported(int M, int N, int K, int splitk, int pf);
 // split-K factors with a compiled reduce (1, 2, 4, 8, 16)
 bool dgemm_splitk_ok(int splitk);
@@ -145,6 +154,7 @@ struct PGemmArgs {
   const int* offs;  // grouped: [groups] cumulative row ends (device)
   int groups;       // 0 = dense
   int M, N, K, ldx, ldy;
+  int stagger;      // unit body: workgroups start their K loops at decorrelated offsets
 };
 bool pgemm_supported(int M, int N, int K);
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st);

@@ -64,6 +64,7 @@ __global__ __launch_bounds__(256, 1) void kgemm_kernel(DGemmArgs p) {
   const int tn = lt / tiles_m, tm = lt % tiles_m;  // a column tile's row tiles share an XCD
   const int m0 = tm * BM, n0 = tn * KBN;
   const int nst = p.K / KST;
+  const int st0 = gemm_stagger0(p.stag, tm, tn, nst);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const bf16* X = static_cast<const bf16*>(p.X);
@@ -88,7 +89,9 @@ __global__ __launch_bounds__(256, 1) void kgemm_kernel(DGemmArgs p) {
   }
   auto issue = [&](int st) {
     bf16x8* slot = lds + (st % KNS) * SU;
-    const int k0 = st * KST;
+    int ks = st + st0;
+    if (ks >= nst) ks -= nst;
+    const int k0 = ks * KST;
 #pragma unroll
     for (int i = 0; i < G; ++i) {
       // instruction (w, i) stages rows 2 (w G + i) and + 1: X rows below BM, weight rows above

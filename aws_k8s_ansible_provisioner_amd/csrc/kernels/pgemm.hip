@@ -424,7 +424,7 @@ template <bool SILU_ROWS, typename ACC>
 __device__ __forceinline__ void pg_mainloop_u(bf16x8* lds, const __amdgpu_buffer_rsrc_t rx,
                                               const __amdgpu_buffer_rsrc_t rw, int ldx, int K,
                                               int nhalf, int m0, int n0, int ku0, int nu,
-                                              ACC& accs) {
+                                              int st0, ACC& accs) {
   auto& acc = accs.v;  // [8][8]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -453,7 +453,11 @@ __device__ __forceinline__ void pg_mainloop_u(bf16x8* lds, const __amdgpu_buffer
     // units past the end are issued too (no branch in the pipelined body) with a scalar
     // offset past every descriptor's range: the buffer unit drops them without a memory
     // access (the slot they land in is never read again)
-    const uint32_t kb = u < nu ? (uint32_t)((ku0 + u) * 32 * 2) : 0x7fff0000u;
+    // st0: this workgroup's K start ("StaggerU"): units are visited from st0, wrapping, so
+    // workgroups sharing an operand panel do not request the same lines at the same time
+    int ku = u + st0;
+    if (ku >= nu) ku -= nu;
+    const uint32_t kb = u < nu ? (uint32_t)((ku0 + ku) * 32 * 2) : 0x7fff0000u;
 #if defined(__HIP_DEVICE_COMPILE__)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(e < 4 ? rx : rw,
                                              (__attribute__((address_space(3))) void*)dst, 16,
@@ -559,7 +563,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void pgemm_kernel(PGemmArgs p) {
   auto& acc = accs.v;
   if constexpr (SCHED == 3) {
     static_assert(WAVES == 4, "the unit-pipelined body is the 4-wave 128 x 128 form");
-    pg_mainloop_u<EPI == EPI_SILU>(lds, rx, rw, p.ldx, p.K, p.N >> 1, m0, n0, 0, p.K / 32,
+    const int nu = p.K / 32;
+    const int id = (int)blockIdx.x;  // decorrelate ids that share an X panel (id, id + 8) and
+    const int h = (id ^ (id >> 3)) & 7;  // those that share a W panel (consecutive ids)
+    const int st0 = p.stagger ? (h * nu) / 8 : 0;
+    pg_mainloop_u<EPI == EPI_SILU>(lds, rx, rw, p.ldx, p.K, p.N >> 1, m0, n0, 0, nu, st0,
                                    accs);
   } else {
     pg_mainloop<NB, EPI == EPI_SILU, WAVES, decltype(accs), SCHED>(lds, rx, rw, p.ldx, p.K,
@@ -888,7 +896,13 @@ void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
   const int grid = p.groups > 0 ? ((p.M + PG_T - 1) / PG_T + p.groups) * tiles_n
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
   if (pgemm_sched() == 3 && p.K % 128 == 0) {  // unit-pipelined 4-wave body (K >= 128)
-    launch_pgemm_w<4, 3>(p, epi, grid, st);
+    static const int stag = [] {
+      const char* e = getenv("AKAP_PGEMM_STAGGER");
+      return e ? atoi(e) : 0;
+    }();
+    PGemmArgs q = p;
+    q.stagger = stag;
+    launch_pgemm_w<4, 3>(q, epi, grid, st);
     return;
   }
   // two barriers per K tile (measured 1-4 % faster than four, profiles/r4_pgemm_nb_ab.log); the

@@ -415,6 +415,7 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   }
   akap::DGemmArgs a{};
   a.ntw = akap::weight_nt_default();
+  a.stag = akap::gemm_stagger_default();
   a.X = x.data_ptr();
   a.W = w.data_ptr();
   a.Y = out.data_ptr();
@@ -503,6 +504,7 @@ void kgemm(Tensor out, Tensor x, Tensor w, int64_t bm, int64_t epi, double eps,
               "kgemm: aligned rows");
   akap::DGemmArgs a{};
   a.ntw = akap::weight_nt_default();
+  a.stag = akap::gemm_stagger_default();
   a.X = x.data_ptr(); a.W = w.data_ptr(); a.Y = out.data_ptr();
   a.M = M; a.N = N; a.K = K;
   a.ldx = x.stride(0); a.ldw = w.stride(0); a.ldy = out.stride(0);

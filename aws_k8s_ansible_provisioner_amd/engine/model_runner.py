@@ -39,6 +39,10 @@ DECODE_FIELDS = ("input_ids", "positions", "slots", "seeds", "seq_lens", "temper
                  "top_k", "steps", "src_rows", "tail_slot")
 
 
+# fault injection (tests/test_tp_gpu.py): a TP follower that skips its N-th decode replay, so
+# its peers' custom collectives time out inside a replayed graph
+_FAULT_SKIP_REPLAY = int(os.environ.get("AKAP_FAULT_SKIP_REPLAY", "0"))
+
 class ModelRunner:
     def __init__(self, ecfg: EngineConfig, mcfg: ModelConfig,
                  pstate: Optional[ParallelState] = None, log=print):
@@ -255,6 +259,7 @@ class ModelRunner:
         self._pending_err = None
         self._follower_err: list = []
         self._follower_slot = 0
+        self._replays = 0
         self.out_logprobs = torch.zeros(S, dtype=torch.float32, device=self.device)
         self.workspace = ops.decode_workspace(S, self.model.hkv, self.G, self.num_parts,
                                               self.device)
@@ -633,8 +638,10 @@ class ModelRunner:
             if b >= B:
                 n, graph = b, self.graphs[b]
                 break
+        self._replays += 1
         if graph is not None:
-            graph.replay()
+            if self._replays != _FAULT_SKIP_REPLAY:  # fault injection (tests): skip one step
+                graph.replay()
         else:
             self._decode_body(n)
         if self.is_gpu and self.ps.car is not None:

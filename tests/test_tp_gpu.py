@@ -133,3 +133,58 @@ def test_tp4_llama70b_widths_captured_on_one_gpu():
             row = logits[len(p) - 1 + i]
             gap = float((row.max() - row[t]) / (row.std() + 1e-6))
             assert gap <= 0.15, (p[:4], i, t, gap)
+
+
+CHILD_FAULT = r"""
+import json, os, sys
+import torch
+sys.path.insert(0, os.environ["ROOT"])
+from aws_k8s_ansible_provisioner_amd.engine.config import EngineConfig, SamplingParams
+from aws_k8s_ansible_provisioner_amd.parallel.comm import CollectiveTimeout
+from aws_k8s_ansible_provisioner_amd.parallel.tp_worker import make_tp_engine
+ecfg = EngineConfig(model="tiny-llama", device="cuda", max_model_len=256, max_num_seqs=8,
+                    max_num_batched_tokens=64, block_size=32, num_gpu_blocks=96,
+                    tensor_parallel_size=2, shard_init="full", init_std=0.15)
+try:
+    eng, bc = make_tp_engine(ecfg, backend="gloo", log=lambda *a: None)
+except CollectiveTimeout as e:  # the follower may notice the sticky word first
+    print("FOLLOWER " + type(e).__name__, flush=True)
+    os._exit(3)
+if eng is not None:
+    assert eng.runner.graphs, "decode graphs were not captured"
+    got = []
+    try:
+        outs = eng.generate(None, SamplingParams(max_tokens=24, temperature=0, ignore_eos=True),
+                            prompt_ids=[list(range(5, 40)), [100, 101]])
+        got = [o.output_ids for o in outs]
+        print("RESULT " + json.dumps(got), flush=True)
+    except CollectiveTimeout as e:
+        print("FAULT " + type(e).__name__ + " " + str(e)[:80], flush=True)
+    os._exit(0)  # the follower is left waiting for a header: the test ends it
+"""
+
+
+def test_collective_timeout_in_replayed_graph_fails_the_step():
+    """rank 1 of a captured TP=2 decode skips one graph replay (fault
+    injection), so rank 0's custom all-reduce waits inside its replayed graph time out and only
+    set the kernels' sticky error word.  The runner's host check of that word (copied to pinned
+    memory behind the step) must fail the step with CollectiveTimeout instead of returning its
+    tokens."""
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, ROOT=ROOT, RANK=str(r), WORLD_SIZE="2", AKAP_MOE_MODE="tp",
+                   AKAP_CUSTOM_AR_GLOO="1", AKAP_GEMM_TUNE="0", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if r == 1:
+            env["AKAP_FAULT_SKIP_REPLAY"] = "3"
+        procs.append(subprocess.Popen([sys.executable, "-c", CHILD_FAULT], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        out0, err0 = procs[0].communicate(timeout=240)
+    finally:
+        procs[1].kill()
+        procs[1].communicate(timeout=60)
+    assert procs[0].returncode == 0, err0[-3000:]
+    assert "FAULT CollectiveTimeout" in out0, (out0[-2000:], err0[-2000:])
+    assert "RESULT" not in out0

@@ -44,6 +44,7 @@ struct Args {
   unsigned* out;
   int map;  // 0: xcd_remap (a column tile's row tiles on one XCD), 1: identity
   int op;   // 0: X and W rows, 1: X rows only (both halves from X), 2: W rows only
+  int stag; // 1: each workgroup walks K from stage (blockIdx.x % stages), wrapping ("StaggerU")
 };
 
 __device__ __forceinline__ int tile_id(const Args& a, int nwg) {
@@ -118,12 +119,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_c(Args a) {
     const int row = u / cpr, ch = u % cpr;
     src[i] = src_row(a, row, m0, n0) + ch * 8;
   }
+  const int st0 = a.stag ? (int)(blockIdx.x % nst) : 0;
   auto issue = [&](int st) {
     u32x4* slot = ring + (st % NS) * units;
+    int ks = st + st0;
+    if (ks >= nst) ks -= nst;
 #pragma unroll
     for (int i = 0; i < P; ++i)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src[i] + (size_t)st * a.KST),
+          (const __attribute__((address_space(1))) void*)(src[i] + (size_t)ks * a.KST),
           (__attribute__((address_space(3))) void*)(slot + (w * P + i) * 64), 16, 0, 0);
   };
   unsigned acc = 0;
@@ -161,10 +165,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_reg(Args a) {
   }
   u32x4 acc = {0, 0, 0, 0};
   u32x4 buf[D][P];
+  const int st0 = a.stag ? (int)(blockIdx.x % nst) : 0;
+  auto ko = [&](int st) { int k = st + st0; if (k >= nst) k -= nst; return (size_t)k * a.KST / 8; };
 #pragma unroll
   for (int s = 0; s < D; ++s)
 #pragma unroll
-    for (int i = 0; i < P; ++i) buf[s][i] = s < nst ? src[i][(size_t)s * a.KST / 8] : acc;
+    for (int i = 0; i < P; ++i) buf[s][i] = s < nst ? src[i][ko(s)] : acc;
   for (int t = 0; t < nst; t += D) {
 #pragma unroll
     for (int s = 0; s < D; ++s) {
@@ -172,7 +178,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_reg(Args a) {
       for (int i = 0; i < P; ++i) acc ^= buf[s][i];
       if (t + s + D < nst) {
 #pragma unroll
-        for (int i = 0; i < P; ++i) buf[s][i] = src[i][(size_t)(t + s + D) * a.KST / 8];
+        for (int i = 0; i < P; ++i) buf[s][i] = src[i][ko(t + s + D)];
       }
     }
   }
@@ -207,12 +213,12 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  printf("shape,tile,kst,ns,waves,path,map,op,weights,us,bytes_per_cu_KB,GBps_per_cu,wgs\n");
+  printf("shape,tile,kst,ns,waves,path,map,op,stag,weights,us,bytes_per_cu_KB,GBps_per_cu,wgs\n");
   auto run = [&](const char* nm, const Shape& s, int BM, int BN, int KST, int NS, int waves,
-                 const char* path, int map, int op, auto launch) {
+                 const char* path, int map, int op, int stag, auto launch) {
     char key[128];
-    snprintf(key, sizeof key, "%s,%dx%d,%d,%d,%d,%s,%d,%d", nm, BM, BN, KST, NS, waves, path,
-             map, op);
+    snprintf(key, sizeof key, "%s,%dx%d,%d,%d,%d,%s,%d,%d,%d", nm, BM, BN, KST, NS, waves,
+             path, map, op, stag);
     if (filt && strncmp(key, filt, strlen(filt)) != 0) return;
     const int wgs = (M / BM) * (s.N / BN);
     const double per_cu = (double)(BM + BN) * s.K * 2;
@@ -247,16 +253,17 @@ int main(int argc, char** argv) {
       const int units = (t.BM + t.BN) * t.KST / 8;
       const int pieces = units / 64;
       for (int map = 0; map < 2; ++map)
-        for (int op = 0; op < 3; ++op) {
+        for (int op = 0; op < 3; ++op)
+        for (int stag = 0; stag < 2; ++stag) {
           for (int NS : {4}) {
             const size_t lds = (size_t)NS * units * 16;
             if (lds > 160 * 1024) continue;
-            Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, NS, out, map, op};
+            Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, NS, out, map, op, stag};
             if (pieces % 4 == 0) {
               const int P = pieces / 4;
 #define CASE(PP, NN)                                                                   \
   if (P == PP && NS == NN)                                                             \
-    run(s.name, s, t.BM, t.BN, t.KST, NS, 4, "lds_counted", map, op,                   \
+    run(s.name, s, t.BM, t.BN, t.KST, NS, 4, "lds_counted", map, op, stag,             \
         [&](int wgs) { k_ingress_c<4, PP, NN><<<wgs, 256, lds, 0>>>(a); });
               CASE(4, 4) CASE(8, 4) CASE(6, 4) CASE(5, 4) CASE(10, 4) CASE(12, 4)
 #undef CASE
@@ -264,10 +271,10 @@ int main(int argc, char** argv) {
           }
           if (pieces % 4 == 0) {
             const int P = pieces / 4;
-            Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, 0, out, map, op};
+            Args a{X, W, M, s.N, s.K, t.BM, t.BN, t.KST, 0, out, map, op, stag};
 #define RCASE(PP, DD)                                                                    \
   if (P == PP)                                                                           \
-    run(s.name, s, t.BM, t.BN, t.KST, DD, 4, "reg", map, op,                             \
+    run(s.name, s, t.BM, t.BN, t.KST, DD, 4, "reg", map, op, stag,                       \
         [&](int wgs) { k_ingress_reg<4, PP, DD><<<wgs, 256, 0, 0>>>(a); });
             RCASE(4, 2) RCASE(8, 2) RCASE(6, 2) RCASE(5, 2) RCASE(10, 2) RCASE(12, 2)
 #undef RCASE
