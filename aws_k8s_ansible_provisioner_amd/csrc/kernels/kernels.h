@@ -155,6 +155,7 @@ struct PGemmArgs {
   int groups;       // 0 = dense
   int M, N, K, ldx, ldy;
   int stagger;      // unit body: workgroups start their K loops at decorrelated offsets
+  int gm;           // raster: M tiles per block of the tile map (0 = 8)
 };
 bool pgemm_supported(int M, int N, int K);
 void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st);

@@ -122,7 +122,7 @@ using H3 = HalfTile<3>;  // A rows of the bottom quadrants
 template <bool GROUPED>
 __device__ __forceinline__ bool pg_tile(const PGemmArgs& p, int& tm, int& tn, int& group,
                                         int& row_lo, int& row_hi) {
-  constexpr int GM = 8;
+  const int GM = p.gm > 0 ? p.gm : 8;
   const int tiles_n = p.N / PG_T;
   const int nwg = gridDim.x;
   const int id = xcd_remap(blockIdx.x, nwg);
@@ -890,8 +890,14 @@ static void launch_pgemm_w(const PGemmArgs& p, int epi, int grid, hipStream_t st
   }
 }
 
-void launch_pgemm(const PGemmArgs& p, int epi, hipStream_t st) {
-  if (p.M == 0) return;
+void launch_pgemm(const PGemmArgs& a, int epi, hipStream_t st) {
+  if (a.M == 0) return;
+  static const int gm = [] {  // raster block height (AKAP_PGEMM_GM, A/B knob; default 8)
+    const char* e = getenv("AKAP_PGEMM_GM");
+    return e ? atoi(e) : 0;
+  }();
+  PGemmArgs p = a;
+  p.gm = gm;
   const int tiles_n = p.N / PG_T;
   const int grid = p.groups > 0 ? ((p.M + PG_T - 1) / PG_T + p.groups) * tiles_n
                                  : ((p.M + PG_T - 1) / PG_T) * tiles_n;
