@@ -23,6 +23,9 @@
 //    waits on the prologue's cache stores (profiles/r3_attn_rework_ab.log,
 //    r3_attn_fused_breakdown.log).
 //  * Prefill: grid (q-tile, kv_head); each wave walks the causal range of its rows.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -626,16 +629,27 @@ __device__ __forceinline__ void fa_glds16(const void* g, void* lds_wave_base) {
 // the per-lane DMA source address (the LDS destination of a DMA is lane-linear).
 // NW = waves per workgroup (4: 128 q rows, two workgroups per CU; 8: 256 q rows, one
 // workgroup per CU -- every staged K/V tile feeds twice the rows).
-template <bool F8, bool GL, int NW = 4>
+// STAG (8 waves only): the compute/load ping-pong of the two waves that share a SIMD.  Waves
+// 0-3 and 4-7 land on the same four SIMDs (one of each per SIMD) and run the same program in
+// lock-step between the per-tile barriers, so both do their Q K^T MFMAs, then both their
+// softmax VALU (the matrix pipe idle), then both their P V MFMAs.  With STAG the late half
+// (waves 4-7) defers tile t's P V MFMAs past the next barrier: per SIMD one wave's P V(t-1)
+// then Q K^T(t) run beside the other's Q K^T(t) then softmax(t) -- matrix work beside VALU
+// work (MI355X_MICROARCH.md "Two waves per SIMD" item 9).  The deferred P V re-reads V(t) from
+// LDS, so the ring has THREE buffers (tile t's survives until the barrier of t + 2); only the
+// bf16 P fragments and the rescale factor stay in registers (+17 VGPRs).
+template <bool F8, bool GL, int NW = 4, bool STAG = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(AttnParams p) {
   constexpr int ROWS = 32 * NW;
   constexpr int NT = 64 * NW;    // threads
   constexpr int PW = 16 / NW;    // 1-KiB K (and V) DMA pieces per wave per tile
+  constexpr int NBUF = STAG ? 3 : 2;
   static_assert(NW == 4 || (NW == 8 && GL), "the register-staged path assumes 256 threads");
-  // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB + the block ids of the first
-  // kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 2 * kFaKeys * kD + 2 * kFaBtCache];
-  int* bt_s = reinterpret_cast<int*>(lds + 2 * 2 * kFaKeys * kD);
+  static_assert(!STAG || (NW == 8 && GL), "the ping-pong pairs waves w and w + 4");
+  // [buf][K | V][64 keys * 128 dims] bf16 = 64 KiB (96 KiB with STAG) + the block ids of the
+  // first kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
+  __shared__ __attribute__((aligned(16))) bf16 lds[NBUF * 2 * kFaKeys * kD + 2 * kFaBtCache];
+  int* bt_s = reinterpret_cast<int*>(lds + NBUF * 2 * kFaKeys * kD);
   // causal work grows with a tile's position: dispatch the map back to front so the
   // longest tiles start first and the grid's tail is made of short ones
   const int tile = gridDim.x - 1 - blockIdx.x;
@@ -841,22 +855,56 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
 #pragma unroll
     for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
+  // STAG, late waves: tile t-1's P fragments and rescale, applied after the next barrier
+  bf16x8 pd[2][2];
+  float alpha_d = 1.f;
+  bool resc_d = false, pend = false;
+  // the deferred O^T += V^T P^T of tile tp (its V still in LDS buffer tp % NBUF)
+  auto deferred_pv = [&](int tp) {
+    if (resc_d) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha_d;
+    }
+    const bf16* vlp = lds + (size_t)(tp % NBUF) * 2 * kFaKeys * kD + kFaKeys * kD;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 v4[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          v4[dt] = *reinterpret_cast<const bf16x8*>(vlp + ((4 * k + 2 * s2 + h) * kD + 32 * dt + r) * 8);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v4[dt], pd[k][s2], oacc[dt], 0, 0, 0);
+      }
+    pend = false;
+  };
+  // the K/V loop, instantiated once per wave role: the early and late STAG paths keep
+  // different registers live across the barrier, so one runtime-branching loop would have to
+  // hold both sets (it spilled); two loops let each keep only its own
+  auto kv_loop = [&](auto late_c) {
+  constexpr bool late = decltype(late_c)::value;
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
+    const int buf = STAG ? t % NBUF : (t & 1);
     const bool more = t + 1 < ntiles;
     if constexpr (GL) {
       // tile t (issued one iteration ago) landed for this wave; every wave's LDS reads of
-      // buffer buf^1 (tile t-1) are done -> after the barrier it may be refilled
+      // the buffer tile t+1 goes into (tile t-1, or t-2 with STAG) are done -> after the
+      // barrier it may be refilled
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (more) {
-        stage_glds(t + 1, buf ^ 1, blk_next);
+        stage_glds(t + 1, STAG ? (t + 1) % NBUF : (buf ^ 1), blk_next);
         blk_next = blk_of(t + 2);
       }
     } else {
       if (more) stage_load(t + 1);
     }
+    if (late && pend) deferred_pv(t - 1);
     const int key0 = t * kFaKeys;
     if (wave_active && key0 <= w_limit) {
       const bf16* kl = lds + (size_t)buf * 2 * kFaKeys * kD;
@@ -884,15 +932,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
         for (int k = 0; k < 2; ++k)
           sacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s8][k], qf[s8], sacc[k], 0, 0, 0);
       // likewise the V^T fragments: requested now, their latency hides under the softmax
+      // (late STAG waves re-read them when their deferred P V runs)
       bf16x8 vf[2][2][4];
+      if (!late) {
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < 2; ++k)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
+          for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt)
-            vf[k][s2][dt] = *reinterpret_cast<const bf16x8*>(
-                vl + ((4 * k + 2 * s2 + h) * kD + 32 * dt + r) * 8);
+            for (int dt = 0; dt < 4; ++dt)
+              vf[k][s2][dt] = *reinterpret_cast<const bf16x8*>(
+                  vl + ((4 * k + 2 * s2 + h) * kD + 32 * dt + r) * 8);
+      }
       // causal mask (wave-uniform branch: only tiles that cross this wave's diagonal pay for
       // it) and the running max on the raw scores -- the log2-domain scale is positive, so
       // it commutes with max and folds into the exponent's FMA below
@@ -928,6 +979,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
         }
       const float rs = xor32_sum((rsp[0] + rsp[1]) + (rsp[2] + rsp[3]));
       l_run = l_run * alpha + rs;
+      if (late) {  // P V of this tile after the next barrier (deferred_pv)
+        resc_d = __any(m_new != m_run);
+        alpha_d = alpha;
+        m_run = m_new;
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pd[k][s2][j] = f2bf(sacc[k][8 * s2 + j]);
+        pend = true;
+        continue;
+      }
       // rescale only when some row's running max moved (alpha == 1 exactly otherwise): past
       // the first tiles of a causal row the max rarely changes
       if (__any(m_new != m_run)) {
@@ -957,6 +1021,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
       if (more) stage_store(buf ^ 1);
       __syncthreads();
     }
+  }
+  if (late && pend) deferred_pv(ntiles - 1);
+  };
+  if constexpr (STAG) {
+    if (w >= 4) kv_loop(std::true_type{});
+    else kv_loop(std::false_type{});
+  } else {
+    kv_loop(std::false_type{});
   }
   // O^T accumulator of lane (r, h): row r's dims 32 dt + 8 j4 + 4 h + (0..3).  Each pair of
   // 8-dim groups (j4 = 2 kp, 2 kp + 1) is exchanged between the lane halves with two
@@ -1024,8 +1096,15 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows
                                hipStream_t s) {
   if (num_tiles == 0) return;
   const dim3 grid(num_tiles, p.Hkv);
-  if (tile_rows == 2 * kFaRows && !p.kv_fp8)  // 256 rows, 8 waves (bf16 caches)
-    paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(p);
+  // AKAP_PREFILL_STAGGER=1: the 8-wave kernel's compute/load ping-pong (STAG above)
+  static const bool stag = [] {
+    const char* e = std::getenv("AKAP_PREFILL_STAGGER");
+    return e != nullptr && std::atoi(e) == 1;
+  }();
+  if (tile_rows == 2 * kFaRows && !p.kv_fp8) {  // 256 rows, 8 waves (bf16 caches)
+    if (stag) paged_attn_prefill_fa_kernel<false, true, 8, true><<<grid, 512, 0, s>>>(p);
+    else paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(p);
+  }
   else if (p.kv_fp8)  // fp8 caches: register-staged (widened to bf16 on the way into LDS)
     paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
   else  // bf16 caches: LDS-DMA staging

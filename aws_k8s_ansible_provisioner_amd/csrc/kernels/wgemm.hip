@@ -165,6 +165,134 @@ __global__ __launch_bounds__(512, 2) void wgemm_kernel(WGemmArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Wide form for 129..256 rows: 256 x 256 tiles.  The LM head at M = 256 is bound by the L2 ->
+// CU traffic of all workgroups together (~9 TB/s chip-wide for decode-GEMM tile streams,
+// profiles/r6_decode_gemm_ingress.md), and with 256 x 128 tiles two thirds of that traffic is
+// the 512 KB activation block re-read by every one of the 1,187 column tiles (911 MB per call
+// for Qwen3-0.6B = the measured ~101 us).  256-wide tiles halve the re-reads (594 tiles, 594 MB).
+// 8 waves as 4 (M) x 2 (N), wave tile 64 x 128 (128 accumulator registers); 32-deep k-steps
+// (rows of 64 B, chunk c stored at c ^ g((row >> 2) & 3), g = {0, 2, 3, 1}: conflict-free for
+// ds_read_b128 fragment reads, see pgemm.hip pu_swz) through a 4-slot ring of 32 KB, three
+// k-steps in flight; one DMA instruction = 16 rows x 64 B.
+__device__ __forceinline__ int ww_swz(int row, int c) {
+  return row * 4 + (c ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3));
+}
+
+template <bool NTW>
+__global__ __launch_bounds__(512, 1) void wgemm_wide_kernel(WGemmArgs p) {
+  constexpr int BM = 256, BN = 256, BK = 32, NS = 4;
+  constexpr int SU = (BM + BN) * 4;             // 16-B units per slot (32 KB)
+  constexpr int GA = BM / 16 / 8, GW = BN / 16 / 8;  // DMA instructions per wave per k-step
+  constexpr int G = GA + GW;
+  constexpr int WC = 128, JN = 8, EP = WC + 8;  // wave tile 64 x 128; epilogue row pitch
+  constexpr int RING = NS * SU, EPI_UNITS = 8 * 64 * EP / 8;
+  __shared__ bf16x8 lds[RING > EPI_UNITS ? RING : EPI_UNITS];
+
+  const int tn = blockIdx.x;
+  const int n0 = tn * BN;
+  const int nk = p.K / BK;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const bf16* X = static_cast<const bf16*>(p.X);
+  const bf16* W = static_cast<const bf16*>(p.W);
+  // lane -> row lane / 4 of the instruction's 16, LDS chunk lane % 4 holding logical chunk
+  // (lane % 4) ^ g((row >> 2) & 3) (instructions start on multiples of 16 rows)
+  const int lr = lane >> 2;
+  const int lc = (lane & 3) ^ ((0x1320 >> (4 * ((lr >> 2) & 3))) & 3);
+  const bf16* asrc[GA];
+  const bf16* wsrc[GW];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int row = (w * GA + i) * 16 + lr;
+    asrc[i] = X + (size_t)(row < p.M ? row : 0) * p.ldx + lc * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < GW; ++i) {
+    const int v = n0 + (w * GW + i) * 16 + lr;
+    wsrc[i] = W + (size_t)(v < p.N ? v : 0) * p.ldw + lc * 8;
+  }
+  auto issue = [&](int step) {
+    bf16x8* slot = lds + (step % NS) * SU;
+    const int k0 = step * BK;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) wglds16(asrc[i] + k0, slot + (w * GA + i) * 64);
+#pragma unroll
+    for (int i = 0; i < GW; ++i)
+      wglds16<NTW ? 2 : 0>(wsrc[i] + k0, slot + BM * 4 + (w * GW + i) * 64);
+  };
+
+  f32x4 acc[4][JN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s);
+  for (int t = 0; t < nk; ++t) {
+    // retire step t (steps t+1, t+2 stay in flight when they exist)
+    if (t + 2 < nk) wwait_vm<2 * G>();
+    else if (t + 1 < nk) wwait_vm<G>();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMAs of step t landed; slot t-1 is free
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    const bf16x8* slot = lds + (t % NS) * SU;
+    bf16x8 af[4], bfr[JN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = slot[ww_swz(wm * 64 + i * 16 + fr, fg)];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) bfr[j] = slot[BM * 4 + ww_swz(wn * WC + j * 16 + fr, fg)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+
+  // ---- epilogue: as wgemm_kernel (wave tile through LDS, 16-byte row-segment stores) ----
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  bf16* et = reinterpret_cast<bf16*>(lds) + (size_t)w * 64 * EP;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) et[(i * 16 + fg * 4 + r) * EP + j * 16 + fr] = f2bf(acc[i][j][r]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bf16* Y = static_cast<bf16*>(p.Y);
+  constexpr int CPR = WC / 8;
+  for (int e = lane; e < 64 * CPR; e += 64) {
+    const int rr = e / CPR, cc = e % CPR;
+    const int row = wm * 64 + rr;
+    const int col = n0 + wn * WC + cc * 8;
+    if (row >= p.M || col >= p.N) continue;
+    const bf16* src = et + rr * EP + cc * 8;
+    bf16* dst = Y + (size_t)row * p.ldy + col;
+    if (col + 8 <= p.N) {
+      bf16x8 v;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = src[q];
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    } else {
+      for (int q = 0; q < p.N - col; ++q) dst[q] = src[q];
+    }
+  }
+}
+
+// AKAP_WGEMM_WIDE: 1 -> the 256 x 256 form for 129..256 rows (K % 32 == 0), 0 -> 256 x 128
+static int wgemm_wide() {
+  static const int v = [] {
+    const char* e = std::getenv("AKAP_WGEMM_WIDE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 int wgemm_rows(int M) { return M <= 64 ? 1 : (M <= 128 ? 2 : 4); }
 
 bool wgemm_supported(int M, int N, int K, int ldx, int ldw, int ldy) {
@@ -184,6 +312,12 @@ void launch_wgemm(const WGemmArgs& p, hipStream_t st) {
     const char* e = std::getenv("AKAP_WGEMM_NT");
     return e == nullptr || std::atoi(e) != 0;
   }();
+  if (wmr == 4 && p.M <= 256 && wgemm_wide() == 1 && p.K % 32 == 0) {
+    const dim3 gw((p.N + 255) / 256);
+    if (nt) wgemm_wide_kernel<true><<<gw, 512, 0, st>>>(p);
+    else wgemm_wide_kernel<false><<<gw, 512, 0, st>>>(p);
+    return;
+  }
   switch (wmr) {
     case 1: if (nt) wgemm_kernel<1, true><<<grid, 512, 0, st>>>(p); else wgemm_kernel<1><<<grid, 512, 0, st>>>(p); break;
     case 2: if (nt) wgemm_kernel<2, true><<<grid, 512, 0, st>>>(p); else wgemm_kernel<2><<<grid, 512, 0, st>>>(p); break;
