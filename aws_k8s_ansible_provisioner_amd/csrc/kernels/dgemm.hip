@@ -37,13 +37,19 @@
 namespace akap {
 
 constexpr int DBM = 64, DBN = 64, DBK = 64;
+constexpr int kDgSc1 = 16;  // buffer op cache bits: sc1 (write-through stores, L1-bypass loads)
 
 __device__ __forceinline__ int dswz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
 __device__ __forceinline__ float silu_bf(float g) { return bf2f(f2bf(g / (1.f + __expf(-g)))); }
 
-template <int PRO, int EPI, int PF, bool SPLIT>
+// SPL: 0 whole K, 1 fp32 partial slabs for the separate reduce pass, 2 in-launch combine of
+// the S slices (plain prologue only): fragment-native sc1 slabs + a per-tile last-arriver ticket,
+// as gdgemm.hip SPL 2 -- the reduce launch (5.0 us at Qwen3 down, M = 256) and its kernel
+// boundary go away (VERDICT r5 "Step A")
+template <int PRO, int EPI, int PF, int SPL, int S = 1>
 __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
+  static_assert(SPL != 2 || PRO == PRO_PLAIN, "in-launch combine: plain prologue");
   // ONE __shared__ object (a second one makes hipcc drain vmcnt inside the k-loop,
   // cdna_hip_programming.md "Projection GEMM at M = 256" item 4a):
   // [buf 2][A|B][64 rows * 8 chunks] bf16x8, then 64 fp32 row sums of squares
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
   // (no per-load "ss_in or 0" select: hipcc would branch around each load and wait on it --
   // without ss_in the loads read valid W bytes and the epilogue ignores them; host-checked)
   const float* ssp = p.ss_in != nullptr ? p.ss_in : static_cast<const float*>(p.W);
-  if constexpr (!SPLIT) {
+  if constexpr (SPL != 1) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -224,6 +230,51 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
     mfma(buf);
   }
 
+  if constexpr (SPL == 2) {
+    // ---- in-launch split-K combine (gdgemm.hip header, SPL 2) ----
+    constexpr int NF = 4;  // f32x4 fragments per lane
+    const int ntiles = tiles_n * tiles_m;
+    constexpr size_t tile_stride = (size_t)NF * 256;
+    const size_t zs = (size_t)ntiles * tile_stride;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        p.ws, (short)0, (int)((size_t)S * zs * 16), 0x00020000);
+    const size_t mine = ((size_t)kz * ntiles + lt) * tile_stride + tid;  // f32x4 units
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[f >> 1][f & 1]), rs,
+                                             (int)((mine + (size_t)f * 256) * 16), 0, kDgSc1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(rowss);  // the plain prologue leaves rowss unused
+    if (tid == 0) {
+      int* ticket = p.counters + (size_t)lt * kCtrStride;
+      const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == S - 1;
+      if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+    // all S slabs (own included), every load issued before any sum; sc1 loads bypass the
+    // per-XCD caches a slice on another XCD could not have written through
+    const size_t t0 = (size_t)lt * tile_stride + tid;
+    f32x4 v[S][NF];
+#pragma unroll
+    for (int z = 0; z < S; ++z)
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        v[z][f] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                       rs, (int)((t0 + (size_t)z * zs + (size_t)f * 256) * 16), 0, kDgSc1));
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      f32x4 s = v[0][f];
+#pragma unroll
+      for (int z = 1; z < S; ++z) s += v[z][f];
+      acc[f >> 1][f & 1] = s;
+    }
+  }
   if constexpr (PRO == PRO_ADDNORM) {
     // 8 consecutive lanes share a staging row: wave-local butterfly, then one LDS slot/row
 #pragma unroll
@@ -234,7 +285,7 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
       v += __shfl_xor(v, 4, kWave);
       if ((tid & 7) == 0) {
         rowss[s_row[c]] = v;
-        if (SPLIT && tn == 0 && a_ok[c])
+        if (SPL == 1 && tn == 0 && a_ok[c])
           p.ws[(size_t)gridDim.y * p.M * p.N + (size_t)kz * p.M + m0 + s_row[c]] = v;
       }
     }
@@ -249,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(DGemmArgs p) {
       const int lrow = wm * 32 + i * 16 + fg * 4 + r;
       const int row = m0 + lrow;
       const bool row_ok = row < p.M;
-      if constexpr (SPLIT) {
+      if constexpr (SPL == 1) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int col = n0 + wn * 32 + j * 16 + fr;
@@ -374,29 +425,33 @@ bool dgemm_epi_supported(int N, int epi, int splitk) {
   return true;
 }
 
-template <int PRO, int EPI, bool SPL>
+template <int PRO, int EPI, int SPL, int S = 1>
 static void dgemm_pf(const DGemmArgs& p, dim3 grid, int pf, hipStream_t st) {
   switch (pf) {
     case 8:  // deepest ring: plain operand only (the prologue forms would exceed 256 VGPRs)
-      if constexpr (PRO == PRO_PLAIN) dgemm_kernel<PRO, EPI, 8, SPL><<<grid, 256, 0, st>>>(p);
-      else dgemm_kernel<PRO, EPI, 4, SPL><<<grid, 256, 0, st>>>(p);
+      if constexpr (PRO == PRO_PLAIN) dgemm_kernel<PRO, EPI, 8, SPL, S><<<grid, 256, 0, st>>>(p);
+      else dgemm_kernel<PRO, EPI, 4, SPL, S><<<grid, 256, 0, st>>>(p);
       break;
-    case 4: dgemm_kernel<PRO, EPI, 4, SPL><<<grid, 256, 0, st>>>(p); break;
-    case 2: dgemm_kernel<PRO, EPI, 2, SPL><<<grid, 256, 0, st>>>(p); break;
-    default: dgemm_kernel<PRO, EPI, 1, SPL><<<grid, 256, 0, st>>>(p); break;
+    case 4: dgemm_kernel<PRO, EPI, 4, SPL, S><<<grid, 256, 0, st>>>(p); break;
+    case 2: dgemm_kernel<PRO, EPI, 2, SPL, S><<<grid, 256, 0, st>>>(p); break;
+    default: dgemm_kernel<PRO, EPI, 1, SPL, S><<<grid, 256, 0, st>>>(p); break;
   }
 }
 
-template <bool SPL>
+template <int SPL, int S = 1>
 static void dgemm_main(const DGemmArgs& p, dim3 grid, int pro, int epi, int pf, hipStream_t st) {
-  if (pro == PRO_ADDNORM) {
+  if constexpr (SPL == 2) {  // in-launch combine: plain prologue, every epilogue
+    if (epi == EPI_RESNORM) dgemm_pf<PRO_PLAIN, EPI_RESNORM, 2, S>(p, grid, pf, st);
+    else if (epi == EPI_SILU) dgemm_pf<PRO_PLAIN, EPI_SILU, 2, S>(p, grid, pf, st);
+    else dgemm_pf<PRO_PLAIN, EPI_STORE, 2, S>(p, grid, pf, st);
+  } else if (pro == PRO_ADDNORM) {
     dgemm_pf<PRO_ADDNORM, EPI_STORE, SPL>(p, grid, pf, st);
   } else if (pro == PRO_SILU) {
     dgemm_pf<PRO_SILU, EPI_STORE, SPL>(p, grid, pf, st);
   } else if (epi == EPI_RESNORM) {
     dgemm_pf<PRO_PLAIN, EPI_RESNORM, SPL>(p, grid, pf, st);
   } else if (epi == EPI_SILU) {
-    if constexpr (!SPL) dgemm_pf<PRO_PLAIN, EPI_SILU, false>(p, grid, pf, st);
+    if constexpr (SPL == 0) dgemm_pf<PRO_PLAIN, EPI_SILU, 0>(p, grid, pf, st);
   } else {
     dgemm_pf<PRO_PLAIN, EPI_STORE, SPL>(p, grid, pf, st);
   }
@@ -526,11 +581,16 @@ void launch_dgemm(const DGemmArgs& a, int pro, int splitk, int pf, hipStream_t s
   }
   const int tiles = ((a.M + DBM - 1) / DBM) * ((a.N + DBN - 1) / DBN);
   dim3 grid(tiles, splitk);
-  if (splitk > 1) {
-    dgemm_main<true>(p, grid, pro, p.epi, pf, st);
+  if (splitk > 1 && p.counters != nullptr && pro == PRO_PLAIN &&
+      (splitk == 2 || splitk == 4 || splitk == 8)) {  // in-launch combine
+    if (splitk == 2) dgemm_main<2, 2>(p, grid, pro, p.epi, pf, st);
+    else if (splitk == 4) dgemm_main<2, 4>(p, grid, pro, p.epi, pf, st);
+    else dgemm_main<2, 8>(p, grid, pro, p.epi, pf, st);
+  } else if (splitk > 1) {
+    dgemm_main<1>(p, grid, pro, p.epi, pf, st);
     launch_dgemm_reduce(p, pro, splitk, st);
   } else {
-    dgemm_main<false>(p, grid, pro, p.epi, pf, st);
+    dgemm_main<0>(p, grid, pro, p.epi, pf, st);
   }
 }
 

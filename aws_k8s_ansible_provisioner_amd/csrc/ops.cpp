@@ -397,7 +397,12 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
               "dgemm: unsupported M/N/K/splitk/pf/bn");
   TORCH_CHECK(!sk || splitk == 1 || counters.has_value(),
               "dgemm bn=256: split-K needs the counters (2 per tile)");
-  const bool inlaunch = counters.has_value() && splitk > 1 && bn > 0;
+  // in-launch split-K combine: the LDS-DMA variants (bn > 0) and, with the plain prologue and
+  // 2 | 4 | 8 slices, the register-ring kernel (64 x 64 tiles)
+  const bool inlaunch = counters.has_value() && splitk > 1 &&
+                        (bn > 0 || (pro == akap::PRO_PLAIN && (splitk == 2 || splitk == 4 ||
+                                                               splitk == 8)));
+  const int tile_n = bn > 0 ? (int)bn : 64, tile_m = bn > 0 ? (int)bm : 64;
   TORCH_CHECK(inlaunch ? (epi != akap::EPI_SILU || N % 32 == 0)
                        : akap::dgemm_epi_supported(N, epi, splitk),
               "dgemm: unsupported epilogue/N/splitk");
@@ -406,11 +411,11 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
               "dgemm: 16-byte aligned rows");
   if (splitk > 1) {
     const int64_t need = sk ? akap::pgemm_sk_ws_floats(M, N, (int)splitk)
-                         : bn > 0 ? akap::gdgemm_ws_floats(M, N, (int)splitk, (int)bn, (int)bm)
-                                  : splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
+                         : inlaunch ? akap::gdgemm_ws_floats(M, N, (int)splitk, tile_n, tile_m)
+                                    : splitk * M * N + (pro == akap::PRO_ADDNORM ? splitk * M : 0);
     TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= need,
                 "dgemm: fp32 workspace of splitk*M*N (+ splitk*M for the norm)");
-    TORCH_CHECK(out.stride(0) == N || (counters.has_value() && bn > 0),
+    TORCH_CHECK(out.stride(0) == N || inlaunch || sk,
                 "dgemm: split-K output must be dense (separate reduce pass)");
   }
   akap::DGemmArgs a{};
@@ -427,12 +432,12 @@ void dgemm(Tensor out, Tensor x, Tensor w, Tensor ws, int64_t pro, int64_t split
   a.bn = (int)bn;
   a.ns = (int)ns;
   a.bm = (int)bm;
-  if (counters && splitk > 1 && bn > 0) {
+  if (inlaunch || (sk && counters && splitk > 1)) {
     // in-launch split-K combine: one zeroed int32 ticket per output tile
     TORCH_CHECK(counters->scalar_type() == at::kInt && counters->is_cuda() &&
                     counters->numel() >= (sk ? (int64_t)akap::kCtrInts
-                                             : (int64_t)((M + bm - 1) / bm) *
-                                                   ((N + bn - 1) / bn) * akap::kCtrStride),
+                                             : (int64_t)((M + tile_m - 1) / tile_m) *
+                                                   ((N + tile_n - 1) / tile_n) * akap::kCtrStride),
                 "dgemm: counters int32, one L2 line per output tile (bn=256: the kCtrInts array)");
     a.counters = counters->data_ptr<int>();
   }

@@ -405,7 +405,8 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
     plain prologue only); 0 the register-ring kernel (prefetch depth pf).  For bn > 0:
     ns >= 6 selects the deep LDS ring (one block per CU, ~7 k-steps in flight), and with
     splitk > 1 inlaunch=True combines the K slices inside the launch (last-arriver ticket,
-    no separate reduce kernel; also allows split-K with the SwiGLU epilogue).
+    no separate reduce kernel; also allows split-K with the SwiGLU epilogue) -- for bn = 0
+    too (register-ring kernel, plain prologue, splitk 2 | 4 | 8).
     bm = 128 (with bn = 128): 128-row LDS-DMA tiles (weights cross L2 -> CU half as often at
     M = 256; the large-weight projections); bm = 256 (bn 64 | 128, 8 waves): the whole
     256-row batch per tile, every weight byte crosses L2 -> CU once.
@@ -449,10 +450,11 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, pro: int = PRO_PLAIN, splitk: int = 
         return out
     counters = None
     if splitk > 1:
-        n = (gdgemm_ws_floats(M, N, splitk, bn, bm) if bn else
+        inl = inlaunch and (bn or (pro == PRO_PLAIN and splitk in (2, 4, 8)))
+        n = (gdgemm_ws_floats(M, N, splitk, bn or 64, bm if bn else 64) if (bn or inl) else
              splitk * M * N + (splitk * M if pro == PRO_ADDNORM else 0))
         ws = torch.empty(n, dtype=torch.float32, device=x.device)
-        if (inlaunch and bn) or bn == 256:  # bn 256: the combine is always in the launch
+        if inl or bn == 256:  # bn 256: the combine is always in the launch
             counters = gemm_counters(x.device)
     else:
         ws = _EMPTY_F32.get(x.device)
@@ -474,7 +476,9 @@ def dgemm_supported(M: int, N: int, K: int, splitk: int, pf: int, epi: int = EPI
         return False
     if bm != 64 and not (bm == 128 and bn == 128) and not (bm == 256 and bn in (64, 128)):
         return False
-    inl = inlaunch and bn and splitk > 1
+    inl = inlaunch and splitk > 1 and (bn or splitk in (2, 4, 8))
+    if inlaunch and splitk > 1 and not bn and splitk not in (2, 4, 8):
+        return False  # the register-ring combine has 2 | 4 | 8 slices
     if epi == EPI_SILU and ((splitk != 1 and not inl) or N % 32):
         return False
     if epi == EPI_RESNORM and splitk > 1 and N % 256 and not inl:

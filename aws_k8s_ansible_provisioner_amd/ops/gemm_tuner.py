@@ -129,6 +129,25 @@ def _gd_call(M, N, K, s, bn, ns, inl, out, x, weights, epi, ss_in, ss_out, a_out
                                           bm)
 
 
+def _rr_inl_ok(s: int) -> bool:
+    """Time the register-ring in-launch combine at split s (AKAP_DGEMM_RR_INL=0: never, the
+    round-5 candidate set, for A/Bs)."""
+    import os
+
+    return s in (2, 4, 8) and os.environ.get("AKAP_DGEMM_RR_INL", "1") != "0"
+
+
+def _rr_inl_call(M, N, s, pf, out, x, weights, epi, ss_in, ss_out, a_out, ln_out):
+    """fn(i): the register-ring dgemm with its s K slices combined inside the launch."""
+    from . import gdgemm_ws_floats, gemm_counters
+
+    ws = torch.empty(gdgemm_ws_floats(M, N, s, 64, 64), device=x.device, dtype=torch.float32)
+    cnt = gemm_counters(x.device)
+    n = len(weights)
+    return lambda i: torch.ops.akap.dgemm(out, x, weights[i % n], ws, 0, s, pf, None, None, None,
+                                          1e-6, epi, ss_in, ss_out, a_out, ln_out, 0, 0, cnt, 64)
+
+
 # choice rankings of the anchor batch sizes (shape class pruning, see tune_model)
 _RANK: dict = {}
 
@@ -155,6 +174,9 @@ def _plain_candidates(M, weights, x, y, splits, pfs, bns, kms, lm_head):
             ws = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
             yield ("dgemm", s, pf), (lambda i, ws=ws, s=s, pf=pf: torch.ops.akap.dgemm(
                 y, x, weights[i % n], ws, 0, s, pf))
+            if _rr_inl_ok(s):  # the same with the slices combined inside the launch
+                yield (("dgemm", s, pf, 0, 0, True),
+                       _rr_inl_call(M, N, s, pf, y, x, weights, 0, None, None, None, None))
         for bn, ns, inl, bm in _gd_variants(s, bns, M):  # LDS-DMA staged variants (gdgemm.hip)
             if (not dgemm_supported(M, N, K, s, 1, bn=bn, inlaunch=inl, bm=bm)
                     or (s > 1 and K // s < 256) or (lm_head and bm != 256)):
@@ -238,6 +260,8 @@ def _gd_name(v) -> str:
     bn, ns, inl, km, bm = variant_fields(v)[:5]
     if km:
         return f"k{km}"
+    if not bn:  # register ring (prefetch depth printed by the caller)
+        return "i" if inl else ""
     if bm in (128, 256):
         return f"g{bn}x{bm}" + ("i" if inl else "")
     return f"g{bn}" + ("d" if ns >= 6 else "") + ("i" if inl else "")
@@ -273,7 +297,8 @@ def tune_model(model, Ms: Sequence[int], log=print) -> dict:
     log(f"[gemm-tuner] {len(summary)} decode GEMM shapes, HIP kernel chosen for "
         f"{len(wins)}: " + ", ".join(
             f"M={m} {n} {c[0]}" + (f" s{c[1]}" if len(c) > 1 else "") +
-            (f"p{c[2]}" if len(c) == 3 else "") +
+            (f"p{c[2]}" if len(c) == 3 or (len(c) > 3 and not c[3] and
+                                          not variant_fields(c[3:])[3]) else "") +
             (_gd_name(c[3:]) if len(c) > 3 else "")
             for (m, n), c in sorted(wins.items())))
     return summary
@@ -312,13 +337,17 @@ def _time_unfused(M: int, model) -> float:
 
 
 def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2, 4, 8),
-               verbose: bool = False, bns=(64, 128), kms=(16, 32)) -> dict:
+               verbose: Optional[bool] = None, bns=(64, 128), kms=(16, 32)) -> dict:
     """Pick (split-K, prefetch) for each fused-chain GEMM at each M and keep the fused chain
     for the M where it beats the unfused chain (both timed on the real cold layer weights)."""
     from . import EPI_SILU, dgemm_supported, kgemm_supported
 
     if not model.layers or any(getattr(l, "moe", None) is not None for l in model.layers):
         return {}
+    if verbose is None:  # AKAP_GEMM_TUNE_VERBOSE=1: per-role winners and runners-up
+        import os
+
+        verbose = os.environ.get("AKAP_GEMM_TUNE_VERBOSE", "0") == "1"
     L = len(model.layers)
     dev = model.layers[0].w_o.device
     dt = model.layers[0].w_o.dtype
@@ -354,6 +383,7 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
             a_o_, ln_ = (a_o if epi == 1 else None), (ln if epi == 1 else None)
             for s in splits:
                 cands = [(pf, 0, 0, False, 0, 64) for pf in pfs] + \
+                    [(pf, 0, 0, True, 0, 64) for pf in pfs if _rr_inl_ok(s)] + \
                     [(1, bn, ns, inl, 0, bm) for bn, ns, inl, bm in _gd_variants(s, bns, M)]
                 if s == 1:
                     cands += [(1, 0, 0, False, km, 64) for km in kms
@@ -375,6 +405,9 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
                     if bn:
                         fn = _gd_call(M, N, K, s, bn, ns, inl, out, x, ws_, epi, ss_in_,
                                       ss_out_, a_o_, ln_, bm)
+                    elif inl:
+                        fn = _rr_inl_call(M, N, s, pf, out, x, ws_, epi, ss_in_, ss_out_, a_o_,
+                                          ln_)
                     else:
                         wsp = torch.empty(max(1, s * M * N), device=dev, dtype=torch.float32)
                         fn = (lambda i, s=s, pf=pf, wsp=wsp: torch.ops.akap.dgemm(
@@ -385,13 +418,19 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
                     if best is None or t < best[0]:
                         best = (t, s, pf, bn, ns, inl, 0, bm)
             franks[(M, name)] = [c for _, c in sorted(timed_c, key=lambda tc: tc[0])]
+            if verbose:
+                log(f"[gemm-tuner] M={M} {name} top: " + ", ".join(
+                    f"{t:.2f}us s{c[0]}" + (_gd_name(c[2:]) if (c[2] or c[5]) else
+                                          f"p{c[1]}" + ("i" if c[4] else ""))
+                    for t, c in sorted(timed_c, key=lambda tc: tc[0])[:5]))
             if best is None:
                 plan_m = None
                 break
             plan_m[name] = best[1:]
             t_fused += best[0]
             detail.append(f"{name} {best[0]:.1f}/{t_plain:.1f} (s{best[1]}"
-                          + (_gd_name(best[3:]) if (best[3] or best[6]) else f"p{best[2]}")
+                          + (_gd_name(best[3:]) if (best[3] or best[6]) else
+                             f"p{best[2]}" + ("i" if best[5] else ""))
                           + ")")
         if plan_m is not None and t_fused < t_unfused:
             _FUSED[M] = plan_m
@@ -597,6 +636,9 @@ def _time_best_plain(M: int, name: str, weights) -> float:
             bn, ns, inl, _, bm = variant_fields(c[3:])[:5]
             return _timed(_gd_call(M, N, K, c[1], bn, ns, inl, y, x, weights, 0, None, None,
                                    None, None, bm), n)
+        if len(c) > 5 and c[5]:
+            return _timed(_rr_inl_call(M, N, c[1], c[2], y, x, weights, 0, None, None, None,
+                                       None), n)
         ws = torch.empty(max(1, c[1] * M * N), device=w0.device, dtype=torch.float32)
         return _timed(lambda i: torch.ops.akap.dgemm(y, x, weights[i % n], ws, 0, c[1], c[2],
                                                      None, None, None, 1e-6, 0, None, None,

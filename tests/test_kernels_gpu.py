@@ -992,6 +992,50 @@ def test_lds_dma_decode_gemm(ring, bn, epi, M, N, K, splitk):
         _close(out, want, atol=2e-2 * want.abs().max().item())
 
 
+@pytest.mark.parametrize("pf", [1, 2, 4, 8])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("scaled", [False, True])
+@pytest.mark.parametrize("M,N,K,splitk", [(256, 1024, 3072, 4), (256, 1024, 2048, 2),
+                                          (37, 1024, 3072, 8), (130, 2048, 1024, 2),
+                                          (1, 256, 4096, 4), (256, 6144, 4096, 8)])
+def test_register_ring_inlaunch_combine(pf, epi, scaled, M, N, K, splitk):
+    """dgemm.hip SPL 2 (register-ring kernel, bn = 0): the K slices stored as sc1 slabs and
+    combined by the tile's last-arriving slice inside the launch -- no reduce kernel -- with
+    each epilogue (store, residual + next norm, SwiGLU), with and without the ss_in row
+    scale, vs fp32 references; a second launch reuses the re-armed tickets bit-exactly."""
+    if not ops.dgemm_supported(M, N, K, splitk, pf, epi, inlaunch=True):
+        pytest.skip("unsupported combination")
+    torch.manual_seed(M + N + K + epi + pf)
+    eps = 1e-6
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    ssi = torch.rand(M, device=DEV) * K + 1.0 if scaled else None
+    y = x.float() @ w.float().t()
+    if scaled:
+        y = y * torch.rsqrt(ssi / K + eps)[:, None]
+    kw = dict(splitk=splitk, pf=pf, inlaunch=True, ss_in=ssi, eps=eps)
+    if epi == ops.EPI_STORE:
+        out = ops.dgemm(x, w, **kw)
+        _close(out, y, atol=2e-2 * y.abs().max().item())
+        out2 = ops.dgemm(x, w, **kw)
+        assert torch.equal(out, out2)
+    elif epi == ops.EPI_RESNORM:
+        res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        res0 = res.clone()
+        ln = torch.rand(N, device=DEV, dtype=torch.bfloat16) + 0.5
+        ss = torch.zeros(M, device=DEV)
+        a = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.dgemm(x, w, out=res, epi=epi, ss_out=ss, a_out=a, ln_out=ln, **kw)
+        want = y.to(torch.bfloat16).float() + res0.float()
+        _close(res, want, atol=2e-2 * want.abs().max().item())
+        _close(a, res.float() * ln.float(), atol=1e-2 * a.float().abs().max().item())
+        assert torch.allclose(ss, res.float().pow(2).sum(-1), rtol=1e-3, atol=1e-2)
+    else:
+        out = ops.dgemm(x, w, epi=epi, **kw)
+        want = ref.silu_and_mul(y.to(torch.bfloat16)).float()
+        _close(out, want, atol=2e-2 * want.abs().max().item())
+
+
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 1024, 1024, 1), (256, 1024, 2048, 4),
                                           (200, 2048, 1024, 3), (256, 4096, 4096, 16),
