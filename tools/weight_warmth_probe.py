@@ -61,7 +61,7 @@ def main() -> int:
             torch.ops.akap.kgemm(res, xs[k], w, 32, ops.EPI_RESNORM, 1e-6, None, ss_o, a_o, ln)
 
     def fl():
-        torch.sum(flush, dtype=torch.float32, out=fl_out)
+        torch.sum(flush, dim=(0,), dtype=torch.float32, out=fl_out)
 
     print(f"M={M}, {L} layer copies; us per launch (best of 3 graph-replay windows)")
     print(f"{'gemm':8s} {'MB':>6s} {'cold':>7s} {'mall':>7s} {'warm':>7s}  flush")
@@ -73,6 +73,25 @@ def main() -> int:
         t_flg = _timed(lambda i: (fl(), call(k, ws[i % 4])), L)
         print(f"{k:8s} {mb:6.1f} {t_cold:7.2f} {t_flg - t_fl:7.2f} {t_warm:7.2f}  {t_fl:.2f}",
               flush=True)
+    # the down projection's split-K forms (VERDICT r5 "Step A"): slabs + the row reduce launch,
+    # the same slices combined inside the launch (dgemm SPL 2), and kgemm (K split inside the
+    # workgroup); cold weights, residual + next-norm epilogue
+    wd = W["down"]
+    ws4 = torch.empty(4 * M * d, device=dev, dtype=torch.float32)
+    ws4i = torch.empty(ops.gdgemm_ws_floats(M, d, 4, 64, 64), device=dev, dtype=torch.float32)
+    cnt = ops.gemm_counters(dev)
+    forms = {
+        "s4p4 slabs + reduce": lambda i: torch.ops.akap.dgemm(
+            res, xs["down"], wd[i % L], ws4, 0, 4, 4, None, None, None, 1e-6, ops.EPI_RESNORM,
+            None, ss_o, a_o, ln, 0),
+        "s4p4 in-launch": lambda i: torch.ops.akap.dgemm(
+            res, xs["down"], wd[i % L], ws4i, 0, 4, 4, None, None, None, 1e-6, ops.EPI_RESNORM,
+            None, ss_o, a_o, ln, 0, 0, cnt, 64),
+        "k32": lambda i: torch.ops.akap.kgemm(res, xs["down"], wd[i % L], 32, ops.EPI_RESNORM,
+                                              1e-6, None, ss_o, a_o, ln),
+    }
+    for name, fn in forms.items():
+        print(f"down {name:22s} {_timed(fn, L):7.2f} us", flush=True)
     return 0
 
 
