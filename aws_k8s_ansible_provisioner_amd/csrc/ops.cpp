@@ -1183,6 +1183,16 @@ Tensor ipc_export(Tensor t) {
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   HIP_OK(hipMemGetAddressRange(&base, &size, t.data_ptr()));
+  // ROCm 7.0.x runtimes (the one PyTorch bundles) hang in the PEER's hipIpcOpenMemHandle when
+  // bit 31 of the allocation size is set (size mod 4 GiB >= 2 GiB; 7.2 maps them):
+  // bench/ipc_import_repro.cpp, profiles/r6_ipc_import_sweep.md.  Refuse here instead of
+  // letting the importer hang; KV segments are sized by models.transformer.ipc_safe_alloc_bytes
+  int rt = 0;
+  HIP_OK(hipRuntimeGetVersion(&rt));
+  TORCH_CHECK(rt >= 70200000 || (size & (size_t(1) << 31)) == 0,
+              "ipc_export: allocation of ", size, " bytes has bit 31 set; a peer's "
+              "hipIpcOpenMemHandle of it hangs on this HIP runtime (", rt,
+              "): pad it to a multiple of 4 GiB (ipc_safe_alloc_bytes)");
   hipIpcMemHandle_t hd;
   HIP_OK(hipIpcGetMemHandle(&hd, base));
   const int64_t off = (int64_t)((char*)t.data_ptr() - (char*)base);

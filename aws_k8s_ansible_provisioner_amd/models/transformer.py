@@ -80,6 +80,33 @@ def _shard_cols(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
     return w[:, rank * n:(rank + 1) * n]
 
 
+def ipc_safe_alloc_bytes(nbytes: int) -> int:
+    """Bytes to allocate for an `nbytes` buffer that a peer process will hipIpc-open: the
+    caching allocator's 2 MiB rounding, then, if bit 31 of the size is set (size mod 4 GiB >=
+    2 GiB -- hipIpcOpenMemHandle of such an allocation hangs on the ROCm 7.0.2 runtime that
+    PyTorch bundles), the next multiple of 4 GiB."""
+    r = -(-int(nbytes) // (2 << 20)) * (2 << 20)
+    if r & (1 << 31):
+        r = ((r >> 32) + 1) << 32
+    return r
+
+
+def kv_segment_layers(L: int, per_layer: int, max_segment_bytes: int,
+                      ipc_safe: bool = True) -> int:
+    """Layers per KV segment: as many as fit `max_segment_bytes`; with ipc_safe, the count in
+    [max/2, max] whose segments need the fewest ipc_safe_alloc_bytes padding bytes (ties: the
+    fewest segments)."""
+    lps_max = max(1, min(L, max_segment_bytes // max(1, per_layer)))
+    if not ipc_safe:
+        return lps_max
+
+    def pad_total(lps: int) -> int:
+        return sum(ipc_safe_alloc_bytes(min(lps, L - l0) * per_layer) -
+                   min(lps, L - l0) * per_layer for l0 in range(0, L, lps))
+
+    return min(range(lps_max, lps_max // 2, -1), key=pad_total)
+
+
 class DecoderLM:
     """Weights + forward for one tensor-parallel rank."""
 
@@ -285,18 +312,33 @@ class DecoderLM:
         [Hkv,BS/8,D,8]) of at most `max_segment_bytes` each (AKAP_KV_SEGMENT_GIB, default 32),
         zero-filled so never-written slots read as finite zeros.  kv_dtype "fp8": uint8
         storage of OCP e4m3fn values (half the bytes of bf16).  Each segment is its own
-        allocation, exported by hipIpc on its own (P/D pull): a single ~86 GiB export hung
-        hipIpcOpenMemHandle for a second importer on one device (profiles/
-        r4_pd_1p2d_one_gpu.log) while 3 x 28.7 GiB opened (profiles/r5_probes_s5b.md)."""
+        allocation, exported by hipIpc on its own (P/D pull).
+
+        On the GPU every allocation's size is kept hipIpc-safe (`ipc_safe_alloc_bytes`): the
+        HIP runtime PyTorch bundles (ROCm 7.0.2) hangs in hipIpcOpenMemHandle when bit 31 of
+        the allocation size is set (size mod 4 GiB >= 2 GiB; 1.5 / 5 / 8 / 9.5 / 36 GiB map,
+        2 / 2.5 / 6.6 GiB hang, at any occupancy -- bench/ipc_import_repro.cpp,
+        profiles/r6_ipc_import_sweep.md; ROCm 7.2's runtime maps them all).  That was the
+        round-4/5 "hang once the device is mostly allocated": big caches made such sizes.
+        The layers per segment are chosen to avoid padding where possible; otherwise the
+        allocation is padded to the next 4 GiB multiple (the tail is never addressed)."""
         per_block = self.hkv * block_size * self.D
         dt = torch.uint8 if kv_dtype.startswith("fp8") else self.dtype
         if max_segment_bytes is None:
             max_segment_bytes = int(float(os.environ.get("AKAP_KV_SEGMENT_GIB", "32")) * 2**30)
         L = self.cfg.num_layers
-        per_layer = 2 * num_blocks * per_block * torch.empty(0, dtype=dt).element_size()
-        lps = max(1, min(L, max_segment_bytes // max(1, per_layer)))
-        return [torch.zeros(min(lps, L - l0), 2, num_blocks, per_block, dtype=dt,
-                            device=self.device) for l0 in range(0, L, lps)]
+        es = torch.empty(0, dtype=dt).element_size()
+        per_layer = 2 * num_blocks * per_block * es
+        gpu = torch.device(self.device).type == "cuda"
+        lps = kv_segment_layers(L, per_layer, max_segment_bytes, ipc_safe=gpu)
+        segs = []
+        for l0 in range(0, L, lps):
+            n = min(lps, L - l0)
+            elems = n * 2 * num_blocks * per_block
+            alloc = ipc_safe_alloc_bytes(elems * es) // es if gpu else elems
+            buf = torch.zeros(alloc, dtype=dt, device=self.device)
+            segs.append(buf[:elems].view(n, 2, num_blocks, per_block))
+        return segs
 
     def cache_views(self, kv, block_size: int):
         """Per-layer K / V views of the cache (one tensor or its list of layer segments)."""

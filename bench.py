@@ -200,14 +200,12 @@ def main() -> int:
                         kv_role=("prefill" if is_prefill else "decode") if pd else "both",
                         kv_cache_dtype=a.kv_cache_dtype,
                         mixed_batching=not a.no_mixed_batching,
-                        # ranks sharing one GPU (single-GPU gloo rehearsal) split its memory;
-                        # P/D ranks sharing one GPU keep <= 28 GiB caches (the headline
-                        # workload needs <= 25 GB of Llama-3-8B KV): a decode rank's hipIpc
-                        # import of a 79-101 GiB peer cache hangs in the driver once the device
-                        # is mostly allocated (profiles/r5_pd_1p2d_one_gpu_ipc.log; 1P:1D
-                        # Llama-3-8B at 101.4 GiB: profiles/r5_pd_llama8b_cache_cap.log)
-                        gpu_memory_utilization=0.90 / max(1, shared_ranks),
-                        kv_cache_max_gib=28.0 if pd and shared_ranks > 1 else None)
+                        # ranks sharing one GPU (single-GPU gloo rehearsal) split its memory.
+                        # No P/D cache cap: the round-5 hipIpc import hang of 79-101 GiB peer
+                        # caches was the bundled runtime's bit-31 allocation-size bug, and the
+                        # KV segments are now sized around it (models.transformer.
+                        # ipc_safe_alloc_bytes, profiles/r6_ipc_import_sweep.md)
+                        gpu_memory_utilization=0.90 / max(1, shared_ranks))
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if rank == 0 else (lambda *x: None)
     tp_bc = None
     if a.tp > 1:

@@ -1,4 +1,4 @@
-// hipIpc import reproducer, HIP only (no torch, no RCCL): does opening a peer process's
+// hipIpc import reproducer, HIP runtime only (no torch, no RCCL): does opening a peer process's
 // exported device memory hang, and what triggers it?  (the P/D rehearsals
 // saw hipIpcOpenMemHandle of a 79-101 GiB peer KV cache hang once the importing process held
 // most of the device, profiles/r5 "hipIpc multi-importer hang")
@@ -7,8 +7,9 @@
 //       allocate Y GiB as ceil(Y / seg) device allocations (the KV exporter's <= 32 GiB
 //       segments, parallel/kv_transfer.py), fill each, write their hipIpcMemHandles to
 //       <dir>/handles.bin, then wait (<= 70 s) for every importer's <dir>/done.<id> and exit
-//   ipc_import_repro import <X_GiB> <dir> [id] [fill]
-//       allocate and hold X GiB of its own first (16 GiB pieces; fill = 1: also write them,
+//   ipc_import_repro import <X_GiB> <dir> [id] [fill] [piece_GiB]
+//       allocate and hold X GiB of its own first (piece_GiB pieces, default 16; 0 = one
+//       allocation, as PyTorch's allocator makes for one big tensor; fill = 1: also write them,
 //       as a zero-filled KV cache is), wait for the handles, open every segment
 //       (hipIpcMemLazyEnablePeerAccess), read 16 bytes of each back, print the free memory
 //       and the time of every step, write <dir>/done.<id>.  Several importers of one export =
@@ -16,7 +17,13 @@
 // Every line is flushed, so a hang shows as the last step printed.  The sweep driver
 // (tools/gpu/s9_ipc_sweep.sh) runs each (X, Y) point under `timeout` and stops at the first
 // hang.  Same-device import: both processes run on GPU 0 (the one-GPU P/D rehearsal layout).
-#include <hip/hip_runtime.h>
+//
+// The HIP runtime is dlopen'ed from $IPC_REPRO_HIPLIB (default /opt/rocm/lib/libamdhip64.so,
+// ROCm 7.2) so the same binary can run on the runtime PyTorch bundles
+// (torch/lib/libamdhip64.so, ROCm 7.0.2), which is the one every engine process uses: both
+// carry the soname libamdhip64.so.7, so a torch process never loads /opt/rocm's.
+// Host-only C++ (no device code): g++ -O2 -std=c++17 ipc_import_repro.cpp -ldl
+#include <dlfcn.h>
 
 #include <chrono>
 #include <cstdio>
@@ -26,10 +33,60 @@
 #include <thread>
 #include <vector>
 
+// the few runtime entry points used, resolved from the chosen library
+typedef int hipError_t;
+struct hipIpcMemHandle_t {
+  char reserved[64];
+};
+constexpr unsigned hipIpcMemLazyEnablePeerAccess = 1;
+constexpr int hipMemcpyDeviceToHost = 2;
+static hipError_t (*hipMalloc)(void**, size_t);
+static hipError_t (*hipFree)(void*);
+static hipError_t (*hipMemset)(void*, int, size_t);
+static hipError_t (*hipDeviceSynchronize)();
+static hipError_t (*hipMemGetInfo)(size_t*, size_t*);
+static hipError_t (*hipIpcGetMemHandle)(hipIpcMemHandle_t*, void*);
+static hipError_t (*hipIpcOpenMemHandle)(void**, hipIpcMemHandle_t, unsigned);
+static hipError_t (*hipMemcpy)(void*, const void*, size_t, int);
+static const char* (*hipGetErrorString)(hipError_t);
+static hipError_t (*hipRuntimeGetVersion)(int*);
+
+static void load_runtime() {
+  const char* path = std::getenv("IPC_REPRO_HIPLIB");
+  if (path == nullptr) path = "/opt/rocm/lib/libamdhip64.so";
+  void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (h == nullptr) {
+    std::printf("dlopen %s: %s\n", path, dlerror());
+    std::exit(8);
+  }
+  auto sym = [&](const char* n) {
+    void* f = dlsym(h, n);
+    if (f == nullptr) {
+      std::printf("missing %s in %s\n", n, path);
+      std::exit(8);
+    }
+    return f;
+  };
+  hipMalloc = reinterpret_cast<decltype(hipMalloc)>(sym("hipMalloc"));
+  hipFree = reinterpret_cast<decltype(hipFree)>(sym("hipFree"));
+  hipMemset = reinterpret_cast<decltype(hipMemset)>(sym("hipMemset"));
+  hipDeviceSynchronize = reinterpret_cast<decltype(hipDeviceSynchronize)>(sym("hipDeviceSynchronize"));
+  hipMemGetInfo = reinterpret_cast<decltype(hipMemGetInfo)>(sym("hipMemGetInfo"));
+  hipIpcGetMemHandle = reinterpret_cast<decltype(hipIpcGetMemHandle)>(sym("hipIpcGetMemHandle"));
+  hipIpcOpenMemHandle = reinterpret_cast<decltype(hipIpcOpenMemHandle)>(sym("hipIpcOpenMemHandle"));
+  hipMemcpy = reinterpret_cast<decltype(hipMemcpy)>(sym("hipMemcpy"));
+  hipGetErrorString = reinterpret_cast<decltype(hipGetErrorString)>(sym("hipGetErrorString"));
+  hipRuntimeGetVersion = reinterpret_cast<decltype(hipRuntimeGetVersion)>(sym("hipRuntimeGetVersion"));
+  int v = 0;
+  hipRuntimeGetVersion(&v);
+  std::printf("[runtime] %s, HIP runtime version %d\n", path, v);
+  std::fflush(stdout);
+}
+
 #define CHECK(x)                                                                       \
   do {                                                                                 \
     hipError_t e_ = (x);                                                               \
-    if (e_ != hipSuccess) {                                                            \
+    if (e_ != 0) {                                                                     \
       std::printf("HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__,     \
                   __LINE__, #x);                                                       \
       std::fflush(stdout);                                                             \
@@ -100,9 +157,10 @@ static int do_export(double y_gib, double seg_gib, const std::string& dir, int n
   return 0;
 }
 
-static int do_import(double x_gib, const std::string& dir, int id, bool fill) {
+static int do_import(double x_gib, const std::string& dir, int id, bool fill, double piece_gib) {
   std::vector<void*> own;
-  const size_t hold = (size_t)(x_gib * 1073741824.0), piece = (size_t)16 << 30;
+  const size_t hold = (size_t)(x_gib * 1073741824.0);
+  const size_t piece = piece_gib > 0 ? (size_t)(piece_gib * 1073741824.0) : (hold ? hold : 1);
   for (size_t off = 0; off < hold; off += piece) {
     void* p = nullptr;
     const size_t n = hold - off < piece ? hold - off : piece;
@@ -155,14 +213,16 @@ static int do_import(double x_gib, const std::string& dir, int id, bool fill) {
 }
 
 int main(int argc, char** argv) {
+  if (argc >= 2 && (!std::strcmp(argv[1], "export") || !std::strcmp(argv[1], "import")))
+    load_runtime();
   if (argc >= 5 && !std::strcmp(argv[1], "export"))
     return do_export(std::atof(argv[2]), std::atof(argv[3]), argv[4],
                      argc >= 6 ? std::atoi(argv[5]) : 1);
   if (argc >= 4 && !std::strcmp(argv[1], "import"))
     return do_import(std::atof(argv[2]), argv[3], argc >= 5 ? std::atoi(argv[4]) : 0,
-                     argc >= 6 && std::atoi(argv[5]) == 1);
+                     argc >= 6 && std::atoi(argv[5]) == 1, argc >= 7 ? std::atof(argv[6]) : 16);
   std::fprintf(stderr,
                "usage: %s export <Y_GiB> <seg_GiB> <dir> [importers] | "
-               "import <X_GiB> <dir> [id] [fill]\n", argv[0]);
+               "import <X_GiB> <dir> [id] [fill] [piece_GiB]\n", argv[0]);
   return 2;
 }

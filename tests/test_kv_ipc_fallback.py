@@ -98,3 +98,41 @@ def test_segmented_kv_cache_views_and_packing():
     finally:
         a1.close()
         a2.close()
+
+
+def test_ipc_safe_alloc_bytes_rule():
+    """The bundled ROCm 7.0.2 runtime hangs in hipIpcOpenMemHandle when bit 31 of the
+    allocation size is set (profiles/r6_ipc_import_sweep.md: 1.5 / 5 / 8 / 9.5 / 36 GiB map,
+    2 / 2.5 / 6.6 GiB hang).  The KV allocator pads such sizes to the next 4 GiB multiple."""
+    from aws_k8s_ansible_provisioner_amd.models.transformer import ipc_safe_alloc_bytes
+
+    G = 2**30
+    for gib in (1.5, 5, 8, 9.5, 36):  # measured to map: unchanged (2 MiB rounding only)
+        assert ipc_safe_alloc_bytes(int(gib * G)) == int(gib * G)
+    for gib, want in ((2, 4), (2.5, 4), (6.6, 8), (31.7, 32), (86, 88)):  # measured / r4-r5 hangs
+        r = ipc_safe_alloc_bytes(int(gib * G))
+        assert r == want * G and not r & (1 << 31)
+    assert ipc_safe_alloc_bytes(1) == 2 << 20  # the caching allocator's 2 MiB rounding
+    for n in (3 * G + 5, 7 * G - 1, 123456789012):
+        r = ipc_safe_alloc_bytes(n)
+        assert r >= n and not r & (1 << 31) and r - n < 2 * G + (2 << 20)
+
+
+def test_kv_segment_layers_avoid_padding():
+    """Layers per segment: the count in [max/2, max] with the fewest padding bytes.  Llama-3-8B
+    at the round-5 1P:1D size (32 layers, ~3.17 GiB each, 32 GiB cap): 10 layers per segment
+    would make 31.7 GiB allocations (bit 31 set); the choice needs no padding at all."""
+    from aws_k8s_ansible_provisioner_amd.models.transformer import (ipc_safe_alloc_bytes,
+                                                                  kv_segment_layers)
+
+    G = 2**30
+    per_layer = int(3.17 * G) // (2 << 20) * (2 << 20)
+    lps = kv_segment_layers(32, per_layer, 32 * G)
+    assert 5 < lps <= 10
+    pad = sum(ipc_safe_alloc_bytes(min(lps, 32 - l0) * per_layer) - min(lps, 32 - l0) * per_layer
+              for l0 in range(0, 32, lps))
+    assert pad == 0
+    assert kv_segment_layers(32, per_layer, 32 * G, ipc_safe=False) == 10
+    assert kv_segment_layers(4, 10 * G, 32 * G) in (2, 3)  # never below half the max
+    assert kv_segment_layers(28, G // 16, 32 * G) == 28  # 1.75 GiB: one unpadded segment
+    assert kv_segment_layers(28, G // 8, 32 * G) == 15  # 3.5 GiB (bit 31): 1.875 + 1.625 GiB
