@@ -148,6 +148,17 @@ def _rr_inl_call(M, N, s, pf, out, x, weights, epi, ss_in, ss_out, a_out, ln_out
                                           1e-6, epi, ss_in, ss_out, a_out, ln_out, 0, 0, cnt, 64)
 
 
+def _rot(weights: Sequence[torch.Tensor], cold_bytes: int = 768 << 20) -> list:
+    """The layer copies a candidate is timed on: enough to stream >= cold_bytes per rotation
+    (3x the 256 MB MALL, so every call still sees cold weights) and at least 4, not all of
+    them -- tuning time scales with the rotation (Llama-3-8B: 32 layers of 50-235 MB each)."""
+    w = list(weights)
+    if not w:
+        return w
+    per = w[0].numel() * w[0].element_size()
+    return w[:max(4, min(len(w), -(-cold_bytes // max(1, per))))]
+
+
 # choice rankings of the anchor batch sizes (shape class pruning, see tune_model)
 _RANK: dict = {}
 
@@ -202,6 +213,7 @@ def tune(M: int, weights: Sequence[torch.Tensor], splits=(1, 2, 4, 8, 16),
     shape-class pruning of tune_model); the ranking lands in _RANK[(M, N, K)]."""
     from . import gemm_counters  # noqa: F401  (ensures the native library is loaded)
 
+    weights = _rot(weights)
     w0 = weights[0]
     N, K = w0.shape
     dev = w0.device
@@ -367,7 +379,8 @@ def tune_fused(model, Ms: Sequence[int], log=print, splits=(1, 2, 4, 8), pfs=(2,
             allowed = _neighbour_allowed(M, anchors,
                                          lambda a, name=name: franks.get((a, name), []))
             timed_c: list = []
-            ws_ = [getattr(l, name) for l in model.layers]
+            ws_ = _rot([getattr(l, name) for l in model.layers])
+            L = len(ws_)
             N, K = ws_[0].shape
             t_plain = _time_best_plain(M, name, ws_)
             t_unfused += t_plain
@@ -622,6 +635,7 @@ def load_cache(path: str, model, Ms: Sequence[int], prefill_m: int = 0) -> bool:
 
 def _time_best_plain(M: int, name: str, weights) -> float:
     """us of the plan's choice for this projection (hipBLASLt unless tuned otherwise)."""
+    weights = _rot(weights)
     w0 = weights[0]
     N, K = w0.shape
     x = torch.randn(M, K, device=w0.device, dtype=w0.dtype) * 0.1

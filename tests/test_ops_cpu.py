@@ -333,3 +333,17 @@ def test_tuner_shape_class_pruning():
                                                        ("torch",)}
     assert gt._neighbour_allowed(200, a, ranks.get) == {("k",), ("g",)}
     assert gt.anchor_ms([16, 32, 64]) == [16, 32, 64]
+
+
+def test_tuner_rotation_keeps_weights_cold():
+    """Candidates are timed on enough layer copies to stream >= 768 MB per rotation (3x the
+    MALL) and at least 4 -- not on every layer (Llama-3-8B cold tuning time)."""
+    from aws_k8s_ansible_provisioner_amd.ops.gemm_tuner import _rot
+
+    def layers(n, mb):
+        return [torch.empty(int(mb * (1 << 20)) // 2, dtype=torch.bfloat16) for _ in range(n)]
+
+    assert len(_rot(layers(28, 8.4))) == 28  # Qwen3 qkv: all 28 (235 MB in total)
+    assert len(_rot(layers(32, 235))) == 4  # Llama-3-8B gate_up: 4 x 235 MB
+    assert len(_rot(layers(32, 50))) == 16  # Llama-3-8B qkv
+    assert len(_rot(layers(2, 1))) == 2 and _rot([]) == []
