@@ -100,7 +100,8 @@ def _gd_variants(s: int, bns, M: int = 0):
     """gdgemm.hip variants at split s: (tile width, ring depth, in-launch split-K combine, tile
     rows).  Depth 0 = shallow ring (two blocks per CU), 8 = deep ring (one block per CU);
     128 x 128 tiles (rows 128) have their own 4-slot ring; 256-row tiles (8 waves, 3-slot
-    ring) only where the batch fills most of them (M > 160).  (The 256-row 6-slot ring of
+    ring) once the batch needs more than one 128-row tile (M > 128: at M = 160 Llama-3-8B's
+    gate_up takes 89 us on two 128-row tiles, 71 us for a whole 256-row batch on one).  (The 256-row 6-slot ring of
     32-deep k-steps, ns = 6, lost on every M = 256 shape: profiles/r3_gemm_m256_deep.log.)"""
     for bn in bns:
         for ns in (0, 8):
@@ -109,7 +110,7 @@ def _gd_variants(s: int, bns, M: int = 0):
         if bn == 128:
             for inl in ((False, True) if s > 1 else (False,)):
                 yield bn, 4, inl, 128
-        if M > 160:
+        if M > 128:
             for inl in ((False, True) if s > 1 else (False,)):
                 yield bn, 3, inl, 256
 
