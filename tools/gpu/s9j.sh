@@ -1,0 +1,9 @@
+# round 6: GPU-idle time at each decode kernel boundary (what a persistent layer could save at
+# most), from a kernel trace of the headline bench (trace kept in /tmp on the box)
+set -u
+O=gpurun_out/s9j; mkdir -p $O
+export TMPDIR=/tmp
+run() { local n=$1 tm=$2; shift 2; timeout -k 10 $tm "$@" > $O/$n.log 2>&1; rc=$?; echo "$n rc=$rc"; [ $rc -eq 0 ]; }
+run prof 600 rocprofv3 --kernel-trace -d /tmp/s9jprof -o run --output-format csv -- python3 -u bench.py --steps 2 --warmup 1 &&
+run bounds 120 python3 tools/decode_boundaries.py /tmp/s9jprof/run_kernel_trace.csv &&
+echo done
