@@ -198,29 +198,35 @@ int main(int argc, char** argv) {
   const int M = 256;
   Shape shapes[] = {{"qkv", 4096, 1024}, {"o", 1024, 2048}, {"gate_up", 6144, 1024},
                     {"down", 1024, 3072}};
-  size_t wmax = 0;
+  size_t wmax = (size_t)4096 * 4096;  // the largest prefill shape below (pf_l8b_o)
   for (auto& s : shapes) wmax = std::max(wmax, (size_t)s.N * s.K);
   bf16raw *X, *W;
   unsigned* out;
   void* flush;
   const size_t flush_bytes = 512ull << 20;
-  CK(hipMalloc(&X, (size_t)M * 4096 * 2));
+  const int MPF = 16384;  // prefill chunk rows (the pgemm / hipBLASLt shapes)
+  CK(hipMalloc(&X, (size_t)MPF * 4096 * 2));
   CK(hipMalloc(&W, wmax * 2));
   CK(hipMalloc(&out, 64));
   CK(hipMalloc(&flush, flush_bytes));
-  CK(hipMemset(X, 1, (size_t)M * 4096 * 2));
+  CK(hipMemset(X, 1, (size_t)MPF * 4096 * 2));
   CK(hipMemset(W, 1, wmax * 2));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   printf("shape,tile,kst,ns,waves,path,map,op,stag,weights,us,bytes_per_cu_KB,GBps_per_cu,wgs\n");
+  int MR = M;  // rows of the current shape set (decode 256, prefill MPF)
   auto run = [&](const char* nm, const Shape& s, int BM, int BN, int KST, int NS, int waves,
                  const char* path, int map, int op, int stag, auto launch) {
     char key[128];
     snprintf(key, sizeof key, "%s,%dx%d,%d,%d,%d,%s,%d,%d,%d", nm, BM, BN, KST, NS, waves,
              path, map, op, stag);
     if (filt && strncmp(key, filt, strlen(filt)) != 0) return;
-    const int wgs = (M / BM) * (s.N / BN);
+    const int wgs = (MR / BM) * (s.N / BN);
+    if ((size_t)s.N * s.K > wmax || (size_t)MR * s.K > (size_t)MPF * 4096) {
+      fprintf(stderr, "skip %s: operands larger than the allocations\n", key);
+      return;
+    }
     const double per_cu = (double)(BM + BN) * s.K * 2;
     for (int cold = 0; cold < 2; ++cold) {
       float tot = 0.f;
@@ -280,6 +286,28 @@ int main(int argc, char** argv) {
 #undef RCASE
           }
         }
+    }
+  }
+  // Prefill GEMM tiles (round 6, the pgemm-vs-hipBLASLt question): 256 x 256 output tiles at
+  // M = 16384, the operand stream of one workgroup per tile (X 256 rows + W 256 rows, all K),
+  // 64 KiB per 64-deep k-step.  Qwen3 o (N 1024, K 2048) is exactly 256 tiles (one per CU):
+  // hipBLASLt runs it at 1.67 us per k-step (~10 TB/s of L2 -> CU), pgemm at ~2.6.
+  MR = MPF;
+  Shape pshapes[] = {{"pf_o", 1024, 2048}, {"pf_qkv", 4096, 1024}, {"pf_down", 1024, 3072},
+                     {"pf_l8b_o", 4096, 4096}};
+  for (auto& s : pshapes) {
+    for (int stag = 0; stag < 2; ++stag) {
+      Args a{X, W, MPF, s.N, s.K, 256, 256, 32, 4, out, 0, 0, stag};
+      run(s.name, s, 256, 256, 32, 4, 8, "lds_counted", 0, 0, stag,
+          [&](int wgs) { k_ingress_c<8, 4, 4><<<wgs, 512, 4 * 2048 * 16, 0>>>(a); });
+      run(s.name, s, 256, 256, 32, 4, 4, "lds_counted", 0, 0, stag,
+          [&](int wgs) { k_ingress_c<4, 8, 4><<<wgs, 256, 4 * 2048 * 16, 0>>>(a); });
+      Args b2{X, W, MPF, s.N, s.K, 256, 256, 64, 2, out, 0, 0, stag};
+      run(s.name, s, 256, 256, 64, 2, 8, "lds_counted", 0, 0, stag,
+          [&](int wgs) { k_ingress_c<8, 8, 2><<<wgs, 512, 2 * 4096 * 16, 0>>>(b2); });
+      Args c{X, W, MPF, s.N, s.K, 256, 256, 32, 0, out, 0, 0, stag};
+      run(s.name, s, 256, 256, 32, 2, 8, "reg", 0, 0, stag,
+          [&](int wgs) { k_ingress_reg<8, 4, 2><<<wgs, 512, 0, 0>>>(c); });
     }
   }
   return 0;
