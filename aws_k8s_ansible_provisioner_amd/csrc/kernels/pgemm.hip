@@ -10,6 +10,12 @@
 // "half-tile" is 128 rows x 64 k (16 KB: two 1-KiB DMA instructions per wave), issued in the
 // order the phases consume them, so every wait is a counted `s_waitcnt vmcnt` (never 0 in
 // steady state: cdna_hip_programming.md "Pipelining across barriers", T3+T4).
+// DEFAULT K loop (SCHED 4, "stream-first", round 6): one counted wait + one barrier per K tile,
+// then the whole next K tile (four half-tiles, 64 KiB) is requested at once and streams into the
+// other buffer under this tile's 64 MFMAs per wave.  A no-math probe of exactly this operand
+// stream runs as fast as hipBLASLt's whole GEMM, and the phase pipeline below measured ~stream +
+// math; the stream-first loop is 5-14 % faster than it (0.70-0.88x hipBLASLt dense, 0.97-1.11x
+// with the SwiGLU epilogue, profiles/r6_pgemm_isa_diff.md).  The phase pipeline (SCHED 1):
 // NB = 2 (plain store; two raw s_barriers per K tile):
 //   phase | counted wait + barrier           | ds_reads issued            | DMA issued
 //   1     | W right + A bottom of tile t     | B right + A bottom (t)     | W right, A bottom (t+1)
@@ -267,6 +273,35 @@ __device__ __forceinline__ void pg_mainloop(bf16x8* lds, const __amdgpu_buffer_r
     __builtin_amdgcn_s_setprio(0);
   };
 
+  if constexpr (SCHED == 4) {
+    // ---- stream-first schedule: the whole next K tile (all four half-tiles, 64 KiB) is
+    // requested right after this tile's barrier and streams under this tile's MFMAs.  The
+    // no-math stream of these tiles (one tile in flight, the same pattern) runs as fast as
+    // hipBLASLt's whole GEMM, while the phase pipeline above measured stream + math
+    // (profiles/r6_pgemm_isa_diff.md, "no-math stream").  One wait, one barrier per K tile.
+    issue(H0{}, 0);
+    issue(H1{}, 0);
+    issue(H2{}, 0);
+    issue(H3{}, 0);
+    for (int t = 0; t < nk; ++t) {
+      const bf16x8* cur = lds + (t & 1) * PG_BUF;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t landed (the only one in flight)
+      pg_sync();  // every wave's pieces of t landed; every read of tile t-1 (slot of t+1) retired
+      issue(H0{}, t + 1);
+      issue(H1{}, t + 1);
+      issue(H2{}, t + 1);
+      issue(H3{}, t + 1);
+      rd_a(at, cur, 0);
+      rd_b(bl, cur, 0);
+      rd_b(br, cur, 1);
+      rd_a(ab, cur, 1);
+      mma(at, bl, 0, 0);
+      mma(at, br, 0, NJ);
+      mma(ab, bl, 4, 0);
+      mma(ab, br, 4, NJ);
+    }
+    return;
+  }
   if constexpr (SCHED == 2) {
     // ---- early-issue schedule: every half-tile goes out as soon as its slot's previous
     // reads retired -- A top / W left of tile t+2 right after phase 1's barrier of tile t
@@ -833,13 +868,16 @@ long pgemm_sk_ws_floats(int M, int N, int splits) {
 
 // Wave form of the 256 x 256 body: AKAP_PGEMM_WAVES = 8 (2 x 4 waves of 128 x 64) or 4 (2 x 2
 // waves of 128 x 128), read once per process.
-// K-loop issue schedule: AKAP_PGEMM_SCHED = 1 (half-tiles requested 1.0-1.25 tiles ahead) or
-// 2 (early issue, 1.25-1.75 tiles ahead; pg_mainloop), read once per process
+// K-loop issue schedule: AKAP_PGEMM_SCHED = 1 (phase pipeline, half-tiles requested 1.0-1.25
+// tiles ahead), 2 (early issue, 1.25-1.75 tiles ahead), 3 (4-wave unit body), 4 (default,
+// stream-first: the whole next tile under this tile's math, 5-14 % faster than 1 on the dense
+// verdict shapes, profiles/r6_pgemm_isa_diff.md; pg_mainloop), read once per process.  The
+// decode split-K form (launch_pgemm_sk) keeps 1 / 2.
 int pgemm_sched() {
   static int v = [] {
     const char* e = getenv("AKAP_PGEMM_SCHED");
-    const int x = e ? atoi(e) : 1;
-    return (x == 2 || x == 3) ? x : 1;
+    const int x = e ? atoi(e) : 4;  // default: the stream-first body (r6_pgemm_isa_diff.md)
+    return (x == 1 || x == 2 || x == 3 || x == 4) ? x : 4;
   }();
   return v;
 }
@@ -865,7 +903,7 @@ static void launch_pgemm_sk_w(const DGemmArgs& p, int splits, hipStream_t st) {
 
 void launch_pgemm_sk(const DGemmArgs& p, int splits, hipStream_t st) {
   if (p.M == 0) return;
-  if (pgemm_waves() == 4) {
+  if (pgemm_waves() == 4) {  // (SCHED 3 / 4 are whole-tile bodies: the split-K form runs 1)
     if (pgemm_sched() == 2) launch_pgemm_sk_w<4, 2>(p, splits, st);
     else launch_pgemm_sk_w<4, 1>(p, splits, st);
   } else {
@@ -909,6 +947,11 @@ void launch_pgemm(const PGemmArgs& a, int epi, hipStream_t st) {
     PGemmArgs q = p;
     q.stagger = stag;
     launch_pgemm_w<4, 3>(q, epi, grid, st);
+    return;
+  }
+  if (pgemm_sched() == 4) {  // stream-first body (AKAP_PGEMM_WAVES 8 | 4)
+    if (pgemm_waves() == 4) launch_pgemm_w<4, 4>(p, epi, grid, st);
+    else launch_pgemm_w<8, 4>(p, epi, grid, st);
     return;
   }
   // two barriers per K tile (measured 1-4 % faster than four, profiles/r4_pgemm_nb_ab.log); the
