@@ -877,7 +877,7 @@ int pgemm_sched() {
   static int v = [] {
     const char* e = getenv("AKAP_PGEMM_SCHED");
     const int x = e ? atoi(e) : 4;  // default: the stream-first body (r6_pgemm_isa_diff.md)
-    return (x == 1 || x == 2 || x == 3 || x == 4) ? x : 4;
+    return (x >= 1 && x <= 4) ? x : 4;
   }();
   return v;
 }
