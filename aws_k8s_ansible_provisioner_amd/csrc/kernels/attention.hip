@@ -965,7 +965,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
           for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sacc[k][j]);
       }
       mx = xor32_max(mx);
-      const float m_new = fmaxf(m_run, mx * p.scale_log2);
+      // deferred max: the running max (and with it every rescale of O and l) moves only when
+      // the tile's max exceeds it by more than rescale_t log2 units -- P entries then reach at
+      // most 2^rescale_t, exact in the fp32 sums and as relative-precision bf16 P.  With one
+      // branch per wave (__any below) an exact running max rescaled almost every tile: some
+      // of the wave's 32 rows nearly always sees a new maximum.
+      const float m_cand = fmaxf(m_run, mx * p.scale_log2);
+      const float m_new = m_cand > m_run + p.rescale_t ? m_cand : m_run;
       // raw v_exp_f32 (no denormal range fix-up: arguments are <= 0, tiny results flush)
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       float rsp[4] = {0.f, 0.f, 0.f, 0.f};  // four short add chains instead of one of 32
@@ -1096,19 +1102,25 @@ void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows
                                hipStream_t s) {
   if (num_tiles == 0) return;
   const dim3 grid(num_tiles, p.Hkv);
+  static const float rescale_t = [] {  // AKAP_FA_RESCALE_T (log2 units; 0 = exact max)
+    const char* e = std::getenv("AKAP_FA_RESCALE_T");
+    return e != nullptr ? (float)std::atof(e) : 8.f;
+  }();
+  AttnParams q = p;
+  q.rescale_t = rescale_t;
   // AKAP_PREFILL_STAGGER=1: the 8-wave kernel's compute/load ping-pong (STAG above)
   static const bool stag = [] {
     const char* e = std::getenv("AKAP_PREFILL_STAGGER");
     return e != nullptr && std::atoi(e) == 1;
   }();
   if (tile_rows == 2 * kFaRows && !p.kv_fp8) {  // 256 rows, 8 waves (bf16 caches)
-    if (stag) paged_attn_prefill_fa_kernel<false, true, 8, true><<<grid, 512, 0, s>>>(p);
-    else paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(p);
+    if (stag) paged_attn_prefill_fa_kernel<false, true, 8, true><<<grid, 512, 0, s>>>(q);
+    else paged_attn_prefill_fa_kernel<false, true, 8><<<grid, 512, 0, s>>>(q);
   }
   else if (p.kv_fp8)  // fp8 caches: register-staged (widened to bf16 on the way into LDS)
-    paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(p);
+    paged_attn_prefill_fa_kernel<true, false><<<grid, 256, 0, s>>>(q);
   else  // bf16 caches: LDS-DMA staging
-    paged_attn_prefill_fa_kernel<false, true><<<grid, 256, 0, s>>>(p);
+    paged_attn_prefill_fa_kernel<false, true><<<grid, 256, 0, s>>>(q);
 }
 
 void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) {

@@ -79,6 +79,10 @@ struct AttnParams {
   // from the tail.  tail_slot: per batch row (decode) / token (writer), -1 = no tail.
   __bf16* v_tail;
   const int* tail_slot;
+  // prefill online softmax: a row's running max moves (and the O / l accumulators are
+  // rescaled) only when the tile's max exceeds it by more than this many log2 units (0 =
+  // every increase); set by launch_paged_attn_prefill (AKAP_FA_RESCALE_T, default 8)
+  float rescale_t;
 };
 // tile_rows: 128 -> flash-style LDS-tiled kernel (4 waves), 256 -> its 8-wave form (bf16 KV)
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows, hipStream_t s);
