@@ -101,7 +101,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress(Args a) {
 
 // Variant with exact counted waits: compile-time pieces per wave (P) and depth (NS) so the
 // vmcnt immediate is exact -- stages t+1..t+NS-2 stay in flight across the barrier.
-template <int WAVES, int P, int NS>
+// RD > 0: each wave also reads RD 16-B LDS words per lane per stage (a GEMM's fragment reads:
+// pgemm's 8-wave tile reads 24 per 64-deep stage), to price the LDS traffic beside the DMA.
+template <int WAVES, int P, int NS, int RD = 0>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_c(Args a) {
   extern __shared__ u32x4 ring[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -140,7 +142,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ingress_c(Args a) {
     __builtin_amdgcn_s_barrier();
     if (t + NS - 1 < nst) issue(t + NS - 1);
     const u32x4* slot = ring + (t % NS) * units;
-    acc ^= slot[(tid * 7) % units].x;
+    if constexpr (RD > 0) {
+      u32x4 v[RD];
+#pragma unroll
+      for (int i = 0; i < RD; ++i) v[i] = slot[(i * 64 * WAVES + tid * 5 + i) % units];
+#pragma unroll
+      for (int i = 0; i < RD; ++i) acc ^= v[i].x ^ v[i].w;
+    } else {
+      acc ^= slot[(tid * 7) % units].x;
+    }
   }
   if (acc == 0x9e3779b9u) a.out[0] = acc;
 }
@@ -305,6 +315,12 @@ int main(int argc, char** argv) {
       Args b2{X, W, MPF, s.N, s.K, 256, 256, 64, 2, out, 0, 0, stag};
       run(s.name, s, 256, 256, 64, 2, 8, "lds_counted", 0, 0, stag,
           [&](int wgs) { k_ingress_c<8, 8, 2><<<wgs, 512, 2 * 4096 * 16, 0>>>(b2); });
+      if (!stag) {  // + the 8-wave GEMM's fragment reads (24 ds_read_b128 per lane per stage)
+        run(s.name, s, 256, 256, 64, 2, 8, "lds_counted_rd24", 0, 0, stag,
+            [&](int wgs) { k_ingress_c<8, 8, 2, 24><<<wgs, 512, 2 * 4096 * 16, 0>>>(b2); });
+        run(s.name, s, 256, 256, 64, 2, 8, "lds_counted_rd12", 0, 0, stag,
+            [&](int wgs) { k_ingress_c<8, 8, 2, 12><<<wgs, 512, 2 * 4096 * 16, 0>>>(b2); });
+      }
       Args c{X, W, MPF, s.N, s.K, 256, 256, 32, 0, out, 0, 0, stag};
       run(s.name, s, 256, 256, 32, 2, 8, "reg", 0, 0, stag,
           [&](int wgs) { k_ingress_reg<8, 4, 2><<<wgs, 512, 0, 0>>>(c); });
