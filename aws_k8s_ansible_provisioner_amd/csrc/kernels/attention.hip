@@ -650,10 +650,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
   // first kFaBtCache 32-key chunks; ONE __shared__ object (a second one makes hipcc drain vmcnt)
   __shared__ __attribute__((aligned(16))) bf16 lds[NBUF * 2 * kFaKeys * kD + 2 * kFaBtCache];
   int* bt_s = reinterpret_cast<int*>(lds + NBUF * 2 * kFaKeys * kD);
-  // causal work grows with a tile's position: dispatch the map back to front so the
-  // longest tiles start first and the grid's tail is made of short ones
-  const int tile = gridDim.x - 1 - blockIdx.x;
-  const int kvh = blockIdx.y;
+  // One flat grid of (tile, kv head) items, kv head innermost, dispatched back to front: the
+  // host map is sorted by ascending causal work (scheduler.cpp), so every head of the longest
+  // tiles starts first and the grid's tail is made of the shortest ones (longest-first over
+  // the whole grid, not per head: a (tile, head) grid put all of head 7's long tiles last).
+  // With Hkv = 8 the dispatcher's round-robin over the 8 XCDs keeps one head's tiles -- which
+  // read the same K/V -- on one XCD's L2.
+  const int flat = gridDim.x - 1 - blockIdx.x;
+  const int tile = flat / p.Hkv;
+  const int kvh = flat - tile * p.Hkv;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar registers
@@ -1101,7 +1106,7 @@ __global__ __launch_bounds__(256) void paged_attn_reduce_kernel(AttnParams p) {
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows,
                                hipStream_t s) {
   if (num_tiles == 0) return;
-  const dim3 grid(num_tiles, p.Hkv);
+  const dim3 grid(num_tiles * p.Hkv);  // flat (tile, kv head), see the kernel
   static const float rescale_t = [] {  // AKAP_FA_RESCALE_T (log2 units; 0 = exact max)
     const char* e = std::getenv("AKAP_FA_RESCALE_T");
     return e != nullptr ? (float)std::atof(e) : 8.f;

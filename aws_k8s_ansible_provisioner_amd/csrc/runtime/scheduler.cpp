@@ -2,9 +2,41 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace akap_rt {
+
+namespace {
+// Orders the step's prefill tile map by ascending causal work: a tile's cost is the key count
+// its last q row attends to (the chunk's context plus its furthest token).  The prefill
+// attention kernel walks one flat (tile, kv head) grid back to front, so this makes the
+// launch longest-first over the whole grid and leaves only the shortest tiles for its tail
+// (attention.hip, paged_attn_prefill_fa_kernel).  Stable: equal-work tiles keep map order.
+void sort_tiles_by_work(BatchBuffers& buf, int tiles, int step_rows, int G) {
+  static const bool on = [] {  // AKAP_TILE_SORT=0: keep map order (A/B knob)
+    const char* e = std::getenv("AKAP_TILE_SORT");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (tiles < 2 || !on) return;
+  std::vector<std::pair<int, int>> key(tiles);  // (work, original index)
+  for (int i = 0; i < tiles; ++i) {
+    const int s = buf.tile_seq[i];
+    const int q = buf.q_start[s + 1] - buf.q_start[s];
+    const int last_tok = std::min(q, (buf.tile_row[i] + step_rows + G - 1) / G);
+    key[i] = {buf.seq_lens[s] - q + last_tok, i};
+  }
+  std::stable_sort(key.begin(), key.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<int32_t> ts(tiles), tr(tiles);
+  for (int i = 0; i < tiles; ++i) {
+    ts[i] = buf.tile_seq[key[i].second];
+    tr[i] = buf.tile_row[key[i].second];
+  }
+  std::copy(ts.begin(), ts.end(), buf.tile_seq);
+  std::copy(tr.begin(), tr.end(), buf.tile_row);
+}
+}  // namespace
 
 Scheduler::Scheduler(const SchedConfig& cfg, int num_blocks, bool prefix_cache)
     : cfg_(cfg), bm_(num_blocks, cfg.block_size, prefix_cache) {
@@ -437,6 +469,7 @@ StepInfo Scheduler::schedule(BatchBuffers& buf) {
     T += q;
   }
   buf.q_start[sched.size()] = T;
+  sort_tiles_by_work(buf, tiles, step_rows, cfg_.gqa_group);
   info.num_seqs = (int)sched.size();
   info.num_tokens = T;
   info.num_tiles = tiles;

@@ -92,7 +92,9 @@ def test_prefill_tile_map_counts_gqa_rows():
     s.add_request(2, [5, 6], 2)               # 2 * 4 = 8 rows -> 1 tile
     i = s.schedule(b)
     assert i["num_tiles"] == 4
-    assert list(b["tile_seq"][:4]) == [0, 0, 0, 1] and list(b["tile_row"][:4]) == [0, 64, 128, 0]
+    # sorted by ascending causal work (keys seen by the tile's last row): seq 1's 2-token
+    # tile, then seq 0's tiles ending at tokens 16, 32, 37 (the kernel runs the map back to front)
+    assert list(b["tile_seq"][:4]) == [1, 0, 0, 0] and list(b["tile_row"][:4]) == [0, 0, 64, 128]
     assert list(b["q_start"][:3]) == [0, 37, 39]
 
 
@@ -105,7 +107,7 @@ def test_prefill_tile_rows_short_steps():
     s2.add_request(2, [5, 6], 2)
     i = s2.schedule(b2)
     assert i["tile_rows"] == 256 and i["num_tiles"] == 2
-    assert list(b2["tile_seq"][:2]) == [0, 1] and list(b2["tile_row"][:2]) == [0, 0]
+    assert list(b2["tile_seq"][:2]) == [1, 0] and list(b2["tile_row"][:2]) == [0, 0]
     s3, b3 = _sched(budget=64, max_len=128, G=4, tile_rows_short=256, short_rows=100)
     s3.add_request(1, list(range(3, 40)), 2)  # 148 rows > 100 -> tile_rows (64)
     i = s3.schedule(b3)

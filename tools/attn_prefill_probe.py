@@ -57,6 +57,9 @@ def main():
                 for r in range(0, L * G, rows):
                     ts.append(s)
                     tr.append(r)
+            if not os.environ.get("PROBE_UNSORTED"):  # the serving scheduler's order
+                order = sorted(range(len(ts)), key=lambda i: min(L, -(-(tr[i] + rows) // G)))
+                ts, tr = [ts[i] for i in order], [tr[i] for i in order]
             ts = torch.tensor(ts, dtype=torch.int32, device=dev)
             tr = torch.tensor(tr, dtype=torch.int32, device=dev)
             us = gt._timed(lambda i: ops.paged_attention_prefill(
