@@ -151,6 +151,13 @@ __device__ __forceinline__ void qk_tok(const bf16* __restrict__ qkv, int qkv_str
 constexpr int V_SPAN = 64;
 constexpr int V_ROWS = V_SPAN + 7;  // a run starting in the span may end 7 tokens past it
 
+//
+// Every global read of the role is issued before the first is consumed: the span's V rows
+// (5 unconditional, index-clamped 16-byte loads per thread) and its slots (slots[t0 - 1 ..
+// t0 + V_ROWS), one per thread) land in registers, then in LDS, and the run scan reads the
+// slots from LDS.  A strided fill loop and a scan of slots[] in global memory made the role a
+// chain of ~5 + 8 dependent round trips per workgroup (round 6: 44 us per 16k-token prefill
+// layer in the serving trace, ~3 TB/s of K/V traffic).
 template <bool F8>
 __device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_stride,
                                        void* __restrict__ v_cache,
@@ -158,7 +165,9 @@ __device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_str
                                        int BS, int span_id, bf16* __restrict__ v_tail,
                                        const int* __restrict__ tail_slot, int num_decode) {
   constexpr int D = 128;
+  constexpr int NL = (V_ROWS * (D / 8) + 255) / 256;  // row pieces per thread
   __shared__ bf16 tile[V_ROWS][D];
+  __shared__ int64_t sl_s[V_ROWS + 1];  // slots[t0 - 1 + i] (-1 outside the batch)
   __shared__ int lead_n[V_SPAN];  // run length if the token leads a run, else 0
   __shared__ int lead_list[V_SPAN];
   __shared__ int n_leads;
@@ -167,20 +176,33 @@ __device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_str
   const int rows = min(V_ROWS, T - t0);
   const int tid = threadIdx.x;
   const bf16* src = qkv + (size_t)t0 * qkv_stride + (Hq + Hkv + vh) * D;
-  for (int i = tid; i < rows * (D / 8); i += 256) {
-    const int r = i >> 4, c = (i & 15) * 8;
-    *reinterpret_cast<bf16x8*>(&tile[r][c]) =
-        *reinterpret_cast<const bf16x8*>(src + (size_t)r * qkv_stride + c);
+  bf16x8 rv[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = min(tid + 256 * j, rows * (D / 8) - 1);
+    rv[j] = *reinterpret_cast<const bf16x8*>(src + (size_t)(i >> 4) * qkv_stride + (i & 15) * 8);
   }
+  int64_t sv = -1;
+  if (tid <= V_ROWS) {
+    const int t = t0 - 1 + tid;
+    if (t >= 0 && t < T) sv = slots[t];
+  }
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + 256 * j;
+    if (i < rows * (D / 8)) *reinterpret_cast<bf16x8*>(&tile[i >> 4][(i & 15) * 8]) = rv[j];
+  }
+  if (tid <= V_ROWS) sl_s[tid] = sv;
+  __syncthreads();
   if (tid < V_SPAN) {
     const int t = t0 + tid;
     int n = 0;
     if (t < T) {
-      const int64_t s = slots[t];
-      if (s >= 0 && (t == 0 || (s & 7) == 0 || slots[t - 1] != s - 1)) {
+      const int64_t s = sl_s[tid + 1];
+      if (s >= 0 && (t == 0 || (s & 7) == 0 || sl_s[tid] != s - 1)) {
         n = 1;
         const int lim = 8 - (int)(s & 7);
-        while (n < lim && t + n < T && slots[t + n] == s + n) ++n;
+        while (n < lim && t + n < T && sl_s[tid + 1 + n] == s + n) ++n;
       }
     }
     lead_n[tid] = n;
@@ -195,7 +217,7 @@ __device__ __forceinline__ void v_span(const bf16* __restrict__ qkv, int qkv_str
     const int i = lead_list[j];
     const int n = lead_n[i];
     const int t = t0 + i;
-    const int64_t s = slots[t];
+    const int64_t s = sl_s[i + 1];
     const int64_t blk = s / BS;
     const int off = (int)(s % BS);
     const int i0 = off & 7;
