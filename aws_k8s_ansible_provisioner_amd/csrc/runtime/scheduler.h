@@ -67,9 +67,9 @@ struct SchedConfig {
   int gqa_group = 1;      // q heads per kv head (prefill tile map)
   int tile_rows = 64;     // flattened query rows per prefill attention workgroup
   // steps whose every prefill chunk has <= short_rows flattened q rows (chunk tokens x
-  // gqa_group) use tile_rows_short instead (0: off): the 8-wave 256-row prefill kernel
-  // wins on short prompts with small GQA groups and loses on long ones
-  // (profiles/r5_prefill_tile_rows.md)
+  // gqa_group) use tile_rows_short instead (0: off).  The engine sets 256 / 128: with the
+  // longest-first grid the 8-wave 256-row kernel wins on long chunks, the 128-row one on
+  // short prompts with small GQA groups (profiles/r6_prefill_tile_order.md)
   int tile_rows_short = 0;
   int short_rows = 1024;
   int eos_id = -1;

@@ -72,15 +72,16 @@ class ModelRunner:
         self.max_seqs = ecfg.max_num_seqs
         # a mixed step holds a full prefill token budget plus one decode row per sequence
         self.cap_tokens = ecfg.max_num_batched_tokens + self.max_seqs
-        # prefill tile map granularity: 128 flattened q rows per workgroup for the flash-style
-        # GPU kernel (the CPU reference attention ignores the tile map)
-        self.tile_rows = 128 if dev == "cuda" else 64
-        # steps whose prefill chunks all have <= 1024 flattened q rows (e.g. 512-token prompts
-        # at GQA 2) take the 8-wave 256-row kernel (bf16 caches): 86.8 vs 100.2 us at 32 x 512
-        # on Qwen3-0.6B heads, while it loses on long prompts and at GQA 4 x 512
-        # (profiles/r5_prefill_tile_rows.md)
-        self.tile_rows_short = 256 if dev == "cuda" and not ecfg.kv_cache_dtype.startswith(
-            "fp8") else 0
+        # prefill tile map granularity (flattened q rows per workgroup of the flash-style GPU
+        # kernel; the CPU reference attention ignores the map): with the longest-first flat
+        # grid (round 6) the 8-wave 256-row tile wins on long chunks (Qwen3 4 x 4096: 284.5 vs
+        # 301.6 us, Llama-3-8B 32 x 512: 149.2 vs 154.5, 4 x 4096: 566.3 vs 578.8, q prep in
+        # the kernel), the 128-row tile on chunks whose every prompt has <= 1024 rows (Qwen3
+        # 32 x 512: 83.8 vs 87.9 us) -- profiles/r6_prefill_tile_order.md.  The 256-row kernel
+        # needs a bf16 KV cache.
+        bf16_kv = dev == "cuda" and not ecfg.kv_cache_dtype.startswith("fp8")
+        self.tile_rows = 256 if bf16_kv else (128 if dev == "cuda" else 64)
+        self.tile_rows_short = 128 if bf16_kv else 0
         if dev == "cuda" and os.environ.get("AKAP_PREFILL_TILE_ROWS") in ("128", "256"):
             self.tile_rows = int(os.environ["AKAP_PREFILL_TILE_ROWS"])  # A/B knob
             self.tile_rows_short = 0
