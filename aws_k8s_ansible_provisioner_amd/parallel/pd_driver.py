@@ -191,7 +191,7 @@ class PDPair:
                     if full > s0:
                         new = iid not in prompt_of
                         if new:
-                            prompt_of[iid] = eng.reqs[iid].prompt_ids
+                            prompt_of[iid] = eng.reqs[iid].prompt_list()
                         ents, blks = per[dest_of(iid)]
                         ents.append((_CHUNK, iid, prompt_of[iid] if new else None, -1, s0,
                                      full - s0, bt[s0:full]))

@@ -286,7 +286,8 @@ def main() -> int:
                 return 0, []
             r = pair.run_decode(sp, time.time())
             return r["output_tokens"], r["ttft"]
-        prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len)).tolist()
+        # int32 rows: the engine hands each to the scheduler in one copy (no per-id conversion)
+        prompts = rng.integers(10, vocab_hi, size=(a.num_requests, a.input_len), dtype=np.int32)
         outs = eng.generate(None, sp, prompt_ids=prompts)
         ntok = sum(len(o.output_ids) for o in outs)
         ttfts = [o.ttft for o in outs if o.ttft is not None]

@@ -197,3 +197,20 @@ def test_decode_partitions_capped_at_the_kernel_limit():
         parts, ps = eng.runner.decode_partitions(n)
         assert ps % 128 == 0 and ps <= ops.DECODE_MAX_PART, (n, parts, ps)
         assert parts * ps >= 40000, (n, parts, ps)
+
+
+def test_numpy_prompt_ids_match_lists():
+    """int32 prompt arrays (the bulk-admission fast path: one copy into the scheduler) give the
+    same greedy outputs as Python lists, and outputs report the prompt as a list."""
+    import numpy as np
+
+    sp = SamplingParams(max_tokens=6, temperature=0.0)
+    prompts = np.random.default_rng(3).integers(3, 200, size=(3, 21), dtype=np.int32)
+    a = _engine("tiny-qwen3").generate(None, sp, prompt_ids=[p.tolist() for p in prompts])
+    b = _engine("tiny-qwen3").generate(None, sp, prompt_ids=prompts)
+    assert [o.output_ids for o in a] == [o.output_ids for o in b]
+    assert all(isinstance(o.prompt_ids, list) and o.prompt_ids == p.tolist()
+               for o, p in zip(b, prompts))
+    # int64 arrays and non-contiguous views are accepted too
+    c = _engine("tiny-qwen3").generate(None, sp, prompt_ids=prompts.astype(np.int64)[:, ::1])
+    assert [o.output_ids for o in a] == [o.output_ids for o in c]
