@@ -319,6 +319,9 @@ __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int 
     } else if (write_kv) {
       const int64_t slot = pp.slot;
       if (slot >= 0) {
+        // tail path with defer_kv: only the LDS images here, the cache / tail stores are
+        // issued at the end of the work item (deferred_kv_stores)
+        const bool gst = !(tail && p.defer_kv);
         const int64_t blk = slot / p.BS;
         const int off = (int)(slot % p.BS);
         if (rr == G) {
@@ -329,7 +332,7 @@ __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int 
             dst[0] = f32x4_to_fp8x4((float)o8[0], (float)o8[1], (float)o8[2], (float)o8[3]);
             dst[1] = f32x4_to_fp8x4((float)o8[4], (float)o8[5], (float)o8[6], (float)o8[7]);
           } else {
-            *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
+            if (gst) *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) = o8;
             if (tail) *reinterpret_cast<bf16x8*>(k_img + 8 * j) = o8;
           }
         } else if (tail) {
@@ -342,7 +345,8 @@ __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int 
           group_units(rows, u);
 #pragma unroll
           for (int k = 0; k < 8; ++k) *reinterpret_cast<bf16x8*>(v_img + (8 * j + k) * 8) = u[k];
-          if (i0 == 7) {
+          if (!gst) {
+          } else if (i0 == 7) {
             bf16* e = (bf16*)p.v_cache + ((size_t)blk * p.Hkv + kvh) * kD * p.BS +
                       (off >> 3) * kD * 8 + (size_t)(8 * j) * 8;
 #pragma unroll
@@ -368,6 +372,47 @@ __device__ __forceinline__ void fused_qkv_prologue_pre(const AttnParams& p, int 
     __builtin_amdgcn_s_barrier();
   } else {
     __syncthreads();
+  }
+}
+
+// The new token's K / V stores of the fused tail path, issued after the work item's combine
+// from the LDS images the prologue built (k_img: the K row; v_img: the token's 8-token V
+// group, [D][8]).  Issued in the prologue they sat in wave 0's in-order vmcnt queue ahead of
+// every later chunk load, so each chunk wait of that wave also waited for the stores' write
+// acknowledgements (bench/attn_fused_ab.py: fused + tail 112.7 us vs 109.4 without the stores).
+// Nothing in this kernel reads those cache lines (the chunk loop patches the token in from the
+// LDS images), and the next kernel sees them after the launch boundary.
+template <bool F8>
+__device__ __forceinline__ void deferred_kv_stores(const AttnParams& p, int kvh,
+                                                   const ProPre<F8>& pp, const bf16* k_img,
+                                                   const bf16* v_img) {
+  const int rr = threadIdx.x >> 4;
+  const int j = threadIdx.x & 15;
+  const int G = p.G;
+  if (rr != G && rr != G + 1) return;
+  const int64_t blk = pp.slot / p.BS;
+  const int off = (int)(pp.slot % p.BS);
+  if (rr == G) {
+    const size_t e = ((size_t)blk * p.Hkv + kvh) * p.BS * kD + k_swz_offset(off) +
+                     k_dim_offset(8 * j);
+    *reinterpret_cast<bf16x8*>((bf16*)p.k_cache + e) =
+        *reinterpret_cast<const bf16x8*>(k_img + 8 * j);
+    return;
+  }
+  const int i0 = off & 7;
+  if (i0 == 7) {  // the group is complete: its [D][8] image goes to the cache
+    bf16* e = (bf16*)p.v_cache + ((size_t)blk * p.Hkv + kvh) * kD * p.BS + (off >> 3) * kD * 8 +
+              (size_t)(8 * j) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      *reinterpret_cast<bf16x8*>(e + 8 * k) =
+          *reinterpret_cast<const bf16x8*>(v_img + (8 * j + k) * 8);
+  } else {  // the token's row (dims 8j..8j+7) goes to the sequence's V tail
+    bf16x8 o8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o8[i] = v_img[(8 * j + i) * 8 + i0];
+    bf16* tb = p.v_tail + ((size_t)pp.tsl * p.Hkv + kvh) * 8 * kD + 8 * j;
+    *reinterpret_cast<bf16x8*>(tb + (size_t)i0 * kD) = o8;
   }
 }
 
@@ -563,6 +608,9 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
         p.part_l[pidx] = L;
       }
     }
+  }
+  if constexpr (FUSED && !F8) {
+    if (use_img && p.defer_kv) deferred_kv_stores<F8>(p, kvh, pp, k_img, v_img);
   }
 #undef OS
 }
@@ -1135,14 +1183,20 @@ void launch_paged_attn_decode(const AttnParams& p, int num_seqs, hipStream_t s) 
                       (p.v_tail ? (size_t)kD * 8 * sizeof(bf16) : 0) +
                       (p.qkv && p.v_tail ? (size_t)kD * sizeof(bf16) : 0);
   const dim3 grid(num_seqs, p.Hkv, p.num_parts);
+  static const int defer_kv = [] {  // AKAP_DECODE_DEFER_KV=0: stores in the prologue (A/B)
+    const char* e = std::getenv("AKAP_DECODE_DEFER_KV");
+    return e != nullptr ? std::atoi(e) : 1;
+  }();
+  AttnParams q = p;
+  q.defer_kv = defer_kv;
   if (p.kv_fp8) {
-    if (p.qkv != nullptr) paged_attn_decode_kernel<true, true><<<grid, 256, smem, s>>>(p);
-    else paged_attn_decode_kernel<false, true><<<grid, 256, smem, s>>>(p);
+    if (p.qkv != nullptr) paged_attn_decode_kernel<true, true><<<grid, 256, smem, s>>>(q);
+    else paged_attn_decode_kernel<false, true><<<grid, 256, smem, s>>>(q);
   } else {
-    if (p.qkv != nullptr) paged_attn_decode_kernel<true, false><<<grid, 256, smem, s>>>(p);
-    else paged_attn_decode_kernel<false, false><<<grid, 256, smem, s>>>(p);
+    if (p.qkv != nullptr) paged_attn_decode_kernel<true, false><<<grid, 256, smem, s>>>(q);
+    else paged_attn_decode_kernel<false, false><<<grid, 256, smem, s>>>(q);
   }
-  if (p.num_parts > 1) paged_attn_reduce_kernel<<<dim3(num_seqs, p.Hkv), 256, 0, s>>>(p);
+  if (p.num_parts > 1) paged_attn_reduce_kernel<<<dim3(num_seqs, p.Hkv), 256, 0, s>>>(q);
 }
 
 }  // namespace akap

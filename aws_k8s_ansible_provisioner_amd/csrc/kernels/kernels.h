@@ -83,6 +83,10 @@ struct AttnParams {
   // rescaled) only when the tile's max exceeds it by more than this many log2 units (0 =
   // every increase); set by launch_paged_attn_prefill (AKAP_FA_RESCALE_T, default 8)
   float rescale_t;
+  // fused decode with the V tail: the new token's K / V cache and tail stores are issued at
+  // the end of the work item from the LDS images instead of in the prologue (set by
+  // launch_paged_attn_decode: AKAP_DECODE_DEFER_KV, default 1)
+  int defer_kv;
 };
 // tile_rows: 128 -> flash-style LDS-tiled kernel (4 waves), 256 -> its 8-wave form (bf16 KV)
 void launch_paged_attn_prefill(const AttnParams& p, int num_tiles, int tile_rows, hipStream_t s);
