@@ -69,6 +69,18 @@ def main() -> int:
     print()
     print(f"total idle per step: {tot:.1f} us")
     print()
+    # idle at each step's start (previous step's sampling end -> this step's first dispatch)
+    # plus inside its first 4 dispatches (the host-launched staging / gather before the graph)
+    head = []
+    for a_, b_ in zip(dec, dec[1:]):
+        head.append(sum(max(0, y[0] - x[1]) for x, y in zip([a_[-1]] + b_[:4], b_[:5])) / 1e3)
+    if head:
+        hs = sorted(head)
+        pct = lambda q: hs[min(len(hs) - 1, int(q * len(hs)))]
+        print(f"step-start idle per step (us): p50 {pct(0.5):.1f}  p90 {pct(0.9):.1f}  "
+              f"p99 {pct(0.99):.1f}  max {hs[-1]:.1f}  mean {statistics.mean(hs):.1f}  "
+              f"steps over 100 us: {sum(h > 100 for h in hs)} of {len(hs)}")
+        print()
     print("| kernel | per step | mean us |")
     print("|---|---:|---:|")
     for k, v in sorted(durs.items(), key=lambda kv: -sum(kv[1])):
