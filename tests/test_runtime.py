@@ -498,3 +498,26 @@ def test_v_tail_slots_follow_each_sequence_and_return_to_the_pool():
     s0.add_request(1, [5, 6, 7], 4)
     s0.schedule(b0)
     assert b0["tail_slot"][:3].tolist() == [-1, -1, -1]
+
+
+def test_prefill_tile_map_sorted_by_causal_work_with_context():
+    """The tile map is sorted by ascending causal work -- keys seen by the tile's last row,
+    context included -- so a continued chunk's tiles (prior context) come after a fresh short
+    prompt's; the prefill attention kernel walks the map back to front (longest first)."""
+    s, b = _sched(budget=40, max_len=128, G=2)
+    s.add_request(1, list(range(3, 63)), 2)   # 60 tokens: 40 now, 20 in the next step
+    i = s.schedule(b)
+    assert i["num_tiles"] == 2  # 80 rows / 64
+    s.update(np.zeros(0, np.int64))
+    s.add_request(2, [5, 6, 7], 2)            # fresh 3-token prompt
+    i = s.schedule(b)
+    n = i["num_tiles"]
+    seqs = list(b["tile_seq"][:n])
+    rows = list(b["tile_row"][:n])
+    qs, sl = list(b["q_start"][:3]), list(b["seq_lens"][:2])
+    work = []
+    for t in range(n):
+        q = qs[seqs[t] + 1] - qs[seqs[t]]
+        work.append(sl[seqs[t]] - q + min(q, -(-(rows[t] + 64) // 2)))
+    assert work == sorted(work) and work == [3, 60]  # fresh 3-token tile, then 40 + 20 keys
+    assert sorted(zip(seqs, rows)) == sorted(set(zip(seqs, rows)))  # no tile lost or doubled
