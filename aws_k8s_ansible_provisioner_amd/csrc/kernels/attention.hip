@@ -750,7 +750,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_attn_prefill_fa_kernel(
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) raw[s8] = *reinterpret_cast<const bf16x8*>(src + 16 * s8);
 #pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8) w8[s8] = *reinterpret_cast<const bf16x8*>(wsrc + 16 * s8 + 8 * h);
+    for (int s8 = 0; s8 < 8; ++s8) {
+      // both 8-dim halves at wave-uniform addresses (scalar loads: 512 B per wave instead of
+      // 8 KB of vector loads of the same 256-B weight row), then the lane's half selected
+      typedef const __attribute__((address_space(4))) bf16x8 cbf16x8;  // constant: s_load
+      const bf16x8 wl = *(cbf16x8*)(size_t)(wsrc + 16 * s8);
+      const bf16x8 wh = *(cbf16x8*)(size_t)(wsrc + 16 * s8 + 8);
+      w8[s8] = h ? wh : wl;
+    }
 #pragma unroll
     for (int s8 = 0; s8 < 4; ++s8)
 #pragma unroll
