@@ -1,3 +1,4 @@
+# (A/B harness: abso/_C_old.so and abso/_C_new.so were built locally from HEAD~ and HEAD and removed afterwards)
 set -u
 O=gpurun_out/s9zm; mkdir -p $O
 P=aws_k8s_ansible_provisioner_amd
