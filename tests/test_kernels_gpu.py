@@ -141,7 +141,8 @@ def test_paged_attention_prefill(bs, hq, hkv, tile_rows):
     _close(out, exp, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8)])
+# odd GQA groups (8/8, 24/8) take the full rotary-row loads, even ones the lane-pair share
+@pytest.mark.parametrize("hq,hkv", [(16, 8), (32, 8), (8, 8), (24, 8)])
 @pytest.mark.parametrize("qk_norm", [True, False])
 @pytest.mark.parametrize("tile_rows", [128, 256])
 def test_paged_attention_prefill_qprep(hq, hkv, qk_norm, tile_rows):
