@@ -617,9 +617,14 @@ __device__ __forceinline__ void decode_item(const AttnParams& p, int seq, int kv
 
 // grid = (num_seqs, Hkv, num_parts): one work item per workgroup.  (Persistent, pipelined
 // persistent, single-buffered 3-WG/CU and barrier-free-prologue forms were measured equal or
-// slower and removed: profiles/r3_attn_rework_ab.log, r3_attn_variants_ab.log.)
+// slower and removed: profiles/r3_attn_rework_ab.log, r3_attn_variants_ab.log.)  Two
+// workgroups per CU: with (256, 1) the serving form took 244 VGPRs + 32 AGPRs (one wave per
+// SIMD, each CU ran its 8 workgroups of a B = 256 step one after another); bounded to two it
+// fits 238 VGPRs with no spills and the next workgroup's prologue overlaps the current one's
+// stream -- 110.7 -> 110.1 us serving, 106.3 -> 105.2 us on a ready q
+// (profiles/r6_decode_kv_store.md).
 template <bool FUSED, bool F8>
-__global__ __launch_bounds__(256, 1) void paged_attn_decode_kernel(AttnParams p) {
+__global__ __launch_bounds__(256, 2) void paged_attn_decode_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
   decode_item<FUSED, F8>(p, blockIdx.x, blockIdx.y, blockIdx.z, dyn_lds);
 }
